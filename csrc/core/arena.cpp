@@ -1,0 +1,483 @@
+// ChunkArena / HbmArena / HostArena implementation.
+#include "ogkm/arena.hpp"
+
+#include <fcntl.h>
+#include <numaif.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <deque>
+#include <sstream>
+
+#include "ogkm/config.hpp"
+#include "ogkm/events.hpp"
+
+namespace ogkm {
+
+ChunkArena::ChunkArena(std::string name, Loc loc, LockOrder order) : name_(std::move(name)), loc_(loc), m_(order) {}
+ChunkArena::~ChunkArena() = default;
+
+void ChunkArena::init_chunks(uint64_t base, uint32_t n) {
+  base_ = base;
+  nchunks_ = n;
+  chunks_.assign(n, ChunkInfo{});
+  free_runs_.clear();
+  if (n) free_runs_[0] = n;
+  st_ = Stats{};
+  st_.capacity = (uint64_t)n << kBlockShift;
+}
+
+int64_t ChunkArena::chunk_of(uint64_t addr) const {
+  if (addr < base_ || addr >= base_ + ((uint64_t)nchunks_ << kBlockShift)) return -1;
+  return (int64_t)((addr - base_) >> kBlockShift);
+}
+
+// ------------------------------------------------------------ free runs
+void ChunkArena::take_run(uint32_t first, uint32_t n) {
+  auto it = free_runs_.upper_bound(first);
+  RT_ASSERT_RELEASE(it != free_runs_.begin());
+  --it;
+  uint32_t s = it->first, l = it->second;
+  RT_ASSERT_RELEASE(s <= first && first + n <= s + l);
+  free_runs_.erase(it);
+  if (first > s) free_runs_[s] = first - s;
+  if (first + n < s + l) free_runs_[first + n] = s + l - (first + n);
+}
+
+void ChunkArena::add_run(uint32_t first, uint32_t n) {
+  uint32_t s = first, e = first + n;
+  auto it = free_runs_.lower_bound(first);
+  if (it != free_runs_.end() && it->first == e) {
+    e += it->second;
+    it = free_runs_.erase(it);
+  }
+  if (it != free_runs_.begin()) {
+    auto pv = std::prev(it);
+    if (pv->first + pv->second == s) {
+      s = pv->first;
+      free_runs_.erase(pv);
+    }
+  }
+  free_runs_[s] = e - s;
+}
+
+// ------------------------------------------------------------ LRU lists
+void ChunkArena::lru_remove(uint32_t i) {
+  ChunkInfo& c = chunks_[i];
+  if (!c.list) return;
+  if (c.prev >= 0) chunks_[c.prev].next = c.next;
+  else head_[c.list] = c.next;
+  if (c.next >= 0) chunks_[c.next].prev = c.prev;
+  else tail_[c.list] = c.prev;
+  if (c.list == 1) st_.unused_list--;
+  else st_.used_list--;
+  c.prev = c.next = -1;
+  c.list = 0;
+}
+
+void ChunkArena::lru_push_tail(uint32_t i, uint8_t list) {
+  ChunkInfo& c = chunks_[i];
+  c.list = list;
+  c.prev = tail_[list];
+  c.next = -1;
+  if (tail_[list] >= 0) chunks_[tail_[list]].next = (int32_t)i;
+  else head_[list] = (int32_t)i;
+  tail_[list] = (int32_t)i;
+  if (list == 1) st_.unused_list++;
+  else st_.used_list++;
+}
+
+// ------------------------------------------------------------ allocation
+Status ChunkArena::alloc(uint32_t n, Block* owner, int64_t hint, uint32_t* first) {
+  if (n == 0) return Status::INVALID_ARGUMENT;
+  std::lock_guard<OrderedMutex> g(m_);
+  int64_t pick = -1;
+  // Honour the hint (keeps a range's blocks adjacent) when that window is free.
+  if (hint >= 0 && hint + n <= nchunks_) {
+    auto it = free_runs_.upper_bound((uint32_t)hint);
+    if (it != free_runs_.begin()) {
+      --it;
+      if (it->first <= hint && hint + n <= (int64_t)it->first + it->second) pick = hint;
+    }
+  }
+  if (pick < 0) {
+    // Best fit: smallest run that holds n chunks (limits fragmentation).
+    uint32_t best = UINT32_MAX;
+    for (auto& r : free_runs_)
+      if (r.second >= n && r.second < best) {
+        best = r.second;
+        pick = r.first;
+        if (best == n) break;
+      }
+  }
+  if (pick < 0) return Status::NO_MEMORY;
+  take_run((uint32_t)pick, n);
+  for (uint32_t i = 0; i < n; ++i) {
+    ChunkInfo& c = chunks_[pick + i];
+    c.state = ChunkState::ALLOCATED;
+    c.owner = owner;
+    c.pin_count = 0;
+    c.last_use = ++clock_;
+    lru_push_tail((uint32_t)pick + i, 1);
+  }
+  st_.allocated += (uint64_t)n << kBlockShift;
+  st_.peak = std::max(st_.peak, st_.allocated);
+  st_.allocs += n;
+  *first = (uint32_t)pick;
+  return Status::OK;
+}
+
+Status ChunkArena::reserve(uint32_t n, Reservation* r) {
+  std::lock_guard<OrderedMutex> g(m_);
+  if (n == 0 || n > nchunks_) return Status::NO_MEMORY;
+  // Fast path: a free run.
+  for (auto& fr : free_runs_)
+    if (fr.second >= n) {
+      r->first = fr.first;
+      r->n = n;
+      r->victims.clear();
+      take_run(fr.first, n);
+      for (uint32_t i = 0; i < n; ++i) chunks_[fr.first + i].state = ChunkState::RESERVED;
+      st_.reservations++;
+      return Status::OK;
+    }
+  if (n == 1) {
+    // Victim order: unused list head, then used LRU head (uvm_pmm_gpu.c:1460-1500).
+    for (int list : {1, 2}) {
+      for (int32_t i = head_[list]; i >= 0; i = chunks_[i].next) {
+        ChunkInfo& c = chunks_[i];
+        if (c.state == ChunkState::ALLOCATED && c.pin_count == 0) {
+          lru_remove((uint32_t)i);
+          c.state = ChunkState::EVICTING;
+          r->first = i;
+          r->n = 1;
+          r->victims = {(uint32_t)i};
+          st_.reservations++;
+          return Status::OK;
+        }
+      }
+    }
+    return Status::NO_MEMORY;
+  }
+  // Sliding window over [0, nchunks): every chunk must be FREE or evictable;
+  // minimise the newest last_use in the window (evict the coldest data).
+  int64_t best_first = -1;
+  uint64_t best_cost = UINT64_MAX;
+  std::deque<uint32_t> dq;  // monotone deque of last_use maxima
+  uint32_t start = 0;
+  for (uint32_t i = 0; i < nchunks_; ++i) {
+    ChunkInfo& c = chunks_[i];
+    bool ok = c.state == ChunkState::FREE || (c.state == ChunkState::ALLOCATED && c.pin_count == 0);
+    if (!ok) {
+      start = i + 1;
+      dq.clear();
+      continue;
+    }
+    uint64_t cost = c.state == ChunkState::FREE ? 0 : c.last_use;
+    while (!dq.empty() && (chunks_[dq.back()].state == ChunkState::FREE ? 0 : chunks_[dq.back()].last_use) <= cost)
+      dq.pop_back();
+    dq.push_back(i);
+    if (i + 1 - start > n) {
+      start = i + 1 - n;
+      while (!dq.empty() && dq.front() < start) dq.pop_front();
+    }
+    if (i + 1 - start == n) {
+      uint64_t wcost = chunks_[dq.front()].state == ChunkState::FREE ? 0 : chunks_[dq.front()].last_use;
+      if (wcost < best_cost) {
+        best_cost = wcost;
+        best_first = start;
+      }
+    }
+  }
+  if (best_first < 0) return Status::NO_MEMORY;
+  r->first = best_first;
+  r->n = n;
+  r->victims.clear();
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t k = (uint32_t)best_first + i;
+    ChunkInfo& c = chunks_[k];
+    if (c.state == ChunkState::FREE) {
+      take_run(k, 1);
+      c.state = ChunkState::RESERVED;
+    } else {
+      lru_remove(k);
+      c.state = ChunkState::EVICTING;
+      r->victims.push_back(k);
+    }
+  }
+  st_.reservations++;
+  return Status::OK;
+}
+
+void ChunkArena::evicted(uint32_t i) {
+  std::lock_guard<OrderedMutex> g(m_);
+  ChunkInfo& c = chunks_[i];
+  RT_ASSERT_RELEASE(c.state == ChunkState::EVICTING);
+  c.state = ChunkState::RESERVED;
+  c.owner = nullptr;
+  st_.allocated -= kBlockSize;
+  st_.evictions++;
+}
+
+void ChunkArena::commit(const Reservation& r) {
+  std::lock_guard<OrderedMutex> g(m_);
+  for (uint32_t i = 0; i < r.n; ++i) {
+    ChunkInfo& c = chunks_[r.first + i];
+    RT_ASSERT_RELEASE(c.state == ChunkState::RESERVED);
+    c.state = ChunkState::ALLOCATED;
+    c.owner = nullptr;
+    c.pin_count = 0;
+    c.last_use = ++clock_;
+    lru_push_tail((uint32_t)r.first + i, 1);
+  }
+  st_.allocated += (uint64_t)r.n << kBlockShift;
+  st_.peak = std::max(st_.peak, st_.allocated);
+  st_.allocs += r.n;
+}
+
+void ChunkArena::cancel(const Reservation& r) {
+  std::lock_guard<OrderedMutex> g(m_);
+  for (uint32_t i = 0; i < r.n; ++i) {
+    uint32_t k = (uint32_t)r.first + i;
+    ChunkInfo& c = chunks_[k];
+    if (c.state == ChunkState::RESERVED) {
+      c.state = ChunkState::FREE;
+      c.owner = nullptr;
+      add_run(k, 1);
+    } else if (c.state == ChunkState::EVICTING) {
+      // eviction failed: the owner keeps the chunk
+      c.state = ChunkState::ALLOCATED;
+      lru_push_tail(k, 2);
+    }
+  }
+}
+
+void ChunkArena::free(uint32_t first, uint32_t n) {
+  std::lock_guard<OrderedMutex> g(m_);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t k = first + i;
+    ChunkInfo& c = chunks_[k];
+    RT_ASSERT_RELEASE(c.state == ChunkState::ALLOCATED);
+    lru_remove(k);
+    c.state = ChunkState::FREE;
+    c.owner = nullptr;
+    c.pin_count = 0;
+    c.zeroed = false;
+  }
+  add_run(first, n);
+  st_.allocated -= (uint64_t)n << kBlockShift;
+  st_.frees += n;
+}
+
+void ChunkArena::set_owner(uint32_t i, Block* b) {
+  std::lock_guard<OrderedMutex> g(m_);
+  chunks_[i].owner = b;
+}
+
+Block* ChunkArena::owner(uint32_t i) {
+  std::lock_guard<OrderedMutex> g(m_);
+  return chunks_[i].owner;
+}
+
+void ChunkArena::touch(uint32_t i, bool has_data) {
+  std::lock_guard<OrderedMutex> g(m_);
+  ChunkInfo& c = chunks_[i];
+  if (c.state != ChunkState::ALLOCATED) return;
+  c.last_use = ++clock_;
+  lru_remove(i);
+  lru_push_tail(i, has_data ? 2 : 1);
+}
+
+void ChunkArena::pin(uint32_t i) {
+  std::lock_guard<OrderedMutex> g(m_);
+  if (chunks_[i].pin_count++ == 0) st_.pinned += kBlockSize;
+}
+
+void ChunkArena::unpin(uint32_t i) {
+  std::lock_guard<OrderedMutex> g(m_);
+  RT_ASSERT_RELEASE(chunks_[i].pin_count > 0);
+  if (--chunks_[i].pin_count == 0) st_.pinned -= kBlockSize;
+}
+
+bool ChunkArena::pinned(uint32_t i) {
+  std::lock_guard<OrderedMutex> g(m_);
+  return chunks_[i].pin_count > 0;
+}
+
+void ChunkArena::add_reuse_fence(uint32_t i, const FenceRef& f) {
+  std::lock_guard<OrderedMutex> g(m_);
+  chunks_[i].reuse_fence.add(f);
+}
+
+Tracker ChunkArena::take_reuse_fence(uint32_t i) {
+  std::lock_guard<OrderedMutex> g(m_);
+  Tracker t = chunks_[i].reuse_fence;
+  chunks_[i].reuse_fence.clear();
+  return t;
+}
+
+ChunkArena::Stats ChunkArena::stats() {
+  std::lock_guard<OrderedMutex> g(m_);
+  return st_;
+}
+
+uint32_t ChunkArena::free_chunks() {
+  std::lock_guard<OrderedMutex> g(m_);
+  uint32_t n = 0;
+  for (auto& r : free_runs_) n += r.second;
+  return n;
+}
+
+uint32_t ChunkArena::largest_free_run() {
+  std::lock_guard<OrderedMutex> g(m_);
+  uint32_t n = 0;
+  for (auto& r : free_runs_) n = std::max(n, r.second);
+  return n;
+}
+
+uint64_t ChunkArena::outstanding_bytes() {
+  std::lock_guard<OrderedMutex> g(m_);
+  return st_.allocated;
+}
+
+std::string ChunkArena::check() {
+  std::lock_guard<OrderedMutex> g(m_);
+  std::ostringstream os;
+  uint32_t nfree = 0, nalloc = 0;
+  std::vector<uint8_t> in_run(nchunks_, 0);
+  uint32_t prev_end = 0;
+  bool first = true;
+  for (auto& r : free_runs_) {
+    if (!first && r.first <= prev_end) os << "free runs overlap/adjacent at " << r.first << "; ";
+    first = false;
+    prev_end = r.first + r.second;
+    for (uint32_t i = r.first; i < r.first + r.second; ++i) {
+      if (i >= nchunks_) { os << "run past end; "; break; }
+      in_run[i] = 1;
+      if (chunks_[i].state != ChunkState::FREE) os << "chunk " << i << " in free run but not FREE; ";
+    }
+    nfree += r.second;
+  }
+  for (uint32_t i = 0; i < nchunks_; ++i) {
+    if (chunks_[i].state == ChunkState::FREE && !in_run[i]) os << "FREE chunk " << i << " not in runs; ";
+    if (chunks_[i].state == ChunkState::ALLOCATED) nalloc++;
+  }
+  uint64_t n_on_lists = 0;
+  for (int l : {1, 2})
+    for (int32_t i = head_[l]; i >= 0; i = chunks_[i].next) {
+      n_on_lists++;
+      if (chunks_[i].state != ChunkState::ALLOCATED) os << "non-allocated chunk " << i << " on LRU; ";
+      if (n_on_lists > nchunks_) { os << "LRU cycle; "; break; }
+    }
+  if (n_on_lists != nalloc) os << "LRU holds " << n_on_lists << " but " << nalloc << " allocated; ";
+  if ((uint64_t)nalloc << kBlockShift != st_.allocated) os << "allocated bytes mismatch; ";
+  return os.str();
+}
+
+// ------------------------------------------------------------ HBM arena
+HbmArena::HbmArena(Backend* be, int dev, uint64_t budget, int provider)
+    : ChunkArena("hbm" + std::to_string(dev), Loc::gpu(dev), LockOrder::HBM_ARENA), be_(be), dev_(dev) {
+  uint32_t n = (uint32_t)(budget >> kBlockShift);
+  bytes_ = (uint64_t)n << kBlockShift;
+  if (n == 0) {
+    init_chunks(0, 0);
+    return;
+  }
+  if (provider == 1 && be->vmm_supported(dev)) {
+    void* va = nullptr;
+    init_ = be->va_reserve(bytes_, &va);
+    if (init_ == Status::OK) {
+      handles_.resize(n);
+      for (uint32_t i = 0; i < n && init_ == Status::OK; ++i) {
+        init_ = be->vmm_create(dev, kBlockSize, &handles_[i]);
+        if (init_ == Status::OK) init_ = be->vmm_map((char*)va + ((uint64_t)i << kBlockShift), kBlockSize, handles_[i], dev);
+        if (init_ != Status::OK) handles_.resize(i);
+      }
+      slab_ = va;
+    }
+  } else {
+    init_ = be->hbm_alloc(dev, bytes_, &slab_);
+  }
+  if (init_ != Status::OK) {
+    RT_ERR("HBM arena init on gpu %d (%llu MB) failed: %s", dev, (unsigned long long)(bytes_ >> 20), status_str(init_));
+    init_chunks(0, 0);
+    return;
+  }
+  init_chunks((uint64_t)slab_, n);
+  RT_INFO("HBM arena gpu%d: %u x 2MB chunks at %p (%s)", dev, n, slab_, handles_.empty() ? "slab" : "vmm");
+}
+
+HbmArena::~HbmArena() {
+  if (!slab_) return;
+  if (!handles_.empty()) {
+    for (size_t i = 0; i < handles_.size(); ++i) {
+      be_->vmm_unmap((char*)slab_ + (i << kBlockShift), kBlockSize);
+      be_->vmm_release(handles_[i]);
+    }
+    be_->va_free(slab_, bytes_);
+  } else {
+    be_->hbm_free(dev_, slab_, bytes_);
+  }
+}
+
+// ------------------------------------------------------------ host / CXL arena
+HostArena::HostArena(Backend* be, Tier tier, int node, uint64_t capacity)
+    : ChunkArena(std::string(tier_str(tier)) + std::to_string(node), Loc{tier, (int16_t)node}, LockOrder::HOST_ARENA),
+      be_(be),
+      node_(node) {
+  uint32_t n = (uint32_t)(capacity >> kBlockShift);
+  bytes_ = (uint64_t)n << kBlockShift;
+  fd_ = memfd_create(name_.c_str(), MFD_CLOEXEC);
+  if (fd_ < 0 || ftruncate(fd_, bytes_) != 0) {
+    init_ = Status::NO_MEMORY;
+    init_chunks(0, 0);
+    return;
+  }
+  view_ = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, 0);
+  if (view_ == MAP_FAILED) {
+    view_ = nullptr;
+    init_ = Status::NO_MEMORY;
+    init_chunks(0, 0);
+    return;
+  }
+  // Bind the pages of this tier to its NUMA node (CXL.mem nodes are CPU-less
+  // NUMA nodes). Shared (shmem) mappings keep the policy on the object.
+  if (node >= 0 && node < 64) {
+    unsigned long mask = 1ul << node;
+    numa_bound_ = mbind(view_, bytes_, MPOL_BIND, &mask, 64, 0) == 0;
+    if (!numa_bound_) RT_DBG("mbind to node %d failed (errno %d); pages use the default policy", node, errno);
+  }
+  seg_registered_.assign((bytes_ + kHostSegment - 1) / kHostSegment, 0);
+  init_chunks((uint64_t)view_, n);
+}
+
+HostArena::~HostArena() {
+  if (view_) {
+    for (size_t s = 0; s < seg_registered_.size(); ++s)
+      if (seg_registered_[s]) be_->host_unregister((char*)view_ + s * kHostSegment);
+    munmap(view_, bytes_);
+  }
+  if (fd_ >= 0) close(fd_);
+}
+
+Status HostArena::ensure_registered(uint32_t first, uint32_t n) {
+  if (!view_) return Status::NO_MEMORY;
+  uint64_t lo = (uint64_t)first << kBlockShift, hi = ((uint64_t)(first + n) << kBlockShift);
+  std::lock_guard<std::mutex> g(seg_m_);
+  for (uint64_t s = lo / kHostSegment; s * kHostSegment < hi; ++s) {
+    if (seg_registered_[s]) continue;
+    char* p = (char*)view_ + s * kHostSegment;
+    uint64_t len = std::min<uint64_t>(kHostSegment, bytes_ - s * kHostSegment);
+    // Populate first (fault in on the bound node), then pin for device DMA.
+    if (madvise(p, len, MADV_POPULATE_WRITE) != 0) {
+      for (uint64_t o = 0; o < len; o += kPageSize) ((volatile char*)p)[o] = 0;
+    }
+    Status st = be_->host_register(p, len);
+    if (st != Status::OK) return st;
+    seg_registered_[s] = 1;
+  }
+  return Status::OK;
+}
+
+}  // namespace ogkm

@@ -1,0 +1,294 @@
+// FakeBackend: CPU-only devices for the test-suite and the CPU-only config.
+// HBM is host memory, streams are in-order worker threads, copies are memcpy.
+// This generalises the reference's fake CE HAL (uvm_page_tree_test.c:65-100),
+// which executes CE memcopy/memset methods on CPU addresses.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "ogkm/backend.hpp"
+
+namespace ogkm {
+
+namespace {
+
+struct FakeEvent {
+  std::atomic<bool> done{true};
+};
+
+class FakeStream {
+ public:
+  FakeStream() : th_([this] { run(); }) {}
+  ~FakeStream() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void enqueue(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(f));
+      ++pending_;
+    }
+    cv_.notify_all();
+  }
+  void sync() {
+    std::unique_lock<std::mutex> g(m_);
+    idle_cv_.wait(g, [&] { return pending_ == 0; });
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+      {
+        std::lock_guard<std::mutex> g(m_);
+        --pending_;
+      }
+      idle_cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, idle_cv_;
+  std::deque<std::function<void()>> q_;
+  size_t pending_ = 0;
+  bool stop_ = false;
+  std::thread th_;
+};
+
+class FakeBackend : public Backend {
+ public:
+  FakeBackend(int ndev, size_t hbm) : ndev_(ndev), hbm_(hbm), used_(ndev, 0) {}
+  const char* name() const override { return "fake"; }
+  bool is_fake() const override { return true; }
+  int device_count() override { return ndev_; }
+  int device_numa_node(int) override { return 0; }
+  Status device_mem_info(int dev, size_t* f, size_t* t) override {
+    if (dev < 0 || dev >= ndev_) return Status::INVALID_ARGUMENT;
+    *t = hbm_;
+    *f = hbm_ - used_[dev];
+    return Status::OK;
+  }
+  Status set_device(int) override { return Status::OK; }
+
+  Status hbm_alloc(int dev, size_t bytes, void** p) override {
+    if (dev < 0 || dev >= ndev_) return Status::INVALID_ARGUMENT;
+    if (used_[dev] + bytes > hbm_) return Status::NO_MEMORY;
+    void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) return Status::NO_MEMORY;
+    used_[dev] += bytes;
+    *p = m;
+    return Status::OK;
+  }
+  void hbm_free(int dev, void* p, size_t bytes) override {
+    if (p) munmap(p, bytes);
+    if (dev >= 0 && dev < ndev_) used_[dev] -= bytes;
+  }
+
+  bool vmm_supported(int) override { return true; }
+  Status vmm_create(int dev, size_t bytes, uint64_t* h) override {
+    if (used_[dev] + bytes > hbm_) return Status::NO_MEMORY;
+    int fd = memfd_create("ogkm-fake-vmm", MFD_CLOEXEC);
+    if (fd < 0 || ftruncate(fd, bytes) != 0) {
+      if (fd >= 0) close(fd);
+      return Status::NO_MEMORY;
+    }
+    used_[dev] += bytes;
+    std::lock_guard<std::mutex> g(m_);
+    handles_[(uint64_t)fd] = {dev, bytes};
+    *h = (uint64_t)fd;
+    return Status::OK;
+  }
+  void vmm_release(uint64_t h) override {
+    std::lock_guard<std::mutex> g(m_);
+    auto it = handles_.find(h);
+    if (it == handles_.end()) return;
+    used_[it->second.first] -= it->second.second;
+    close((int)h);
+    handles_.erase(it);
+  }
+  Status va_reserve(size_t bytes, void** va) override {
+    void* m = mmap(nullptr, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) return Status::NO_MEMORY;
+    *va = m;
+    return Status::OK;
+  }
+  void va_free(void* va, size_t bytes) override { munmap(va, bytes); }
+  Status vmm_map(void* va, size_t bytes, uint64_t h, int) override {
+    void* m = mmap(va, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, (int)h, 0);
+    return m == MAP_FAILED ? Status::IO_ERROR : Status::OK;
+  }
+  Status vmm_unmap(void* va, size_t bytes) override {
+    void* m = mmap(va, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
+    return m == MAP_FAILED ? Status::IO_ERROR : Status::OK;
+  }
+
+  Status host_register(void*, size_t) override { return Status::OK; }
+  void host_unregister(void*) override {}
+  Status host_alloc_coherent(size_t bytes, void** p) override {
+    void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) return Status::NO_MEMORY;
+    std::lock_guard<std::mutex> g(m_);
+    coherent_[m] = bytes;
+    *p = m;
+    return Status::OK;
+  }
+  void host_free_coherent(void* p) override {
+    std::lock_guard<std::mutex> g(m_);
+    auto it = coherent_.find(p);
+    if (it != coherent_.end()) {
+      munmap(p, it->second);
+      coherent_.erase(it);
+    }
+  }
+
+  void* stream_create(int, int) override { return new FakeStream(); }
+  void stream_destroy(void* s) override { delete (FakeStream*)s; }
+  Status stream_sync(void* s) override {
+    if (s) ((FakeStream*)s)->sync();
+    return Status::OK;
+  }
+  void* event_create(int) override { return new FakeEvent(); }
+  void event_destroy(void* e) override { delete (FakeEvent*)e; }
+  Status event_record(void* e, void* s) override {
+    auto* ev = (FakeEvent*)e;
+    if (!s) {
+      ev->done.store(true);
+      return Status::OK;
+    }
+    ev->done.store(false);
+    ((FakeStream*)s)->enqueue([ev] { ev->done.store(true, std::memory_order_release); });
+    return Status::OK;
+  }
+  bool event_query(void* e) override { return ((FakeEvent*)e)->done.load(std::memory_order_acquire); }
+  Status event_sync(void* e) override {
+    auto* ev = (FakeEvent*)e;
+    while (!ev->done.load(std::memory_order_acquire)) std::this_thread::yield();
+    return Status::OK;
+  }
+  Status stream_wait_event(void* s, void* e) override {
+    auto* ev = (FakeEvent*)e;
+    if (!s) return event_sync(e);
+    ((FakeStream*)s)->enqueue([ev] {
+      while (!ev->done.load(std::memory_order_acquire)) std::this_thread::yield();
+    });
+    return Status::OK;
+  }
+
+  void run(void* s, std::function<void()> f) {
+    if (s) ((FakeStream*)s)->enqueue(std::move(f));
+    else f();
+  }
+  Status copy_batch(int, const CopyDesc* d, size_t n, void* s, int) override {
+    std::vector<CopyDesc> v(d, d + n);
+    run(s, [v] {
+      for (auto& c : v) memmove((void*)c.dst, (const void*)c.src, c.bytes);
+    });
+    return Status::OK;
+  }
+  Status gather_pages(int, const PageListDesc& d, void* s) override {
+    std::vector<uint32_t> idx(d.idx, d.idx + d.npages);
+    PageListDesc dd = d;
+    run(s, [dd, idx] {
+      for (uint32_t i = 0; i < dd.npages; ++i)
+        memcpy((char*)dd.contig + (uint64_t)i * dd.page_bytes, (char*)dd.base + (uint64_t)idx[i] * dd.page_bytes,
+               dd.page_bytes);
+    });
+    return Status::OK;
+  }
+  Status scatter_pages(int, const PageListDesc& d, void* s) override {
+    std::vector<uint32_t> idx(d.idx, d.idx + d.npages);
+    PageListDesc dd = d;
+    run(s, [dd, idx] {
+      for (uint32_t i = 0; i < dd.npages; ++i)
+        memcpy((char*)dd.base + (uint64_t)idx[i] * dd.page_bytes, (char*)dd.contig + (uint64_t)i * dd.page_bytes,
+               dd.page_bytes);
+    });
+    return Status::OK;
+  }
+  Status memset32(int, uint64_t dst, uint32_t pat, size_t bytes, void* s) override {
+    run(s, [dst, pat, bytes] {
+      uint32_t* p = (uint32_t*)dst;
+      for (size_t i = 0; i < bytes / 4; ++i) p[i] = pat;
+    });
+    return Status::OK;
+  }
+  Status signal(int, uint64_t* addr, uint64_t v, void* s) override {
+    run(s, [addr, v] { __atomic_store_n(addr, v, __ATOMIC_RELEASE); });
+    return Status::OK;
+  }
+  Status wait_value(void* s, uint64_t* addr, uint64_t v) override {
+    auto f = [addr, v] {
+      while (__atomic_load_n(addr, __ATOMIC_ACQUIRE) < v) std::this_thread::yield();
+    };
+    run(s, f);
+    return Status::OK;
+  }
+
+  LinkType link_type(int a, int b) override { return a == b ? LinkType::SELF : LinkType::XGMI; }
+  bool can_access_peer(int a, int b) override { return a != b && a < ndev_ && b < ndev_; }
+  Status enable_peer(int a, int b) override { return can_access_peer(a, b) ? Status::OK : Status::NOT_SUPPORTED; }
+
+  Status export_dmabuf(void*, size_t, int*, uint64_t*) override { return Status::NOT_SUPPORTED; }
+  Status ipc_handle(void* p, std::string* h) override {
+    char b[32];
+    snprintf(b, sizeof b, "fake:%llx", (unsigned long long)(uintptr_t)p);
+    *h = b;
+    return Status::OK;
+  }
+  Status ipc_open(const std::string& h, void** p) override {
+    if (h.rfind("fake:", 0) != 0) return Status::INVALID_ARGUMENT;
+    *p = (void*)(uintptr_t)strtoull(h.c_str() + 5, nullptr, 16);
+    return Status::OK;
+  }
+  void ipc_close(void*) override {}
+
+ private:
+  int ndev_;
+  size_t hbm_;
+  std::vector<size_t> used_;
+  std::mutex m_;
+  std::map<uint64_t, std::pair<int, size_t>> handles_;
+  std::map<void*, size_t> coherent_;
+};
+
+}  // namespace
+
+std::unique_ptr<Backend> make_fake_backend(int ndev, size_t hbm) {
+  return std::unique_ptr<Backend>(new FakeBackend(ndev, hbm));
+}
+
+std::unique_ptr<Backend> make_backend(const std::string& want) {
+  if (want != "fake") {
+    auto b = make_hip_backend();
+    if (b) return b;
+    if (want == "hip") return nullptr;
+  }
+  const char* nd = getenv("RT_FAKE_DEVICES");
+  const char* hb = getenv("RT_FAKE_HBM_MB");
+  return make_fake_backend(nd ? atoi(nd) : 2, (size_t)(hb ? atoll(hb) : 256) << 20);
+}
+
+}  // namespace ogkm

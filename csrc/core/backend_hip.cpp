@@ -1,0 +1,334 @@
+// HipBackend: MI355X (gfx950) implementation of the runtime HAL.
+//
+// * HBM: one hipMalloc slab per GPU (default) or 2 MB hipMemCreate handles
+//   (VMM provider) mapped at an alias VA.
+// * Host / CXL tiers: memfd pages registered with hipHostRegister (IOMMU-correct
+//   device mapping, identity address) - never raw physical addresses (fixes the
+//   reference's SKIP_IOMMU_MAPPING memdesc, p2p_cxl.c:167-217).
+// * Copies: hand-written copy kernels on side streams (engine 0) or SDMA via
+//   hipMemcpyAsync (engine 1, comparator only).
+// * Completion: k_signal system-scope release into host-coherent memory;
+//   GPU-side waits with hipStreamWaitValue64 / hipStreamWaitEvent.
+#include <hip/hip_runtime.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "ogkm/backend.hpp"
+#include "ogkm/config.hpp"
+#include "ogkm/kernels.hpp"
+
+namespace ogkm {
+
+namespace {
+
+#define HIPCHK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      RT_ERR("%s failed: %s", #expr, hipGetErrorString(e_));                           \
+      last_err_ = hipGetErrorString(e_);                                               \
+      return Status::IO_ERROR;                                                         \
+    }                                                                                  \
+  } while (0)
+
+class HipBackend : public Backend {
+ public:
+  explicit HipBackend(int n) : ndev_(n) {}
+  const char* name() const override { return "hip"; }
+  bool is_fake() const override { return false; }
+  int device_count() override { return ndev_; }
+
+  int device_numa_node(int dev) override {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) return 0;
+    for (char* p = bus; *p; ++p) *p = (char)tolower(*p);
+    std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return 0;
+    int n = 0;
+    if (fscanf(f, "%d", &n) != 1) n = 0;
+    fclose(f);
+    return n < 0 ? 0 : n;
+  }
+  Status device_mem_info(int dev, size_t* f, size_t* t) override {
+    HIPCHK(hipSetDevice(dev));
+    HIPCHK(hipMemGetInfo(f, t));
+    return Status::OK;
+  }
+  Status set_device(int dev) override {
+    HIPCHK(hipSetDevice(dev));
+    return Status::OK;
+  }
+
+  Status hbm_alloc(int dev, size_t bytes, void** p) override {
+    HIPCHK(hipSetDevice(dev));
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+      (void)hipGetLastError();
+      return Status::NO_MEMORY;
+    }
+    HIPCHK(e);
+    return Status::OK;
+  }
+  void hbm_free(int dev, void* p, size_t) override {
+    if (!p) return;
+    (void)hipSetDevice(dev);
+    (void)hipFree(p);
+  }
+
+  bool vmm_supported(int dev) override {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeVirtualMemoryManagementSupported, dev) != hipSuccess) return false;
+    return v != 0;
+  }
+  Status vmm_create(int dev, size_t bytes, uint64_t* h) override {
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    hipMemGenericAllocationHandle_t hh;
+    hipError_t e = hipMemCreate(&hh, bytes, &prop, 0);
+    if (e == hipErrorOutOfMemory) {
+      (void)hipGetLastError();
+      return Status::NO_MEMORY;
+    }
+    HIPCHK(e);
+    *h = (uint64_t)(uintptr_t)hh;
+    return Status::OK;
+  }
+  void vmm_release(uint64_t h) override { (void)hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)h); }
+  Status va_reserve(size_t bytes, void** va) override {
+    HIPCHK(hipMemAddressReserve(va, bytes, kBlockSize, nullptr, 0));
+    return Status::OK;
+  }
+  void va_free(void* va, size_t bytes) override { (void)hipMemAddressFree(va, bytes); }
+  Status vmm_map(void* va, size_t bytes, uint64_t h, int dev) override {
+    HIPCHK(hipMemMap(va, bytes, 0, (hipMemGenericAllocationHandle_t)(uintptr_t)h, 0));
+    hipMemAccessDesc ad = {};
+    ad.location.type = hipMemLocationTypeDevice;
+    ad.location.id = dev;
+    ad.flags = hipMemAccessFlagsProtReadWrite;
+    HIPCHK(hipMemSetAccess(va, bytes, &ad, 1));
+    return Status::OK;
+  }
+  Status vmm_unmap(void* va, size_t bytes) override {
+    HIPCHK(hipMemUnmap(va, bytes));
+    return Status::OK;
+  }
+
+  Status host_register(void* p, size_t bytes) override {
+    HIPCHK(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    return Status::OK;
+  }
+  void host_unregister(void* p) override { (void)hipHostUnregister(p); }
+  Status host_alloc_coherent(size_t bytes, void** p) override {
+    HIPCHK(hipHostMalloc(p, bytes, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+    memset(*p, 0, bytes);
+    return Status::OK;
+  }
+  void host_free_coherent(void* p) override { (void)hipHostFree(p); }
+
+  void* stream_create(int dev, int prio) override {
+    (void)hipSetDevice(dev);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio) != hipSuccess) return nullptr;
+    return s;
+  }
+  void stream_destroy(void* s) override {
+    if (s) (void)hipStreamDestroy((hipStream_t)s);
+  }
+  Status stream_sync(void* s) override {
+    HIPCHK(hipStreamSynchronize((hipStream_t)s));
+    return Status::OK;
+  }
+  void* event_create(int dev) override {
+    std::lock_guard<std::mutex> g(ev_m_);
+    if (dev >= 0 && dev < 64 && !free_events_[dev].empty()) {
+      void* e = free_events_[dev].back();
+      free_events_[dev].pop_back();
+      return e;
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (dev >= 0) (void)hipSetDevice(dev);
+    hipEvent_t e = nullptr;
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (dev >= 0) (void)hipSetDevice(cur);
+    if (r != hipSuccess) return nullptr;
+    ev_dev_[e] = dev;
+    return e;
+  }
+  void event_destroy(void* e) override {
+    std::lock_guard<std::mutex> g(ev_m_);
+    int dev = ev_dev_.count(e) ? ev_dev_[e] : -1;
+    if (dev >= 0 && dev < 64 && free_events_[dev].size() < 4096) {
+      free_events_[dev].push_back(e);
+      return;
+    }
+    ev_dev_.erase(e);
+    (void)hipEventDestroy((hipEvent_t)e);
+  }
+  Status event_record(void* e, void* s) override {
+    HIPCHK(hipEventRecord((hipEvent_t)e, (hipStream_t)s));
+    return Status::OK;
+  }
+  bool event_query(void* e) override { return hipEventQuery((hipEvent_t)e) == hipSuccess; }
+  Status event_sync(void* e) override {
+    HIPCHK(hipEventSynchronize((hipEvent_t)e));
+    return Status::OK;
+  }
+  Status stream_wait_event(void* s, void* e) override {
+    HIPCHK(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0));
+    return Status::OK;
+  }
+
+  Status copy_batch(int dev, const CopyDesc* d, size_t n, void* s, int engine) override {
+    if (n == 0) return Status::OK;
+    if (engine == 1) {  // SDMA comparator
+      for (size_t i = 0; i < n; ++i)
+        HIPCHK(hipMemcpyAsync((void*)d[i].dst, (const void*)d[i].src, d[i].bytes, hipMemcpyDefault, (hipStream_t)s));
+      return Status::OK;
+    }
+    uint32_t piece = (uint32_t)(config().copy_piece_kb * 1024);
+    if (piece < 4096) piece = 4096;
+    uint32_t wgs = (uint32_t)config().copy_workgroups;
+    if (wgs == 0) wgs = 64;
+    for (size_t base = 0; base < n; base += kInlineDescs) {
+      size_t cnt = n - base < (size_t)kInlineDescs ? n - base : (size_t)kInlineDescs;
+      KInlineDescs inl;
+      uint64_t ps = 0;
+      bool hbm_only = engine == 2;
+      for (size_t i = 0; i < cnt; ++i) {
+        inl.d[i] = KCopyDesc{d[base + i].dst, d[base + i].src, d[base + i].bytes};
+        inl.piece_start[i] = ps;
+        ps += (d[base + i].bytes + piece - 1) / piece;
+      }
+      inl.piece_start[cnt] = ps;
+      // HBM<->HBM copies are not PCIe bound: give them the whole chip.
+      uint32_t g = hbm_only ? (wgs * 16 > 2048 ? 2048 : wgs * 16) : wgs;
+      HIPCHK(launch_batch_copy(nullptr, nullptr, &inl, (uint32_t)cnt, ps, piece, g, (hipStream_t)s));
+      launches_++;
+    }
+    return Status::OK;
+  }
+
+  Status page_list(int dev, const PageListDesc& d, void* s, bool scatter) {
+    if (d.npages == 0) return Status::OK;
+    reclaim();
+    void* idx = nullptr;
+    HIPCHK(hipHostMalloc(&idx, d.npages * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocPortable));
+    memcpy(idx, d.idx, d.npages * sizeof(uint32_t));
+    uint32_t wgs = (uint32_t)config().copy_workgroups;
+    HIPCHK(launch_gather_pages(scatter ? d.base : d.base, d.contig, (const uint32_t*)idx, d.npages, d.page_bytes,
+                               scatter, wgs ? wgs : 64, (hipStream_t)s));
+    defer_free(idx, s, dev);
+    return Status::OK;
+  }
+  Status gather_pages(int dev, const PageListDesc& d, void* s) override { return page_list(dev, d, s, false); }
+  Status scatter_pages(int dev, const PageListDesc& d, void* s) override { return page_list(dev, d, s, true); }
+  Status memset32(int, uint64_t dst, uint32_t pat, size_t bytes, void* s) override {
+    HIPCHK(launch_memset32(dst, pat, bytes, (hipStream_t)s));
+    return Status::OK;
+  }
+  Status signal(int, uint64_t* addr, uint64_t v, void* s) override {
+    HIPCHK(launch_signal(addr, v, (hipStream_t)s));
+    return Status::OK;
+  }
+  Status wait_value(void* s, uint64_t* addr, uint64_t v) override {
+    HIPCHK(hipStreamWaitValue64((hipStream_t)s, addr, v, hipStreamWaitValueGte, ~0ull));
+    return Status::OK;
+  }
+
+  LinkType link_type(int a, int b) override {
+    if (a == b) return LinkType::SELF;
+    uint32_t lt = 0, hops = 0;
+    if (hipExtGetLinkTypeAndHopCount(a, b, &lt, &hops) != hipSuccess) return LinkType::NONE;
+    if (lt == HSA_AMD_LINK_INFO_TYPE_XGMI) return LinkType::XGMI;
+    if (lt == HSA_AMD_LINK_INFO_TYPE_PCIE) return LinkType::PCIE;
+    return LinkType::NONE;
+  }
+  bool can_access_peer(int a, int b) override {
+    int v = 0;
+    if (hipDeviceCanAccessPeer(&v, a, b) != hipSuccess) return false;
+    return v != 0;
+  }
+  Status enable_peer(int a, int b) override {
+    HIPCHK(hipSetDevice(a));
+    hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) {
+      (void)hipGetLastError();
+      return Status::OK;
+    }
+    HIPCHK(e);
+    return Status::OK;
+  }
+
+  Status export_dmabuf(void* p, size_t bytes, int* fd, uint64_t* off) override {
+    hsa_status_t s = hsa_amd_portable_export_dmabuf(p, bytes, fd, off);
+    if (s != HSA_STATUS_SUCCESS) {
+      last_err_ = "hsa_amd_portable_export_dmabuf failed";
+      return Status::NOT_SUPPORTED;
+    }
+    return Status::OK;
+  }
+  Status ipc_handle(void* p, std::string* h) override {
+    hipIpcMemHandle_t hh;
+    HIPCHK(hipIpcGetMemHandle(&hh, p));
+    h->assign(reinterpret_cast<const char*>(&hh), sizeof hh);
+    return Status::OK;
+  }
+  Status ipc_open(const std::string& h, void** p) override {
+    if (h.size() != sizeof(hipIpcMemHandle_t)) return Status::INVALID_ARGUMENT;
+    hipIpcMemHandle_t hh;
+    memcpy(&hh, h.data(), sizeof hh);
+    HIPCHK(hipIpcOpenMemHandle(p, hh, hipIpcMemLazyEnablePeerAccess));
+    return Status::OK;
+  }
+  void ipc_close(void* p) override { (void)hipIpcCloseMemHandle(p); }
+  std::string last_error() override { return last_err_; }
+
+ private:
+  void defer_free(void* p, void* s, int dev) {
+    void* e = event_create(dev);
+    if (e) (void)hipEventRecord((hipEvent_t)e, (hipStream_t)s);
+    std::lock_guard<std::mutex> g(df_m_);
+    deferred_.push_back({p, e});
+  }
+  void reclaim() {
+    std::lock_guard<std::mutex> g(df_m_);
+    while (!deferred_.empty()) {
+      auto& f = deferred_.front();
+      if (f.second && hipEventQuery((hipEvent_t)f.second) != hipSuccess) break;
+      (void)hipHostFree(f.first);
+      if (f.second) event_destroy(f.second);
+      deferred_.pop_front();
+    }
+  }
+
+  int ndev_;
+  std::string last_err_;
+  std::mutex ev_m_, df_m_;
+  std::vector<void*> free_events_[64];
+  std::map<void*, int> ev_dev_;
+  std::deque<std::pair<void*, void*>> deferred_;
+  uint64_t launches_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<Backend> make_hip_backend() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return std::unique_ptr<Backend>(new HipBackend(n));
+}
+
+}  // namespace ogkm

@@ -1,0 +1,1172 @@
+// Migration engine: make_resident / populate / evict / acquire / prefetch /
+// fault service / CPU faults.
+//
+// Reference call stacks mirrored here:
+//   service_fault_batch_block_locked  uvm_gpu_replayable_faults.c:1375
+//     -> uvm_perf_thrashing_get_hint  uvm_perf_thrashing.c:1615
+//     -> uvm_va_block_select_residency uvm_va_block.c:11762
+//     -> uvm_va_block_service_locked  uvm_va_block.c:12307 (prefetch hint, copy, finish)
+//   block_populate_pages              uvm_va_block.c:3099   (alloc-retry protocol :2060-2108)
+//   block_copy_resident_pages_between uvm_va_block.c:4069   (run coalescing :4278-4326)
+//   uvm_va_block_evict_chunks         uvm_va_block.c:12999
+//   uvm_migrate                       uvm_migrate.c:635     (two-pass)
+//
+// Lock discipline: VA space (shared) -> one block at a time -> arena -> ring.
+// Eviction never runs with a block lock held: the caller drops its block lock,
+// evicts (locking each victim block individually), and retries - the
+// MORE_PROCESSING_REQUIRED protocol.
+#include <sys/mman.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <thread>
+
+#include "ogkm/runtime.hpp"
+
+namespace ogkm {
+
+namespace {
+
+inline uint64_t page_addr(ChunkArena* a, int64_t chunk, uint32_t page) {
+  return a->chunk_addr((uint32_t)chunk) + ((uint64_t)page << kPageShift);
+}
+
+Counter xfer_counter(const Loc& s, const Loc& d) {
+  if (s.is_gpu() && d.is_gpu()) return Counter::BytesXferDtD;
+  if (!s.is_gpu() && d.is_gpu()) return s.tier == Tier::CXL ? Counter::BytesXferCtD : Counter::BytesXferHtD;
+  if (s.is_gpu() && !d.is_gpu()) return d.tier == Tier::CXL ? Counter::BytesXferDtC : Counter::BytesXferDtH;
+  if (d.tier == Tier::CXL) return Counter::BytesXferHtC;
+  return Counter::BytesXferCtH;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ helpers
+Loc Runtime::demotion_target(const Loc& from) {
+  if (from.is_gpu()) {
+    // Evicted HBM data goes to host DRAM; a CXL preferred location is honoured
+    // by the caller through the block policy.
+    return cpu_loc();
+  }
+  if (from.tier == Tier::HOST) {
+    int n = cxl_topo_.first_node();
+    if (n >= 0) return Loc::cxl(n);
+  }
+  return Loc{Tier::HOST, -1};  // nowhere to go
+}
+
+Status Runtime::alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* first) {
+  if (a->loc().is_gpu()) {
+    int64_t left = inject_.alloc_fail_after.load();
+    if (left == 0) {
+      Tools::get().inc(Counter::InjectedErrors);
+      return Status::NO_MEMORY;
+    }
+    if (left > 0) inject_.alloc_fail_after.fetch_sub(1);
+  } else if (inject_.host_alloc_error.load() > 0 && inject_.host_alloc_error.fetch_sub(1) > 0) {
+    Tools::get().inc(Counter::InjectedErrors);
+    return Status::INJECTED_ERROR;
+  }
+  Status st = a->alloc(n, nullptr, hint, first);
+  if (st == Status::OK && !a->loc().is_gpu()) {
+    st = static_cast<HostArena*>(a)->ensure_registered(*first, n);
+    if (st != Status::OK) a->free(*first, n);
+  }
+  return st;
+}
+
+// Reserve n contiguous chunks, evicting victims (no block lock may be held).
+Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r) {
+  if (a->loc().is_gpu() && !config().global_oversubscription) return Status::NO_MEMORY;
+  Status st = a->reserve(n, r);
+  if (st != Status::OK) return st;
+  for (uint32_t v : r->victims) {
+    Status es = evict_chunk(a, v);
+    if (es != Status::OK) {
+      a->cancel(*r);
+      return es;
+    }
+  }
+  if (!a->loc().is_gpu()) {
+    st = static_cast<HostArena*>(a)->ensure_registered((uint32_t)r->first, r->n);
+    if (st != Status::OK) {
+      a->cancel(*r);
+      return st;
+    }
+  }
+  a->commit(*r);
+  Tools::get().inc(Counter::AllocRetries);
+  return Status::OK;
+}
+
+// Populate: give block b a chunk at location dst (block lock held).
+Status Runtime::populate(Ctx& c, Block* b, Loc dst, int64_t hint, Residency** out) {
+  if (Residency* r = b->find(dst)) {
+    *out = r;
+    return Status::OK;
+  }
+  if (inject_.populate_error.load() > 0 && inject_.populate_error.fetch_sub(1) > 0) {
+    Tools::get().inc(Counter::InjectedErrors);
+    return Status::INJECTED_ERROR;
+  }
+  ChunkArena* a = arena_for(dst);
+  if (!a) return Status::INVALID_ARGUMENT;
+  uint32_t chunk = 0;
+  Status st = alloc_chunks(a, 1, hint, &chunk);
+  if (st == Status::NO_MEMORY) {
+    c.need_arena = a;
+    c.need_n = 1;
+    return Status::MORE_PROCESSING_REQUIRED;
+  }
+  if (st != Status::OK) return st;
+  a->set_owner(chunk, b);
+  Residency& r = b->get_or_add(dst);
+  r.arena = a;
+  r.chunk = chunk;
+  r.resident.zero();
+  *out = &r;
+  return Status::OK;
+}
+
+static Ring* ring_for(Runtime* rt, const Loc& s, const Loc& d) {
+  if (d.is_gpu() && !s.is_gpu()) return rt->ring(d.id, RingKind::CPU_TO_GPU);
+  if (s.is_gpu() && !d.is_gpu()) return rt->ring(s.id, RingKind::GPU_TO_CPU);
+  if (s.is_gpu() && d.is_gpu()) return s.id == d.id ? rt->ring(s.id, RingKind::GPU_INTERNAL)
+                                                    : rt->ring(s.id, RingKind::GPU_TO_GPU);
+  if (config().block_cpu_to_cpu_copy_with_ce && rt->ndev() > 0) return rt->ring(0, RingKind::CPU_TO_GPU);
+  return nullptr;
+}
+
+// Queue copies of `pages` from residency `from` to residency `to` of block b.
+static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from, Residency* to,
+                         const PageMask& pages) {
+  if (pages.empty()) return Status::OK;
+  Ring* ring = ring_for(rt, from->loc, to->loc);
+  Counter ctr = xfer_counter(from->loc, to->loc);
+  uint64_t bytes = (uint64_t)pages.count() << kPageShift;
+  Tools::get().inc(ctr, bytes);
+  if (c.cause == Cause::Prefetch) {
+    if (to->loc.is_gpu()) Tools::get().inc(Counter::PrefetchBytesXferHtD, bytes);
+    else Tools::get().inc(Counter::PrefetchBytesXferDtH, bytes);
+  }
+  uint64_t t0 = now_ns();
+  bool peer_down = from->loc.is_gpu() && to->loc.is_gpu() && from->loc.id != to->loc.id &&
+                   (((rt->inject().peer_link_down.load() >> from->loc.id) & 1) ||
+                    !rt->be()->can_access_peer(to->loc.id, from->loc.id));
+  if (peer_down) {
+    // No peer path: stage GPU->GPU through host memory (uvm_va_block.c:4703-4836).
+    Residency* bounce = nullptr;
+    Loc h = rt->cpu_loc();
+    Status st = rt->populate(c, b, h, -1, &bounce);
+    if (st != Status::OK) return st;
+    PageMask need = pages.andnot(bounce->resident);
+    if (!need.empty()) {
+      st = copy_pages(rt, c, b, from, bounce, need);
+      if (st != Status::OK) return st;
+      Ring* d2h = rt->ring(from->loc.id, RingKind::GPU_TO_CPU);
+      FenceRef f = d2h->submit();
+      b->tracker.add(f);
+      bounce->resident |= need;
+    }
+    return copy_pages(rt, c, b, bounce, to, pages);
+  }
+  // The writer waits for readers of the destination chunk's previous contents
+  // and for pending writes into this block issued on other rings.
+  Tracker reuse = to->arena->take_reuse_fence((uint32_t)to->chunk);
+  Tracker pend = b->tracker;
+  pend.prune();
+  if (!ring) {
+    // CPU <-> CPU (host / CXL tiers): synchronous memcpy.
+    reuse.wait();
+    pend.wait();
+    pages.for_each_run([&](uint32_t p, uint32_t n) {
+      memcpy((void*)page_addr(to->arena, to->chunk, p), (const void*)page_addr(from->arena, from->chunk, p),
+             (uint64_t)n << kPageShift);
+    });
+    tools_event(ToolsEventType::Migration, c.cause, from->loc, to->loc, kCpuProc, b->range->addr() + b->block_offset(),
+                bytes, b->range->id, t0, now_ns());
+    return Status::OK;
+  }
+  for (auto& f : reuse.fences()) {
+    if (f->ring == ring) continue;
+    Sqe w;
+    w.op = SqeOp::WAIT_FENCE;
+    w.wait = f;
+    ring->push(std::move(w));
+  }
+  for (auto& f : pend.fences()) {
+    if (f->ring == ring) continue;
+    Sqe w;
+    w.op = SqeOp::WAIT_FENCE;
+    w.wait = f;
+    ring->push(std::move(w));
+  }
+  pages.for_each_run([&](uint32_t p, uint32_t n) {
+    Sqe s;
+    s.op = SqeOp::COPY;
+    s.dst = page_addr(to->arena, to->chunk, p);
+    s.src = page_addr(from->arena, from->chunk, p);
+    s.bytes = (uint64_t)n << kPageShift;
+    s.user_data = b->range->id;
+    s.file = __FILE__;
+    s.line = __LINE__;
+    if (log_level() >= LogLevel::DEBUG)
+      s.desc = "range " + std::to_string(b->range->id) + " block " + std::to_string(b->index) + " " +
+               from->loc.str() + "->" + to->loc.str();
+    ring->push(std::move(s));
+  });
+  c.use_ring(ring);
+  c.touched.push_back({ring, b});
+  c.chunk_uses.push_back({ring, from->arena, (uint32_t)from->chunk, false});
+  tools_event(ToolsEventType::Migration, c.cause, from->loc, to->loc, to->loc.is_gpu() ? to->loc.id : kCpuProc,
+              b->range->addr() + b->block_offset(), bytes, b->range->id, t0, 0, ring->pushed_seq());
+  return Status::OK;
+}
+
+static Status zero_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* to, const PageMask& pages) {
+  if (pages.empty()) return Status::OK;
+  if (!to->loc.is_gpu()) {
+    Tracker reuse = to->arena->take_reuse_fence((uint32_t)to->chunk);
+    reuse.wait();
+    pages.for_each_run([&](uint32_t p, uint32_t n) {
+      memset((void*)page_addr(to->arena, to->chunk, p), 0, (uint64_t)n << kPageShift);
+    });
+    return Status::OK;
+  }
+  Ring* ring = rt->ring(to->loc.id, RingKind::CPU_TO_GPU);
+  Tracker reuse = to->arena->take_reuse_fence((uint32_t)to->chunk);
+  for (auto& f : reuse.fences()) {
+    if (f->ring == ring) continue;
+    Sqe w;
+    w.op = SqeOp::WAIT_FENCE;
+    w.wait = f;
+    ring->push(std::move(w));
+  }
+  pages.for_each_run([&](uint32_t p, uint32_t n) {
+    Sqe s;
+    s.op = SqeOp::MEMSET;
+    s.dst = page_addr(to->arena, to->chunk, p);
+    s.bytes = (uint64_t)n << kPageShift;
+    s.pattern = 0;
+    s.file = __FILE__;
+    s.line = __LINE__;
+    ring->push(std::move(s));
+  });
+  c.use_ring(ring);
+  c.touched.push_back({ring, b});
+  return Status::OK;
+}
+
+// Release a residency whose pages are all gone (chunk freed after queued readers).
+static void drop_residency(Runtime::Ctx& c, Block* b, const Loc& l) {
+  Residency* r = b->find(l);
+  if (!r) return;
+  if (r->chunk >= 0) {
+    bool queued = false;
+    for (auto& u : c.chunk_uses)
+      if (u.arena == r->arena && u.chunk == (uint32_t)r->chunk) {
+        u.free_after = true;
+        queued = true;
+        break;
+      }
+    if (queued) {
+      // Still read by a queued copy: detach and pin (not an eviction victim)
+      // until finish_ctx frees it behind the copy's fence.
+      r->arena->set_owner((uint32_t)r->chunk, nullptr);
+      r->arena->pin((uint32_t)r->chunk);
+    } else {
+      Tracker t = b->tracker;  // pending writers into the chunk
+      for (auto& f : t.fences()) r->arena->add_reuse_fence((uint32_t)r->chunk, f);
+      r->arena->free((uint32_t)r->chunk, 1);
+    }
+  }
+  b->drop(l);
+}
+
+// Make `pages` of block b resident at dst (block lock held).
+Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc dst, bool read_dup, Cause cause) {
+  PageMask pages = pages_in & b->valid_pages();
+  if (pages.empty()) return Status::OK;
+  c.cause = cause;
+  Residency* to = nullptr;
+  int64_t hint = -1;
+  // Keep a range's blocks adjacent in the destination arena.
+  if (b->index > 0) {
+    Block* prev = b->range->block(b->index - 1);
+    // Reading the neighbour's residency without its lock is a heuristic only.
+    if (prev)
+      for (auto& r : prev->res)
+        if (r.loc == dst && r.chunk >= 0) hint = r.chunk + 1;
+  }
+  Status st = populate(c, b, dst, hint, &to);
+  if (st != Status::OK) return st;
+  PageMask missing = pages.andnot(to->resident);
+  if (!missing.empty()) {
+    // Source = closest resident copy per page: same tier first, then HBM peers,
+    // then host, then CXL.
+    std::vector<Residency*> srcs;
+    for (auto& r : b->res)
+      if (&r != to) srcs.push_back(&r);
+    auto rank = [&](Residency* r) {
+      if (r->loc.is_gpu()) return r->loc.id == dst.id && dst.is_gpu() ? 0 : 1;
+      return r->loc.tier == Tier::HOST ? 2 : 3;
+    };
+    std::sort(srcs.begin(), srcs.end(), [&](Residency* a, Residency* x) { return rank(a) < rank(x); });
+    PageMask left = missing;
+    for (Residency* s : srcs) {
+      PageMask from_here = left & s->resident;
+      if (from_here.empty()) continue;
+      st = copy_pages(this, c, b, s, to, from_here);
+      if (st != Status::OK) return st;
+      left = left.andnot(from_here);
+      if (left.empty()) break;
+    }
+    // Never-populated pages are zero-filled (uvm_va_block.c:2863).
+    if (!left.empty()) {
+      st = zero_pages(this, c, b, to, left);
+      if (st != Status::OK) return st;
+    }
+    to->resident |= missing;
+  }
+  if (!read_dup) {
+    bool moved = false;
+    for (auto& r : b->res)
+      if (!(r.loc == dst) && r.resident.intersects(pages)) moved = true;
+    if (moved && cause != Cause::Eviction) thrash_on_migration(b, dst.slot(), now_ns());
+    // Migration: invalidate every other copy of these pages (revocation).
+    std::vector<Loc> empty_locs;
+    for (auto& r : b->res) {
+      if (&r == to) continue;
+      if (r.resident.intersects(pages)) {
+        if (!r.loc.is_gpu() || !dst.is_gpu()) Tools::get().inc(Counter::Revocations, 0);
+        r.resident = r.resident.andnot(pages);
+        if (r.resident.empty()) empty_locs.push_back(r.loc);
+      }
+    }
+    // `to` may move when residencies are dropped: remember by location.
+    for (auto& l : empty_locs) drop_residency(c, b, l);
+  } else {
+    Tools::get().inc(Counter::ReadDuplications);
+    tools_event(ToolsEventType::ReadDuplicate, cause, Loc::host(0), dst, dst.is_gpu() ? dst.id : kCpuProc,
+                b->range->addr() + b->block_offset(), (uint64_t)pages.count() << kPageShift, b->range->id);
+  }
+  Residency* t = b->find(dst);
+  if (t && t->chunk >= 0) {
+    bool pref_here = b->policy.has_preferred && b->policy.preferred == dst;
+    (void)pref_here;
+    t->arena->touch((uint32_t)t->chunk, true);
+  }
+  b->last_access_ns = now_ns();
+  c.cpu_refresh.push_back(b);
+  Tools::get().bus().notify(PerfEventData{PerfEvent::MIGRATION, b->range->id, b->index, Loc{}, dst, 0,
+                                          (uint64_t)pages.count() << kPageShift, (int)cause, 0, 0, false});
+  return Status::OK;
+}
+
+// Submit every ring used by the context and publish fences to blocks / chunks.
+void Runtime::finish_ctx(Ctx& c, Tracker* out) {
+  std::vector<std::pair<Ring*, FenceRef>> fences;
+  for (Ring* r : c.rings) fences.emplace_back(r, r->submit());
+  auto fence_of = [&](Ring* r) -> FenceRef {
+    for (auto& f : fences)
+      if (f.first == r) return f.second;
+    return nullptr;
+  };
+  for (auto& t : c.touched) {
+    FenceRef f = fence_of(t.ring);
+    if (!f) continue;
+    std::lock_guard<OrderedMutex> g(t.block->lock);
+    t.block->tracker.add(f);
+  }
+  for (auto& u : c.chunk_uses) {
+    FenceRef f = fence_of(u.ring);
+    if (f) u.arena->add_reuse_fence(u.chunk, f);
+    if (u.free_after) {
+      u.arena->unpin(u.chunk);
+      u.arena->free(u.chunk, 1);
+    }
+  }
+  if (out)
+    for (auto& f : fences) out->add(f.second);
+  for (Block* b : c.cpu_refresh) {
+    std::lock_guard<OrderedMutex> g(b->lock);
+    cpu_map_block(b);
+    update_device_table(b);
+    if (b->range->dev_va) stable_map_block(b);
+  }
+  c = Ctx{};
+}
+
+// ------------------------------------------------------------------ eviction
+// Evict chunk `i` of arena `a` (EVICTING state). No block lock may be held.
+Status Runtime::evict_chunk(ChunkArena* a, uint32_t i) {
+  if (inject_.evict_fail.load() > 0 && inject_.evict_fail.fetch_sub(1) > 0) {
+    Tools::get().inc(Counter::InjectedErrors);
+    return Status::INJECTED_ERROR;
+  }
+  Block* b = a->owner(i);
+  if (!b) {
+    a->evicted(i);
+    return Status::OK;
+  }
+  Ctx c;
+  c.cause = Cause::Eviction;
+  Status st = Status::OK;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    {
+      std::lock_guard<OrderedMutex> g(b->lock);
+      Residency* r = nullptr;
+      for (auto& x : b->res)
+        if (x.arena == a && x.chunk == (int64_t)i) r = &x;
+      if (!r) {
+        a->evicted(i);
+        return Status::OK;
+      }
+      if (b->lease_pins || b->user_pins) return Status::BUSY;
+      PageMask others;
+      for (auto& x : b->res)
+        if (&x != r) others |= x.resident;
+      PageMask only_here = r->resident.andnot(others);
+      Loc from = r->loc;
+      uint64_t bytes = (uint64_t)r->resident.count() << kPageShift;
+      if (!only_here.empty()) {
+        Loc dst = demotion_target(from);
+        // Honour a host/CXL preferred location for evicted HBM data.
+        if (from.is_gpu() && b->policy.has_preferred && !b->policy.preferred.is_gpu()) dst = b->policy.preferred;
+        if (dst.id < 0) return Status::NO_MEMORY;
+        Residency* to = nullptr;
+        st = populate(c, b, dst, -1, &to);
+        if (st == Status::MORE_PROCESSING_REQUIRED) goto retry;
+        if (st != Status::OK) return st;
+        r = nullptr;
+        for (auto& x : b->res)
+          if (x.arena == a && x.chunk == (int64_t)i) r = &x;
+        st = copy_pages(this, c, b, r, to, only_here);
+        if (st != Status::OK) return st;
+        to->resident |= only_here;
+        c.cpu_refresh.push_back(b);
+      }
+      // Detach the chunk from the block; the arena keeps it reserved for the
+      // evicting allocator, fenced on the copy-out.
+      Tracker pend = b->tracker;
+      b->drop(from);
+      c.cpu_refresh.push_back(b);
+      for (auto& f : pend.fences()) a->add_reuse_fence(i, f);
+      Tools::get().inc(Counter::Evictions);
+      Tools::get().inc(Counter::EvictedBytes, bytes);
+      tools_event(ToolsEventType::Eviction, Cause::Eviction, from, demotion_target(from), kCpuProc,
+                  b->range->addr() + b->block_offset(), bytes, b->range->id);
+      Tools::get().bus().notify(PerfEventData{PerfEvent::MIGRATION, b->range->id, b->index, from,
+                                              demotion_target(from), kCpuProc, bytes, (int)Cause::Eviction});
+    }
+    // Fences for the copy-out are published by finish_ctx; the chunk itself
+    // is handed to the reserver (evicted), not freed.
+    {
+      std::vector<std::pair<Ring*, FenceRef>> fs;
+      for (Ring* rr : c.rings) fs.emplace_back(rr, rr->submit());
+      for (auto& f : fs) a->add_reuse_fence(i, f.second);
+      for (auto& u : c.chunk_uses)
+        if (u.arena == a && u.chunk == i) u.arena = nullptr;  // the evicted chunk is not freed
+      c.chunk_uses.erase(std::remove_if(c.chunk_uses.begin(), c.chunk_uses.end(),
+                                        [](const Ctx::ChunkUse& u) { return u.arena == nullptr; }),
+                         c.chunk_uses.end());
+      a->evicted(i);
+      finish_ctx(c, nullptr);
+    }
+    return Status::OK;
+  retry:
+    if (c.need_arena) {
+      Reservation rr;
+      Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+      if (es != Status::OK) return es;
+      c.need_arena->free((uint32_t)rr.first, rr.n);
+      c.need_arena = nullptr;
+    }
+  }
+  return Status::NO_MEMORY;
+}
+
+// ------------------------------------------------------------------ prefetch / migrate
+Status Runtime::prefetch(Range* r, uint64_t off, uint64_t len, Loc dst, Tracker* out, Cause cause) {
+  if (global_status() != Status::OK) return global_status();
+  if (!r || off + len > r->size || len == 0) return Status::INVALID_ARGUMENT;
+  if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
+  if (!arena_for(dst)) return Status::INVALID_ARGUMENT;
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  if (r->group && !r->group->migratable) return Status::BUSY;
+  uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
+  Ctx c;
+  c.cause = cause;
+  Status st = Status::OK;
+  for (uint64_t bi = b0; bi <= b1 && st == Status::OK; ++bi) {
+    Block* b = r->block(bi);
+    uint64_t lo = std::max(off, bi << kBlockShift) - (bi << kBlockShift);
+    uint64_t hi = std::min(off + len, (bi + 1) << kBlockShift) - (bi << kBlockShift);
+    PageMask pages = PageMask::range((uint32_t)(lo >> kPageShift), (uint32_t)((hi + kPageSize - 1 - lo) >> kPageShift));
+    for (int attempt = 0; attempt < 8; ++attempt) {
+      {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        if (b->user_pins) {
+          st = Status::BUSY;
+          break;
+        }
+        bool dup = b->policy.read_dup;
+        st = make_resident(c, b, pages, dst, dup, cause);
+      }
+      if (st != Status::MORE_PROCESSING_REQUIRED) break;
+      // Submit what we have so far, then evict outside the block lock.
+      finish_ctx(c, out);
+      Reservation rr;
+      Status es = ensure_capacity(c.need_arena ? c.need_arena : arena_for(dst), c.need_n ? c.need_n : 1, &rr);
+      if (es != Status::OK) {
+        st = es;
+        break;
+      }
+      ChunkArena* a = c.need_arena ? c.need_arena : arena_for(dst);
+      a->free((uint32_t)rr.first, rr.n);
+      c.need_arena = nullptr;
+    }
+  }
+  finish_ctx(c, out);
+  return st;
+}
+
+Status Runtime::migrate_sync(Range* r, uint64_t off, uint64_t len, Loc dst) {
+  // Two-pass scheme (uvm_migrate.c:674-722): pass 1 queues every block's copy,
+  // pass 2 waits and establishes mappings.
+  Tracker t;
+  Status st = prefetch(r, off, len, dst, &t, Cause::ApiMigrate);
+  Status w = t.wait();
+  if (st == Status::OK) st = w;
+  if (st == Status::OK) {
+    std::shared_lock<OrderedRWLock> vg(vs_.lock);
+    uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
+    for (uint64_t bi = b0; bi <= b1; ++bi) {
+      Block* b = r->block(bi);
+      std::lock_guard<OrderedMutex> g(b->lock);
+      b->tracker.prune();
+      cpu_map_block(b);
+    }
+  }
+  return st;
+}
+
+Status Runtime::evict_range(Range* r, Loc from) {
+  if (!r) return Status::INVALID_ARGUMENT;
+  ChunkArena* a = arena_for(from);
+  if (!a) return Status::INVALID_ARGUMENT;
+  std::vector<uint32_t> chunks;
+  {
+    std::shared_lock<OrderedRWLock> vg(vs_.lock);
+    for (auto& bp : r->blocks) {
+      std::lock_guard<OrderedMutex> g(bp->lock);
+      if (Residency* x = bp->find(from))
+        if (x->chunk >= 0) chunks.push_back((uint32_t)x->chunk);
+    }
+  }
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  for (uint32_t ch : chunks) {
+    // Re-check through the reservation path: move the chunk to EVICTING.
+    Reservation rr;
+    rr.first = ch;
+    rr.n = 1;
+    // Explicit eviction: evict the owner block's data, then free the chunk.
+    Block* b = a->owner(ch);
+    if (!b) continue;
+    Ctx c;
+    c.cause = Cause::Eviction;
+    Status st;
+    {
+      std::lock_guard<OrderedMutex> g(b->lock);
+      if (b->lease_pins || b->user_pins) return Status::BUSY;
+      Residency* x = b->find(from);
+      if (!x || x->chunk != (int64_t)ch) continue;
+      PageMask others;
+      for (auto& y : b->res)
+        if (&y != x) others |= y.resident;
+      PageMask only_here = x->resident.andnot(others);
+      if (!only_here.empty()) {
+        Loc dst = demotion_target(from);
+        if (from.is_gpu() && b->policy.has_preferred && !b->policy.preferred.is_gpu()) dst = b->policy.preferred;
+        if (dst.id < 0) return Status::NO_MEMORY;
+        st = make_resident(c, b, only_here, dst, false, Cause::Eviction);
+        if (st != Status::OK) {
+          finish_ctx(c, nullptr);
+          return st;
+        }
+      }
+      // Any pages still only at `from` have been migrated; drop the rest (duplicates).
+      if (b->find(from)) {
+        Residency* y = b->find(from);
+        y->resident.zero();
+        drop_residency(c, b, from);
+      }
+      Tools::get().inc(Counter::Evictions);
+    }
+    finish_ctx(c, nullptr);
+  }
+  return Status::OK;
+}
+
+// ------------------------------------------------------------------ leases
+Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out) {
+  if (global_status() != Status::OK) return global_status();
+  if (quiesced_.load()) return Status::BUSY;
+  if (!r || len == 0 || off + len > r->size) return Status::INVALID_ARGUMENT;
+  if (proc != kCpuProc && (proc < 0 || proc >= ndev())) return Status::INVALID_ARGUMENT;
+  auto L = std::make_unique<Lease>();
+  L->range = r;
+  L->offset = off;
+  L->bytes = len;
+  L->proc = proc;
+  if (r->type == RangeType::EXTERNAL || r->type == RangeType::DEVICE_P2P) {
+    // Foreign / device-P2P memory never migrates: lease the original pointer.
+    L->dptr = r->ext_ptr + off;
+    L->remote = r->ext_dev != proc;
+  } else {
+    std::shared_lock<OrderedRWLock> vg(vs_.lock);
+    uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
+    uint32_t n = (uint32_t)(b1 - b0 + 1);
+    Tools::get().inc(proc == kCpuProc ? Counter::CpuPageFaultCount : Counter::GpuPageFaultCount, n);
+    auto pages_of = [&](uint64_t bi) {
+      uint64_t lo = std::max(off, bi << kBlockShift) - (bi << kBlockShift);
+      uint64_t hi = std::min(off + len, (bi + 1) << kBlockShift) - (bi << kBlockShift);
+      return PageMask::range((uint32_t)(lo >> kPageShift), (uint32_t)((hi - lo + kPageSize - 1 + (lo & (kPageSize - 1))) >> kPageShift));
+    };
+    Loc dst = proc_loc(proc);
+    // 1) residency decisions
+    bool all_remote = proc != kCpuProc;
+    std::vector<ResidencyDecision> dec(n);
+    for (uint32_t k = 0; k < n; ++k) {
+      Block* b = r->block(b0 + k);
+      std::lock_guard<OrderedMutex> g(b->lock);
+      dec[k] = select_residency(this, b, proc, access, pages_of(b0 + k));
+      if (!dec[k].map_remote) all_remote = false;
+    }
+    Ctx c;
+    Status st = Status::OK;
+    if (proc == kCpuProc) {
+      // CPU lease: the CPU view is the pointer; make pages resident on a
+      // CPU-accessible tier and map them.
+      for (uint32_t k = 0; k < n && st == Status::OK; ++k) {
+        Block* b = r->block(b0 + k);
+        for (int attempt = 0; attempt < 8; ++attempt) {
+          {
+            std::lock_guard<OrderedMutex> g(b->lock);
+            Loc d = dec[k].map_remote ? dec[k].dst : (dec[k].dst.is_gpu() ? cpu_loc() : dec[k].dst);
+            st = make_resident(c, b, pages_of(b0 + k), d, dec[k].read_dup, Cause::User);
+            if (st == Status::OK) b->lease_pins++;
+          }
+          if (st != Status::MORE_PROCESSING_REQUIRED) break;
+          finish_ctx(c, nullptr);
+          Reservation rr;
+          Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+          if (es != Status::OK) {
+            st = es;
+            break;
+          }
+          c.need_arena->free((uint32_t)rr.first, rr.n);
+        }
+        if (st == Status::OK) L->blocks.push_back(b);
+      }
+      finish_ctx(c, &L->ready);
+      L->ready.wait();
+      for (Block* b : L->blocks) {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        b->tracker.prune();
+        cpu_map_block(b);
+      }
+      L->dptr = r->addr() + off;
+      if (st != Status::OK) {
+        for (Block* b : L->blocks) {
+          std::lock_guard<OrderedMutex> g(b->lock);
+          b->lease_pins--;
+        }
+        return st;
+      }
+    } else if (all_remote) {
+      // Remote (zero-copy) lease: the data stays where it is and the GPU reads it
+      // over PCIe/xGMI. Requires the remote copy to be contiguous.
+      int64_t first = -1;
+      ChunkArena* ra = nullptr;
+      bool contiguous = true;
+      for (uint32_t k = 0; k < n && st == Status::OK; ++k) {
+        Block* b = r->block(b0 + k);
+        for (int attempt = 0; attempt < 8; ++attempt) {
+          {
+            std::lock_guard<OrderedMutex> g(b->lock);
+            int64_t hint = first >= 0 ? first + k : -1;
+            Residency* x = b->find(dec[k].dst);
+            if (!x) {
+              st = populate(c, b, dec[k].dst, hint, &x);
+              if (st == Status::OK) {
+                c.cpu_refresh.push_back(b);
+              }
+            }
+            if (st == Status::OK) {
+              PageMask need = pages_of(b0 + k).andnot(x->resident);
+              if (!need.empty()) st = make_resident(c, b, need, dec[k].dst, true, Cause::User);
+              x = b->find(dec[k].dst);
+            }
+            if (st == Status::OK) {
+              if (k == 0) {
+                first = x->chunk;
+                ra = x->arena;
+              } else if (x->arena != ra || x->chunk != first + k) {
+                contiguous = false;
+              }
+              b->lease_pins++;
+              x->arena->pin((uint32_t)x->chunk);
+              L->pinned_chunks.emplace_back(x->arena, (uint32_t)x->chunk);
+              L->blocks.push_back(b);
+              if (b->thrash.detected) Tools::get().inc(Counter::MapRemote);
+            }
+          }
+          if (st != Status::MORE_PROCESSING_REQUIRED) break;
+          finish_ctx(c, nullptr);
+          Reservation rr;
+          Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+          if (es != Status::OK) {
+            st = es;
+            break;
+          }
+          c.need_arena->free((uint32_t)rr.first, rr.n);
+        }
+      }
+      finish_ctx(c, &L->ready);
+      if (st == Status::OK && !contiguous) {
+        // Fall back to a local copy.
+        for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
+        for (Block* b : L->blocks) {
+          std::lock_guard<OrderedMutex> g(b->lock);
+          b->lease_pins--;
+        }
+        L->pinned_chunks.clear();
+        L->blocks.clear();
+        all_remote = false;
+        for (auto& d : dec) d.map_remote = false;
+      } else if (st == Status::OK) {
+        L->remote = true;
+        L->dptr = ra->chunk_addr((uint32_t)first) + (off - (b0 << kBlockShift));
+        for (Block* b : L->blocks) {
+          std::lock_guard<OrderedMutex> g(b->lock);
+          L->ready.merge(b->tracker);
+        }
+        Tools::get().inc(Counter::MapRemote, n);
+      } else {
+        for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
+        for (Block* b : L->blocks) {
+          std::lock_guard<OrderedMutex> g(b->lock);
+          b->lease_pins--;
+        }
+        return st;
+      }
+    }
+    if (proc != kCpuProc && !all_remote) {
+      // Local GPU lease: the blocks must occupy n consecutive HBM chunks.
+      ChunkArena* ga = arena_for(dst);
+      if (!ga) return Status::INVALID_ARGUMENT;
+      int64_t first = -1;
+      bool in_place = true;
+      {
+        // Are the blocks already laid out contiguously (or extendable in place)?
+        int64_t c0 = -1;
+        for (uint32_t k = 0; k < n && in_place; ++k) {
+          Block* b = r->block(b0 + k);
+          std::lock_guard<OrderedMutex> g(b->lock);
+          Residency* x = b->find(dst);
+          if (!x) {
+            in_place = false;
+            break;
+          }
+          if (k == 0) c0 = x->chunk;
+          else if (x->chunk != c0 + k) in_place = false;
+        }
+        if (in_place) first = c0;
+      }
+      Reservation rv;
+      if (!in_place) {
+        // Fresh extent for all n blocks: free run, else evict LRU victims.
+        uint32_t f = 0;
+        st = alloc_chunks(ga, n, -1, &f);
+        if (st == Status::OK) {
+          rv.first = f;
+          rv.n = n;
+        } else if (st == Status::NO_MEMORY) {
+          st = ensure_capacity(ga, n, &rv);
+        }
+        if (st != Status::OK) return st;
+        first = rv.first;
+      }
+      for (uint32_t k = 0; k < n && st == Status::OK; ++k) {
+        Block* b = r->block(b0 + k);
+        uint32_t target = (uint32_t)(first + k);
+        for (int attempt = 0; attempt < 8; ++attempt) {
+          {
+            std::lock_guard<OrderedMutex> g(b->lock);
+            Residency* x = b->find(dst);
+            if (x && x->chunk != (int64_t)target) {
+              // Relocate: copy the resident pages into the new extent (D2D).
+              ga->set_owner(target, b);
+              Residency tmp;
+              tmp.slot = x->slot;
+              tmp.loc = dst;
+              tmp.arena = ga;
+              tmp.chunk = target;
+              st = copy_pages(this, c, b, x, &tmp, x->resident);
+              if (st == Status::OK) {
+                // mark the old chunk for freeing after the copy
+                bool queued = false;
+                for (auto& u : c.chunk_uses)
+                  if (u.arena == x->arena && u.chunk == (uint32_t)x->chunk && !u.free_after) {
+                    u.free_after = true;
+                    x->arena->set_owner((uint32_t)x->chunk, nullptr);
+                    x->arena->pin((uint32_t)x->chunk);
+                    queued = true;
+                    break;
+                  }
+                if (!queued) x->arena->free((uint32_t)x->chunk, 1);
+                x->chunk = target;
+                x->arena = ga;
+              }
+            } else if (!x) {
+              ga->set_owner(target, b);
+              Residency& nr = b->get_or_add(dst);
+              nr.arena = ga;
+              nr.chunk = target;
+              nr.resident.zero();
+            } else {
+              ga->set_owner(target, b);
+            }
+            if (st == Status::OK) {
+              PageMask want = pages_of(b0 + k);
+              // Prefetch hint: grow the request inside the block (51% rule).
+              if (config().perf_prefetch_enable && proc != kCpuProc) {
+                Residency* y = b->find(dst);
+                PageMask hint = prefetch_hint(y->resident, want, b->npages, (uint32_t)config().perf_prefetch_threshold);
+                PageMask populated = b->resident_anywhere();
+                want |= (hint & populated);
+              }
+              st = make_resident(c, b, want, dst, dec[k].read_dup, c.cause);
+            }
+            if (st == Status::OK) {
+              Residency* y = b->find(dst);
+              b->lease_pins++;
+              y->arena->pin((uint32_t)y->chunk);
+              L->pinned_chunks.emplace_back(y->arena, (uint32_t)y->chunk);
+              L->blocks.push_back(b);
+              if (b->policy.has_preferred && b->policy.preferred == dst) y->arena->touch((uint32_t)y->chunk, true);
+            }
+          }
+          if (st != Status::MORE_PROCESSING_REQUIRED) break;
+          finish_ctx(c, nullptr);
+          Reservation rr;
+          Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+          if (es != Status::OK) {
+            st = es;
+            break;
+          }
+          c.need_arena->free((uint32_t)rr.first, rr.n);
+          c.need_arena = nullptr;
+        }
+      }
+      finish_ctx(c, &L->ready);
+      if (st != Status::OK) {
+        for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
+        for (Block* b : L->blocks) {
+          std::lock_guard<OrderedMutex> g(b->lock);
+          b->lease_pins--;
+        }
+        return st;
+      }
+      for (Block* b : L->blocks) {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        L->ready.merge(b->tracker);
+      }
+      L->dptr = ga->chunk_addr((uint32_t)first) + (off - (b0 << kBlockShift));
+    }
+  }
+  r->views.fetch_add(1);
+  std::lock_guard<std::mutex> g(leases_m_);
+  L->id = next_lease_++;
+  *out = L.get();
+  leases_[L->id] = std::move(L);
+  return Status::OK;
+}
+
+Status Runtime::release(Lease* l, void* stream) {
+  if (!l) return Status::INVALID_ARGUMENT;
+  std::unique_ptr<Lease> own;
+  {
+    std::lock_guard<std::mutex> g(leases_m_);
+    auto it = leases_.find(l->id);
+    if (it == leases_.end()) return Status::NOT_FOUND;
+    own = std::move(it->second);
+    leases_.erase(it);
+  }
+  FenceRef f;
+  if (l->proc != kCpuProc && !l->pinned_chunks.empty()) f = fence_record(be_.get(), l->proc, stream);
+  for (auto& pc : l->pinned_chunks) {
+    if (f) pc.first->add_reuse_fence(pc.second, f);
+    pc.first->unpin(pc.second);
+    pc.first->touch(pc.second, true);
+  }
+  {
+    std::shared_lock<OrderedRWLock> vg(vs_.lock);
+    for (Block* b : l->blocks) {
+      std::lock_guard<OrderedMutex> g(b->lock);
+      if (b->lease_pins) b->lease_pins--;
+      if (f && l->proc != kCpuProc) {
+        // GPU readers of this block: a later migration away must wait for them.
+        b->tracker.add(f);
+      }
+    }
+  }
+  l->range->views.fetch_sub(1);
+  return Status::OK;
+}
+
+Lease* Runtime::lease_by_id(uint64_t id) {
+  std::lock_guard<std::mutex> g(leases_m_);
+  auto it = leases_.find(id);
+  return it == leases_.end() ? nullptr : it->second.get();
+}
+
+// ------------------------------------------------------------------ fault batches
+// Batch service (uvm_parent_gpu_service_replayable_faults, :2906): preprocess
+// (sort by range, block, access; coalesce duplicates), then service per block
+// with thrashing hints, residency selection and prefetch expansion.
+Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
+  if (faults.empty()) return Status::OK;
+  if (global_status() != Status::OK) return global_status();
+  Tools::get().inc(Counter::FaultBatches);
+  for (auto& f : faults) {
+    f.block = f.offset >> kBlockShift;
+    f.first_page = (uint32_t)((f.offset & (kBlockSize - 1)) >> kPageShift);
+    uint64_t end = std::min<uint64_t>(f.offset + std::max<uint64_t>(f.bytes, 1), (f.block + 1) << kBlockShift);
+    f.npages = (uint32_t)((end - (f.block << kBlockShift) + kPageSize - 1) >> kPageShift) - f.first_page;
+  }
+  std::sort(faults.begin(), faults.end(), [](const FaultEntry& a, const FaultEntry& b) {
+    if (a.range_id != b.range_id) return a.range_id < b.range_id;
+    if (a.block != b.block) return a.block < b.block;
+    if (a.proc != b.proc) return a.proc < b.proc;
+    return (int)a.access > (int)b.access;  // writes first: the highest access wins
+  });
+  uint64_t coalesced = 0;
+  if (config().perf_fault_coalesce) {
+    for (size_t i = 1; i < faults.size(); ++i) {
+      FaultEntry& p = faults[i - 1];
+      FaultEntry& f = faults[i];
+      if (f.range_id == p.range_id && f.block == p.block && f.proc == p.proc && f.first_page == p.first_page &&
+          f.npages == p.npages) {
+        f.duplicate = true;
+        coalesced++;
+      }
+    }
+  }
+  Tools::get().inc(Counter::FaultsCoalesced, coalesced);
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  Ctx c;
+  c.cause = Cause::User;
+  Status result = Status::OK;
+  size_t i = 0;
+  uint32_t throttled = 0;
+  while (i < faults.size()) {
+    // Group: same (range, block, proc)
+    size_t j = i;
+    PageMask pages;
+    Access acc = Access::READ;
+    while (j < faults.size() && faults[j].range_id == faults[i].range_id && faults[j].block == faults[i].block &&
+           faults[j].proc == faults[i].proc) {
+      if (!faults[j].duplicate) {
+        pages.set_range(faults[j].first_page, faults[j].npages);
+        if ((int)faults[j].access > (int)acc && faults[j].access != Access::PREFETCH) acc = faults[j].access;
+      }
+      ++j;
+    }
+    Range* r = vs_.by_id_locked(faults[i].range_id);
+    int proc = faults[i].proc;
+    if (!r || faults[i].block >= r->nblocks || r->type != RangeType::MANAGED) {
+      result = Status::INVALID_ARGUMENT;  // fatal fault: cancelled
+      tools_event(ToolsEventType::FatalFault, Cause::User, Loc{}, Loc{}, proc, faults[i].offset, 0, faults[i].range_id);
+      i = j;
+      continue;
+    }
+    Block* b = r->block(faults[i].block);
+    Status st = Status::OK;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+      {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        b->faults_by_proc[proc == kCpuProc ? kMaxGpus : proc]++;
+        tools_event(proc == kCpuProc ? ToolsEventType::CpuFault : ToolsEventType::GpuFault, Cause::User, Loc{}, Loc{},
+                    proc, r->addr() + b->block_offset(), (uint64_t)pages.count() << kPageShift, r->id);
+        ResidencyDecision d = select_residency(this, b, proc, acc, pages);
+        if (d.map_remote) {
+          // Keep in place; make sure the pages exist somewhere reachable.
+          PageMask have = b->resident_anywhere();
+          PageMask need = pages.andnot(have);
+          if (!need.empty()) st = make_resident(c, b, need, d.dst, false, Cause::User);
+          if (b->thrash.detected) throttled++;
+        } else {
+          PageMask want = pages;
+          Residency* y = b->find(d.dst);
+          if (config().perf_prefetch_enable &&
+              b->faults_by_proc[proc == kCpuProc ? kMaxGpus : proc] >= (uint32_t)config().perf_prefetch_min_faults) {
+            PageMask hint = prefetch_hint(y ? y->resident : PageMask{}, pages, b->npages,
+                                          (uint32_t)config().perf_prefetch_threshold);
+            want |= hint & b->resident_anywhere();
+          }
+          st = make_resident(c, b, want, d.dst, d.read_dup, Cause::User);
+        }
+      }
+      if (st != Status::MORE_PROCESSING_REQUIRED) break;
+      finish_ctx(c, out);
+      Reservation rr;
+      Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+      if (es != Status::OK) {
+        st = es;
+        break;
+      }
+      c.need_arena->free((uint32_t)rr.first, rr.n);
+      c.need_arena = nullptr;
+    }
+    if (st != Status::OK && result == Status::OK) result = st;
+    if (throttled > (uint32_t)config().perf_fault_max_throttle_per_service) break;
+    i = j;
+  }
+  finish_ctx(c, out);
+  // Replay: with BATCH_FLUSH the waiting processors resume once every copy of the
+  // batch has landed (the caller waits on `out`).
+  tools_event(ToolsEventType::GpuFaultReplay, Cause::User, Loc{}, Loc{}, 0, 0, faults.size(), 0);
+  return result;
+}
+
+// ------------------------------------------------------------------ CPU faults
+Status Runtime::cpu_fault(uint64_t addr, bool write) {
+  Range* r = nullptr;
+  {
+    std::shared_lock<OrderedRWLock> vg(vs_.lock);
+    r = vs_.find_locked(addr);
+  }
+  if (!r || r->type != RangeType::MANAGED) return Status::NOT_FOUND;
+  uint64_t off = addr - r->addr();
+  if (off >= r->cpu_view_bytes) return Status::NOT_FOUND;
+  if (off >= align_up(r->size, kPageSize)) return Status::INVALID_ARGUMENT;  // past the allocation
+  Tools::get().inc(Counter::CpuPageFaultCount);
+  std::vector<FaultEntry> f(1);
+  f[0].range_id = r->id;
+  f[0].offset = align_down(off, kPageSize);
+  f[0].bytes = kPageSize;
+  f[0].proc = kCpuProc;
+  f[0].access = write ? Access::WRITE : Access::READ;
+  f[0].ts_ns = now_ns();
+  Tracker t;
+  Status st = service_faults(f, &t);
+  t.wait();
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  Block* b = r->block(off >> kBlockShift);
+  std::lock_guard<OrderedMutex> g(b->lock);
+  b->tracker.wait();
+  b->tracker.clear();
+  uint32_t page = (uint32_t)((off & (kBlockSize - 1)) >> kPageShift);
+  if (write) {
+    // A CPU write collapses read duplication: revoke every other copy of the page.
+    Residency* cpu_res = nullptr;
+    for (auto& x : b->res)
+      if (!x.loc.is_gpu() && x.resident.test(page)) cpu_res = &x;
+    if (cpu_res) {
+      Ctx c;
+      PageMask one;
+      one.set(page);
+      Loc keep = cpu_res->loc;
+      std::vector<Loc> drop;
+      for (auto& x : b->res)
+        if (!(x.loc == keep) && x.resident.test(page)) {
+          x.resident.clear(page);
+          Tools::get().inc(Counter::Revocations);
+          tools_event(ToolsEventType::ReadDuplicateInvalidate, Cause::Coherence, x.loc, keep, kCpuProc, addr,
+                      kPageSize, r->id);
+          if (x.resident.empty()) drop.push_back(x.loc);
+        }
+      for (auto& l : drop) drop_residency(c, b, l);
+    }
+  }
+  cpu_map_block(b);
+  update_device_table(b);
+  if (r->dev_va) stable_map_block(b);
+  return st;
+}
+
+// ------------------------------------------------------------------ device faults
+size_t Runtime::poll_device_faults(int dev) {
+  if (dev < 0 || dev >= ndev()) return 0;
+  DeviceFaultBuffer& fb = devs_[dev]->fault_buf;
+  if (!fb.put) return 0;
+  uint32_t put = __atomic_load_n(fb.put, __ATOMIC_ACQUIRE);
+  uint32_t n = std::min(put, fb.entries);
+  if (put > fb.entries) {
+    fb.overflows += put - fb.entries;
+    tools_event(ToolsEventType::FaultBufferOverflow, Cause::User, Loc{}, Loc{}, dev, 0, put - fb.entries, 0);
+  }
+  std::vector<FaultEntry> faults;
+  std::vector<std::pair<uint64_t, uint32_t>> remote_hits;
+  for (uint32_t i = 0; i < n; ++i) {
+    const DeviceFaultRecord& rec = fb.recs[i];
+    if (rec.kind == 1) {
+      remote_hits.emplace_back(rec.range_id, rec.block);
+      continue;
+    }
+    FaultEntry f;
+    f.range_id = rec.range_id;
+    f.offset = ((uint64_t)rec.block << kBlockShift) + ((uint64_t)rec.page << kPageShift);
+    f.bytes = kPageSize;
+    f.proc = (int)rec.proc;
+    f.access = rec.access == 2 ? Access::WRITE : Access::READ;
+    faults.push_back(f);
+  }
+  __atomic_store_n(fb.put, 0u, __ATOMIC_RELEASE);
+  // Access counters (uvm_gpu_access_counters.c:1617): migrate hot remote blocks.
+  int64_t mig = config().perf_access_counter_migration_enable;
+  if (!remote_hits.empty()) {
+    std::vector<std::pair<Range*, uint64_t>> hot;
+    {
+      std::shared_lock<OrderedRWLock> vg(vs_.lock);
+      for (auto& h : remote_hits) {
+        Range* r = vs_.by_id_locked(h.first);
+        if (!r || h.second >= r->nblocks) continue;
+        Block* b = r->block(h.second);
+        std::lock_guard<OrderedMutex> g(b->lock);
+        Tools::get().inc(Counter::AccessCounterNotifications);
+        uint32_t& cnt = b->counters.remote_hits[dev];
+        if (++cnt >= (uint64_t)config().perf_access_counter_threshold) {
+          cnt = 0;
+          if (mig != 0) hot.emplace_back(r, h.second);
+        }
+      }
+    }
+    for (auto& h : hot) {
+      Tracker t;
+      if (prefetch(h.first, h.second << kBlockShift,
+                   std::min<uint64_t>(kBlockSize, h.first->size - (h.second << kBlockShift)), Loc::gpu(dev), &t,
+                   Cause::AccessCounters) == Status::OK)
+        Tools::get().inc(Counter::AccessCounterMigrations);
+    }
+  }
+  if (!faults.empty()) {
+    Tracker t;
+    service_faults(faults, &t);
+    t.wait();
+  }
+  return n;
+}
+
+}  // namespace ogkm
+
+namespace ogkm {
+void Runtime::drop_copy(Ctx& c, Block* b, const Loc& l) { drop_residency(c, b, l); }
+Status Runtime::queue_copy(Ctx& c, Block* b, Residency* from, Residency* to, const PageMask& pages) {
+  return copy_pages(this, c, b, from, to, pages);
+}
+}  // namespace ogkm

@@ -1,0 +1,193 @@
+// SQ/CQ ring implementation.
+#include "ogkm/ring.hpp"
+
+#include <thread>
+
+#include "ogkm/config.hpp"
+#include "ogkm/events.hpp"
+#include "ogkm/runtime.hpp"
+
+namespace ogkm {
+
+const char* ring_kind_str(RingKind k) {
+  static const char* n[] = {"cpu_to_gpu", "gpu_to_cpu", "gpu_internal", "gpu_to_gpu", "memops", "cxl"};
+  return n[(int)k];
+}
+
+Ring::Ring(Backend* be, int dev, RingKind kind, uint32_t entries) : be_(be), dev_(dev), kind_(kind), entries_(entries) {
+  // Migration rings get high priority (-1) so copies are not starved by compute.
+  stream_ = be_->stream_create(dev, kind == RingKind::MEMOPS ? 0 : -1);
+  void* p = nullptr;
+  if (be_->host_alloc_coherent(64, &p) == Status::OK) {
+    sem_ = (uint64_t*)p;
+    *sem_ = 0;
+  }
+  if (!stream_ || !sem_) {
+    err_ = Status::NO_MEMORY;
+    RT_ERR("ring %s/%d init failed", ring_kind_str(kind), dev);
+  }
+}
+
+Ring::~Ring() {
+  if (stream_) {
+    be_->stream_sync(stream_);
+    last_fence_.reset();
+    be_->stream_destroy(stream_);
+  }
+  if (sem_) be_->host_free_coherent(sem_);
+}
+
+uint64_t Ring::push(Sqe&& s) {
+  std::unique_lock<OrderedMutex> g(m_);
+  // SQ full (GPFIFO full): submit, then wait for the oldest in-flight entries.
+  while (sq_.size() + inflight_.size() >= entries_) {
+    if (!sq_.empty()) submit_locked();
+    uint64_t oldest = inflight_.empty() ? 0 : inflight_.front().first;
+    if (oldest) {
+      g.unlock();
+      wait_seq(oldest);
+      g.lock();
+      while (!inflight_.empty() && inflight_.front().first <= completed_seq()) inflight_.pop_front();
+    }
+  }
+  uint64_t seq = next_seq_++;
+  sq_.emplace_back(seq, std::move(s));
+  return seq;
+}
+
+FenceRef Ring::submit() {
+  std::lock_guard<OrderedMutex> g(m_);
+  return submit_locked();
+}
+
+FenceRef Ring::submit_locked() {
+  if (sq_.empty()) {
+    if (last_fence_) return last_fence_;
+    auto f = std::make_shared<Fence>();
+    f->done.store(true);
+    return f;
+  }
+  Runtime* rt = Runtime::get();
+  Status st = err_;
+  uint64_t last = 0;
+  std::vector<CopyDesc> batch;
+  int engine = kind_ == RingKind::GPU_INTERNAL ? 2 : (int)config().copy_engine;
+  auto flush = [&]() {
+    if (batch.empty() || st != Status::OK) {
+      batch.clear();
+      return;
+    }
+    st = be_->copy_batch(dev_, batch.data(), batch.size(), stream_, engine);
+    Tools::get().inc(Counter::CopyKernelLaunches);
+    batch.clear();
+  };
+  std::vector<std::pair<uint64_t, Cqe>> done;
+  for (auto& e : sq_) {
+    Sqe& s = e.second;
+    int32_t cqe_status = 0;
+    if (st == Status::OK) {
+      switch (s.op) {
+        case SqeOp::COPY:
+          if (rt && rt->inject().copy_drop.load() > 0 && rt->inject().copy_drop.fetch_sub(1) > 0) {
+            // Simulated link error: the copy is dropped and reported
+            // (NVLink error injection analog, uvm_volta_ce.c:137-138).
+            Tools::get().inc(Counter::InjectedErrors);
+            cqe_status = (int32_t)Status::INJECTED_ERROR;
+            err_ = Status::INJECTED_ERROR;
+            err_desc_ = std::string(s.file) + ":" + std::to_string(s.line) + " " + s.desc;
+            st = Status::INJECTED_ERROR;
+            break;
+          }
+          batch.push_back(CopyDesc{s.dst, s.src, s.bytes});
+          break;
+        case SqeOp::GATHER:
+        case SqeOp::SCATTER: {
+          flush();
+          PageListDesc d{s.op == SqeOp::GATHER ? s.src : s.dst, s.op == SqeOp::GATHER ? s.dst : s.src, s.idx.data(),
+                         (uint32_t)s.idx.size(), s.page_bytes};
+          if (st == Status::OK) st = s.op == SqeOp::GATHER ? be_->gather_pages(dev_, d, stream_)
+                                                          : be_->scatter_pages(dev_, d, stream_);
+          break;
+        }
+        case SqeOp::MEMSET:
+          flush();
+          if (st == Status::OK) st = be_->memset32(dev_, s.dst, s.pattern, s.bytes, stream_);
+          break;
+        case SqeOp::WAIT_FENCE:
+          flush();
+          if (st == Status::OK && s.wait && !s.wait->done.load()) {
+            if (s.wait->event) st = be_->stream_wait_event(stream_, s.wait->event);
+            else st = s.wait->wait();
+          }
+          break;
+        case SqeOp::NOP:
+          break;
+      }
+      if (st != Status::OK && cqe_status == 0) {
+        cqe_status = (int32_t)st;
+        if (err_ == Status::OK) {
+          err_ = st;
+          err_desc_ = std::string(s.file) + ":" + std::to_string(s.line) + " " + s.desc;
+        }
+      }
+    } else {
+      cqe_status = (int32_t)st;
+    }
+    last = e.first;
+    done.emplace_back(e.first, Cqe{s.user_data, e.first, cqe_status});
+  }
+  flush();
+  sq_.clear();
+  if (st == Status::OK) st = be_->signal(dev_, sem_, last, stream_);
+  if (st != Status::OK) {
+    if (err_ == Status::OK) err_ = st;
+    // Robust-channel style: mark the ring failed; CPU waiters must not hang.
+    __atomic_store_n(sem_, last, __ATOMIC_RELEASE);
+    RT_ERR("ring %s/%d error %s at %s", ring_kind_str(kind_), dev_, status_str(err_), err_desc_.c_str());
+    if (err_ != Status::INJECTED_ERROR) set_fatal(err_, "ring submission failed");
+    tools_event(ToolsEventType::RingError, Cause::User, Loc::gpu(dev_), Loc::gpu(dev_), dev_, 0, 0, 0);
+  }
+  for (auto& d : done) inflight_.push_back(d);
+  submitted_ = last;
+  batches_++;
+  Tools::get().inc(Counter::RingSubmissions);
+  last_fence_ = fence_record(be_, dev_, stream_, this, last);
+  return last_fence_;
+}
+
+uint64_t Ring::completed_seq() { return sem_ ? __atomic_load_n(sem_, __ATOMIC_ACQUIRE) : 0; }
+
+Status Ring::wait_seq(uint64_t seq) {
+  if (seq > submitted_) submit();
+  uint64_t spins = 0;
+  while (completed_seq() < seq) {
+    if (++spins > 64) std::this_thread::yield();
+    if (spins > (1ull << 34)) return Status::TIMEOUT;
+  }
+  return err_;
+}
+
+size_t Ring::reap(Cqe* out, size_t max) {
+  std::lock_guard<OrderedMutex> g(m_);
+  uint64_t c = completed_seq();
+  size_t n = 0;
+  while (!inflight_.empty() && inflight_.front().first <= c && n < max) {
+    out[n++] = inflight_.front().second;
+    inflight_.pop_front();
+  }
+  Tools::get().inc(Counter::RingCompletions, n);
+  return n;
+}
+
+void Ring::clear_error_for_test() {
+  std::lock_guard<OrderedMutex> g(m_);
+  err_ = Status::OK;
+  err_desc_.clear();
+}
+
+std::string Ring::last_error_desc() {
+  std::lock_guard<OrderedMutex> g(m_);
+  return err_desc_;
+}
+
+}  // namespace ogkm

@@ -1,0 +1,1025 @@
+// Runtime: init/shutdown, tiers, ranges, policy, data helpers, introspection,
+// CPU/stable-VA mapping maintenance, CXL DMA, quiesce/resume and the
+// residency-map checkpoint format.
+#include "ogkm/runtime.hpp"
+
+#include <signal.h>
+#include <sys/mman.h>
+#include <ucontext.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <shared_mutex>
+
+namespace ogkm {
+
+static std::atomic<Runtime*> g_rt{nullptr};
+static std::mutex g_rt_m;
+
+Runtime* Runtime::get() { return g_rt.load(std::memory_order_acquire); }
+
+Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fake_hbm_bytes) {
+  std::lock_guard<std::mutex> g(g_rt_m);
+  if (Runtime* r = g_rt.load()) return r;
+  auto* rt = new Runtime();
+  if (backend == "fake") rt->be_ = make_fake_backend(fake_devices > 0 ? fake_devices : 2, fake_hbm_bytes);
+  else rt->be_ = make_backend(backend);
+  if (!rt->be_) {
+    delete rt;
+    return nullptr;
+  }
+  Config& cfg = config();
+  int nd = rt->be_->device_count();
+  rt->host_node_ = cfg.host_node >= 0 ? (int)cfg.host_node : (nd > 0 ? rt->be_->device_numa_node(0) : 0);
+  rt->cxl_topo_.discover((int)cfg.cxl_emulate_node);
+  rt->cxl_ = std::make_unique<CxlRegistry>(rt->be_.get());
+  rt->cxl_->init(system_ram_bytes() / 100 * (uint64_t)cfg.cxl_pin_budget_pct, (uint32_t)cfg.cxl_max_buffers,
+                 (uint64_t)cfg.cxl_max_buffer_gb << 30);
+  for (int d = 0; d < nd; ++d) {
+    auto dev = std::make_unique<Device>();
+    dev->id = d;
+    dev->numa = rt->be_->device_numa_node(d);
+    for (int k = 0; k < (int)RingKind::COUNT; ++k)
+      dev->rings[k] = std::make_unique<Ring>(rt->be_.get(), d, (RingKind)k, (uint32_t)cfg.channel_num_gpfifo_entries);
+    void* p = nullptr;
+    const uint32_t entries = (uint32_t)cfg.perf_fault_batch_count * 16;
+    if (rt->be_->host_alloc_coherent(64 + (size_t)entries * sizeof(DeviceFaultRecord), &p) == Status::OK) {
+      dev->fault_buf.put = (uint32_t*)p;
+      dev->fault_buf.recs = (DeviceFaultRecord*)((char*)p + 64);
+      dev->fault_buf.entries = entries;
+    }
+    rt->devs_.push_back(std::move(dev));
+  }
+  g_rt.store(rt, std::memory_order_release);
+  install_cpu_fault_handler();
+  RT_INFO("runtime up: backend=%s devices=%d host_node=%d cxl_nodes=%zu", rt->be_->name(), nd, rt->host_node_,
+          rt->cxl_topo_.info().numa_nodes.size());
+  return rt;
+}
+
+void Runtime::shutdown() {
+  std::lock_guard<std::mutex> g(g_rt_m);
+  Runtime* rt = g_rt.exchange(nullptr);
+  delete rt;
+}
+
+Runtime::~Runtime() {
+  for (auto& d : devs_)
+    for (auto& r : d->rings)
+      if (r) r->submit();
+  sync_all();
+  {
+    std::lock_guard<std::mutex> g(leases_m_);
+    leases_.clear();
+  }
+  // Ranges reference arenas: free them first.
+  std::vector<Range*> rs;
+  for (auto& kv : vs_.ranges) rs.push_back(kv.second.get());
+  for (Range* r : rs) {
+    r->views.store(0);
+    free_range(r);
+  }
+  for (auto& t : dev_tables_)
+    if (t.second->entries) be_->host_free_coherent(t.second->entries);
+  cxl_.reset();
+  for (auto& d : devs_) {
+    for (auto& r : d->rings) r.reset();
+    if (d->fault_buf.put) be_->host_free_coherent(d->fault_buf.put);
+    d->hbm.reset();
+  }
+  host_arenas_.clear();
+}
+
+// ------------------------------------------------------------------ tiers
+Status Runtime::init_device(int d, uint64_t budget) {
+  if (d < 0 || d >= ndev()) return Status::INVALID_ARGUMENT;
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  if (devs_[d]->hbm && devs_[d]->hbm->outstanding_bytes()) return Status::BUSY;
+  devs_[d]->hbm.reset();
+  if (budget == 0) {
+    size_t f = 0, t = 0;
+    if (be_->device_mem_info(d, &f, &t) != Status::OK) return Status::IO_ERROR;
+    budget = config().hbm_budget_mb ? (uint64_t)config().hbm_budget_mb << 20 : f / 2;
+  }
+  devs_[d]->hbm = std::make_unique<HbmArena>(be_.get(), d, budget, (int)config().hbm_provider);
+  return devs_[d]->hbm->init_status();
+}
+
+HostArena* Runtime::host_arena(Tier t, int node) {
+  if (node < 0 || node >= kMaxNodes) return nullptr;
+  std::lock_guard<std::mutex> g(host_arenas_m_);
+  size_t idx = (size_t)(t == Tier::CXL ? 1 : 0) * kMaxNodes + node;
+  if (host_arenas_.size() <= idx) host_arenas_.resize(2 * kMaxNodes);
+  if (!host_arenas_[idx]) {
+    uint64_t cap = config().host_budget_mb ? (uint64_t)config().host_budget_mb << 20
+                                           : system_ram_bytes() / 100 * (uint64_t)config().cxl_pin_budget_pct;
+    auto a = std::make_unique<HostArena>(be_.get(), t, node, cap);
+    if (a->init_status() != Status::OK) return nullptr;
+    host_arenas_[idx] = std::move(a);
+  }
+  return host_arenas_[idx].get();
+}
+
+ChunkArena* Runtime::arena_for(const Loc& l) {
+  if (l.is_gpu()) {
+    if (l.id < 0 || l.id >= ndev()) return nullptr;
+    if (!devs_[l.id]->hbm) {
+      size_t f = 0, t = 0;
+      if (be_->device_mem_info(l.id, &f, &t) != Status::OK) return nullptr;
+      uint64_t budget = config().hbm_budget_mb ? (uint64_t)config().hbm_budget_mb << 20 : f / 2;
+      static std::mutex m;
+      std::lock_guard<std::mutex> g(m);
+      if (!devs_[l.id]->hbm) devs_[l.id]->hbm = std::make_unique<HbmArena>(be_.get(), l.id, budget, (int)config().hbm_provider);
+    }
+    return devs_[l.id]->hbm.get();
+  }
+  if (l.tier == Tier::CXL && !cxl_topo_.is_cxl_node(l.id)) return nullptr;
+  return host_arena(l.tier, l.id);
+}
+
+// ------------------------------------------------------------------ ranges
+Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string& name, Range** out, int stable_dev) {
+  if (global_status() != Status::OK) return global_status();
+  if (size == 0) return Status::INVALID_ARGUMENT;
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  uint64_t id = vs_.next_range_id++;
+  auto r = std::make_unique<Range>(&vs_, id, RangeType::MANAGED, size, flags, name);
+  if (!(flags & RANGE_NO_CPU_VIEW) && !r->cpu_view) return Status::NO_MEMORY;
+  if (flags & RANGE_STABLE_VA) {
+    if (stable_dev < 0 || stable_dev >= ndev()) return Status::INVALID_ARGUMENT;
+    vg.unlock();
+    ChunkArena* a = arena_for(Loc::gpu(stable_dev));
+    vg.lock();
+    if (!a || !static_cast<HbmArena*>(a)->vmm()) return Status::NOT_SUPPORTED;  // needs hbm_provider=1
+    void* va = nullptr;
+    Status st = be_->va_reserve(r->cpu_view_bytes, &va);
+    if (st != Status::OK) return st;
+    r->dev_va = va;
+    r->stable_dev = stable_dev;
+  }
+  if (r->cpu_view) vs_.tree[r->addr()] = r.get();
+  *out = r.get();
+  vs_.ranges[id] = std::move(r);
+  return Status::OK;
+}
+
+Status Runtime::map_external(uint64_t ptr, uint64_t size, int dev, const std::string& name, Range** out) {
+  if (!ptr || !size || dev < 0 || dev >= ndev()) return Status::INVALID_ARGUMENT;
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  uint64_t id = vs_.next_range_id++;
+  auto r = std::make_unique<Range>(&vs_, id, RangeType::EXTERNAL, size, RANGE_NO_CPU_VIEW, name);
+  r->ext_ptr = ptr;
+  r->ext_dev = dev;
+  *out = r.get();
+  vs_.ranges[id] = std::move(r);
+  return Status::OK;
+}
+
+Status Runtime::alloc_device_p2p(uint64_t size, int dev, const std::string& name, Range** out) {
+  if (!size || dev < 0 || dev >= ndev()) return Status::INVALID_ARGUMENT;
+  void* p = nullptr;
+  Status st = be_->hbm_alloc(dev, align_up(size, kBlockSize), &p);
+  if (st != Status::OK) return st;
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  uint64_t id = vs_.next_range_id++;
+  auto r = std::make_unique<Range>(&vs_, id, RangeType::DEVICE_P2P, size, RANGE_NO_CPU_VIEW, name);
+  r->ext_ptr = (uint64_t)p;
+  r->ext_dev = dev;
+  r->ext_owned = true;
+  *out = r.get();
+  vs_.ranges[id] = std::move(r);
+  return Status::OK;
+}
+
+Status Runtime::free_range(Range* r) {
+  if (!r) return Status::INVALID_ARGUMENT;
+  if (r->views.load() > 0) return Status::BUSY;
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  auto it = vs_.ranges.find(r->id);
+  if (it == vs_.ranges.end()) return Status::NOT_FOUND;
+  for (auto& bp : r->blocks) {
+    Block* b = bp.get();
+    std::lock_guard<OrderedMutex> g(b->lock);
+    b->tracker.wait();
+    if (r->dev_va && b->stable_chunk >= 0) be_->vmm_unmap((char*)r->dev_va + b->block_offset(), kBlockSize);
+    for (auto& x : b->res)
+      if (x.chunk >= 0) x.arena->free((uint32_t)x.chunk, 1);
+    b->res.clear();
+    Tools::get().bus().notify(PerfEventData{PerfEvent::BLOCK_DESTROY, r->id, b->index});
+  }
+  if (r->dev_va) be_->va_free(r->dev_va, r->cpu_view_bytes);
+  if (r->ext_owned && r->ext_ptr) be_->hbm_free(r->ext_dev, (void*)r->ext_ptr, align_up(r->size, kBlockSize));
+  if (r->group) {
+    auto& v = r->group->ranges;
+    v.erase(std::remove(v.begin(), v.end(), r), v.end());
+  }
+  if (r->cpu_view) vs_.tree.erase(r->addr());
+  {
+    std::lock_guard<std::mutex> g(dev_tables_m_);
+    auto t = dev_tables_.find(r->id);
+    if (t != dev_tables_.end()) {
+      be_->host_free_coherent(t->second->entries);
+      dev_tables_.erase(t);
+    }
+  }
+  Tools::get().bus().notify(PerfEventData{PerfEvent::RANGE_DESTROY, r->id});
+  vs_.ranges.erase(it);
+  return Status::OK;
+}
+
+Range* Runtime::find_range(uint64_t addr) {
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  return vs_.find_locked(addr);
+}
+
+Range* Runtime::range_by_id(uint64_t id) {
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  return vs_.by_id_locked(id);
+}
+
+// ------------------------------------------------------------------ policy
+Status Runtime::mem_advise(Range* r, uint64_t off, uint64_t len, Advice a, Loc loc, int proc) {
+  if (!r || len == 0 || off + len > r->size) return Status::INVALID_ARGUMENT;
+  if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
+  if (a == Advice::SET_PREFERRED_LOCATION && !arena_for(loc)) return Status::INVALID_ARGUMENT;
+  if ((a == Advice::SET_ACCESSED_BY || a == Advice::UNSET_ACCESSED_BY) &&
+      !(proc == kCpuProc || (proc >= 0 && proc < ndev())))
+    return Status::INVALID_ARGUMENT;
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
+  for (uint64_t bi = b0; bi <= b1; ++bi) {
+    Block* b = r->block(bi);
+    Ctx c;
+    {
+      std::lock_guard<OrderedMutex> g(b->lock);
+      Policy& p = b->policy;
+      switch (a) {
+        case Advice::SET_READ_MOSTLY: p.read_dup = true; break;
+        case Advice::UNSET_READ_MOSTLY: {
+          p.read_dup = false;
+          // Collapse duplicates: keep the preferred copy, else a host copy, else the first.
+          PageMask seen;
+          std::vector<Residency*> order;
+          if (p.has_preferred)
+            if (Residency* x = b->find(p.preferred)) order.push_back(x);
+          for (auto& x : b->res)
+            if (!x.loc.is_gpu() && std::find(order.begin(), order.end(), &x) == order.end()) order.push_back(&x);
+          for (auto& x : b->res)
+            if (std::find(order.begin(), order.end(), &x) == order.end()) order.push_back(&x);
+          std::vector<Loc> empty;
+          for (Residency* x : order) {
+            PageMask dup = x->resident & seen;
+            seen |= x->resident;
+            if (!dup.empty()) {
+              x->resident = x->resident.andnot(dup);
+              Tools::get().inc(Counter::Revocations);
+              if (x->resident.empty()) empty.push_back(x->loc);
+            }
+          }
+          for (auto& l : empty) drop_copy(c, b, l);
+          c.cpu_refresh.push_back(b);
+          break;
+        }
+        case Advice::SET_PREFERRED_LOCATION:
+          p.has_preferred = true;
+          p.preferred = loc;
+          break;
+        case Advice::UNSET_PREFERRED_LOCATION: p.has_preferred = false; break;
+        case Advice::SET_ACCESSED_BY: p.accessed_by |= 1ull << (proc == kCpuProc ? kCpuProc : proc); break;
+        case Advice::UNSET_ACCESSED_BY: p.accessed_by &= ~(1ull << (proc == kCpuProc ? kCpuProc : proc)); break;
+      }
+    }
+    finish_ctx(c, nullptr);
+  }
+  return Status::OK;
+}
+
+Status Runtime::create_range_group(uint64_t* id) {
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  uint64_t g = vs_.next_group_id++;
+  vs_.groups[g] = std::make_unique<RangeGroup>(g);
+  *id = g;
+  return Status::OK;
+}
+
+Status Runtime::set_range_group(Range* r, uint64_t gid) {
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  if (r->group) {
+    auto& v = r->group->ranges;
+    v.erase(std::remove(v.begin(), v.end(), r), v.end());
+    r->group = nullptr;
+  }
+  if (gid == 0) return Status::OK;
+  auto it = vs_.groups.find(gid);
+  if (it == vs_.groups.end()) return Status::NOT_FOUND;
+  r->group = it->second.get();
+  r->group->ranges.push_back(r);
+  return Status::OK;
+}
+
+Status Runtime::set_group_migratable(uint64_t gid, bool m) {
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  auto it = vs_.groups.find(gid);
+  if (it == vs_.groups.end()) return Status::NOT_FOUND;
+  it->second->migratable = m;
+  return Status::OK;
+}
+
+// ------------------------------------------------------------------ CPU view / stable VA / device tables
+void Runtime::cpu_map_block(Block* b) {
+  Range* r = b->range;
+  if (!r->cpu_view) return;
+  uint8_t* win = r->cpu_view + b->block_offset();
+  Residency* h = nullptr;
+  if (Residency* x = b->find(cpu_loc())) h = x;
+  if (!h)
+    for (auto& x : b->res)
+      if (!x.loc.is_gpu() && x.chunk >= 0) {
+        h = &x;
+        break;
+      }
+  if (!h) {
+    if (b->cpu_arena) {
+      mmap(win, kBlockSize, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
+      b->cpu_arena = nullptr;
+      b->cpu_chunk = -1;
+    }
+    b->cpu_ro.zero();
+    b->cpu_rw.zero();
+    return;
+  }
+  HostArena* ha = static_cast<HostArena*>(h->arena);
+  if (b->cpu_arena != h->arena || b->cpu_chunk != h->chunk) {
+    void* m = mmap(win, kBlockSize, PROT_NONE, MAP_SHARED | MAP_FIXED, ha->fd(), (off_t)ha->file_offset((uint32_t)h->chunk));
+    if (m == MAP_FAILED) {
+      RT_ERR("CPU view remap failed for range %llu block %llu", (unsigned long long)r->id,
+             (unsigned long long)b->index);
+      return;
+    }
+    b->cpu_arena = h->arena;
+    b->cpu_chunk = h->chunk;
+    b->cpu_ro.zero();
+    b->cpu_rw.zero();
+  }
+  bool pending = !b->tracker.query();
+  PageMask others;
+  for (auto& x : b->res)
+    if (&x != h) others |= x.resident;
+  PageMask rw, ro;
+  if (!pending) {
+    rw = h->resident.andnot(others) & b->valid_pages();
+    ro = (h->resident & others) & b->valid_pages();
+  }
+  if (rw == b->cpu_rw && ro == b->cpu_ro) return;
+  // Apply protections run by run.
+  uint32_t p = 0;
+  while (p < kPagesPerBlock) {
+    int prot = rw.test(p) ? (PROT_READ | PROT_WRITE) : (ro.test(p) ? PROT_READ : PROT_NONE);
+    uint32_t e = p + 1;
+    while (e < kPagesPerBlock) {
+      int pe = rw.test(e) ? (PROT_READ | PROT_WRITE) : (ro.test(e) ? PROT_READ : PROT_NONE);
+      if (pe != prot) break;
+      ++e;
+    }
+    mprotect(win + ((uint64_t)p << kPageShift), (uint64_t)(e - p) << kPageShift, prot);
+    p = e;
+  }
+  b->cpu_rw = rw;
+  b->cpu_ro = ro;
+}
+
+void Runtime::stable_map_block(Block* b) {
+  Range* r = b->range;
+  if (!r->dev_va) return;
+  Residency* g = b->find(Loc::gpu(r->stable_dev));
+  int64_t want = (g && g->chunk >= 0) ? g->chunk : -1;
+  if (want == b->stable_chunk) return;
+  char* va = (char*)r->dev_va + b->block_offset();
+  if (b->stable_chunk >= 0) be_->vmm_unmap(va, kBlockSize);
+  b->stable_chunk = -1;
+  if (want >= 0) {
+    HbmArena* ha = static_cast<HbmArena*>(g->arena);
+    if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) b->stable_chunk = want;
+  }
+}
+
+void Runtime::update_device_table(Block* b) {
+  std::lock_guard<std::mutex> g(dev_tables_m_);
+  auto it = dev_tables_.find(b->range->id);
+  if (it == dev_tables_.end()) return;
+  DeviceResidencyTable* t = it->second.get();
+  uint64_t hbm = 0, rem = 0;
+  PageMask valid = b->valid_pages();
+  for (auto& x : b->res) {
+    if ((x.resident & valid) == valid) {
+      if (x.loc == Loc::gpu(t->dev)) hbm = x.arena->chunk_addr((uint32_t)x.chunk);
+      else if (!x.loc.is_gpu() && !rem) rem = x.arena->chunk_addr((uint32_t)x.chunk);
+    }
+  }
+  bool pending = !b->tracker.query();
+  __atomic_store_n(&t->entries[2 * b->index], pending ? 0 : hbm, __ATOMIC_RELEASE);
+  __atomic_store_n(&t->entries[2 * b->index + 1], pending ? 0 : rem, __ATOMIC_RELEASE);
+}
+
+Status Runtime::device_table(Range* r, DeviceResidencyTable** out) {
+  {
+    std::lock_guard<std::mutex> g(dev_tables_m_);
+    auto it = dev_tables_.find(r->id);
+    if (it != dev_tables_.end()) {
+      *out = it->second.get();
+      return Status::OK;
+    }
+    auto t = std::make_unique<DeviceResidencyTable>();
+    void* p = nullptr;
+    Status st = be_->host_alloc_coherent(std::max<uint64_t>(16, r->nblocks * 16), &p);
+    if (st != Status::OK) return st;
+    t->entries = (uint64_t*)p;
+    t->nblocks = r->nblocks;
+    t->dev = 0;
+    *out = t.get();
+    dev_tables_[r->id] = std::move(t);
+  }
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  for (auto& bp : r->blocks) {
+    std::lock_guard<OrderedMutex> g(bp->lock);
+    update_device_table(bp.get());
+  }
+  return Status::OK;
+}
+
+// ------------------------------------------------------------------ data helpers
+Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev) {
+  if (!r || off + bytes > r->size) return Status::INVALID_ARGUMENT;
+  if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
+  if (bytes == 0) return Status::OK;
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  uint64_t pos = off;
+  while (pos < off + bytes) {
+    uint64_t bi = pos >> kBlockShift;
+    uint64_t end = std::min(off + bytes, (bi + 1) << kBlockShift);
+    Block* b = r->block(bi);
+    uint64_t lo = pos - (bi << kBlockShift), hi = end - (bi << kBlockShift);
+    uint32_t p0 = (uint32_t)(lo >> kPageShift), p1 = (uint32_t)((hi + kPageSize - 1) >> kPageShift);
+    PageMask pages = PageMask::range(p0, p1 - p0);
+    // Fully-overwritten pages need no old data.
+    PageMask full = pages;
+    if (lo & (kPageSize - 1)) full.clear(p0);
+    if ((hi & (kPageSize - 1)) && hi < ((uint64_t)b->npages << kPageShift)) full.clear(p1 - 1);
+    Status st = Status::OK;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+      Ctx c;
+      c.cause = Cause::User;
+      {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        Loc dst;
+        if (b->policy.has_preferred) dst = b->policy.preferred;
+        else if (!b->res.empty()) dst = b->res.front().loc;
+        else dst = src_dev >= 0 ? Loc::gpu(src_dev) : cpu_loc();
+        Loc stage = dst;
+        if (src_dev < 0 && dst.is_gpu()) stage = cpu_loc();  // pageable host source: stage on host
+        Residency* to = nullptr;
+        st = populate(c, b, stage, -1, &to);
+        if (st == Status::OK) {
+          // Old data only for partially covered pages.
+          PageMask partial = pages.andnot(full);
+          if (!partial.empty()) st = make_resident(c, b, partial, stage, false, Cause::User);
+          to = b->find(stage);
+        }
+        if (st == Status::OK) {
+          // Invalidate other copies of the written pages.
+          std::vector<Loc> empty;
+          for (auto& x : b->res)
+            if (&x != to && x.resident.intersects(pages)) {
+              x.resident = x.resident.andnot(pages);
+              if (x.resident.empty()) empty.push_back(x.loc);
+            }
+          for (auto& l : empty) drop_copy(c, b, l);
+          to = b->find(stage);
+          to->resident |= pages;
+          uint64_t dst_addr = to->arena->chunk_addr((uint32_t)to->chunk) + lo;
+          const char* s = (const char*)src + (pos - off);
+          if (src_dev < 0) {
+            Tracker t = b->tracker;
+            t.wait();
+            Tracker rf = to->arena->take_reuse_fence((uint32_t)to->chunk);
+            rf.wait();
+            memcpy((void*)dst_addr, s, end - pos);
+          } else {
+            Loc sl = Loc::gpu(src_dev);
+            Ring* rg = stage.is_gpu() ? (stage.id == src_dev ? ring(src_dev, RingKind::GPU_INTERNAL)
+                                                            : ring(src_dev, RingKind::GPU_TO_GPU))
+                                      : ring(src_dev, RingKind::GPU_TO_CPU);
+            Tracker rf = to->arena->take_reuse_fence((uint32_t)to->chunk);
+            rf.merge(b->tracker);
+            for (auto& f : rf.fences()) {
+              Sqe w;
+              w.op = SqeOp::WAIT_FENCE;
+              w.wait = f;
+              rg->push(std::move(w));
+            }
+            Sqe cp;
+            cp.op = SqeOp::COPY;
+            cp.dst = dst_addr;
+            cp.src = (uint64_t)s;
+            cp.bytes = end - pos;
+            cp.file = __FILE__;
+            cp.line = __LINE__;
+            rg->push(std::move(cp));
+            FenceRef f = rg->submit();
+            Tools::get().inc(stage.is_gpu() ? Counter::BytesXferDtD : Counter::BytesXferDtH, end - pos);
+            (void)sl;
+            st = f->wait();
+          }
+          c.cpu_refresh.push_back(b);
+        }
+        if (st == Status::OK && !(stage == dst)) st = make_resident(c, b, pages, dst, false, Cause::User);
+      }
+      if (st == Status::MORE_PROCESSING_REQUIRED) {
+        finish_ctx(c, nullptr);
+        Reservation rr;
+        Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+        if (es != Status::OK) return es;
+        c.need_arena->free((uint32_t)rr.first, rr.n);
+        continue;
+      }
+      Tracker t;
+      finish_ctx(c, &t);
+      Status w = t.wait();
+      if (st == Status::OK) st = w;
+      break;
+    }
+    if (st != Status::OK) return st;
+    pos = end;
+  }
+  return Status::OK;
+}
+
+Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_dev) {
+  if (!r || off + bytes > r->size) return Status::INVALID_ARGUMENT;
+  if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  uint64_t pos = off;
+  while (pos < off + bytes) {
+    uint64_t bi = pos >> kBlockShift;
+    uint64_t end = std::min(off + bytes, (bi + 1) << kBlockShift);
+    Block* b = r->block(bi);
+    std::lock_guard<OrderedMutex> g(b->lock);
+    b->tracker.wait();
+    uint64_t lo = pos - (bi << kBlockShift);
+    char* out = (char*)dst + (pos - off);
+    // Walk page by page, coalescing by source.
+    uint64_t cur = pos;
+    while (cur < end) {
+      uint32_t p = (uint32_t)((cur - (bi << kBlockShift)) >> kPageShift);
+      uint64_t pend = std::min(end, (bi << kBlockShift) + ((uint64_t)(p + 1) << kPageShift));
+      Residency* src = nullptr;
+      for (auto& x : b->res)
+        if (x.resident.test(p) && (!src || (!x.loc.is_gpu() && src->loc.is_gpu()))) src = &x;
+      char* o = out + (cur - pos);
+      uint64_t n = pend - cur;
+      uint64_t in_chunk = cur - (bi << kBlockShift);
+      if (!src) {
+        if (dst_dev < 0) memset(o, 0, n);
+        else {
+          Ring* rg = ring(dst_dev, RingKind::MEMOPS);
+          Sqe s;
+          s.op = SqeOp::MEMSET;
+          s.dst = (uint64_t)o;
+          s.bytes = n;
+          rg->push(std::move(s));
+          rg->submit()->wait();
+        }
+      } else if (dst_dev < 0 && !src->loc.is_gpu()) {
+        memcpy(o, (const void*)(src->arena->chunk_addr((uint32_t)src->chunk) + in_chunk), n);
+      } else {
+        Ring* rg;
+        int d = src->loc.is_gpu() ? src->loc.id : dst_dev;
+        if (dst_dev < 0) {
+          // GPU -> pageable host: bounce through a pinned host chunk.
+          HostArena* ha = host_arena(Tier::HOST, host_node_);
+          uint32_t tmp;
+          Status st = ha ? alloc_chunks(ha, 1, -1, &tmp) : Status::NO_MEMORY;
+          if (st != Status::OK) return st;
+          rg = ring(d, RingKind::GPU_TO_CPU);
+          Sqe s;
+          s.op = SqeOp::COPY;
+          s.dst = ha->chunk_addr(tmp);
+          s.src = src->arena->chunk_addr((uint32_t)src->chunk) + in_chunk;
+          s.bytes = n;
+          rg->push(std::move(s));
+          st = rg->submit()->wait();
+          memcpy(o, (const void*)ha->chunk_addr(tmp), n);
+          ha->free(tmp, 1);
+          if (st != Status::OK) return st;
+        } else {
+          rg = src->loc.is_gpu() ? (src->loc.id == dst_dev ? ring(d, RingKind::GPU_INTERNAL) : ring(d, RingKind::GPU_TO_GPU))
+                                 : ring(dst_dev, RingKind::CPU_TO_GPU);
+          Sqe s;
+          s.op = SqeOp::COPY;
+          s.dst = (uint64_t)o;
+          s.src = src->arena->chunk_addr((uint32_t)src->chunk) + in_chunk;
+          s.bytes = n;
+          rg->push(std::move(s));
+          Status st = rg->submit()->wait();
+          if (st != Status::OK) return st;
+        }
+      }
+      cur = pend;
+    }
+    (void)lo;
+    pos = end;
+  }
+  return Status::OK;
+}
+
+Status Runtime::fill(Range* r, uint64_t off, uint64_t bytes, uint32_t pattern) {
+  if (!r || off + bytes > r->size || (off & 3) || (bytes & 3)) return Status::INVALID_ARGUMENT;
+  std::vector<uint32_t> buf(std::min<uint64_t>(bytes, kBlockSize) / 4, pattern);
+  uint64_t pos = off;
+  while (pos < off + bytes) {
+    uint64_t n = std::min<uint64_t>(off + bytes - pos, kBlockSize - (pos & (kBlockSize - 1)));
+    Status st = write(r, pos, buf.data(), n, -1);
+    if (st != Status::OK) return st;
+    pos += n;
+  }
+  return Status::OK;
+}
+
+// ------------------------------------------------------------------ introspection
+Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
+  if (!r || off >= r->size) return Status::INVALID_ARGUMENT;
+  *out = ResidencyInfo{};
+  if (r->type != RangeType::MANAGED) {
+    out->resident_on.push_back(Loc::gpu(r->ext_dev));
+    out->chunk.push_back(-1);
+    out->pages.push_back((uint32_t)(std::min<uint64_t>(r->size, kBlockSize) >> kPageShift));
+    out->mapped_on.push_back(r->ext_dev);
+    return Status::OK;
+  }
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  Block* b = r->block(off >> kBlockShift);
+  std::lock_guard<OrderedMutex> g(b->lock);
+  PageMask seen, dup;
+  for (auto& x : b->res) {
+    out->resident_on.push_back(x.loc);
+    out->chunk.push_back(x.chunk);
+    out->pages.push_back(x.resident.count());
+    dup |= seen & x.resident;
+    seen |= x.resident;
+  }
+  out->read_dup = !dup.empty();
+  if (!b->cpu_ro.empty() || !b->cpu_rw.empty()) out->mapped_on.push_back(kCpuProc);
+  if (b->stable_chunk >= 0) out->mapped_on.push_back(r->stable_dev);
+  if (b->lease_pins)
+    for (auto& x : b->res)
+      if (x.loc.is_gpu()) out->mapped_on.push_back(x.loc.id);
+  out->pinned = thrash_pinned(b, now_ns()) || b->user_pins > 0;
+  out->thrashing = b->thrash.detected;
+  out->policy = b->policy;
+  return Status::OK;
+}
+
+Status Runtime::sync_all() {
+  Status st = Status::OK;
+  for (auto& d : devs_)
+    for (auto& r : d->rings) {
+      if (!r) continue;
+      FenceRef f = r->submit();
+      Status s = f->wait();
+      if (s != Status::OK && st == Status::OK) st = s;
+    }
+  return st;
+}
+
+Status Runtime::enable_peer(int a, int b) {
+  if (a < 0 || b < 0 || a >= ndev() || b >= ndev() || a == b) return Status::INVALID_ARGUMENT;
+  Status st = be_->enable_peer(a, b);
+  if (st != Status::OK) return st;
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  for (auto& p : vs_.peer_pairs)
+    if (p.first == a && p.second == b) return Status::OK;
+  vs_.peer_pairs.emplace_back(a, b);
+  return Status::OK;
+}
+
+void Runtime::set_prefetch_enabled(bool on) { config().perf_prefetch_enable = on ? 1 : 0; }
+
+// ------------------------------------------------------------------ CXL DMA
+Status Runtime::cxl_dma(uint64_t handle, uint64_t gpu_ptr, int dev, uint64_t cxl_off, uint64_t size, int dir,
+                        bool async, uint64_t* tid) {
+  if (global_status() != Status::OK) return global_status();
+  if (dev < 0 || dev >= ndev() || !gpu_ptr || size == 0) return Status::INVALID_ARGUMENT;
+  CxlBuffer buf;
+  Status st = cxl_->lookup(handle, &buf);
+  if (st != Status::OK) return st;
+  if (cxl_off > buf.size || size > buf.size - cxl_off) return Status::INVALID_ARGUMENT;
+  Ring* rg = ring(dev, RingKind::CXL);
+  uint64_t piece = (uint64_t)config().cxl_max_dma_mb << 20;
+  if (piece == 0) piece = size;
+  uint64_t seq = 0;
+  for (uint64_t o = 0; o < size; o += piece) {
+    uint64_t n = std::min(piece, size - o);
+    Sqe s;
+    s.op = SqeOp::COPY;
+    uint64_t cxl_addr = buf.base + cxl_off + o;
+    if (dir & 1) {  // CXL -> GPU
+      s.src = cxl_addr;
+      s.dst = gpu_ptr + o;
+    } else {
+      s.src = gpu_ptr + o;
+      s.dst = cxl_addr;
+    }
+    s.bytes = n;
+    s.user_data = handle;
+    s.file = __FILE__;
+    s.line = __LINE__;
+    s.desc = "cxl_dma";
+    seq = rg->push(std::move(s));
+  }
+  rg->submit();
+  Tools::get().inc(Counter::CxlDmaRequests);
+  Tools::get().inc(Counter::CxlDmaBytes, size);
+  tools_event(ToolsEventType::CxlDma, Cause::Cxl, (dir & 1) ? Loc::cxl(buf.numa_node) : Loc::gpu(dev),
+              (dir & 1) ? Loc::gpu(dev) : Loc::cxl(buf.numa_node), dev, buf.base + cxl_off, size, 0);
+  *tid = ((uint64_t)dev << 56) | seq;
+  if (!async) return rg->wait_seq(seq);
+  return rg->error();
+}
+
+Status Runtime::cxl_dma_wait(uint64_t tid) {
+  int dev = (int)(tid >> 56);
+  if (dev < 0 || dev >= ndev()) return Status::INVALID_ARGUMENT;
+  return ring(dev, RingKind::CXL)->wait_seq(tid & ((1ull << 56) - 1));
+}
+
+// ------------------------------------------------------------------ quiesce / checkpoint
+Status Runtime::quiesce() {
+  pm_.lock();
+  quiesced_.store(true);
+  Status st = sync_all();
+  for (int d = 0; d < ndev(); ++d) poll_device_faults(d);
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  for (auto& kv : vs_.ranges)
+    for (auto& bp : kv.second->blocks) {
+      std::lock_guard<OrderedMutex> g(bp->lock);
+      bp->tracker.wait();
+      bp->tracker.clear();
+    }
+  return st;
+}
+
+Status Runtime::resume() {
+  if (!quiesced_.load()) return Status::INVALID_ARGUMENT;
+  quiesced_.store(false);
+  pm_.unlock();
+  return Status::OK;
+}
+
+namespace {
+constexpr char kMagic[8] = {'O', 'G', 'K', 'M', 'R', 'M', 'A', 'P'};
+constexpr uint32_t kCkptVersion = 1;
+template <class T> void wr(std::ostream& o, const T& v) { o.write((const char*)&v, sizeof v); }
+template <class T> bool rd(std::istream& i, T* v) { return (bool)i.read((char*)v, sizeof *v); }
+}  // namespace
+
+// Residency-map checkpoint: one record per 2 MB block with
+// per-location page masks, policy, and thrash pin state; optionally the data.
+Status Runtime::checkpoint_save(const std::string& path, bool with_data) {
+  bool was_quiesced = quiesced_.load();
+  if (!was_quiesced) quiesce();
+  std::ofstream o(path, std::ios::binary);
+  if (!o) {
+    if (!was_quiesced) resume();
+    return Status::IO_ERROR;
+  }
+  o.write(kMagic, 8);
+  wr(o, kCkptVersion);
+  uint32_t flags = with_data ? 1 : 0;
+  wr(o, flags);
+  std::vector<Range*> rs;
+  {
+    std::shared_lock<OrderedRWLock> vg(vs_.lock);
+    for (auto& kv : vs_.ranges)
+      if (kv.second->type == RangeType::MANAGED) rs.push_back(kv.second.get());
+  }
+  std::sort(rs.begin(), rs.end(), [](Range* a, Range* b) { return a->id < b->id; });
+  uint64_t n = rs.size();
+  wr(o, n);
+  std::vector<char> page(kBlockSize);
+  for (Range* r : rs) {
+    wr(o, r->id);
+    wr(o, (uint32_t)r->type);
+    wr(o, r->flags);
+    wr(o, r->size);
+    wr(o, r->nblocks);
+    uint32_t nl = (uint32_t)r->name.size();
+    wr(o, nl);
+    o.write(r->name.data(), nl);
+    uint64_t gid = r->group ? r->group->id : 0;
+    uint8_t gm = r->group ? (uint8_t)r->group->migratable : 1;
+    wr(o, gid);
+    wr(o, gm);
+    std::shared_lock<OrderedRWLock> vg(vs_.lock);
+    for (auto& bp : r->blocks) {
+      Block* b = bp.get();
+      std::lock_guard<OrderedMutex> g(b->lock);
+      wr(o, b->index);
+      wr(o, b->npages);
+      uint8_t rdup = b->policy.read_dup, hp = b->policy.has_preferred, pt = (uint8_t)b->policy.preferred.tier;
+      int16_t pid = b->policy.preferred.id;
+      wr(o, rdup);
+      wr(o, hp);
+      wr(o, pt);
+      wr(o, pid);
+      wr(o, b->policy.accessed_by);
+      uint8_t pinned = thrash_pinned(b, now_ns());
+      wr(o, pinned);
+      uint32_t nres = (uint32_t)b->res.size();
+      wr(o, nres);
+      for (auto& x : b->res) {
+        uint8_t t = (uint8_t)x.loc.tier;
+        wr(o, t);
+        wr(o, x.loc.id);
+        o.write((const char*)x.resident.w, sizeof x.resident.w);
+      }
+    }
+    if (with_data) {
+      for (auto& bp : r->blocks) {
+        uint64_t bytes = (uint64_t)bp->npages << kPageShift;
+        Status st = read(r, bp->block_offset(), page.data(), std::min(bytes, r->size - bp->block_offset()), -1);
+        if (st != Status::OK) {
+          if (!was_quiesced) resume();
+          return st;
+        }
+        o.write(page.data(), std::min(bytes, r->size - bp->block_offset()));
+      }
+    }
+  }
+  tools_event(ToolsEventType::Checkpoint, Cause::User, Loc{}, Loc{}, kCpuProc, 0, n, 0);
+  if (!was_quiesced) resume();
+  return o ? Status::OK : Status::IO_ERROR;
+}
+
+Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::vector<uint64_t>* new_ids) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) return Status::NOT_FOUND;
+  char magic[8];
+  in.read(magic, 8);
+  if (!in || memcmp(magic, kMagic, 8) != 0) return Status::INVALID_ARGUMENT;
+  uint32_t ver = 0, flags = 0;
+  rd(in, &ver);
+  rd(in, &flags);
+  if (ver != kCkptVersion) return Status::NOT_SUPPORTED;
+  bool has_data = flags & 1;
+  uint64_t n = 0;
+  rd(in, &n);
+  std::vector<char> page(kBlockSize);
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t id, size, nblocks, gid;
+    uint32_t type, rflags, nl;
+    uint8_t gm;
+    if (!rd(in, &id) || !rd(in, &type) || !rd(in, &rflags) || !rd(in, &size) || !rd(in, &nblocks) ||
+        !rd(in, &nl))
+      return Status::IO_ERROR;
+    std::string name(nl, '\0');
+    in.read(&name[0], nl);
+    rd(in, &gid);
+    rd(in, &gm);
+    Range* r = nullptr;
+    Status st = malloc_managed(size, rflags & ~RANGE_STABLE_VA, name, &r, 0);
+    if (st != Status::OK) return st;
+    if (new_ids) new_ids->push_back(r->id);
+    struct BlockRec {
+      Policy pol;
+      std::vector<std::pair<Loc, PageMask>> res;
+    };
+    std::vector<BlockRec> recs(nblocks);
+    for (uint64_t k = 0; k < nblocks; ++k) {
+      uint64_t idx;
+      uint32_t np, nres;
+      uint8_t rdup, hp, pt, pinned;
+      int16_t pid;
+      uint64_t ab;
+      rd(in, &idx);
+      rd(in, &np);
+      rd(in, &rdup);
+      rd(in, &hp);
+      rd(in, &pt);
+      rd(in, &pid);
+      rd(in, &ab);
+      rd(in, &pinned);
+      rd(in, &nres);
+      if (!in || idx >= nblocks) return Status::IO_ERROR;
+      recs[idx].pol.read_dup = rdup;
+      recs[idx].pol.has_preferred = hp;
+      recs[idx].pol.preferred = Loc{(Tier)pt, pid};
+      recs[idx].pol.accessed_by = ab;
+      for (uint32_t q = 0; q < nres; ++q) {
+        uint8_t t;
+        int16_t lid;
+        PageMask m;
+        rd(in, &t);
+        rd(in, &lid);
+        in.read((char*)m.w, sizeof m.w);
+        recs[idx].res.emplace_back(Loc{(Tier)t, lid}, m);
+      }
+    }
+    for (uint64_t k = 0; k < nblocks; ++k) {
+      Block* b = r->block(k);
+      std::lock_guard<OrderedMutex> g(b->lock);
+      b->policy = recs[k].pol;
+    }
+    if (has_data) {
+      for (uint64_t k = 0; k < nblocks; ++k) {
+        uint64_t boff = k << kBlockShift;
+        uint64_t bytes = std::min<uint64_t>(kBlockSize, size - boff);
+        in.read(page.data(), bytes);
+        if (!in) return Status::IO_ERROR;
+        if (!with_data) continue;
+        // Restore data at the first recorded location, then re-create copies.
+        const auto& rs = recs[k].res;
+        if (rs.empty()) continue;
+        Loc primary = rs.front().first;
+        bool ok_loc = arena_for(primary) != nullptr;
+        {
+          std::lock_guard<OrderedMutex> g(r->block(k)->lock);
+          Policy saved = r->block(k)->policy;
+          r->block(k)->policy.has_preferred = ok_loc;
+          if (ok_loc) r->block(k)->policy.preferred = primary;
+          (void)saved;
+        }
+        // write() honours the (temporary) preferred location.
+        st = write(r, boff, page.data(), bytes, -1);
+        {
+          std::lock_guard<OrderedMutex> g(r->block(k)->lock);
+          r->block(k)->policy = recs[k].pol;
+        }
+        if (st != Status::OK) return st;
+        for (size_t q = 1; q < rs.size(); ++q) {
+          if (!arena_for(rs[q].first)) continue;
+          Tracker t;
+          uint32_t first = rs[q].second.next_set(0);
+          if (first >= kPagesPerBlock) continue;
+          // Re-create the duplicate copy (read duplication) of the recorded pages.
+          Ctx c;
+          {
+            std::shared_lock<OrderedRWLock> vg(vs_.lock);
+            Block* b = r->block(k);
+            std::lock_guard<OrderedMutex> g(b->lock);
+            st = make_resident(c, b, rs[q].second, rs[q].first, true, Cause::User);
+          }
+          finish_ctx(c, &t);
+          t.wait();
+          if (st != Status::OK && st != Status::MORE_PROCESSING_REQUIRED) return st;
+        }
+      }
+    }
+    if (gid) {
+      uint64_t ng;
+      create_range_group(&ng);
+      set_range_group(r, ng);
+      set_group_migratable(ng, gm);
+    }
+  }
+  return Status::OK;
+}
+
+// ------------------------------------------------------------------ SIGSEGV
+static struct sigaction g_prev_segv;
+static std::atomic<bool> g_handler_installed{false};
+
+static void segv_handler(int sig, siginfo_t* si, void* uc) {
+  Runtime* rt = Runtime::get();
+  uint64_t addr = (uint64_t)si->si_addr;
+  bool write = false;
+#if defined(__x86_64__)
+  write = (((ucontext_t*)uc)->uc_mcontext.gregs[REG_ERR] & 2) != 0;
+#endif
+  if (rt && rt->cpu_fault(addr, write) == Status::OK) return;
+  if (g_prev_segv.sa_flags & SA_SIGINFO) {
+    if (g_prev_segv.sa_sigaction) {
+      g_prev_segv.sa_sigaction(sig, si, uc);
+      return;
+    }
+  } else if (g_prev_segv.sa_handler != SIG_DFL && g_prev_segv.sa_handler != SIG_IGN) {
+    g_prev_segv.sa_handler(sig);
+    return;
+  }
+  signal(SIGSEGV, SIG_DFL);  // re-fault with the default action
+}
+
+void install_cpu_fault_handler() {
+  bool expected = false;
+  if (!g_handler_installed.compare_exchange_strong(expected, true)) return;
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sa_sigaction = segv_handler;
+  sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prev_segv);
+}
+
+}  // namespace ogkm

@@ -1,0 +1,99 @@
+// Fences and trackers.
+#include "ogkm/tracker.hpp"
+
+#include <algorithm>
+
+#include "ogkm/ring.hpp"
+
+namespace ogkm {
+
+Fence::~Fence() {
+  if (be && event) be->event_destroy(event);
+}
+
+bool Fence::query() {
+  if (done.load(std::memory_order_acquire)) return true;
+  bool d = true;
+  if (ring && ring->completed_seq() < seq) d = false;
+  if (d && be && event) d = be->event_query(event);
+  if (d) done.store(true, std::memory_order_release);
+  return d;
+}
+
+Status Fence::wait() {
+  if (done.load(std::memory_order_acquire)) return Status::OK;
+  Status s = Status::OK;
+  if (be && event) s = be->event_sync(event);
+  if (s == Status::OK && ring) s = ring->wait_seq(seq);
+  if (s == Status::OK) done.store(true, std::memory_order_release);
+  return s;
+}
+
+FenceRef fence_record(Backend* be, int dev, void* stream, Ring* ring, uint64_t seq) {
+  auto f = std::make_shared<Fence>();
+  f->be = be;
+  f->dev = dev;
+  f->ring = ring;
+  f->seq = seq;
+  f->event = be->event_create(dev);
+  if (!f->event || be->event_record(f->event, stream) != Status::OK) {
+    // Could not record: degrade to a ring-only fence (or completed).
+    if (f->event) be->event_destroy(f->event);
+    f->event = nullptr;
+    if (!ring) f->done.store(true);
+  }
+  return f;
+}
+
+void Tracker::add(const FenceRef& f) {
+  if (!f || f->done.load(std::memory_order_relaxed)) return;
+  for (auto& x : fences_)
+    if (x == f) return;
+  // Keep only the newest fence per ring: ring fences complete in order.
+  if (f->ring) {
+    for (auto& x : fences_)
+      if (x->ring == f->ring && x->event && f->event) {
+        if (x->seq <= f->seq) x = f;
+        return;
+      }
+  }
+  fences_.push_back(f);
+  if (fences_.size() > 16) prune();
+}
+
+void Tracker::merge(const Tracker& o) {
+  for (auto& f : o.fences_) add(f);
+}
+
+void Tracker::prune() {
+  fences_.erase(std::remove_if(fences_.begin(), fences_.end(), [](const FenceRef& f) { return f->query(); }),
+                fences_.end());
+}
+
+bool Tracker::query() {
+  prune();
+  return fences_.empty();
+}
+
+Status Tracker::wait() {
+  Status st = Status::OK;
+  for (auto& f : fences_) {
+    Status s = f->wait();
+    if (s != Status::OK && st == Status::OK) st = s;
+  }
+  if (st == Status::OK) fences_.clear();
+  return st;
+}
+
+Status Tracker::gpu_wait(Backend* be, void* stream) const {
+  for (auto& f : fences_) {
+    if (f->done.load(std::memory_order_relaxed)) continue;
+    Status s;
+    if (f->event) s = be->stream_wait_event(stream, f->event);
+    else s = f->wait();
+    if (s != Status::OK) return s;
+  }
+  return Status::OK;
+}
+
+}  // namespace ogkm

@@ -1,0 +1,170 @@
+// Physical memory managers for every tier.
+//
+// ChunkArena is the common 2 MB root-chunk allocator (analog of the GPU PMM,
+// uvm_pmm_gpu.c, and of the sysmem PMM, uvm_pmm_sysmem.c):
+//   * chunks are 2 MB (UVM_CHUNK_SIZE_MAX, uvm_pmm_gpu.h:79) carved out of one
+//     device-usable region (an HBM slab, or a NUMA-bound memfd mapping for
+//     host / CXL tiers);
+//   * contiguous extents are allocated from a free-run map (range allocator,
+//     uvm_range_allocator.c:27-67) so a tensor's blocks can be viewed as one
+//     contiguous device buffer;
+//   * allocated chunks sit on an UNUSED or USED LRU list (uvm_pmm_gpu.c:99-112)
+//     and victims are chosen free -> unused -> used-LRU
+//     (pick_root_chunk_to_evict, uvm_pmm_gpu.c:1460-1500);
+//   * eviction is a two-phase protocol: the arena *reserves* a window and marks
+//     victims EVICTING under its own lock, drops the lock, the owner blocks are
+//     evicted under their block locks, then the window is committed
+//     (lock-order discipline of uvm_pmm_gpu.c:1181-1202);
+//   * every chunk carries a reuse fence (Tracker) that the next writer waits on
+//     GPU-side, so a clean chunk can be recycled without stalling the CPU.
+#pragma once
+
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ogkm/backend.hpp"
+#include "ogkm/common.hpp"
+#include "ogkm/lock_order.hpp"
+#include "ogkm/tracker.hpp"
+
+namespace ogkm {
+
+class Block;
+
+enum class ChunkState : uint8_t { FREE = 0, RESERVED = 1, ALLOCATED = 2, EVICTING = 3 };
+
+struct ChunkInfo {
+  ChunkState state = ChunkState::FREE;
+  uint8_t list = 0;      // 0 none, 1 unused, 2 used
+  bool zeroed = false;
+  uint32_t pin_count = 0;
+  Block* owner = nullptr;
+  int32_t prev = -1, next = -1;  // LRU links
+  uint64_t last_use = 0;         // logical clock
+  Tracker reuse_fence;           // work that must finish before the chunk is overwritten
+};
+
+struct Reservation {
+  int64_t first = -1;
+  uint32_t n = 0;
+  std::vector<uint32_t> victims;  // chunks that must be evicted before commit
+};
+
+class ChunkArena {
+ public:
+  ChunkArena(std::string name, Loc loc, LockOrder order);
+  virtual ~ChunkArena();
+
+  const std::string& name() const { return name_; }
+  Loc loc() const { return loc_; }
+  uint64_t base() const { return base_; }          // device-usable address of chunk 0
+  uint32_t nchunks() const { return nchunks_; }
+  uint64_t chunk_addr(uint32_t i) const { return base_ + ((uint64_t)i << kBlockShift); }
+  int64_t chunk_of(uint64_t addr) const;
+
+  // Contiguous allocation of n chunks without eviction. `hint` = preferred first chunk.
+  Status alloc(uint32_t n, Block* owner_for_all, int64_t hint, uint32_t* first);
+  // Reserve a window of n contiguous chunks, possibly containing evictable chunks.
+  Status reserve(uint32_t n, Reservation* r);
+  void commit(const Reservation& r);                // window -> ALLOCATED (owners set later)
+  void cancel(const Reservation& r);                // give the window back
+  void free(uint32_t first, uint32_t n);
+  void set_owner(uint32_t i, Block* b);
+  Block* owner(uint32_t i);
+  // Evictor calls this once the owner has let go of an EVICTING chunk.
+  void evicted(uint32_t i);
+
+  void touch(uint32_t i, bool has_data);            // LRU bump
+  void pin(uint32_t i);
+  void unpin(uint32_t i);
+  bool pinned(uint32_t i);
+  void add_reuse_fence(uint32_t i, const FenceRef& f);
+  Tracker take_reuse_fence(uint32_t i);             // moves the fence out (for the next writer)
+
+  struct Stats {
+    uint64_t capacity = 0, allocated = 0, peak = 0, pinned = 0, evictions = 0, allocs = 0, frees = 0,
+             used_list = 0, unused_list = 0, reservations = 0;
+  };
+  Stats stats();
+  uint32_t free_chunks();
+  uint32_t largest_free_run();
+  // Leak check (uvm_kvmalloc / UVM_TEST_PMM_CHECK_LEAK analog).
+  uint64_t outstanding_bytes();
+  // Consistency check used by tests; returns empty string when consistent.
+  std::string check();
+
+ protected:
+  void init_chunks(uint64_t base, uint32_t n);
+  std::string name_;
+  Loc loc_;
+  uint64_t base_ = 0;
+  uint32_t nchunks_ = 0;
+
+ private:
+  void lru_remove(uint32_t i);
+  void lru_push_tail(uint32_t i, uint8_t list);
+  void take_run(uint32_t first, uint32_t n);  // remove [first,first+n) from free runs
+  void add_run(uint32_t first, uint32_t n);   // insert + coalesce
+
+  OrderedMutex m_;
+  std::vector<ChunkInfo> chunks_;
+  std::map<uint32_t, uint32_t> free_runs_;  // start -> len
+  int32_t head_[3] = {-1, -1, -1}, tail_[3] = {-1, -1, -1};
+  uint64_t clock_ = 0;
+  Stats st_;
+};
+
+// HBM of one GPU: a slab from the backend (hipMalloc) or VMM handles mapped
+// contiguously at an alias VA (needed for stable-VA managed ranges).
+class HbmArena : public ChunkArena {
+ public:
+  HbmArena(Backend* be, int dev, uint64_t budget_bytes, int provider);
+  ~HbmArena() override;
+  int dev() const { return dev_; }
+  bool vmm() const { return !handles_.empty(); }
+  uint64_t handle(uint32_t i) const { return handles_.empty() ? 0 : handles_[i]; }
+  Status init_status() const { return init_; }
+
+ private:
+  Backend* be_;
+  int dev_;
+  void* slab_ = nullptr;
+  uint64_t bytes_ = 0;
+  std::vector<uint64_t> handles_;
+  Status init_ = Status::OK;
+};
+
+// Host DRAM or CXL.mem of one NUMA node: a memfd mapped once (the arena view,
+// device-registered segment by segment) and bound to the node with mbind.
+// CPU views of managed ranges map the same memfd pages with MAP_FIXED, so the
+// CPU VA of a block can be remapped without copying.
+class HostArena : public ChunkArena {
+ public:
+  HostArena(Backend* be, Tier tier, int node, uint64_t capacity_bytes);
+  ~HostArena() override;
+  int fd() const { return fd_; }
+  int node() const { return node_; }
+  uint64_t file_offset(uint32_t chunk) const { return (uint64_t)chunk << kBlockShift; }
+  // Ensure the segment(s) backing [first, first+n) are populated and registered.
+  Status ensure_registered(uint32_t first, uint32_t n);
+  Status init_status() const { return init_; }
+  bool numa_bound() const { return numa_bound_; }
+
+ private:
+  Backend* be_;
+  int node_;
+  int fd_ = -1;
+  void* view_ = nullptr;
+  uint64_t bytes_ = 0;
+  std::vector<uint8_t> seg_registered_;  // per 1 GB segment
+  std::mutex seg_m_;
+  bool numa_bound_ = false;
+  Status init_ = Status::OK;
+};
+
+constexpr uint64_t kHostSegment = 1ull << 30;
+
+}  // namespace ogkm

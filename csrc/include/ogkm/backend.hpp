@@ -1,0 +1,117 @@
+// Backend = the runtime's hardware abstraction (analog of the UVM HAL tables,
+// uvm_hal.h:779-883, and of the nvUvmInterface bridge, nv_uvm_interface.c:142-1740).
+//
+// Two implementations:
+//   * HipBackend  - MI355X (gfx950): HBM slabs / VMM handles, hipHostRegister'd
+//                   host tiers, side hipStreams, hand-written CDNA4 copy kernels
+//                   (csrc/kernels/copy_kernels.hip) with an SDMA comparator.
+//   * FakeBackend - CPU-only "devices" whose HBM is a memfd and whose streams are
+//                   worker threads doing memcpy (the fake CE HAL of
+//                   uvm_page_tree_test.c:65-100, generalised). Used by the CPU
+//                   test-suite and by the CPU-only north-star config.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ogkm/common.hpp"
+
+namespace ogkm {
+
+// One contiguous copy. Addresses are device-usable pointers (HBM, registered host/CXL).
+struct CopyDesc {
+  uint64_t dst;
+  uint64_t src;
+  uint64_t bytes;
+};
+
+// Page-list pack/unpack (k_gather_pages / k_scatter_pages): copies `npages`
+// pages of `page_bytes` each; page i goes from src_base + idx[i]*page_bytes to
+// dst (contiguous) for gather, or the reverse for scatter.
+struct PageListDesc {
+  uint64_t base;        // sparse side
+  uint64_t contig;      // packed side
+  const uint32_t* idx;  // host pointer to page indices (copied by the backend)
+  uint32_t npages;
+  uint32_t page_bytes;
+};
+
+enum class LinkType : int { NONE = 0, SELF = 1, PCIE = 2, XGMI = 3 };
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual const char* name() const = 0;
+  virtual bool is_fake() const = 0;
+  virtual int device_count() = 0;
+  virtual int device_numa_node(int dev) = 0;
+  virtual Status device_mem_info(int dev, size_t* free_b, size_t* total_b) = 0;
+  virtual Status set_device(int dev) = 0;
+
+  // ---- HBM slab provider (one large allocation carved into 2 MB root chunks)
+  virtual Status hbm_alloc(int dev, size_t bytes, void** ptr) = 0;
+  virtual void hbm_free(int dev, void* ptr, size_t bytes) = 0;
+  // ---- VMM provider (stable VA): physical 2 MB handles mapped into reserved VA
+  virtual bool vmm_supported(int dev) = 0;
+  virtual Status vmm_create(int dev, size_t bytes, uint64_t* handle) = 0;
+  virtual void vmm_release(uint64_t handle) = 0;
+  virtual Status va_reserve(size_t bytes, void** va) = 0;
+  virtual void va_free(void* va, size_t bytes) = 0;
+  virtual Status vmm_map(void* va, size_t bytes, uint64_t handle, int dev) = 0;
+  virtual Status vmm_unmap(void* va, size_t bytes) = 0;
+
+  // ---- host memory pinning (device-visible at the same address)
+  virtual Status host_register(void* p, size_t bytes) = 0;
+  virtual void host_unregister(void* p) = 0;
+  // Fine-grained, coherent host memory for completion queues / fault rings.
+  virtual Status host_alloc_coherent(size_t bytes, void** p) = 0;
+  virtual void host_free_coherent(void* p) = 0;
+
+  // ---- streams and events
+  virtual void* stream_create(int dev, int priority) = 0;
+  virtual void stream_destroy(void* s) = 0;
+  virtual Status stream_sync(void* s) = 0;
+  virtual void* event_create(int dev) = 0;
+  virtual void event_destroy(void* e) = 0;
+  virtual Status event_record(void* e, void* stream) = 0;
+  virtual bool event_query(void* e) = 0;
+  virtual Status event_sync(void* e) = 0;
+  virtual Status stream_wait_event(void* stream, void* e) = 0;
+
+  // ---- work submission (ordered on `stream`)
+  // engine: 0 = copy kernel with the PCIe CU budget, 1 = SDMA, 2 = copy kernel
+  // with the whole chip (HBM<->HBM).
+  virtual Status copy_batch(int dev, const CopyDesc* d, size_t n, void* stream, int engine) = 0;
+  virtual Status gather_pages(int dev, const PageListDesc& d, void* stream) = 0;
+  virtual Status scatter_pages(int dev, const PageListDesc& d, void* stream) = 0;
+  virtual Status memset32(int dev, uint64_t dst, uint32_t pattern, size_t bytes, void* stream) = 0;
+  // Write `value` to *addr (host-coherent) once all prior work on `stream` is done,
+  // with system-scope release (the tracking-semaphore release of uvm_channel.c:1484-1580).
+  virtual Status signal(int dev, uint64_t* addr, uint64_t value, void* stream) = 0;
+  // Make `stream` wait until *addr >= value (GPU-side wait, no CPU involvement).
+  virtual Status wait_value(void* stream, uint64_t* addr, uint64_t value) = 0;
+
+  // ---- peers
+  virtual LinkType link_type(int a, int b) = 0;
+  virtual bool can_access_peer(int a, int b) = 0;
+  virtual Status enable_peer(int a, int b) = 0;
+
+  // ---- export (dma-buf for NICs / importers; IPC for peer processes)
+  virtual Status export_dmabuf(void* p, size_t bytes, int* fd, uint64_t* offset) = 0;
+  virtual Status ipc_handle(void* p, std::string* handle) = 0;
+  virtual Status ipc_open(const std::string& handle, void** p) = 0;
+  virtual void ipc_close(void* p) = 0;
+
+  virtual std::string last_error() { return ""; }
+};
+
+// Creates the best available backend: HIP when a gfx950 GPU is visible and
+// RT_BACKEND != "fake", else the fake backend.
+std::unique_ptr<Backend> make_backend(const std::string& want);
+std::unique_ptr<Backend> make_fake_backend(int ndev, size_t hbm_bytes_per_dev);
+std::unique_ptr<Backend> make_hip_backend();  // nullptr when unavailable
+
+}  // namespace ogkm

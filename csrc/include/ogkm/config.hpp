@@ -1,0 +1,94 @@
+// Runtime configuration: one flat table of integer knobs, loaded
+// defaults -> RT_<NAME> environment variables -> rt.configure(**kw).
+//
+// Knob names and defaults intentionally match the reference's UVM module
+// parameters so behaviour is comparable:
+//   prefetch   uvm_perf_prefetch.c:37-61
+//   thrashing  uvm_perf_thrashing.c:241-318
+//   faults     uvm_gpu_replayable_faults.c:65-116
+//   access ctr uvm_gpu_access_counters.c:40-84
+//   pmm        uvm_pmm_gpu.c:183-192
+//   channels   uvm_channel.c:82-85, uvm_channel.h:49
+//   CXL fork   p2p_cxl.c:137-144, nv-p2p.c:1049,1079-1080, kern_bus_ctrl.c:769-774
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace ogkm {
+
+#define OGKM_CONFIG_KNOBS(X)                                                                          \
+  /* prefetch heuristic */                                                                           \
+  X(perf_prefetch_enable, 1, "enable the bitmap-tree prefetcher")                                    \
+  X(perf_prefetch_threshold, 51, "percent of a subregion resident+faulted before it is prefetched")  \
+  X(perf_prefetch_min_faults, 1, "faults to a block by the same processor before prefetching")       \
+  /* thrashing detection */                                                                          \
+  X(perf_thrashing_enable, 1, "enable thrashing detection")                                          \
+  X(perf_thrashing_threshold, 3, "migrations within lapse that count as thrashing")                  \
+  X(perf_thrashing_pin_threshold, 10, "throttles before a block is pinned")                          \
+  X(perf_thrashing_lapse_usec, 500, "thrashing detection window (us)")                               \
+  X(perf_thrashing_nap, 1, "throttle nap in lapses")                                                 \
+  X(perf_thrashing_epoch, 2000, "lapses before thrashing state resets")                              \
+  X(perf_thrashing_pin, 300, "pin duration in lapses")                                               \
+  X(perf_thrashing_max_resets, 4, "max thrashing resets per block")                                  \
+  X(perf_map_remote_on_native_atomics_fault, 0, "map remotely on atomics faults")                    \
+  /* fault service */                                                                                \
+  X(perf_fault_batch_count, 256, "faults fetched per batch")                                         \
+  X(perf_fault_replay_policy, 2, "0=BLOCK 1=BATCH 2=BATCH_FLUSH 3=ONCE")                            \
+  X(perf_fault_replay_update_put_ratio, 50, "duplicate percent that forces a put update")            \
+  X(perf_fault_max_batches_per_service, 20, "batches per service call")                              \
+  X(perf_fault_max_throttle_per_service, 5, "throttled faults tolerated per service call")           \
+  X(perf_fault_coalesce, 1, "coalesce duplicate faults")                                             \
+  X(perf_reenable_prefetch_faults_lapse_msec, 1000, "re-enable prefetch faults after (ms)")          \
+  /* access counters */                                                                              \
+  X(perf_access_counter_migration_enable, -1, "-1=auto 0=off 1=on")                                  \
+  X(perf_access_counter_batch_count, 256, "notifications per batch")                                 \
+  X(perf_access_counter_threshold, 256, "remote accesses to a 2MB region before migration")          \
+  /* physical memory managers */                                                                     \
+  X(global_oversubscription, 1, "allow eviction from HBM under pressure")                            \
+  X(perf_pma_batch_nonpinned_order, 6, "log2 of chunks evicted per batch")                           \
+  X(hbm_budget_mb, 0, "per-GPU HBM budget for the arena in MB (0 = 90% of free)")                   \
+  X(hbm_provider, 0, "0=slab (one hipMalloc) 1=vmm (hipMemCreate handles, enables stable VA)")       \
+  X(host_node, -1, "NUMA node for the host tier (-1 = GPU-local node)")                              \
+  X(host_budget_mb, 0, "host-tier arena limit in MB (0 = pin budget)")                               \
+  /* channels / ring */                                                                              \
+  X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \
+  X(copy_engine, 0, "0=HIP copy kernels 1=SDMA (hipMemcpyAsync) comparator")                         \
+  X(copy_workgroups, 64, "workgroups per copy-kernel launch (CU budget for migration)")              \
+  X(copy_piece_kb, 64, "bytes per copy work item (KB)")                                              \
+  X(peer_copy, 1, "0=phys 1=virt peer addressing")                                                   \
+  /* misc UVM knobs */                                                                               \
+  X(fault_force_sysmem, 0, "always service faults in system memory")                                 \
+  X(perf_map_remote_on_eviction, 0, "map evicted blocks remotely instead of refaulting")             \
+  X(block_cpu_to_cpu_copy_with_ce, 0, "use the copy engine for CPU->CPU copies")                     \
+  /* CXL fork constants */                                                                           \
+  X(cxl_max_buffers, 256, "max registered CXL buffers")                                              \
+  X(cxl_max_buffer_gb, 1024, "max single CXL buffer (GB)")                                           \
+  X(cxl_pin_budget_pct, 90, "max pinned bytes as percent of system RAM")                             \
+  X(cxl_max_dma_mb, 4095, "single CXL DMA request clamp (MB)")                                       \
+  X(cxl_emulate_node, -1, "treat this NUMA node as CXL when no CXL hardware (-1 = off)")             \
+  /* debug */                                                                                        \
+  X(lock_check, 0, "enable the lock-order checker")                                                  \
+  X(leak_check, 1, "track outstanding arena bytes")                                                  \
+  X(release_asserts, 1, "release asserts set the sticky fatal error")                                \
+  X(tools_queue_entries, 4096, "entries per tools event queue")
+
+struct Config {
+#define OGKM_DECL(name, def, doc) int64_t name = def;
+  OGKM_CONFIG_KNOBS(OGKM_DECL)
+#undef OGKM_DECL
+
+  bool set(const std::string& name, int64_t v);
+  bool get(const std::string& name, int64_t* v) const;
+  void load_env();  // RT_<UPPER_NAME>
+  std::vector<std::string> names() const;
+  std::string doc(const std::string& name) const;
+};
+
+Config& config();
+std::mutex& config_mutex();
+
+}  // namespace ogkm

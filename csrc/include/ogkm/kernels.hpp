@@ -1,0 +1,51 @@
+// Launchers for the hand-written CDNA4 (gfx950) kernels of the migration data
+// plane (csrc/kernels/copy_kernels.hip). Each kernel replaces a Copy-Engine
+// method the reference encodes into pushbuffers:
+//   k_batch_copy      <- ce_hal->memcopy / memcopy_v_to_v  (uvm_volta_ce.c:119-181)
+//   k_gather_pages    <- staged pack of scattered pages     (uvm_va_block.c:3673-3860)
+//   k_scatter_pages   <- staged unpack
+//   k_memset32        <- ce_hal->memset_4                   (uvm_volta_ce.c:259-300)
+//   k_signal          <- semaphore_release                  (uvm_hal.h:789-792)
+//   k_managed_gather  <- replayable-fault producer + access counters (device side)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ogkm {
+
+struct KCopyDesc {      // device-side copy descriptor (24 B)
+  uint64_t dst;
+  uint64_t src;
+  uint64_t bytes;
+};
+
+constexpr int kInlineDescs = 32;
+struct KInlineDescs {   // passed by value as a kernel argument for small batches
+  KCopyDesc d[kInlineDescs];
+  uint64_t piece_start[kInlineDescs + 1];
+};
+
+// Copies n descriptors. `d_descs`/`d_piece_start` are device pointers (large
+// batches) or null with `inl` used. piece_bytes must be a multiple of 4096.
+hipError_t launch_batch_copy(const KCopyDesc* d_descs, const uint64_t* d_piece_start, const KInlineDescs* inl,
+                             uint32_t n, uint64_t total_pieces, uint32_t piece_bytes, uint32_t workgroups,
+                             hipStream_t s);
+hipError_t launch_gather_pages(uint64_t base, uint64_t contig, const uint32_t* d_idx, uint32_t npages,
+                               uint32_t page_bytes, bool scatter, uint32_t workgroups, hipStream_t s);
+hipError_t launch_memset32(uint64_t dst, uint32_t pattern, uint64_t bytes, hipStream_t s);
+hipError_t launch_signal(uint64_t* host_addr, uint64_t value, hipStream_t s);
+
+// Gather `nrows` rows (row_bytes each) of a managed table through its device
+// residency table; misses read zero and are recorded as faults, remote hits are
+// recorded as access-counter notifications.
+struct KFaultBuf {
+  uint32_t* put;
+  void* recs;       // DeviceFaultRecord[entries]
+  uint32_t entries;
+};
+hipError_t launch_managed_gather(const uint64_t* table, uint64_t range_id, const int64_t* rows, uint32_t nrows,
+                                 uint32_t row_bytes, void* out, KFaultBuf fb, uint32_t proc, hipStream_t s);
+
+}  // namespace ogkm

@@ -1,0 +1,103 @@
+// io_uring-style submission/completion ring per (GPU, channel kind).
+//
+// Analog of the UVM channel / pushbuffer / GPFIFO machinery
+// (uvm_channel.c:934 begin_push, :1484-1580 end_push + doorbell, uvm_push.c,
+// uvm_pushbuffer.c) re-designed for MI355X:
+//   * producers append SQEs (copy / gather / scatter / memset / fence-wait)
+//     to a fixed-size submission queue (channel_num_gpfifo_entries, default 1024);
+//   * submit() drains the SQ onto the ring's side hipStream, coalescing
+//     consecutive copies into ONE copy-kernel launch (a batch of descriptors),
+//     then issues a system-scope release of the ring's tracking value into
+//     host-coherent memory (the tracking semaphore) and records a fence;
+//   * completions are reaped as CQEs {user_data, seq, status}; every SQE keeps
+//     its push description (file:line + text, uvm_push.c:169) so a ring error
+//     can name the work that failed (uvm_channel.c:2080-2112);
+//   * errors are sticky per ring and propagate to the runtime's fatal status.
+#pragma once
+
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "ogkm/backend.hpp"
+#include "ogkm/common.hpp"
+#include "ogkm/lock_order.hpp"
+#include "ogkm/tracker.hpp"
+
+namespace ogkm {
+
+enum class RingKind : int {
+  CPU_TO_GPU = 0,   // H2D (host / CXL -> HBM)
+  GPU_TO_CPU = 1,   // D2H
+  GPU_INTERNAL = 2, // D2D within one GPU (compaction, relocation)
+  GPU_TO_GPU = 3,   // peer pushes over xGMI (issued by the source GPU)
+  MEMOPS = 4,       // memset / zero-fill of new chunks
+  CXL = 5,          // cxl_dma requests
+  COUNT = 6
+};
+const char* ring_kind_str(RingKind k);
+
+enum class SqeOp : uint8_t { COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP };
+
+struct Sqe {
+  SqeOp op = SqeOp::NOP;
+  uint64_t user_data = 0;
+  uint64_t dst = 0, src = 0, bytes = 0;
+  uint32_t pattern = 0;            // MEMSET
+  uint32_t page_bytes = 0;         // GATHER / SCATTER
+  std::vector<uint32_t> idx;       // GATHER / SCATTER page indices
+  FenceRef wait;                   // WAIT_FENCE
+  const char* file = "";
+  int line = 0;
+  std::string desc;
+};
+
+struct Cqe {
+  uint64_t user_data;
+  uint64_t seq;
+  int32_t status;
+};
+
+class Ring {
+ public:
+  Ring(Backend* be, int dev, RingKind kind, uint32_t entries);
+  ~Ring();
+  // Append an SQE. Returns its sequence number (tracking value).
+  uint64_t push(Sqe&& s);
+  // Submit everything pushed so far; returns the fence of the last batch
+  // (an already-completed fence if nothing was pending).
+  FenceRef submit();
+  // Highest sequence number known complete (read from host-coherent memory).
+  uint64_t completed_seq();
+  uint64_t submitted_seq() const { return submitted_; }
+  uint64_t pushed_seq() const { return next_seq_ - 1; }
+  Status wait_seq(uint64_t seq);
+  size_t reap(Cqe* out, size_t max);
+  Status error() const { return err_; }
+  void clear_error_for_test();
+  void* stream() const { return stream_; }
+  int dev() const { return dev_; }
+  RingKind kind() const { return kind_; }
+  uint64_t batches() const { return batches_; }
+  std::string last_error_desc();
+
+ private:
+  FenceRef submit_locked();
+  Backend* be_;
+  int dev_;
+  RingKind kind_;
+  uint32_t entries_;
+  void* stream_ = nullptr;
+  uint64_t* sem_ = nullptr;  // host-coherent tracking semaphore
+  OrderedMutex m_{LockOrder::RING};
+  std::deque<std::pair<uint64_t, Sqe>> sq_;   // pushed, not yet submitted
+  std::deque<std::pair<uint64_t, Cqe>> inflight_;  // submitted, not yet reaped
+  uint64_t next_seq_ = 1;
+  uint64_t submitted_ = 0;
+  uint64_t batches_ = 0;
+  FenceRef last_fence_;
+  Status err_ = Status::OK;
+  std::string err_desc_;
+};
+
+}  // namespace ogkm

@@ -1,0 +1,286 @@
+// The runtime: devices, tiers, rings, the VA space, and every operation of the
+// public API (cudaMallocManaged / cudaMemAdvise / cudaMemPrefetchAsync-shaped,
+// in our own namespace), plus fault service, eviction, leases, CXL, checkpoint,
+// injection and stats. One Runtime per process (analog of the per-fd VA space
+// created by UVM_INITIALIZE, uvm.c:950, plus uvm_global.c state).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "ogkm/arena.hpp"
+#include "ogkm/backend.hpp"
+#include "ogkm/common.hpp"
+#include "ogkm/config.hpp"
+#include "ogkm/cxl.hpp"
+#include "ogkm/events.hpp"
+#include "ogkm/ring.hpp"
+#include "ogkm/tracker.hpp"
+#include "ogkm/va_space.hpp"
+
+namespace ogkm {
+
+enum class Advice : int {
+  SET_READ_MOSTLY = 1,
+  UNSET_READ_MOSTLY = 2,
+  SET_PREFERRED_LOCATION = 3,
+  UNSET_PREFERRED_LOCATION = 4,
+  SET_ACCESSED_BY = 5,
+  UNSET_ACCESSED_BY = 6,
+};
+
+enum class Access : int { READ = 1, WRITE = 2, ATOMIC = 3, PREFETCH = 4 };
+
+// One software fault: a processor is about to access [offset, offset+bytes) of a range.
+struct FaultEntry {
+  uint64_t range_id = 0;
+  uint64_t offset = 0;
+  uint64_t bytes = 0;
+  int proc = 0;             // GPU id or kCpuProc
+  Access access = Access::READ;
+  uint64_t ts_ns = 0;
+  // filled by preprocessing
+  uint64_t block = 0;
+  uint32_t first_page = 0, npages = 0;
+  bool duplicate = false;
+};
+
+// Device-recorded miss / access-counter record (written by HIP kernels into
+// host-coherent memory; layout shared with csrc/kernels/*.hip).
+struct DeviceFaultRecord {
+  uint64_t range_id;
+  uint32_t block;
+  uint16_t page;
+  uint8_t access;   // 1 read 2 write
+  uint8_t kind;     // 0 miss (fault), 1 remote access (access counter)
+  uint32_t proc;
+  uint32_t pad;
+};
+static_assert(sizeof(DeviceFaultRecord) == 24, "device fault record layout");
+
+// Replayable fault buffer analog (uvm_gpu_replayable_faults.c:844-988): a
+// ring in host-coherent memory that device code appends to with atomics.
+struct DeviceFaultBuffer {
+  uint32_t* put = nullptr;      // device-incremented
+  uint32_t get = 0;
+  uint32_t entries = 0;
+  DeviceFaultRecord* recs = nullptr;
+  uint64_t overflows = 0;
+};
+
+// Per-range device residency table (2 entries per block: hbm address, remote
+// address; 0 = absent). Lives in host-coherent memory so kernels can consult
+// it and record misses without a host round trip.
+struct DeviceResidencyTable {
+  uint64_t* entries = nullptr;
+  uint64_t nblocks = 0;
+  int dev = 0;
+};
+
+struct Lease {
+  uint64_t id = 0;
+  Range* range = nullptr;
+  uint64_t offset = 0, bytes = 0;
+  int proc = 0;
+  bool remote = false;   // pointer targets host/CXL/peer memory (zero-copy)
+  uint64_t dptr = 0;     // device pointer of range byte `offset`
+  std::vector<std::pair<ChunkArena*, uint32_t>> pinned_chunks;
+  std::vector<Block*> blocks;
+  Tracker ready;         // consumer must wait on this before use
+};
+
+struct Device {
+  int id = 0;
+  int numa = 0;
+  std::unique_ptr<HbmArena> hbm;
+  std::unique_ptr<Ring> rings[(int)RingKind::COUNT];
+  DeviceFaultBuffer fault_buf;
+};
+
+struct Injection {
+  std::atomic<int64_t> alloc_fail_after{-1};   // HBM chunk allocations that succeed before failing
+  std::atomic<int64_t> evict_fail{0};          // next N evictions fail
+  std::atomic<int64_t> copy_drop{0};           // next N ring copies are dropped (link error)
+  std::atomic<uint64_t> peer_link_down{0};     // bit g: peer link of GPU g down
+  std::atomic<int64_t> populate_error{0};      // next N populates fail
+  std::atomic<int64_t> host_alloc_error{0};    // next N host chunk allocs fail
+};
+
+struct ResidencyInfo {   // UVM_TEST_VA_RESIDENCY_INFO analog (uvm_test_ioctl.h:626-674)
+  std::vector<Loc> resident_on;
+  std::vector<int64_t> chunk;       // per resident_on entry
+  std::vector<uint32_t> pages;      // resident page count per entry
+  std::vector<int> mapped_on;       // processors with a mapping (CPU view / stable VA / leases)
+  bool read_dup = false;
+  bool pinned = false;
+  bool thrashing = false;
+  Policy policy;
+};
+
+class Runtime {
+ public:
+  static Runtime* get();                          // nullptr before init
+  static Runtime* init(const std::string& backend, int fake_devices, uint64_t fake_hbm_bytes);
+  static void shutdown();
+  ~Runtime();
+
+  Backend* be() { return be_.get(); }
+  int ndev() const { return (int)devs_.size(); }
+  Device& dev(int i) { return *devs_[i]; }
+  VaSpace& vs() { return vs_; }
+  Injection& inject() { return inject_; }
+  CxlTopology& cxl_topology() { return cxl_topo_; }
+  CxlRegistry& cxl() { return *cxl_; }
+  int host_node() const { return host_node_; }
+  Loc cpu_loc() const { return Loc::host(host_node_); }
+  Loc proc_loc(int proc) const { return proc == kCpuProc ? cpu_loc() : Loc::gpu(proc); }
+
+  // ---- tiers
+  Status init_device(int d, uint64_t budget_bytes);   // (re)create the HBM arena of d
+  HostArena* host_arena(Tier t, int node);            // created on first use
+  ChunkArena* arena_for(const Loc& l);
+  Ring* ring(int dev, RingKind k) { return devs_[dev]->rings[(int)k].get(); }
+
+  // ---- allocation / ranges (UvmMemMap + mmap analog)
+  Status malloc_managed(uint64_t size, uint32_t flags, const std::string& name, Range** out, int stable_dev = 0);
+  Status map_external(uint64_t ptr, uint64_t size, int dev, const std::string& name, Range** out);
+  Status alloc_device_p2p(uint64_t size, int dev, const std::string& name, Range** out);
+  Status free_range(Range* r);
+  Range* find_range(uint64_t addr);
+  Range* range_by_id(uint64_t id);
+
+  // ---- policy (uvm_policy.c)
+  Status mem_advise(Range* r, uint64_t off, uint64_t len, Advice a, Loc loc, int proc);
+  Status create_range_group(uint64_t* id);
+  Status set_range_group(Range* r, uint64_t group_id);
+  Status set_group_migratable(uint64_t group_id, bool migratable);
+
+  // ---- migration (uvm_migrate.c / uvm_va_block.c make_resident)
+  Status prefetch(Range* r, uint64_t off, uint64_t len, Loc dst, Tracker* out, Cause cause = Cause::ApiMigrate);
+  Status migrate_sync(Range* r, uint64_t off, uint64_t len, Loc dst);
+  Status evict_range(Range* r, Loc from);  // push blocks resident at `from` down a tier
+
+  // ---- software faults / leases
+  Status service_faults(std::vector<FaultEntry>& faults, Tracker* out);
+  Status acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out);
+  Status release(Lease* l, void* stream);  // consumer's last use recorded on `stream`
+  Lease* lease_by_id(uint64_t id);
+  Status cpu_fault(uint64_t addr, bool write);        // SIGSEGV path
+  size_t poll_device_faults(int dev);                  // service device-recorded faults
+  Status device_table(Range* r, DeviceResidencyTable** out);
+
+  // ---- data movement helpers
+  Status write(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev);
+  Status read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_dev);
+  Status fill(Range* r, uint64_t off, uint64_t bytes, uint32_t pattern);
+
+  // ---- introspection
+  Status residency_info(Range* r, uint64_t off, ResidencyInfo* out);
+  Status sync_all();
+
+  // ---- CXL (fork capability)
+  Status cxl_dma(uint64_t handle, uint64_t gpu_ptr, int dev, uint64_t cxl_off, uint64_t size, int dir, bool async,
+                 uint64_t* transfer_id);
+  Status cxl_dma_wait(uint64_t transfer_id);
+
+  // ---- checkpoint (residency map, §5.4) + suspend/resume (uvm_global.c:272-415)
+  Status quiesce();
+  Status resume();
+  Status checkpoint_save(const std::string& path, bool with_data);
+  Status checkpoint_load(const std::string& path, bool with_data, std::vector<uint64_t>* new_range_ids);
+
+  // ---- peers
+  Status enable_peer(int a, int b);
+
+  // ---- perf modules
+  void set_prefetch_enabled(bool on);
+  // internal helpers used by engine files
+  ThrashState& thrash_of(Block* b) { return b->thrash; }
+
+  std::mutex leases_m_;
+  std::unordered_map<uint64_t, std::unique_ptr<Lease>> leases_;
+  uint64_t next_lease_ = 1;
+
+  // Engine internals (migrate.cpp)
+  struct Ctx;  // per-operation migration context
+  Status make_resident(Ctx& c, Block* b, const PageMask& pages, Loc dst, bool read_dup, Cause cause);
+  Status populate(Ctx& c, Block* b, Loc dst, int64_t chunk_hint, Residency** out);
+  Status evict_chunk(ChunkArena* a, uint32_t chunk);
+  Status ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r);
+  Status alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* first);
+  Loc demotion_target(const Loc& from);
+  void cpu_map_block(Block* b);  // refresh CPU view protections
+  void stable_map_block(Block* b);
+  void finish_ctx(Ctx& c, Tracker* out);
+  void drop_copy(Ctx& c, Block* b, const Loc& l);  // release a residency (block lock held)
+  Status queue_copy(Ctx& c, Block* b, Residency* from, Residency* to, const PageMask& pages);
+  void update_device_table(Block* b);
+
+  std::atomic<bool> quiesced_{false};
+  std::atomic<uint64_t> cxl_transfers_{0};
+
+ private:
+  Runtime() = default;
+  std::unique_ptr<Backend> be_;
+  std::vector<std::unique_ptr<Device>> devs_;
+  std::vector<std::unique_ptr<HostArena>> host_arenas_;  // index = tier*kMaxNodes + node
+  std::mutex host_arenas_m_;
+  VaSpace vs_;
+  Injection inject_;
+  CxlTopology cxl_topo_;
+  std::unique_ptr<CxlRegistry> cxl_;
+  int host_node_ = 0;
+  std::unordered_map<uint64_t, std::unique_ptr<DeviceResidencyTable>> dev_tables_;
+  std::mutex dev_tables_m_;
+  std::unordered_map<uint64_t, std::pair<Ring*, uint64_t>> cxl_pending_;
+  std::mutex cxl_m_;
+  OrderedMutex pm_{LockOrder::GLOBAL_PM};
+};
+
+// Per-operation migration context: rings used, blocks touched, chunks read by
+// queued copies (their reuse fences) and chunks to free once those copies land.
+struct Runtime::Ctx {
+  Cause cause = Cause::User;
+  struct Touch { Ring* ring; Block* block; };
+  struct ChunkUse { Ring* ring; ChunkArena* arena; uint32_t chunk; bool free_after; };
+  std::vector<Touch> touched;
+  std::vector<ChunkUse> chunk_uses;
+  std::vector<Ring*> rings;
+  std::vector<Block*> cpu_refresh;    // CPU views to refresh after submission
+  ChunkArena* need_arena = nullptr;   // set on MORE_PROCESSING_REQUIRED
+  uint32_t need_n = 0;
+  void use_ring(Ring* r) {
+    for (Ring* x : rings)
+      if (x == r) return;
+    rings.push_back(r);
+  }
+};
+
+// Select where a fault from `proc` on block `b` should be serviced
+// (uvm_va_block_select_residency, uvm_va_block.c:11560-11762).
+struct ResidencyDecision {
+  Loc dst;
+  bool read_dup = false;
+  bool map_remote = false;  // keep data where it is, access it remotely
+};
+ResidencyDecision select_residency(Runtime* rt, Block* b, int proc, Access access, const PageMask& pages);
+
+// Bitmap-tree prefetch hint (uvm_perf_prefetch.c:102-250).
+PageMask prefetch_hint(const PageMask& resident_on_dst, const PageMask& faulted, uint32_t npages, uint32_t threshold_pct);
+
+// Thrashing hint (uvm_perf_thrashing.c:1615).
+enum class ThrashHint { NONE = 0, THROTTLE = 1, PIN = 2 };
+ThrashHint thrash_on_migration(Block* b, int dst_slot, uint64_t now);
+bool thrash_pinned(Block* b, uint64_t now);
+
+// SIGSEGV handler installation for CPU faults on managed CPU views.
+void install_cpu_fault_handler();
+
+}  // namespace ogkm

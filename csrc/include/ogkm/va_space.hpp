@@ -1,0 +1,164 @@
+// Virtual-address data model: VaSpace -> Range -> 2 MB Block.
+//
+//  * VaSpace  (uvm_va_space.h:186): per-runtime container of ranges, keyed by the
+//    CPU view address in an ordered map (range tree, uvm_range_tree.c:98-156).
+//  * Range    (uvm_va_range.h:107-113): MANAGED, EXTERNAL, CXL or DEVICE_P2P.
+//    A managed range owns a CPU view (mmap reservation whose 2 MB windows are
+//    mapped onto host/CXL arena pages on demand) and, in stable-VA mode, a
+//    device VA reservation whose blocks are VMM-mapped onto HBM chunks.
+//  * Block    (uvm_va_block.h:101-523): residency per memory location as 4 KB
+//    page masks plus the backing chunk, CPU mapping state, policy, perf state,
+//    lease pins and a tracker of outstanding copies.
+//  * Policy   (uvm_va_policy.h:57-82): read duplication, preferred location
+//    (incl. NUMA node -> CXL tier), accessed_by.
+#pragma once
+
+#include <atomic>
+#include <deque>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ogkm/arena.hpp"
+#include "ogkm/common.hpp"
+#include "ogkm/lock_order.hpp"
+#include "ogkm/tracker.hpp"
+
+namespace ogkm {
+
+class Range;
+class VaSpace;
+class RangeGroup;
+
+struct Policy {
+  bool read_dup = false;
+  bool has_preferred = false;
+  Loc preferred{};
+  ProcMask accessed_by = 0;
+};
+
+// Thrashing detection state (uvm_perf_thrashing.c:37-82 analog, block granularity).
+struct ThrashState {
+  uint64_t last_migration_ns = 0;
+  uint64_t window_start_ns = 0;
+  uint32_t events_in_window = 0;
+  uint32_t throttles = 0;
+  uint32_t resets = 0;
+  uint64_t epoch_start_ns = 0;
+  uint64_t pinned_until_ns = 0;
+  int last_dst_slot = -1;
+  bool detected = false;
+};
+
+// Software access counters (uvm_gpu_access_counters.c analog): remote accesses
+// per accessing processor to this 2 MB region.
+struct AccessCounterState {
+  uint32_t remote_hits[kMaxGpus + 1] = {0};
+};
+
+struct Residency {
+  int slot = -1;             // Loc::slot()
+  Loc loc{};
+  PageMask resident;
+  ChunkArena* arena = nullptr;
+  int64_t chunk = -1;
+};
+
+class Block {
+ public:
+  Block(Range* r, uint64_t index, uint32_t npages) : range(r), index(index), npages(npages) {}
+  Range* range;
+  uint64_t index;      // block number inside the range
+  uint32_t npages;     // < 512 for a partial last block
+  OrderedMutex lock{LockOrder::VA_BLOCK};
+  Policy policy;
+
+  // One entry per location holding a chunk. A deque: appending never moves
+  // existing entries, so Residency* stay valid while copies are queued.
+  std::deque<Residency> res;
+  PageMask cpu_ro, cpu_rw;     // CPU view protection state
+  ChunkArena* cpu_arena = nullptr;  // host/CXL chunk currently mapped in the CPU window
+  int64_t cpu_chunk = -1;
+  int64_t stable_chunk = -1;   // HBM chunk VMM-mapped at the stable device VA (-1 = none)
+  uint32_t lease_pins = 0;
+  uint32_t user_pins = 0;      // range-group / explicit pins (non-migratable)
+  uint64_t last_access_ns = 0;
+  uint32_t faults_by_proc[kMaxGpus + 1] = {0};
+  ThrashState thrash;
+  AccessCounterState counters;
+  Tracker tracker;             // outstanding copies touching this block
+
+  Residency* find(const Loc& l);
+  Residency* find_slot(int slot);
+  Residency& get_or_add(const Loc& l);
+  void drop(const Loc& l);
+  PageMask resident_anywhere() const;
+  LocMask resident_locs(const PageMask& pages) const;  // locations holding any of `pages`
+  uint64_t block_offset() const { return index << kBlockShift; }
+  PageMask valid_pages() const { return PageMask::range(0, npages); }
+};
+
+enum class RangeType : int { MANAGED = 0, EXTERNAL = 1, CXL = 2, DEVICE_P2P = 3 };
+const char* range_type_str(RangeType t);
+
+enum RangeFlags : uint32_t {
+  RANGE_STABLE_VA = 1u << 0,   // device VA fixed for the lifetime (VMM mapped)
+  RANGE_NO_CPU_VIEW = 1u << 1, // skip the CPU view reservation
+};
+
+class Range {
+ public:
+  Range(VaSpace* vs, uint64_t id, RangeType t, uint64_t size, uint32_t flags, std::string name);
+  ~Range();
+  VaSpace* vs;
+  uint64_t id;
+  RangeType type;
+  uint64_t size;        // requested bytes
+  uint64_t nblocks;
+  uint32_t flags;
+  std::string name;
+  uint8_t* cpu_view = nullptr;  // CPU VA (reserved PROT_NONE, 2 MB aligned)
+  uint64_t cpu_view_bytes = 0;
+  void* dev_va = nullptr;       // stable VA reservation
+  int stable_dev = -1;
+  // EXTERNAL / DEVICE_P2P: foreign memory registered into the VA space
+  uint64_t ext_ptr = 0;
+  int ext_dev = -1;
+  bool ext_owned = false;       // allocated by the runtime (DEVICE_P2P)
+  RangeGroup* group = nullptr;
+  std::vector<std::unique_ptr<Block>> blocks;
+  std::atomic<int64_t> views{0};  // live tensor views / leases
+  bool destroyed = false;
+
+  uint64_t addr() const { return (uint64_t)cpu_view; }
+  Block* block(uint64_t i) { return i < blocks.size() ? blocks[i].get() : nullptr; }
+};
+
+class RangeGroup {
+ public:
+  explicit RangeGroup(uint64_t id) : id(id) {}
+  uint64_t id;
+  bool migratable = true;   // false = residency frozen (UVM non-migratable range group)
+  std::vector<Range*> ranges;
+};
+
+class VaSpace {
+ public:
+  VaSpace() = default;
+  OrderedRWLock lock{LockOrder::VA_SPACE};
+  std::map<uint64_t, Range*> tree;  // cpu_view start -> range
+  std::unordered_map<uint64_t, std::unique_ptr<Range>> ranges;
+  std::unordered_map<uint64_t, std::unique_ptr<RangeGroup>> groups;
+  uint64_t next_range_id = 1;
+  uint64_t next_group_id = 1;
+  ProcMask registered_gpus = 0;
+  uint64_t peers_enabled = 0;  // bit (a*kMaxGpus+b) compressed into a set below
+  std::vector<std::pair<int, int>> peer_pairs;
+
+  Range* find_locked(uint64_t addr);  // caller holds lock (shared or exclusive)
+  Range* by_id_locked(uint64_t id);
+};
+
+}  // namespace ogkm

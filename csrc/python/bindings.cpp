@@ -1,0 +1,697 @@
+// pybind11 bindings: the `_ogkm` extension module (loaded by
+// open-gpu-kernel-modules_amd/_native.py). Thin: every call maps to one Runtime
+// operation; Status codes become Python exceptions with the status name.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "ogkm/kernels.hpp"
+#include "ogkm/lock_order.hpp"
+#include "ogkm/runtime.hpp"
+
+namespace py = pybind11;
+using namespace ogkm;
+
+namespace ogkm {
+void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs);
+void* torch_alloc(size_t size, int device);
+void torch_free(void* p, int device);
+}  // namespace ogkm
+
+namespace {
+
+struct StatusError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+void check(Status s, const char* what) {
+  if (s != Status::OK) throw StatusError(std::string(what) + ": " + status_str(s));
+}
+
+Runtime* rt() {
+  Runtime* r = Runtime::get();
+  if (!r) throw StatusError("runtime not initialised: call ogkm.rt.init()");
+  return r;
+}
+
+Range* range(uint64_t id) {
+  Range* r = rt()->range_by_id(id);
+  if (!r) throw StatusError("unknown range id " + std::to_string(id));
+  return r;
+}
+
+Loc make_loc(int tier, int id) {
+  if (tier < 0 || tier > 2) throw StatusError("bad tier");
+  return Loc{(Tier)tier, (int16_t)id};
+}
+
+py::dict loc_dict(const Loc& l) {
+  py::dict d;
+  d["tier"] = tier_str(l.tier);
+  d["id"] = l.id;
+  return d;
+}
+
+// ---- DLPack (ABI-compatible definitions; consumed by torch.from_dlpack)
+struct DLDevice { int32_t device_type; int32_t device_id; };
+struct DLDataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+struct DLCtx {
+  std::vector<int64_t> shape;
+  uint64_t range_id = 0;
+};
+
+void dl_deleter(DLManagedTensor* t) {
+  auto* c = (DLCtx*)t->manager_ctx;
+  if (c->range_id)
+    if (Runtime* r = Runtime::get())
+      if (Range* rg = r->range_by_id(c->range_id)) rg->views.fetch_sub(1);
+  delete c;
+  delete t;
+}
+
+void capsule_destructor(PyObject* cap) {
+  if (PyCapsule_IsValid(cap, "dltensor")) {
+    auto* t = (DLManagedTensor*)PyCapsule_GetPointer(cap, "dltensor");
+    if (t && t->deleter) t->deleter(t);
+  }
+}
+
+py::object make_capsule(uint64_t ptr, std::vector<int64_t> shape, int code, int bits, int device_type, int device_id,
+                        uint64_t range_id) {
+  auto* t = new DLManagedTensor();
+  auto* c = new DLCtx();
+  c->shape = std::move(shape);
+  c->range_id = range_id;
+  if (range_id)
+    if (Range* rg = rt()->range_by_id(range_id)) rg->views.fetch_add(1);
+  t->dl_tensor.data = (void*)ptr;
+  t->dl_tensor.device = DLDevice{device_type, device_id};
+  t->dl_tensor.ndim = (int32_t)c->shape.size();
+  t->dl_tensor.dtype = DLDataType{(uint8_t)code, (uint8_t)bits, 1};
+  t->dl_tensor.shape = c->shape.data();
+  t->dl_tensor.strides = nullptr;
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = c;
+  t->deleter = dl_deleter;
+  return py::reinterpret_steal<py::object>(PyCapsule_New(t, "dltensor", capsule_destructor));
+}
+
+class PyTracker {
+ public:
+  Tracker t;
+  void wait() {
+    py::gil_scoped_release nogil;
+    check(t.wait(), "tracker wait");
+  }
+  bool query() { return t.query(); }
+  void gpu_wait(uint64_t stream) { check(t.gpu_wait(rt()->be(), (void*)stream), "tracker gpu_wait"); }
+  size_t size() const { return t.size(); }
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_ogkm, m) {
+  m.doc() = "ogkm: MI355X-native unified-memory + CXL tiering runtime (native core)";
+  py::register_exception<StatusError>(m, "RuntimeStatusError");
+
+  py::class_<PyTracker>(m, "Tracker")
+      .def(py::init<>())
+      .def("wait", &PyTracker::wait)
+      .def("query", &PyTracker::query)
+      .def("gpu_wait", &PyTracker::gpu_wait)
+      .def("__len__", &PyTracker::size);
+
+  // ---- lifecycle
+  m.def("init", [](const std::string& backend, int fake_devices, uint64_t fake_hbm_mb) {
+    Runtime* r = Runtime::init(backend, fake_devices, fake_hbm_mb << 20);
+    if (!r) throw StatusError("no backend available for '" + backend + "'");
+    return std::string(r->be()->name());
+  }, py::arg("backend") = "auto", py::arg("fake_devices") = 2, py::arg("fake_hbm_mb") = 256);
+  m.def("shutdown", [] {
+    py::gil_scoped_release nogil;
+    Runtime::shutdown();
+  });
+  m.def("is_initialized", [] { return Runtime::get() != nullptr; });
+  m.def("backend_name", [] { return std::string(rt()->be()->name()); });
+  m.def("device_count", [] { return rt()->ndev(); });
+  m.def("host_node", [] { return rt()->host_node(); });
+  m.def("device_numa_node", [](int d) { return rt()->dev(d).numa; });
+  m.def("global_status", [] { return std::string(status_str(global_status())); });
+  m.def("clear_fatal_for_test", [] { clear_fatal_for_test(); });
+  m.def("init_device", [](int d, uint64_t budget) { check(rt()->init_device(d, budget), "init_device"); });
+  m.def("sync_all", [] {
+    py::gil_scoped_release nogil;
+    check(rt()->sync_all(), "sync_all");
+  });
+
+  // ---- config
+  m.def("configure", [](const std::string& name, int64_t v) {
+    std::lock_guard<std::mutex> g(config_mutex());
+    if (!config().set(name, v)) throw StatusError("unknown config knob " + name);
+    if (name == "lock_check") lockcheck::set_enabled(v != 0);
+  });
+  m.def("get_config", [](const std::string& name) {
+    int64_t v;
+    if (!config().get(name, &v)) throw StatusError("unknown config knob " + name);
+    return v;
+  });
+  m.def("config_names", [] { return config().names(); });
+  m.def("config_doc", [](const std::string& n) { return config().doc(n); });
+  m.def("set_log_level", [](int l) { set_log_level((LogLevel)l); });
+
+  // ---- ranges
+  m.def("malloc_managed", [](uint64_t size, uint32_t flags, const std::string& name, int stable_dev) {
+    Range* r;
+    check(rt()->malloc_managed(size, flags, name, &r, stable_dev), "malloc_managed");
+    return r->id;
+  }, py::arg("size"), py::arg("flags") = 0, py::arg("name") = "", py::arg("stable_dev") = 0);
+  m.def("free", [](uint64_t id) {
+    py::gil_scoped_release nogil;
+    check(rt()->free_range(range(id)), "free");
+  });
+  m.def("map_external", [](uint64_t ptr, uint64_t size, int dev, const std::string& name) {
+    Range* r;
+    check(rt()->map_external(ptr, size, dev, name, &r), "map_external");
+    return r->id;
+  });
+  m.def("alloc_device_p2p", [](uint64_t size, int dev, const std::string& name) {
+    Range* r;
+    check(rt()->alloc_device_p2p(size, dev, name, &r), "alloc_device_p2p");
+    return r->id;
+  });
+  m.def("range_info", [](uint64_t id) {
+    Range* r = range(id);
+    py::dict d;
+    d["id"] = r->id;
+    d["size"] = r->size;
+    d["addr"] = r->addr();
+    d["nblocks"] = r->nblocks;
+    d["type"] = range_type_str(r->type);
+    d["name"] = r->name;
+    d["dev_va"] = (uint64_t)r->dev_va;
+    d["stable_dev"] = r->stable_dev;
+    d["ext_ptr"] = r->ext_ptr;
+    d["views"] = r->views.load();
+    d["group"] = r->group ? r->group->id : 0;
+    return d;
+  });
+  m.def("find_range", [](uint64_t addr) -> int64_t {
+    Range* r = rt()->find_range(addr);
+    return r ? (int64_t)r->id : -1;
+  });
+  m.def("range_ids", [] {
+    std::vector<uint64_t> ids;
+    std::shared_lock<OrderedRWLock> g(rt()->vs().lock);
+    for (auto& kv : rt()->vs().ranges) ids.push_back(kv.first);
+    return ids;
+  });
+
+  // ---- policy / migration
+  m.def("mem_advise", [](uint64_t id, uint64_t off, uint64_t len, int advice, int tier, int loc, int proc) {
+    check(rt()->mem_advise(range(id), off, len, (Advice)advice, make_loc(tier, loc), proc), "mem_advise");
+  });
+  m.def("prefetch", [](uint64_t id, uint64_t off, uint64_t len, int tier, int loc) {
+    auto t = std::make_unique<PyTracker>();
+    Status s;
+    {
+      py::gil_scoped_release nogil;
+      s = rt()->prefetch(range(id), off, len, make_loc(tier, loc), &t->t, Cause::Prefetch);
+    }
+    check(s, "prefetch");
+    return t;
+  });
+  m.def("migrate", [](uint64_t id, uint64_t off, uint64_t len, int tier, int loc) {
+    Range* r = range(id);
+    py::gil_scoped_release nogil;
+    check(rt()->migrate_sync(r, off, len, make_loc(tier, loc)), "migrate");
+  });
+  m.def("evict", [](uint64_t id, int tier, int loc) {
+    Range* r = range(id);
+    py::gil_scoped_release nogil;
+    check(rt()->evict_range(r, make_loc(tier, loc)), "evict");
+  });
+  m.def("create_range_group", [] {
+    uint64_t g;
+    check(rt()->create_range_group(&g), "create_range_group");
+    return g;
+  });
+  m.def("set_range_group", [](uint64_t id, uint64_t g) { check(rt()->set_range_group(range(id), g), "set_range_group"); });
+  m.def("set_group_migratable", [](uint64_t g, bool mig) {
+    check(rt()->set_group_migratable(g, mig), "set_group_migratable");
+  });
+
+  // ---- leases
+  m.def("acquire", [](uint64_t id, uint64_t off, uint64_t len, int proc, int access) {
+    Range* r = range(id);
+    Lease* l = nullptr;
+    Status s;
+    {
+      py::gil_scoped_release nogil;
+      s = rt()->acquire(r, off, len, proc, (Access)access, &l);
+    }
+    check(s, "acquire");
+    py::dict d;
+    d["id"] = l->id;
+    d["dptr"] = l->dptr;
+    d["remote"] = l->remote;
+    d["pending"] = l->ready.size();
+    return d;
+  });
+  m.def("lease_wait", [](uint64_t lid, uint64_t stream) {
+    Lease* l = rt()->lease_by_id(lid);
+    if (!l) throw StatusError("unknown lease");
+    if (stream) check(l->ready.gpu_wait(rt()->be(), (void*)stream), "lease gpu_wait");
+    else {
+      py::gil_scoped_release nogil;
+      check(l->ready.wait(), "lease wait");
+    }
+  });
+  m.def("release", [](uint64_t lid, uint64_t stream) {
+    Lease* l = rt()->lease_by_id(lid);
+    if (!l) throw StatusError("unknown lease");
+    check(rt()->release(l, (void*)stream), "release");
+  });
+  m.def("service_faults", [](std::vector<std::tuple<uint64_t, uint64_t, uint64_t, int, int>> fs) {
+    std::vector<FaultEntry> faults;
+    for (auto& f : fs) {
+      FaultEntry e;
+      e.range_id = std::get<0>(f);
+      e.offset = std::get<1>(f);
+      e.bytes = std::get<2>(f);
+      e.proc = std::get<3>(f);
+      e.access = (Access)std::get<4>(f);
+      e.ts_ns = now_ns();
+      faults.push_back(e);
+    }
+    py::gil_scoped_release nogil;
+    Tracker t;
+    Status s = rt()->service_faults(faults, &t);
+    t.wait();
+    check(s, "service_faults");
+  });
+  m.def("cpu_fault", [](uint64_t addr, bool write) { check(rt()->cpu_fault(addr, write), "cpu_fault"); });
+  m.def("poll_device_faults", [](int dev) {
+    py::gil_scoped_release nogil;
+    return rt()->poll_device_faults(dev);
+  });
+  m.def("device_table", [](uint64_t id) {
+    DeviceResidencyTable* t;
+    check(rt()->device_table(range(id), &t), "device_table");
+    return (uint64_t)t->entries;
+  });
+  m.def("managed_gather", [](uint64_t id, uint64_t rows_dptr, uint32_t nrows, uint32_t row_bytes, uint64_t out_dptr,
+                             int dev, uint64_t stream) {
+    Runtime* r = rt();
+    if (r->be()->is_fake()) throw StatusError("managed_gather needs the HIP backend");
+    Range* rg = range(id);
+    DeviceResidencyTable* t;
+    check(r->device_table(rg, &t), "device_table");
+    DeviceFaultBuffer& fb = r->dev(dev).fault_buf;
+    KFaultBuf kfb{fb.put, fb.recs, fb.entries};
+    hipError_t e = launch_managed_gather(t->entries, rg->id, (const int64_t*)rows_dptr, nrows, row_bytes,
+                                         (void*)out_dptr, kfb, (uint32_t)dev, (hipStream_t)stream);
+    if (e != hipSuccess) throw StatusError(std::string("managed_gather launch: ") + hipGetErrorString(e));
+  });
+
+  // ---- data
+  m.def("write", [](uint64_t id, uint64_t off, uint64_t ptr, uint64_t bytes, int src_dev) {
+    Range* r = range(id);
+    py::gil_scoped_release nogil;
+    check(rt()->write(r, off, (const void*)ptr, bytes, src_dev), "write");
+  });
+  m.def("read", [](uint64_t id, uint64_t off, uint64_t ptr, uint64_t bytes, int dst_dev) {
+    Range* r = range(id);
+    py::gil_scoped_release nogil;
+    check(rt()->read(r, off, (void*)ptr, bytes, dst_dev), "read");
+  });
+  m.def("fill", [](uint64_t id, uint64_t off, uint64_t bytes, uint32_t pattern) {
+    Range* r = range(id);
+    py::gil_scoped_release nogil;
+    check(rt()->fill(r, off, bytes, pattern), "fill");
+  });
+  m.def("dlpack", &make_capsule, py::arg("ptr"), py::arg("shape"), py::arg("code"), py::arg("bits"),
+        py::arg("device_type"), py::arg("device_id"), py::arg("range_id") = 0);
+
+  // ---- introspection
+  m.def("residency_info", [](uint64_t id, uint64_t off) {
+    ResidencyInfo ri;
+    check(rt()->residency_info(range(id), off, &ri), "residency_info");
+    py::dict d;
+    py::list res;
+    for (size_t i = 0; i < ri.resident_on.size(); ++i) {
+      py::dict e = loc_dict(ri.resident_on[i]);
+      e["pages"] = ri.pages[i];
+      e["chunk"] = ri.chunk[i];
+      res.append(e);
+    }
+    d["resident_on"] = res;
+    d["mapped_on"] = ri.mapped_on;
+    d["read_dup"] = ri.read_dup;
+    d["pinned"] = ri.pinned;
+    d["thrashing"] = ri.thrashing;
+    d["read_mostly"] = ri.policy.read_dup;
+    d["preferred"] = ri.policy.has_preferred ? py::object(loc_dict(ri.policy.preferred)) : py::object(py::none());
+    d["accessed_by"] = ri.policy.accessed_by;
+    return d;
+  });
+  m.def("stats", [] {
+    Runtime* r = rt();
+    py::dict d;
+    for (int c = 0; c < (int)Counter::NumCounters; ++c) d[counter_name((Counter)c)] = Tools::get().counter((Counter)c);
+    d["lock_violations"] = lockcheck::violations();
+    py::list arenas;
+    for (int g = 0; g < r->ndev(); ++g) {
+      if (!r->dev(g).hbm) continue;
+      auto s = r->dev(g).hbm->stats();
+      py::dict a;
+      a["name"] = r->dev(g).hbm->name();
+      a["capacity"] = s.capacity;
+      a["allocated"] = s.allocated;
+      a["peak"] = s.peak;
+      a["pinned"] = s.pinned;
+      a["evictions"] = s.evictions;
+      a["free_chunks"] = r->dev(g).hbm->free_chunks();
+      a["largest_free_run"] = r->dev(g).hbm->largest_free_run();
+      uint64_t al, pk, na;
+      torch_alloc_stats(g, &al, &pk, &na);
+      a["torch_allocated"] = al;
+      a["torch_peak"] = pk;
+      arenas.append(a);
+    }
+    for (int t = 1; t <= 2; ++t)
+      for (int n = 0; n < kMaxNodes; ++n) {
+        // only arenas that exist
+        ChunkArena* ha = nullptr;
+        if (t == 2 && !r->cxl_topology().is_cxl_node(n)) continue;
+        // host_arena() creates on demand; only report created ones via arena_for on HOST nodes in use
+        (void)ha;
+      }
+    d["arenas"] = arenas;
+    py::list rings;
+    for (int g = 0; g < r->ndev(); ++g)
+      for (int k = 0; k < (int)RingKind::COUNT; ++k) {
+        Ring* rg = r->ring(g, (RingKind)k);
+        py::dict x;
+        x["dev"] = g;
+        x["kind"] = ring_kind_str((RingKind)k);
+        x["pushed"] = rg->pushed_seq();
+        x["submitted"] = rg->submitted_seq();
+        x["completed"] = rg->completed_seq();
+        x["batches"] = rg->batches();
+        x["error"] = status_str(rg->error());
+        rings.append(x);
+      }
+    d["rings"] = rings;
+    d["global_status"] = status_str(global_status());
+    return d;
+  });
+  m.def("reset_counters", [] { Tools::get().reset_counters(); });
+  m.def("arena_stats", [](int tier, int id) {
+    ChunkArena* a = rt()->arena_for(make_loc(tier, id));
+    if (!a) throw StatusError("no such arena");
+    auto s = a->stats();
+    py::dict d;
+    d["capacity"] = s.capacity;
+    d["allocated"] = s.allocated;
+    d["peak"] = s.peak;
+    d["pinned"] = s.pinned;
+    d["evictions"] = s.evictions;
+    d["allocs"] = s.allocs;
+    d["frees"] = s.frees;
+    d["used_list"] = s.used_list;
+    d["unused_list"] = s.unused_list;
+    d["free_chunks"] = a->free_chunks();
+    d["nchunks"] = a->nchunks();
+    d["base"] = a->base();
+    return d;
+  });
+  m.def("arena_check", [](int tier, int id) {
+    ChunkArena* a = rt()->arena_for(make_loc(tier, id));
+    if (!a) throw StatusError("no such arena");
+    return a->check();
+  });
+  m.def("ring_reap", [](int dev, int kind) {
+    Cqe buf[256];
+    size_t n = rt()->ring(dev, (RingKind)kind)->reap(buf, 256);
+    std::vector<std::tuple<uint64_t, uint64_t, int>> out;
+    for (size_t i = 0; i < n; ++i) out.emplace_back(buf[i].user_data, buf[i].seq, buf[i].status);
+    return out;
+  });
+  m.def("ring_error", [](int dev, int kind) {
+    Ring* r = rt()->ring(dev, (RingKind)kind);
+    return std::make_pair(std::string(status_str(r->error())), r->last_error_desc());
+  });
+  m.def("ring_clear_error", [](int dev, int kind) { rt()->ring(dev, (RingKind)kind)->clear_error_for_test(); });
+  m.def("ring_copy", [](int dev, int kind, uint64_t dst, uint64_t src, uint64_t bytes, bool wait) {
+    // Direct ring access (used by benchmarks and the CE-style tests).
+    Ring* r = rt()->ring(dev, (RingKind)kind);
+    Sqe s;
+    s.op = SqeOp::COPY;
+    s.dst = dst;
+    s.src = src;
+    s.bytes = bytes;
+    uint64_t seq = r->push(std::move(s));
+    FenceRef f = r->submit();
+    if (wait) {
+      py::gil_scoped_release nogil;
+      check(f->wait(), "ring_copy");
+    }
+    return seq;
+  });
+  m.def("ring_memset", [](int dev, int kind, uint64_t dst, uint32_t pattern, uint64_t bytes) {
+    Ring* r = rt()->ring(dev, (RingKind)kind);
+    Sqe s;
+    s.op = SqeOp::MEMSET;
+    s.dst = dst;
+    s.pattern = pattern;
+    s.bytes = bytes;
+    r->push(std::move(s));
+    py::gil_scoped_release nogil;
+    check(r->submit()->wait(), "ring_memset");
+  });
+  m.def("ring_gather", [](int dev, uint64_t base, uint64_t contig, std::vector<uint32_t> idx, uint32_t page_bytes,
+                          bool scatter) {
+    Ring* r = rt()->ring(dev, RingKind::GPU_INTERNAL);
+    Sqe s;
+    s.op = scatter ? SqeOp::SCATTER : SqeOp::GATHER;
+    s.src = scatter ? contig : base;
+    s.dst = scatter ? base : contig;
+    s.idx = std::move(idx);
+    s.page_bytes = page_bytes;
+    r->push(std::move(s));
+    py::gil_scoped_release nogil;
+    check(r->submit()->wait(), "ring_gather");
+  });
+  m.def("ring_stream", [](int dev, int kind) { return (uint64_t)rt()->ring(dev, (RingKind)kind)->stream(); });
+
+  // ---- tools
+  m.def("tools_create_queue", [](uint32_t entries, uint32_t mask, const std::string& shm) {
+    return Tools::get().create_queue(entries, mask, shm);
+  }, py::arg("entries") = 4096, py::arg("mask") = 0xffffffffu, py::arg("shm") = "");
+  m.def("tools_destroy_queue", [](int q) { Tools::get().destroy_queue(q); });
+  m.def("tools_read", [](int q, size_t max) {
+    EventQueue* eq = Tools::get().queue(q);
+    if (!eq) throw StatusError("bad queue");
+    std::vector<ToolsEvent> ev(max);
+    size_t n = eq->pop(ev.data(), max);
+    return py::bytes((const char*)ev.data(), n * sizeof(ToolsEvent));
+  });
+  m.def("tools_dropped", [](int q) {
+    EventQueue* eq = Tools::get().queue(q);
+    if (!eq) throw StatusError("bad queue");
+    std::vector<uint64_t> d;
+    for (int i = 0; i < (int)ToolsEventType::NumTypes; ++i) d.push_back(eq->ctrl()->dropped[i].load());
+    return d;
+  });
+  m.def("counter_names", [] {
+    std::vector<std::string> n;
+    for (int c = 0; c < (int)Counter::NumCounters; ++c) n.push_back(counter_name((Counter)c));
+    return n;
+  });
+
+  // ---- lock checker
+  m.def("lock_violations", [] { return lockcheck::violations(); });
+  m.def("reset_lock_violations", [] { lockcheck::reset_violations(); });
+  m.def("set_lock_check", [](bool on) { lockcheck::set_enabled(on); });
+  m.def("lock_check_self_test", [] {
+    // Deliberately take VA_BLOCK then VA_SPACE (inverted) and report detection.
+    uint64_t before = lockcheck::violations();
+    OrderedMutex blk(LockOrder::VA_BLOCK);
+    OrderedRWLock vs(LockOrder::VA_SPACE);
+    blk.lock();
+    vs.lock_shared();
+    vs.unlock_shared();
+    blk.unlock();
+    // A trylock out of order is legal.
+    blk.lock();
+    OrderedMutex blk2(LockOrder::GLOBAL);
+    bool got = blk2.try_lock();
+    if (got) blk2.unlock();
+    blk.unlock();
+    return lockcheck::violations() - before;
+  });
+
+  // ---- injection
+  m.def("inject", [](const std::string& kind, int64_t v) {
+    Injection& in = rt()->inject();
+    if (kind == "alloc_fail_after") in.alloc_fail_after.store(v);
+    else if (kind == "evict_fail") in.evict_fail.store(v);
+    else if (kind == "copy_drop") in.copy_drop.store(v);
+    else if (kind == "peer_link_down") in.peer_link_down.store((uint64_t)v);
+    else if (kind == "populate_error") in.populate_error.store(v);
+    else if (kind == "host_alloc_error") in.host_alloc_error.store(v);
+    else throw StatusError("unknown injection " + kind);
+  });
+
+  // ---- CXL
+  m.def("cxl_info", [] {
+    const CxlInfo& i = rt()->cxl_topology().info();
+    py::dict d;
+    d["link_up"] = i.link_up;
+    d["memory_expander"] = i.memory_expander;
+    d["num_devices"] = i.num_devices;
+    d["max_links"] = i.max_links;
+    d["link_mask"] = i.link_mask;
+    d["per_link_bw_mbps"] = i.per_link_bw_mbps;
+    d["cxl_version"] = i.cxl_version;
+    d["remote_type"] = i.remote_type;
+    d["emulated"] = i.emulated;
+    d["numa_nodes"] = i.numa_nodes;
+    py::list devs;
+    for (auto& x : i.devices) {
+      py::dict e;
+      e["name"] = x.name;
+      e["numa_node"] = x.numa_node;
+      e["bytes"] = x.bytes;
+      e["version"] = x.version;
+      e["link_up"] = x.link_up;
+      devs.append(e);
+    }
+    d["devices"] = devs;
+    d["registered_buffers"] = rt()->cxl().count();
+    d["pinned_bytes"] = rt()->cxl().pins().pinned();
+    d["pin_budget_bytes"] = rt()->cxl().pins().max_bytes();
+    return d;
+  });
+  m.def("cxl_rediscover", [](int emulate_node, const std::string& root) {
+    rt()->cxl_topology().discover(emulate_node, root);
+  }, py::arg("emulate_node") = -1, py::arg("root") = "/sys");
+  m.def("cxl_set_measured_bw", [](double mbps) { rt()->cxl_topology().mutable_info().per_link_bw_mbps = mbps; });
+  m.def("cxl_register", [](uint64_t base, uint64_t size, int version) {
+    uint64_t h;
+    check(rt()->cxl().register_buffer(base, size, version, &h), "cxl_register");
+    return h;
+  });
+  m.def("cxl_unregister", [](uint64_t h) { check(rt()->cxl().unregister_buffer(h), "cxl_unregister"); });
+  m.def("cxl_buffer", [](uint64_t h) {
+    CxlBuffer b;
+    check(rt()->cxl().lookup(h, &b), "cxl_buffer");
+    py::dict d;
+    d["base"] = b.base;
+    d["size"] = b.size;
+    d["version"] = b.version;
+    d["page_size"] = b.page_size;
+    d["numa_node"] = b.numa_node;
+    d["page_refs"] = b.page_refs;
+    return d;
+  });
+  m.def("cxl_pages", [](uint64_t h, uint64_t off, uint64_t len) {
+    std::vector<CxlExtent> ex;
+    check(rt()->cxl().pages(h, off, len, &ex), "cxl_pages");
+    std::vector<std::pair<uint64_t, uint64_t>> out;
+    for (auto& e : ex) out.emplace_back(e.addr, e.bytes);
+    return out;
+  });
+  m.def("cxl_put_pages", [](uint64_t h) { check(rt()->cxl().put_pages(h), "cxl_put_pages"); });
+  m.def("cxl_dma", [](uint64_t h, uint64_t gpu_ptr, int dev, uint64_t off, uint64_t size, int dir, bool async) {
+    uint64_t tid;
+    Status s;
+    {
+      py::gil_scoped_release nogil;
+      s = rt()->cxl_dma(h, gpu_ptr, dev, off, size, dir, async, &tid);
+    }
+    check(s, "cxl_dma");
+    return tid;
+  });
+  m.def("cxl_dma_wait", [](uint64_t tid) {
+    py::gil_scoped_release nogil;
+    check(rt()->cxl_dma_wait(tid), "cxl_dma_wait");
+  });
+
+  // ---- checkpoint / PM
+  m.def("quiesce", [] {
+    py::gil_scoped_release nogil;
+    check(rt()->quiesce(), "quiesce");
+  });
+  m.def("resume", [] { check(rt()->resume(), "resume"); });
+  m.def("checkpoint_save", [](const std::string& path, bool with_data) {
+    py::gil_scoped_release nogil;
+    check(rt()->checkpoint_save(path, with_data), "checkpoint_save");
+  });
+  m.def("checkpoint_load", [](const std::string& path, bool with_data) {
+    std::vector<uint64_t> ids;
+    Status s;
+    {
+      py::gil_scoped_release nogil;
+      s = rt()->checkpoint_load(path, with_data, &ids);
+    }
+    check(s, "checkpoint_load");
+    return ids;
+  });
+
+  // ---- peers / export
+  m.def("enable_peer", [](int a, int b) { check(rt()->enable_peer(a, b), "enable_peer"); });
+  m.def("link_type", [](int a, int b) { return (int)rt()->be()->link_type(a, b); });
+  m.def("can_access_peer", [](int a, int b) { return rt()->be()->can_access_peer(a, b); });
+  m.def("export_dmabuf", [](uint64_t ptr, uint64_t size) {
+    int fd = -1;
+    uint64_t off = 0;
+    check(rt()->be()->export_dmabuf((void*)ptr, size, &fd, &off), "export_dmabuf");
+    return std::make_pair(fd, off);
+  });
+  m.def("ipc_handle", [](uint64_t ptr) {
+    std::string h;
+    check(rt()->be()->ipc_handle((void*)ptr, &h), "ipc_handle");
+    return py::bytes(h);
+  });
+  m.def("ipc_open", [](py::bytes h) {
+    void* p = nullptr;
+    check(rt()->be()->ipc_open(std::string(h), &p), "ipc_open");
+    return (uint64_t)p;
+  });
+  m.def("ipc_close", [](uint64_t p) { rt()->be()->ipc_close((void*)p); });
+
+  // ---- pinned host helpers (tests / CXL emulation)
+  m.def("alloc_coherent", [](uint64_t bytes) {
+    void* p = nullptr;
+    check(rt()->be()->host_alloc_coherent(bytes, &p), "alloc_coherent");
+    return (uint64_t)p;
+  });
+  m.def("free_coherent", [](uint64_t p) { rt()->be()->host_free_coherent((void*)p); });
+
+  // ---- torch pluggable allocator (in-process use / tests)
+  m.def("torch_alloc", [](uint64_t size, int dev) { return (uint64_t)torch_alloc(size, dev); });
+  m.def("torch_free", [](uint64_t p, int dev) { torch_free((void*)p, dev); });
+  m.def("torch_alloc_stats", [](int dev) {
+    uint64_t a, p, n;
+    torch_alloc_stats(dev, &a, &p, &n);
+    return py::make_tuple(a, p, n);
+  });
+}
