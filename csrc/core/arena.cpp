@@ -143,19 +143,28 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
       return Status::OK;
     }
   if (n == 1) {
-    // Victim order: unused list head, then used LRU head (uvm_pmm_gpu.c:1460-1500).
-    for (int list : {1, 2}) {
-      for (int32_t i = head_[list]; i >= 0; i = chunks_[i].next) {
+    // Victim order: unused list head, then used LRU head (uvm_pmm_gpu.c:1460-1500),
+    // then chunks whose data prefers this tier.
+    // Within a list, the oldest few candidates compete on recency (prefetched
+    // chunks carry a recency bonus and lose to genuinely cold data).
+    for (int list : {1, 2, 3}) {
+      int32_t best = -1;
+      int scanned = 0;
+      for (int32_t i = head_[list]; i >= 0 && scanned < 64; i = chunks_[i].next) {
         ChunkInfo& c = chunks_[i];
-        if (c.state == ChunkState::ALLOCATED && c.pin_count == 0) {
-          lru_remove((uint32_t)i);
-          c.state = ChunkState::EVICTING;
-          r->first = i;
-          r->n = 1;
-          r->victims = {(uint32_t)i};
-          st_.reservations++;
-          return Status::OK;
-        }
+        if (c.state != ChunkState::ALLOCATED || c.pin_count != 0) continue;
+        ++scanned;
+        if (best < 0 || c.last_use < chunks_[best].last_use) best = i;
+      }
+      if (best >= 0) {
+        ChunkInfo& c = chunks_[best];
+        lru_remove((uint32_t)best);
+        c.state = ChunkState::EVICTING;
+        r->first = best;
+        r->n = 1;
+        r->victims = {(uint32_t)best};
+        st_.reservations++;
+        return Status::OK;
       }
     }
     return Status::NO_MEMORY;
@@ -166,6 +175,13 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
   uint64_t best_cost = UINT64_MAX;
   std::deque<uint32_t> dq;  // monotone deque of last_use maxima
   uint32_t start = 0;
+  // Cost of evicting a chunk: 0 if free, its recency otherwise; chunks on the
+  // preferred list cost more than any ordinary chunk.
+  auto cost_of = [&](uint32_t i) -> uint64_t {
+    const ChunkInfo& c = chunks_[i];
+    if (c.state == ChunkState::FREE) return 0;
+    return c.last_use + (c.list == 3 ? (1ull << 62) : 0);
+  };
   for (uint32_t i = 0; i < nchunks_; ++i) {
     ChunkInfo& c = chunks_[i];
     bool ok = c.state == ChunkState::FREE || (c.state == ChunkState::ALLOCATED && c.pin_count == 0);
@@ -174,16 +190,15 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
       dq.clear();
       continue;
     }
-    uint64_t cost = c.state == ChunkState::FREE ? 0 : c.last_use;
-    while (!dq.empty() && (chunks_[dq.back()].state == ChunkState::FREE ? 0 : chunks_[dq.back()].last_use) <= cost)
-      dq.pop_back();
+    uint64_t cost = cost_of(i);
+    while (!dq.empty() && cost_of(dq.back()) <= cost) dq.pop_back();
     dq.push_back(i);
     if (i + 1 - start > n) {
       start = i + 1 - n;
       while (!dq.empty() && dq.front() < start) dq.pop_front();
     }
     if (i + 1 - start == n) {
-      uint64_t wcost = chunks_[dq.front()].state == ChunkState::FREE ? 0 : chunks_[dq.front()].last_use;
+      uint64_t wcost = cost_of(dq.front());
       if (wcost < best_cost) {
         best_cost = wcost;
         best_first = start;
@@ -280,13 +295,15 @@ Block* ChunkArena::owner(uint32_t i) {
   return chunks_[i].owner;
 }
 
-void ChunkArena::touch(uint32_t i, bool has_data) {
+void ChunkArena::touch(uint32_t i, bool has_data, bool preferred, bool prefetched) {
   std::lock_guard<OrderedMutex> g(m_);
   ChunkInfo& c = chunks_[i];
   if (c.state != ChunkState::ALLOCATED) return;
-  c.last_use = ++clock_;
+  c.last_use = ++clock_ + (prefetched ? kPrefetchBoost : 0);
+  // A chunk keeps its preferred status until it loses its data.
+  bool pref = has_data && (preferred || c.list == 3);
   lru_remove(i);
-  lru_push_tail(i, has_data ? 2 : 1);
+  lru_push_tail(i, !has_data ? 1 : (pref ? 3 : 2));
 }
 
 void ChunkArena::pin(uint32_t i) {
@@ -364,7 +381,7 @@ std::string ChunkArena::check() {
     if (chunks_[i].state == ChunkState::ALLOCATED) nalloc++;
   }
   uint64_t n_on_lists = 0;
-  for (int l : {1, 2})
+  for (int l : {1, 2, 3})
     for (int32_t i = head_[l]; i >= 0; i = chunks_[i].next) {
       n_on_lists++;
       if (chunks_[i].state != ChunkState::ALLOCATED) os << "non-allocated chunk " << i << " on LRU; ";

@@ -101,6 +101,14 @@ Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r) {
   return Status::OK;
 }
 
+// LRU bump of a block's chunk at one location: data-less chunks go to the
+// unused list, chunks whose data prefers this location to the protected list.
+void Runtime::touch_residency(Block* b, Residency* r, bool prefetched) {
+  if (!r || r->chunk < 0) return;
+  bool pref = b->policy.has_preferred && b->policy.preferred == r->loc;
+  r->arena->touch((uint32_t)r->chunk, !r->resident.empty(), pref, prefetched);
+}
+
 // Populate: give block b a chunk at location dst (block lock held).
 Status Runtime::populate(Ctx& c, Block* b, Loc dst, int64_t hint, Residency** out) {
   if (Residency* r = b->find(dst)) {
@@ -190,14 +198,14 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     return Status::OK;
   }
   for (auto& f : reuse.fences()) {
-    if (f->ring == ring) continue;
+    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
     Sqe w;
     w.op = SqeOp::WAIT_FENCE;
     w.wait = f;
     ring->push(std::move(w));
   }
   for (auto& f : pend.fences()) {
-    if (f->ring == ring) continue;
+    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
     Sqe w;
     w.op = SqeOp::WAIT_FENCE;
     w.wait = f;
@@ -238,7 +246,7 @@ static Status zero_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* to, 
   Ring* ring = rt->ring(to->loc.id, RingKind::CPU_TO_GPU);
   Tracker reuse = to->arena->take_reuse_fence((uint32_t)to->chunk);
   for (auto& f : reuse.fences()) {
-    if (f->ring == ring) continue;
+    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
     Sqe w;
     w.op = SqeOp::WAIT_FENCE;
     w.wait = f;
@@ -352,12 +360,7 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
     tools_event(ToolsEventType::ReadDuplicate, cause, Loc::host(0), dst, dst.is_gpu() ? dst.id : kCpuProc,
                 b->range->addr() + b->block_offset(), (uint64_t)pages.count() << kPageShift, b->range->id);
   }
-  Residency* t = b->find(dst);
-  if (t && t->chunk >= 0) {
-    bool pref_here = b->policy.has_preferred && b->policy.preferred == dst;
-    (void)pref_here;
-    t->arena->touch((uint32_t)t->chunk, true);
-  }
+  if (Residency* t = b->find(dst)) touch_residency(b, t, cause == Cause::Prefetch);
   b->last_access_ns = now_ns();
   c.cpu_refresh.push_back(b);
   Tools::get().bus().notify(PerfEventData{PerfEvent::MIGRATION, b->range->id, b->index, Loc{}, dst, 0,
@@ -496,6 +499,13 @@ Status Runtime::prefetch(Range* r, uint64_t off, uint64_t len, Loc dst, Tracker*
   if (!arena_for(dst)) return Status::INVALID_ARGUMENT;
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   if (r->group && !r->group->migratable) return Status::BUSY;
+  if (dst.is_gpu()) {
+    // GPU destinations are laid out as one contiguous extent so a later
+    // acquire() finds the span in place (no relocation).
+    for (uint64_t bi = off >> kBlockShift; bi <= (off + len - 1) >> kBlockShift; ++bi)
+      if (r->block(bi)->user_pins) return Status::BUSY;
+    return gpu_extent_resident(r, off, len, dst.id, {}, nullptr, out, cause);
+  }
   uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
   Ctx c;
   c.cause = cause;
@@ -606,6 +616,159 @@ Status Runtime::evict_range(Range* r, Loc from) {
       Tools::get().inc(Counter::Evictions);
     }
     finish_ctx(c, nullptr);
+  }
+  return Status::OK;
+}
+
+// ------------------------------------------------------------------ GPU extents
+// Make [off, off+len) of r resident on `gpu` in n CONSECUTIVE HBM chunks, so the
+// span is one contiguous device buffer (what a kernel / torch view needs).
+// Blocks already laid out in place only fetch missing pages; otherwise a fresh
+// extent is allocated (evicting cold chunks through the reservation protocol)
+// and resident pages are relocated D2D. With a lease, chunks are pinned.
+Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
+                                    Lease* L, Tracker* out, Cause cause) {
+  Loc dst = Loc::gpu(gpu);
+  ChunkArena* ga = arena_for(dst);
+  if (!ga) return Status::INVALID_ARGUMENT;
+  uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
+  uint32_t n = (uint32_t)(b1 - b0 + 1);
+  auto pages_of = [&](uint64_t bi) {
+    uint64_t lo = std::max(off, bi << kBlockShift) - (bi << kBlockShift);
+    uint64_t hi = std::min(off + len, (bi + 1) << kBlockShift) - (bi << kBlockShift);
+    uint32_t p0 = (uint32_t)(lo >> kPageShift), p1 = (uint32_t)((hi + kPageSize - 1) >> kPageShift);
+    return PageMask::range(p0, p1 - p0);
+  };
+  Ctx c;
+  c.cause = cause;
+  Status st = Status::OK;
+  int64_t first = -1;
+  bool in_place = true;
+  {
+    int64_t c0 = -1;
+    for (uint32_t k = 0; k < n && in_place; ++k) {
+      Block* b = r->block(b0 + k);
+      std::lock_guard<OrderedMutex> g(b->lock);
+      Residency* x = b->find(dst);
+      if (!x) in_place = false;
+      else if (k == 0) c0 = x->chunk;
+      else if (x->chunk != c0 + k) in_place = false;
+    }
+    if (in_place) first = c0;
+  }
+  if (!in_place) {
+    uint32_t f = 0;
+    st = alloc_chunks(ga, n, -1, &f);
+    if (st == Status::OK) {
+      first = f;
+    } else if (st == Status::NO_MEMORY) {
+      Reservation rv;
+      st = ensure_capacity(ga, n, &rv);
+      first = rv.first;
+    }
+    if (st != Status::OK) return st;
+  }
+  std::vector<Block*> done;
+  for (uint32_t k = 0; k < n && st == Status::OK; ++k) {
+    Block* b = r->block(b0 + k);
+    uint32_t target = (uint32_t)(first + k);
+    for (int attempt = 0; attempt < 8; ++attempt) {
+      {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        Residency* x = b->find(dst);
+        if (x && x->chunk != (int64_t)target) {
+          // Relocate: copy the resident pages into the new extent (D2D).
+          ga->set_owner(target, b);
+          Residency tmp;
+          tmp.slot = x->slot;
+          tmp.loc = dst;
+          tmp.arena = ga;
+          tmp.chunk = target;
+          st = copy_pages(this, c, b, x, &tmp, x->resident);
+          if (st == Status::OK) {
+            bool queued = false;
+            for (auto& u : c.chunk_uses)
+              if (u.arena == x->arena && u.chunk == (uint32_t)x->chunk && !u.free_after) {
+                u.free_after = true;
+                x->arena->set_owner((uint32_t)x->chunk, nullptr);
+                x->arena->pin((uint32_t)x->chunk);
+                queued = true;
+                break;
+              }
+            if (!queued) x->arena->free((uint32_t)x->chunk, 1);
+            x->chunk = target;
+            x->arena = ga;
+          }
+        } else if (!x) {
+          ga->set_owner(target, b);
+          Residency& nr = b->get_or_add(dst);
+          nr.arena = ga;
+          nr.chunk = target;
+          nr.resident.zero();
+        }
+        if (st == Status::OK) {
+          PageMask want = pages_of(b0 + k);
+          // Prefetch hint: grow the request inside the block (51% rule).
+          if (config().perf_prefetch_enable) {
+            Residency* y = b->find(dst);
+            PageMask hint = prefetch_hint(y->resident, want, b->npages, (uint32_t)config().perf_prefetch_threshold);
+            want |= (hint & b->resident_anywhere());
+          }
+          st = make_resident(c, b, want, dst, read_dup.empty() ? b->policy.read_dup : read_dup[k], cause);
+        }
+        if (st == Status::OK) {
+          Residency* y = b->find(dst);
+          touch_residency(b, y, cause == Cause::Prefetch && !L);
+          if (L) {
+            b->lease_pins++;
+            y->arena->pin((uint32_t)y->chunk);
+            L->pinned_chunks.emplace_back(y->arena, (uint32_t)y->chunk);
+            L->blocks.push_back(b);
+          }
+          done.push_back(b);
+        }
+      }
+      if (st != Status::MORE_PROCESSING_REQUIRED) break;
+      finish_ctx(c, out);
+      Reservation rr;
+      Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+      if (es != Status::OK) {
+        st = es;
+        break;
+      }
+      c.need_arena->free((uint32_t)rr.first, rr.n);
+      c.need_arena = nullptr;
+    }
+  }
+  // Chunks of the extent that were never handed to a block (error path) go back.
+  if (st != Status::OK && !in_place) {
+    for (uint32_t k = 0; k < n; ++k) {
+      Block* b = r->block(b0 + k);
+      bool used = false;
+      for (Block* d : done)
+        if (d == b) used = true;
+      if (!used && ga->owner((uint32_t)(first + k)) == nullptr) ga->free((uint32_t)(first + k), 1);
+    }
+  }
+  finish_ctx(c, out);
+  if (st != Status::OK) {
+    if (L) {
+      for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
+      for (Block* b : L->blocks) {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        b->lease_pins--;
+      }
+      L->pinned_chunks.clear();
+      L->blocks.clear();
+    }
+    return st;
+  }
+  if (L) {
+    for (Block* b : L->blocks) {
+      std::lock_guard<OrderedMutex> g(b->lock);
+      L->ready.merge(b->tracker);
+    }
+    L->dptr = ga->chunk_addr((uint32_t)first) + (off - (b0 << kBlockShift));
   }
   return Status::OK;
 }
@@ -765,127 +928,10 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
       }
     }
     if (proc != kCpuProc && !all_remote) {
-      // Local GPU lease: the blocks must occupy n consecutive HBM chunks.
-      ChunkArena* ga = arena_for(dst);
-      if (!ga) return Status::INVALID_ARGUMENT;
-      int64_t first = -1;
-      bool in_place = true;
-      {
-        // Are the blocks already laid out contiguously (or extendable in place)?
-        int64_t c0 = -1;
-        for (uint32_t k = 0; k < n && in_place; ++k) {
-          Block* b = r->block(b0 + k);
-          std::lock_guard<OrderedMutex> g(b->lock);
-          Residency* x = b->find(dst);
-          if (!x) {
-            in_place = false;
-            break;
-          }
-          if (k == 0) c0 = x->chunk;
-          else if (x->chunk != c0 + k) in_place = false;
-        }
-        if (in_place) first = c0;
-      }
-      Reservation rv;
-      if (!in_place) {
-        // Fresh extent for all n blocks: free run, else evict LRU victims.
-        uint32_t f = 0;
-        st = alloc_chunks(ga, n, -1, &f);
-        if (st == Status::OK) {
-          rv.first = f;
-          rv.n = n;
-        } else if (st == Status::NO_MEMORY) {
-          st = ensure_capacity(ga, n, &rv);
-        }
-        if (st != Status::OK) return st;
-        first = rv.first;
-      }
-      for (uint32_t k = 0; k < n && st == Status::OK; ++k) {
-        Block* b = r->block(b0 + k);
-        uint32_t target = (uint32_t)(first + k);
-        for (int attempt = 0; attempt < 8; ++attempt) {
-          {
-            std::lock_guard<OrderedMutex> g(b->lock);
-            Residency* x = b->find(dst);
-            if (x && x->chunk != (int64_t)target) {
-              // Relocate: copy the resident pages into the new extent (D2D).
-              ga->set_owner(target, b);
-              Residency tmp;
-              tmp.slot = x->slot;
-              tmp.loc = dst;
-              tmp.arena = ga;
-              tmp.chunk = target;
-              st = copy_pages(this, c, b, x, &tmp, x->resident);
-              if (st == Status::OK) {
-                // mark the old chunk for freeing after the copy
-                bool queued = false;
-                for (auto& u : c.chunk_uses)
-                  if (u.arena == x->arena && u.chunk == (uint32_t)x->chunk && !u.free_after) {
-                    u.free_after = true;
-                    x->arena->set_owner((uint32_t)x->chunk, nullptr);
-                    x->arena->pin((uint32_t)x->chunk);
-                    queued = true;
-                    break;
-                  }
-                if (!queued) x->arena->free((uint32_t)x->chunk, 1);
-                x->chunk = target;
-                x->arena = ga;
-              }
-            } else if (!x) {
-              ga->set_owner(target, b);
-              Residency& nr = b->get_or_add(dst);
-              nr.arena = ga;
-              nr.chunk = target;
-              nr.resident.zero();
-            } else {
-              ga->set_owner(target, b);
-            }
-            if (st == Status::OK) {
-              PageMask want = pages_of(b0 + k);
-              // Prefetch hint: grow the request inside the block (51% rule).
-              if (config().perf_prefetch_enable && proc != kCpuProc) {
-                Residency* y = b->find(dst);
-                PageMask hint = prefetch_hint(y->resident, want, b->npages, (uint32_t)config().perf_prefetch_threshold);
-                PageMask populated = b->resident_anywhere();
-                want |= (hint & populated);
-              }
-              st = make_resident(c, b, want, dst, dec[k].read_dup, c.cause);
-            }
-            if (st == Status::OK) {
-              Residency* y = b->find(dst);
-              b->lease_pins++;
-              y->arena->pin((uint32_t)y->chunk);
-              L->pinned_chunks.emplace_back(y->arena, (uint32_t)y->chunk);
-              L->blocks.push_back(b);
-              if (b->policy.has_preferred && b->policy.preferred == dst) y->arena->touch((uint32_t)y->chunk, true);
-            }
-          }
-          if (st != Status::MORE_PROCESSING_REQUIRED) break;
-          finish_ctx(c, nullptr);
-          Reservation rr;
-          Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
-          if (es != Status::OK) {
-            st = es;
-            break;
-          }
-          c.need_arena->free((uint32_t)rr.first, rr.n);
-          c.need_arena = nullptr;
-        }
-      }
-      finish_ctx(c, &L->ready);
-      if (st != Status::OK) {
-        for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
-        for (Block* b : L->blocks) {
-          std::lock_guard<OrderedMutex> g(b->lock);
-          b->lease_pins--;
-        }
-        return st;
-      }
-      for (Block* b : L->blocks) {
-        std::lock_guard<OrderedMutex> g(b->lock);
-        L->ready.merge(b->tracker);
-      }
-      L->dptr = ga->chunk_addr((uint32_t)first) + (off - (b0 << kBlockShift));
+      std::vector<bool> dup(n);
+      for (uint32_t k = 0; k < n; ++k) dup[k] = dec[k].read_dup;
+      st = gpu_extent_resident(r, off, len, proc, dup, L.get(), &L->ready, Cause::User);
+      if (st != Status::OK) return st;
     }
   }
   r->views.fetch_add(1);

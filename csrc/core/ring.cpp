@@ -98,7 +98,13 @@ FenceRef Ring::submit_locked() {
             st = Status::INJECTED_ERROR;
             break;
           }
-          batch.push_back(CopyDesc{s.dst, s.src, s.bytes});
+          // Coalesce physically adjacent copies (consecutive 2 MB blocks of one
+          // extent) into a single descriptor.
+          if (!batch.empty() && batch.back().dst + batch.back().bytes == s.dst &&
+              batch.back().src + batch.back().bytes == s.src)
+            batch.back().bytes += s.bytes;
+          else
+            batch.push_back(CopyDesc{s.dst, s.src, s.bytes});
           break;
         case SqeOp::GATHER:
         case SqeOp::SCATTER: {

@@ -499,6 +499,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
           for (auto& l : empty) drop_copy(c, b, l);
           to = b->find(stage);
           to->resident |= pages;
+          touch_residency(b, to);
           uint64_t dst_addr = to->arena->chunk_addr((uint32_t)to->chunk) + lo;
           const char* s = (const char*)src + (pos - off);
           if (src_dev < 0) {

@@ -157,6 +157,11 @@ void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t
 }  // namespace ogkm
 
 extern "C" {
-void* ogkm_torch_alloc(size_t size, int device, void* /*stream*/) { return ogkm::torch_alloc(size, device); }
-void ogkm_torch_free(void* ptr, size_t /*size*/, int device, void* /*stream*/) { ogkm::torch_free(ptr, device); }
+__attribute__((visibility("default"))) void* ogkm_torch_alloc(size_t size, int device, void* /*stream*/) {
+  return ogkm::torch_alloc(size, device);
+}
+__attribute__((visibility("default"))) void ogkm_torch_free(void* ptr, size_t /*size*/, int device,
+                                                            void* /*stream*/) {
+  ogkm::torch_free(ptr, device);
+}
 }

@@ -38,7 +38,7 @@ enum class ChunkState : uint8_t { FREE = 0, RESERVED = 1, ALLOCATED = 2, EVICTIN
 
 struct ChunkInfo {
   ChunkState state = ChunkState::FREE;
-  uint8_t list = 0;      // 0 none, 1 unused, 2 used
+  uint8_t list = 0;      // 0 none, 1 unused, 2 used, 3 used + preferred here
   bool zeroed = false;
   uint32_t pin_count = 0;
   Block* owner = nullptr;
@@ -77,7 +77,13 @@ class ChunkArena {
   // Evictor calls this once the owner has let go of an EVICTING chunk.
   void evicted(uint32_t i);
 
-  void touch(uint32_t i, bool has_data);            // LRU bump
+  // LRU bump. `preferred`: the owner's preferred location is this tier - such
+  // chunks sit on their own list and are evicted only after every other
+  // allocated chunk (protects the planned resident set from streaming traffic).
+  // `prefetched`: the data was brought in ahead of its use - it ranks as newer than
+  // every chunk that has actually been used until its first access (otherwise a
+  // layer-ahead prefetch would be the LRU victim of the next prefetch).
+  void touch(uint32_t i, bool has_data, bool preferred = false, bool prefetched = false);
   void pin(uint32_t i);
   void unpin(uint32_t i);
   bool pinned(uint32_t i);
@@ -112,7 +118,7 @@ class ChunkArena {
   OrderedMutex m_;
   std::vector<ChunkInfo> chunks_;
   std::map<uint32_t, uint32_t> free_runs_;  // start -> len
-  int32_t head_[3] = {-1, -1, -1}, tail_[3] = {-1, -1, -1};
+  int32_t head_[4] = {-1, -1, -1, -1}, tail_[4] = {-1, -1, -1, -1};
   uint64_t clock_ = 0;
   Stats st_;
 };
@@ -166,5 +172,6 @@ class HostArena : public ChunkArena {
 };
 
 constexpr uint64_t kHostSegment = 1ull << 30;
+constexpr uint64_t kPrefetchBoost = 1ull << 40;  // recency bonus of not-yet-used prefetched chunks
 
 }  // namespace ogkm

@@ -84,6 +84,10 @@ struct Config {
   bool set(const std::string& name, int64_t v);
   bool get(const std::string& name, int64_t* v) const;
   void load_env();  // RT_<UPPER_NAME>
+  void reset() {
+    *this = Config();
+    load_env();
+  }
   std::vector<std::string> names() const;
   std::string doc(const std::string& name) const;
 };

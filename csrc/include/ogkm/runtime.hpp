@@ -220,6 +220,9 @@ class Runtime {
   void stable_map_block(Block* b);
   void finish_ctx(Ctx& c, Tracker* out);
   void drop_copy(Ctx& c, Block* b, const Loc& l);  // release a residency (block lock held)
+  void touch_residency(Block* b, Residency* r, bool prefetched = false);  // LRU bump (preferred / prefetch aware)
+  Status gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
+                             Lease* L, Tracker* out, Cause cause);
   Status queue_copy(Ctx& c, Block* b, Residency* from, Residency* to, const PageMask& pages);
   void update_device_table(Block* b);
 
@@ -256,10 +259,18 @@ struct Runtime::Ctx {
   std::vector<Block*> cpu_refresh;    // CPU views to refresh after submission
   ChunkArena* need_arena = nullptr;   // set on MORE_PROCESSING_REQUIRED
   uint32_t need_n = 0;
+  std::vector<std::pair<Ring*, Fence*>> waited;  // GPU-side waits already queued
   void use_ring(Ring* r) {
     for (Ring* x : rings)
       if (x == r) return;
     rings.push_back(r);
+  }
+  // True the first time (ring, fence) is seen: one WAIT_FENCE per pair per operation.
+  bool first_wait(Ring* r, Fence* f) {
+    for (auto& w : waited)
+      if (w.first == r && w.second == f) return false;
+    waited.emplace_back(r, f);
+    return true;
   }
 };
 

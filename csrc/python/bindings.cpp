@@ -98,9 +98,10 @@ py::object make_capsule(uint64_t ptr, std::vector<int64_t> shape, int code, int 
   auto* t = new DLManagedTensor();
   auto* c = new DLCtx();
   c->shape = std::move(shape);
-  c->range_id = range_id;
-  if (range_id)
-    if (Range* rg = rt()->range_by_id(range_id)) rg->views.fetch_add(1);
+  // Tensor views do not pin the range (only leases do): a view is valid while
+  // its lease / buffer is, like any pointer into a freed allocation.
+  c->range_id = 0;
+  (void)range_id;
   t->dl_tensor.data = (void*)ptr;
   t->dl_tensor.device = DLDevice{device_type, device_id};
   t->dl_tensor.ndim = (int32_t)c->shape.size();
@@ -173,6 +174,11 @@ PYBIND11_MODULE(_ogkm, m) {
     return v;
   });
   m.def("config_names", [] { return config().names(); });
+  m.def("config_reset", [] {
+    std::lock_guard<std::mutex> g(config_mutex());
+    config().reset();
+    lockcheck::set_enabled(config().lock_check != 0);
+  });
   m.def("config_doc", [](const std::string& n) { return config().doc(n); });
   m.def("set_log_level", [](int l) { set_log_level((LogLevel)l); });
 

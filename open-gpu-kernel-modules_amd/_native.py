@@ -17,6 +17,11 @@ SO_PATH = _PKG_DIR / ("_ogkm" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
 def _load():
+    # PyTorch-ROCm bundles its own libamdhip64 / libhsa-runtime64 (same sonames as
+    # /opt/rocm). Import torch first so the extension binds to the copy torch
+    # already loaded: two HIP runtimes in one process cannot share the GPU.
+    import torch  # noqa: F401
+
     if not SO_PATH.exists():
         if os.environ.get("OGKM_AUTOBUILD", "1") == "1":
             import subprocess

@@ -17,6 +17,7 @@ pool (config ``cxl_emulate_node``) - results are then labelled ``emulated``.
 from __future__ import annotations
 
 import ctypes
+import ctypes.util
 import mmap
 import time
 from typing import Optional
@@ -90,8 +91,6 @@ def _mbind(addr: int, size: int, node: int) -> None:
     try:
         mbind = libc.mbind
     except AttributeError:
-        import ctypes.util
-
         mbind = ctypes.CDLL(ctypes.util.find_library("numa")).mbind
     mask = ctypes.c_ulong(1 << node)
     MPOL_BIND = 2

@@ -1,1 +1,3 @@
-"""parallel"""
+"""Parallelism: RCCL process groups (comm), tensor parallel (tp), peer-shard
+weights over xGMI (shards), and GPU peer topology (topology)."""
+from . import comm, tp  # noqa: F401
