@@ -23,8 +23,16 @@ namespace ogkm {
 
 namespace {
 
+// Events may be destroyed while a stream still holds a queued record/wait on
+// them (like hipEventDestroy on a pending event): they are reference counted
+// by the owner plus every queued operation.
 struct FakeEvent {
   std::atomic<bool> done{true};
+  std::atomic<int> refs{1};
+  void ref() { refs.fetch_add(1, std::memory_order_relaxed); }
+  void unref() {
+    if (refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete this;
+  }
 };
 
 class FakeStream {
@@ -171,7 +179,7 @@ class FakeBackend : public Backend {
     return Status::OK;
   }
   void* event_create(int) override { return new FakeEvent(); }
-  void event_destroy(void* e) override { delete (FakeEvent*)e; }
+  void event_destroy(void* e) override { ((FakeEvent*)e)->unref(); }
   Status event_record(void* e, void* s) override {
     auto* ev = (FakeEvent*)e;
     if (!s) {
@@ -179,7 +187,11 @@ class FakeBackend : public Backend {
       return Status::OK;
     }
     ev->done.store(false);
-    ((FakeStream*)s)->enqueue([ev] { ev->done.store(true, std::memory_order_release); });
+    ev->ref();
+    ((FakeStream*)s)->enqueue([ev] {
+      ev->done.store(true, std::memory_order_release);
+      ev->unref();
+    });
     return Status::OK;
   }
   bool event_query(void* e) override { return ((FakeEvent*)e)->done.load(std::memory_order_acquire); }
@@ -191,8 +203,10 @@ class FakeBackend : public Backend {
   Status stream_wait_event(void* s, void* e) override {
     auto* ev = (FakeEvent*)e;
     if (!s) return event_sync(e);
+    ev->ref();
     ((FakeStream*)s)->enqueue([ev] {
       while (!ev->done.load(std::memory_order_acquire)) std::this_thread::yield();
+      ev->unref();
     });
     return Status::OK;
   }

@@ -348,7 +348,11 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
     for (auto& r : b->res) {
       if (&r == to) continue;
       if (r.resident.intersects(pages)) {
-        if (!r.loc.is_gpu() || !dst.is_gpu()) Tools::get().inc(Counter::Revocations, 0);
+        Tools::get().inc(Counter::Revocations);
+        if (b->policy.read_dup)
+          tools_event(ToolsEventType::ReadDuplicateInvalidate, Cause::Coherence, r.loc, dst, kCpuProc,
+                      b->range->addr() + b->block_offset(), (uint64_t)(r.resident & pages).count() << kPageShift,
+                      b->range->id);
         r.resident = r.resident.andnot(pages);
         if (r.resident.empty()) empty_locs.push_back(r.loc);
       }
@@ -998,6 +1002,8 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
     if (a.range_id != b.range_id) return a.range_id < b.range_id;
     if (a.block != b.block) return a.block < b.block;
     if (a.proc != b.proc) return a.proc < b.proc;
+    if (a.first_page != b.first_page) return a.first_page < b.first_page;
+    if (a.npages != b.npages) return a.npages < b.npages;
     return (int)a.access > (int)b.access;  // writes first: the highest access wins
   });
   uint64_t coalesced = 0;

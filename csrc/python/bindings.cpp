@@ -532,6 +532,22 @@ PYBIND11_MODULE(_ogkm, m) {
     return n;
   });
 
+  // ---- heuristics test hooks (UVM_TEST_SET_PAGE_PREFETCH_POLICY-style introspection)
+  m.def("prefetch_hint", [](std::vector<uint32_t> resident, std::vector<uint32_t> faulted, uint32_t npages,
+                            uint32_t threshold) {
+    PageMask r, f;
+    for (auto p : resident) r.set(p);
+    for (auto p : faulted) f.set(p);
+    PageMask h = prefetch_hint(r, f, npages, threshold);
+    std::vector<uint32_t> out;
+    for (uint32_t p = h.next_set(0); p < kPagesPerBlock; p = h.next_set(p + 1)) out.push_back(p);
+    return out;
+  });
+  m.def("fault_buffer_info", [](int dev) {
+    DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
+    return py::make_tuple((uint64_t)fb.put, (uint64_t)fb.recs, fb.entries, fb.overflows);
+  });
+
   // ---- lock checker
   m.def("lock_violations", [] { return lockcheck::violations(); });
   m.def("reset_lock_violations", [] { lockcheck::reset_violations(); });

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace (rocpd SQLite output) into markdown.
+
+    python tools/prof_summary.py gpurun_out/prof8b/k_results.db [--top 25] > profiles/x.md
+"""
+from __future__ import annotations
+
+import argparse
+import sqlite3
+
+
+def summarize(db: str, top: int = 25, title: str = "") -> str:
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, count(*), sum(duration), avg(duration), min(start), max(end) from kernels "
+                     "group by name order by sum(duration) desc").fetchall()
+    total = sum(r[2] for r in rows) or 1
+    span = (max(r[5] for r in rows) - min(r[4] for r in rows)) if rows else 0
+    out = [f"## {title or db}", "", f"kernel time total {total/1e6:.1f} ms over a {span/1e6:.1f} ms trace window", "",
+           "| kernel | calls | total ms | % | avg us |", "|---|---:|---:|---:|---:|"]
+    for name, n, tot, avg, _, _ in rows[:top]:
+        short = name.split("(")[0][:90]
+        out.append(f"| `{short}` | {n} | {tot/1e6:.2f} | {100*tot/total:.1f} | {avg/1e3:.1f} |")
+    return "\n".join(out) + "\n"
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--title", default="")
+    a = ap.parse_args()
+    print(summarize(a.db, a.top, a.title))
+
+
+if __name__ == "__main__":
+    main()
