@@ -80,6 +80,10 @@ Status Runtime::alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* 
 // Reserve n contiguous chunks, evicting victims (no block lock may be held).
 Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r) {
   if (a->loc().is_gpu() && !config().global_oversubscription) return Status::NO_MEMORY;
+  if (a->loc().is_gpu() && inject_.alloc_fail_after.load() == 0) {
+    Tools::get().inc(Counter::InjectedErrors);
+    return Status::NO_MEMORY;  // injected allocation failure: eviction cannot help either
+  }
   Status st = a->reserve(n, r);
   if (st != Status::OK) return st;
   for (uint32_t v : r->victims) {
@@ -311,6 +315,7 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
   Status st = populate(c, b, dst, hint, &to);
   if (st != Status::OK) return st;
   PageMask missing = pages.andnot(to->resident);
+  bool copied = false;
   if (!missing.empty()) {
     // Source = closest resident copy per page: same tier first, then HBM peers,
     // then host, then CXL.
@@ -328,6 +333,7 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
       if (from_here.empty()) continue;
       st = copy_pages(this, c, b, s, to, from_here);
       if (st != Status::OK) return st;
+      copied = true;
       left = left.andnot(from_here);
       if (left.empty()) break;
     }
@@ -343,6 +349,12 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
     for (auto& r : b->res)
       if (!(r.loc == dst) && r.resident.intersects(pages)) moved = true;
     if (moved && cause != Cause::Eviction) thrash_on_migration(b, dst.slot(), now_ns());
+    if (copied) {
+      // Sources stay valid until the replacing copies are submitted (finish_ctx).
+      c.invals.push_back(Ctx::Inval{b, dst, pages});
+      goto done;
+    }
+    {
     // Migration: invalidate every other copy of these pages (revocation).
     std::vector<Loc> empty_locs;
     for (auto& r : b->res) {
@@ -359,11 +371,13 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
     }
     // `to` may move when residencies are dropped: remember by location.
     for (auto& l : empty_locs) drop_residency(c, b, l);
+    }
   } else {
     Tools::get().inc(Counter::ReadDuplications);
     tools_event(ToolsEventType::ReadDuplicate, cause, Loc::host(0), dst, dst.is_gpu() ? dst.id : kCpuProc,
                 b->range->addr() + b->block_offset(), (uint64_t)pages.count() << kPageShift, b->range->id);
   }
+done:
   if (Residency* t = b->find(dst)) touch_residency(b, t, cause == Cause::Prefetch);
   b->last_access_ns = now_ns();
   c.cpu_refresh.push_back(b);
@@ -372,10 +386,31 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
   return Status::OK;
 }
 
-// Submit every ring used by the context and publish fences to blocks / chunks.
-void Runtime::finish_ctx(Ctx& c, Tracker* out) {
+// Free the chunk behind residency `r` once every pending writer/reader of the
+// block has finished (block lock held), and forget the residency.
+static void release_residency_now(Block* b, const Loc& l) {
+  Residency* r = b->find(l);
+  if (!r) return;
+  if (r->chunk >= 0) {
+    for (auto& f : b->tracker.fences()) r->arena->add_reuse_fence((uint32_t)r->chunk, f);
+    r->arena->free((uint32_t)r->chunk, 1);
+  }
+  b->drop(l);
+}
+
+// Submit every ring used by the context, publish fences to blocks / chunks and
+// apply (or, on a failed submission, reverse) the deferred invalidations.
+Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
   std::vector<std::pair<Ring*, FenceRef>> fences;
-  for (Ring* r : c.rings) fences.emplace_back(r, r->submit());
+  std::vector<Ring*> failed;
+  Status result = Status::OK;
+  for (Ring* r : c.rings) {
+    fences.emplace_back(r, r->submit());
+    if (r->error() != Status::OK) {
+      failed.push_back(r);
+      if (result == Status::OK) result = r->error();
+    }
+  }
   auto fence_of = [&](Ring* r) -> FenceRef {
     for (auto& f : fences)
       if (f.first == r) return f.second;
@@ -395,6 +430,23 @@ void Runtime::finish_ctx(Ctx& c, Tracker* out) {
       u.arena->free(u.chunk, 1);
     }
   }
+  for (auto& iv : c.invals) {
+    bool bad = false;
+    for (auto& t : c.touched)
+      if (t.block == iv.b && std::find(failed.begin(), failed.end(), t.ring) != failed.end()) bad = true;
+    std::lock_guard<OrderedMutex> g(iv.b->lock);
+    std::vector<Loc> empty;
+    for (auto& r : iv.b->res) {
+      bool is_dst = r.loc == iv.dst;
+      if (bad ? !is_dst : is_dst) continue;  // failed copy: the destination is what becomes invalid
+      if (!r.resident.intersects(iv.pages)) continue;
+      if (!bad) Tools::get().inc(Counter::Revocations);
+      r.resident = r.resident.andnot(iv.pages);
+      if (r.resident.empty()) empty.push_back(r.loc);
+    }
+    for (auto& l : empty) release_residency_now(iv.b, l);
+    c.cpu_refresh.push_back(iv.b);
+  }
   if (out)
     for (auto& f : fences) out->add(f.second);
   for (Block* b : c.cpu_refresh) {
@@ -404,6 +456,7 @@ void Runtime::finish_ctx(Ctx& c, Tracker* out) {
     if (b->range->dev_va) stable_map_block(b);
   }
   c = Ctx{};
+  return result;
 }
 
 // ------------------------------------------------------------------ eviction
@@ -543,8 +596,8 @@ Status Runtime::prefetch(Range* r, uint64_t off, uint64_t len, Loc dst, Tracker*
       c.need_arena = nullptr;
     }
   }
-  finish_ctx(c, out);
-  return st;
+  Status fs = finish_ctx(c, out);
+  return st != Status::OK ? st : fs;
 }
 
 Status Runtime::migrate_sync(Range* r, uint64_t off, uint64_t len, Loc dst) {
@@ -754,7 +807,8 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
       if (!used && ga->owner((uint32_t)(first + k)) == nullptr) ga->free((uint32_t)(first + k), 1);
     }
   }
-  finish_ctx(c, out);
+  Status fs = finish_ctx(c, out);
+  if (st == Status::OK) st = fs;
   if (st != Status::OK) {
     if (L) {
       for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
@@ -838,7 +892,8 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
         }
         if (st == Status::OK) L->blocks.push_back(b);
       }
-      finish_ctx(c, &L->ready);
+      Status fs = finish_ctx(c, &L->ready);
+      if (st == Status::OK) st = fs;
       L->ready.wait();
       for (Block* b : L->blocks) {
         std::lock_guard<OrderedMutex> g(b->lock);
@@ -902,7 +957,8 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
           c.need_arena->free((uint32_t)rr.first, rr.n);
         }
       }
-      finish_ctx(c, &L->ready);
+      Status fs = finish_ctx(c, &L->ready);
+      if (st == Status::OK) st = fs;
       if (st == Status::OK && !contiguous) {
         // Fall back to a local copy.
         for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
@@ -1088,7 +1144,8 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
     if (throttled > (uint32_t)config().perf_fault_max_throttle_per_service) break;
     i = j;
   }
-  finish_ctx(c, out);
+  Status fs = finish_ctx(c, out);
+  if (result == Status::OK) result = fs;
   // Replay: with BATCH_FLUSH the waiting processors resume once every copy of the
   // batch has landed (the caller waits on `out`).
   tools_event(ToolsEventType::GpuFaultReplay, Cause::User, Loc{}, Loc{}, 0, 0, faults.size(), 0);

@@ -547,8 +547,9 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
         continue;
       }
       Tracker t;
-      finish_ctx(c, &t);
+      Status fs = finish_ctx(c, &t);
       Status w = t.wait();
+      if (st == Status::OK) st = fs;
       if (st == Status::OK) st = w;
       break;
     }
@@ -823,6 +824,7 @@ Status Runtime::checkpoint_save(const std::string& path, bool with_data) {
     uint8_t gm = r->group ? (uint8_t)r->group->migratable : 1;
     wr(o, gid);
     wr(o, gm);
+    {
     std::shared_lock<OrderedRWLock> vg(vs_.lock);
     for (auto& bp : r->blocks) {
       Block* b = bp.get();
@@ -847,6 +849,7 @@ Status Runtime::checkpoint_save(const std::string& path, bool with_data) {
         o.write((const char*)x.resident.w, sizeof x.resident.w);
       }
     }
+    }  // block table written; read() below takes the VA-space lock itself
     if (with_data) {
       for (auto& bp : r->blocks) {
         uint64_t bytes = (uint64_t)bp->npages << kPageShift;

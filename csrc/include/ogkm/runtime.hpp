@@ -218,7 +218,7 @@ class Runtime {
   Loc demotion_target(const Loc& from);
   void cpu_map_block(Block* b);  // refresh CPU view protections
   void stable_map_block(Block* b);
-  void finish_ctx(Ctx& c, Tracker* out);
+  Status finish_ctx(Ctx& c, Tracker* out);
   void drop_copy(Ctx& c, Block* b, const Loc& l);  // release a residency (block lock held)
   void touch_residency(Block* b, Residency* r, bool prefetched = false);  // LRU bump (preferred / prefetch aware)
   Status gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
@@ -260,6 +260,11 @@ struct Runtime::Ctx {
   ChunkArena* need_arena = nullptr;   // set on MORE_PROCESSING_REQUIRED
   uint32_t need_n = 0;
   std::vector<std::pair<Ring*, Fence*>> waited;  // GPU-side waits already queued
+  // Migration invalidations are applied only once the copies that replace the
+  // data were submitted successfully; a failed submission invalidates the
+  // destination instead, so a link/copy error never loses the source.
+  struct Inval { Block* b; Loc dst; PageMask pages; };
+  std::vector<Inval> invals;
   void use_ring(Ring* r) {
     for (Ring* x : rings)
       if (x == r) return;

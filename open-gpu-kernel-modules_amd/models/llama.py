@@ -174,9 +174,15 @@ class TieredLlama:
         self.kv_lease = self.kv.acquire(device, rt.WRITE)
         self.kv_lease.wait()
         kv = self.kv_lease.tensor((cfg.n_layers, 2, batch, self.hkv, self.T, hd), torch.bfloat16)
+        # Synthetic prefilled context, generated at full head count and sliced to
+        # this rank's KV heads so every TP degree decodes the same model state.
         g = torch.Generator(device=self.tdev).manual_seed(seed + 7919)
-        for i in range(cfg.n_layers):  # synthetic prefilled context
-            kv[i, :, :, :, :context].normal_(0.0, 1.0, generator=g)
+        h0 = self.rank * self.hkv
+        for i in range(cfg.n_layers):
+            full = torch.empty(2, batch, cfg.n_kv_heads, context, hd, dtype=torch.bfloat16, device=self.tdev)
+            full.normal_(0.0, 1.0, generator=g)
+            kv[i, :, :, :, :context].copy_(full[:, :, h0:h0 + self.hkv])
+            del full
         self.kv_t = kv
         self.pos = context
         # ---- streaming schedule: use order within a step
@@ -185,6 +191,8 @@ class TieredLlama:
         self._pf_next = 0           # next index in stream_seq to prefetch (cyclic)
         self._inflight: list = []   # prefetched, not yet consumed
         self._views: dict = {}
+        self.keep_logits = False   # tests: keep the full-vocab logits of the last step
+        self.last_logits = None
         self.init_seconds = time.perf_counter() - t0
         if verbose:
             self.describe()
@@ -329,6 +337,8 @@ class TieredLlama:
         head = rt._tensor_from_ptr(lease.dptr, (self.vocab_local, cfg.dim), torch.bfloat16,
                                    "cpu" if self.fake else "cuda", self.dev)
         logits = x @ head.t()
+        if self.keep_logits:
+            self.last_logits = comm.all_gather_cat(logits.float(), dim=-1)
         nxt = tpmod.vocab_parallel_argmax(logits, self.rank, self.world)
         lease.release(0 if self.fake else None)
         self.pos += 1

@@ -1,0 +1,128 @@
+"""CXL tier tests - the fork's tests/cxl_p2p_test.c, rebuilt so they can fail on
+data corruption (the reference's cannot: mismatches only print warnings)."""
+from __future__ import annotations
+
+import ctypes
+import mmap
+
+import pytest
+import torch
+
+from ogkm import cxl, rt
+from ogkm._native import lib
+
+MB = 1 << 20
+
+
+def _fake_sysfs(tmp_path, with_cxl_bus=True):
+    nodes = tmp_path / "devices" / "system" / "node"
+    for nid, cpus, kb in ((0, "0-7", 1 << 20), (1, "8-15", 1 << 20), (2, "", 512 << 10)):
+        d = nodes / f"node{nid}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(cpus + "\n")
+        (d / "meminfo").write_text(f"Node {nid} MemTotal:       {kb} kB\n")
+    if with_cxl_bus:
+        port = tmp_path / "bus" / "cxl" / "devices" / "port0"
+        mem = tmp_path / "bus" / "cxl" / "devices" / "mem0"
+        port.mkdir(parents=True)
+        (mem / "ram").mkdir(parents=True)
+        (mem / "ram" / "size").write_text(str(512 << 20))
+        (mem / "numa_node").write_text("2")
+        (tmp_path / "bus" / "cxl" / "devices" / "current_link_speed").write_text("32.0 GT/s PCIe")
+        (tmp_path / "bus" / "cxl" / "devices" / "current_link_width").write_text("8")
+    return tmp_path
+
+
+def test_topology_from_sysfs(fake_rt, tmp_path):
+    root = _fake_sysfs(tmp_path)
+    info = cxl.rediscover(-1, str(root))
+    assert info["numa_nodes"] == [2]
+    assert info["memory_expander"] and info["link_up"] and not info["emulated"]
+    assert info["cxl_version"] == 2  # Gen5 link
+    assert any(d["name"] == "mem0" and d["numa_node"] == 2 for d in info["devices"])
+    assert cxl.p2p_caps(0)["connectivity"] == "CXL"
+
+
+def test_emulated_node(fake_rt, tmp_path):
+    root = _fake_sysfs(tmp_path, with_cxl_bus=False)
+    for p in (root / "devices" / "system" / "node" / "node2").iterdir():
+        p.unlink()
+    (root / "devices" / "system" / "node" / "node2").rmdir()
+    info = cxl.rediscover(1, str(root))
+    assert info["emulated"] and info["numa_nodes"] == [1]
+
+
+def _buf(size):
+    m = mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    return m, ctypes.addressof(ctypes.c_char.from_buffer(m))
+
+
+def test_register_validation_and_unregister(fake_rt):
+    m, base = _buf(8 * MB)
+    with pytest.raises(rt.RuntimeStatusError):
+        lib.cxl_register(base, 0, 2)          # size 0
+    with pytest.raises(rt.RuntimeStatusError):
+        lib.cxl_register(base, 8 * MB, 4)     # version must be 1..3
+    with pytest.raises(rt.RuntimeStatusError):
+        lib.cxl_register(base + 1, 4096, 2)   # unaligned
+    h = lib.cxl_register(base, 8 * MB, 2)
+    assert h >> 32 >= 1 and (h & 0xFFFFFFFF) >= 1   # opaque generation-checked handle
+    with pytest.raises(rt.RuntimeStatusError, match="BUSY"):
+        lib.cxl_register(base + 4 * MB, 4 * MB, 2)  # overlap
+    assert lib.cxl_buffer(h)["page_size"] in (4096, 2 * MB)
+    lib.cxl_unregister(h)
+    with pytest.raises(rt.RuntimeStatusError, match="NOT_FOUND"):
+        lib.cxl_unregister(h)               # stale handle
+    h2 = lib.cxl_register(base, 8 * MB, 2)
+    assert h2 != h                          # new generation
+    lib.cxl_unregister(h2)
+
+
+def test_buffer_limit_and_pin_budget(fake_rt):
+    lib.shutdown()
+    lib.config_reset()
+    rt.init("fake", fake_devices=1, fake_hbm_mb=64, cxl_max_buffers=2)
+    bufs = [_buf(2 * MB) for _ in range(3)]
+    h = [lib.cxl_register(b, 2 * MB, 1) for _, b in bufs[:2]]
+    with pytest.raises(rt.RuntimeStatusError, match="LIMIT_EXCEEDED"):
+        lib.cxl_register(bufs[2][1], 2 * MB, 1)
+    assert lib.cxl_info()["registered_buffers"] == 2
+    assert lib.cxl_info()["pinned_bytes"] == 4 * MB
+    for x in h:
+        lib.cxl_unregister(x)
+    assert lib.cxl_info()["pinned_bytes"] == 0
+
+
+def test_pages_refcount_blocks_unregister(fake_rt):
+    m, base = _buf(4 * MB)
+    h = lib.cxl_register(base, 4 * MB, 3)
+    ext = lib.cxl_pages(h, 4096, 3 * MB)
+    assert sum(n for _, n in ext) == 3 * MB and ext[0][0] == base + 4096
+    with pytest.raises(rt.RuntimeStatusError, match="BUSY"):
+        lib.cxl_unregister(h)
+    lib.cxl_put_pages(h)
+    lib.cxl_unregister(h)
+
+
+def test_dma_roundtrip_verifies_data(fake_rt):
+    """GPU -> CXL then CXL -> GPU; any corruption fails the test."""
+    buf = cxl.CxlBuffer.allocate(4 * MB)
+    g = rt.malloc_managed(4 * MB, "g")
+    lg = g.acquire(0, rt.WRITE)
+    lg.wait(0)
+    pattern = (torch.arange(4 * MB, dtype=torch.int64) + 0xAB).remainder(256).to(torch.uint8)
+    lg.tensor((4 * MB,), torch.uint8).copy_(pattern)
+    cxl.wait(buf.dma(lg.dptr, 0, 0, 4 * MB, cxl.DIR_GPU_TO_CXL))
+    host = (ctypes.c_uint8 * (4 * MB)).from_address(buf.base)
+    assert bytes(host[:16]) == bytes(pattern[:16].tolist())
+    lg.tensor((4 * MB,), torch.uint8).zero_()
+    tid = buf.dma(lg.dptr, 0, 0, 4 * MB, cxl.DIR_CXL_TO_GPU, async_=True)
+    cxl.wait(tid)
+    assert torch.equal(lg.tensor((4 * MB,), torch.uint8), pattern)
+    with pytest.raises(rt.RuntimeStatusError):
+        buf.dma(lg.dptr, 0, 2 * MB, 4 * MB, cxl.DIR_CXL_TO_GPU)  # out of bounds
+    s = lib.stats()
+    assert s["cxl_dma_requests"] == 2 and s["cxl_dma_bytes"] == 8 * MB
+    lg.release(0)
+    g.free()
+    buf.unregister()
