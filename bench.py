@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--oversub", type=float, default=2.0)
     ap.add_argument("--lookahead", type=int, default=2)
     ap.add_argument("--no-aux", action="store_true", help="skip the HBM<->host/CXL bandwidth probe")
+    ap.add_argument("--no-packed", action="store_true",
+                    help="store streamed host copies as raw bf16 instead of lossless BF12")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -110,7 +112,7 @@ def main() -> None:
     t_init = time.perf_counter()
     model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 2,
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=world, seed=1234,
-                              lookahead=a.lookahead, verbose=a.verbose)
+                              lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed)
     plan = model.describe()
     init_s = time.perf_counter() - t_init
     g = torch.Generator(device="cpu").manual_seed(42)
@@ -154,10 +156,12 @@ def main() -> None:
                 "resident_layers": plan["resident_layers"],
                 "streamed_layers": plan["streamed_layers"],
                 "streamed_gb_per_step_per_gpu": round(plan["streamed_gb_per_step"], 2),
+                "host_copy_format": "bf12-lossless" if plan["packed_host_copies"] else "bf16",
             },
             "aux": {
                 **aux,
-                "stream_gbps_per_gpu": round(s["bytes_xfer_htd"] / max(dt, 1e-9) / 1e9, 2),
+                "link_gbps_per_gpu": round(s["bytes_xfer_htd"] / max(dt, 1e-9) / 1e9, 2),
+                "delivered_bf16_gbps_per_gpu": round(max(s["decoded_bytes"], s["bytes_xfer_htd"]) / max(dt, 1e-9) / 1e9, 2),
                 "evictions": s["evictions"],
                 "init_s": round(init_s, 1),
             },

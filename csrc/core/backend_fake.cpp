@@ -18,6 +18,7 @@
 #include <thread>
 
 #include "ogkm/backend.hpp"
+#include "ogkm/codec.hpp"
 
 namespace ogkm {
 
@@ -219,6 +220,13 @@ class FakeBackend : public Backend {
     std::vector<CopyDesc> v(d, d + n);
     run(s, [v] {
       for (auto& c : v) memmove((void*)c.dst, (const void*)c.src, c.bytes);
+    });
+    return Status::OK;
+  }
+  Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s) override {
+    std::vector<DecodeDesc> v(d, d + n);
+    run(s, [v] {
+      for (auto& x : v) bf12_decode((const uint8_t*)x.src, (uint16_t*)x.dst, x.n_values);
     });
     return Status::OK;
   }

@@ -20,6 +20,7 @@
 #include <string>
 
 #include "ogkm/backend.hpp"
+#include "ogkm/codec.hpp"
 #include "ogkm/config.hpp"
 #include "ogkm/kernels.hpp"
 
@@ -213,6 +214,25 @@ class HipBackend : public Backend {
       // HBM<->HBM copies are not PCIe bound: give them the whole chip.
       uint32_t g = hbm_only ? (wgs * 16 > 2048 ? 2048 : wgs * 16) : wgs;
       HIPCHK(launch_batch_copy(nullptr, nullptr, &inl, (uint32_t)cnt, ps, piece, g, (hipStream_t)s));
+      launches_++;
+    }
+    return Status::OK;
+  }
+
+  Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s) override {
+    uint32_t wgs = (uint32_t)config().copy_workgroups * 2;
+    if (wgs == 0) wgs = 128;
+    for (size_t base = 0; base < n; base += kInlineDescs) {
+      size_t cnt = n - base < (size_t)kInlineDescs ? n - base : (size_t)kInlineDescs;
+      KBf12Descs inl;
+      uint64_t items = 0;
+      for (size_t i = 0; i < cnt; ++i) {
+        inl.d[i] = KBf12Desc{d[base + i].src, d[base + i].dst, d[base + i].n_values, 0};
+        inl.item_start[i] = items;
+        items += (d[base + i].n_values + kBf12Tile - 1) / kBf12Tile;
+      }
+      inl.item_start[cnt] = items;
+      HIPCHK(launch_bf12_decode(inl, (uint32_t)cnt, wgs, (hipStream_t)s));
       launches_++;
     }
     return Status::OK;

@@ -1,0 +1,80 @@
+// BF12 host-side codec (reference implementation; the GPU decoder in
+// csrc/kernels/bf12_kernels.hip must produce bit-identical output).
+#include "ogkm/codec.hpp"
+
+#include <cstring>
+#include <vector>
+
+namespace ogkm {
+
+uint64_t bf12_encode(const uint16_t* in, uint32_t n, uint8_t* out, uint64_t cap) {
+  if (n == 0 || (n & 1) || n > kBf12Tile * kBf12MaxTiles) return 0;
+  // 1) exponent histogram -> base maximising the values covered by codes 0..14
+  uint32_t hist[256] = {0};
+  for (uint32_t i = 0; i < n; ++i) hist[(in[i] >> 7) & 0xFF]++;
+  uint32_t best = 0, best_cnt = 0, win = 0;
+  for (uint32_t e = 0; e < 15; ++e) win += hist[e];
+  best_cnt = win;
+  for (uint32_t b = 1; b + 15 <= 256; ++b) {
+    win += hist[b + 14] - hist[b - 1];
+    if (win > best_cnt) {
+      best_cnt = win;
+      best = b;
+    }
+  }
+  uint32_t n_exc = n - best_cnt;
+  uint64_t need = bf12_encoded_bytes(n, n_exc);
+  if (need > cap) return 0;
+  // 2) planes + per-tile exception lists
+  Bf12Header h;
+  memset(&h, 0, sizeof h);
+  h.magic = kBf12Magic;
+  h.base = best;
+  h.n_values = n;
+  h.n_exc = n_exc;
+  uint8_t* sm = out + kBf12HeaderBytes;
+  uint8_t* codes = sm + n;
+  Bf12Exception* exc = reinterpret_cast<Bf12Exception*>(codes + n / 2);
+  uint32_t ntiles = (n + kBf12Tile - 1) / kBf12Tile;
+  uint32_t e_out = 0;
+  for (uint32_t t = 0; t < ntiles; ++t) {
+    h.exc_off[t] = e_out;
+    uint32_t lo = t * kBf12Tile, hi = lo + kBf12Tile < n ? lo + kBf12Tile : n;
+    for (uint32_t i = lo; i < hi; i += 2) {
+      uint8_t nib[2];
+      for (int k = 0; k < 2; ++k) {
+        uint16_t v = in[i + k];
+        uint32_t e = (v >> 7) & 0xFF;
+        sm[i + k] = (uint8_t)(((v >> 8) & 0x80) | (v & 0x7F));
+        uint32_t c = e - best;
+        if (e < best || c >= 15) {
+          c = 15;
+          exc[e_out++] = Bf12Exception{i + k, v, 0};
+        }
+        nib[k] = (uint8_t)c;
+      }
+      codes[i >> 1] = (uint8_t)(nib[0] | (nib[1] << 4));
+    }
+  }
+  for (uint32_t t = ntiles; t <= kBf12MaxTiles; ++t) h.exc_off[t] = e_out;
+  memcpy(out, &h, sizeof h);
+  return need;
+}
+
+bool bf12_decode(const uint8_t* in, uint16_t* out, uint32_t n) {
+  Bf12Header h;
+  memcpy(&h, in, sizeof h);
+  if (h.magic != kBf12Magic || h.n_values != n) return false;
+  const uint8_t* sm = in + kBf12HeaderBytes;
+  const uint8_t* codes = sm + n;
+  const Bf12Exception* exc = reinterpret_cast<const Bf12Exception*>(codes + n / 2);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t c = (codes[i >> 1] >> ((i & 1) * 4)) & 0xF;
+    uint32_t s = sm[i];
+    out[i] = (uint16_t)(((s & 0x80) << 8) | (((h.base + c) & 0xFF) << 7) | (s & 0x7F));
+  }
+  for (uint32_t k = 0; k < h.n_exc; ++k) out[exc[k].index] = exc[k].bits;
+  return true;
+}
+
+}  // namespace ogkm

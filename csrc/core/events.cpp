@@ -127,7 +127,9 @@ const char* counter_name(Counter c) {
                             "cxl_dma_requests",
                             "cxl_dma_bytes",
                             "alloc_retries",
-                            "injected_errors"};
+                            "injected_errors",
+                            "decoded_bytes",
+                            "encoded_bytes"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

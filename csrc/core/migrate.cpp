@@ -23,6 +23,7 @@
 #include <shared_mutex>
 #include <thread>
 
+#include "ogkm/codec.hpp"
 #include "ogkm/runtime.hpp"
 
 namespace ogkm {
@@ -157,8 +158,10 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
   if (pages.empty()) return Status::OK;
   Ring* ring = ring_for(rt, from->loc, to->loc);
   Counter ctr = xfer_counter(from->loc, to->loc);
-  uint64_t bytes = (uint64_t)pages.count() << kPageShift;
+  // Bytes that actually cross the link (an encoded block moves its encoded size).
+  uint64_t bytes = from->fmt == 1 ? from->enc_bytes : (uint64_t)pages.count() << kPageShift;
   Tools::get().inc(ctr, bytes);
+  if (from->fmt == 1 && to->loc.is_gpu()) Tools::get().inc(Counter::DecodedBytes, (uint64_t)b->npages << kPageShift);
   if (c.cause == Cause::Prefetch) {
     if (to->loc.is_gpu()) Tools::get().inc(Counter::PrefetchBytesXferHtD, bytes);
     else Tools::get().inc(Counter::PrefetchBytesXferDtH, bytes);
@@ -193,10 +196,17 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     // CPU <-> CPU (host / CXL tiers): synchronous memcpy.
     reuse.wait();
     pend.wait();
-    pages.for_each_run([&](uint32_t p, uint32_t n) {
-      memcpy((void*)page_addr(to->arena, to->chunk, p), (const void*)page_addr(from->arena, from->chunk, p),
-             (uint64_t)n << kPageShift);
-    });
+    if (from->fmt == 1) {
+      memcpy((void*)page_addr(to->arena, to->chunk, 0), (const void*)page_addr(from->arena, from->chunk, 0),
+             from->enc_bytes);
+      to->fmt = 1;
+      to->enc_bytes = from->enc_bytes;
+    } else {
+      pages.for_each_run([&](uint32_t p, uint32_t n) {
+        memcpy((void*)page_addr(to->arena, to->chunk, p), (const void*)page_addr(from->arena, from->chunk, p),
+               (uint64_t)n << kPageShift);
+      });
+    }
     tools_event(ToolsEventType::Migration, c.cause, from->loc, to->loc, kCpuProc, b->range->addr() + b->block_offset(),
                 bytes, b->range->id, t0, now_ns());
     return Status::OK;
@@ -215,22 +225,41 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     w.wait = f;
     ring->push(std::move(w));
   }
-  pages.for_each_run([&](uint32_t p, uint32_t n) {
+  if (from->fmt == 1) {
+    // Encoded source: one fused copy+decode of the whole block into HBM, or a
+    // verbatim copy of the encoded bytes into another host / CXL chunk.
     Sqe s;
-    s.op = SqeOp::COPY;
-    s.dst = page_addr(to->arena, to->chunk, p);
-    s.src = page_addr(from->arena, from->chunk, p);
-    s.bytes = (uint64_t)n << kPageShift;
+    s.op = to->loc.is_gpu() ? SqeOp::DECODE_BF12 : SqeOp::COPY;
+    s.dst = page_addr(to->arena, to->chunk, 0);
+    s.src = page_addr(from->arena, from->chunk, 0);
+    s.bytes = to->loc.is_gpu() ? (uint64_t)b->npages << kPageShift : from->enc_bytes;
     s.user_data = b->range->id;
     s.file = __FILE__;
     s.line = __LINE__;
-    if (log_level() >= LogLevel::DEBUG)
-      s.desc = "range " + std::to_string(b->range->id) + " block " + std::to_string(b->index) + " " +
-               from->loc.str() + "->" + to->loc.str();
     ring->push(std::move(s));
-  });
+    if (!to->loc.is_gpu()) {
+      to->fmt = 1;
+      to->enc_bytes = from->enc_bytes;
+    }
+  } else {
+    pages.for_each_run([&](uint32_t p, uint32_t n) {
+      Sqe s;
+      s.op = SqeOp::COPY;
+      s.dst = page_addr(to->arena, to->chunk, p);
+      s.src = page_addr(from->arena, from->chunk, p);
+      s.bytes = (uint64_t)n << kPageShift;
+      s.user_data = b->range->id;
+      s.file = __FILE__;
+      s.line = __LINE__;
+      if (log_level() >= LogLevel::DEBUG)
+        s.desc = "range " + std::to_string(b->range->id) + " block " + std::to_string(b->index) + " " +
+                 from->loc.str() + "->" + to->loc.str();
+      ring->push(std::move(s));
+    });
+  }
   c.use_ring(ring);
   c.touched.push_back({ring, b});
+  b->unpublished++;
   c.chunk_uses.push_back({ring, from->arena, (uint32_t)from->chunk, false});
   tools_event(ToolsEventType::Migration, c.cause, from->loc, to->loc, to->loc.is_gpu() ? to->loc.id : kCpuProc,
               b->range->addr() + b->block_offset(), bytes, b->range->id, t0, 0, ring->pushed_seq());
@@ -268,6 +297,7 @@ static Status zero_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* to, 
   });
   c.use_ring(ring);
   c.touched.push_back({ring, b});
+  b->unpublished++;
   return Status::OK;
 }
 
@@ -301,6 +331,14 @@ static void drop_residency(Runtime::Ctx& c, Block* b, const Loc& l) {
 Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc dst, bool read_dup, Cause cause) {
   PageMask pages = pages_in & b->valid_pages();
   if (pages.empty()) return Status::OK;
+  if (b->range->flags & RANGE_COMPRESS_BF16) {
+    // Encoded blocks move whole, and GPU copies are read-only duplicates.
+    bool encoded_src = false;
+    for (auto& r : b->res)
+      if (r.fmt == 1) encoded_src = true;
+    if (encoded_src) pages = b->valid_pages();
+    if (dst.is_gpu()) read_dup = true;
+  }
   c.cause = cause;
   Residency* to = nullptr;
   int64_t hint = -1;
@@ -316,6 +354,17 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
   if (st != Status::OK) return st;
   PageMask missing = pages.andnot(to->resident);
   bool copied = false;
+  if (!missing.empty() && to->fmt == 1) {
+    // Raw pages are about to land in an encoded chunk: expand it in place first.
+    std::vector<uint16_t> tmp((size_t)b->npages << (kPageShift - 1));
+    uint8_t* base = (uint8_t*)to->arena->chunk_addr((uint32_t)to->chunk);
+    Tracker t = b->tracker;
+    t.wait();
+    if (!bf12_decode(base, tmp.data(), (uint32_t)tmp.size())) return Status::IO_ERROR;
+    memcpy(base, tmp.data(), tmp.size() * 2);
+    to->fmt = 0;
+    to->enc_bytes = 0;
+  }
   if (!missing.empty()) {
     // Source = closest resident copy per page: same tier first, then HBM peers,
     // then host, then CXL.
@@ -386,6 +435,18 @@ done:
   return Status::OK;
 }
 
+// Snapshot of a block's tracker once every queued copy into it has published
+// its fence (another thread may be between make_resident and finish_ctx).
+Tracker Runtime::published_tracker(Block* b) {
+  for (;;) {
+    {
+      std::lock_guard<OrderedMutex> g(b->lock);
+      if (b->unpublished == 0) return b->tracker;
+    }
+    std::this_thread::yield();
+  }
+}
+
 // Free the chunk behind residency `r` once every pending writer/reader of the
 // block has finished (block lock held), and forget the residency.
 static void release_residency_now(Block* b, const Loc& l) {
@@ -418,9 +479,9 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
   };
   for (auto& t : c.touched) {
     FenceRef f = fence_of(t.ring);
-    if (!f) continue;
     std::lock_guard<OrderedMutex> g(t.block->lock);
-    t.block->tracker.add(f);
+    if (f) t.block->tracker.add(f);
+    if (t.block->unpublished) t.block->unpublished--;
   }
   for (auto& u : c.chunk_uses) {
     FenceRef f = fence_of(u.ring);
@@ -822,10 +883,7 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
     return st;
   }
   if (L) {
-    for (Block* b : L->blocks) {
-      std::lock_guard<OrderedMutex> g(b->lock);
-      L->ready.merge(b->tracker);
-    }
+    for (Block* b : L->blocks) L->ready.merge(published_tracker(b));
     L->dptr = ga->chunk_addr((uint32_t)first) + (off - (b0 << kBlockShift));
   }
   return Status::OK;
@@ -842,6 +900,9 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
   L->offset = off;
   L->bytes = len;
   L->proc = proc;
+  const bool packed = (r->flags & RANGE_COMPRESS_BF16) != 0;
+  if (packed && (proc == kCpuProc || access == Access::WRITE || access == Access::ATOMIC))
+    return Status::NOT_SUPPORTED;  // packed ranges are GPU-read-only (the host copy is encoded)
   if (r->type == RangeType::EXTERNAL || r->type == RangeType::DEVICE_P2P) {
     // Foreign / device-P2P memory never migrates: lease the original pointer.
     L->dptr = r->ext_ptr + off;
@@ -864,6 +925,11 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
       Block* b = r->block(b0 + k);
       std::lock_guard<OrderedMutex> g(b->lock);
       dec[k] = select_residency(this, b, proc, access, pages_of(b0 + k));
+      if (packed) {  // encoded bytes cannot be read remotely: always decode into HBM
+        dec[k].map_remote = false;
+        dec[k].dst = dst;
+        dec[k].read_dup = true;
+      }
       if (!dec[k].map_remote) all_remote = false;
     }
     Ctx c;
@@ -896,6 +962,7 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
       if (st == Status::OK) st = fs;
       L->ready.wait();
       for (Block* b : L->blocks) {
+        published_tracker(b).wait();
         std::lock_guard<OrderedMutex> g(b->lock);
         b->tracker.prune();
         cpu_map_block(b);
@@ -973,10 +1040,7 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
       } else if (st == Status::OK) {
         L->remote = true;
         L->dptr = ra->chunk_addr((uint32_t)first) + (off - (b0 << kBlockShift));
-        for (Block* b : L->blocks) {
-          std::lock_guard<OrderedMutex> g(b->lock);
-          L->ready.merge(b->tracker);
-        }
+        for (Block* b : L->blocks) L->ready.merge(published_tracker(b));
         Tools::get().inc(Counter::MapRemote, n);
       } else {
         for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
@@ -1176,9 +1240,11 @@ Status Runtime::cpu_fault(uint64_t addr, bool write) {
   t.wait();
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   Block* b = r->block(off >> kBlockShift);
+  // Concurrent faults (e.g. a multi-threaded memcpy over the CPU view) may still
+  // be publishing copies into this block: wait for all of them, not just ours.
+  published_tracker(b).wait();
   std::lock_guard<OrderedMutex> g(b->lock);
-  b->tracker.wait();
-  b->tracker.clear();
+  b->tracker.prune();
   uint32_t page = (uint32_t)((off & (kBlockSize - 1)) >> kPageShift);
   if (write) {
     // A CPU write collapses read duplication: revoke every other copy of the page.

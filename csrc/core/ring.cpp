@@ -71,15 +71,19 @@ FenceRef Ring::submit_locked() {
   Status st = err_;
   uint64_t last = 0;
   std::vector<CopyDesc> batch;
+  std::vector<DecodeDesc> dbatch;
   int engine = kind_ == RingKind::GPU_INTERNAL ? 2 : (int)config().copy_engine;
   auto flush = [&]() {
-    if (batch.empty() || st != Status::OK) {
-      batch.clear();
-      return;
+    if (st == Status::OK && !batch.empty()) {
+      st = be_->copy_batch(dev_, batch.data(), batch.size(), stream_, engine);
+      Tools::get().inc(Counter::CopyKernelLaunches);
     }
-    st = be_->copy_batch(dev_, batch.data(), batch.size(), stream_, engine);
-    Tools::get().inc(Counter::CopyKernelLaunches);
+    if (st == Status::OK && !dbatch.empty()) {
+      st = be_->decode_bf12(dev_, dbatch.data(), dbatch.size(), stream_);
+      Tools::get().inc(Counter::CopyKernelLaunches);
+    }
     batch.clear();
+    dbatch.clear();
   };
   std::vector<std::pair<uint64_t, Cqe>> done;
   for (auto& e : sq_) {
@@ -98,6 +102,7 @@ FenceRef Ring::submit_locked() {
             st = Status::INJECTED_ERROR;
             break;
           }
+          if (!dbatch.empty()) flush();
           // Coalesce physically adjacent copies (consecutive 2 MB blocks of one
           // extent) into a single descriptor.
           if (!batch.empty() && batch.back().dst + batch.back().bytes == s.dst &&
@@ -105,6 +110,10 @@ FenceRef Ring::submit_locked() {
             batch.back().bytes += s.bytes;
           else
             batch.push_back(CopyDesc{s.dst, s.src, s.bytes});
+          break;
+        case SqeOp::DECODE_BF12:
+          if (!batch.empty()) flush();
+          dbatch.push_back(DecodeDesc{s.src, s.dst, (uint32_t)(s.bytes / 2)});
           break;
         case SqeOp::GATHER:
         case SqeOp::SCATTER: {

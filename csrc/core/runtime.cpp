@@ -2,6 +2,7 @@
 // CPU/stable-VA mapping maintenance, CXL DMA, quiesce/resume and the
 // residency-map checkpoint format.
 #include "ogkm/runtime.hpp"
+#include "ogkm/codec.hpp"
 
 #include <signal.h>
 #include <sys/mman.h>
@@ -144,6 +145,10 @@ ChunkArena* Runtime::arena_for(const Loc& l) {
 Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string& name, Range** out, int stable_dev) {
   if (global_status() != Status::OK) return global_status();
   if (size == 0) return Status::INVALID_ARGUMENT;
+  if (flags & RANGE_COMPRESS_BF16) {
+    if ((size & (kPageSize - 1)) || (flags & RANGE_STABLE_VA)) return Status::INVALID_ARGUMENT;
+    flags |= RANGE_NO_CPU_VIEW;  // the host copy is encoded: no direct CPU mapping
+  }
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
   uint64_t id = vs_.next_range_id++;
   auto r = std::make_unique<Range>(&vs_, id, RangeType::MANAGED, size, flags, name);
@@ -364,7 +369,7 @@ void Runtime::cpu_map_block(Block* b) {
     b->cpu_ro.zero();
     b->cpu_rw.zero();
   }
-  bool pending = !b->tracker.query();
+  bool pending = b->unpublished > 0 || !b->tracker.query();
   PageMask others;
   for (auto& x : b->res)
     if (&x != h) others |= x.resident;
@@ -416,10 +421,10 @@ void Runtime::update_device_table(Block* b) {
   for (auto& x : b->res) {
     if ((x.resident & valid) == valid) {
       if (x.loc == Loc::gpu(t->dev)) hbm = x.arena->chunk_addr((uint32_t)x.chunk);
-      else if (!x.loc.is_gpu() && !rem) rem = x.arena->chunk_addr((uint32_t)x.chunk);
+      else if (!x.loc.is_gpu() && !rem && x.fmt == 0) rem = x.arena->chunk_addr((uint32_t)x.chunk);
     }
   }
-  bool pending = !b->tracker.query();
+  bool pending = b->unpublished > 0 || !b->tracker.query();
   __atomic_store_n(&t->entries[2 * b->index], pending ? 0 : hbm, __ATOMIC_RELEASE);
   __atomic_store_n(&t->entries[2 * b->index + 1], pending ? 0 : rem, __ATOMIC_RELEASE);
 }
@@ -451,10 +456,130 @@ Status Runtime::device_table(Range* r, DeviceResidencyTable** out) {
 }
 
 // ------------------------------------------------------------------ data helpers
+// Write whole blocks of a RANGE_COMPRESS_BF16 range: the host / CXL copy is
+// stored BF12-encoded (raw when a block does not compress). Encoding runs on a
+// small thread pool; GPU sources are staged through pinned host chunks.
+Status Runtime::write_compressed(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev) {
+  if ((off & (kBlockSize - 1)) || ((bytes & (kBlockSize - 1)) && off + bytes != r->size)) return Status::INVALID_ARGUMENT;
+  uint64_t b0 = off >> kBlockShift, nb = (bytes + kBlockSize - 1) >> kBlockShift;
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  const uint64_t batch = 64;
+  HostArena* stage = nullptr;
+  uint32_t stage_first = 0;
+  if (src_dev >= 0) {
+    stage = host_arena(Tier::HOST, host_node_);
+    if (!stage) return Status::NO_MEMORY;
+    Status st = alloc_chunks(stage, (uint32_t)std::min<uint64_t>(batch, nb), -1, &stage_first);
+    if (st != Status::OK) return st;
+  }
+  Status result = Status::OK;
+  unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  for (uint64_t s = 0; s < nb && result == Status::OK; s += batch) {
+    uint64_t n = std::min(batch, nb - s);
+    // 1) raw source pointers (staging GPU data to host first)
+    std::vector<const uint8_t*> raw(n);
+    if (src_dev >= 0) {
+      Ring* rg = ring(src_dev, RingKind::GPU_TO_CPU);
+      for (uint64_t k = 0; k < n; ++k) {
+        uint64_t boff = (b0 + s + k) << kBlockShift;
+        Sqe cp;
+        cp.op = SqeOp::COPY;
+        cp.dst = stage->chunk_addr(stage_first + (uint32_t)k);
+        cp.src = (uint64_t)src + (boff - off);
+        cp.bytes = std::min<uint64_t>(kBlockSize, r->size - boff);
+        rg->push(std::move(cp));
+        raw[k] = (const uint8_t*)stage->chunk_addr(stage_first + (uint32_t)k);
+      }
+      result = rg->submit()->wait();
+      if (result != Status::OK) break;
+    } else {
+      for (uint64_t k = 0; k < n; ++k) raw[k] = (const uint8_t*)src + (((b0 + s + k) << kBlockShift) - off);
+    }
+    // 2) destination chunks (one block lock at a time)
+    std::vector<Residency*> dst(n, nullptr);
+    for (uint64_t k = 0; k < n && result == Status::OK; ++k) {
+      Block* b = r->block(b0 + s + k);
+      for (int attempt = 0; attempt < 8; ++attempt) {
+        Ctx c;
+        Status st;
+        {
+          std::lock_guard<OrderedMutex> g(b->lock);
+          Loc d = b->policy.has_preferred && !b->policy.preferred.is_gpu() ? b->policy.preferred : cpu_loc();
+          st = populate(c, b, d, -1, &dst[k]);
+          if (st == Status::OK) {
+            b->tracker.wait();
+            Tracker rf = dst[k]->arena->take_reuse_fence((uint32_t)dst[k]->chunk);
+            rf.wait();
+          }
+        }
+        if (st != Status::MORE_PROCESSING_REQUIRED) {
+          result = st;
+          break;
+        }
+        Reservation rr;
+        Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+        if (es != Status::OK) {
+          result = es;
+          break;
+        }
+        c.need_arena->free((uint32_t)rr.first, rr.n);
+      }
+    }
+    if (result != Status::OK) break;
+    // 3) encode in parallel (no locks: the chunks carry no resident pages yet)
+    std::vector<uint64_t> enc(n, 0);
+    std::atomic<uint64_t> next{0};
+    auto work = [&] {
+      for (uint64_t k; (k = next.fetch_add(1)) < n;) {
+        Block* b = r->block(b0 + s + k);
+        uint8_t* out = (uint8_t*)dst[k]->arena->chunk_addr((uint32_t)dst[k]->chunk);
+        uint32_t nv = b->npages << (kPageShift - 1);
+        uint64_t nbytes = std::min<uint64_t>(kBlockSize, r->size - b->block_offset());
+        if (nbytes == ((uint64_t)b->npages << kPageShift)) enc[k] = bf12_encode((const uint16_t*)raw[k], nv, out, kBlockSize);
+        if (!enc[k]) {
+          memcpy(out, raw[k], nbytes);
+          if (nbytes < ((uint64_t)b->npages << kPageShift)) memset(out + nbytes, 0, ((uint64_t)b->npages << kPageShift) - nbytes);
+        }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < std::min<uint64_t>(nthreads, n); ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    // 4) publish: this copy becomes the only valid one
+    for (uint64_t k = 0; k < n; ++k) {
+      Block* b = r->block(b0 + s + k);
+      Ctx c;
+      {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        Residency* d = dst[k];
+        d->fmt = enc[k] ? 1 : 0;
+        d->enc_bytes = (uint32_t)enc[k];
+        d->resident = b->valid_pages();
+        if (enc[k]) Tools::get().inc(Counter::EncodedBytes, (uint64_t)b->npages << kPageShift);
+        Loc keep = d->loc;
+        std::vector<Loc> drop;
+        for (auto& x : b->res)
+          if (!(x.loc == keep)) drop.push_back(x.loc);
+        for (auto& l : drop) {
+          b->find(l)->resident.zero();
+          drop_copy(c, b, l);
+        }
+        touch_residency(b, b->find(keep));
+        c.cpu_refresh.push_back(b);
+      }
+      finish_ctx(c, nullptr);
+    }
+  }
+  if (stage) stage->free(stage_first, (uint32_t)std::min<uint64_t>(batch, nb));
+  return result;
+}
+
 Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev) {
   if (!r || off + bytes > r->size) return Status::INVALID_ARGUMENT;
   if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
   if (bytes == 0) return Status::OK;
+  if (r->flags & RANGE_COMPRESS_BF16) return write_compressed(r, off, src, bytes, src_dev);
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   uint64_t pos = off;
   while (pos < off + bytes) {
@@ -572,6 +697,34 @@ Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_
     b->tracker.wait();
     uint64_t lo = pos - (bi << kBlockShift);
     char* out = (char*)dst + (pos - off);
+    // An encoded copy is decoded into a pinned scratch chunk and read from there.
+    Residency decoded;
+    Residency* encoded = nullptr;
+    HostArena* scratch_arena = nullptr;
+    for (auto& x : b->res)
+      if (x.fmt == 1) encoded = &x;
+    if (encoded) {
+      scratch_arena = host_arena(Tier::HOST, host_node_);
+      uint32_t tmp;
+      Status st = scratch_arena ? alloc_chunks(scratch_arena, 1, -1, &tmp) : Status::NO_MEMORY;
+      if (st != Status::OK) return st;
+      decoded = *encoded;
+      decoded.arena = scratch_arena;
+      decoded.chunk = tmp;
+      decoded.fmt = 0;
+      if (!bf12_decode((const uint8_t*)encoded->arena->chunk_addr((uint32_t)encoded->chunk),
+                       (uint16_t*)scratch_arena->chunk_addr(tmp), b->npages << (kPageShift - 1))) {
+        scratch_arena->free(tmp, 1);
+        return Status::IO_ERROR;
+      }
+    }
+    struct ScratchGuard {
+      HostArena* a;
+      Residency* r;
+      ~ScratchGuard() {
+        if (a) a->free((uint32_t)r->chunk, 1);
+      }
+    } guard{scratch_arena, &decoded};
     // Walk page by page, coalescing by source.
     uint64_t cur = pos;
     while (cur < end) {
@@ -580,6 +733,7 @@ Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_
       Residency* src = nullptr;
       for (auto& x : b->res)
         if (x.resident.test(p) && (!src || (!x.loc.is_gpu() && src->loc.is_gpu()))) src = &x;
+      if (src && src == encoded) src = &decoded;
       char* o = out + (cur - pos);
       uint64_t n = pend - cur;
       uint64_t in_chunk = cur - (bi << kBlockShift);
@@ -669,6 +823,7 @@ Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
     out->resident_on.push_back(x.loc);
     out->chunk.push_back(x.chunk);
     out->pages.push_back(x.resident.count());
+    out->enc_bytes.push_back(x.fmt == 1 ? x.enc_bytes : 0);
     dup |= seen & x.resident;
     seen |= x.resident;
   }

@@ -39,6 +39,13 @@ struct PageListDesc {
   uint32_t page_bytes;
 };
 
+// One fused copy+decode of a BF12-encoded block (codec.hpp) into raw bf16.
+struct DecodeDesc {
+  uint64_t src;       // encoded block (device-readable host / CXL memory)
+  uint64_t dst;       // raw bf16 output (HBM)
+  uint32_t n_values;
+};
+
 enum class LinkType : int { NONE = 0, SELF = 1, PCIE = 2, XGMI = 3 };
 
 class Backend {
@@ -85,6 +92,7 @@ class Backend {
   // engine: 0 = copy kernel with the PCIe CU budget, 1 = SDMA, 2 = copy kernel
   // with the whole chip (HBM<->HBM).
   virtual Status copy_batch(int dev, const CopyDesc* d, size_t n, void* stream, int engine) = 0;
+  virtual Status decode_bf12(int dev, const DecodeDesc* d, size_t n, void* stream) = 0;
   virtual Status gather_pages(int dev, const PageListDesc& d, void* stream) = 0;
   virtual Status scatter_pages(int dev, const PageListDesc& d, void* stream) = 0;
   virtual Status memset32(int dev, uint64_t dst, uint32_t pattern, size_t bytes, void* stream) = 0;

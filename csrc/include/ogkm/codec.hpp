@@ -1,0 +1,59 @@
+// BF12: lossless packed-bf16 format for the host / CXL tiers.
+//
+// Streaming decode at 2x oversubscription is bound by PCIe bytes, so the host
+// copy of a bf16 weight block is stored packed and the H2D copy kernel decodes
+// it on the fly (csrc/kernels/bf12_kernels.hip): fewer bytes on the link, the
+// exact same bf16 bits in HBM.
+//
+// A bf16 value is s(1) e(8) m(7). Weights cluster in a narrow exponent band, so
+// per 2 MB block we pick a base exponent and store
+//   sm byte    = s << 7 | m                        (1 byte / value)
+//   code       = e - base  if 0 <= e - base < 15   (4 bits / value)
+//              = 15        otherwise (escape: exact value in the exception list)
+// Layout of one encoded block (all offsets from the block start):
+//   [0, 256)                  Bf12Header
+//   [256, 256 + n)            sm bytes
+//   [256 + n, 256 + 1.5 n)    code nibbles (value 2i in the low nibble of byte i)
+//   [256 + 1.5 n, ...)        exceptions {u32 index, u16 bits, u16 pad}, grouped by
+//                             32768-value tile (tile t owns [exc_off[t], exc_off[t+1]))
+// 12 bits/value + 8 B per exception: 0.75x for typical weights. A block whose
+// encoding would not fit 2 MB is stored raw (Bf12 returns false).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+namespace ogkm {
+
+constexpr uint32_t kBf12Magic = 0x32314642;  // "BF12"
+constexpr uint32_t kBf12Tile = 32768;        // values per decode tile (64 KB of bf16)
+constexpr uint32_t kBf12MaxTiles = 32;       // 2 MB block / 64 KB
+constexpr uint32_t kBf12HeaderBytes = 256;
+
+struct Bf12Header {
+  uint32_t magic;
+  uint32_t base;       // exponent of code 0
+  uint32_t n_values;
+  uint32_t n_exc;
+  uint32_t exc_off[kBf12MaxTiles + 1];
+  uint32_t reserved[(kBf12HeaderBytes / 4) - 4 - (kBf12MaxTiles + 1)];
+};
+static_assert(sizeof(Bf12Header) == kBf12HeaderBytes, "BF12 header is 256 bytes");
+
+struct Bf12Exception {
+  uint32_t index;
+  uint16_t bits;
+  uint16_t pad;
+};
+
+inline uint64_t bf12_encoded_bytes(uint32_t n_values, uint32_t n_exc) {
+  return kBf12HeaderBytes + (uint64_t)n_values + (uint64_t)n_values / 2 + (uint64_t)n_exc * sizeof(Bf12Exception);
+}
+
+// Encode n_values bf16 (n_values even) into `out` (capacity `cap` bytes).
+// Returns the encoded size, or 0 when the block does not compress into `cap`.
+uint64_t bf12_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);
+// Decode an encoded block into n_values bf16.
+bool bf12_decode(const uint8_t* in, uint16_t* out, uint32_t n_values);
+
+}  // namespace ogkm

@@ -171,6 +171,8 @@ enum class Counter : int {
   CxlDmaBytes,
   AllocRetries,
   InjectedErrors,
+  DecodedBytes,     // raw bytes produced by the fused BF12 copy+decode
+  EncodedBytes,     // raw bytes stored BF12-packed in host / CXL tiers
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -37,6 +37,19 @@ hipError_t launch_gather_pages(uint64_t base, uint64_t contig, const uint32_t* d
 hipError_t launch_memset32(uint64_t dst, uint32_t pattern, uint64_t bytes, hipStream_t s);
 hipError_t launch_signal(uint64_t* host_addr, uint64_t value, hipStream_t s);
 
+// Fused copy + BF12 decode of up to kInlineDescs encoded blocks (codec.hpp).
+struct KBf12Desc {
+  uint64_t src;        // encoded block (pinned host / CXL)
+  uint64_t dst;        // bf16 output (HBM)
+  uint32_t n_values;
+  uint32_t pad;
+};
+struct KBf12Descs {
+  KBf12Desc d[kInlineDescs];
+  uint64_t item_start[kInlineDescs + 1];  // prefix sum of 32768-value tiles
+};
+hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgroups, hipStream_t s);
+
 // Gather `nrows` rows (row_bytes each) of a managed table through its device
 // residency table; misses read zero and are recorded as faults, remote hits are
 // recorded as access-counter notifications.

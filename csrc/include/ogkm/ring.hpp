@@ -37,7 +37,8 @@ enum class RingKind : int {
 };
 const char* ring_kind_str(RingKind k);
 
-enum class SqeOp : uint8_t { COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP };
+// DECODE_BF12: fused copy + decode of an encoded block (dst = raw bf16, bytes = 2 * values).
+enum class SqeOp : uint8_t { COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP, DECODE_BF12 };
 
 struct Sqe {
   SqeOp op = SqeOp::NOP;

@@ -117,6 +117,7 @@ struct ResidencyInfo {   // UVM_TEST_VA_RESIDENCY_INFO analog (uvm_test_ioctl.h:
   std::vector<Loc> resident_on;
   std::vector<int64_t> chunk;       // per resident_on entry
   std::vector<uint32_t> pages;      // resident page count per entry
+  std::vector<uint32_t> enc_bytes;  // encoded size per entry (0 = raw)
   std::vector<int> mapped_on;       // processors with a mapping (CPU view / stable VA / leases)
   bool read_dup = false;
   bool pinned = false;
@@ -178,6 +179,7 @@ class Runtime {
 
   // ---- data movement helpers
   Status write(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev);
+  Status write_compressed(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev);
   Status read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_dev);
   Status fill(Range* r, uint64_t off, uint64_t bytes, uint32_t pattern);
 
@@ -221,6 +223,7 @@ class Runtime {
   Status finish_ctx(Ctx& c, Tracker* out);
   void drop_copy(Ctx& c, Block* b, const Loc& l);  // release a residency (block lock held)
   void touch_residency(Block* b, Residency* r, bool prefetched = false);  // LRU bump (preferred / prefetch aware)
+  Tracker published_tracker(Block* b);  // tracker once all queued copies into b published their fences
   Status gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
                              Lease* L, Tracker* out, Cause cause);
   Status queue_copy(Ctx& c, Block* b, Residency* from, Residency* to, const PageMask& pages);

@@ -64,6 +64,8 @@ struct Residency {
   PageMask resident;
   ChunkArena* arena = nullptr;
   int64_t chunk = -1;
+  uint8_t fmt = 0;           // chunk content: 0 raw pages, 1 BF12-encoded block (codec.hpp)
+  uint32_t enc_bytes = 0;    // encoded size when fmt == 1
 };
 
 class Block {
@@ -89,6 +91,10 @@ class Block {
   ThrashState thrash;
   AccessCounterState counters;
   Tracker tracker;             // outstanding copies touching this block
+  // Copies queued into this block whose fence is not yet in `tracker` (between
+  // make_resident and finish_ctx). While non-zero the new residency bits must
+  // not be trusted by another thread (CPU mapping, leases).
+  uint32_t unpublished = 0;
 
   Residency* find(const Loc& l);
   Residency* find_slot(int slot);
@@ -106,6 +112,9 @@ const char* range_type_str(RangeType t);
 enum RangeFlags : uint32_t {
   RANGE_STABLE_VA = 1u << 0,   // device VA fixed for the lifetime (VMM mapped)
   RANGE_NO_CPU_VIEW = 1u << 1, // skip the CPU view reservation
+  // Contents are bf16 and read-only on GPUs: host / CXL copies are stored
+  // BF12-packed (lossless) and decoded by the H2D copy kernel. Implies no CPU view.
+  RANGE_COMPRESS_BF16 = 1u << 2,
 };
 
 class Range {

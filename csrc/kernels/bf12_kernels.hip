@@ -1,0 +1,129 @@
+// Fused H2D copy + BF12 decode (see ogkm/codec.hpp for the format).
+//
+// One work item = one 32768-value tile (64 KB of bf16 output) of one block. A
+// workgroup of 256 threads (4 waves):
+//   1. streams the tile's packed planes straight from pinned host / CXL memory
+//      (16-B sign|mantissa loads + 8-B exponent-code loads per lane, non-temporal:
+//      48 KB cross PCIe instead of 64 KB),
+//   2. rebuilds the bf16 words into an LDS staging tile (64 KB),
+//   3. patches the tile's escaped values into LDS,
+//   4. writes the finished tile to HBM with 16-B non-temporal stores.
+// The kernel is PCIe-bound like the plain copy kernel; LDS staging keeps the HBM
+// write pass fully coalesced and writes every output byte exactly once.
+#include <hip/hip_runtime.h>
+
+#include "ogkm/codec.hpp"
+#include "ogkm/kernels.hpp"
+
+namespace ogkm {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kDecThreads = 256;
+
+// 4 values: sign|mantissa bytes in `s` (one per byte), 4 codes in the low 16
+// bits of `c` (one nibble each) -> two u32 words of packed bf16 pairs.
+__device__ __forceinline__ u32x2 dec4(uint32_t s, uint32_t c, uint32_t base) {
+  u32x2 r;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      int k = 2 * p + q;
+      uint32_t sm = (s >> (8 * k)) & 0xFF;
+      uint32_t e = (base + ((c >> (4 * k)) & 0xF)) & 0xFF;
+      uint32_t v = ((sm & 0x80) << 8) | (e << 7) | (sm & 0x7F);
+      w |= v << (16 * q);
+    }
+    r[p] = w;
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(kDecThreads)
+    k_bf12_decode(KBf12Descs inl, uint32_t n, uint64_t total_items) {
+  __shared__ u32x4 tile[kBf12Tile * 2 / 16];  // 64 KB staging tile
+  __shared__ uint32_t s_desc, s_base, s_e0, s_e1;
+  uint32_t hint = 0;
+  for (uint64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
+    if (threadIdx.x == 0) {
+      uint32_t i = hint;
+      while (i + 1 < n && inl.item_start[i + 1] <= item) ++i;
+      if (inl.item_start[i] > item) {
+        i = 0;
+        while (i + 1 < n && inl.item_start[i + 1] <= item) ++i;
+      }
+      s_desc = i;
+      const Bf12Header* h = reinterpret_cast<const Bf12Header*>(inl.d[i].src);
+      uint32_t t = (uint32_t)(item - inl.item_start[i]);
+      s_base = __builtin_nontemporal_load(&h->base);
+      s_e0 = __builtin_nontemporal_load(&h->exc_off[t]);
+      s_e1 = __builtin_nontemporal_load(&h->exc_off[t + 1]);
+    }
+    __syncthreads();
+    const uint32_t di = s_desc;
+    hint = di;
+    const KBf12Desc d = inl.d[di];
+    const uint32_t t = (uint32_t)(item - inl.item_start[di]);
+    const uint32_t lo = t * kBf12Tile;
+    const uint32_t cnt = d.n_values - lo < kBf12Tile ? d.n_values - lo : kBf12Tile;
+    const uint32_t base = s_base;
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(d.src);
+    const u32x4* sm16 = reinterpret_cast<const u32x4*>(src + kBf12HeaderBytes + lo);
+    const u32x2* cd8 = reinterpret_cast<const u32x2*>(src + kBf12HeaderBytes + d.n_values + lo / 2);
+    const uint32_t groups = cnt / 16;  // 16 values per lane-iteration
+    // 1+2: stream packed planes from host memory, rebuild bf16 into LDS.
+    uint32_t g = threadIdx.x;
+    for (; g + 3 * kDecThreads < groups; g += 4 * kDecThreads) {
+      u32x4 s[4];
+      u32x2 c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s[u] = __builtin_nontemporal_load(sm16 + g + u * kDecThreads);
+        c[u] = __builtin_nontemporal_load(cd8 + g + u * kDecThreads);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        uint32_t gg = g + u * kDecThreads;
+        u32x2 a0 = dec4(s[u][0], c[u][0], base), a1 = dec4(s[u][1], c[u][0] >> 16, base);
+        u32x2 a2 = dec4(s[u][2], c[u][1], base), a3 = dec4(s[u][3], c[u][1] >> 16, base);
+        tile[2 * gg] = u32x4{a0[0], a0[1], a1[0], a1[1]};
+        tile[2 * gg + 1] = u32x4{a2[0], a2[1], a3[0], a3[1]};
+      }
+    }
+    for (; g < groups; g += kDecThreads) {
+      u32x4 s = __builtin_nontemporal_load(sm16 + g);
+      u32x2 c = __builtin_nontemporal_load(cd8 + g);
+      u32x2 a0 = dec4(s[0], c[0], base), a1 = dec4(s[1], c[0] >> 16, base);
+      u32x2 a2 = dec4(s[2], c[1], base), a3 = dec4(s[3], c[1] >> 16, base);
+      tile[2 * g] = u32x4{a0[0], a0[1], a1[0], a1[1]};
+      tile[2 * g + 1] = u32x4{a2[0], a2[1], a3[0], a3[1]};
+    }
+    __syncthreads();
+    // 3: patch escaped values (rare) in LDS.
+    const Bf12Exception* exc =
+        reinterpret_cast<const Bf12Exception*>(src + kBf12HeaderBytes + d.n_values + d.n_values / 2);
+    uint16_t* t16 = reinterpret_cast<uint16_t*>(tile);
+    for (uint32_t k = s_e0 + threadIdx.x; k < s_e1; k += kDecThreads) {
+      Bf12Exception ex = exc[k];
+      t16[ex.index - lo] = ex.bits;
+    }
+    __syncthreads();
+    // 4: coalesced write of the finished tile to HBM.
+    u32x4* dst = reinterpret_cast<u32x4*>(d.dst + (uint64_t)lo * 2);
+    for (uint32_t q = threadIdx.x; q < cnt / 8; q += kDecThreads) __builtin_nontemporal_store(tile[q], dst + q);
+    __syncthreads();
+  }
+}
+
+hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgroups, hipStream_t s) {
+  uint64_t total = inl.item_start[n];
+  if (n == 0 || total == 0) return hipSuccess;
+  uint32_t grid = (uint32_t)(total < workgroups ? total : workgroups);
+  hipLaunchKernelGGL(k_bf12_decode, dim3(grid), dim3(kDecThreads), 0, s, inl, n, total);
+  return hipGetLastError();
+}
+
+}  // namespace ogkm

@@ -8,6 +8,7 @@
 
 #include <cstring>
 
+#include "ogkm/codec.hpp"
 #include "ogkm/kernels.hpp"
 #include "ogkm/lock_order.hpp"
 #include "ogkm/runtime.hpp"
@@ -365,6 +366,7 @@ PYBIND11_MODULE(_ogkm, m) {
       py::dict e = loc_dict(ri.resident_on[i]);
       e["pages"] = ri.pages[i];
       e["chunk"] = ri.chunk[i];
+      if (i < ri.enc_bytes.size() && ri.enc_bytes[i]) e["encoded_bytes"] = ri.enc_bytes[i];
       res.append(e);
     }
     d["resident_on"] = res;
@@ -542,6 +544,19 @@ PYBIND11_MODULE(_ogkm, m) {
     std::vector<uint32_t> out;
     for (uint32_t p = h.next_set(0); p < kPagesPerBlock; p = h.next_set(p + 1)) out.push_back(p);
     return out;
+  });
+  m.def("bf12_encode", [](py::bytes raw) {
+    std::string s = raw;
+    std::string out(kBlockSize + kBf12HeaderBytes, '\0');
+    uint64_t n = bf12_encode((const uint16_t*)s.data(), (uint32_t)(s.size() / 2), (uint8_t*)out.data(), out.size());
+    out.resize(n);
+    return py::bytes(out);
+  });
+  m.def("bf12_decode", [](py::bytes enc, uint32_t n_values) {
+    std::string s = enc;
+    std::string out((size_t)n_values * 2, '\0');
+    if (!bf12_decode((const uint8_t*)s.data(), (uint16_t*)out.data(), n_values)) throw StatusError("bf12_decode: bad block");
+    return py::bytes(out);
   });
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;

@@ -100,7 +100,8 @@ class LayerLayout:
 class TieredLlama:
     def __init__(self, cfg: LlamaConfig, batch: int, context: int, max_new_tokens: int = 64, oversub: float = 2.0,
                  device: int = 0, tp_rank: int = 0, tp_world: int = 1, seed: int = 0, lookahead: int = 2,
-                 hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False):
+                 hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
+                 packed: bool = True):
         assert cfg.n_heads % tp_world == 0 and cfg.n_kv_heads % tp_world == 0 and cfg.ffn_dim % tp_world == 0
         assert cfg.vocab % tp_world == 0
         self.cfg, self.B, self.ctx = cfg, batch, context
@@ -152,16 +153,19 @@ class TieredLlama:
         self.embed.set_accessed_by(device)
         self.kv = rt.malloc_managed(self.kv_bytes, "kv")
         self.kv.set_preferred_location(gpu)
+        # Streamed tensors keep a BF12-packed (lossless) host copy: the H2D copy
+        # kernel decodes it on the fly, so ~25% fewer bytes cross PCIe per step.
+        self.packed = packed
         self.layers = []
         for i in range(cfg.n_layers):
-            b = rt.malloc_managed(self.layer_bytes, f"layer{i}")
+            b = rt.malloc_managed(self.layer_bytes, f"layer{i}", packed_bf16=packed and not self.resident[i])
             if self.resident[i]:
                 b.set_preferred_location(gpu)
             else:
                 b.set_preferred_location(host)
                 b.set_read_mostly(True)
             self.layers.append(b)
-        self.head = rt.malloc_managed(self.head_bytes, "lm_head")
+        self.head = rt.malloc_managed(self.head_bytes, "lm_head", packed_bf16=packed and not self.head_resident)
         if self.head_resident:
             self.head.set_preferred_location(gpu)
         else:
@@ -206,6 +210,7 @@ class TieredLlama:
             "layer_gb": self.layer_bytes / 1e9, "resident_layers": sum(self.resident),
             "streamed_layers": self.cfg.n_layers - sum(self.resident), "head_resident": self.head_resident,
             "streamed_gb_per_step": self.streamed_bytes / 1e9, "init_s": getattr(self, "init_seconds", None),
+            "packed_host_copies": getattr(self, "packed", False),
         }
         if self.verbose and self.rank == 0:
             print("[ogkm] plan:", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}, flush=True)

@@ -44,6 +44,7 @@ CPU = 32  # processor id of the CPU (GPUs are 0..31)
 
 RANGE_STABLE_VA = 1
 RANGE_NO_CPU_VIEW = 2
+RANGE_PACKED_BF16 = 4
 
 _TIERS = {"gpu": 0, "hbm": 0, "host": 1, "cpu": 1, "cxl": 2}
 
@@ -329,8 +330,12 @@ class ManagedBuffer:
 
 
 def malloc_managed(nbytes: int, name: str = "", stable_va: bool = False, device: int = 0,
-                   cpu_view: bool = True) -> ManagedBuffer:
-    flags = (RANGE_STABLE_VA if stable_va else 0) | (0 if cpu_view else RANGE_NO_CPU_VIEW)
+                   cpu_view: bool = True, packed_bf16: bool = False) -> ManagedBuffer:
+    """``packed_bf16``: the contents are bf16 and read-only on GPUs; host / CXL
+    copies are stored BF12-packed (lossless, ~0.75x) and decoded by the H2D copy
+    kernel, cutting PCIe bytes for streamed weights. Implies no CPU view."""
+    flags = ((RANGE_STABLE_VA if stable_va else 0) | (0 if cpu_view else RANGE_NO_CPU_VIEW)
+             | (RANGE_PACKED_BF16 if packed_bf16 else 0))
     return ManagedBuffer(lib.malloc_managed(int(nbytes), flags, name, device))
 
 

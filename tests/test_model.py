@@ -48,9 +48,11 @@ def test_streaming_matches_plan(fake_rt):
     for _ in range(steps):
         tok = m.step(tok)
     s = lib.stats()
-    per_step = s["bytes_xfer_htd"] / steps
-    # every streamed tensor crosses the link once per step (+/- the wrap-around prefetch)
+    per_step = s["decoded_bytes"] / steps
+    # every streamed tensor is delivered once per step (+/- the wrap-around prefetch)
     assert 0.9 * m.streamed_bytes <= per_step <= 1.15 * m.streamed_bytes, (per_step, m.streamed_bytes)
+    # ... while only the BF12-packed bytes cross the link (lossless, ~0.75x)
+    assert s["bytes_xfer_htd"] < 0.8 * s["decoded_bytes"]
     assert s["bytes_xfer_dth"] == 0  # streamed weights are clean read-duplicates: never written back
     m.close()
 

@@ -1,13 +1,17 @@
 #!/bin/bash
-# One GPU session: smoke, 8B + 70B benches, and a rocprofv3 kernel-trace of the 8B decode.
+# One GPU session: GPU tests, smoke, and the 70B bench (packed + raw host copies),
+# with a rocprofv3 kernel trace of the packed run. Every GPU step has its own
+# time limit and the chain stops at the first failure.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$(pwd)
+timeout -k 10 600 python -m pytest tests -m gpu -q -rA > gpurun_out/gpu_tests.log 2>&1; rc=$?
+tail -25 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || { echo GPU_TESTS_FAIL; exit 1; }
 timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -30 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
-timeout -k 10 300 python bench.py --model llama3-8b --steps 4 --warmup 2 --verbose > gpurun_out/bench8b.log 2>&1 || { echo B8_FAIL; tail -30 gpurun_out/bench8b.log; exit 1; }
-tail -1 gpurun_out/bench8b.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof8b -o k -- python $R/bench.py --model llama3-8b --steps 3 --warmup 1 --no-aux > gpurun_out/prof8b.log 2>&1 || { echo PROF_FAIL; tail -30 gpurun_out/prof8b.log; exit 1; }
-timeout -k 10 700 python bench.py --steps 4 --warmup 2 --verbose > gpurun_out/bench70b.log 2>&1 || { echo B70_FAIL; tail -30 gpurun_out/bench70b.log; exit 1; }
-tail -1 gpurun_out/bench70b.log
+timeout -k 10 700 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof70b -o k -- python $R/bench.py --steps 4 --warmup 2 --verbose > gpurun_out/bench70b.log 2>&1 || { echo B70_FAIL; tail -30 gpurun_out/bench70b.log; exit 1; }
+grep '^{' gpurun_out/bench70b.log
+timeout -k 10 600 python bench.py --steps 4 --warmup 2 --no-packed --no-aux > gpurun_out/bench70b_raw.log 2>&1 || { echo B70RAW_FAIL; tail -30 gpurun_out/bench70b_raw.log; exit 1; }
+grep '^{' gpurun_out/bench70b_raw.log
