@@ -220,8 +220,8 @@ class HipBackend : public Backend {
   }
 
   Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s) override {
-    uint32_t wgs = (uint32_t)config().copy_workgroups * 2;
-    if (wgs == 0) wgs = 128;
+    uint32_t wgs = (uint32_t)config().decode_workgroups;
+    if (wgs == 0) wgs = 256;
     for (size_t base = 0; base < n; base += kInlineDescs) {
       size_t cnt = n - base < (size_t)kInlineDescs ? n - base : (size_t)kInlineDescs;
       KBf12Descs inl;

@@ -1279,6 +1279,8 @@ size_t Runtime::poll_device_faults(int dev) {
   if (dev < 0 || dev >= ndev()) return 0;
   DeviceFaultBuffer& fb = devs_[dev]->fault_buf;
   if (!fb.put) return 0;
+  static std::mutex poll_m;  // the service thread and API callers drain one at a time
+  std::unique_lock<std::mutex> pg(poll_m);
   uint32_t put = __atomic_load_n(fb.put, __ATOMIC_ACQUIRE);
   uint32_t n = std::min(put, fb.entries);
   if (put > fb.entries) {
@@ -1302,6 +1304,7 @@ size_t Runtime::poll_device_faults(int dev) {
     faults.push_back(f);
   }
   __atomic_store_n(fb.put, 0u, __ATOMIC_RELEASE);
+  pg.unlock();
   // Access counters (uvm_gpu_access_counters.c:1617): migrate hot remote blocks.
   int64_t mig = config().perf_access_counter_migration_enable;
   if (!remote_hits.empty()) {

@@ -68,6 +68,7 @@ void Runtime::shutdown() {
 }
 
 Runtime::~Runtime() {
+  stop_fault_service();
   for (auto& d : devs_)
     for (auto& r : d->rings)
       if (r) r->submit();
@@ -863,6 +864,41 @@ Status Runtime::enable_peer(int a, int b) {
 }
 
 void Runtime::set_prefetch_enabled(bool on) { config().perf_prefetch_enable = on ? 1 : 0; }
+
+// ------------------------------------------------------------------ fault service threads
+Status Runtime::start_fault_service(uint32_t poll_us) {
+  std::lock_guard<std::mutex> g(fs_m_);
+  if (!fs_threads_.empty()) return Status::OK;
+  fs_stop_.store(false);
+  for (int d = 0; d < ndev(); ++d) {
+    fs_threads_.emplace_back([this, d, poll_us] {
+      DeviceFaultBuffer& fb = devs_[d]->fault_buf;
+      while (!fs_stop_.load(std::memory_order_acquire)) {
+        // Top half: cheap check of the device-written put index.
+        uint32_t put = fb.put ? __atomic_load_n(fb.put, __ATOMIC_ACQUIRE) : 0;
+        if (put == 0) {
+          std::this_thread::sleep_for(std::chrono::microseconds(poll_us ? poll_us : 50));
+          continue;
+        }
+        // Bottom half: fetch + coalesce + service the batch.
+        if (global_status() != Status::OK || quiesced_.load()) {
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+          continue;
+        }
+        poll_device_faults(d);
+        fs_batches_.fetch_add(1, std::memory_order_relaxed);
+      }
+    });
+  }
+  return Status::OK;
+}
+
+void Runtime::stop_fault_service() {
+  std::lock_guard<std::mutex> g(fs_m_);
+  fs_stop_.store(true);
+  for (auto& t : fs_threads_) t.join();
+  fs_threads_.clear();
+}
 
 // ------------------------------------------------------------------ CXL DMA
 Status Runtime::cxl_dma(uint64_t handle, uint64_t gpu_ptr, int dev, uint64_t cxl_off, uint64_t size, int dir,

@@ -59,6 +59,7 @@ namespace ogkm {
   X(copy_engine, 0, "0=HIP copy kernels 1=SDMA (hipMemcpyAsync) comparator")                         \
   X(copy_workgroups, 64, "workgroups per copy-kernel launch (CU budget for migration)")              \
   X(copy_piece_kb, 64, "bytes per copy work item (KB)")                                              \
+  X(decode_workgroups, 256, "workgroups per fused copy+BF12-decode launch")                           \
   X(peer_copy, 1, "0=phys 1=virt peer addressing")                                                   \
   /* misc UVM knobs */                                                                               \
   X(fault_force_sysmem, 0, "always service faults in system memory")                                 \

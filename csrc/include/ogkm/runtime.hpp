@@ -201,6 +201,14 @@ class Runtime {
   // ---- peers
   Status enable_peer(int a, int b);
 
+  // ---- fault service threads (ISR top half + bottom half analog,
+  // uvm_gpu_isr.c:86-119,218-280,598-700): one host thread per GPU polls the
+  // device fault buffer's put index and services batches (faults + access
+  // counter notifications) without any caller involvement.
+  Status start_fault_service(uint32_t poll_us);
+  void stop_fault_service();
+  uint64_t fault_service_batches() const { return fs_batches_.load(); }
+
   // ---- perf modules
   void set_prefetch_enabled(bool on);
   // internal helpers used by engine files
@@ -247,6 +255,10 @@ class Runtime {
   std::mutex dev_tables_m_;
   std::unordered_map<uint64_t, std::pair<Ring*, uint64_t>> cxl_pending_;
   std::mutex cxl_m_;
+  std::vector<std::thread> fs_threads_;
+  std::atomic<bool> fs_stop_{false};
+  std::atomic<uint64_t> fs_batches_{0};
+  std::mutex fs_m_;
   OrderedMutex pm_{LockOrder::GLOBAL_PM};
 };
 

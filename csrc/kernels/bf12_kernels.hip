@@ -71,42 +71,44 @@ __global__ void __launch_bounds__(kDecThreads)
     const uint32_t cnt = d.n_values - lo < kBf12Tile ? d.n_values - lo : kBf12Tile;
     const uint32_t base = s_base;
     const uint8_t* src = reinterpret_cast<const uint8_t*>(d.src);
-    const u32x4* sm16 = reinterpret_cast<const u32x4*>(src + kBf12HeaderBytes + lo);
-    const u32x2* cd8 = reinterpret_cast<const u32x2*>(src + kBf12HeaderBytes + d.n_values + lo / 2);
-    const uint32_t groups = cnt / 16;  // 16 values per lane-iteration
-    // 1+2: stream packed planes from host memory, rebuild bf16 into LDS.
-    uint32_t g = threadIdx.x;
-    for (; g + 3 * kDecThreads < groups; g += 4 * kDecThreads) {
-      u32x4 s[4];
-      u32x2 c[4];
+    // 8 values per lane-group: 8 B of sign|mantissa + 4 B of codes -> 16 B of bf16,
+    // so consecutive lanes write consecutive 16-B LDS slots (conflict-free).
+    const u32x2* sm8 = reinterpret_cast<const u32x2*>(src + kBf12HeaderBytes + lo);
+    const uint32_t* cd4 = reinterpret_cast<const uint32_t*>(src + kBf12HeaderBytes + d.n_values + lo / 2);
+    const uint32_t groups = cnt / 8;  // <= 4096 -> 16 per thread
+    const Bf12Exception* exc =
+        reinterpret_cast<const Bf12Exception*>(src + kBf12HeaderBytes + d.n_values + d.n_values / 2);
+    const uint32_t e0 = s_e0, e1 = s_e1;
+    // 1: issue every load of the tile (and this lane's first exception) before
+    //    using any of it: 48 KB per workgroup in flight across PCIe.
+    constexpr int kPer = kBf12Tile / 8 / kDecThreads;  // 16
+    u32x2 s[kPer];
+    uint32_t c[kPer];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        s[u] = __builtin_nontemporal_load(sm16 + g + u * kDecThreads);
-        c[u] = __builtin_nontemporal_load(cd8 + g + u * kDecThreads);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        uint32_t gg = g + u * kDecThreads;
-        u32x2 a0 = dec4(s[u][0], c[u][0], base), a1 = dec4(s[u][1], c[u][0] >> 16, base);
-        u32x2 a2 = dec4(s[u][2], c[u][1], base), a3 = dec4(s[u][3], c[u][1] >> 16, base);
-        tile[2 * gg] = u32x4{a0[0], a0[1], a1[0], a1[1]};
-        tile[2 * gg + 1] = u32x4{a2[0], a2[1], a3[0], a3[1]};
+    for (int u = 0; u < kPer; ++u) {
+      uint32_t g = threadIdx.x + u * kDecThreads;
+      if (g < groups) {
+        s[u] = __builtin_nontemporal_load(sm8 + g);
+        c[u] = __builtin_nontemporal_load(cd4 + g);
       }
     }
-    for (; g < groups; g += kDecThreads) {
-      u32x4 s = __builtin_nontemporal_load(sm16 + g);
-      u32x2 c = __builtin_nontemporal_load(cd8 + g);
-      u32x2 a0 = dec4(s[0], c[0], base), a1 = dec4(s[1], c[0] >> 16, base);
-      u32x2 a2 = dec4(s[2], c[1], base), a3 = dec4(s[3], c[1] >> 16, base);
-      tile[2 * g] = u32x4{a0[0], a0[1], a1[0], a1[1]};
-      tile[2 * g + 1] = u32x4{a2[0], a2[1], a3[0], a3[1]};
+    const bool has_ex = e0 + threadIdx.x < e1;
+    Bf12Exception ex0 = {0, 0, 0};
+    if (has_ex) ex0 = exc[e0 + threadIdx.x];
+    // 2: rebuild bf16 words into the LDS staging tile.
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      uint32_t g = threadIdx.x + u * kDecThreads;
+      if (g < groups) {
+        u32x2 a0 = dec4(s[u][0], c[u], base), a1 = dec4(s[u][1], c[u] >> 16, base);
+        tile[g] = u32x4{a0[0], a0[1], a1[0], a1[1]};
+      }
     }
     __syncthreads();
     // 3: patch escaped values (rare) in LDS.
-    const Bf12Exception* exc =
-        reinterpret_cast<const Bf12Exception*>(src + kBf12HeaderBytes + d.n_values + d.n_values / 2);
     uint16_t* t16 = reinterpret_cast<uint16_t*>(tile);
-    for (uint32_t k = s_e0 + threadIdx.x; k < s_e1; k += kDecThreads) {
+    if (has_ex) t16[ex0.index - lo] = ex0.bits;
+    for (uint32_t k = e0 + threadIdx.x + kDecThreads; k < e1; k += kDecThreads) {
       Bf12Exception ex = exc[k];
       t16[ex.index - lo] = ex.bits;
     }

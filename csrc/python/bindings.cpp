@@ -318,6 +318,13 @@ PYBIND11_MODULE(_ogkm, m) {
     py::gil_scoped_release nogil;
     return rt()->poll_device_faults(dev);
   });
+  m.def("start_fault_service", [](uint32_t poll_us) { check(rt()->start_fault_service(poll_us), "start_fault_service"); },
+        py::arg("poll_us") = 50);
+  m.def("stop_fault_service", [] {
+    py::gil_scoped_release nogil;
+    rt()->stop_fault_service();
+  });
+  m.def("fault_service_batches", [] { return rt()->fault_service_batches(); });
   m.def("device_table", [](uint64_t id) {
     DeviceResidencyTable* t;
     check(rt()->device_table(range(id), &t), "device_table");
