@@ -7,9 +7,9 @@
 namespace ogkm {
 
 const char* lock_order_name(LockOrder o) {
-  static const char* n[] = {"GLOBAL_PM", "GLOBAL",     "VA_SPACE",    "CXL_REGISTRY", "RANGE_GROUP",
-                            "VA_BLOCK",  "PERF",       "HBM_ARENA",   "HOST_ARENA",   "STREAM_POOL",
-                            "RING",      "TOOLS",      "LEAF"};
+  static const char* n[] = {"GLOBAL_PM",  "GLOBAL",    "VA_SPACE",   "CXL_REGISTRY", "RANGE_GROUP",
+                            "RANGE_PLACE", "VA_BLOCK", "PERF",       "HBM_ARENA",    "HOST_ARENA",
+                            "STREAM_POOL", "RING",     "TOOLS",      "LEAF"};
   int i = (int)o;
   return i >= 0 && i < (int)LockOrder::COUNT ? n[i] : "?";
 }

@@ -340,6 +340,13 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
     if (dst.is_gpu()) read_dup = true;
   }
   c.cause = cause;
+  if (!read_dup && b->lease_pins) {
+    // A leased device pointer cannot be revoked under the holder: migrating
+    // these pages away from a pinned copy must wait for the lease to end.
+    for (auto& r : b->res)
+      if (!(r.loc == dst) && r.chunk >= 0 && r.resident.intersects(pages) && r.arena->pinned((uint32_t)r.chunk))
+        return Status::BUSY;
+  }
   Residency* to = nullptr;
   int64_t hint = -1;
   // Keep a range's blocks adjacent in the destination arena.
@@ -757,6 +764,8 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
     uint32_t p0 = (uint32_t)(lo >> kPageShift), p1 = (uint32_t)((hi + kPageSize - 1) >> kPageShift);
     return PageMask::range(p0, p1 - p0);
   };
+  // Concurrent acquires of one range must agree on one extent.
+  std::lock_guard<OrderedMutex> placement(r->place_lock);
   Ctx c;
   c.cause = cause;
   Status st = Status::OK;
@@ -794,7 +803,9 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
       {
         std::lock_guard<OrderedMutex> g(b->lock);
         Residency* x = b->find(dst);
-        if (x && x->chunk != (int64_t)target) {
+        if (x && x->chunk != (int64_t)target && b->lease_pins) {
+          st = Status::BUSY;  // another lease pins this block's chunk: it cannot move
+        } else if (x && x->chunk != (int64_t)target) {
           // Relocate: copy the resident pages into the new extent (D2D).
           ga->set_owner(target, b);
           Residency tmp;
@@ -930,6 +941,8 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
         dec[k].dst = dst;
         dec[k].read_dup = true;
       }
+      // Readers never revoke another processor's leased copy: duplicate instead.
+      if (access == Access::READ && b->lease_pins) dec[k].read_dup = true;
       if (!dec[k].map_remote) all_remote = false;
     }
     Ctx c;

@@ -21,15 +21,16 @@ enum class LockOrder : int {
   VA_SPACE = 2,    // range tree (reader/writer)
   CXL_REGISTRY = 3,
   RANGE_GROUP = 4,
-  VA_BLOCK = 5,    // per 2 MB block state
-  PERF = 6,        // thrashing / prefetch / access-counter state
-  HBM_ARENA = 7,   // per-GPU chunk allocator (taken under a block lock)
-  HOST_ARENA = 8,
-  STREAM_POOL = 9,
-  RING = 10,       // SQ/CQ ring
-  TOOLS = 11,      // event queues
-  LEAF = 12,
-  COUNT = 13
+  RANGE_PLACE = 5, // per-range GPU extent placement (serialises concurrent acquires of one range)
+  VA_BLOCK = 6,    // per 2 MB block state
+  PERF = 7,        // thrashing / prefetch / access-counter state
+  HBM_ARENA = 8,   // per-GPU chunk allocator (taken under a block lock)
+  HOST_ARENA = 9,
+  STREAM_POOL = 10,
+  RING = 11,       // SQ/CQ ring
+  TOOLS = 12,      // event queues
+  LEAF = 13,
+  COUNT = 14
 };
 const char* lock_order_name(LockOrder o);
 

@@ -15,6 +15,7 @@
 //   * errors are sticky per ring and propagate to the runtime's fatal status.
 #pragma once
 
+#include <atomic>
 #include <deque>
 #include <string>
 #include <vector>
@@ -94,10 +95,10 @@ class Ring {
   std::deque<std::pair<uint64_t, Sqe>> sq_;   // pushed, not yet submitted
   std::deque<std::pair<uint64_t, Cqe>> inflight_;  // submitted, not yet reaped
   uint64_t next_seq_ = 1;
-  uint64_t submitted_ = 0;
+  std::atomic<uint64_t> submitted_{0};  // read lock-free by wait_seq
   uint64_t batches_ = 0;
   FenceRef last_fence_;
-  Status err_ = Status::OK;
+  std::atomic<Status> err_{Status::OK};
   std::string err_desc_;
 };
 

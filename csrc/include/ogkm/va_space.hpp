@@ -140,6 +140,7 @@ class Range {
   std::vector<std::unique_ptr<Block>> blocks;
   std::atomic<int64_t> views{0};  // live tensor views / leases
   bool destroyed = false;
+  OrderedMutex place_lock{LockOrder::RANGE_PLACE};  // GPU extent placement
 
   uint64_t addr() const { return (uint64_t)cpu_view; }
   Block* block(uint64_t i) { return i < blocks.size() ? blocks[i].get() : nullptr; }
