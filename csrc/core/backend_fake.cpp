@@ -102,17 +102,38 @@ class FakeBackend : public Backend {
   }
   Status set_device(int) override { return Status::OK; }
 
+  // Fake HBM is a shared memfd mapping, so an allocation can be exported as a
+  // file descriptor (the dma-buf stand-in) and opened by another process.
   Status hbm_alloc(int dev, size_t bytes, void** p) override {
     if (dev < 0 || dev >= ndev_) return Status::INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(m_);
     if (used_[dev] + bytes > hbm_) return Status::NO_MEMORY;
-    void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    if (m == MAP_FAILED) return Status::NO_MEMORY;
+    int fd = memfd_create("ogkm-fake-hbm", MFD_CLOEXEC);
+    if (fd < 0) return Status::NO_MEMORY;
+    if (ftruncate(fd, bytes) != 0) {
+      close(fd);
+      return Status::NO_MEMORY;
+    }
+    void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_NORESERVE, fd, 0);
+    if (m == MAP_FAILED) {
+      close(fd);
+      return Status::NO_MEMORY;
+    }
     used_[dev] += bytes;
+    allocs_[(uint64_t)m] = FakeAlloc{fd, bytes, dev};
     *p = m;
     return Status::OK;
   }
   void hbm_free(int dev, void* p, size_t bytes) override {
-    if (p) munmap(p, bytes);
+    std::lock_guard<std::mutex> g(m_);
+    if (p) {
+      munmap(p, bytes);
+      auto it = allocs_.find((uint64_t)p);
+      if (it != allocs_.end()) {
+        close(it->second.fd);
+        allocs_.erase(it);
+      }
+    }
     if (dev >= 0 && dev < ndev_) used_[dev] -= bytes;
   }
 
@@ -273,27 +294,73 @@ class FakeBackend : public Backend {
   bool can_access_peer(int a, int b) override { return a != b && a < ndev_ && b < ndev_; }
   Status enable_peer(int a, int b) override { return can_access_peer(a, b) ? Status::OK : Status::NOT_SUPPORTED; }
 
-  Status export_dmabuf(void*, size_t, int*, uint64_t*) override { return Status::NOT_SUPPORTED; }
+  Status export_dmabuf(void* p, size_t bytes, int* fd, uint64_t* off) override {
+    std::lock_guard<std::mutex> g(m_);
+    const FakeAlloc* a = containing((uint64_t)p, bytes, off);
+    if (!a) return Status::INVALID_ARGUMENT;
+    *fd = fcntl(a->fd, F_DUPFD_CLOEXEC, 0);
+    return *fd < 0 ? Status::IO_ERROR : Status::OK;
+  }
+  // Handle = "fake:<pid>:<fd>:<offset>:<alloc bytes>"; another process opens the
+  // allocation's memfd through /proc/<pid>/fd (hipIpcGetMemHandle analog).
   Status ipc_handle(void* p, std::string* h) override {
-    char b[32];
-    snprintf(b, sizeof b, "fake:%llx", (unsigned long long)(uintptr_t)p);
+    std::lock_guard<std::mutex> g(m_);
+    uint64_t off = 0;
+    const FakeAlloc* a = containing((uint64_t)p, 1, &off);
+    if (!a) return Status::INVALID_ARGUMENT;
+    char b[96];
+    snprintf(b, sizeof b, "fake:%d:%d:%llu:%llu", (int)getpid(), a->fd, (unsigned long long)off,
+             (unsigned long long)a->bytes);
     *h = b;
     return Status::OK;
   }
   Status ipc_open(const std::string& h, void** p) override {
-    if (h.rfind("fake:", 0) != 0) return Status::INVALID_ARGUMENT;
-    *p = (void*)(uintptr_t)strtoull(h.c_str() + 5, nullptr, 16);
+    int pid = 0, fd = -1;
+    unsigned long long off = 0, bytes = 0;
+    if (sscanf(h.c_str(), "fake:%d:%d:%llu:%llu", &pid, &fd, &off, &bytes) != 4 || off >= bytes)
+      return Status::INVALID_ARGUMENT;
+    char path[64];
+    snprintf(path, sizeof path, "/proc/%d/fd/%d", pid, fd);
+    int lfd = open(path, O_RDWR | O_CLOEXEC);
+    if (lfd < 0) return Status::NOT_FOUND;
+    void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, lfd, 0);
+    close(lfd);
+    if (m == MAP_FAILED) return Status::NO_MEMORY;
+    std::lock_guard<std::mutex> g(m_);
+    opened_[(uint64_t)m + off] = {(uint64_t)m, (size_t)bytes};
+    *p = (char*)m + off;
     return Status::OK;
   }
-  void ipc_close(void*) override {}
+  void ipc_close(void* p) override {
+    std::lock_guard<std::mutex> g(m_);
+    auto it = opened_.find((uint64_t)p);
+    if (it == opened_.end()) return;
+    munmap((void*)it->second.first, it->second.second);
+    opened_.erase(it);
+  }
 
  private:
+  struct FakeAlloc {
+    int fd;
+    size_t bytes;
+    int dev;
+  };
+  const FakeAlloc* containing(uint64_t p, size_t bytes, uint64_t* off) const {
+    auto it = allocs_.upper_bound(p);
+    if (it == allocs_.begin()) return nullptr;
+    --it;
+    if (p + bytes > it->first + it->second.bytes) return nullptr;
+    *off = p - it->first;
+    return &it->second;
+  }
   int ndev_;
   size_t hbm_;
   std::vector<size_t> used_;
   std::mutex m_;
   std::map<uint64_t, std::pair<int, size_t>> handles_;
   std::map<void*, size_t> coherent_;
+  std::map<uint64_t, FakeAlloc> allocs_;                        // base -> memfd
+  std::map<uint64_t, std::pair<uint64_t, size_t>> opened_;      // ipc ptr -> (map base, bytes)
 };
 
 }  // namespace

@@ -297,20 +297,44 @@ class HipBackend : public Backend {
     }
     return Status::OK;
   }
+  // Handle = hipIpcMemHandle_t of the containing allocation + 8-byte offset of
+  // `p` inside it (arena chunks live inside one slab allocation).
   Status ipc_handle(void* p, std::string* h) override {
     hipIpcMemHandle_t hh;
-    HIPCHK(hipIpcGetMemHandle(&hh, p));
+    void* base = nullptr;
+    size_t len = 0;
+    HIPCHK(hipMemGetAddressRange(&base, &len, p));
+    HIPCHK(hipIpcGetMemHandle(&hh, base));
+    uint64_t off = (uint64_t)((char*)p - (char*)base);
     h->assign(reinterpret_cast<const char*>(&hh), sizeof hh);
+    h->append(reinterpret_cast<const char*>(&off), sizeof off);
     return Status::OK;
   }
   Status ipc_open(const std::string& h, void** p) override {
-    if (h.size() != sizeof(hipIpcMemHandle_t)) return Status::INVALID_ARGUMENT;
+    if (h.size() != sizeof(hipIpcMemHandle_t) + sizeof(uint64_t)) return Status::INVALID_ARGUMENT;
     hipIpcMemHandle_t hh;
+    uint64_t off = 0;
     memcpy(&hh, h.data(), sizeof hh);
-    HIPCHK(hipIpcOpenMemHandle(p, hh, hipIpcMemLazyEnablePeerAccess));
+    memcpy(&off, h.data() + sizeof hh, sizeof off);
+    void* base = nullptr;
+    HIPCHK(hipIpcOpenMemHandle(&base, hh, hipIpcMemLazyEnablePeerAccess));
+    *p = (char*)base + off;
+    std::lock_guard<std::mutex> g(ev_m_);
+    ipc_base_[*p] = base;
     return Status::OK;
   }
-  void ipc_close(void* p) override { (void)hipIpcCloseMemHandle(p); }
+  void ipc_close(void* p) override {
+    void* base = p;
+    {
+      std::lock_guard<std::mutex> g(ev_m_);
+      auto it = ipc_base_.find(p);
+      if (it != ipc_base_.end()) {
+        base = it->second;
+        ipc_base_.erase(it);
+      }
+    }
+    (void)hipIpcCloseMemHandle(base);
+  }
   std::string last_error() override { return last_err_; }
 
  private:
@@ -336,6 +360,7 @@ class HipBackend : public Backend {
   std::mutex ev_m_, df_m_;
   std::vector<void*> free_events_[64];
   std::map<void*, int> ev_dev_;
+  std::map<void*, void*> ipc_base_;  // opened IPC pointer -> mapped allocation base
   std::deque<std::pair<void*, void*>> deferred_;
   uint64_t launches_ = 0;
 };

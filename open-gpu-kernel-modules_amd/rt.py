@@ -224,6 +224,10 @@ class Lease:
 
 
 # --------------------------------------------------------------------------- managed buffers
+# Callables run with the buffer just before a range is freed (see p2p.py).
+_free_hooks: list = []
+
+
 class ManagedBuffer:
     """A managed allocation (one VA range of 2 MB blocks)."""
 
@@ -322,6 +326,10 @@ class ManagedBuffer:
 
     def free(self) -> None:
         if not self._freed:
+            # Importers of this memory (p2p regions) are told first, so their
+            # pins are dropped before the range goes away (peermem free callback).
+            for hook in list(_free_hooks):
+                hook(self)
             lib.free(self.id)
             self._freed = True
 
