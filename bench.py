@@ -17,6 +17,12 @@ streams only its shard over its own PCIe link.
 One step = one decode token for every sequence (weights streamed, KV appended,
 greedy sampling). ``value`` = global tokens/s = batch * K / max-over-ranks time.
 
+Weights rest losslessly packed (BF12, ~0.75x, bit-exact bf16 after unpack) in
+every tier and are unpacked into a bf16 staging buffer right before each layer
+runs; the oversubscription ratio and HBM budget are computed on the logical bf16
+footprint (weights + KV + embedding + head), and the staging buffer is carved out
+of that budget. ``--weights bf16`` runs the raw-weight path for comparison.
+
 Also reported (aux): HBM<->host and HBM<->CXL GB/s measured through the runtime's
 rings (the CXL pool is an emulated NUMA node when the box has no CXL device).
 
@@ -47,8 +53,11 @@ def parse():
     ap.add_argument("--oversub", type=float, default=2.0)
     ap.add_argument("--lookahead", type=int, default=2)
     ap.add_argument("--no-aux", action="store_true", help="skip the HBM<->host/CXL bandwidth probe")
+    ap.add_argument("--weights", choices=("bf12", "bf16"), default="bf12",
+                    help="bf12: weights rest losslessly packed in every tier (HBM included) and are unpacked "
+                         "per layer; bf16: raw weights")
     ap.add_argument("--no-packed", action="store_true",
-                    help="store streamed host copies as raw bf16 instead of lossless BF12")
+                    help="with --weights bf16: raw host copies instead of BF12 copies decoded in the H2D kernel")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -112,7 +121,8 @@ def main() -> None:
     t_init = time.perf_counter()
     model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 2,
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=world, seed=1234,
-                              lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed)
+                              lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
+                              weight_format=a.weights)
     plan = model.describe()
     init_s = time.perf_counter() - t_init
     g = torch.Generator(device="cpu").manual_seed(42)
@@ -156,7 +166,10 @@ def main() -> None:
                 "resident_layers": plan["resident_layers"],
                 "streamed_layers": plan["streamed_layers"],
                 "streamed_gb_per_step_per_gpu": round(plan["streamed_gb_per_step"], 2),
-                "host_copy_format": "bf12-lossless" if plan["packed_host_copies"] else "bf16",
+                "weight_format": plan["weight_format"],
+                "host_copy_format": ("bf12-lossless" if plan["packed_host_copies"] or plan["weight_format"] == "bf12"
+                                     else "bf16"),
+                "hbm_copy_format": "bf12-lossless (unpacked per layer)" if plan["weight_format"] == "bf12" else "bf16",
             },
             "aux": {
                 **aux,

@@ -244,11 +244,16 @@ class FakeBackend : public Backend {
     });
     return Status::OK;
   }
-  Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s) override {
+  Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s, uint32_t) override {
     std::vector<DecodeDesc> v(d, d + n);
     run(s, [v] {
       for (auto& x : v) bf12_decode((const uint8_t*)x.src, (uint16_t*)x.dst, x.n_values);
     });
+    return Status::OK;
+  }
+  Status unpack_bf12_stream(int, uint64_t src, uint64_t dst, uint32_t, uint32_t, uint64_t n, void* s,
+                            uint32_t) override {
+    run(s, [src, dst, n] { bf12_unpack((const uint8_t*)src, (uint16_t*)dst, n); });
     return Status::OK;
   }
   Status gather_pages(int, const PageListDesc& d, void* s) override {

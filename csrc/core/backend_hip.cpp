@@ -219,8 +219,8 @@ class HipBackend : public Backend {
     return Status::OK;
   }
 
-  Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s) override {
-    uint32_t wgs = (uint32_t)config().decode_workgroups;
+  Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s, uint32_t workgroups) override {
+    uint32_t wgs = workgroups ? workgroups : (uint32_t)config().decode_workgroups;
     if (wgs == 0) wgs = 256;
     for (size_t base = 0; base < n; base += kInlineDescs) {
       size_t cnt = n - base < (size_t)kInlineDescs ? n - base : (size_t)kInlineDescs;
@@ -235,6 +235,13 @@ class HipBackend : public Backend {
       HIPCHK(launch_bf12_decode(inl, (uint32_t)cnt, wgs, (hipStream_t)s));
       launches_++;
     }
+    return Status::OK;
+  }
+
+  Status unpack_bf12_stream(int, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values, uint64_t,
+                            void* s, uint32_t workgroups) override {
+    HIPCHK(launch_bf12_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s));
+    launches_++;
     return Status::OK;
   }
 

@@ -2,7 +2,9 @@
 // csrc/kernels/bf12_kernels.hip must produce bit-identical output).
 #include "ogkm/codec.hpp"
 
+#include <algorithm>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 namespace ogkm {
@@ -74,6 +76,71 @@ bool bf12_decode(const uint8_t* in, uint16_t* out, uint32_t n) {
     out[i] = (uint16_t)(((s & 0x80) << 8) | (((h.base + c) & 0xFF) << 7) | (s & 0x7F));
   }
   for (uint32_t k = 0; k < h.n_exc; ++k) out[exc[k].index] = exc[k].bits;
+  return true;
+}
+
+uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_t* out, uint64_t cap,
+                   unsigned threads) {
+  if (!n || chunk_values < 8192 || (chunk_values & (chunk_values - 1)) || chunk_values > kBf12Tile * kBf12MaxTiles)
+    return 0;
+  if (cap < bf12_pack_bound(n, chunk_values)) return 0;
+  const uint64_t nch = (n + chunk_values - 1) / chunk_values;
+  const uint64_t head = bf12_stream_head_bytes(nch);
+  const uint64_t slot = (uint64_t)chunk_values * 2 + 512;  // worst case per chunk
+  std::vector<Bf12StreamChunk> table(nch);
+  std::vector<uint64_t> bytes(nch);
+  // 1) every chunk encodes into its worst-case slot, in parallel
+  auto work = [&](uint64_t c0, uint64_t c1) {
+    for (uint64_t c = c0; c < c1; ++c) {
+      uint64_t lo = c * chunk_values;
+      uint32_t cnt = (uint32_t)std::min<uint64_t>(chunk_values, n - lo);
+      uint8_t* dst = out + head + c * slot;
+      uint64_t e = (cnt % 8 == 0) ? bf12_encode(in + lo, cnt, dst, (uint64_t)cnt * 2) : 0;
+      table[c].n_values = cnt;
+      table[c].encoded = e ? 1 : 0;
+      if (!e) {
+        memcpy(dst, in + lo, (size_t)cnt * 2);
+        e = (uint64_t)cnt * 2;
+      }
+      bytes[c] = e;
+    }
+  };
+  threads = std::max(1u, std::min<unsigned>(threads, (unsigned)nch));
+  std::vector<std::thread> th;
+  uint64_t per = (nch + threads - 1) / threads;
+  for (unsigned k = 0; k < threads; ++k) {
+    uint64_t c0 = k * per, c1 = std::min(nch, c0 + per);
+    if (c0 < c1) th.emplace_back(work, c0, c1);
+  }
+  for (auto& x : th) x.join();
+  // 2) compact left (destinations never pass their sources)
+  uint64_t off = head;
+  for (uint64_t c = 0; c < nch; ++c) {
+    uint64_t from = head + c * slot;
+    if (off != from) memmove(out + off, out + from, bytes[c]);
+    table[c].offset = off;
+    off = (off + bytes[c] + 255) & ~255ull;
+  }
+  Bf12StreamHeader h{kBf12StreamMagic, (uint32_t)nch, chunk_values, 0, n, off};
+  memset(out, 0, head);
+  memcpy(out, &h, sizeof h);
+  memcpy(out + sizeof h, table.data(), nch * sizeof(Bf12StreamChunk));
+  return off;
+}
+
+bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n) {
+  Bf12StreamHeader h;
+  memcpy(&h, stream, sizeof h);
+  if (h.magic != kBf12StreamMagic || h.n_values != n) return false;
+  const Bf12StreamChunk* t = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof h);
+  for (uint32_t c = 0; c < h.nchunks; ++c) {
+    uint16_t* dst = out + (uint64_t)c * h.chunk_values;
+    if (t[c].encoded) {
+      if (!bf12_decode(stream + t[c].offset, dst, t[c].n_values)) return false;
+    } else {
+      memcpy(dst, stream + t[c].offset, (size_t)t[c].n_values * 2);
+    }
+  }
   return true;
 }
 

@@ -90,6 +90,7 @@ Runtime::~Runtime() {
   for (auto& d : devs_) {
     for (auto& r : d->rings) r.reset();
     if (d->fault_buf.put) be_->host_free_coherent(d->fault_buf.put);
+    d->hbm_live.store(nullptr);
     d->hbm.reset();
   }
   host_arenas_.clear();
@@ -100,6 +101,7 @@ Status Runtime::init_device(int d, uint64_t budget) {
   if (d < 0 || d >= ndev()) return Status::INVALID_ARGUMENT;
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
   if (devs_[d]->hbm && devs_[d]->hbm->outstanding_bytes()) return Status::BUSY;
+  devs_[d]->hbm_live.store(nullptr);
   devs_[d]->hbm.reset();
   if (budget == 0) {
     size_t f = 0, t = 0;
@@ -107,6 +109,7 @@ Status Runtime::init_device(int d, uint64_t budget) {
     budget = config().hbm_budget_mb ? (uint64_t)config().hbm_budget_mb << 20 : f / 2;
   }
   devs_[d]->hbm = std::make_unique<HbmArena>(be_.get(), d, budget, (int)config().hbm_provider);
+  devs_[d]->hbm_live.store(devs_[d]->hbm.get(), std::memory_order_release);
   return devs_[d]->hbm->init_status();
 }
 
@@ -128,15 +131,19 @@ HostArena* Runtime::host_arena(Tier t, int node) {
 ChunkArena* Runtime::arena_for(const Loc& l) {
   if (l.is_gpu()) {
     if (l.id < 0 || l.id >= ndev()) return nullptr;
-    if (!devs_[l.id]->hbm) {
-      size_t f = 0, t = 0;
-      if (be_->device_mem_info(l.id, &f, &t) != Status::OK) return nullptr;
-      uint64_t budget = config().hbm_budget_mb ? (uint64_t)config().hbm_budget_mb << 20 : f / 2;
-      static std::mutex m;
-      std::lock_guard<std::mutex> g(m);
-      if (!devs_[l.id]->hbm) devs_[l.id]->hbm = std::make_unique<HbmArena>(be_.get(), l.id, budget, (int)config().hbm_provider);
+    Device& d = *devs_[l.id];
+    if (HbmArena* a = d.hbm_live.load(std::memory_order_acquire)) return a;
+    // First touch of a GPU: create its arena with the default budget (once).
+    size_t f = 0, t = 0;
+    if (be_->device_mem_info(l.id, &f, &t) != Status::OK) return nullptr;
+    uint64_t budget = config().hbm_budget_mb ? (uint64_t)config().hbm_budget_mb << 20 : f / 2;
+    static std::mutex m;
+    std::lock_guard<std::mutex> g(m);
+    if (!d.hbm) {
+      d.hbm = std::make_unique<HbmArena>(be_.get(), l.id, budget, (int)config().hbm_provider);
+      d.hbm_live.store(d.hbm.get(), std::memory_order_release);
     }
-    return devs_[l.id]->hbm.get();
+    return d.hbm.get();
   }
   if (l.tier == Tier::CXL && !cxl_topo_.is_cxl_node(l.id)) return nullptr;
   return host_arena(l.tier, l.id);

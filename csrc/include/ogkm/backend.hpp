@@ -92,7 +92,12 @@ class Backend {
   // engine: 0 = copy kernel with the PCIe CU budget, 1 = SDMA, 2 = copy kernel
   // with the whole chip (HBM<->HBM).
   virtual Status copy_batch(int dev, const CopyDesc* d, size_t n, void* stream, int engine) = 0;
-  virtual Status decode_bf12(int dev, const DecodeDesc* d, size_t n, void* stream) = 0;
+  // workgroups = 0: config().decode_workgroups (sized for H2D streaming); HBM->HBM
+  // unpacking passes a full-chip grid.
+  virtual Status decode_bf12(int dev, const DecodeDesc* d, size_t n, void* stream, uint32_t workgroups = 0) = 0;
+  // Unpack a device-resident BF12 stream (codec.hpp) of n_values into bf16 at dst.
+  virtual Status unpack_bf12_stream(int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
+                                    uint64_t n_values, void* stream, uint32_t workgroups) = 0;
   virtual Status gather_pages(int dev, const PageListDesc& d, void* stream) = 0;
   virtual Status scatter_pages(int dev, const PageListDesc& d, void* stream) = 0;
   virtual Status memset32(int dev, uint64_t dst, uint32_t pattern, size_t bytes, void* stream) = 0;

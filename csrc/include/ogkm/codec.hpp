@@ -22,6 +22,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 namespace ogkm {
 
@@ -55,5 +56,41 @@ inline uint64_t bf12_encoded_bytes(uint32_t n_values, uint32_t n_exc) {
 uint64_t bf12_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);
 // Decode an encoded block into n_values bf16.
 bool bf12_decode(const uint8_t* in, uint16_t* out, uint32_t n_values);
+
+// BF12 stream: a whole tensor kept packed in ANY tier, HBM included (the
+// weights of a tiered model stay packed where they rest and are unpacked into a
+// bf16 staging buffer right before use: k_bf12_unpack). The tensor is cut into
+// chunks of `chunk_values` (a power of two, 8 Ki .. 1 Mi values); each chunk is
+// a BF12 block, or raw bf16 when it does not compress / has a tail that is not
+// a multiple of 8. The stream is self-describing:
+//   [0, 32)            Bf12StreamHeader
+//   [32, 32 + 16 n)    Bf12StreamChunk table
+//   256-B aligned      chunk payloads (offsets are from the stream start)
+constexpr uint32_t kBf12StreamMagic = 0x31534642;  // "BFS1"
+struct Bf12StreamHeader {
+  uint32_t magic;
+  uint32_t nchunks;
+  uint32_t chunk_values;
+  uint32_t reserved;
+  uint64_t n_values;
+  uint64_t bytes;  // total stream size
+};
+struct Bf12StreamChunk {
+  uint64_t offset;
+  uint32_t n_values;
+  uint32_t encoded;  // 1 = BF12 block, 0 = raw bf16
+};
+static_assert(sizeof(Bf12StreamHeader) == 32 && sizeof(Bf12StreamChunk) == 16, "stream layout");
+inline uint64_t bf12_stream_head_bytes(uint64_t nchunks) { return (32 + 16 * nchunks + 255) & ~255ull; }
+inline uint64_t bf12_pack_bound(uint64_t n_values, uint32_t chunk_values) {
+  uint64_t chunks = (n_values + chunk_values - 1) / chunk_values;
+  return bf12_stream_head_bytes(chunks) + n_values * 2 + chunks * 512;
+}
+// Pack n_values bf16 with `threads` encoder threads into `out` (capacity >=
+// bf12_pack_bound). Returns the stream size, 0 on bad arguments.
+uint64_t bf12_pack(const uint16_t* in, uint64_t n_values, uint32_t chunk_values, uint8_t* out, uint64_t cap,
+                   unsigned threads);
+// Reference unpack of a whole stream (CPU).
+bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n_values);
 
 }  // namespace ogkm

@@ -49,6 +49,10 @@ struct KBf12Descs {
   uint64_t item_start[kInlineDescs + 1];  // prefix sum of 32768-value tiles
 };
 hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgroups, hipStream_t s);
+// Unpack a whole BF12 stream (codec.hpp) that lives in device memory into bf16
+// at `dst`: one launch, one work item per 32768-value tile of every chunk.
+hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
+                              uint32_t workgroups, hipStream_t s);
 
 // Gather `nrows` rows (row_bytes each) of a managed table through its device
 // residency table; misses read zero and are recorded as faults, remote hits are

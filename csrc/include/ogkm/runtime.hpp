@@ -100,6 +100,7 @@ struct Device {
   int id = 0;
   int numa = 0;
   std::unique_ptr<HbmArena> hbm;
+  std::atomic<HbmArena*> hbm_live{nullptr};  // published `hbm` for lock-free readers (arena_for)
   std::unique_ptr<Ring> rings[(int)RingKind::COUNT];
   DeviceFaultBuffer fault_buf;
 };

@@ -128,4 +128,86 @@ hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgr
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// HBM-resident streams: unpack a packed tensor (codec.hpp "BFS1") into a bf16
+// staging buffer right before use. Both sides are HBM, so there is no PCIe
+// latency to hide and no need for LDS: every lane decodes 16 groups of 8 values
+// straight from registers into coalesced 16-B stores (consecutive lanes ->
+// consecutive 16 B), then, after a workgroup barrier, the tile's rare escaped
+// values are patched in place. No LDS means many workgroups per CU; the grid is
+// one item per tile (a 70B layer is ~27k items, >> 256 CUs).
+__global__ void __launch_bounds__(kDecThreads)
+    k_bf12_unpack(const uint8_t* __restrict__ stream, uint8_t* __restrict__ out, uint32_t chunk_values,
+                  uint32_t tile_shift, uint64_t total_items) {
+  const Bf12StreamChunk* table = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof(Bf12StreamHeader));
+  for (uint64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
+    const uint64_t c = item >> tile_shift;
+    const uint32_t t = (uint32_t)(item & ((1u << tile_shift) - 1));
+    const Bf12StreamChunk ch = table[c];  // uniform: scalar loads
+    const uint32_t lo = t * kBf12Tile;
+    if (lo >= ch.n_values) continue;     // uniform across the workgroup
+    const uint32_t cnt = ch.n_values - lo < kBf12Tile ? ch.n_values - lo : kBf12Tile;
+    const uint8_t* blk = stream + ch.offset;
+    u32x4* dst = reinterpret_cast<u32x4*>(out + (c * chunk_values + lo) * 2);
+    if (!ch.encoded) {  // raw chunk: plain tile copy (cnt may have an odd tail)
+      const u32x4* src = reinterpret_cast<const u32x4*>(blk + (uint64_t)lo * 2);
+      for (uint32_t q = threadIdx.x; q < cnt / 8; q += kDecThreads) __builtin_nontemporal_store(src[q], dst + q);
+      const uint16_t* s16 = reinterpret_cast<const uint16_t*>(blk) + lo;
+      uint16_t* d16 = reinterpret_cast<uint16_t*>(out) + c * chunk_values + lo;
+      for (uint32_t k = (cnt & ~7u) + threadIdx.x; k < cnt; k += kDecThreads) d16[k] = s16[k];
+      continue;
+    }
+    const Bf12Header* h = reinterpret_cast<const Bf12Header*>(blk);
+    const uint32_t n = ch.n_values;
+    const uint32_t base = h->base;
+    const uint32_t e0 = h->exc_off[t], e1 = h->exc_off[t + 1];
+    const u32x2* sm8 = reinterpret_cast<const u32x2*>(blk + kBf12HeaderBytes + lo);
+    const uint32_t* cd4 = reinterpret_cast<const uint32_t*>(blk + kBf12HeaderBytes + n + lo / 2);
+    const uint32_t groups = cnt / 8;
+    constexpr int kPer = kBf12Tile / 8 / kDecThreads;  // 16
+    u32x2 sv[kPer];
+    uint32_t cv[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      uint32_t g = threadIdx.x + u * kDecThreads;
+      if (g < groups) {
+        sv[u] = __builtin_nontemporal_load(sm8 + g);
+        cv[u] = __builtin_nontemporal_load(cd4 + g);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      uint32_t g = threadIdx.x + u * kDecThreads;
+      if (g < groups) {
+        u32x2 a0 = dec4(sv[u][0], cv[u], base), a1 = dec4(sv[u][1], cv[u] >> 16, base);
+        dst[g] = u32x4{a0[0], a0[1], a1[0], a1[1]};
+      }
+    }
+    if (e1 > e0) {  // uniform branch: only tiles with escapes pay the barrier
+      __syncthreads();  // workgroup-scope ordering: the patch lands after the bulk store
+      const Bf12Exception* exc =
+          reinterpret_cast<const Bf12Exception*>(blk + kBf12HeaderBytes + n + n / 2);
+      uint16_t* d16 = reinterpret_cast<uint16_t*>(out) + c * chunk_values;
+      for (uint32_t k = e0 + threadIdx.x; k < e1; k += kDecThreads) {
+        Bf12Exception ex = exc[k];
+        d16[ex.index] = ex.bits;
+      }
+    }
+  }
+}
+
+hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
+                              uint32_t workgroups, hipStream_t s) {
+  if (nchunks == 0) return hipSuccess;
+  if (chunk_values < 8192 || (chunk_values & (chunk_values - 1)) || chunk_values > kBf12Tile * kBf12MaxTiles)
+    return hipErrorInvalidValue;
+  uint32_t shift = 0;
+  while ((kBf12Tile << shift) < chunk_values) ++shift;  // tiles per chunk = 1 << shift
+  uint64_t total = (uint64_t)nchunks << shift;
+  uint64_t grid = workgroups && workgroups < total ? workgroups : total;
+  hipLaunchKernelGGL(k_bf12_unpack, dim3((uint32_t)grid), dim3(kDecThreads), 0, s, (const uint8_t*)stream,
+                     (uint8_t*)dst, chunk_values, shift, total);
+  return hipGetLastError();
+}
+
 }  // namespace ogkm

@@ -565,6 +565,33 @@ PYBIND11_MODULE(_ogkm, m) {
     if (!bf12_decode((const uint8_t*)s.data(), (uint16_t*)out.data(), n_values)) throw StatusError("bf12_decode: bad block");
     return py::bytes(out);
   });
+  // Self-describing BF12 streams of whole tensors (ops/bf12.py).
+  m.def("bf12_pack_bound", [](uint64_t n, uint32_t chunk_values) { return bf12_pack_bound(n, chunk_values); });
+  m.def("bf12_pack", [](uint64_t src, uint64_t n_values, uint64_t dst, uint64_t cap, uint32_t chunk_values,
+                        unsigned threads) {
+    uint64_t total;
+    {
+      py::gil_scoped_release nogil;
+      total = bf12_pack((const uint16_t*)src, n_values, chunk_values, (uint8_t*)dst, cap, threads);
+    }
+    if (!total) throw StatusError("bf12_pack: bad arguments or buffer too small");
+    return total;
+  });
+  m.def("bf12_unpack_host", [](uint64_t src, uint64_t dst, uint64_t n_values) {
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = bf12_unpack((const uint8_t*)src, (uint16_t*)dst, n_values);
+    }
+    if (!ok) throw StatusError("bf12_unpack_host: corrupt stream");
+  });
+  // Unpack a stream resident on device `dev` into `dst` on `stream` (k_bf12_unpack).
+  m.def("bf12_unpack", [](int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
+                          uint64_t n_values, uint64_t stream, uint32_t workgroups) {
+    check(rt()->be()->unpack_bf12_stream(dev, src, dst, nchunks, chunk_values, n_values, (void*)stream, workgroups),
+          "bf12_unpack");
+  }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("nchunks"), py::arg("chunk_values"),
+     py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0);
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
     return py::make_tuple((uint64_t)fb.put, (uint64_t)fb.recs, fb.entries, fb.overflows);

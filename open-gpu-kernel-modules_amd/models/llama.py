@@ -32,6 +32,7 @@ import torch
 
 from .. import rt
 from .._native import lib
+from ..ops import bf12
 from ..ops import decode as D
 from ..ops.memory import managed_embedding
 from ..parallel import comm, tp as tpmod
@@ -101,7 +102,7 @@ class TieredLlama:
     def __init__(self, cfg: LlamaConfig, batch: int, context: int, max_new_tokens: int = 64, oversub: float = 2.0,
                  device: int = 0, tp_rank: int = 0, tp_world: int = 1, seed: int = 0, lookahead: int = 2,
                  hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
-                 packed: bool = True):
+                 packed: bool = True, weight_format: str = "bf12"):
         assert cfg.n_heads % tp_world == 0 and cfg.n_kv_heads % tp_world == 0 and cfg.ffn_dim % tp_world == 0
         assert cfg.vocab % tp_world == 0
         self.cfg, self.B, self.ctx = cfg, batch, context
@@ -126,52 +127,87 @@ class TieredLlama:
         blk = 2 << 20
         budget = hbm_budget if hbm_budget is not None else int(self.footprint / oversub)
         self.budget = budget // blk * blk
-        lib.init_device(device, self.budget)
-        # ---- residency plan
+
         def chunks(n):
             return (n + blk - 1) // blk * blk
-        staging = (lookahead + 1) * chunks(max(self.layer_bytes, self.head_bytes))
-        avail = self.budget - chunks(self.kv_bytes) - staging
+        # Weight storage. "bf12": every weight rests packed (lossless BF12, ~0.75x)
+        # in whatever tier holds it - host, CXL and HBM - and is unpacked into one
+        # bf16 staging buffer right before its layer runs (ops/bf12.py). The
+        # staging buffer is carved out of the same HBM budget. "bf16": raw
+        # weights; with ``packed`` the runtime keeps streamed host copies BF12 and
+        # decodes them inside the H2D copy kernel (RANGE_PACKED_BF16).
+        if weight_format not in ("bf12", "bf16"):
+            raise ValueError("weight_format must be 'bf12' or 'bf16'")
+        self.wfmt = weight_format
+        self.packed = packed and weight_format == "bf16"
+        self.stage_bytes = chunks(max(self.layer_bytes, self.head_bytes)) if weight_format == "bf12" else 0
+        self.arena_bytes = self.budget - self.stage_bytes
+        lib.init_device(device, self.arena_bytes)
+        self.pinfo: dict = {}
+        gpu = rt.Loc.gpu(device)
+        host = rt.Loc.host()
+        t0 = time.perf_counter()
+        self._seed, self._std = seed, init_std
+        if weight_format == "bf12":
+            # The packed size of layer 0 sizes the plan (all layers share one distribution).
+            first, info0 = bf12.pack(self._gen_layer(0))
+            ratio = info0.nbytes / (self.layer_bytes)
+            self.res_layer_bytes = _al(int(self.layer_bytes * ratio * 1.002) + 4096)
+            self.res_head_bytes = _al(int(self.head_bytes * ratio * 1.002) + 4096)
+        else:
+            first = None
+            self.res_layer_bytes, self.res_head_bytes = self.layer_bytes, self.head_bytes
+        # ---- residency plan (in resting bytes: packed or raw)
+        staging = (lookahead + 1) * chunks(max(self.res_layer_bytes, self.res_head_bytes))
+        avail = self.arena_bytes - chunks(self.kv_bytes) - staging
         if avail < 0:
             raise ValueError(f"HBM budget {self.budget/2**30:.1f} GiB too small for KV + staging "
-                             f"({(chunks(self.kv_bytes) + staging)/2**30:.1f} GiB)")
-        n_res = max(0, min(cfg.n_layers, avail // chunks(self.layer_bytes)))
-        left = avail - n_res * chunks(self.layer_bytes)
-        self.head_resident = left >= chunks(self.head_bytes)
+                             f"({(chunks(self.kv_bytes) + staging + self.stage_bytes)/2**30:.1f} GiB)")
+        n_res = max(0, min(cfg.n_layers, avail // chunks(self.res_layer_bytes)))
+        left = avail - n_res * chunks(self.res_layer_bytes)
+        self.head_resident = left >= chunks(self.res_head_bytes)
         # spread resident layers evenly so streaming continues behind them
         self.resident = [((i + 1) * n_res) // cfg.n_layers > (i * n_res) // cfg.n_layers for i in range(cfg.n_layers)]
         self.lookahead = lookahead
-        self.window_bytes = lookahead * chunks(max(self.layer_bytes, self.head_bytes))
-        self.streamed_bytes = (sum(self.layer_bytes for r in self.resident if not r)
-                               + (0 if self.head_resident else self.head_bytes))
+        self.window_bytes = lookahead * chunks(max(self.res_layer_bytes, self.res_head_bytes))
+        self.streamed_bytes = (sum(self.res_layer_bytes for r in self.resident if not r)
+                               + (0 if self.head_resident else self.res_head_bytes))
         # ---- allocate + init
-        t0 = time.perf_counter()
-        gpu = rt.Loc.gpu(device)
-        host = rt.Loc.host()
         self.embed = rt.malloc_managed(self.embed_bytes, "embed")
         self.embed.set_preferred_location(host)
         self.embed.set_accessed_by(device)
         self.kv = rt.malloc_managed(self.kv_bytes, "kv")
         self.kv.set_preferred_location(gpu)
-        # Streamed tensors keep a BF12-packed (lossless) host copy: the H2D copy
-        # kernel decodes it on the fly, so ~25% fewer bytes cross PCIe per step.
-        self.packed = packed
         self.layers = []
         for i in range(cfg.n_layers):
-            b = rt.malloc_managed(self.layer_bytes, f"layer{i}", packed_bf16=packed and not self.resident[i])
-            if self.resident[i]:
-                b.set_preferred_location(gpu)
+            if weight_format == "bf12":
+                stream, info = (first, info0) if i == 0 else bf12.pack(self._gen_layer(i))
+                b = rt.malloc_managed(info.nbytes, f"layer{i}", cpu_view=False)
+                self.pinfo[("layer", i)] = info
             else:
-                b.set_preferred_location(host)
-                b.set_read_mostly(True)
+                stream = self._gen_layer(i)
+                b = rt.malloc_managed(self.layer_bytes, f"layer{i}", packed_bf16=self.packed and not self.resident[i])
+            self._place(b, self.resident[i], gpu, host)
+            b.write(stream)
             self.layers.append(b)
-        self.head = rt.malloc_managed(self.head_bytes, "lm_head", packed_bf16=packed and not self.head_resident)
-        if self.head_resident:
-            self.head.set_preferred_location(gpu)
+            del stream
+        first = None
+        head = self._gen_head()
+        if weight_format == "bf12":
+            stream, info = bf12.pack(head)
+            self.head = rt.malloc_managed(info.nbytes, "lm_head", cpu_view=False)
+            self.pinfo[("head", 0)] = info
         else:
-            self.head.set_preferred_location(host)
-            self.head.set_read_mostly(True)
-        self._init_weights(seed, init_std)
+            stream = head
+            self.head = rt.malloc_managed(self.head_bytes, "lm_head", packed_bf16=self.packed and not self.head_resident)
+        self._place(self.head, self.head_resident, gpu, host)
+        self.head.write(stream)
+        del head, stream
+        self.embed.write(self._gen_embed())
+        if not self.fake:
+            torch.cuda.synchronize(self.dev)
+        self.stage = (torch.empty(self.stage_bytes // 2, dtype=torch.bfloat16, device=self.tdev)
+                      if weight_format == "bf12" else None)
         self.final_norm = torch.ones(cfg.dim, dtype=torch.bfloat16, device=self.tdev)
         self.cos, self.sin = D.rope_tables(hd, self.T, cfg.rope_theta, self.tdev)
         # KV cache: leased for the model's lifetime (hot, written every step)
@@ -211,6 +247,8 @@ class TieredLlama:
             "streamed_layers": self.cfg.n_layers - sum(self.resident), "head_resident": self.head_resident,
             "streamed_gb_per_step": self.streamed_bytes / 1e9, "init_s": getattr(self, "init_seconds", None),
             "packed_host_copies": getattr(self, "packed", False),
+            "weight_format": self.wfmt, "resting_layer_gb": self.res_layer_bytes / 1e9,
+            "stage_gb": self.stage_bytes / 1e9,
         }
         if self.verbose and self.rank == 0:
             print("[ogkm] plan:", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}, flush=True)
@@ -224,47 +262,69 @@ class TieredLlama:
         kind, i = key
         return self.layers[i] if kind == "layer" else self.head
 
-    def _init_weights(self, seed: int, std: float) -> None:
+    @staticmethod
+    def _place(b, resident: bool, gpu, host) -> None:
+        if resident:
+            b.set_preferred_location(gpu)
+        else:
+            b.set_preferred_location(host)
+            b.set_read_mostly(True)
+
+    def _gen_layer(self, i: int) -> torch.Tensor:
+        """Layer i's weights (this TP rank's shard) in the LayerLayout, as a flat
+        bf16 tensor of layer_bytes / 2 values (random init, deterministic)."""
         cfg, L = self.cfg, self.layout
         hd = cfg.head_dim
-        dev = self.tdev
-        scratch = torch.empty(self.layer_bytes, dtype=torch.uint8, device=dev)
+        dev, std = self.tdev, self._std
+        flat = torch.zeros(self.layer_bytes // 2, dtype=torch.bfloat16, device=dev)
 
         def put(name, t):
-            off = L.offsets[name]
-            n = t.numel() * 2
-            scratch[off:off + n].copy_(t.reshape(-1).view(torch.uint8))
+            off = L.offsets[name] // 2
+            flat[off:off + t.numel()].copy_(t.reshape(-1))
 
-        for i in range(cfg.n_layers):
-            g = torch.Generator(device=dev).manual_seed(seed * 1000003 + i)
-            wq = torch.empty(cfg.n_heads * hd, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-            wk = torch.empty(cfg.n_kv_heads * hd, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-            wv = torch.empty(cfg.n_kv_heads * hd, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-            put("wqkv", tpmod.shard_qkv(wq, wk, wv, self.rank, self.world))
-            del wq, wk, wv
-            wo = torch.empty(cfg.dim, cfg.n_heads * hd, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-            put("wo", tpmod.shard_cols(wo, self.rank, self.world))
-            del wo
-            wg = torch.empty(cfg.ffn_dim, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-            wu = torch.empty(cfg.ffn_dim, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-            put("wgu", tpmod.shard_gate_up(wg, wu, self.rank, self.world))
-            del wg, wu
-            wd = torch.empty(cfg.dim, cfg.ffn_dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-            put("wd", tpmod.shard_cols(wd, self.rank, self.world))
-            del wd
-            one = torch.ones(cfg.dim, dtype=torch.bfloat16, device=dev)
-            put("attn_norm", one)
-            put("mlp_norm", one)
-            self.layers[i].write(scratch)
-        del scratch
-        g = torch.Generator(device=dev).manual_seed(seed * 1000003 + 999983)
-        emb = torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, 1.0, generator=g)
-        self.embed.write(emb)
-        head = torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-        self.head.write(tpmod.shard_rows(head, self.rank, self.world).contiguous())
-        del emb, head
-        if not self.fake:
-            torch.cuda.synchronize(self.dev)
+        g = torch.Generator(device=dev).manual_seed(self._seed * 1000003 + i)
+        wq = torch.empty(cfg.n_heads * hd, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
+        wk = torch.empty(cfg.n_kv_heads * hd, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
+        wv = torch.empty(cfg.n_kv_heads * hd, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
+        put("wqkv", tpmod.shard_qkv(wq, wk, wv, self.rank, self.world))
+        del wq, wk, wv
+        wo = torch.empty(cfg.dim, cfg.n_heads * hd, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
+        put("wo", tpmod.shard_cols(wo, self.rank, self.world))
+        del wo
+        wg = torch.empty(cfg.ffn_dim, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
+        wu = torch.empty(cfg.ffn_dim, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
+        put("wgu", tpmod.shard_gate_up(wg, wu, self.rank, self.world))
+        del wg, wu
+        wd = torch.empty(cfg.dim, cfg.ffn_dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
+        put("wd", tpmod.shard_cols(wd, self.rank, self.world))
+        del wd
+        one = torch.ones(cfg.dim, dtype=torch.bfloat16, device=dev)
+        put("attn_norm", one)
+        put("mlp_norm", one)
+        return flat
+
+    def _head_gen(self) -> torch.Generator:
+        return torch.Generator(device=self.tdev).manual_seed(self._seed * 1000003 + 999983)
+
+    def _gen_embed(self) -> torch.Tensor:
+        cfg = self.cfg
+        return torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=self.tdev).normal_(
+            0, 1.0, generator=self._head_gen())
+
+    def _gen_head(self) -> torch.Tensor:
+        cfg = self.cfg
+        g = self._head_gen()
+        torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=self.tdev).normal_(0, 1.0, generator=g)  # embed draw
+        head = torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=self.tdev).normal_(0, self._std, generator=g)
+        return tpmod.shard_rows(head, self.rank, self.world).contiguous()
+
+    def host_weights(self, key) -> torch.Tensor:
+        """The bf16 bytes of a layer / head as stored (unpacked on the host) - for
+        reference numerics."""
+        raw = self._buf(key).read()
+        if self.wfmt == "bf12":
+            return bf12.unpack_host(raw, self.pinfo[key]).view(torch.uint8)
+        return raw
 
     # ------------------------------------------------------------------ streaming
     def _prefetch_ahead(self) -> None:
@@ -284,23 +344,31 @@ class TieredLlama:
             self._pf_next = (self._pf_next + 1) % n
 
     def _use(self, key):
+        """Fault the tensor in (lease) and return (lease or None, base pointer of
+        its bf16 weights). bf12: the packed stream is unpacked into the staging
+        buffer on the compute stream and the lease is released right away (the
+        ring reuses the chunks only after the unpack has read them)."""
         if not self._is_resident(key):
             if self._inflight and self._inflight[0] == key:
                 self._inflight.pop(0)
             self._prefetch_ahead()
         lease = self._buf(key).acquire(self.dev, rt.READ)
         lease.wait(0 if self.fake else None)
-        return lease
+        if self.wfmt == "bf12":
+            bf12.unpack_into(self.stage, lease.dptr, self.pinfo[key], self.dev, 0 if self.fake else None)
+            lease.release(0 if self.fake else None)
+            return None, self.stage.data_ptr()
+        return lease, lease.dptr
 
-    def _layer_views(self, lease) -> dict:
-        v = self._views.get(lease.dptr)
+    def _layer_views(self, ptr: int) -> dict:
+        v = self._views.get(ptr)
         if v is None:
-            v = {name: rt._tensor_from_ptr(lease.dptr + self.layout.offsets[name], shape, torch.bfloat16,
+            v = {name: rt._tensor_from_ptr(ptr + self.layout.offsets[name], shape, torch.bfloat16,
                                            "cpu" if self.fake else "cuda", self.dev)
                  for name, shape in self.layout.shapes.items()}
             if len(self._views) > 4 * len(self.order):
                 self._views.clear()
-            self._views[lease.dptr] = v
+            self._views[ptr] = v
         return v
 
     # ------------------------------------------------------------------ decode
@@ -317,8 +385,8 @@ class TieredLlama:
             x = x.to(self.tdev)
         cos, sin = self.cos[pos], self.sin[pos]
         for i in range(cfg.n_layers):
-            lease = self._use(("layer", i))
-            w = self._layer_views(lease)
+            lease, ptr = self._use(("layer", i))
+            w = self._layer_views(ptr)
             h = D.rms_norm(x, w["attn_norm"], cfg.norm_eps)
             qkv = h @ w["wqkv"].t()
             q = qkv[:, :self.hq * hd].view(B, self.hq, hd)
@@ -336,16 +404,18 @@ class TieredLlama:
             gu = h @ w["wgu"].t()
             d = D.silu_mul(gu) @ w["wd"].t()
             x = x + tpmod.row_parallel_reduce(d)
-            lease.release(0 if self.fake else None)
+            if lease is not None:
+                lease.release(0 if self.fake else None)
         x = D.rms_norm(x, self.final_norm, cfg.norm_eps)
-        lease = self._use(("head", 0))
-        head = rt._tensor_from_ptr(lease.dptr, (self.vocab_local, cfg.dim), torch.bfloat16,
+        lease, ptr = self._use(("head", 0))
+        head = rt._tensor_from_ptr(ptr, (self.vocab_local, cfg.dim), torch.bfloat16,
                                    "cpu" if self.fake else "cuda", self.dev)
         logits = x @ head.t()
         if self.keep_logits:
             self.last_logits = comm.all_gather_cat(logits.float(), dim=-1)
         nxt = tpmod.vocab_parallel_argmax(logits, self.rank, self.world)
-        lease.release(0 if self.fake else None)
+        if lease is not None:
+            lease.release(0 if self.fake else None)
         self.pos += 1
         return nxt
 
@@ -369,7 +439,7 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
     x = emb[tokens.cpu()].to(dev)
     cos, sin = model.cos[pos], model.sin[pos]
     for i in range(cfg.n_layers):
-        raw = model.layers[i].read()
+        raw = model.host_weights(("layer", i))
         w = {n: raw[model.layout.offsets[n]:model.layout.offsets[n] + math.prod(s) * 2].view(torch.bfloat16)
              .view(*s).float().to(dev) for n, s in model.layout.shapes.items()}
         h = D.rms_norm(x, w["attn_norm"], cfg.norm_eps)
@@ -387,7 +457,7 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
         h = D.rms_norm(x, w["mlp_norm"], cfg.norm_eps)
         x = x + D.silu_mul(h @ w["wgu"].t()) @ w["wd"].t()
     x = D.rms_norm(x, model.final_norm.float(), cfg.norm_eps)
-    head = model.head.read().view(torch.bfloat16).view(model.vocab_local, cfg.dim).float().to(dev)
+    head = model.host_weights(("head", 0)).view(torch.bfloat16).view(model.vocab_local, cfg.dim).float().to(dev)
     return x @ head.t()
 
 

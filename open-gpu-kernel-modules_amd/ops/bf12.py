@@ -1,0 +1,88 @@
+"""BF12 packed tensors: lossless ~0.75x bf16 storage for data that rests in any
+tier - host, CXL *and HBM* - and is unpacked into a bf16 staging buffer right
+before use.
+
+Why: at 2x oversubscription a decode step is bound by the bytes that cross
+PCIe per step. Keeping the weights packed where they rest shrinks both the
+streamed bytes and the HBM each resident layer occupies, so more of the model
+stays resident (the managed footprint the runtime moves is the packed one).
+The unpack (csrc/kernels/bf12_kernels.hip k_bf12_unpack) runs HBM->HBM at a
+few TB/s, i.e. well under a millisecond per 70B layer.
+
+Format: codec.hpp "BFS1" stream = header + chunk table + 256-B aligned chunks
+(each a BF12 block: sign|mantissa bytes + 4-bit exponent codes relative to a
+per-chunk base + an exception list for escaped exponents; or raw bf16).
+"""
+from __future__ import annotations
+
+import os
+import struct
+from dataclasses import dataclass
+
+import torch
+
+from .._native import lib
+
+CHUNK_VALUES = 1 << 20  # 2 MB of bf16 per chunk (32 decode tiles)
+HEADER = struct.Struct("<IIIIQQ")
+MAGIC = 0x31534642
+
+
+@dataclass
+class PackedInfo:
+    n_values: int
+    nbytes: int          # stream size
+    nchunks: int
+    chunk_values: int
+
+    @property
+    def ratio(self) -> float:
+        return self.nbytes / max(1, self.n_values * 2)
+
+
+def _threads() -> int:
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
+
+
+def pack(t: torch.Tensor, chunk_values: int = CHUNK_VALUES, out: torch.Tensor | None = None
+         ) -> tuple[torch.Tensor, PackedInfo]:
+    """Pack a bf16 tensor (any device; encoded on the host) -> (uint8 CPU stream, info)."""
+    if t.dtype != torch.bfloat16:
+        raise TypeError("pack expects bf16")
+    src = t.detach().reshape(-1).contiguous().cpu()
+    n = src.numel()
+    bound = lib.bf12_pack_bound(n, chunk_values)
+    if out is None or out.numel() < bound:
+        out = torch.empty(bound, dtype=torch.uint8)
+    total = lib.bf12_pack(src.data_ptr(), n, out.data_ptr(), bound, chunk_values, _threads())
+    return out[:total], info_of(out[:64])
+
+
+def info_of(stream_head: torch.Tensor) -> PackedInfo:
+    """Parse a stream header (the first 32 bytes, CPU tensor or bytes)."""
+    raw = bytes(stream_head[:HEADER.size].cpu().numpy()) if isinstance(stream_head, torch.Tensor) else stream_head
+    magic, nch, cv, _r, n, nbytes = HEADER.unpack(raw[:HEADER.size])
+    if magic != MAGIC:
+        raise ValueError("not a BF12 stream")
+    return PackedInfo(n, nbytes, nch, cv)
+
+
+def unpack_host(stream: torch.Tensor, info: PackedInfo) -> torch.Tensor:
+    """CPU reference unpack -> bf16 tensor of info.n_values."""
+    out = torch.empty(info.n_values, dtype=torch.bfloat16)
+    s = stream.contiguous()
+    lib.bf12_unpack_host(s.data_ptr(), out.data_ptr(), info.n_values)
+    return out
+
+
+def unpack_into(dst: torch.Tensor, src_ptr: int, info: PackedInfo, device: int = 0, stream: int | None = None,
+                workgroups: int = 0) -> torch.Tensor:
+    """Unpack the stream at device address ``src_ptr`` into ``dst`` (bf16, at least
+    n_values) on ``stream`` (default: the current torch stream of ``device``)."""
+    if dst.dtype != torch.bfloat16 or dst.numel() < info.n_values:
+        raise ValueError("dst must be bf16 with room for n_values")
+    if stream is None:
+        stream = int(torch.cuda.current_stream(device).cuda_stream) if dst.is_cuda else 0
+    lib.bf12_unpack(device, src_ptr, dst.data_ptr(), info.nchunks, info.chunk_values, info.n_values, stream,
+                    workgroups)
+    return dst

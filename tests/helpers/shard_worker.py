@@ -36,7 +36,11 @@ def main():
     pipe.drain()
     res = {"rank": e.rank, "ok": ok, "gathers": pipe.stats["gathers"], "shard_bytes": sw.shard_bytes()}
     sw.free()
-    print("SHARDRESULT " + json.dumps(res), flush=True)
+    allres = [None] * e.world
+    torch.distributed.all_gather_object(allres, res)
+    if e.rank == 0:
+        for r in allres:
+            print("SHARDRESULT " + json.dumps(r), flush=True)
     comm.shutdown()
 
 

@@ -20,7 +20,7 @@ def main():
     e = comm.init("gloo")
     rt.init("fake", fake_devices=1, fake_hbm_mb=512, host_budget_mb=2048)
     cfg = llama.CONFIGS["tiny"]
-    m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=4, oversub=1.5, lookahead=1,
+    m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=4, oversub=1.2, lookahead=1,
                           tp_rank=e.rank, tp_world=e.world, seed=5)
     m.keep_logits = True
     out = []
