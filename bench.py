@@ -17,7 +17,7 @@ streams only its shard over its own PCIe link.
 One step = one decode token for every sequence (weights streamed, KV appended,
 greedy sampling). ``value`` = global tokens/s = batch * K / max-over-ranks time.
 
-Weights rest losslessly packed (BF12, ~0.75x, bit-exact bf16 after unpack) in
+Weights rest losslessly packed (BF11, ~0.69x, bit-exact bf16 after unpack) in
 every tier and are unpacked into a bf16 staging buffer right before each layer
 runs; the oversubscription ratio and HBM budget are computed on the logical bf16
 footprint (weights + KV + embedding + head), and the staging buffer is carved out
@@ -53,9 +53,9 @@ def parse():
     ap.add_argument("--oversub", type=float, default=2.0)
     ap.add_argument("--lookahead", type=int, default=2)
     ap.add_argument("--no-aux", action="store_true", help="skip the HBM<->host/CXL bandwidth probe")
-    ap.add_argument("--weights", choices=("bf12", "bf16"), default="bf12",
-                    help="bf12: weights rest losslessly packed in every tier (HBM included) and are unpacked "
-                         "per layer; bf16: raw weights")
+    ap.add_argument("--weights", choices=("bf11", "bf12", "bf16"), default="bf11",
+                    help="bf11/bf12: weights rest losslessly packed (~0.69x / 0.75x) in every tier (HBM included) "
+                         "and are unpacked per layer; bf16: raw weights")
     ap.add_argument("--no-packed", action="store_true",
                     help="with --weights bf16: raw host copies instead of BF12 copies decoded in the H2D kernel")
     ap.add_argument("--verbose", action="store_true")
@@ -167,9 +167,11 @@ def main() -> None:
                 "streamed_layers": plan["streamed_layers"],
                 "streamed_gb_per_step_per_gpu": round(plan["streamed_gb_per_step"], 2),
                 "weight_format": plan["weight_format"],
-                "host_copy_format": ("bf12-lossless" if plan["packed_host_copies"] or plan["weight_format"] == "bf12"
-                                     else "bf16"),
-                "hbm_copy_format": "bf12-lossless (unpacked per layer)" if plan["weight_format"] == "bf12" else "bf16",
+                "host_copy_format": (f"{plan['weight_format']}-lossless" if plan["weight_format"] != "bf16"
+                                     else "bf12-lossless" if plan["packed_host_copies"] else "bf16"),
+                "hbm_copy_format": (f"{plan['weight_format']}-lossless (unpacked per layer)"
+                                    if plan["weight_format"] != "bf16" else "bf16"),
+                "resting_bytes_ratio": round(plan["resting_layer_gb"] / plan["layer_gb"], 4),
             },
             "aux": {
                 **aux,

@@ -79,8 +79,131 @@ bool bf12_decode(const uint8_t* in, uint16_t* out, uint32_t n) {
   return true;
 }
 
+
+// ---------------------------------------------------------------------------
+// BF11 (two-level exponent code)
+
+static inline uint64_t al8(uint64_t x) { return (x + 7) & ~7ull; }
+
+uint64_t bf11_encode(const uint16_t* in, uint32_t n, uint8_t* out, uint64_t cap) {
+  if (n == 0 || (n & 7) || n > kBf12Tile * kBf12MaxTiles) return 0;
+  uint32_t hist[256] = {0};
+  for (uint32_t i = 0; i < n; ++i) hist[(in[i] >> 7) & 0xFF]++;
+  // primary: the three most frequent exponents
+  uint8_t prim[3] = {0, 0, 0};
+  bool taken[256] = {false};
+  for (int k = 0; k < 3; ++k) {
+    uint32_t best = 0, cnt = 0;
+    bool any = false;
+    for (uint32_t e = 0; e < 256; ++e)
+      if (!taken[e] && (!any || hist[e] > cnt)) {
+        best = e;
+        cnt = hist[e];
+        any = true;
+      }
+    prim[k] = (uint8_t)best;
+    taken[best] = true;
+  }
+  int8_t pcode[256];
+  for (int e = 0; e < 256; ++e) pcode[e] = -1;
+  for (int k = 0; k < 3; ++k) pcode[prim[k]] = (int8_t)k;
+  // secondary window: 15 consecutive exponents covering most escaped values
+  uint32_t rest[256];
+  for (int e = 0; e < 256; ++e) rest[e] = pcode[e] >= 0 ? 0 : hist[e];
+  uint32_t sbase = 0, win = 0, best_win;
+  for (uint32_t e = 0; e < 15; ++e) win += rest[e];
+  best_win = win;
+  for (uint32_t b = 1; b + 15 <= 256; ++b) {
+    win += rest[b + 14] - rest[b - 1];
+    if (win > best_win) {
+      best_win = win;
+      sbase = b;
+    }
+  }
+  uint32_t n_sec = 0;
+  for (int e = 0; e < 256; ++e) n_sec += rest[e];
+  uint32_t n_exc = n_sec - best_win;
+  const uint32_t ngroups = (n + kBf11Group - 1) / kBf11Group;
+  Bf11Header h;
+  memset(&h, 0, sizeof h);
+  h.magic = kBf11Magic;
+  h.n_values = n;
+  h.n_exc = n_exc;
+  h.prim = prim[0] | (prim[1] << 8) | (prim[2] << 16);
+  h.sec_base = sbase;
+  h.n_sec = n_sec;
+  h.off_prim = kBf11HeaderBytes + n;
+  h.off_wg = (uint32_t)al8(h.off_prim + n / 4);
+  h.off_sec = (uint32_t)al8(h.off_wg + 2ull * ngroups);
+  h.off_exc = (uint32_t)al8(h.off_sec + (n_sec + 1) / 2 + 8);
+  const uint64_t need = (uint64_t)h.off_exc + (uint64_t)n_exc * sizeof(Bf12Exception);
+  if (need > cap) return 0;
+  uint8_t* sm = out + kBf11HeaderBytes;
+  uint8_t* pc = out + h.off_prim;
+  uint16_t* wg = reinterpret_cast<uint16_t*>(out + h.off_wg);
+  uint8_t* sec = out + h.off_sec;
+  Bf12Exception* exc = reinterpret_cast<Bf12Exception*>(out + h.off_exc);
+  memset(pc, 0, n / 4);
+  memset(sec, 0, h.off_exc - h.off_sec);
+  uint32_t nib = 0, e_out = 0;
+  const uint32_t ntiles = (n + kBf12Tile - 1) / kBf12Tile;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (i % kBf12Tile == 0) {
+      h.exc_off[i / kBf12Tile] = e_out;
+      h.sec_tile[i / kBf12Tile] = nib;
+    }
+    if (i % kBf11Group == 0) wg[i / kBf11Group] = (uint16_t)(nib - h.sec_tile[i / kBf12Tile]);
+    const uint16_t v = in[i];
+    const uint32_t e = (v >> 7) & 0xFF;
+    sm[i] = (uint8_t)(((v >> 8) & 0x80) | (v & 0x7F));
+    uint32_t c = pcode[e] >= 0 ? (uint32_t)pcode[e] : 3u;
+    pc[i >> 2] |= (uint8_t)(c << (2 * (i & 3)));
+    if (c == 3) {
+      uint32_t sc = e - sbase;
+      if (e < sbase || sc >= 15) {
+        sc = 15;
+        exc[e_out++] = Bf12Exception{i, v, 0};
+      }
+      sec[nib >> 1] |= (uint8_t)(sc << (4 * (nib & 1)));
+      ++nib;
+    }
+  }
+  for (uint32_t t = ntiles; t <= kBf12MaxTiles; ++t) {
+    h.exc_off[t] = e_out;
+    h.sec_tile[t] = nib;
+  }
+  memcpy(out, &h, sizeof h);
+  return need;
+}
+
+bool bf11_decode(const uint8_t* in, uint16_t* out, uint32_t n) {
+  Bf11Header h;
+  memcpy(&h, in, sizeof h);
+  if (h.magic != kBf11Magic || h.n_values != n) return false;
+  const uint8_t* sm = in + kBf11HeaderBytes;
+  const uint8_t* pc = in + h.off_prim;
+  const uint8_t* sec = in + h.off_sec;
+  const Bf12Exception* exc = reinterpret_cast<const Bf12Exception*>(in + h.off_exc);
+  uint32_t nib = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t c = (pc[i >> 2] >> (2 * (i & 3))) & 3;
+    uint32_t e;
+    if (c < 3) {
+      e = (h.prim >> (8 * c)) & 0xFF;
+    } else {
+      e = (h.sec_base + ((sec[nib >> 1] >> (4 * (nib & 1))) & 0xF)) & 0xFF;
+      ++nib;
+    }
+    uint32_t s = sm[i];
+    out[i] = (uint16_t)(((s & 0x80) << 8) | (e << 7) | (s & 0x7F));
+  }
+  if (nib != h.n_sec) return false;
+  for (uint32_t k = 0; k < h.n_exc; ++k) out[exc[k].index] = exc[k].bits;
+  return true;
+}
+
 uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_t* out, uint64_t cap,
-                   unsigned threads) {
+                   unsigned threads, PackFormat fmt) {
   if (!n || chunk_values < 8192 || (chunk_values & (chunk_values - 1)) || chunk_values > kBf12Tile * kBf12MaxTiles)
     return 0;
   if (cap < bf12_pack_bound(n, chunk_values)) return 0;
@@ -95,9 +218,29 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_
       uint64_t lo = c * chunk_values;
       uint32_t cnt = (uint32_t)std::min<uint64_t>(chunk_values, n - lo);
       uint8_t* dst = out + head + c * slot;
-      uint64_t e = (cnt % 8 == 0) ? bf12_encode(in + lo, cnt, dst, (uint64_t)cnt * 2) : 0;
+      uint64_t e = 0;
+      uint32_t kind = 0;
+      if (cnt % 8 == 0 && fmt == PackFormat::BF11) {
+        e = bf11_encode(in + lo, cnt, dst, (uint64_t)cnt * 2);
+        kind = e ? 2 : 0;
+        // BF11 wins for weight-like data; keep BF12 where it is smaller
+        // (e.g. flat exponent histograms that escape most values).
+        if (e && e > (uint64_t)cnt * 3 / 2 + kBf12HeaderBytes) {
+          uint64_t e12 = bf12_encode(in + lo, cnt, dst, e);
+          if (e12) {
+            e = e12;
+            kind = 1;
+          } else {
+            e = bf11_encode(in + lo, cnt, dst, (uint64_t)cnt * 2);
+          }
+        }
+      }
+      if (!e && cnt % 8 == 0) {
+        e = bf12_encode(in + lo, cnt, dst, (uint64_t)cnt * 2);
+        kind = e ? 1 : 0;
+      }
       table[c].n_values = cnt;
-      table[c].encoded = e ? 1 : 0;
+      table[c].encoded = kind;
       if (!e) {
         memcpy(dst, in + lo, (size_t)cnt * 2);
         e = (uint64_t)cnt * 2;
@@ -135,7 +278,9 @@ bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n) {
   const Bf12StreamChunk* t = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof h);
   for (uint32_t c = 0; c < h.nchunks; ++c) {
     uint16_t* dst = out + (uint64_t)c * h.chunk_values;
-    if (t[c].encoded) {
+    if (t[c].encoded == 2) {
+      if (!bf11_decode(stream + t[c].offset, dst, t[c].n_values)) return false;
+    } else if (t[c].encoded == 1) {
       if (!bf12_decode(stream + t[c].offset, dst, t[c].n_values)) return false;
     } else {
       memcpy(dst, stream + t[c].offset, (size_t)t[c].n_values * 2);

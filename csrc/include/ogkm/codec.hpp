@@ -51,6 +51,46 @@ inline uint64_t bf12_encoded_bytes(uint32_t n_values, uint32_t n_exc) {
   return kBf12HeaderBytes + (uint64_t)n_values + (uint64_t)n_values / 2 + (uint64_t)n_exc * sizeof(Bf12Exception);
 }
 
+// BF11: two-level exponent code, ~11 bits/value for weight-like data (a
+// Gaussian's exponent carries ~2.5 bits of entropy; BF12 spends 4).
+//   sm byte       = s << 7 | m                                     (8 bits / value)
+//   primary code  = index of e in prim[0..2]; 3 = escape           (2 bits / value)
+//   secondary     = e - sec_base for escaped values, 15 = exception (4 bits / escape)
+// With the three most frequent exponents primary, ~24% of Gaussian values
+// escape: 8 + 2 + 0.24 * 4 ~= 11 bits (0.69x). The secondary nibbles of a block
+// are stored in value order; a 512-value wave group (one wave, 8 values per lane)
+// finds its first nibble from a per-tile base + a u16 per group, and each lane
+// its own from a wave prefix count of escapes (4 ballots + mbcnt on gfx950), so
+// every value decodes at a fixed cost with no serial dependency.
+// Layout (offsets from the block start, recorded in the header):
+//   [0, 512)            Bf11Header
+//   off_prim            n/4 bytes of 2-bit codes (value i in bits 2(i%4) of byte i/4)
+//   off_wg              u16 per 512-value group: nibble offset from its tile's sec_tile base
+//   off_sec             secondary nibbles (value order, low nibble first) + 8 B pad
+//   off_exc             Bf12Exception list grouped by 32768-value tile
+// The sm plane sits right after the header at 512.
+constexpr uint32_t kBf11Magic = 0x31314642;  // "BF11"
+constexpr uint32_t kBf11HeaderBytes = 512;
+constexpr uint32_t kBf11Group = 512;         // values per wave group (64 lanes x 8)
+struct Bf11Header {
+  uint32_t magic;
+  uint32_t n_values;
+  uint32_t n_exc;
+  uint32_t prim;       // exponents of primary codes 0..2 in bytes 0..2
+  uint32_t sec_base;   // exponent of secondary code 0
+  uint32_t n_sec;      // secondary nibbles
+  uint32_t off_prim, off_wg, off_sec, off_exc;
+  uint32_t exc_off[kBf12MaxTiles + 1];
+  uint32_t sec_tile[kBf12MaxTiles + 1];
+  uint32_t reserved[(kBf11HeaderBytes / 4) - 10 - 2 * (kBf12MaxTiles + 1)];
+};
+static_assert(sizeof(Bf11Header) == kBf11HeaderBytes, "BF11 header is 512 bytes");
+
+// Encode n_values bf16 (n_values a multiple of 8, <= 1 Mi) as a BF11 block.
+// Returns the encoded size, or 0 when it does not fit `cap`.
+uint64_t bf11_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);
+bool bf11_decode(const uint8_t* in, uint16_t* out, uint32_t n_values);
+
 // Encode n_values bf16 (n_values even) into `out` (capacity `cap` bytes).
 // Returns the encoded size, or 0 when the block does not compress into `cap`.
 uint64_t bf12_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);
@@ -78,8 +118,9 @@ struct Bf12StreamHeader {
 struct Bf12StreamChunk {
   uint64_t offset;
   uint32_t n_values;
-  uint32_t encoded;  // 1 = BF12 block, 0 = raw bf16
+  uint32_t encoded;  // 0 = raw bf16, 1 = BF12 block, 2 = BF11 block
 };
+enum class PackFormat : uint32_t { BF12 = 1, BF11 = 2 };
 static_assert(sizeof(Bf12StreamHeader) == 32 && sizeof(Bf12StreamChunk) == 16, "stream layout");
 inline uint64_t bf12_stream_head_bytes(uint64_t nchunks) { return (32 + 16 * nchunks + 255) & ~255ull; }
 inline uint64_t bf12_pack_bound(uint64_t n_values, uint32_t chunk_values) {
@@ -87,9 +128,10 @@ inline uint64_t bf12_pack_bound(uint64_t n_values, uint32_t chunk_values) {
   return bf12_stream_head_bytes(chunks) + n_values * 2 + chunks * 512;
 }
 // Pack n_values bf16 with `threads` encoder threads into `out` (capacity >=
-// bf12_pack_bound). Returns the stream size, 0 on bad arguments.
+// bf12_pack_bound). Each chunk takes the smallest of {BF11 (when fmt is BF11),
+// BF12, raw}. Returns the stream size, 0 on bad arguments.
 uint64_t bf12_pack(const uint16_t* in, uint64_t n_values, uint32_t chunk_values, uint8_t* out, uint64_t cap,
-                   unsigned threads);
+                   unsigned threads, PackFormat fmt = PackFormat::BF12);
 // Reference unpack of a whole stream (CPU).
 bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n_values);
 

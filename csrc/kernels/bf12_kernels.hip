@@ -128,6 +128,105 @@ hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgr
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// BF11 tile decode (codec.hpp): one 32768-value tile of a BF11 block, HBM ->
+// HBM. Each wave owns 16 of the tile's 64 wave groups (512 values; 8 per lane).
+// Phase 1 issues every sign|mantissa (8 B) and primary-code (2 B) load; phase 2
+// turns each lane's escape count into its first secondary nibble with a wave
+// prefix count (4 ballots + mbcnt - no LDS, no barrier) and issues the nibble
+// loads; phase 3 rebuilds the bf16 words and stores 16 B per lane.
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Escapes before this lane in the wave, for per-lane counts 0..8.
+__device__ __forceinline__ uint32_t wave_excl_prefix8(uint32_t cnt) {
+  const uint64_t b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u), b3 = __ballot(cnt & 8u);
+  return mbcnt64(b0) + 2u * mbcnt64(b1) + 4u * mbcnt64(b2) + 8u * mbcnt64(b3);
+}
+
+__device__ __forceinline__ uint32_t bf11_word(uint32_t sm, uint32_t pcv, uint32_t& nibs, uint32_t prim,
+                                              uint32_t sbase, int k) {
+  const uint32_t c = (pcv >> (2 * k)) & 3u;
+  const bool esc = c == 3u;
+  const uint32_t e = esc ? ((sbase + (nibs & 15u)) & 0xFFu) : ((prim >> (8u * c)) & 0xFFu);
+  nibs = esc ? nibs >> 4 : nibs;
+  const uint32_t b = (sm >> (8 * (k & 3))) & 0xFFu;
+  return ((b & 0x80u) << 8) | (e << 7) | (b & 0x7Fu);
+}
+
+__device__ __forceinline__ void bf11_decode_tile(const uint8_t* __restrict__ blk, uint16_t* __restrict__ out,
+                                                 uint32_t t) {
+  const Bf11Header* h = reinterpret_cast<const Bf11Header*>(blk);
+  const uint32_t n = h->n_values;
+  const uint32_t prim = h->prim, sbase = h->sec_base;
+  const uint32_t tile_sec = h->sec_tile[t];
+  const uint8_t* sm_plane = blk + kBf11HeaderBytes;
+  const uint16_t* pc_plane = reinterpret_cast<const uint16_t*>(blk + h->off_prim);
+  const uint16_t* wg_plane = reinterpret_cast<const uint16_t*>(blk + h->off_wg);
+  const uint32_t* sec32 = reinterpret_cast<const uint32_t*>(blk + h->off_sec);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int kPer = kBf12Tile / kBf11Group / (kDecThreads / 64);  // 16 groups per wave
+  u32x2 smv[kPer];
+  uint32_t pcv[kPer];
+  uint32_t valid = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const uint32_t g = t * (kBf12Tile / kBf11Group) + (uint32_t)u * (kDecThreads / 64) + wave;
+    const uint32_t v0 = g * kBf11Group + lane * 8u;
+    pcv[u] = 0;
+    if (v0 < n) {
+      smv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(sm_plane + v0));
+      pcv[u] = __builtin_nontemporal_load(pc_plane + (v0 >> 3));
+      valid |= 1u << u;
+    }
+  }
+  uint32_t nib[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const uint32_t g = t * (kBf12Tile / kBf11Group) + (uint32_t)u * (kDecThreads / 64) + wave;
+    const uint32_t escm = pcv[u] & (pcv[u] >> 1) & 0x5555u;
+    const uint32_t pre = wave_excl_prefix8((uint32_t)__builtin_popcount(escm));  // every lane joins
+    nib[u] = 0;
+    if ((valid >> u) & 1u) {
+      const uint32_t idx = tile_sec + (uint32_t)wg_plane[g] + pre;
+      if (escm) {
+        const uint32_t q = idx >> 3, sh = (idx & 7u) * 4u;
+        const uint64_t w = ((uint64_t)sec32[q + 1] << 32) | sec32[q];
+        nib[u] = (uint32_t)(w >> sh);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    if ((valid >> u) & 1u) {
+      const uint32_t g = t * (kBf12Tile / kBf11Group) + (uint32_t)u * (kDecThreads / 64) + wave;
+      const uint32_t v0 = g * kBf11Group + lane * 8u;
+      uint32_t nb = nib[u];
+      u32x4 o;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const uint32_t sm = smv[u][p >> 1];
+        const uint32_t lo = bf11_word(sm, pcv[u], nb, prim, sbase, 2 * p);
+        const uint32_t hi = bf11_word(sm, pcv[u], nb, prim, sbase, 2 * p + 1);
+        o[p] = lo | (hi << 16);
+      }
+      __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + v0));
+    }
+  }
+  const uint32_t e0 = h->exc_off[t], e1 = h->exc_off[t + 1];
+  if (e1 > e0) {  // uniform: only tiles with exceptions pay the barrier
+    __syncthreads();
+    const Bf12Exception* exc = reinterpret_cast<const Bf12Exception*>(blk + h->off_exc);
+    for (uint32_t k = e0 + threadIdx.x; k < e1; k += kDecThreads) {
+      Bf12Exception ex = exc[k];
+      out[ex.index] = ex.bits;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // HBM-resident streams: unpack a packed tensor (codec.hpp "BFS1") into a bf16
 // staging buffer right before use. Both sides are HBM, so there is no PCIe
@@ -155,6 +254,10 @@ __global__ void __launch_bounds__(kDecThreads)
       const uint16_t* s16 = reinterpret_cast<const uint16_t*>(blk) + lo;
       uint16_t* d16 = reinterpret_cast<uint16_t*>(out) + c * chunk_values + lo;
       for (uint32_t k = (cnt & ~7u) + threadIdx.x; k < cnt; k += kDecThreads) d16[k] = s16[k];
+      continue;
+    }
+    if (ch.encoded == 2) {
+      bf11_decode_tile(blk, reinterpret_cast<uint16_t*>(out) + c * chunk_values, t);
       continue;
     }
     const Bf12Header* h = reinterpret_cast<const Bf12Header*>(blk);

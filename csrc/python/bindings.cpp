@@ -567,16 +567,30 @@ PYBIND11_MODULE(_ogkm, m) {
   });
   // Self-describing BF12 streams of whole tensors (ops/bf12.py).
   m.def("bf12_pack_bound", [](uint64_t n, uint32_t chunk_values) { return bf12_pack_bound(n, chunk_values); });
+  m.def("bf11_encode", [](py::bytes raw) {
+    std::string s = raw;
+    std::string out((size_t)kBlockSize + kBf11HeaderBytes, '\0');
+    uint64_t n = bf11_encode((const uint16_t*)s.data(), (uint32_t)(s.size() / 2), (uint8_t*)out.data(), out.size());
+    out.resize(n);
+    return py::bytes(out);
+  });
+  m.def("bf11_decode", [](py::bytes enc, uint32_t n_values) {
+    std::string s = enc;
+    std::string out((size_t)n_values * 2, '\0');
+    if (!bf11_decode((const uint8_t*)s.data(), (uint16_t*)out.data(), n_values)) throw StatusError("bf11_decode: bad block");
+    return py::bytes(out);
+  });
   m.def("bf12_pack", [](uint64_t src, uint64_t n_values, uint64_t dst, uint64_t cap, uint32_t chunk_values,
-                        unsigned threads) {
+                        unsigned threads, uint32_t fmt) {
     uint64_t total;
     {
       py::gil_scoped_release nogil;
-      total = bf12_pack((const uint16_t*)src, n_values, chunk_values, (uint8_t*)dst, cap, threads);
+      total = bf12_pack((const uint16_t*)src, n_values, chunk_values, (uint8_t*)dst, cap, threads, (PackFormat)fmt);
     }
     if (!total) throw StatusError("bf12_pack: bad arguments or buffer too small");
     return total;
-  });
+  }, py::arg("src"), py::arg("n_values"), py::arg("dst"), py::arg("cap"), py::arg("chunk_values"),
+     py::arg("threads"), py::arg("fmt") = 1);
   m.def("bf12_unpack_host", [](uint64_t src, uint64_t dst, uint64_t n_values) {
     bool ok;
     {

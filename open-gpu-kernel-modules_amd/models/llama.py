@@ -102,7 +102,7 @@ class TieredLlama:
     def __init__(self, cfg: LlamaConfig, batch: int, context: int, max_new_tokens: int = 64, oversub: float = 2.0,
                  device: int = 0, tp_rank: int = 0, tp_world: int = 1, seed: int = 0, lookahead: int = 2,
                  hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
-                 packed: bool = True, weight_format: str = "bf12"):
+                 packed: bool = True, weight_format: str = "bf11"):
         assert cfg.n_heads % tp_world == 0 and cfg.n_kv_heads % tp_world == 0 and cfg.ffn_dim % tp_world == 0
         assert cfg.vocab % tp_world == 0
         self.cfg, self.B, self.ctx = cfg, batch, context
@@ -136,11 +136,12 @@ class TieredLlama:
         # staging buffer is carved out of the same HBM budget. "bf16": raw
         # weights; with ``packed`` the runtime keeps streamed host copies BF12 and
         # decodes them inside the H2D copy kernel (RANGE_PACKED_BF16).
-        if weight_format not in ("bf12", "bf16"):
-            raise ValueError("weight_format must be 'bf12' or 'bf16'")
+        if weight_format not in ("bf11", "bf12", "bf16"):
+            raise ValueError("weight_format must be 'bf11', 'bf12' or 'bf16'")
         self.wfmt = weight_format
+        self.wpacked = weight_format in ("bf11", "bf12")   # weights rest packed in every tier
         self.packed = packed and weight_format == "bf16"
-        self.stage_bytes = chunks(max(self.layer_bytes, self.head_bytes)) if weight_format == "bf12" else 0
+        self.stage_bytes = chunks(max(self.layer_bytes, self.head_bytes)) if self.wpacked else 0
         self.arena_bytes = self.budget - self.stage_bytes
         lib.init_device(device, self.arena_bytes)
         self.pinfo: dict = {}
@@ -148,9 +149,9 @@ class TieredLlama:
         host = rt.Loc.host()
         t0 = time.perf_counter()
         self._seed, self._std = seed, init_std
-        if weight_format == "bf12":
+        if self.wpacked:
             # The packed size of layer 0 sizes the plan (all layers share one distribution).
-            first, info0 = bf12.pack(self._gen_layer(0))
+            first, info0 = bf12.pack(self._gen_layer(0), fmt=weight_format)
             ratio = info0.nbytes / (self.layer_bytes)
             self.res_layer_bytes = _al(int(self.layer_bytes * ratio * 1.002) + 4096)
             self.res_head_bytes = _al(int(self.head_bytes * ratio * 1.002) + 4096)
@@ -180,8 +181,8 @@ class TieredLlama:
         self.kv.set_preferred_location(gpu)
         self.layers = []
         for i in range(cfg.n_layers):
-            if weight_format == "bf12":
-                stream, info = (first, info0) if i == 0 else bf12.pack(self._gen_layer(i))
+            if self.wpacked:
+                stream, info = (first, info0) if i == 0 else bf12.pack(self._gen_layer(i), fmt=weight_format)
                 b = rt.malloc_managed(info.nbytes, f"layer{i}", cpu_view=False)
                 self.pinfo[("layer", i)] = info
             else:
@@ -193,8 +194,8 @@ class TieredLlama:
             del stream
         first = None
         head = self._gen_head()
-        if weight_format == "bf12":
-            stream, info = bf12.pack(head)
+        if self.wpacked:
+            stream, info = bf12.pack(head, fmt=weight_format)
             self.head = rt.malloc_managed(info.nbytes, "lm_head", cpu_view=False)
             self.pinfo[("head", 0)] = info
         else:
@@ -207,7 +208,7 @@ class TieredLlama:
         if not self.fake:
             torch.cuda.synchronize(self.dev)
         self.stage = (torch.empty(self.stage_bytes // 2, dtype=torch.bfloat16, device=self.tdev)
-                      if weight_format == "bf12" else None)
+                      if self.wpacked else None)
         self.final_norm = torch.ones(cfg.dim, dtype=torch.bfloat16, device=self.tdev)
         self.cos, self.sin = D.rope_tables(hd, self.T, cfg.rope_theta, self.tdev)
         # KV cache: leased for the model's lifetime (hot, written every step)
@@ -322,7 +323,7 @@ class TieredLlama:
         """The bf16 bytes of a layer / head as stored (unpacked on the host) - for
         reference numerics."""
         raw = self._buf(key).read()
-        if self.wfmt == "bf12":
+        if self.wpacked:
             return bf12.unpack_host(raw, self.pinfo[key]).view(torch.uint8)
         return raw
 
@@ -354,7 +355,7 @@ class TieredLlama:
             self._prefetch_ahead()
         lease = self._buf(key).acquire(self.dev, rt.READ)
         lease.wait(0 if self.fake else None)
-        if self.wfmt == "bf12":
+        if self.wpacked:
             bf12.unpack_into(self.stage, lease.dptr, self.pinfo[key], self.dev, 0 if self.fake else None)
             lease.release(0 if self.fake else None)
             return None, self.stage.data_ptr()

@@ -9,9 +9,16 @@ stays resident (the managed footprint the runtime moves is the packed one).
 The unpack (csrc/kernels/bf12_kernels.hip k_bf12_unpack) runs HBM->HBM at a
 few TB/s, i.e. well under a millisecond per 70B layer.
 
-Format: codec.hpp "BFS1" stream = header + chunk table + 256-B aligned chunks
-(each a BF12 block: sign|mantissa bytes + 4-bit exponent codes relative to a
-per-chunk base + an exception list for escaped exponents; or raw bf16).
+Format: codec.hpp "BFS1" stream = header + chunk table + 256-B aligned chunks,
+each one of
+  * BF11 (default): sign|mantissa bytes + a 2-bit primary exponent code (the
+    chunk's three most frequent exponents) + a 4-bit secondary code only for the
+    values that escape it, ~11 bits/value (~0.69x) for weight-like data;
+  * BF12: sign|mantissa bytes + 4-bit exponent codes relative to a per-chunk
+    base, 12 bits/value (0.75x);
+  * raw bf16 (incompressible chunks / odd tails).
+All carry an exception list for exponents outside their code space, so every
+bf16 bit pattern round-trips.
 """
 from __future__ import annotations
 
@@ -44,9 +51,13 @@ def _threads() -> int:
     return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
 
 
-def pack(t: torch.Tensor, chunk_values: int = CHUNK_VALUES, out: torch.Tensor | None = None
+FORMATS = {"bf12": 1, "bf11": 2}
+
+
+def pack(t: torch.Tensor, chunk_values: int = CHUNK_VALUES, out: torch.Tensor | None = None, fmt: str = "bf11"
          ) -> tuple[torch.Tensor, PackedInfo]:
-    """Pack a bf16 tensor (any device; encoded on the host) -> (uint8 CPU stream, info)."""
+    """Pack a bf16 tensor (any device; encoded on the host) -> (uint8 CPU stream, info).
+    ``fmt``: "bf11" (per chunk the smaller of BF11 / BF12 / raw) or "bf12"."""
     if t.dtype != torch.bfloat16:
         raise TypeError("pack expects bf16")
     src = t.detach().reshape(-1).contiguous().cpu()
@@ -54,7 +65,7 @@ def pack(t: torch.Tensor, chunk_values: int = CHUNK_VALUES, out: torch.Tensor | 
     bound = lib.bf12_pack_bound(n, chunk_values)
     if out is None or out.numel() < bound:
         out = torch.empty(bound, dtype=torch.uint8)
-    total = lib.bf12_pack(src.data_ptr(), n, out.data_ptr(), bound, chunk_values, _threads())
+    total = lib.bf12_pack(src.data_ptr(), n, out.data_ptr(), bound, chunk_values, _threads(), FORMATS[fmt])
     return out[:total], info_of(out[:64])
 
 

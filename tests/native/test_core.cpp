@@ -136,6 +136,44 @@ static void test_codec() {
   CHECK(bf12_encode(in.data(), n, enc.data(), enc.size()) == 0);
 }
 
+static void test_codec_bf11() {
+  std::mt19937 rng(11);
+  std::normal_distribution<float> nd(0.f, 0.02f);
+  for (uint32_t n : {1u << 20, 8u, 520u, 32768u + 512u + 8u}) {
+    std::vector<uint16_t> in(n), out(n);
+    for (uint32_t i = 0; i < n; ++i) {
+      float f = nd(rng);
+      uint32_t bits;
+      memcpy(&bits, &f, 4);
+      in[i] = (uint16_t)(bits >> 16);
+    }
+    const uint16_t specials[] = {0x0000, 0x8000, 0x7F80, 0xFF80, 0x7FC0, 0x0001, 0x3F80, 0xC2F7};
+    for (uint32_t i = 0; i < 8 && i * 61 < n; ++i) in[i * 61] = specials[i];
+    std::vector<uint8_t> enc(2ull * n + 4096);
+    uint64_t sz = bf11_encode(in.data(), n, enc.data(), enc.size());
+    CHECK(sz > 0);
+    if (n == (1u << 20)) CHECK(sz < (uint64_t)(0.70 * 2 * n));
+    std::fill(out.begin(), out.end(), 0xAAAA);
+    CHECK(bf11_decode(enc.data(), out.data(), n));
+    CHECK(memcmp(in.data(), out.data(), 2ull * n) == 0);
+  }
+  // streams: BF11 chunks, an incompressible chunk and a raw odd tail
+  const uint64_t n = (3u << 20) + 6;
+  std::vector<uint16_t> in(n), out(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    float f = nd(rng);
+    uint32_t bits;
+    memcpy(&bits, &f, 4);
+    in[i] = (uint16_t)(bits >> 16);
+  }
+  for (uint64_t i = 1u << 20; i < (2u << 20); ++i) in[i] = (uint16_t)rng();
+  std::vector<uint8_t> st(bf12_pack_bound(n, 1u << 20));
+  uint64_t total = bf12_pack(in.data(), n, 1u << 20, st.data(), st.size(), 4, PackFormat::BF11);
+  CHECK(total > 0 && total < 2 * n);
+  CHECK(bf12_unpack(st.data(), out.data(), n));
+  CHECK(memcmp(in.data(), out.data(), 2 * n) == 0);
+}
+
 static void test_lockcheck() {
   lockcheck::set_enabled(true);
   uint64_t v0 = lockcheck::violations();
@@ -215,6 +253,7 @@ int main() {
   RUN(test_arena_alloc_reserve);
   RUN(test_arena_random);
   RUN(test_codec);
+  RUN(test_codec_bf11);
   RUN(test_lockcheck);
   RUN(test_runtime_end_to_end);
   if (g_fail) {

@@ -1,0 +1,52 @@
+"""Lossless weight codecs (csrc/core/codec.cpp): BF12 and BF11 blocks and the
+self-describing streams built from them must round-trip every bf16 bit pattern.
+CPU only; the GPU decoders are checked bit-for-bit against these encoders in
+tests/test_gpu_runtime.py."""
+from __future__ import annotations
+
+import pytest
+import torch
+from hypothesis import given, settings, strategies as st
+
+from ogkm.ops import bf12
+
+
+def _roundtrip(ref: torch.Tensor, fmt: str, chunk: int = bf12.CHUNK_VALUES):
+    stream, info = bf12.pack(ref, chunk_values=chunk, fmt=fmt)
+    out = bf12.unpack_host(stream, info)
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+    return info
+
+
+@pytest.mark.parametrize("std", [0.02, 1.0, 1e-3, 300.0])
+def test_bf11_ratio_and_exactness_gaussian(std):
+    torch.manual_seed(1)
+    ref = (torch.randn((2 << 20) + 8) * std).to(torch.bfloat16)
+    i11 = _roundtrip(ref, "bf11")
+    i12 = _roundtrip(ref, "bf12")
+    assert i11.ratio < 0.70 < 0.75 < i12.ratio < 0.76
+
+
+def test_specials_and_exceptions_every_tile():
+    torch.manual_seed(2)
+    ref = (torch.randn(1 << 20) * 0.02).to(torch.bfloat16)
+    specials = torch.tensor([0.0, -0.0, float("inf"), float("-inf"), float("nan"), 3.0e38, 1e-40, -2.5, 1.0],
+                            dtype=torch.bfloat16)
+    for t in range(32):  # one burst of out-of-code-space exponents in every 32768-value tile
+        ref[t * 32768 + 100:t * 32768 + 109] = specials
+    _roundtrip(ref, "bf11")
+
+
+def test_incompressible_falls_back():
+    ref = torch.randint(-32768, 32767, (1 << 20,), dtype=torch.int16).view(torch.bfloat16)
+    info = _roundtrip(ref, "bf11")
+    assert info.ratio <= 1.001
+
+
+@settings(max_examples=40, deadline=None)
+@given(n=st.integers(1, 40000).map(lambda k: 2 * k), std=st.sampled_from([0.02, 1.0, 1e-30, 1e30]),
+       chunk=st.sampled_from([8192, 16384, 1 << 20]), seed=st.integers(0, 2**31 - 1))
+def test_bf11_property_roundtrip(n, std, chunk, seed):
+    g = torch.Generator().manual_seed(seed)
+    ref = (torch.randn(n, generator=g) * std).to(torch.bfloat16)
+    _roundtrip(ref, "bf11", chunk)

@@ -58,14 +58,15 @@ def test_streaming_matches_plan_runtime_packed(fake_rt):
     m.close()
 
 
-def test_streaming_matches_plan_hbm_packed(fake_rt):
-    """bf12 weights: packed in every tier, unpacked into the staging buffer per layer."""
+@pytest.mark.parametrize("fmt,ratio", [("bf12", 0.8), ("bf11", 0.74)])
+def test_streaming_matches_plan_hbm_packed(fake_rt, fmt, ratio):
+    """bf11/bf12 weights: packed in every tier, unpacked into the staging buffer per layer."""
     lib.shutdown()
     rt.init("fake", fake_devices=1, fake_hbm_mb=512, lock_check=1, host_budget_mb=1024)
     cfg = llama.CONFIGS["small"]
-    m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=8, oversub=2.0, lookahead=1, weight_format="bf12")
+    m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=8, oversub=2.0, lookahead=1, weight_format=fmt)
     assert 1.9 < m.footprint / m.budget < 2.1
-    assert m.res_layer_bytes < 0.8 * m.layer_bytes
+    assert m.res_layer_bytes < ratio * m.layer_bytes
     tok = torch.tensor([1, 2])
     tok = m.step(tok)
     tok = m.step(tok)
@@ -85,7 +86,7 @@ def test_streaming_matches_plan_hbm_packed(fake_rt):
 def test_bf12_weights_bit_identical_to_bf16(fake_rt):
     cfg = llama.CONFIGS["tiny"]
     out = {}
-    for fmt in ("bf16", "bf12"):
+    for fmt in ("bf16", "bf12", "bf11"):
         m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=4, oversub=1.5, lookahead=1, seed=9,
                               weight_format=fmt)
         m.keep_logits = True
@@ -96,8 +97,9 @@ def test_bf12_weights_bit_identical_to_bf16(fake_rt):
             logs.append(m.last_logits.clone())
         out[fmt] = logs
         m.close()
-    for a, b in zip(out["bf16"], out["bf12"]):
-        assert torch.equal(a, b)
+    for fmt in ("bf12", "bf11"):
+        for a, b in zip(out["bf16"], out[fmt]):
+            assert torch.equal(a, b)
 
 
 def _free_port() -> int:
