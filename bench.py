@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--context", type=int, default=1024)
     ap.add_argument("--oversub", type=float, default=2.0)
-    ap.add_argument("--lookahead", type=int, default=2)
+    ap.add_argument("--lookahead", type=int, default=int(os.environ.get("OGKM_LOOKAHEAD", "2")))
     ap.add_argument("--no-aux", action="store_true", help="skip the HBM<->host/CXL bandwidth probe")
     ap.add_argument("--weights", choices=("bf11", "bf12", "bf16"), default="bf11",
                     help="bf11/bf12: weights rest losslessly packed (~0.69x / 0.75x) in every tier (HBM included) "

@@ -256,6 +256,14 @@ class FakeBackend : public Backend {
     run(s, [src, dst, n] { bf12_unpack((const uint8_t*)src, (uint16_t*)dst, n); });
     return Status::OK;
   }
+  Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {
+    run(s, [a, mode] { dgemm_cpu(a, mode != DGEMM_W_RAW); });
+    return Status::OK;
+  }
+  Status dgemm_reduce(int, const DGemmReduceArgs& a, void* s) override {
+    run(s, [a] { dgemm_reduce_cpu(a); });
+    return Status::OK;
+  }
   Status gather_pages(int, const PageListDesc& d, void* s) override {
     std::vector<uint32_t> idx(d.idx, d.idx + d.npages);
     PageListDesc dd = d;

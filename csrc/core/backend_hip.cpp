@@ -125,9 +125,23 @@ class HipBackend : public Backend {
 
   Status host_register(void* p, size_t bytes) override {
     HIPCHK(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    std::lock_guard<std::mutex> g(reg_m_);
+    regs_[(uint64_t)p] = bytes;
     return Status::OK;
   }
-  void host_unregister(void* p) override { (void)hipHostUnregister(p); }
+  void host_unregister(void* p) override {
+    (void)hipHostUnregister(p);
+    std::lock_guard<std::mutex> g(reg_m_);
+    regs_.erase((uint64_t)p);
+  }
+  // Bytes from `a` to the end of the host registration that contains it (0 = none).
+  uint64_t reg_room(uint64_t a) {
+    std::lock_guard<std::mutex> g(reg_m_);
+    auto it = regs_.upper_bound(a);
+    if (it == regs_.begin()) return 0;
+    --it;
+    return a < it->first + it->second ? it->first + it->second - a : 0;
+  }
   Status host_alloc_coherent(size_t bytes, void** p) override {
     HIPCHK(hipHostMalloc(p, bytes, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
     memset(*p, 0, bytes);
@@ -191,9 +205,20 @@ class HipBackend : public Backend {
 
   Status copy_batch(int dev, const CopyDesc* d, size_t n, void* s, int engine) override {
     if (n == 0) return Status::OK;
-    if (engine == 1) {  // SDMA comparator
-      for (size_t i = 0; i < n; ++i)
-        HIPCHK(hipMemcpyAsync((void*)d[i].dst, (const void*)d[i].src, d[i].bytes, hipMemcpyDefault, (hipStream_t)s));
+    if (engine == 1) {  // SDMA: split at host-registration boundaries (one hipMemcpy per allocation)
+      for (size_t i = 0; i < n; ++i) {
+        uint64_t dst = d[i].dst, src = d[i].src, left = d[i].bytes;
+        while (left) {
+          uint64_t len = left;
+          uint64_t rs = reg_room(src), rd = reg_room(dst);
+          if (rs && rs < len) len = rs;
+          if (rd && rd < len) len = rd;
+          HIPCHK(hipMemcpyAsync((void*)dst, (const void*)src, len, hipMemcpyDefault, (hipStream_t)s));
+          dst += len;
+          src += len;
+          left -= len;
+        }
+      }
       return Status::OK;
     }
     uint32_t piece = (uint32_t)(config().copy_piece_kb * 1024);
@@ -241,6 +266,17 @@ class HipBackend : public Backend {
   Status unpack_bf12_stream(int, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values, uint64_t,
                             void* s, uint32_t workgroups) override {
     HIPCHK(launch_bf12_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s));
+    launches_++;
+    return Status::OK;
+  }
+
+  Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {
+    HIPCHK(launch_dgemm(a, mode, (hipStream_t)s));
+    launches_++;
+    return Status::OK;
+  }
+  Status dgemm_reduce(int, const DGemmReduceArgs& a, void* s) override {
+    HIPCHK(launch_dgemm_reduce(a, (hipStream_t)s));
     launches_++;
     return Status::OK;
   }
@@ -364,7 +400,8 @@ class HipBackend : public Backend {
 
   int ndev_;
   std::string last_err_;
-  std::mutex ev_m_, df_m_;
+  std::mutex ev_m_, df_m_, reg_m_;
+  std::map<uint64_t, uint64_t> regs_;  // host registrations: base -> bytes
   std::vector<void*> free_events_[64];
   std::map<void*, int> ev_dev_;
   std::map<void*, void*> ipc_base_;  // opened IPC pointer -> mapped allocation base

@@ -132,15 +132,17 @@ uint64_t bf11_encode(const uint16_t* in, uint32_t n, uint8_t* out, uint64_t cap)
   h.prim = prim[0] | (prim[1] << 8) | (prim[2] << 16);
   h.sec_base = sbase;
   h.n_sec = n_sec;
-  h.off_prim = kBf11HeaderBytes + n;
-  h.off_wg = (uint32_t)al8(h.off_prim + n / 4);
-  h.off_sec = (uint32_t)al8(h.off_wg + 2ull * ngroups);
+  const Bf11Layout lay = bf11_layout(n);
+  h.off_prim = lay.off_prim;
+  h.off_wg = lay.off_wg;
+  h.off_sec = lay.off_sec;
+  (void)ngroups;
   h.off_exc = (uint32_t)al8(h.off_sec + (n_sec + 1) / 2 + 8);
   const uint64_t need = (uint64_t)h.off_exc + (uint64_t)n_exc * sizeof(Bf12Exception);
   if (need > cap) return 0;
   uint8_t* sm = out + kBf11HeaderBytes;
   uint8_t* pc = out + h.off_prim;
-  uint16_t* wg = reinterpret_cast<uint16_t*>(out + h.off_wg);
+  uint32_t* wg = reinterpret_cast<uint32_t*>(out + h.off_wg);
   uint8_t* sec = out + h.off_sec;
   Bf12Exception* exc = reinterpret_cast<Bf12Exception*>(out + h.off_exc);
   memset(pc, 0, n / 4);
@@ -152,7 +154,7 @@ uint64_t bf11_encode(const uint16_t* in, uint32_t n, uint8_t* out, uint64_t cap)
       h.exc_off[i / kBf12Tile] = e_out;
       h.sec_tile[i / kBf12Tile] = nib;
     }
-    if (i % kBf11Group == 0) wg[i / kBf11Group] = (uint16_t)(nib - h.sec_tile[i / kBf12Tile]);
+    if (i % kBf11Group == 0) wg[i / kBf11Group] = nib;
     const uint16_t v = in[i];
     const uint32_t e = (v >> 7) & 0xFF;
     sm[i] = (uint8_t)(((v >> 8) & 0x80) | (v & 0x7F));
@@ -202,6 +204,39 @@ bool bf11_decode(const uint8_t* in, uint16_t* out, uint32_t n) {
   return true;
 }
 
+void bf11_decode_group(const uint8_t* in, uint32_t v, uint16_t* out) {
+  Bf11Header h;
+  memcpy(&h, in, sizeof h);
+  const uint8_t* sm = in + kBf11HeaderBytes;
+  const uint8_t* pc = in + h.off_prim;
+  const uint8_t* sec = in + h.off_sec;
+  uint32_t nib;
+  memcpy(&nib, in + h.off_wg + 4ull * (v / kBf11Group), 4);
+  const uint32_t cnt = std::min<uint32_t>(kBf11Group, h.n_values - v);
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const uint32_t i = v + k;
+    const uint32_t c = (pc[i >> 2] >> (2 * (i & 3))) & 3;
+    uint32_t e;
+    bool exc = false;
+    if (c < 3) {
+      e = (h.prim >> (8 * c)) & 0xFF;
+    } else {
+      const uint32_t sc = (sec[nib >> 1] >> (4 * (nib & 1))) & 0xF;
+      exc = sc == 15;
+      e = (h.sec_base + sc) & 0xFF;
+      ++nib;
+    }
+    const uint32_t s = sm[i];
+    out[k] = (uint16_t)(((s & 0x80) << 8) | (e << 7) | (s & 0x7F));
+    if (exc) {
+      const Bf12Exception* ex = reinterpret_cast<const Bf12Exception*>(in + h.off_exc);
+      const uint32_t t = i / kBf12Tile;
+      for (uint32_t q = h.exc_off[t]; q < h.exc_off[t + 1]; ++q)
+        if (ex[q].index == i) out[k] = ex[q].bits;
+    }
+  }
+}
+
 uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_t* out, uint64_t cap,
                    unsigned threads, PackFormat fmt) {
   if (!n || chunk_values < 8192 || (chunk_values & (chunk_values - 1)) || chunk_values > kBf12Tile * kBf12MaxTiles)
@@ -220,7 +255,10 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_
       uint8_t* dst = out + head + c * slot;
       uint64_t e = 0;
       uint32_t kind = 0;
-      if (cnt % 8 == 0 && fmt == PackFormat::BF11) {
+      if (cnt % 8 == 0 && fmt == PackFormat::BF11_STRICT) {
+        e = bf11_encode(in + lo, cnt, dst, (uint64_t)cnt * 2);
+        kind = e ? 2 : 0;
+      } else if (cnt % 8 == 0 && fmt == PackFormat::BF11) {
         e = bf11_encode(in + lo, cnt, dst, (uint64_t)cnt * 2);
         kind = e ? 2 : 0;
         // BF11 wins for weight-like data; keep BF12 where it is smaller
@@ -235,7 +273,7 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_
           }
         }
       }
-      if (!e && cnt % 8 == 0) {
+      if (!e && cnt % 8 == 0 && fmt != PackFormat::BF11_STRICT) {
         e = bf12_encode(in + lo, cnt, dst, (uint64_t)cnt * 2);
         kind = e ? 1 : 0;
       }

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "ogkm/common.hpp"
+#include "ogkm/dgemm.hpp"
 
 namespace ogkm {
 
@@ -98,6 +99,9 @@ class Backend {
   // Unpack a device-resident BF12 stream (codec.hpp) of n_values into bf16 at dst.
   virtual Status unpack_bf12_stream(int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
                                     uint64_t n_values, void* stream, uint32_t workgroups) = 0;
+  // Decode GEMM (ogkm/dgemm.hpp): split-K partials, then the fused epilogue.
+  virtual Status dgemm(int dev, const DGemmArgs& a, int mode, void* stream) = 0;
+  virtual Status dgemm_reduce(int dev, const DGemmReduceArgs& a, void* stream) = 0;
   virtual Status gather_pages(int dev, const PageListDesc& d, void* stream) = 0;
   virtual Status scatter_pages(int dev, const PageListDesc& d, void* stream) = 0;
   virtual Status memset32(int dev, uint64_t dst, uint32_t pattern, size_t bytes, void* stream) = 0;

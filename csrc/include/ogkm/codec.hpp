@@ -65,7 +65,7 @@ inline uint64_t bf12_encoded_bytes(uint32_t n_values, uint32_t n_exc) {
 // Layout (offsets from the block start, recorded in the header):
 //   [0, 512)            Bf11Header
 //   off_prim            n/4 bytes of 2-bit codes (value i in bits 2(i%4) of byte i/4)
-//   off_wg              u16 per 512-value group: nibble offset from its tile's sec_tile base
+//   off_wg              u32 per 512-value group: its first secondary nibble (absolute)
 //   off_sec             secondary nibbles (value order, low nibble first) + 8 B pad
 //   off_exc             Bf12Exception list grouped by 32768-value tile
 // The sm plane sits right after the header at 512.
@@ -86,10 +86,32 @@ struct Bf11Header {
 };
 static_assert(sizeof(Bf11Header) == kBf11HeaderBytes, "BF11 header is 512 bytes");
 
+// Plane offsets are a pure function of n_values (readers may compute them
+// instead of loading them from the header: the decode GEMM does, to keep its
+// scalar-load chain short). Only off_exc depends on the data.
+#ifdef __HIPCC__
+#define OGKM_HD __host__ __device__
+#else
+#define OGKM_HD
+#endif
+struct Bf11Layout {
+  uint32_t off_prim, off_wg, off_sec;
+};
+OGKM_HD inline Bf11Layout bf11_layout(uint32_t n) {
+  Bf11Layout l;
+  l.off_prim = kBf11HeaderBytes + n;
+  l.off_wg = (l.off_prim + n / 4 + 7u) & ~7u;
+  l.off_sec = (l.off_wg + 4u * ((n + kBf11Group - 1) / kBf11Group) + 7u) & ~7u;
+  return l;
+}
+
 // Encode n_values bf16 (n_values a multiple of 8, <= 1 Mi) as a BF11 block.
 // Returns the encoded size, or 0 when it does not fit `cap`.
 uint64_t bf11_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);
 bool bf11_decode(const uint8_t* in, uint16_t* out, uint32_t n_values);
+// Decode the 512-value wave group starting at value v (a multiple of 512) of a
+// BF11 block, exceptions included (the decode-GEMM fragment path).
+void bf11_decode_group(const uint8_t* in, uint32_t v, uint16_t* out512);
 
 // Encode n_values bf16 (n_values even) into `out` (capacity `cap` bytes).
 // Returns the encoded size, or 0 when the block does not compress into `cap`.
@@ -120,7 +142,9 @@ struct Bf12StreamChunk {
   uint32_t n_values;
   uint32_t encoded;  // 0 = raw bf16, 1 = BF12 block, 2 = BF11 block
 };
-enum class PackFormat : uint32_t { BF12 = 1, BF11 = 2 };
+// BF11_STRICT: BF11 or raw only (streams read by the decode GEMM, which decodes
+// those two chunk kinds in registers).
+enum class PackFormat : uint32_t { BF12 = 1, BF11 = 2, BF11_STRICT = 3 };
 static_assert(sizeof(Bf12StreamHeader) == 32 && sizeof(Bf12StreamChunk) == 16, "stream layout");
 inline uint64_t bf12_stream_head_bytes(uint64_t nchunks) { return (32 + 16 * nchunks + 255) & ~255ull; }
 inline uint64_t bf12_pack_bound(uint64_t n_values, uint32_t chunk_values) {

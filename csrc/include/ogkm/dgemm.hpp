@@ -1,0 +1,52 @@
+// Decode-GEMM argument blocks shared by the HIP kernels (decode_gemm.hip), the
+// backends (HIP launch / fake CPU reference) and the bindings. No HIP headers.
+#pragma once
+
+#include <cstdint>
+
+namespace ogkm {
+
+// Decode GEMM (csrc/kernels/decode_gemm.hip): part[ks][M][N] = X[M,K] . W[N,K]^T
+// over K split `ks`, with W in fragment order (16x32 MFMA A-tiles, 1 KB each)
+// either as raw bf16 or inside a BF11/raw packed stream (decoded in registers).
+struct DGemmArgs {
+  const uint8_t* w;       // raw: bf16 fragment-ordered weights; packed: stream base
+  uint64_t w_off;         // value offset of this tensor (raw: from w; packed: in the stream's value space)
+  const uint16_t* x;      // [M, K] bf16, row stride ldx (elements, multiple of 8)
+  float* part;            // [ksplit][M][N] f32
+  uint32_t M, N, K, ldx;
+  uint32_t ksplit, klen;  // K range per split (multiple of 32)
+  uint32_t row_blocks;    // ceil(N / 64)
+  uint32_t chunk_shift;   // packed: log2(stream chunk_values)
+  uint32_t unroll;        // K steps per pipelined block (1, 2 or 4; 0 = default)
+};
+// Weight source: raw bf16 fragments; a packed stream with BF11 and raw chunks;
+// a packed stream whose chunks are all BF11 (fast, phase-pipelined path).
+enum DGemmWeights : int { DGEMM_W_RAW = 0, DGEMM_W_PACKED = 1, DGEMM_W_PACKED_BF11 = 2 };
+enum DGemmEpilogue : uint32_t { DGEMM_EPI_STORE = 0, DGEMM_EPI_RESID = 1, DGEMM_EPI_SILU_MUL = 2 };
+struct DGemmReduceArgs {
+  const float* part;
+  uint32_t ksplit, M, N;   // N = columns of part (SILU_MUL: 2 f, gate then up)
+  uint32_t epi;
+  const uint16_t* resid;   // RESID: bf16 [M, ldr]
+  uint32_t ldr, ldo;
+  uint16_t* out;           // bf16 [M, ldo] (may alias resid)
+};
+// Split-K plan: enough waves to fill the chip (>= ~4 per CU over 256 CUs) while
+// keeping each split's K range a multiple of 32.
+inline void dgemm_plan(uint32_t N, uint32_t K, uint32_t target_units, uint32_t* ksplit, uint32_t* klen) {
+  const uint32_t rb = (N / 16 + 3) / 4;
+  uint32_t ks = rb >= target_units ? 1 : (target_units + rb - 1) / rb;
+  const uint32_t ksteps = K / 32;
+  const uint32_t max_ks = ksteps / 4 ? ksteps / 4 : 1;  // >= 128 of K per split
+  if (ks > max_ks) ks = max_ks;
+  uint32_t steps = (ksteps + ks - 1) / ks;
+  *klen = steps * 32;
+  *ksplit = (K + *klen - 1) / *klen;
+}
+
+// CPU reference of k_dgemm / k_dgemm_reduce (fake backend, tests).
+void dgemm_cpu(const DGemmArgs& a, bool packed);
+void dgemm_reduce_cpu(const DGemmReduceArgs& a);
+
+}  // namespace ogkm

@@ -13,6 +13,8 @@
 
 #include <cstdint>
 
+#include "ogkm/dgemm.hpp"
+
 namespace ogkm {
 
 struct KCopyDesc {      // device-side copy descriptor (24 B)
@@ -53,6 +55,10 @@ hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgr
 // at `dst`: one launch, one work item per 32768-value tile of every chunk.
 hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
                               uint32_t workgroups, hipStream_t s);
+
+// Decode GEMM (csrc/kernels/decode_gemm.hip); argument structs in ogkm/dgemm.hpp.
+hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);
+hipError_t launch_dgemm_reduce(const DGemmReduceArgs& a, hipStream_t s);
 
 // Gather `nrows` rows (row_bytes each) of a managed table through its device
 // residency table; misses read zero and are recorded as faults, remote hits are

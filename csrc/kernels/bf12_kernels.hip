@@ -161,10 +161,9 @@ __device__ __forceinline__ void bf11_decode_tile(const uint8_t* __restrict__ blk
   const Bf11Header* h = reinterpret_cast<const Bf11Header*>(blk);
   const uint32_t n = h->n_values;
   const uint32_t prim = h->prim, sbase = h->sec_base;
-  const uint32_t tile_sec = h->sec_tile[t];
   const uint8_t* sm_plane = blk + kBf11HeaderBytes;
   const uint16_t* pc_plane = reinterpret_cast<const uint16_t*>(blk + h->off_prim);
-  const uint16_t* wg_plane = reinterpret_cast<const uint16_t*>(blk + h->off_wg);
+  const uint32_t* wg_plane = reinterpret_cast<const uint32_t*>(blk + h->off_wg);
   const uint32_t* sec32 = reinterpret_cast<const uint32_t*>(blk + h->off_sec);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -191,7 +190,7 @@ __device__ __forceinline__ void bf11_decode_tile(const uint8_t* __restrict__ blk
     const uint32_t pre = wave_excl_prefix8((uint32_t)__builtin_popcount(escm));  // every lane joins
     nib[u] = 0;
     if ((valid >> u) & 1u) {
-      const uint32_t idx = tile_sec + (uint32_t)wg_plane[g] + pre;
+      const uint32_t idx = wg_plane[g] + pre;
       if (escm) {
         const uint32_t q = idx >> 3, sh = (idx & 7u) * 4u;
         const uint64_t w = ((uint64_t)sec32[q + 1] << 32) | sec32[q];

@@ -606,6 +606,40 @@ PYBIND11_MODULE(_ogkm, m) {
           "bf12_unpack");
   }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("nchunks"), py::arg("chunk_values"),
      py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0);
+  // Decode GEMM + fused epilogue in one call: out = epi(X . W^T) (ops/dgemm.py).
+  m.def("dgemm_plan", [](uint32_t N, uint32_t K, uint32_t target_units) {
+    uint32_t ks, kl;
+    dgemm_plan(N, K, target_units, &ks, &kl);
+    return py::make_tuple(ks, kl);
+  });
+  m.def("dgemm", [](int dev, uint64_t stream, uint64_t w, uint64_t w_off, int mode, uint32_t chunk_shift,
+                    uint64_t x, uint32_t ldx, uint32_t M, uint32_t N, uint32_t K, uint64_t part, uint64_t part_bytes,
+                    uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo, uint32_t target_units, uint32_t unroll) {
+    if (N % 16 || K % 32 || ldx % 8 || !M) throw StatusError("dgemm: N % 16, K % 32, ldx % 8 and M > 0 required");
+    if (epi == DGEMM_EPI_SILU_MUL && (N % 32)) throw StatusError("dgemm: SILU_MUL needs N % 32 == 0");
+    DGemmArgs a{};
+    a.w = (const uint8_t*)w;
+    a.w_off = w_off;
+    a.x = (const uint16_t*)x;
+    a.part = (float*)part;
+    a.M = M; a.N = N; a.K = K; a.ldx = ldx;
+    dgemm_plan(N, K, target_units, &a.ksplit, &a.klen);
+    a.row_blocks = (N / 16 + 3) / 4;
+    a.chunk_shift = chunk_shift;
+    a.unroll = unroll;
+    if ((uint64_t)a.ksplit * M * N * 4 > part_bytes) throw StatusError("dgemm: partial workspace too small");
+    if (mode < DGEMM_W_RAW || mode > DGEMM_W_PACKED_BF11) throw StatusError("dgemm: bad weight mode");
+    check(rt()->be()->dgemm(dev, a, mode, (void*)stream), "dgemm");
+    DGemmReduceArgs r{};
+    r.part = a.part;
+    r.ksplit = a.ksplit; r.M = M; r.N = N; r.epi = epi;
+    r.resid = (const uint16_t*)resid; r.ldr = ldr; r.ldo = ldo;
+    r.out = (uint16_t*)out;
+    check(rt()->be()->dgemm_reduce(dev, r, (void*)stream), "dgemm_reduce");
+    return a.ksplit;
+  }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("w_off"), py::arg("mode"), py::arg("chunk_shift"),
+     py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("part"), py::arg("part_bytes"),
+     py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("target_units") = 2048, py::arg("unroll") = 0);
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
     return py::make_tuple((uint64_t)fb.put, (uint64_t)fb.recs, fb.entries, fb.overflows);

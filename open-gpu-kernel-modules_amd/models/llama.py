@@ -32,7 +32,7 @@ import torch
 
 from .. import rt
 from .._native import lib
-from ..ops import bf12
+from ..ops import bf12, dgemm
 from ..ops import decode as D
 from ..ops.memory import managed_embedding
 from ..parallel import comm, tp as tpmod
@@ -78,7 +78,11 @@ def _al(n: int) -> int:
 
 @dataclass
 class LayerLayout:
-    """Byte offsets of one TP shard's tensors inside a layer buffer (bf16, 4 KB aligned)."""
+    """Byte offsets of one TP shard's GEMM weights inside a layer buffer (bf16,
+    4 KB aligned). Every matrix is stored in the decode GEMM's fragment order
+    (ops/dgemm.py: 16x32 MFMA A-tiles), so the kernel streams it - raw or
+    BF11-packed - with one coalesced 1 KB wave access per tile. The RMSNorm
+    weights live in a separate small resident buffer (TieredLlama.norms)."""
 
     shapes: dict = field(default_factory=dict)
     offsets: dict = field(default_factory=dict)
@@ -89,9 +93,8 @@ class LayerLayout:
         hd = cfg.head_dim
         hq, hkv, f = cfg.n_heads // world, cfg.n_kv_heads // world, cfg.ffn_dim // world
         L = LayerLayout()
-        for name, shape in (("attn_norm", (cfg.dim,)), ("wqkv", ((hq + 2 * hkv) * hd, cfg.dim)),
-                            ("wo", (cfg.dim, hq * hd)), ("mlp_norm", (cfg.dim,)), ("wgu", (2 * f, cfg.dim)),
-                            ("wd", (cfg.dim, f))):
+        for name, shape in (("wqkv", ((hq + 2 * hkv) * hd, cfg.dim)), ("wo", (cfg.dim, hq * hd)),
+                            ("wgu", (2 * f, cfg.dim)), ("wd", (cfg.dim, f))):
             L.shapes[name] = shape
             L.offsets[name] = L.nbytes
             L.nbytes += _al(math.prod(shape) * 2)
@@ -122,7 +125,9 @@ class TieredLlama:
         self.embed_bytes = _al(cfg.vocab * cfg.dim * 2)
         self.kv_layer_bytes = 2 * batch * self.hkv * self.T * hd * 2
         self.kv_bytes = cfg.n_layers * self.kv_layer_bytes
-        self.footprint = self.embed_bytes + cfg.n_layers * self.layer_bytes + self.head_bytes + self.kv_bytes
+        self.norm_bytes = _al((2 * cfg.n_layers + 1) * cfg.dim * 2)
+        self.footprint = (self.embed_bytes + cfg.n_layers * self.layer_bytes + self.head_bytes + self.kv_bytes
+                          + self.norm_bytes)
         self.oversub = oversub
         blk = 2 << 20
         budget = hbm_budget if hbm_budget is not None else int(self.footprint / oversub)
@@ -130,28 +135,33 @@ class TieredLlama:
 
         def chunks(n):
             return (n + blk - 1) // blk * blk
-        # Weight storage. "bf12": every weight rests packed (lossless BF12, ~0.75x)
-        # in whatever tier holds it - host, CXL and HBM - and is unpacked into one
-        # bf16 staging buffer right before its layer runs (ops/bf12.py). The
-        # staging buffer is carved out of the same HBM budget. "bf16": raw
-        # weights; with ``packed`` the runtime keeps streamed host copies BF12 and
-        # decodes them inside the H2D copy kernel (RANGE_PACKED_BF16).
+        # Weight storage (every matrix in the decode GEMM's fragment order).
+        # "bf11": every weight rests packed (lossless BF11, ~0.70x) in whatever
+        # tier holds it - host, CXL and HBM - and the decode GEMM reads the packed
+        # stream directly (decoded in registers: no bf16 copy exists anywhere).
+        # "bf12": packed BF12 (0.75x), unpacked into a bf16 staging buffer
+        # right before its layer runs (carved out of the same HBM budget).
+        # "bf16": raw weights; with ``packed`` the runtime keeps streamed host
+        # copies BF12 and decodes them inside the H2D copy kernel.
         if weight_format not in ("bf11", "bf12", "bf16"):
             raise ValueError("weight_format must be 'bf11', 'bf12' or 'bf16'")
         self.wfmt = weight_format
         self.wpacked = weight_format in ("bf11", "bf12")   # weights rest packed in every tier
         self.packed = packed and weight_format == "bf16"
-        self.stage_bytes = chunks(max(self.layer_bytes, self.head_bytes)) if self.wpacked else 0
+        self.staged = weight_format == "bf12"
+        self.packfmt = "bf11s" if weight_format == "bf11" else weight_format
+        self.stage_bytes = chunks(max(self.layer_bytes, self.head_bytes)) if self.staged else 0
         self.arena_bytes = self.budget - self.stage_bytes
         lib.init_device(device, self.arena_bytes)
         self.pinfo: dict = {}
+        self.pmode: dict = {}
         gpu = rt.Loc.gpu(device)
         host = rt.Loc.host()
         t0 = time.perf_counter()
         self._seed, self._std = seed, init_std
         if self.wpacked:
             # The packed size of layer 0 sizes the plan (all layers share one distribution).
-            first, info0 = bf12.pack(self._gen_layer(0), fmt=weight_format)
+            first, info0 = bf12.pack(self._gen_layer(0), fmt=self.packfmt)
             ratio = info0.nbytes / (self.layer_bytes)
             self.res_layer_bytes = _al(int(self.layer_bytes * ratio * 1.002) + 4096)
             self.res_head_bytes = _al(int(self.head_bytes * ratio * 1.002) + 4096)
@@ -160,7 +170,7 @@ class TieredLlama:
             self.res_layer_bytes, self.res_head_bytes = self.layer_bytes, self.head_bytes
         # ---- residency plan (in resting bytes: packed or raw)
         staging = (lookahead + 1) * chunks(max(self.res_layer_bytes, self.res_head_bytes))
-        avail = self.arena_bytes - chunks(self.kv_bytes) - staging
+        avail = self.arena_bytes - chunks(_al(self.kv_bytes) + self.norm_bytes) - staging
         if avail < 0:
             raise ValueError(f"HBM budget {self.budget/2**30:.1f} GiB too small for KV + staging "
                              f"({(chunks(self.kv_bytes) + staging + self.stage_bytes)/2**30:.1f} GiB)")
@@ -177,14 +187,16 @@ class TieredLlama:
         self.embed = rt.malloc_managed(self.embed_bytes, "embed")
         self.embed.set_preferred_location(host)
         self.embed.set_accessed_by(device)
-        self.kv = rt.malloc_managed(self.kv_bytes, "kv")
+        # KV cache + the RMSNorm weights (tiny) share one resident range
+        self.kv = rt.malloc_managed(_al(self.kv_bytes) + self.norm_bytes, "kv")
         self.kv.set_preferred_location(gpu)
         self.layers = []
         for i in range(cfg.n_layers):
             if self.wpacked:
-                stream, info = (first, info0) if i == 0 else bf12.pack(self._gen_layer(i), fmt=weight_format)
+                stream, info = (first, info0) if i == 0 else bf12.pack(self._gen_layer(i), fmt=self.packfmt)
                 b = rt.malloc_managed(info.nbytes, f"layer{i}", cpu_view=False)
                 self.pinfo[("layer", i)] = info
+                self.pmode[("layer", i)] = dgemm.packed_mode(stream) if not self.staged else dgemm.MODE_RAW
             else:
                 stream = self._gen_layer(i)
                 b = rt.malloc_managed(self.layer_bytes, f"layer{i}", packed_bf16=self.packed and not self.resident[i])
@@ -195,9 +207,10 @@ class TieredLlama:
         first = None
         head = self._gen_head()
         if self.wpacked:
-            stream, info = bf12.pack(head, fmt=weight_format)
+            stream, info = bf12.pack(head, fmt=self.packfmt)
             self.head = rt.malloc_managed(info.nbytes, "lm_head", cpu_view=False)
             self.pinfo[("head", 0)] = info
+            self.pmode[("head", 0)] = dgemm.packed_mode(stream) if not self.staged else dgemm.MODE_RAW
         else:
             stream = head
             self.head = rt.malloc_managed(self.head_bytes, "lm_head", packed_bf16=self.packed and not self.head_resident)
@@ -208,13 +221,17 @@ class TieredLlama:
         if not self.fake:
             torch.cuda.synchronize(self.dev)
         self.stage = (torch.empty(self.stage_bytes // 2, dtype=torch.bfloat16, device=self.tdev)
-                      if self.wpacked else None)
-        self.final_norm = torch.ones(cfg.dim, dtype=torch.bfloat16, device=self.tdev)
+                      if self.staged else None)
+        # RMSNorm weights of every layer + the final norm (after the KV cache)
+        self.kv.write(torch.ones((2 * cfg.n_layers + 1) * cfg.dim, dtype=torch.bfloat16), offset=_al(self.kv_bytes))
         self.cos, self.sin = D.rope_tables(hd, self.T, cfg.rope_theta, self.tdev)
         # KV cache: leased for the model's lifetime (hot, written every step)
         self.kv_lease = self.kv.acquire(device, rt.WRITE)
         self.kv_lease.wait()
         kv = self.kv_lease.tensor((cfg.n_layers, 2, batch, self.hkv, self.T, hd), torch.bfloat16)
+        self.norm_w = rt._tensor_from_ptr(self.kv_lease.dptr + _al(self.kv_bytes), (2 * cfg.n_layers + 1, cfg.dim),
+                                          torch.bfloat16, "cpu" if self.fake else "cuda", device)
+        self.final_norm = self.norm_w[2 * cfg.n_layers]
         # Synthetic prefilled context, generated at full head count and sliced to
         # this rank's KV heads so every TP degree decodes the same model state.
         g = torch.Generator(device=self.tdev).manual_seed(seed + 7919)
@@ -281,7 +298,7 @@ class TieredLlama:
 
         def put(name, t):
             off = L.offsets[name] // 2
-            flat[off:off + t.numel()].copy_(t.reshape(-1))
+            flat[off:off + t.numel()].copy_(dgemm.frag_permute(t.contiguous()))
 
         g = torch.Generator(device=dev).manual_seed(self._seed * 1000003 + i)
         wq = torch.empty(cfg.n_heads * hd, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
@@ -299,9 +316,6 @@ class TieredLlama:
         wd = torch.empty(cfg.dim, cfg.ffn_dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
         put("wd", tpmod.shard_cols(wd, self.rank, self.world))
         del wd
-        one = torch.ones(cfg.dim, dtype=torch.bfloat16, device=dev)
-        put("attn_norm", one)
-        put("mlp_norm", one)
         return flat
 
     def _head_gen(self) -> torch.Generator:
@@ -317,15 +331,27 @@ class TieredLlama:
         g = self._head_gen()
         torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=self.tdev).normal_(0, 1.0, generator=g)  # embed draw
         head = torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=self.tdev).normal_(0, self._std, generator=g)
-        return tpmod.shard_rows(head, self.rank, self.world).contiguous()
+        return dgemm.frag_permute(tpmod.shard_rows(head, self.rank, self.world).contiguous())
 
     def host_weights(self, key) -> torch.Tensor:
-        """The bf16 bytes of a layer / head as stored (unpacked on the host) - for
-        reference numerics."""
+        """The bf16 bytes of a layer / head as stored (unpacked on the host, still
+        in fragment order) - for reference numerics."""
         raw = self._buf(key).read()
         if self.wpacked:
             return bf12.unpack_host(raw, self.pinfo[key]).view(torch.uint8)
         return raw
+
+    def host_matrix(self, key, name: str = "head") -> torch.Tensor:
+        """One weight matrix as a plain [N, K] bf16 CPU tensor (reference numerics)."""
+        raw = self.host_weights(key)
+        if key[0] == "head":
+            n, k = self.vocab_local, self.cfg.dim
+            off = 0
+        else:
+            n, k = self.layout.shapes[name]
+            off = self.layout.offsets[name]
+        flat = raw[off:off + n * k * 2].view(torch.bfloat16)
+        return dgemm.frag_unpermute(flat, n, k)
 
     # ------------------------------------------------------------------ streaming
     def _prefetch_ahead(self) -> None:
@@ -345,8 +371,9 @@ class TieredLlama:
             self._pf_next = (self._pf_next + 1) % n
 
     def _use(self, key):
-        """Fault the tensor in (lease) and return (lease or None, base pointer of
-        its bf16 weights). bf12: the packed stream is unpacked into the staging
+        """Fault the tensor in (lease) and return (lease or None, weight refs by
+        name). bf11: the GEMMs read the packed stream in place (the lease is held
+        until they are enqueued). bf12: the stream is unpacked into the staging
         buffer on the compute stream and the lease is released right away (the
         ring reuses the chunks only after the unpack has read them)."""
         if not self._is_resident(key):
@@ -355,22 +382,19 @@ class TieredLlama:
             self._prefetch_ahead()
         lease = self._buf(key).acquire(self.dev, rt.READ)
         lease.wait(0 if self.fake else None)
-        if self.wpacked:
+        if self.staged:
             bf12.unpack_into(self.stage, lease.dptr, self.pinfo[key], self.dev, 0 if self.fake else None)
             lease.release(0 if self.fake else None)
-            return None, self.stage.data_ptr()
-        return lease, lease.dptr
+            return None, self._refs(key, self.stage.data_ptr(), dgemm.MODE_RAW)
+        mode = self.pmode.get(key, dgemm.MODE_RAW)
+        return lease, self._refs(key, lease.dptr, mode)
 
-    def _layer_views(self, ptr: int) -> dict:
-        v = self._views.get(ptr)
-        if v is None:
-            v = {name: rt._tensor_from_ptr(ptr + self.layout.offsets[name], shape, torch.bfloat16,
-                                           "cpu" if self.fake else "cuda", self.dev)
-                 for name, shape in self.layout.shapes.items()}
-            if len(self._views) > 4 * len(self.order):
-                self._views.clear()
-            self._views[ptr] = v
-        return v
+    def _refs(self, key, ptr: int, mode: int) -> dict:
+        shift = (self.pinfo[key].chunk_values.bit_length() - 1) if key in self.pinfo else 20
+        if key[0] == "head":
+            return {"head": dgemm.WeightRef(ptr, 0, self.vocab_local, self.cfg.dim, mode, shift)}
+        return {name: dgemm.WeightRef(ptr, self.layout.offsets[name] // 2, n, k, mode, shift)
+                for name, (n, k) in self.layout.shapes.items()}
 
     # ------------------------------------------------------------------ decode
     @torch.no_grad()
@@ -385,11 +409,11 @@ class TieredLlama:
         if self.fake:
             x = x.to(self.tdev)
         cos, sin = self.cos[pos], self.sin[pos]
+        dv = self.dev
         for i in range(cfg.n_layers):
-            lease, ptr = self._use(("layer", i))
-            w = self._layer_views(ptr)
-            h = D.rms_norm(x, w["attn_norm"], cfg.norm_eps)
-            qkv = h @ w["wqkv"].t()
+            lease, w = self._use(("layer", i))
+            h = D.rms_norm(x, self.norm_w[2 * i], cfg.norm_eps)
+            qkv = dgemm.linear(h, w["wqkv"], device_index=dv)
             q = qkv[:, :self.hq * hd].view(B, self.hq, hd)
             k = qkv[:, self.hq * hd:(self.hq + self.hkv) * hd].view(B, self.hkv, hd)
             v = qkv[:, (self.hq + self.hkv) * hd:].view(B, self.hkv, hd)
@@ -399,19 +423,15 @@ class TieredLlama:
             kc[:, :, pos].copy_(k)
             vc[:, :, pos].copy_(v)
             a = D.gqa_decode_attention(q, kc, vc, pos + 1)
-            o = a @ w["wo"].t()
-            x = x + tpmod.row_parallel_reduce(o)
-            h = D.rms_norm(x, w["mlp_norm"], cfg.norm_eps)
-            gu = h @ w["wgu"].t()
-            d = D.silu_mul(gu) @ w["wd"].t()
-            x = x + tpmod.row_parallel_reduce(d)
+            x = self._row_parallel(a, w["wo"], x)
+            h = D.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps)
+            g = dgemm.linear(h, w["wgu"], "silu_mul", device_index=dv)
+            x = self._row_parallel(g, w["wd"], x)
             if lease is not None:
                 lease.release(0 if self.fake else None)
         x = D.rms_norm(x, self.final_norm, cfg.norm_eps)
-        lease, ptr = self._use(("head", 0))
-        head = rt._tensor_from_ptr(ptr, (self.vocab_local, cfg.dim), torch.bfloat16,
-                                   "cpu" if self.fake else "cuda", self.dev)
-        logits = x @ head.t()
+        lease, w = self._use(("head", 0))
+        logits = dgemm.linear(x, w["head"], device_index=dv)
         if self.keep_logits:
             self.last_logits = comm.all_gather_cat(logits.float(), dim=-1)
         nxt = tpmod.vocab_parallel_argmax(logits, self.rank, self.world)
@@ -419,6 +439,14 @@ class TieredLlama:
             lease.release(0 if self.fake else None)
         self.pos += 1
         return nxt
+
+    def _row_parallel(self, a: torch.Tensor, w: "dgemm.WeightRef", x: torch.Tensor) -> torch.Tensor:
+        """x + (a @ W^T) summed over TP ranks. One rank: the residual add is fused
+        into the GEMM epilogue (in place on x); else partial GEMM + RCCL all-reduce."""
+        if self.world == 1:
+            return dgemm.linear(a, w, "resid", resid=x, out=x, device_index=self.dev)
+        o = dgemm.linear(a, w, device_index=self.dev)
+        return x + tpmod.row_parallel_reduce(o)
 
     def reset(self, position: Optional[int] = None) -> None:
         self.pos = self.ctx if position is None else position
@@ -439,11 +467,10 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
     emb = model.embed.read().view(torch.bfloat16).view(cfg.vocab, cfg.dim).float()
     x = emb[tokens.cpu()].to(dev)
     cos, sin = model.cos[pos], model.sin[pos]
+    norms = model.norm_w.float().cpu().to(dev)
     for i in range(cfg.n_layers):
-        raw = model.host_weights(("layer", i))
-        w = {n: raw[model.layout.offsets[n]:model.layout.offsets[n] + math.prod(s) * 2].view(torch.bfloat16)
-             .view(*s).float().to(dev) for n, s in model.layout.shapes.items()}
-        h = D.rms_norm(x, w["attn_norm"], cfg.norm_eps)
+        w = {n: model.host_matrix(("layer", i), n).float().to(dev) for n in model.layout.shapes}
+        h = D.rms_norm(x, norms[2 * i], cfg.norm_eps)
         qkv = h @ w["wqkv"].t()
         q = qkv[:, :model.hq * hd].view(B, model.hq, hd)
         k = qkv[:, model.hq * hd:(model.hq + model.hkv) * hd].view(B, model.hkv, hd)
@@ -455,10 +482,10 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
         vc[:, :, pos] = v
         a = D.gqa_decode_attention(q, kc, vc, pos + 1)
         x = x + a @ w["wo"].t()
-        h = D.rms_norm(x, w["mlp_norm"], cfg.norm_eps)
+        h = D.rms_norm(x, norms[2 * i + 1], cfg.norm_eps)
         x = x + D.silu_mul(h @ w["wgu"].t()) @ w["wd"].t()
-    x = D.rms_norm(x, model.final_norm.float(), cfg.norm_eps)
-    head = model.host_weights(("head", 0)).view(torch.bfloat16).view(model.vocab_local, cfg.dim).float().to(dev)
+    x = D.rms_norm(x, norms[2 * cfg.n_layers], cfg.norm_eps)
+    head = model.host_matrix(("head", 0)).float().to(dev)
     return x @ head.t()
 
 

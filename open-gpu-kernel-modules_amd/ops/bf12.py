@@ -51,7 +51,7 @@ def _threads() -> int:
     return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
 
 
-FORMATS = {"bf12": 1, "bf11": 2}
+FORMATS = {"bf12": 1, "bf11": 2, "bf11s": 3}  # bf11s: BF11-or-raw chunks (decode-GEMM weights)
 
 
 def pack(t: torch.Tensor, chunk_values: int = CHUNK_VALUES, out: torch.Tensor | None = None, fmt: str = "bf11"
@@ -97,3 +97,10 @@ def unpack_into(dst: torch.Tensor, src_ptr: int, info: PackedInfo, device: int =
     lib.bf12_unpack(device, src_ptr, dst.data_ptr(), info.nchunks, info.chunk_values, info.n_values, stream,
                     workgroups)
     return dst
+
+
+def chunk_kinds(stream: torch.Tensor) -> set:
+    """Chunk encodings present in a (CPU) stream: 0 raw, 1 BF12, 2 BF11."""
+    info = info_of(stream[:64])
+    table = stream[32:32 + 16 * info.nchunks].view(torch.int32).view(-1, 4)
+    return set(int(k) for k in table[:, 3].unique().tolist())

@@ -1,0 +1,159 @@
+"""Decode GEMM (csrc/kernels/decode_gemm.hip, CPU reference csrc/core/dgemm_ref.cpp)
+vs a plain fp32 PyTorch reference: fragment order, raw and BF11-packed weights
+(decoded in registers, exceptions included), split-K and every fused epilogue.
+CPU tests run the fake backend's reference; the GPU tests run the MFMA kernel."""
+from __future__ import annotations
+
+import time
+
+import pytest
+import torch
+
+from ogkm.ops import bf12, dgemm
+
+
+def _weights(n, k, seed, specials=True):
+    g = torch.Generator().manual_seed(seed)
+    w = (torch.randn(n, k, generator=g) * 0.02).to(torch.bfloat16)
+    if specials:  # exponents outside every code space -> BF11 exceptions in several tiles
+        w[1, 3] = 1e30
+        w[n - 1, k - 1] = -3e-30
+        w[n // 2, 7] = 7e20
+    return w
+
+
+def _ref(x, w, epi, resid=None):
+    y = (x.float() @ w.float().t())
+    if epi == "store":
+        return y
+    if epi == "resid":
+        return y.to(torch.bfloat16).float() + resid.float()
+    f = w.shape[0] // 2
+    g, u = y[:, :f].to(torch.bfloat16).float(), y[:, f:].to(torch.bfloat16).float()
+    return torch.nn.functional.silu(g) * u
+
+
+def _place(w, packed, device):
+    flat = dgemm.frag_permute(w).contiguous()
+    if packed:
+        # a 2048-value pad in front puts the tensor at a non-zero stream offset
+        pad = torch.zeros(2048, dtype=torch.bfloat16)
+        stream, info = bf12.pack(torch.cat([pad, flat]), chunk_values=1 << 16, fmt="bf11s")
+        buf = stream.to(device)
+        mode = dgemm.packed_mode(stream) if packed is True else dgemm.MODE_PACKED
+        return buf, dgemm.WeightRef(buf.data_ptr(), 2048, w.shape[0], w.shape[1], mode, 16)
+    buf = flat.to(device)
+    return buf, dgemm.WeightRef(buf.data_ptr(), 0, w.shape[0], w.shape[1], dgemm.MODE_RAW)
+
+
+def test_frag_permute_roundtrip():
+    w = torch.arange(64 * 96, dtype=torch.float32).reshape(64, 96).to(torch.bfloat16)
+    flat = dgemm.frag_permute(w)
+    # lane l of fragment (0, 0) holds W[l & 15][8 (l >> 4) + j]
+    assert flat[5 * 8 + 3].item() == w[5, 3].item()
+    assert flat[(16 + 2) * 8 + 1].item() == w[2, 9].item()
+    assert torch.equal(dgemm.frag_unpermute(flat, 64, 96), w)
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("epi", ["store", "resid", "silu_mul"])
+def test_dgemm_cpu_reference(fake_rt, packed, epi):
+    m, n, k = 5, 96, 256
+    w = _weights(n, k, 3)
+    x = (torch.randn(m, k) * 0.5).to(torch.bfloat16)
+    resid = (torch.randn(m, n) * 0.1).to(torch.bfloat16)
+    buf, ref_w = _place(w, packed, "cpu")
+    out = dgemm.linear(x, ref_w, epi, resid=resid.clone() if epi == "resid" else None)
+    want = _ref(x, w, epi, resid)
+    torch.testing.assert_close(out.float(), want, atol=2e-2, rtol=2e-2)
+
+
+def test_dgemm_cpu_strided_x_and_inplace_resid(fake_rt):
+    m, n, k = 3, 64, 128
+    w = _weights(n, k, 4, specials=False)
+    big = (torch.randn(m, k + 64) * 0.5).to(torch.bfloat16)
+    x = big[:, 32:32 + k]  # row stride k + 64
+    resid = (torch.randn(m, n) * 0.1).to(torch.bfloat16)
+    want = _ref(x, w, "resid", resid)
+    buf, ref_w = _place(w, False, "cpu")
+    r = resid.clone()
+    dgemm.linear(x, ref_w, "resid", resid=r, out=r)
+    torch.testing.assert_close(r.float(), want, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("packed", [False, True, "generic"])
+@pytest.mark.parametrize("epi", ["store", "resid", "silu_mul"])
+@pytest.mark.parametrize("m", [1, 7, 64, 80])
+def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m):
+    n, k = 320, 1024
+    w = _weights(n, k, 5)
+    x = (torch.randn(m, k) * 0.5).to(torch.bfloat16)
+    resid = (torch.randn(m, n) * 0.1).to(torch.bfloat16)
+    buf, ref_w = _place(w, packed, "cuda")
+    xd = x.cuda()
+    rd = resid.cuda() if epi == "resid" else None
+    out = dgemm.linear(xd, ref_w, epi, resid=rd)
+    torch.cuda.synchronize()
+    want = _ref(x, w, epi, resid)
+    torch.testing.assert_close(out.float().cpu(), want, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_dgemm_gpu_matches_cpu_reference_bits_packed_vs_raw(gpu_rt):
+    """The packed path decodes to exactly the raw bf16 weights: identical outputs."""
+    n, k, m = 256, 2048, 64
+    w = _weights(n, k, 6)
+    x = (torch.randn(m, k) * 0.5).to(torch.bfloat16).cuda()
+    b0, r0 = _place(w, False, "cuda")
+    b1, r1 = _place(w, True, "cuda")
+    b2, r2 = _place(w, "generic", "cuda")
+    assert r1.mode == dgemm.MODE_PACKED_BF11
+    o0 = dgemm.linear(x, r0).clone()
+    o1 = dgemm.linear(x, r1).clone()
+    o2 = dgemm.linear(x, r2)
+    torch.cuda.synchronize()
+    assert torch.equal(o0, o1) and torch.equal(o0, o2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("packed", [False, True])
+def test_dgemm_gpu_bandwidth_70b_shapes(gpu_rt, packed):
+    """Weight-streaming rate at Llama-3-70B decode shapes (M = 64): the GEMM must
+    move its weight bytes at a large fraction of HBM bandwidth."""
+    m = 64
+    x_all = {}
+    total_bytes, total_t = 0, 0.0
+    for n, k in ((10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672)):
+        w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
+        flat = dgemm.frag_permute(w).contiguous()
+        del w
+        if packed:
+            stream, info = bf12.pack(flat, fmt="bf11s")
+            buf = stream.cuda()
+            ref_w = dgemm.WeightRef(buf.data_ptr(), 0, n, k, dgemm.packed_mode(stream), 20)
+            nbytes = info.nbytes
+        else:
+            buf = flat
+            ref_w = dgemm.WeightRef(buf.data_ptr(), 0, n, k, dgemm.MODE_RAW)
+            nbytes = n * k * 2
+        x = x_all.setdefault(k, (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16))
+        out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+        for _ in range(3):
+            dgemm.linear(x, ref_w, out=out)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        it = 10
+        for _ in range(it):
+            dgemm.linear(x, ref_w, out=out)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / it
+        print(f"dgemm {'bf11' if packed else 'bf16'} N={n} K={k}: {dt*1e3:.3f} ms, {nbytes/dt/1e9:.0f} GB/s weights, "
+              f"{n*k*2/dt/1e9:.0f} GB/s bf16-equivalent")
+        total_bytes += nbytes
+        total_t += dt
+        del buf
+    print(f"dgemm {'bf11' if packed else 'bf16'} layer total: {total_t*1e3:.3f} ms ({total_bytes/total_t/1e9:.0f} GB/s)")
+    # raw bf16 streams at >= 2.5 TB/s; the in-register BF11 decode currently
+    # reaches ~0.8 TB/s of packed bytes (its speed-of-light is the raw rate)
+    assert total_bytes / total_t > (0.6e12 if packed else 2.5e12)

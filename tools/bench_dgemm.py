@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Decode-GEMM microbenchmark at Llama-3-70B decode shapes (M = batch): raw
+bf16 fragment-order weights vs BF11-packed weights decoded in registers, for
+each K unroll, and the staged alternative (k_bf12_unpack to bf16 + raw GEMM).
+Prints one JSON line per variant."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch  # noqa: E402
+
+from ogkm import rt  # noqa: E402
+from ogkm.ops import bf12, dgemm  # noqa: E402
+
+SHAPES = ((10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672))
+
+
+def timeit(fn, it=10):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(it):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / it
+
+
+def main():
+    m = int(os.environ.get("M", "64"))
+    rt.init("hip", host_budget_mb=4096)
+    ws = {}
+    for n, k in SHAPES:
+        w = (torch.randn(n, k, device="cuda") * 0.02).to(torch.bfloat16)
+        flat = dgemm.frag_permute(w).contiguous()
+        del w
+        stream, info = bf12.pack(flat, fmt="bf11s")
+        ws[(n, k)] = (flat, stream.cuda(), info, dgemm.packed_mode(stream))
+    xs = {k: (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16) for _, k in SHAPES}
+    stage = torch.empty(max(n * k for n, k in SHAPES), dtype=torch.bfloat16, device="cuda")
+    variants = [("raw", u) for u in (2, 4)] + [("bf11", u) for u in (1, 2, 4)] + [("staged", 2)]
+    if os.environ.get("VARIANTS"):  # e.g. "bf11:2,raw:2"
+        variants = [(v.split(":")[0], int(v.split(":")[1])) for v in os.environ["VARIANTS"].split(",")]
+    for kind, u in variants:
+        dgemm.UNROLL = u
+        tot_t, tot_b, per = 0.0, 0, {}
+        for (n, k), (flat, pk, info, mode) in ws.items():
+            out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+            x = xs[k]
+            if kind == "raw":
+                ref = dgemm.WeightRef(flat.data_ptr(), 0, n, k, dgemm.MODE_RAW)
+                fn = lambda: dgemm.linear(x, ref, out=out)  # noqa: E731
+                nb = n * k * 2
+            elif kind == "bf11":
+                ref = dgemm.WeightRef(pk.data_ptr(), 0, n, k, mode, 20)
+                fn = lambda: dgemm.linear(x, ref, out=out)  # noqa: E731
+                nb = info.nbytes
+            else:
+                ref = dgemm.WeightRef(stage.data_ptr(), 0, n, k, dgemm.MODE_RAW)
+
+                def fn(pk=pk, info=info, ref=ref, out=out, x=x):
+                    bf12.unpack_into(stage, pk.data_ptr(), info, 0)
+                    dgemm.linear(x, ref, out=out)
+                nb = info.nbytes
+            dt = timeit(fn)
+            per[f"{n}x{k}"] = round(dt * 1e3, 4)
+            tot_t += dt
+            tot_b += nb
+        print(json.dumps({"variant": kind, "unroll": u, "M": m, "layer_ms": round(tot_t * 1e3, 3),
+                          "weight_gbps": round(tot_b / tot_t / 1e9, 1), "per_shape_ms": per}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
