@@ -52,6 +52,20 @@ void PageMask::set_range(uint32_t first, uint32_t n) {
   }
 }
 
+uint32_t PageMask::count_range(uint32_t first, uint32_t n) const {
+  uint32_t end = first + n, c = 0;
+  if (end > kPagesPerBlock) end = kPagesPerBlock;
+  for (uint32_t p = first; p < end;) {
+    uint32_t wi = p >> 6, bi = p & 63;
+    uint32_t take = 64 - bi;
+    if (take > end - p) take = end - p;
+    uint64_t m = take == 64 ? ~0ull : (((1ull << take) - 1) << bi);
+    c += (uint32_t)__builtin_popcountll(w[wi] & m);
+    p += take;
+  }
+  return c;
+}
+
 void PageMask::clear_range(uint32_t first, uint32_t n) {
   uint32_t end = first + n;
   if (end > kPagesPerBlock) end = kPagesPerBlock;

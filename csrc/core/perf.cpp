@@ -117,17 +117,20 @@ PageMask prefetch_hint(const PageMask& resident_on_dst, const PageMask& faulted,
   PageMask valid = PageMask::range(0, npages);
   uint32_t p = faulted.next_set(0);
   while (p < npages) {
-    // Largest aligned region first (the root of the bitmap tree), then descend.
-    for (int lvl = 9; lvl >= 0; --lvl) {
-      uint32_t size = 1u << lvl;
-      uint32_t start = p & ~(size - 1);
-      if (start >= npages) continue;
-      uint32_t len = std::min(size, npages - start);
-      PageMask region = PageMask::range(start, len);
-      uint32_t cnt = (have & region).count();
-      if (cnt * 100 > thr * len) {
-        out |= region;
-        break;
+    // A faulted page inside a region already chosen would choose that same
+    // region (its larger ancestors did not qualify): skip it.
+    if (!out.test(p)) {
+      // Largest aligned region first (the root of the bitmap tree), then descend.
+      for (int lvl = 9; lvl >= 0; --lvl) {
+        uint32_t size = 1u << lvl;
+        uint32_t start = p & ~(size - 1);
+        if (start >= npages) continue;
+        uint32_t len = std::min(size, npages - start);
+        if (have.count_range(start, len) * 100 > thr * len) {
+          out.set_range(start, len);
+          p = start + len - 1;  // continue after the region
+          break;
+        }
       }
     }
     p = faulted.next_set(p + 1);

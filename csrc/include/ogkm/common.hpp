@@ -77,6 +77,7 @@ struct PageMask {
   bool test(uint32_t p) const { return (w[p >> 6] >> (p & 63)) & 1; }
   void set_range(uint32_t first, uint32_t n);
   void clear_range(uint32_t first, uint32_t n);
+  uint32_t count_range(uint32_t first, uint32_t n) const;  // set pages in [first, first+n)
   void fill() { for (auto& x : w) x = ~0ull; }
   void zero() { for (auto& x : w) x = 0; }
   bool empty() const { for (auto x : w) if (x) return false; return true; }
