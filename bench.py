@@ -51,13 +51,20 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--context", type=int, default=1024)
     ap.add_argument("--oversub", type=float, default=2.0)
-    ap.add_argument("--lookahead", type=int, default=int(os.environ.get("OGKM_LOOKAHEAD", "2")))
+    ap.add_argument("--lookahead", type=int, default=int(os.environ.get("OGKM_LOOKAHEAD", "1")),
+                    help="streamed tensors in flight beyond the one in use (each costs a staging slot of HBM)")
     ap.add_argument("--no-aux", action="store_true", help="skip the HBM<->host/CXL bandwidth probe")
     ap.add_argument("--weights", choices=("bf11", "bf12", "bf16"), default="bf11",
                     help="bf11/bf12: weights rest losslessly packed (~0.69x / 0.75x) in every tier (HBM included) "
                          "and are unpacked per layer; bf16: raw weights")
     ap.add_argument("--no-packed", action="store_true",
                     help="with --weights bf16: raw host copies instead of BF12 copies decoded in the H2D kernel")
+    ap.add_argument("--tiers", choices=("host", "host+cxl"), default="host",
+                    help="where streamed weights rest: host DRAM, or interleaved host DRAM / CXL.mem (three-tier)")
+    ap.add_argument("--cxl-frac", type=float, default=0.5, help="share of streamed tensors resting in CXL.mem")
+    ap.add_argument("--simulate-tp", type=int, default=0,
+                    help="single-process run of TP rank 0 of N (per-GPU shard of an N-GPU job; collectives "
+                         "skipped, numerics not meaningful) - for configs larger than the box, e.g. 405B tp8")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -119,10 +126,11 @@ def main() -> None:
         aux = bandwidth_probe(dev)
     comm.barrier()
     t_init = time.perf_counter()
+    sim = a.simulate_tp > 1 and world == 1
     model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 2,
-                              oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=world, seed=1234,
-                              lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
-                              weight_format=a.weights)
+                              oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
+                              seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
+                              weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac)
     plan = model.describe()
     init_s = time.perf_counter() - t_init
     g = torch.Generator(device="cpu").manual_seed(42)
@@ -142,8 +150,10 @@ def main() -> None:
     tokens = a.batch * a.steps
     value = tokens / dt
     if e.rank == 0:
+        name = {"llama3-70b": "Llama-3-70B", "llama3-405b": "Llama-3-405B", "llama3-8b": "Llama-3-8B"}.get(a.model,
+                                                                                                        a.model)
         out = {
-            "metric": "tokens/sec Llama-3-70B 2x oversubscribe",
+            "metric": f"tokens/sec {name} {a.oversub:g}x oversubscribe",
             "value": round(value, 3),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -159,7 +169,9 @@ def main() -> None:
                 "model": a.model,
                 "global_batch": a.batch,
                 "seq_len": a.context,
-                "parallelism": f"tp{world}",
+                "parallelism": f"tp{a.simulate_tp}-rank0-simulated" if sim else f"tp{world}",
+                "tiers": plan["tiers"],
+                "cxl_streamed_gb_per_step_per_gpu": round(plan["cxl_streamed_gb_per_step"], 2),
                 "oversubscription": round(plan["oversubscription"], 3),
                 "hbm_budget_gb_per_gpu": round(plan["hbm_budget_gb"], 2),
                 "managed_footprint_gb_per_gpu": round(plan["footprint_gb"], 2),
@@ -175,8 +187,8 @@ def main() -> None:
             },
             "aux": {
                 **aux,
-                "link_gbps_per_gpu": round(s["bytes_xfer_htd"] / max(dt, 1e-9) / 1e9, 2),
-                "delivered_bf16_gbps_per_gpu": round(max(s["decoded_bytes"], s["bytes_xfer_htd"]) / max(dt, 1e-9) / 1e9, 2),
+                "link_gbps_per_gpu": round((s["bytes_xfer_htd"] + s["bytes_xfer_ctd"]) / max(dt, 1e-9) / 1e9, 2),
+                "cxl_to_hbm_gbps_per_gpu": round(s["bytes_xfer_ctd"] / max(dt, 1e-9) / 1e9, 2),
                 "evictions": s["evictions"],
                 "init_s": round(init_s, 1),
             },

@@ -105,7 +105,7 @@ class TieredLlama:
     def __init__(self, cfg: LlamaConfig, batch: int, context: int, max_new_tokens: int = 64, oversub: float = 2.0,
                  device: int = 0, tp_rank: int = 0, tp_world: int = 1, seed: int = 0, lookahead: int = 2,
                  hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
-                 packed: bool = True, weight_format: str = "bf11"):
+                 packed: bool = True, weight_format: str = "bf11", tiers: str = "host", cxl_frac: float = 0.5):
         assert cfg.n_heads % tp_world == 0 and cfg.n_kv_heads % tp_world == 0 and cfg.ffn_dim % tp_world == 0
         assert cfg.vocab % tp_world == 0
         self.cfg, self.B, self.ctx = cfg, batch, context
@@ -183,6 +183,23 @@ class TieredLlama:
         self.window_bytes = lookahead * chunks(max(self.res_layer_bytes, self.res_head_bytes))
         self.streamed_bytes = (sum(self.res_layer_bytes for r in self.resident if not r)
                                + (0 if self.head_resident else self.res_head_bytes))
+        # ---- where streamed tensors rest: host DRAM, or split host DRAM / CXL.mem
+        # (three-tier: HBM + host + CXL). Streamed tensors are interleaved over
+        # the two so every step reads both pools (capacity tiering; both cross
+        # the same PCIe link to the GPU).
+        if tiers not in ("host", "host+cxl"):
+            raise ValueError("tiers must be 'host' or 'host+cxl'")
+        self.tiers = tiers
+        streamed_keys = [("layer", i) for i in range(cfg.n_layers) if not self.resident[i]]
+        if not self.head_resident:
+            streamed_keys.append(("head", 0))
+        self.rest_loc = {}
+        cxl_loc = rt.Loc.cxl() if tiers == "host+cxl" else None
+        for j, key in enumerate(streamed_keys):
+            to_cxl = cxl_loc is not None and int((j + 1) * cxl_frac) > int(j * cxl_frac)
+            self.rest_loc[key] = cxl_loc if to_cxl else host
+        self.cxl_streamed_bytes = sum(self.res_layer_bytes if k[0] == "layer" else self.res_head_bytes
+                                      for k, l in self.rest_loc.items() if l is cxl_loc and cxl_loc is not None)
         # ---- allocate + init
         self.embed = rt.malloc_managed(self.embed_bytes, "embed")
         self.embed.set_preferred_location(host)
@@ -200,7 +217,7 @@ class TieredLlama:
             else:
                 stream = self._gen_layer(i)
                 b = rt.malloc_managed(self.layer_bytes, f"layer{i}", packed_bf16=self.packed and not self.resident[i])
-            self._place(b, self.resident[i], gpu, host)
+            self._place(b, self.resident[i], gpu, self.rest_loc.get(("layer", i), host))
             b.write(stream)
             self.layers.append(b)
             del stream
@@ -214,7 +231,7 @@ class TieredLlama:
         else:
             stream = head
             self.head = rt.malloc_managed(self.head_bytes, "lm_head", packed_bf16=self.packed and not self.head_resident)
-        self._place(self.head, self.head_resident, gpu, host)
+        self._place(self.head, self.head_resident, gpu, self.rest_loc.get(("head", 0), host))
         self.head.write(stream)
         del head, stream
         self.embed.write(self._gen_embed())
@@ -266,7 +283,8 @@ class TieredLlama:
             "streamed_gb_per_step": self.streamed_bytes / 1e9, "init_s": getattr(self, "init_seconds", None),
             "packed_host_copies": getattr(self, "packed", False),
             "weight_format": self.wfmt, "resting_layer_gb": self.res_layer_bytes / 1e9,
-            "stage_gb": self.stage_bytes / 1e9,
+            "stage_gb": self.stage_bytes / 1e9, "tiers": self.tiers,
+            "cxl_streamed_gb_per_step": self.cxl_streamed_bytes / 1e9,
         }
         if self.verbose and self.rank == 0:
             print("[ogkm] plan:", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}, flush=True)

@@ -129,3 +129,37 @@ def test_tensor_parallel_two_ranks_matches_single(fake_rt):
     assert len(tp) == 3
     for (tok1, log1), step in zip(single, tp):
         torch.testing.assert_close(torch.tensor(step["logits"]), log1, atol=0.05, rtol=0.05)
+
+
+def test_three_tier_host_and_cxl_streaming(fake_rt):
+    """Config 5 shape: HBM + host DRAM + CXL.mem. Streamed tensors rest
+    interleaved on the host and (emulated) CXL tiers; decode output is identical
+    to the two-tier run and every step streams the planned bytes."""
+    from ogkm import cxl
+
+    lib.shutdown()
+    rt.init("fake", fake_devices=1, fake_hbm_mb=512, lock_check=1, host_budget_mb=1024)
+    cxl.rediscover(lib.host_node(), "/sys")
+    cfg = llama.CONFIGS["small"]
+    outs = {}
+    for tiers in ("host", "host+cxl"):
+        m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=8, oversub=2.0, lookahead=1, seed=3,
+                              tiers=tiers)
+        m.keep_logits = True
+        tok = torch.tensor([4, 9])
+        logs = []
+        for s in range(3):
+            m.step(tok + s)
+            logs.append(m.last_logits.clone())
+        outs[tiers] = logs
+        if tiers == "host+cxl":
+            assert m.cxl_streamed_bytes > 0
+            locs = set()
+            for i, b in enumerate(m.layers):
+                if not m.resident[i]:
+                    info = b.residency(0)
+                    locs |= {x["tier"] for x in info["resident_on"]}
+            assert {"cxl", "host"} <= locs, locs
+        m.close()
+    for a, b in zip(outs["host"], outs["host+cxl"]):
+        assert torch.equal(a, b)
