@@ -59,6 +59,9 @@ def parse():
                          "and are unpacked per layer; bf16: raw weights")
     ap.add_argument("--no-packed", action="store_true",
                     help="with --weights bf16: raw host copies instead of BF12 copies decoded in the H2D kernel")
+    ap.add_argument("--kv-format", choices=("bf11", "bf16"), default="bf11",
+                    help="bf11: the prefilled KV context rests losslessly packed in HBM (unpacked per layer into a "
+                         "one-layer scratch), decode tokens raw; bf16: raw KV cache")
     ap.add_argument("--tiers", choices=("host", "host+cxl"), default="host",
                     help="where streamed weights rest: host DRAM, or interleaved host DRAM / CXL.mem (three-tier)")
     ap.add_argument("--cxl-frac", type=float, default=0.5, help="share of streamed tensors resting in CXL.mem")
@@ -130,7 +133,7 @@ def main() -> None:
     model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 2,
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
                               seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
-                              weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac)
+                              weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac, kv_format=a.kv_format)
     plan = model.describe()
     init_s = time.perf_counter() - t_init
     g = torch.Generator(device="cpu").manual_seed(42)
@@ -171,6 +174,8 @@ def main() -> None:
                 "seq_len": a.context,
                 "parallelism": f"tp{a.simulate_tp}-rank0-simulated" if sim else f"tp{world}",
                 "tiers": plan["tiers"],
+                "kv_format": plan["kv_format"],
+                "kv_resident_gb_per_gpu": round(plan["kv_resident_gb"], 2),
                 "cxl_streamed_gb_per_step_per_gpu": round(plan["cxl_streamed_gb_per_step"], 2),
                 "oversubscription": round(plan["oversubscription"], 3),
                 "hbm_budget_gb_per_gpu": round(plan["hbm_budget_gb"], 2),
@@ -181,8 +186,9 @@ def main() -> None:
                 "weight_format": plan["weight_format"],
                 "host_copy_format": (f"{plan['weight_format']}-lossless" if plan["weight_format"] != "bf16"
                                      else "bf12-lossless" if plan["packed_host_copies"] else "bf16"),
-                "hbm_copy_format": (f"{plan['weight_format']}-lossless (unpacked per layer)"
-                                    if plan["weight_format"] != "bf16" else "bf16"),
+                "hbm_copy_format": ("bf11-lossless (decoded in the GEMM's registers)" if plan["weight_format"] == "bf11"
+                                    else "bf12-lossless (unpacked per layer)" if plan["weight_format"] == "bf12"
+                                    else "bf16"),
                 "resting_bytes_ratio": round(plan["resting_layer_gb"] / plan["layer_gb"], 4),
             },
             "aux": {

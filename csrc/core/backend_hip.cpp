@@ -264,8 +264,9 @@ class HipBackend : public Backend {
   }
 
   Status unpack_bf12_stream(int, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values, uint64_t,
-                            void* s, uint32_t workgroups) override {
-    HIPCHK(launch_bf12_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s));
+                            void* s, uint32_t workgroups, uint64_t dst_stride) override {
+    HIPCHK(launch_bf12_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s,
+                              dst_stride));
     launches_++;
     return Status::OK;
   }

@@ -309,13 +309,13 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_
   return off;
 }
 
-bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n) {
+bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n, uint64_t dst_stride) {
   Bf12StreamHeader h;
   memcpy(&h, stream, sizeof h);
   if (h.magic != kBf12StreamMagic || h.n_values != n) return false;
   const Bf12StreamChunk* t = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof h);
   for (uint32_t c = 0; c < h.nchunks; ++c) {
-    uint16_t* dst = out + (uint64_t)c * h.chunk_values;
+    uint16_t* dst = out + (uint64_t)c * (dst_stride ? dst_stride : h.chunk_values);
     if (t[c].encoded == 2) {
       if (!bf11_decode(stream + t[c].offset, dst, t[c].n_values)) return false;
     } else if (t[c].encoded == 1) {

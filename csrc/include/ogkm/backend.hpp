@@ -97,8 +97,9 @@ class Backend {
   // unpacking passes a full-chip grid.
   virtual Status decode_bf12(int dev, const DecodeDesc* d, size_t n, void* stream, uint32_t workgroups = 0) = 0;
   // Unpack a device-resident BF12 stream (codec.hpp) of n_values into bf16 at dst.
+  // Chunk c lands at dst + c * dst_stride values (0 = contiguous).
   virtual Status unpack_bf12_stream(int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
-                                    uint64_t n_values, void* stream, uint32_t workgroups) = 0;
+                                    uint64_t n_values, void* stream, uint32_t workgroups, uint64_t dst_stride = 0) = 0;
   // Decode GEMM (ogkm/dgemm.hpp): split-K partials, then the fused epilogue.
   virtual Status dgemm(int dev, const DGemmArgs& a, int mode, void* stream) = 0;
   virtual Status dgemm_reduce(int dev, const DGemmReduceArgs& a, void* stream) = 0;

@@ -157,6 +157,7 @@ inline uint64_t bf12_pack_bound(uint64_t n_values, uint32_t chunk_values) {
 uint64_t bf12_pack(const uint16_t* in, uint64_t n_values, uint32_t chunk_values, uint8_t* out, uint64_t cap,
                    unsigned threads, PackFormat fmt = PackFormat::BF12);
 // Reference unpack of a whole stream (CPU).
-bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n_values);
+// dst_stride: chunk c lands at out + c * dst_stride values (0 = contiguous).
+bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n_values, uint64_t dst_stride = 0);
 
 }  // namespace ogkm

@@ -52,9 +52,10 @@ struct KBf12Descs {
 };
 hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgroups, hipStream_t s);
 // Unpack a whole BF12 stream (codec.hpp) that lives in device memory into bf16
-// at `dst`: one launch, one work item per 32768-value tile of every chunk.
+// at `dst` (chunk c at dst + c * dst_stride values; 0 = contiguous): one
+// launch, one work item per 32768-value tile of every chunk.
 hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
-                              uint32_t workgroups, hipStream_t s);
+                              uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0);
 
 // Decode GEMM (csrc/kernels/decode_gemm.hip); argument structs in ogkm/dgemm.hpp.
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);

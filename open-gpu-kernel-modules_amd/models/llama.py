@@ -105,7 +105,8 @@ class TieredLlama:
     def __init__(self, cfg: LlamaConfig, batch: int, context: int, max_new_tokens: int = 64, oversub: float = 2.0,
                  device: int = 0, tp_rank: int = 0, tp_world: int = 1, seed: int = 0, lookahead: int = 2,
                  hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
-                 packed: bool = True, weight_format: str = "bf11", tiers: str = "host", cxl_frac: float = 0.5):
+                 packed: bool = True, weight_format: str = "bf11", tiers: str = "host", cxl_frac: float = 0.5,
+                 kv_format: str = "bf16"):
         assert cfg.n_heads % tp_world == 0 and cfg.n_kv_heads % tp_world == 0 and cfg.ffn_dim % tp_world == 0
         assert cfg.vocab % tp_world == 0
         self.cfg, self.B, self.ctx = cfg, batch, context
@@ -152,6 +153,8 @@ class TieredLlama:
         self.packfmt = "bf11s" if weight_format == "bf11" else weight_format
         self.stage_bytes = chunks(max(self.layer_bytes, self.head_bytes)) if self.staged else 0
         self.arena_bytes = self.budget - self.stage_bytes
+        if kv_format == "bf11":
+            self.arena_bytes -= chunks(self.kv_layer_bytes)  # the per-layer KV scratch
         lib.init_device(device, self.arena_bytes)
         self.pinfo: dict = {}
         self.pmode: dict = {}
@@ -159,6 +162,31 @@ class TieredLlama:
         host = rt.Loc.host()
         t0 = time.perf_counter()
         self._seed, self._std = seed, init_std
+        # ---- KV cache format. "bf16": raw [L, 2, B, hkv, T, hd]. "bf11": the
+        # prefilled context rests losslessly packed (one BF11 chunk per (k|v, b,
+        # head) row block of ctx x hd values), decode tokens in a raw tail; per
+        # layer the prefix is unpacked (k_bf12_unpack, strided into row blocks of
+        # T x hd) into one [2, B, hkv, T, hd] scratch that attention reads.
+        if kv_format not in ("bf16", "bf11"):
+            raise ValueError("kv_format must be 'bf16' or 'bf11'")
+        cv = context * hd
+        if kv_format == "bf11" and (cv & (cv - 1) or cv < 8192 or cv > (1 << 20)):
+            raise ValueError("kv_format='bf11' needs context * head_dim to be a power of two in [8 Ki, 1 Mi]")
+        self.kv_format = kv_format
+        self.tail = self.T - context
+        self.kv_tail_bytes = cfg.n_layers * 2 * batch * self.hkv * self.tail * hd * 2
+        self.kv_scratch_bytes = self.kv_layer_bytes if kv_format == "bf11" else 0
+        self.kv_streams, self.kv_infos, self.kv_slot = [], [], 0
+        if kv_format == "bf11":
+            for i, full in enumerate(self._gen_prefill()):
+                st, inf = bf12.pack(full, chunk_values=cv, fmt="bf11")
+                self.kv_streams.append(st)
+                self.kv_infos.append(inf)
+                del full
+            self.kv_slot = _al(max(i.nbytes for i in self.kv_infos))
+            self.kv_resident_bytes = cfg.n_layers * self.kv_slot + _al(self.kv_tail_bytes)
+        else:
+            self.kv_resident_bytes = _al(self.kv_bytes)
         if self.wpacked:
             # The packed size of layer 0 sizes the plan (all layers share one distribution).
             first, info0 = bf12.pack(self._gen_layer(0), fmt=self.packfmt)
@@ -170,7 +198,7 @@ class TieredLlama:
             self.res_layer_bytes, self.res_head_bytes = self.layer_bytes, self.head_bytes
         # ---- residency plan (in resting bytes: packed or raw)
         staging = (lookahead + 1) * chunks(max(self.res_layer_bytes, self.res_head_bytes))
-        avail = self.arena_bytes - chunks(_al(self.kv_bytes) + self.norm_bytes) - staging
+        avail = self.arena_bytes - chunks(self.kv_resident_bytes + self.norm_bytes) - staging
         if avail < 0:
             raise ValueError(f"HBM budget {self.budget/2**30:.1f} GiB too small for KV + staging "
                              f"({(chunks(self.kv_bytes) + staging + self.stage_bytes)/2**30:.1f} GiB)")
@@ -205,7 +233,7 @@ class TieredLlama:
         self.embed.set_preferred_location(host)
         self.embed.set_accessed_by(device)
         # KV cache + the RMSNorm weights (tiny) share one resident range
-        self.kv = rt.malloc_managed(_al(self.kv_bytes) + self.norm_bytes, "kv")
+        self.kv = rt.malloc_managed(self.kv_resident_bytes + self.norm_bytes, "kv")
         self.kv.set_preferred_location(gpu)
         self.layers = []
         for i in range(cfg.n_layers):
@@ -240,25 +268,31 @@ class TieredLlama:
         self.stage = (torch.empty(self.stage_bytes // 2, dtype=torch.bfloat16, device=self.tdev)
                       if self.staged else None)
         # RMSNorm weights of every layer + the final norm (after the KV cache)
-        self.kv.write(torch.ones((2 * cfg.n_layers + 1) * cfg.dim, dtype=torch.bfloat16), offset=_al(self.kv_bytes))
+        self.kv.write(torch.ones((2 * cfg.n_layers + 1) * cfg.dim, dtype=torch.bfloat16),
+                      offset=self.kv_resident_bytes)
+        for i, st in enumerate(self.kv_streams):
+            self.kv.write(st, offset=i * self.kv_slot)
+        self.kv_streams = []
         self.cos, self.sin = D.rope_tables(hd, self.T, cfg.rope_theta, self.tdev)
         # KV cache: leased for the model's lifetime (hot, written every step)
         self.kv_lease = self.kv.acquire(device, rt.WRITE)
         self.kv_lease.wait()
-        kv = self.kv_lease.tensor((cfg.n_layers, 2, batch, self.hkv, self.T, hd), torch.bfloat16)
-        self.norm_w = rt._tensor_from_ptr(self.kv_lease.dptr + _al(self.kv_bytes), (2 * cfg.n_layers + 1, cfg.dim),
-                                          torch.bfloat16, "cpu" if self.fake else "cuda", device)
+        tdev = "cpu" if self.fake else "cuda"
+        self.norm_w = rt._tensor_from_ptr(self.kv_lease.dptr + self.kv_resident_bytes, (2 * cfg.n_layers + 1, cfg.dim),
+                                          torch.bfloat16, tdev, device)
         self.final_norm = self.norm_w[2 * cfg.n_layers]
-        # Synthetic prefilled context, generated at full head count and sliced to
-        # this rank's KV heads so every TP degree decodes the same model state.
-        g = torch.Generator(device=self.tdev).manual_seed(seed + 7919)
-        h0 = self.rank * self.hkv
-        for i in range(cfg.n_layers):
-            full = torch.empty(2, batch, cfg.n_kv_heads, context, hd, dtype=torch.bfloat16, device=self.tdev)
-            full.normal_(0.0, 1.0, generator=g)
-            kv[i, :, :, :, :context].copy_(full[:, :, h0:h0 + self.hkv])
-            del full
-        self.kv_t = kv
+        if kv_format == "bf16":
+            kv = self.kv_lease.tensor((cfg.n_layers, 2, batch, self.hkv, self.T, hd), torch.bfloat16)
+            for i, full in enumerate(self._gen_prefill()):
+                kv[i, :, :, :, :context].copy_(full)
+                del full
+            self.kv_t = kv
+        else:
+            self.kv_t = None
+            self.kv_tail_t = rt._tensor_from_ptr(self.kv_lease.dptr + cfg.n_layers * self.kv_slot,
+                                                 (cfg.n_layers, 2, batch, self.hkv, max(self.tail, 1), hd),
+                                                 torch.bfloat16, tdev, device)
+            self.kv_scratch = torch.empty(2, batch, self.hkv, self.T, hd, dtype=torch.bfloat16, device=self.tdev)
         self.pos = context
         # ---- streaming schedule: use order within a step
         self.order = [("layer", i) for i in range(cfg.n_layers)] + [("head", 0)]
@@ -283,7 +317,8 @@ class TieredLlama:
             "streamed_gb_per_step": self.streamed_bytes / 1e9, "init_s": getattr(self, "init_seconds", None),
             "packed_host_copies": getattr(self, "packed", False),
             "weight_format": self.wfmt, "resting_layer_gb": self.res_layer_bytes / 1e9,
-            "stage_gb": self.stage_bytes / 1e9, "tiers": self.tiers,
+            "stage_gb": self.stage_bytes / 1e9, "tiers": self.tiers, "kv_format": self.kv_format,
+            "kv_resident_gb": self.kv_resident_bytes / 1e9,
             "cxl_streamed_gb_per_step": self.cxl_streamed_bytes / 1e9,
         }
         if self.verbose and self.rank == 0:
@@ -335,6 +370,53 @@ class TieredLlama:
         put("wd", tpmod.shard_cols(wd, self.rank, self.world))
         del wd
         return flat
+
+    def _gen_prefill(self):
+        """Synthetic prefilled context per layer, [2, B, hkv, ctx, hd] bf16,
+        generated at full head count and sliced to this rank's KV heads so every
+        TP degree decodes the same model state."""
+        cfg = self.cfg
+        g = torch.Generator(device=self.tdev).manual_seed(self._seed + 7919)
+        h0 = self.rank * self.hkv
+        for _ in range(cfg.n_layers):
+            full = torch.empty(2, self.B, cfg.n_kv_heads, self.ctx, cfg.head_dim, dtype=torch.bfloat16,
+                               device=self.tdev)
+            full.normal_(0.0, 1.0, generator=g)
+            yield full[:, :, h0:h0 + self.hkv].contiguous()
+            del full
+
+    def _kv_layer(self, i: int, pos: int) -> torch.Tensor:
+        """Layer i's KV cache as [2, B, hkv, T, hd], valid for positions < pos."""
+        if self.kv_format == "bf16":
+            return self.kv_t[i]
+        sc = self.kv_scratch
+        bf12.unpack_into(sc, self.kv_lease.dptr + i * self.kv_slot, self.kv_infos[i], self.dev,
+                         0 if self.fake else None, dst_stride=self.T * self.cfg.head_dim)
+        t = pos - self.ctx
+        if t > 0:
+            sc[:, :, :, self.ctx:pos].copy_(self.kv_tail_t[i, :, :, :, :t])
+        return sc
+
+    def _kv_append(self, i: int, pos: int, kv_layer: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> None:
+        kv_layer[0, :, :, pos].copy_(k)
+        kv_layer[1, :, :, pos].copy_(v)
+        if self.kv_format == "bf11":
+            t = pos - self.ctx
+            self.kv_tail_t[i, 0, :, :, t].copy_(k)
+            self.kv_tail_t[i, 1, :, :, t].copy_(v)
+
+    def host_kv(self, i: int) -> torch.Tensor:
+        """Layer i's KV cache [2, B, hkv, T, hd] on the host (reference numerics)."""
+        if self.kv_format == "bf16":
+            return self.kv_t[i].cpu()
+        if not self.fake:
+            torch.cuda.synchronize(self.dev)
+        raw = self.kv.read(offset=i * self.kv_slot, nbytes=self.kv_infos[i].nbytes)
+        out = torch.zeros(2, self.B, self.hkv, self.T, self.cfg.head_dim, dtype=torch.bfloat16)
+        pre = bf12.unpack_host(raw, self.kv_infos[i]).view(2, self.B, self.hkv, self.ctx, self.cfg.head_dim)
+        out[:, :, :, :self.ctx] = pre
+        out[:, :, :, self.ctx:] = self.kv_tail_t[i, :, :, :, :self.tail].cpu()
+        return out
 
     def _head_gen(self) -> torch.Generator:
         return torch.Generator(device=self.tdev).manual_seed(self._seed * 1000003 + 999983)
@@ -437,10 +519,9 @@ class TieredLlama:
             v = qkv[:, (self.hq + self.hkv) * hd:].view(B, self.hkv, hd)
             q = D.apply_rope(q, cos, sin)
             k = D.apply_rope(k, cos, sin)
-            kc, vc = self.kv_t[i, 0], self.kv_t[i, 1]
-            kc[:, :, pos].copy_(k)
-            vc[:, :, pos].copy_(v)
-            a = D.gqa_decode_attention(q, kc, vc, pos + 1)
+            kvl = self._kv_layer(i, pos)
+            self._kv_append(i, pos, kvl, k, v)
+            a = D.gqa_decode_attention(q, kvl[0], kvl[1], pos + 1)
             x = self._row_parallel(a, w["wo"], x)
             h = D.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps)
             g = dgemm.linear(h, w["wgu"], "silu_mul", device_index=dv)
@@ -494,8 +575,9 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
         k = qkv[:, model.hq * hd:(model.hq + model.hkv) * hd].view(B, model.hkv, hd)
         v = qkv[:, (model.hq + model.hkv) * hd:].view(B, model.hkv, hd)
         q, k = D.apply_rope(q, cos, sin), D.apply_rope(k, cos, sin)
-        kc = model.kv_t[i, 0].float().clone()
-        vc = model.kv_t[i, 1].float().clone()
+        kvh = model.host_kv(i).float().to(dev)
+        kc = kvh[0].clone()
+        vc = kvh[1].clone()
         kc[:, :, pos] = k
         vc[:, :, pos] = v
         a = D.gqa_decode_attention(q, kc, vc, pos + 1)

@@ -87,15 +87,21 @@ def unpack_host(stream: torch.Tensor, info: PackedInfo) -> torch.Tensor:
 
 
 def unpack_into(dst: torch.Tensor, src_ptr: int, info: PackedInfo, device: int = 0, stream: int | None = None,
-                workgroups: int = 0) -> torch.Tensor:
-    """Unpack the stream at device address ``src_ptr`` into ``dst`` (bf16, at least
-    n_values) on ``stream`` (default: the current torch stream of ``device``)."""
-    if dst.dtype != torch.bfloat16 or dst.numel() < info.n_values:
-        raise ValueError("dst must be bf16 with room for n_values")
+                workgroups: int = 0, dst_stride: int = 0) -> torch.Tensor:
+    """Unpack the stream at device address ``src_ptr`` into ``dst`` (bf16) on
+    ``stream`` (default: the current torch stream of ``device``). ``dst_stride``:
+    chunk c lands at element c * dst_stride (0 = contiguous), e.g. KV row blocks
+    into a cache with room for more tokens per row."""
+    need = info.n_values if not dst_stride else (info.nchunks - 1) * dst_stride + (
+        info.n_values - (info.nchunks - 1) * info.chunk_values)
+    if dst_stride and dst_stride < info.chunk_values:
+        raise ValueError("dst_stride must be >= chunk_values")
+    if dst.dtype != torch.bfloat16 or dst.numel() < need:
+        raise ValueError("dst must be bf16 with room for the unpacked chunks")
     if stream is None:
         stream = int(torch.cuda.current_stream(device).cuda_stream) if dst.is_cuda else 0
     lib.bf12_unpack(device, src_ptr, dst.data_ptr(), info.nchunks, info.chunk_values, info.n_values, stream,
-                    workgroups)
+                    workgroups, dst_stride)
     return dst
 
 

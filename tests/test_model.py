@@ -18,9 +18,11 @@ from ogkm.models import llama
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_tiny_decode_matches_fp32_reference(fake_rt):
+@pytest.mark.parametrize("kv_format,context", [("bf16", 8), ("bf11", 128)])
+def test_tiny_decode_matches_fp32_reference(fake_rt, kv_format, context):
     cfg = llama.CONFIGS["tiny"]
-    m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=4, oversub=1.5, lookahead=1, seed=5)
+    m = llama.TieredLlama(cfg, batch=2, context=context, max_new_tokens=4, oversub=1.5, lookahead=1, seed=5,
+                          kv_format=kv_format)
     m.keep_logits = True
     tok = torch.tensor([3, 11])
     for _ in range(3):
@@ -163,3 +165,25 @@ def test_three_tier_host_and_cxl_streaming(fake_rt):
         m.close()
     for a, b in zip(outs["host"], outs["host+cxl"]):
         assert torch.equal(a, b)
+
+
+def test_bf11_kv_cache_bit_identical_to_bf16(fake_rt):
+    """The packed (BF11 prefix + raw tail) KV cache decodes the exact bf16
+    context: logits are bit-identical to the raw cache, and it rests smaller."""
+    cfg = llama.CONFIGS["tiny"]
+    out, res = {}, {}
+    for fmt in ("bf16", "bf11"):
+        m = llama.TieredLlama(cfg, batch=2, context=128, max_new_tokens=4, oversub=1.2, lookahead=1, seed=9,
+                              kv_format=fmt)
+        m.keep_logits = True
+        tok = torch.tensor([5, 7])
+        logs = []
+        for s in range(3):
+            tok = m.step(tok)
+            logs.append(m.last_logits.clone())
+        out[fmt] = logs
+        res[fmt] = m.kv_resident_bytes
+        m.close()
+    for a, b in zip(out["bf16"], out["bf11"]):
+        assert torch.equal(a, b)
+    assert res["bf11"] < 0.8 * res["bf16"]
