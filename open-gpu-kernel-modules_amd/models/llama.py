@@ -24,6 +24,7 @@ layer Megatron-style; each rank streams only its shard over its own PCIe link.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -197,12 +198,22 @@ class TieredLlama:
             first = None
             self.res_layer_bytes, self.res_head_bytes = self.layer_bytes, self.head_bytes
         # ---- residency plan (in resting bytes: packed or raw)
-        staging = (lookahead + 1) * chunks(max(self.res_layer_bytes, self.res_head_bytes))
-        avail = self.arena_bytes - chunks(self.kv_resident_bytes + self.norm_bytes) - staging
+        # Streaming slots: the tensor in use + `lookahead` prefetched + one more,
+        # because the host runs ahead of the GPU: when tensor i+lookahead is
+        # prefetched, tensor i-1 may still be read by queued kernels (its chunks
+        # free only when they finish). Without that slot the allocator evicts a
+        # resident layer instead of waiting, and it is re-streamed later.
+        slot = chunks(max(self.res_layer_bytes, self.res_head_bytes))
+        fixed = chunks(self.kv_resident_bytes + self.norm_bytes)
+        staging = (lookahead + 2) * slot
+        if self.arena_bytes - fixed - staging < slot:  # tiny budgets: no room for the run-ahead slot
+            staging = (lookahead + 1) * slot
+        avail = self.arena_bytes - fixed - staging
         if avail < 0:
             raise ValueError(f"HBM budget {self.budget/2**30:.1f} GiB too small for KV + staging "
                              f"({(chunks(self.kv_bytes) + staging + self.stage_bytes)/2**30:.1f} GiB)")
-        n_res = max(0, min(cfg.n_layers, avail // chunks(self.res_layer_bytes)))
+        n_res = max(0, min(cfg.n_layers, avail // chunks(self.res_layer_bytes)
+                           - int(os.environ.get("OGKM_RESIDENT_MARGIN", "0"))))
         left = avail - n_res * chunks(self.res_layer_bytes)
         self.head_resident = left >= chunks(self.res_head_bytes)
         # spread resident layers evenly so streaming continues behind them
