@@ -141,6 +141,8 @@ def main() -> None:
     for _ in range(a.warmup):
         tok = model.step(tok)
     lib.reset_counters()
+    if a.verbose:
+        model.byte_trace = {}
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -150,6 +152,12 @@ def main() -> None:
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
     s = lib.stats()
+    if a.verbose and model.byte_trace is not None and e.rank == 0:
+        res = {k: v for k, v in model.byte_trace.items() if model._is_resident(k) and v}
+        print("[ogkm] H2D bytes/step around resident tensors:",
+              {f"{k[0]}{k[1]}": round(v / a.steps / 1e9, 3) for k, v in res.items()}, flush=True)
+        print(f"[ogkm] H2D GB/step total {s['bytes_xfer_htd'] / a.steps / 1e9:.2f}, planned streamed "
+              f"{plan['streamed_gb_per_step']:.2f}", flush=True)
     tokens = a.batch * a.steps
     value = tokens / dt
     if e.rank == 0:

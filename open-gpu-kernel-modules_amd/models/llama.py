@@ -311,6 +311,7 @@ class TieredLlama:
         self._pf_next = 0           # next index in stream_seq to prefetch (cyclic)
         self._inflight: list = []   # prefetched, not yet consumed
         self._views: dict = {}
+        self.byte_trace = None     # diagnostics: {key: H2D bytes submitted around its use}
         self.keep_logits = False   # tests: keep the full-vocab logits of the last step
         self.last_logits = None
         self.init_seconds = time.perf_counter() - t0
@@ -487,11 +488,16 @@ class TieredLlama:
         until they are enqueued). bf12: the stream is unpacked into the staging
         buffer on the compute stream and the lease is released right away (the
         ring reuses the chunks only after the unpack has read them)."""
+        acct = self.byte_trace is not None
+        if acct:
+            b0 = lib.stats()["bytes_xfer_htd"]
         if not self._is_resident(key):
             if self._inflight and self._inflight[0] == key:
                 self._inflight.pop(0)
             self._prefetch_ahead()
         lease = self._buf(key).acquire(self.dev, rt.READ)
+        if acct:  # H2D bytes submitted while servicing this tensor (prefetch window + its own faults)
+            self.byte_trace[key] = self.byte_trace.get(key, 0) + lib.stats()["bytes_xfer_htd"] - b0
         lease.wait(0 if self.fake else None)
         if self.staged:
             bf12.unpack_into(self.stage, lease.dptr, self.pinfo[key], self.dev, 0 if self.fake else None)
