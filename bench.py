@@ -130,7 +130,7 @@ def main() -> None:
     comm.barrier()
     t_init = time.perf_counter()
     sim = a.simulate_tp > 1 and world == 1
-    model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 2,
+    model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 3,
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
                               seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
                               weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac, kv_format=a.kv_format)
@@ -152,6 +152,17 @@ def main() -> None:
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
     s = lib.stats()
+    if a.verbose:
+        # host enqueue time of one step (no sync inside) vs its synchronized time
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        tok = model.step(tok)
+        h1 = time.perf_counter()
+        torch.cuda.synchronize()
+        h2 = time.perf_counter()
+        if e.rank == 0:
+            print(f"[ogkm] one step: host enqueue {1e3 * (h1 - h0):.1f} ms, synchronized {1e3 * (h2 - h0):.1f} ms",
+                  flush=True)
     if a.verbose and model.byte_trace is not None and e.rank == 0:
         res = {k: v for k, v in model.byte_trace.items() if model._is_resident(k) and v}
         print("[ogkm] H2D bytes/step around resident tensors:",

@@ -264,6 +264,19 @@ class FakeBackend : public Backend {
     run(s, [a] { dgemm_reduce_cpu(a); });
     return Status::OK;
   }
+  Status rmsnorm(int, const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim, uint32_t ldx,
+                 uint32_t ldy, float eps, void* s) override {
+    run(s, [=] { rmsnorm_cpu(x, w, y, rows, dim, ldx, ldy, eps); });
+    return Status::OK;
+  }
+  Status rope_kv(int, const RopeKvArgs& a, void* s) override {
+    run(s, [a] { rope_kv_cpu(a); });
+    return Status::OK;
+  }
+  Status attn_decode(int, const AttnArgs& a, void* s) override {
+    run(s, [a] { attn_decode_cpu(a); });
+    return Status::OK;
+  }
   Status gather_pages(int, const PageListDesc& d, void* s) override {
     std::vector<uint32_t> idx(d.idx, d.idx + d.npages);
     PageListDesc dd = d;

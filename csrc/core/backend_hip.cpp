@@ -281,6 +281,19 @@ class HipBackend : public Backend {
     launches_++;
     return Status::OK;
   }
+  Status rmsnorm(int, const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim, uint32_t ldx,
+                 uint32_t ldy, float eps, void* s) override {
+    HIPCHK(launch_rmsnorm(x, w, y, rows, dim, ldx, ldy, eps, (hipStream_t)s));
+    return Status::OK;
+  }
+  Status rope_kv(int, const RopeKvArgs& a, void* s) override {
+    HIPCHK(launch_rope_kv(a, (hipStream_t)s));
+    return Status::OK;
+  }
+  Status attn_decode(int, const AttnArgs& a, void* s) override {
+    HIPCHK(launch_attn_decode(a, (hipStream_t)s));
+    return Status::OK;
+  }
 
   Status page_list(int dev, const PageListDesc& d, void* s, bool scatter) {
     if (d.npages == 0) return Status::OK;

@@ -2,6 +2,7 @@
 // backend and tests: same fragment order, same packed-stream decode (one BF11
 // wave group per fragment, exceptions included), same split-K partial layout
 // and epilogues, f32 accumulation.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -94,6 +95,78 @@ void dgemm_reduce_cpu(const DGemmReduceArgs& a) {
       a.out[(uint64_t)m * a.ldo + n] = f2bf(y);
     }
   }
+}
+
+void rmsnorm_cpu(const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim, uint32_t ldx,
+                 uint32_t ldy, float eps) {
+  for (uint32_t r = 0; r < rows; ++r) {
+    const uint16_t* xr = x + (uint64_t)r * ldx;
+    float ss = 0.f;
+    for (uint32_t i = 0; i < dim; ++i) ss += bf2f(xr[i]) * bf2f(xr[i]);
+    const float inv = 1.f / std::sqrt(ss / (float)dim + eps);
+    for (uint32_t i = 0; i < dim; ++i) y[(uint64_t)r * ldy + i] = f2bf(bf2f(f2bf(bf2f(xr[i]) * inv)) * bf2f(w[i]));
+  }
+}
+
+void rope_kv_cpu(const RopeKvArgs& a) {
+  const uint32_t half = a.hd / 2, heads = a.hq + 2 * a.hkv;
+  for (uint32_t b = 0; b < a.B; ++b)
+    for (uint32_t hh = 0; hh < heads; ++hh)
+      for (uint32_t i = 0; i < half; ++i) {
+        const uint16_t* src = a.qkv + (uint64_t)b * a.ldqkv + (uint64_t)hh * a.hd;
+        float x1 = bf2f(src[i]), x2 = bf2f(src[i + half]);
+        if (hh < a.hq + a.hkv) {
+          const float c = a.cos[i], s = a.sin[i];
+          const float r1 = x1 * c - x2 * s, r2 = x2 * c + x1 * s;
+          x1 = r1;
+          x2 = r2;
+        }
+        const uint16_t o1 = f2bf(x1), o2 = f2bf(x2);
+        if (hh < a.hq) {
+          uint16_t* q = a.q_out + ((uint64_t)b * a.hq + hh) * a.hd;
+          q[i] = o1;
+          q[i + half] = o2;
+          continue;
+        }
+        const uint32_t kv = hh < a.hq + a.hkv ? 0u : 1u;
+        const uint32_t h = hh - a.hq - kv * a.hkv;
+        uint16_t* c = a.cache + ((((uint64_t)kv * a.B + b) * a.hkv + h) * a.T + a.pos) * a.hd;
+        c[i] = o1;
+        c[i + half] = o2;
+        if (a.tail) {
+          uint16_t* t = a.tail + ((((uint64_t)kv * a.B + b) * a.hkv + h) * a.tail_T + a.tail_pos) * a.hd;
+          t[i] = o1;
+          t[i + half] = o2;
+        }
+      }
+}
+
+void attn_decode_cpu(const AttnArgs& a) {
+  const uint32_t g = a.hq / a.hkv;
+  std::vector<float> sc(a.len), o(a.hd);
+  for (uint32_t b = 0; b < a.B; ++b)
+    for (uint32_t qh = 0; qh < a.hq; ++qh) {
+      const uint32_t kvh = qh / g;
+      const uint16_t* q = a.q + ((uint64_t)b * a.hq + qh) * a.hd;
+      const uint16_t* kb = a.cache + (((uint64_t)0 * a.B + b) * a.hkv + kvh) * (uint64_t)a.T * a.hd;
+      const uint16_t* vb = a.cache + (((uint64_t)1 * a.B + b) * a.hkv + kvh) * (uint64_t)a.T * a.hd;
+      float m = -INFINITY;
+      for (uint32_t t = 0; t < a.len; ++t) {
+        float s = 0.f;
+        for (uint32_t d = 0; d < a.hd; ++d) s += bf2f(q[d]) * a.scale * bf2f(kb[(uint64_t)t * a.hd + d]);
+        sc[t] = s;
+        m = std::max(m, s);
+      }
+      float l = 0.f;
+      for (uint32_t t = 0; t < a.len; ++t) {
+        sc[t] = std::exp(sc[t] - m);
+        l += sc[t];
+      }
+      std::fill(o.begin(), o.end(), 0.f);
+      for (uint32_t t = 0; t < a.len; ++t)
+        for (uint32_t d = 0; d < a.hd; ++d) o[d] += sc[t] * bf2f(vb[(uint64_t)t * a.hd + d]);
+      for (uint32_t d = 0; d < a.hd; ++d) a.out[((uint64_t)b * a.hq + qh) * a.hd + d] = f2bf(o[d] / l);
+    }
 }
 
 }  // namespace ogkm

@@ -45,6 +45,35 @@ inline void dgemm_plan(uint32_t N, uint32_t K, uint32_t target_units, uint32_t* 
   *ksplit = (K + *klen - 1) / *klen;
 }
 
+// ---- fused decode-step ops (csrc/kernels/decode_ops.hip)
+// KV cache layout: [2][B][Hkv][T][hd] bf16 (k then v).
+struct RopeKvArgs {
+  const uint16_t* qkv;     // [B, (hq + 2 hkv) * hd], row stride ldqkv
+  uint32_t ldqkv;
+  const float* cos;        // [hd / 2] at this position
+  const float* sin;
+  uint16_t* q_out;         // [B, hq, hd] rotated q
+  uint16_t* cache;         // [2][B][hkv][T][hd]: rotated k and v written at `pos`
+  uint16_t* tail;          // optional second copy [2][B][hkv][tail_T][hd] at `tail_pos`
+  uint32_t B, hq, hkv, hd, T, pos, tail_T, tail_pos;
+};
+struct AttnArgs {
+  const uint16_t* q;       // [B, hq, hd] (rotated)
+  const uint16_t* cache;   // [2][B][hkv][T][hd]
+  uint16_t* out;           // [B, hq * hd]
+  float* part_o;           // [B * hq * nsplit, hd] split partials (f32)
+  float* part_ml;          // [B * hq * nsplit, 2]  (max, sum) per split
+  uint32_t B, hq, hkv, hd, T, len, nsplit;
+  float scale;
+};
+constexpr uint32_t kAttnSplitTokens = 256;
+
+// CPU references of the decode-step ops (fake backend, tests).
+void rmsnorm_cpu(const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim, uint32_t ldx,
+                 uint32_t ldy, float eps);
+void rope_kv_cpu(const RopeKvArgs& a);
+void attn_decode_cpu(const AttnArgs& a);
+
 // CPU reference of k_dgemm / k_dgemm_reduce (fake backend, tests).
 void dgemm_cpu(const DGemmArgs& a, bool packed);
 void dgemm_reduce_cpu(const DGemmReduceArgs& a);

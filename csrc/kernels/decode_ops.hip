@@ -1,0 +1,250 @@
+// Fused decode-step kernels around the decode GEMM (one launch each, replacing
+// 5-20 framework kernels per op):
+//   k_rmsnorm       y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w)   one workgroup per row
+//   k_rope_kv       q/k rotate-half RoPE at one position, k/v appended into the
+//                   KV cache (and a second copy, the packed cache's raw tail)
+//   k_attn_decode   GQA decode attention, flash-decoding split over the
+//                   context: one workgroup per (batch, kv head, 256-token split)
+//                   computes the group's 8 query heads' scores (lane = token),
+//                   softmax partials and P.V (lane = head-dim pair) in f32;
+//   k_attn_combine  merges the splits (log-sum-exp) and writes bf16.
+// The KV cache layout is [2][B][Hkv][T][hd] (k then v), bf16.
+#include <hip/hip_runtime.h>
+
+#include "ogkm/kernels.hpp"
+
+namespace ogkm {
+
+__device__ __forceinline__ float dbf(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
+__device__ __forceinline__ uint16_t df2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- RMSNorm
+__global__ void __launch_bounds__(256) k_rmsnorm(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                 uint16_t* __restrict__ y, uint32_t dim, uint32_t ldx, uint32_t ldy,
+                                                 float eps) {
+  __shared__ float red[4];
+  const uint16_t* xr = x + (uint64_t)blockIdx.x * ldx;
+  uint16_t* yr = y + (uint64_t)blockIdx.x * ldy;
+  float ss = 0.f;
+  for (uint32_t i = threadIdx.x * 2; i < dim; i += 512) {
+    const uint32_t p = *reinterpret_cast<const uint32_t*>(xr + i);
+    const float a = dbf((uint16_t)p), b = dbf((uint16_t)(p >> 16));
+    ss += a * a + b * b;
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float r = rsqrtf(tot / (float)dim + eps);
+  for (uint32_t i = threadIdx.x * 2; i < dim; i += 512) {
+    const uint32_t p = *reinterpret_cast<const uint32_t*>(xr + i);
+    const uint32_t q = *reinterpret_cast<const uint32_t*>(w + i);
+    const float a = dbf(df2bf(dbf((uint16_t)p) * r)) * dbf((uint16_t)q);
+    const float b = dbf(df2bf(dbf((uint16_t)(p >> 16)) * r)) * dbf((uint16_t)(q >> 16));
+    *reinterpret_cast<uint32_t*>(yr + i) = (uint32_t)df2bf(a) | ((uint32_t)df2bf(b) << 16);
+  }
+}
+
+// ---------------------------------------------------------------- RoPE + KV append
+// One thread per (b, head, i < hd/2) over the q heads, then the k heads (rotated,
+// appended) and the v heads (appended).
+__global__ void __launch_bounds__(256) k_rope_kv(RopeKvArgs a) {
+  const uint32_t half = a.hd / 2;
+  const uint32_t heads = a.hq + 2 * a.hkv;
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (uint64_t)a.B * heads * half) return;
+  const uint32_t i = (uint32_t)(idx % half);
+  const uint32_t hh = (uint32_t)((idx / half) % heads);
+  const uint32_t b = (uint32_t)(idx / ((uint64_t)half * heads));
+  const uint16_t* src = a.qkv + (uint64_t)b * a.ldqkv + (uint64_t)hh * a.hd;
+  float x1 = dbf(src[i]), x2 = dbf(src[i + half]);
+  if (hh < a.hq + a.hkv) {
+    const float c = a.cos[i], s = a.sin[i];
+    const float r1 = x1 * c - x2 * s, r2 = x2 * c + x1 * s;
+    x1 = r1;
+    x2 = r2;
+  }
+  const uint16_t o1 = df2bf(x1), o2 = df2bf(x2);
+  if (hh < a.hq) {
+    uint16_t* q = a.q_out + ((uint64_t)b * a.hq + hh) * a.hd;
+    q[i] = o1;
+    q[i + half] = o2;
+    return;
+  }
+  const uint32_t kv = hh < a.hq + a.hkv ? 0u : 1u;
+  const uint32_t h = hh - a.hq - kv * a.hkv;
+  uint16_t* c = a.cache + ((((uint64_t)kv * a.B + b) * a.hkv + h) * a.T + a.pos) * a.hd;
+  c[i] = o1;
+  c[i + half] = o2;
+  if (a.tail) {
+    uint16_t* t = a.tail + ((((uint64_t)kv * a.B + b) * a.hkv + h) * a.tail_T + a.tail_pos) * a.hd;
+    t[i] = o1;
+    t[i + half] = o2;
+  }
+}
+
+// ---------------------------------------------------------------- attention
+constexpr int kAttnSplit = 256;  // tokens per workgroup
+constexpr int kMaxGroup = 16;    // query heads per kv head
+constexpr int kMaxHd = 128;
+
+__global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a) {
+  __shared__ float qs[kMaxGroup][kMaxHd];       // this kv head's query group, f32
+  __shared__ float ps[kMaxGroup][kAttnSplit];   // scores -> probabilities
+  __shared__ float ms[kMaxGroup], ls[kMaxGroup];
+  __shared__ float part[4][kMaxGroup][kMaxHd / 2 * 2];  // per-wave P.V partials
+  const uint32_t split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const uint32_t g = a.hq / a.hkv;
+  const uint32_t t0 = split * kAttnSplit;
+  const uint32_t nt = a.len - t0 < (uint32_t)kAttnSplit ? a.len - t0 : (uint32_t)kAttnSplit;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (uint32_t e = tid; e < g * a.hd; e += 256) {
+    const uint32_t h = e / a.hd, d = e - h * a.hd;
+    qs[h][d] = dbf(a.q[((uint64_t)b * a.hq + kvh * g + h) * a.hd + d]) * a.scale;
+  }
+  __syncthreads();
+  const uint16_t* kbase = a.cache + (((uint64_t)0 * a.B + b) * a.hkv + kvh) * (uint64_t)a.T * a.hd;
+  const uint16_t* vbase = a.cache + (((uint64_t)1 * a.B + b) * a.hkv + kvh) * (uint64_t)a.T * a.hd;
+  // scores: lane = token
+  if (tid < nt) {
+    const uint16_t* kr = kbase + (uint64_t)(t0 + tid) * a.hd;
+    float acc[kMaxGroup];
+#pragma unroll
+    for (int h = 0; h < kMaxGroup; ++h) acc[h] = 0.f;
+    for (uint32_t d = 0; d < a.hd; d += 8) {
+      const uint4 kv8 = *reinterpret_cast<const uint4*>(kr + d);
+      const uint32_t w4[4] = {kv8.x, kv8.y, kv8.z, kv8.w};
+      float kf[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        kf[2 * j] = dbf((uint16_t)w4[j]);
+        kf[2 * j + 1] = dbf((uint16_t)(w4[j] >> 16));
+      }
+#pragma unroll
+      for (int h = 0; h < kMaxGroup; ++h) {
+        if ((uint32_t)h < g) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[h] += kf[j] * qs[h][d + j];
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kMaxGroup; ++h)
+      if ((uint32_t)h < g) ps[h][tid] = acc[h];
+  }
+  __syncthreads();
+  // softmax partials per head: wave w reduces heads w, w+4, ...
+  for (uint32_t h = wave; h < g; h += 4) {
+    float m = -INFINITY;
+    for (uint32_t t = lane; t < nt; t += 64) m = fmaxf(m, ps[h][t]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (uint32_t t = lane; t < nt; t += 64) {
+      const float p = __expf(ps[h][t] - m);
+      ps[h][t] = p;
+      l += p;
+    }
+    l = wave_sum(l);
+    if (lane == 0) {
+      ms[h] = m;
+      ls[h] = l;
+    }
+  }
+  __syncthreads();
+  // P.V: lane = pair of head dims, wave = quarter of the tokens
+  const uint32_t d0 = lane * 2;
+  float o0[kMaxGroup], o1[kMaxGroup];
+#pragma unroll
+  for (int h = 0; h < kMaxGroup; ++h) o0[h] = o1[h] = 0.f;
+  if (d0 < a.hd) {
+    for (uint32_t t = wave; t < nt; t += 4) {
+      const uint32_t vv = *reinterpret_cast<const uint32_t*>(vbase + (uint64_t)(t0 + t) * a.hd + d0);
+      const float v0 = dbf((uint16_t)vv), v1 = dbf((uint16_t)(vv >> 16));
+#pragma unroll
+      for (int h = 0; h < kMaxGroup; ++h) {
+        if ((uint32_t)h < g) {
+          const float p = ps[h][t];
+          o0[h] += p * v0;
+          o1[h] += p * v1;
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kMaxGroup; ++h)
+      if ((uint32_t)h < g) {
+        part[wave][h][d0] = o0[h];
+        part[wave][h][d0 + 1] = o1[h];
+      }
+  }
+  __syncthreads();
+  // reduce the 4 waves and store this split's partial (unnormalised) + m, l
+  for (uint32_t e = tid; e < g * a.hd; e += 256) {
+    const uint32_t h = e / a.hd, d = e - h * a.hd;
+    const float o = part[0][h][d] + part[1][h][d] + part[2][h][d] + part[3][h][d];
+    const uint64_t row = ((uint64_t)b * a.hq + kvh * g + h) * a.nsplit + split;
+    a.part_o[row * a.hd + d] = o;
+    if (d == 0) {
+      a.part_ml[row * 2] = ms[h];
+      a.part_ml[row * 2 + 1] = ls[h];
+    }
+  }
+}
+
+// One workgroup of hd threads per (b, q head): merge the splits.
+__global__ void k_attn_combine(AttnArgs a) {
+  const uint32_t bh = blockIdx.x;  // b * hq + h
+  const uint32_t d = threadIdx.x;
+  float M = -INFINITY;
+  for (uint32_t s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[((uint64_t)bh * a.nsplit + s) * 2]);
+  float num = 0.f, den = 0.f;
+  for (uint32_t s = 0; s < a.nsplit; ++s) {
+    const uint64_t row = (uint64_t)bh * a.nsplit + s;
+    const float w = __expf(a.part_ml[row * 2] - M);
+    den += w * a.part_ml[row * 2 + 1];
+    if (d < a.hd) num += w * a.part_o[row * a.hd + d];
+  }
+  if (d < a.hd) a.out[(uint64_t)bh * a.hd + d] = df2bf(num / den);
+}
+
+hipError_t launch_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim,
+                          uint32_t ldx, uint32_t ldy, float eps, hipStream_t s) {
+  if (dim % 2 || ldx % 2 || ldy % 2 || !rows) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rmsnorm, dim3(rows), dim3(256), 0, s, x, w, y, dim, ldx, ldy, eps);
+  return hipGetLastError();
+}
+
+hipError_t launch_rope_kv(const RopeKvArgs& a, hipStream_t s) {
+  if (a.hd % 2 || a.pos >= a.T || (a.tail && a.tail_pos >= a.tail_T)) return hipErrorInvalidValue;
+  const uint64_t n = (uint64_t)a.B * (a.hq + 2 * a.hkv) * (a.hd / 2);
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_rope_kv, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
+  if (!a.hkv || a.hq % a.hkv || a.hq / a.hkv > (uint32_t)kMaxGroup || a.hd > (uint32_t)kMaxHd || a.hd % 8 ||
+      !a.len || a.len > a.T)
+    return hipErrorInvalidValue;
+  if (a.nsplit != (a.len + kAttnSplit - 1) / kAttnSplit) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_attn_decode, dim3(a.nsplit, a.hkv, a.B), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_attn_combine, dim3(a.B * a.hq), dim3(a.hd < 64 ? 64 : a.hd), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace ogkm

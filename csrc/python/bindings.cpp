@@ -641,6 +641,35 @@ PYBIND11_MODULE(_ogkm, m) {
   }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("w_off"), py::arg("mode"), py::arg("chunk_shift"),
      py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("part"), py::arg("part_bytes"),
      py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("target_units") = 2048, py::arg("unroll") = 0);
+  // Fused decode-step ops (ops/fused.py).
+  m.def("rmsnorm", [](int dev, uint64_t stream, uint64_t x, uint64_t w, uint64_t y, uint32_t rows, uint32_t dim,
+                      uint32_t ldx, uint32_t ldy, float eps) {
+    check(rt()->be()->rmsnorm(dev, (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, rows, dim, ldx, ldy, eps,
+                              (void*)stream),
+          "rmsnorm");
+  });
+  m.def("rope_kv", [](int dev, uint64_t stream, uint64_t qkv, uint32_t ldqkv, uint64_t cos, uint64_t sin,
+                      uint64_t q_out, uint64_t cache, uint64_t tail, uint32_t B, uint32_t hq, uint32_t hkv,
+                      uint32_t hd, uint32_t T, uint32_t pos, uint32_t tail_T, uint32_t tail_pos) {
+    RopeKvArgs a{(const uint16_t*)qkv, ldqkv, (const float*)cos, (const float*)sin, (uint16_t*)q_out,
+                 (uint16_t*)cache, (uint16_t*)tail, B, hq, hkv, hd, T, pos, tail_T, tail_pos};
+    check(rt()->be()->rope_kv(dev, a, (void*)stream), "rope_kv");
+  });
+  m.def("attn_decode", [](int dev, uint64_t stream, uint64_t q, uint64_t cache, uint64_t out, uint64_t part,
+                          uint64_t part_bytes, uint32_t B, uint32_t hq, uint32_t hkv, uint32_t hd, uint32_t T,
+                          uint32_t len, float scale) {
+    AttnArgs a{};
+    a.q = (const uint16_t*)q;
+    a.cache = (const uint16_t*)cache;
+    a.out = (uint16_t*)out;
+    a.B = B; a.hq = hq; a.hkv = hkv; a.hd = hd; a.T = T; a.len = len; a.scale = scale;
+    a.nsplit = (len + kAttnSplitTokens - 1) / kAttnSplitTokens;
+    const uint64_t rows = (uint64_t)B * hq * a.nsplit;
+    if (rows * (hd + 2) * 4 > part_bytes) throw StatusError("attn_decode: partial workspace too small");
+    a.part_o = (float*)part;
+    a.part_ml = (float*)part + rows * hd;
+    check(rt()->be()->attn_decode(dev, a, (void*)stream), "attn_decode");
+  });
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
     return py::make_tuple((uint64_t)fb.put, (uint64_t)fb.recs, fb.entries, fb.overflows);

@@ -33,7 +33,7 @@ import torch
 
 from .. import rt
 from .._native import lib
-from ..ops import bf12, dgemm
+from ..ops import bf12, dgemm, fused
 from ..ops import decode as D
 from ..ops.memory import managed_embedding
 from ..parallel import comm, tp as tpmod
@@ -312,6 +312,8 @@ class TieredLlama:
         self._inflight: list = []   # prefetched, not yet consumed
         self._views: dict = {}
         self.byte_trace = None     # diagnostics: {key: H2D bytes submitted around its use}
+        self._pinned: dict = {}    # resident tensors: key -> weight refs (leased for the model's lifetime)
+        self._pin_leases: list = []
         self.keep_logits = False   # tests: keep the full-vocab logits of the last step
         self.last_logits = None
         self.init_seconds = time.perf_counter() - t0
@@ -409,13 +411,12 @@ class TieredLlama:
             sc[:, :, :, self.ctx:pos].copy_(self.kv_tail_t[i, :, :, :, :t])
         return sc
 
-    def _kv_append(self, i: int, pos: int, kv_layer: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> None:
-        kv_layer[0, :, :, pos].copy_(k)
-        kv_layer[1, :, :, pos].copy_(v)
-        if self.kv_format == "bf11":
-            t = pos - self.ctx
-            self.kv_tail_t[i, 0, :, :, t].copy_(k)
-            self.kv_tail_t[i, 1, :, :, t].copy_(v)
+    def _rope_append(self, i: int, pos: int, kv_layer: torch.Tensor, qkv: torch.Tensor) -> torch.Tensor:
+        """RoPE on q/k + append k/v at pos (into the cache / scratch and the
+        packed cache's raw tail) in one fused kernel; returns rotated q."""
+        tail = self.kv_tail_t[i] if self.kv_format == "bf11" else None
+        return fused.rope_kv(qkv, self.cos[pos], self.sin[pos], kv_layer, pos, self.hq, self.hkv, tail=tail,
+                             tail_pos=pos - self.ctx, device_index=self.dev)
 
     def host_kv(self, i: int) -> torch.Tensor:
         """Layer i's KV cache [2, B, hkv, T, hd] on the host (reference numerics)."""
@@ -488,6 +489,9 @@ class TieredLlama:
         until they are enqueued). bf12: the stream is unpacked into the staging
         buffer on the compute stream and the lease is released right away (the
         ring reuses the chunks only after the unpack has read them)."""
+        pin = self._pinned.get(key)
+        if pin is not None:  # resident tensor: long-lived lease taken at init, refs cached
+            return None, pin
         acct = self.byte_trace is not None
         if acct:
             b0 = lib.stats()["bytes_xfer_htd"]
@@ -504,7 +508,14 @@ class TieredLlama:
             lease.release(0 if self.fake else None)
             return None, self._refs(key, self.stage.data_ptr(), dgemm.MODE_RAW)
         mode = self.pmode.get(key, dgemm.MODE_RAW)
-        return lease, self._refs(key, lease.dptr, mode)
+        refs = self._refs(key, lease.dptr, mode)
+        if self._is_resident(key) and not self.staged:
+            # Planned-resident tensors keep their lease (and so their HBM chunks)
+            # for the model's lifetime: later uses cost no runtime call.
+            self._pinned[key] = refs
+            self._pin_leases.append(lease)
+            return None, refs
+        return lease, refs
 
     def _refs(self, key, ptr: int, mode: int) -> dict:
         shift = (self.pinfo[key].chunk_values.bit_length() - 1) if key in self.pinfo else 20
@@ -525,27 +536,21 @@ class TieredLlama:
         x = managed_embedding(self.embed, tokens, cfg.dim, torch.bfloat16, self.dev)
         if self.fake:
             x = x.to(self.tdev)
-        cos, sin = self.cos[pos], self.sin[pos]
         dv = self.dev
         for i in range(cfg.n_layers):
             lease, w = self._use(("layer", i))
-            h = D.rms_norm(x, self.norm_w[2 * i], cfg.norm_eps)
+            h = fused.rms_norm(x, self.norm_w[2 * i], cfg.norm_eps, device_index=dv)
             qkv = dgemm.linear(h, w["wqkv"], device_index=dv)
-            q = qkv[:, :self.hq * hd].view(B, self.hq, hd)
-            k = qkv[:, self.hq * hd:(self.hq + self.hkv) * hd].view(B, self.hkv, hd)
-            v = qkv[:, (self.hq + self.hkv) * hd:].view(B, self.hkv, hd)
-            q = D.apply_rope(q, cos, sin)
-            k = D.apply_rope(k, cos, sin)
             kvl = self._kv_layer(i, pos)
-            self._kv_append(i, pos, kvl, k, v)
-            a = D.gqa_decode_attention(q, kvl[0], kvl[1], pos + 1)
+            q = self._rope_append(i, pos, kvl, qkv)
+            a = fused.attention(q, kvl, pos + 1, device_index=dv)
             x = self._row_parallel(a, w["wo"], x)
-            h = D.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps)
+            h = fused.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps, device_index=dv)
             g = dgemm.linear(h, w["wgu"], "silu_mul", device_index=dv)
             x = self._row_parallel(g, w["wd"], x)
             if lease is not None:
                 lease.release(0 if self.fake else None)
-        x = D.rms_norm(x, self.final_norm, cfg.norm_eps)
+        x = fused.rms_norm(x, self.final_norm, cfg.norm_eps, device_index=dv)
         lease, w = self._use(("head", 0))
         logits = dgemm.linear(x, w["head"], device_index=dv)
         if self.keep_logits:
@@ -569,6 +574,9 @@ class TieredLlama:
 
     def close(self) -> None:
         self.kv_lease.release(0 if self.fake else None)
+        for lease in self._pin_leases:
+            lease.release(0 if self.fake else None)
+        self._pin_leases, self._pinned = [], {}
         lib.sync_all()
         for b in [self.embed, self.kv, self.head] + self.layers:
             b.free()

@@ -84,6 +84,7 @@ class _Workspace:
 
 
 _WS = _Workspace()
+_PLANS: dict = {}
 
 
 def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tensor | None = None,
@@ -100,7 +101,10 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     if epi == "resid":
         if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
             raise ValueError("dgemm.linear: resid must match out")
-    ksplit, _ = lib.dgemm_plan(w.n, w.k, TARGET_UNITS)
+    ks = _PLANS.get((w.n, w.k, TARGET_UNITS))
+    if ks is None:
+        ks = _PLANS[(w.n, w.k, TARGET_UNITS)] = lib.dgemm_plan(w.n, w.k, TARGET_UNITS)[0]
+    ksplit = ks
     part = _WS.get(x.device, ksplit * m * w.n * 4)
     stream = int(torch.cuda.current_stream(device_index).cuda_stream) if x.is_cuda else 0
     lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), x.stride(0), m, w.n, w.k,
