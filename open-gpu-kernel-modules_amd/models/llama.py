@@ -152,7 +152,8 @@ class TieredLlama:
         self.packed = packed and weight_format == "bf16"
         self.staged = weight_format == "bf12"
         self.packfmt = "bf11s" if weight_format == "bf11" else weight_format
-        self.stage_bytes = chunks(max(self.layer_bytes, self.head_bytes)) if self.staged else 0
+        self.stage_bytes = (chunks(max(math.prod(sh) * 2 for sh in self.layout.shapes.values()) + (1 << 20))
+                            if self.staged else 0)
         self.arena_bytes = self.budget - self.stage_bytes
         if kv_format == "bf11":
             self.arena_bytes -= chunks(self.kv_layer_bytes)  # the per-layer KV scratch
@@ -188,38 +189,51 @@ class TieredLlama:
             self.kv_resident_bytes = cfg.n_layers * self.kv_slot + _al(self.kv_tail_bytes)
         else:
             self.kv_resident_bytes = _al(self.kv_bytes)
+        # ---- streamed units: each layer's four matrices and the LM head split
+        # into row parts no larger than the largest matrix. Streaming per unit
+        # (not per layer) keeps the HBM reserved for in-flight streaming at a
+        # few units instead of a few whole layers - those bytes hold resident
+        # layers instead, so fewer bytes cross PCIe every step.
+        self.parts = tuple(self.layout.shapes)
+        part_raw = {n: math.prod(sh) * 2 for n, sh in self.layout.shapes.items()}
+        self.head_rows = self._head_split(max(part_raw.values()))
+        first_parts = None
         if self.wpacked:
-            # The packed size of layer 0 sizes the plan (all layers share one distribution).
-            first, info0 = bf12.pack(self._gen_layer(0), fmt=self.packfmt)
-            ratio = info0.nbytes / (self.layer_bytes)
-            self.res_layer_bytes = _al(int(self.layer_bytes * ratio * 1.002) + 4096)
-            self.res_head_bytes = _al(int(self.head_bytes * ratio * 1.002) + 4096)
+            # Layer 0's packed sizes size the plan (all layers share one distribution).
+            first_parts = self._pack_parts(self._gen_layer(0))
+            ratio = sum(inf.nbytes for _, inf in first_parts.values()) / sum(part_raw.values())
+            self.res_part = {n: _al(int(first_parts[n][1].nbytes * 1.002) + 4096) for n in self.parts}
+            self.res_head_part = [_al(int((r1 - r0) * cfg.dim * 2 * ratio * 1.002) + 8192)
+                                  for r0, r1 in self.head_rows]
         else:
-            first = None
-            self.res_layer_bytes, self.res_head_bytes = self.layer_bytes, self.head_bytes
+            self.res_part = {n: _al(b) for n, b in part_raw.items()}
+            self.res_head_part = [_al((r1 - r0) * cfg.dim * 2) for r0, r1 in self.head_rows]
+        self.res_layer_bytes = sum(self.res_part.values())
+        self.res_head_bytes = sum(self.res_head_part)
         # ---- residency plan (in resting bytes: packed or raw)
-        # Streaming slots: the tensor in use + `lookahead` prefetched + one more,
-        # because the host runs ahead of the GPU: when tensor i+lookahead is
-        # prefetched, tensor i-1 may still be read by queued kernels (its chunks
-        # free only when they finish). Without that slot the allocator evicts a
-        # resident layer instead of waiting, and it is re-streamed later.
-        slot = chunks(max(self.res_layer_bytes, self.res_head_bytes))
+        # Streaming slots: the unit in use + `lookahead` prefetched + one
+        # run-ahead slot (the host runs ahead of the GPU: when unit u+lookahead is
+        # prefetched, unit u-1 may still be read by queued kernels).
+        slot = max([chunks(b) for b in self.res_part.values()] + [chunks(b) for b in self.res_head_part])
+        self.slot_bytes = slot
+        layer_cost = sum(chunks(b) for b in self.res_part.values())
+        head_cost = sum(chunks(b) for b in self.res_head_part)
         fixed = chunks(self.kv_resident_bytes + self.norm_bytes)
-        staging = (lookahead + 2) * slot
+        runahead = int(os.environ.get("OGKM_RUNAHEAD", "1"))
+        staging = (lookahead + 1 + runahead) * slot
         if self.arena_bytes - fixed - staging < slot:  # tiny budgets: no room for the run-ahead slot
             staging = (lookahead + 1) * slot
         avail = self.arena_bytes - fixed - staging
         if avail < 0:
             raise ValueError(f"HBM budget {self.budget/2**30:.1f} GiB too small for KV + staging "
-                             f"({(chunks(self.kv_bytes) + staging + self.stage_bytes)/2**30:.1f} GiB)")
-        n_res = max(0, min(cfg.n_layers, avail // chunks(self.res_layer_bytes)
-                           - int(os.environ.get("OGKM_RESIDENT_MARGIN", "0"))))
-        left = avail - n_res * chunks(self.res_layer_bytes)
-        self.head_resident = left >= chunks(self.res_head_bytes)
+                             f"({(fixed + staging + self.stage_bytes)/2**30:.1f} GiB)")
+        n_res = max(0, min(cfg.n_layers, avail // layer_cost - int(os.environ.get("OGKM_RESIDENT_MARGIN", "0"))))
+        left = avail - n_res * layer_cost
+        self.head_resident = left >= head_cost
         # spread resident layers evenly so streaming continues behind them
         self.resident = [((i + 1) * n_res) // cfg.n_layers > (i * n_res) // cfg.n_layers for i in range(cfg.n_layers)]
         self.lookahead = lookahead
-        self.window_bytes = lookahead * chunks(max(self.res_layer_bytes, self.res_head_bytes))
+        self.window_bytes = lookahead * slot
         self.streamed_bytes = (sum(self.res_layer_bytes for r in self.resident if not r)
                                + (0 if self.head_resident else self.res_head_bytes))
         # ---- where streamed tensors rest: host DRAM, or split host DRAM / CXL.mem
@@ -229,16 +243,16 @@ class TieredLlama:
         if tiers not in ("host", "host+cxl"):
             raise ValueError("tiers must be 'host' or 'host+cxl'")
         self.tiers = tiers
-        streamed_keys = [("layer", i) for i in range(cfg.n_layers) if not self.resident[i]]
-        if not self.head_resident:
-            streamed_keys.append(("head", 0))
+        self.order = ([("layer", i, n) for i in range(cfg.n_layers) for n in self.parts]
+                      + [("head", j) for j in range(len(self.head_rows))])
+        streamed_keys = [k for k in self.order if not self._is_resident(k)]
         self.rest_loc = {}
         cxl_loc = rt.Loc.cxl() if tiers == "host+cxl" else None
         for j, key in enumerate(streamed_keys):
             to_cxl = cxl_loc is not None and int((j + 1) * cxl_frac) > int(j * cxl_frac)
             self.rest_loc[key] = cxl_loc if to_cxl else host
-        self.cxl_streamed_bytes = sum(self.res_layer_bytes if k[0] == "layer" else self.res_head_bytes
-                                      for k, l in self.rest_loc.items() if l is cxl_loc and cxl_loc is not None)
+        self.cxl_streamed_bytes = sum(self._unit_bytes(k) for k, l in self.rest_loc.items()
+                                      if l is cxl_loc and cxl_loc is not None)
         # ---- allocate + init
         self.embed = rt.malloc_managed(self.embed_bytes, "embed")
         self.embed.set_preferred_location(host)
@@ -246,33 +260,28 @@ class TieredLlama:
         # KV cache + the RMSNorm weights (tiny) share one resident range
         self.kv = rt.malloc_managed(self.kv_resident_bytes + self.norm_bytes, "kv")
         self.kv.set_preferred_location(gpu)
-        self.layers = []
+        self.ubuf: dict = {}
         for i in range(cfg.n_layers):
             if self.wpacked:
-                stream, info = (first, info0) if i == 0 else bf12.pack(self._gen_layer(i), fmt=self.packfmt)
-                b = rt.malloc_managed(info.nbytes, f"layer{i}", cpu_view=False)
-                self.pinfo[("layer", i)] = info
-                self.pmode[("layer", i)] = dgemm.packed_mode(stream) if not self.staged else dgemm.MODE_RAW
+                packs = first_parts if i == 0 else self._pack_parts(self._gen_layer(i))
             else:
-                stream = self._gen_layer(i)
-                b = rt.malloc_managed(self.layer_bytes, f"layer{i}", packed_bf16=self.packed and not self.resident[i])
-            self._place(b, self.resident[i], gpu, self.rest_loc.get(("layer", i), host))
-            b.write(stream)
-            self.layers.append(b)
-            del stream
-        first = None
-        head = self._gen_head()
-        if self.wpacked:
-            stream, info = bf12.pack(head, fmt=self.packfmt)
-            self.head = rt.malloc_managed(info.nbytes, "lm_head", cpu_view=False)
-            self.pinfo[("head", 0)] = info
-            self.pmode[("head", 0)] = dgemm.packed_mode(stream) if not self.staged else dgemm.MODE_RAW
-        else:
-            stream = head
-            self.head = rt.malloc_managed(self.head_bytes, "lm_head", packed_bf16=self.packed and not self.head_resident)
-        self._place(self.head, self.head_resident, gpu, self.rest_loc.get(("head", 0), host))
-        self.head.write(stream)
-        del head, stream
+                flat = self._gen_layer(i)
+                packs = {n: (flat[self.layout.offsets[n] // 2:self.layout.offsets[n] // 2
+                                  + math.prod(self.layout.shapes[n])].clone(), None) for n in self.parts}
+                del flat
+            for n in self.parts:
+                self._alloc_unit(("layer", i, n), packs[n][0], packs[n][1], gpu, host)
+            del packs
+        first_parts = None
+        head = self._gen_head_rows()
+        for j, (r0, r1) in enumerate(self.head_rows):
+            part = dgemm.frag_permute(head[r0:r1].contiguous())
+            if self.wpacked:
+                st, inf = bf12.pack(part, fmt=self.packfmt)
+                self._alloc_unit(("head", j), st, inf, gpu, host)
+            else:
+                self._alloc_unit(("head", j), part, None, gpu, host)
+        del head
         self.embed.write(self._gen_embed())
         if not self.fake:
             torch.cuda.synchronize(self.dev)
@@ -306,7 +315,6 @@ class TieredLlama:
             self.kv_scratch = torch.empty(2, batch, self.hkv, self.T, hd, dtype=torch.bfloat16, device=self.tdev)
         self.pos = context
         # ---- streaming schedule: use order within a step
-        self.order = [("layer", i) for i in range(cfg.n_layers)] + [("head", 0)]
         self.stream_seq = [k for k in self.order if not self._is_resident(k)]
         self._pf_next = 0           # next index in stream_seq to prefetch (cyclic)
         self._inflight: list = []   # prefetched, not yet consumed
@@ -334,18 +342,62 @@ class TieredLlama:
             "stage_gb": self.stage_bytes / 1e9, "tiers": self.tiers, "kv_format": self.kv_format,
             "kv_resident_gb": self.kv_resident_bytes / 1e9,
             "cxl_streamed_gb_per_step": self.cxl_streamed_bytes / 1e9,
+            "stream_slot_gb": self.slot_bytes / 1e9, "head_parts": len(self.head_rows),
         }
         if self.verbose and self.rank == 0:
             print("[ogkm] plan:", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}, flush=True)
         return d
 
     def _is_resident(self, key) -> bool:
-        kind, i = key
-        return self.resident[i] if kind == "layer" else self.head_resident
+        return self.resident[key[1]] if key[0] == "layer" else self.head_resident
 
     def _buf(self, key) -> "rt.ManagedBuffer":
-        kind, i = key
-        return self.layers[i] if kind == "layer" else self.head
+        return self.ubuf[key]
+
+    def _unit_bytes(self, key) -> int:
+        return self.res_part[key[2]] if key[0] == "layer" else self.res_head_part[key[1]]
+
+    def _unit_shape(self, key) -> tuple:
+        if key[0] == "layer":
+            return self.layout.shapes[key[2]]
+        r0, r1 = self.head_rows[key[1]]
+        return (r1 - r0, self.cfg.dim)
+
+    def _head_split(self, max_part_bytes: int) -> list:
+        """Row ranges (multiples of 16) splitting the LM head into parts of at
+        most ~max_part_bytes of bf16."""
+        rows = self.vocab_local
+        row_bytes = self.cfg.dim * 2
+        n = max(1, -(-rows * row_bytes // max_part_bytes))
+        per = -(-rows // n)
+        per = -(-per // 16) * 16
+        out, r = [], 0
+        while r < rows:
+            out.append((r, min(rows, r + per)))
+            r += per
+        return out
+
+    def _pack_parts(self, flat: torch.Tensor) -> dict:
+        """Split a layer's flat fragment-ordered weights into its matrices and
+        pack each one (its own BF11/BF12 stream)."""
+        out = {}
+        for n in self.parts:
+            off = self.layout.offsets[n] // 2
+            out[n] = bf12.pack(flat[off:off + math.prod(self.layout.shapes[n])], fmt=self.packfmt)
+        return out
+
+    def _alloc_unit(self, key, data: torch.Tensor, info, gpu, host) -> None:
+        name = "-".join(str(x) for x in key)
+        resident = self._is_resident(key)
+        if info is not None:
+            b = rt.malloc_managed(info.nbytes, name, cpu_view=False)
+            self.pinfo[key] = info
+            self.pmode[key] = dgemm.packed_mode(data) if not self.staged else dgemm.MODE_RAW
+        else:
+            b = rt.malloc_managed(data.numel() * 2, name, packed_bf16=self.packed and not resident)
+        self._place(b, resident, gpu, self.rest_loc.get(key, host))
+        b.write(data)
+        self.ubuf[key] = b
 
     @staticmethod
     def _place(b, resident: bool, gpu, host) -> None:
@@ -439,32 +491,29 @@ class TieredLlama:
         return torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=self.tdev).normal_(
             0, 1.0, generator=self._head_gen())
 
-    def _gen_head(self) -> torch.Tensor:
+    def _gen_head_rows(self) -> torch.Tensor:
+        """This rank's LM-head rows [vocab_local, dim] (row-major, not permuted)."""
         cfg = self.cfg
         g = self._head_gen()
         torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=self.tdev).normal_(0, 1.0, generator=g)  # embed draw
         head = torch.empty(cfg.vocab, cfg.dim, dtype=torch.bfloat16, device=self.tdev).normal_(0, self._std, generator=g)
-        return dgemm.frag_permute(tpmod.shard_rows(head, self.rank, self.world).contiguous())
+        return tpmod.shard_rows(head, self.rank, self.world).contiguous()
 
     def host_weights(self, key) -> torch.Tensor:
-        """The bf16 bytes of a layer / head as stored (unpacked on the host, still
-        in fragment order) - for reference numerics."""
+        """The bf16 values of one unit as stored (unpacked on the host, still in
+        fragment order) - for reference numerics."""
         raw = self._buf(key).read()
         if self.wpacked:
-            return bf12.unpack_host(raw, self.pinfo[key]).view(torch.uint8)
-        return raw
+            return bf12.unpack_host(raw, self.pinfo[key])
+        return raw.view(torch.bfloat16)
 
-    def host_matrix(self, key, name: str = "head") -> torch.Tensor:
-        """One weight matrix as a plain [N, K] bf16 CPU tensor (reference numerics)."""
-        raw = self.host_weights(key)
-        if key[0] == "head":
-            n, k = self.vocab_local, self.cfg.dim
-            off = 0
-        else:
-            n, k = self.layout.shapes[name]
-            off = self.layout.offsets[name]
-        flat = raw[off:off + n * k * 2].view(torch.bfloat16)
-        return dgemm.frag_unpermute(flat, n, k)
+    def host_matrix(self, key) -> torch.Tensor:
+        """One weight matrix as a plain [N, K] bf16 CPU tensor (reference numerics):
+        key ("layer", i, name), ("head", j) or ("head",) for the whole LM head."""
+        if key == ("head",):
+            return torch.cat([self.host_matrix(("head", j)) for j in range(len(self.head_rows))])
+        n, k = self._unit_shape(key)
+        return dgemm.frag_unpermute(self.host_weights(key)[:n * k], n, k)
 
     # ------------------------------------------------------------------ streaming
     def _prefetch_ahead(self) -> None:
@@ -484,11 +533,11 @@ class TieredLlama:
             self._pf_next = (self._pf_next + 1) % n
 
     def _use(self, key):
-        """Fault the tensor in (lease) and return (lease or None, weight refs by
-        name). bf11: the GEMMs read the packed stream in place (the lease is held
-        until they are enqueued). bf12: the stream is unpacked into the staging
-        buffer on the compute stream and the lease is released right away (the
-        ring reuses the chunks only after the unpack has read them)."""
+        """Fault one unit in (lease) and return (lease or None, its WeightRef).
+        bf11: the GEMM reads the packed stream in place (the lease is held until
+        it is enqueued). bf12: the stream is unpacked into the staging buffer on
+        the compute stream and the lease is released right away (the ring reuses
+        the chunks only after the unpack has read them)."""
         pin = self._pinned.get(key)
         if pin is not None:  # resident tensor: long-lived lease taken at init, refs cached
             return None, pin
@@ -506,9 +555,9 @@ class TieredLlama:
         if self.staged:
             bf12.unpack_into(self.stage, lease.dptr, self.pinfo[key], self.dev, 0 if self.fake else None)
             lease.release(0 if self.fake else None)
-            return None, self._refs(key, self.stage.data_ptr(), dgemm.MODE_RAW)
+            return None, self._ref(key, self.stage.data_ptr(), dgemm.MODE_RAW)
         mode = self.pmode.get(key, dgemm.MODE_RAW)
-        refs = self._refs(key, lease.dptr, mode)
+        refs = self._ref(key, lease.dptr, mode)
         if self._is_resident(key) and not self.staged:
             # Planned-resident tensors keep their lease (and so their HBM chunks)
             # for the model's lifetime: later uses cost no runtime call.
@@ -517,12 +566,14 @@ class TieredLlama:
             return None, refs
         return lease, refs
 
-    def _refs(self, key, ptr: int, mode: int) -> dict:
+    def _ref(self, key, ptr: int, mode: int) -> "dgemm.WeightRef":
         shift = (self.pinfo[key].chunk_values.bit_length() - 1) if key in self.pinfo else 20
-        if key[0] == "head":
-            return {"head": dgemm.WeightRef(ptr, 0, self.vocab_local, self.cfg.dim, mode, shift)}
-        return {name: dgemm.WeightRef(ptr, self.layout.offsets[name] // 2, n, k, mode, shift)
-                for name, (n, k) in self.layout.shapes.items()}
+        n, k = self._unit_shape(key)
+        return dgemm.WeightRef(ptr, 0, n, k, mode, shift)
+
+    def _done(self, lease) -> None:
+        if lease is not None:
+            lease.release(0 if self.fake else None)
 
     # ------------------------------------------------------------------ decode
     @torch.no_grad()
@@ -538,26 +589,32 @@ class TieredLlama:
             x = x.to(self.tdev)
         dv = self.dev
         for i in range(cfg.n_layers):
-            lease, w = self._use(("layer", i))
             h = fused.rms_norm(x, self.norm_w[2 * i], cfg.norm_eps, device_index=dv)
-            qkv = dgemm.linear(h, w["wqkv"], device_index=dv)
+            lease, w = self._use(("layer", i, "wqkv"))
+            qkv = dgemm.linear(h, w, device_index=dv)
+            self._done(lease)
             kvl = self._kv_layer(i, pos)
             q = self._rope_append(i, pos, kvl, qkv)
             a = fused.attention(q, kvl, pos + 1, device_index=dv)
-            x = self._row_parallel(a, w["wo"], x)
+            lease, w = self._use(("layer", i, "wo"))
+            x = self._row_parallel(a, w, x)
+            self._done(lease)
             h = fused.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps, device_index=dv)
-            g = dgemm.linear(h, w["wgu"], "silu_mul", device_index=dv)
-            x = self._row_parallel(g, w["wd"], x)
-            if lease is not None:
-                lease.release(0 if self.fake else None)
+            lease, w = self._use(("layer", i, "wgu"))
+            g = dgemm.linear(h, w, "silu_mul", device_index=dv)
+            self._done(lease)
+            lease, w = self._use(("layer", i, "wd"))
+            x = self._row_parallel(g, w, x)
+            self._done(lease)
         x = fused.rms_norm(x, self.final_norm, cfg.norm_eps, device_index=dv)
-        lease, w = self._use(("head", 0))
-        logits = dgemm.linear(x, w["head"], device_index=dv)
+        logits = torch.empty(B, self.vocab_local, dtype=torch.bfloat16, device=x.device)
+        for j, (r0, r1) in enumerate(self.head_rows):
+            lease, w = self._use(("head", j))
+            dgemm.linear(x, w, out=logits[:, r0:r1], device_index=dv)
+            self._done(lease)
         if self.keep_logits:
             self.last_logits = comm.all_gather_cat(logits.float(), dim=-1)
         nxt = tpmod.vocab_parallel_argmax(logits, self.rank, self.world)
-        if lease is not None:
-            lease.release(0 if self.fake else None)
         self.pos += 1
         return nxt
 
@@ -578,7 +635,7 @@ class TieredLlama:
             lease.release(0 if self.fake else None)
         self._pin_leases, self._pinned = [], {}
         lib.sync_all()
-        for b in [self.embed, self.kv, self.head] + self.layers:
+        for b in [self.embed, self.kv] + list(self.ubuf.values()):
             b.free()
 
 
@@ -593,7 +650,7 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
     cos, sin = model.cos[pos], model.sin[pos]
     norms = model.norm_w.float().cpu().to(dev)
     for i in range(cfg.n_layers):
-        w = {n: model.host_matrix(("layer", i), n).float().to(dev) for n in model.layout.shapes}
+        w = {n: model.host_matrix(("layer", i, n)).float().to(dev) for n in model.parts}
         h = D.rms_norm(x, norms[2 * i], cfg.norm_eps)
         qkv = h @ w["wqkv"].t()
         q = qkv[:, :model.hq * hd].view(B, model.hq, hd)
@@ -610,7 +667,7 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
         h = D.rms_norm(x, norms[2 * i + 1], cfg.norm_eps)
         x = x + D.silu_mul(h @ w["wgu"].t()) @ w["wd"].t()
     x = D.rms_norm(x, norms[2 * cfg.n_layers], cfg.norm_eps)
-    head = model.host_matrix(("head", 0)).float().to(dev)
+    head = model.host_matrix(("head",)).float().to(dev)
     return x @ head.t()
 
 

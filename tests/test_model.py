@@ -157,8 +157,8 @@ def test_three_tier_host_and_cxl_streaming(fake_rt):
         if tiers == "host+cxl":
             assert m.cxl_streamed_bytes > 0
             locs = set()
-            for i, b in enumerate(m.layers):
-                if not m.resident[i]:
+            for key, b in m.ubuf.items():
+                if not m._is_resident(key):
                     info = b.residency(0)
                     locs |= {x["tier"] for x in info["resident_on"]}
             assert {"cxl", "host"} <= locs, locs
