@@ -54,12 +54,13 @@ def parse():
     ap.add_argument("--lookahead", type=int, default=int(os.environ.get("OGKM_LOOKAHEAD", "1")),
                     help="streamed tensors in flight beyond the one in use (each costs a staging slot of HBM)")
     ap.add_argument("--no-aux", action="store_true", help="skip the HBM<->host/CXL bandwidth probe")
-    ap.add_argument("--weights", choices=("bf11", "bf12", "bf16"), default="bf11",
-                    help="bf11/bf12: weights rest losslessly packed (~0.69x / 0.75x) in every tier (HBM included) "
-                         "and are unpacked per layer; bf16: raw weights")
+    ap.add_argument("--weights", choices=("bf11", "bf12", "ans", "bf16"), default="bf11",
+                    help="bf11/ans/bf12: weights rest losslessly packed (~0.70x / ~0.67x / 0.75x) in every tier (HBM "
+                         "included); bf11 is decoded in the GEMM's registers, ans/bf12 unpacked per matrix into a "
+                         "bf16 staging buffer; bf16: raw weights")
     ap.add_argument("--no-packed", action="store_true",
                     help="with --weights bf16: raw host copies instead of BF12 copies decoded in the H2D kernel")
-    ap.add_argument("--kv-format", choices=("bf11", "bf16"), default="bf11",
+    ap.add_argument("--kv-format", choices=("bf11", "ans", "bf16"), default="bf11",
                     help="bf11: the prefilled KV context rests losslessly packed in HBM (unpacked per layer into a "
                          "one-layer scratch), decode tokens raw; bf16: raw KV cache")
     ap.add_argument("--tiers", choices=("host", "host+cxl"), default="host",
@@ -72,8 +73,14 @@ def parse():
     return ap.parse_args()
 
 
-def bandwidth_probe(dev: int, nbytes: int = 1 << 30) -> dict:
-    """HBM<->host and HBM<->CXL GB/s through the runtime (HIP copy kernels on the rings)."""
+PROBE_KEYS = ("host_to_hbm", "hbm_to_host", "cxl_to_hbm", "hbm_to_cxl")
+
+
+def bandwidth_probe(dev: int, barrier, nbytes: int = 1 << 30) -> tuple[dict, dict]:
+    """HBM<->host and HBM<->CXL GB/s through the runtime (HIP copy kernels on the
+    rings). Every rank runs it at once (``barrier`` before each timed direction),
+    so with N GPUs the sum over ranks is the node's aggregate HBM<->host/CXL rate
+    (BASELINE metric: "HBM<->CXL GB/s at 1/2/4/8 GPU"). Returns (rates, info)."""
     import torch
 
     from ogkm import cxl
@@ -82,23 +89,48 @@ def bandwidth_probe(dev: int, nbytes: int = 1 << 30) -> dict:
     out = {}
     g = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
     h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-    for name, ring, dst, src in (("host_to_hbm_gbps", 0, g.data_ptr(), h.data_ptr()),
-                                 ("hbm_to_host_gbps", 1, h.data_ptr(), g.data_ptr())):
+    for name, ring, dst, src in (("host_to_hbm", 0, g.data_ptr(), h.data_ptr()),
+                                 ("hbm_to_host", 1, h.data_ptr(), g.data_ptr())):
         lib.ring_copy(dev, ring, dst, src, nbytes, True)
+        barrier()
         t0 = time.perf_counter()
         for _ in range(3):
             lib.ring_copy(dev, ring, dst, src, nbytes, True)
-        out[name] = round(3 * nbytes / (time.perf_counter() - t0) / 1e9, 2)
+        out[name] = 3 * nbytes / (time.perf_counter() - t0) / 1e9
     del g, h
     info = cxl.get_info()
     node = info["numa_nodes"][0] if info["numa_nodes"] else lib.host_node()
+    meta = {"cxl_numa_node": node, "emulated": bool(info["emulated"] or not info["numa_nodes"])}
     try:
-        r = cxl.measure_bandwidth(dev, nbytes, iters=3, node=node)
-        out["hbm_cxl_gbps"] = {"cxl_to_hbm": round(r["cxl_to_gpu_gbps"], 2), "hbm_to_cxl": round(r["gpu_to_cxl_gbps"], 2),
-                               "cxl_numa_node": node, "emulated": bool(info["emulated"] or not info["numa_nodes"])}
+        r = cxl.measure_bandwidth(dev, nbytes, iters=3, node=node, barrier=barrier)
+        out["cxl_to_hbm"], out["hbm_to_cxl"] = r["cxl_to_gpu_gbps"], r["gpu_to_cxl_gbps"]
     except Exception as e:  # no CXL / registration refused: report, do not fail the bench
-        out["hbm_cxl_gbps"] = {"error": str(e)}
-    return out
+        out["cxl_to_hbm"] = out["hbm_to_cxl"] = 0.0
+        meta["error"] = str(e)
+    return out, meta
+
+
+def probe_all_ranks(dev: int, rank: int) -> dict:
+    """Run the probe on every rank concurrently; rank 0 gets per-GPU and aggregate GB/s."""
+    import torch
+
+    from ogkm.parallel import comm
+
+    rates, meta = bandwidth_probe(dev, comm.barrier)
+    e = comm.env()
+    t = torch.tensor([[rates[k] for k in PROBE_KEYS]], dtype=torch.float64,
+                     device=f"cuda:{dev}" if e.backend == "nccl" else "cpu")
+    allr = comm.all_gather_cat(t, dim=0).cpu()  # [world, 4]
+    return {
+        "host_to_hbm_gbps": round(rates["host_to_hbm"], 2),
+        "hbm_to_host_gbps": round(rates["hbm_to_host"], 2),
+        "hbm_cxl_gbps": {"cxl_to_hbm": round(rates["cxl_to_hbm"], 2), "hbm_to_cxl": round(rates["hbm_to_cxl"], 2),
+                         **meta},
+        # all N GPUs copying at once (each over its own PCIe link to the host / CXL pool)
+        "aggregate_gbps": {"n_gpus": int(allr.shape[0]),
+                           **{k: round(float(allr[:, j].sum()), 2) for j, k in enumerate(PROBE_KEYS)},
+                           "min_per_gpu": {k: round(float(allr[:, j].min()), 2) for j, k in enumerate(PROBE_KEYS)}},
+    }
 
 
 def main() -> None:
@@ -125,8 +157,8 @@ def main() -> None:
     if not lib.cxl_info()["numa_nodes"] and other:
         lib.cxl_rediscover(other[0], "/sys")
     aux = {}
-    if not a.no_aux and e.rank == 0:
-        aux = bandwidth_probe(dev)
+    if not a.no_aux:
+        aux = probe_all_ranks(dev, e.rank)
     comm.barrier()
     t_init = time.perf_counter()
     sim = a.simulate_tp > 1 and world == 1
@@ -206,8 +238,8 @@ def main() -> None:
                 "host_copy_format": (f"{plan['weight_format']}-lossless" if plan["weight_format"] != "bf16"
                                      else "bf12-lossless" if plan["packed_host_copies"] else "bf16"),
                 "hbm_copy_format": ("bf11-lossless (decoded in the GEMM's registers)" if plan["weight_format"] == "bf11"
-                                    else "bf12-lossless (unpacked per layer)" if plan["weight_format"] == "bf12"
-                                    else "bf16"),
+                                    else f"{plan['weight_format']}-lossless (unpacked per matrix)"
+                                    if plan["weight_format"] in ("bf12", "ans") else "bf16"),
                 "resting_bytes_ratio": round(plan["resting_layer_gb"] / plan["layer_gb"], 4),
             },
             "aux": {

@@ -1,0 +1,152 @@
+// ANS1 chunk codec (CPU encoder + reference decoder). Format: codec.hpp.
+//
+// The encoder runs each segment's (step, lane) sequence backwards, pushing
+// renormalisation words; reversing the word list yields exactly the order in
+// which the wave-parallel decoder (csrc/kernels/ans_kernels.hip) consumes them:
+// step by step, lanes in ascending order within a step.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "ogkm/codec.hpp"
+
+namespace ogkm {
+
+namespace {
+
+constexpr uint32_t kM = 1u << kAnsPrecBits;
+
+inline uint32_t seg_value(uint32_t t, uint32_t lane) { return ((t >> 3) * 64u + lane) * 8u + (t & 7u); }
+
+// Exponent histogram -> frequencies summing to 2^12, every present symbol >= 1,
+// at least two symbols (so every frequency fits 12 bits).
+void normalise(const uint32_t* cnt, uint32_t n, uint16_t* freq) {
+  int64_t sum = 0;
+  int present = 0, top = -1;
+  for (int s = 0; s < 256; ++s) {
+    freq[s] = 0;
+    if (!cnt[s]) continue;
+    ++present;
+    uint32_t f = (uint32_t)(((uint64_t)cnt[s] * kM + n / 2) / n);
+    freq[s] = (uint16_t)std::max<uint32_t>(1u, f);
+    sum += freq[s];
+    if (top < 0 || cnt[s] > cnt[top]) top = s;
+  }
+  if (present == 1) {  // a second (unused) symbol keeps the top frequency < 2^12
+    freq[top ^ 1] = 1;
+    sum += 1;
+  }
+  int64_t diff = (int64_t)kM - sum;
+  if (diff >= 0 || freq[top] + diff >= 1) {
+    freq[top] = (uint16_t)(freq[top] + diff);
+    return;
+  }
+  // Too many rare symbols rounded up: take the excess from the largest ones.
+  while (diff < 0) {
+    int best = -1;
+    for (int s = 0; s < 256; ++s)
+      if (freq[s] > 1 && (best < 0 || freq[s] > freq[best])) best = s;
+    --freq[best];
+    ++diff;
+  }
+}
+
+}  // namespace
+
+uint64_t ans_encode(const uint16_t* in, uint32_t n, uint8_t* out, uint64_t cap) {
+  if (!n || n % 512 || n > (1u << 20)) return 0;
+  const uint32_t n_seg = (n + kAnsSegValues - 1) / kAnsSegValues;
+  const uint32_t off_dir = (kAnsHeaderBytes + n + 3u) & ~3u;
+  uint64_t pos = off_dir + 4ull * (n_seg + 1);
+  if (pos > cap) return 0;
+  uint32_t cnt[256] = {0};
+  for (uint32_t i = 0; i < n; ++i) cnt[(in[i] >> 7) & 0xFF]++;
+  AnsHeader h;
+  memset(&h, 0, sizeof h);
+  h.magic = kAnsMagic;
+  h.n_values = n;
+  h.n_seg = n_seg;
+  h.off_dir = off_dir;
+  normalise(cnt, n, h.freq);
+  uint32_t cum[257];
+  cum[0] = 0;
+  for (int s = 0; s < 256; ++s) cum[s + 1] = cum[s] + h.freq[s];
+  uint8_t* sm = out + kAnsHeaderBytes;
+  for (uint32_t i = 0; i < n; ++i) sm[i] = (uint8_t)(((in[i] >> 8) & 0x80u) | (in[i] & 0x7Fu));
+  std::vector<uint32_t> dir(n_seg + 1);
+  std::vector<uint16_t> words;
+  for (uint32_t s = 0; s < n_seg; ++s) {
+    const uint32_t base = s * kAnsSegValues;
+    const uint32_t steps = std::min(kAnsSegValues, n - base) / 64u;
+    uint32_t x[64];
+    for (auto& v : x) v = kAnsLowBound;
+    words.clear();
+    for (uint32_t t = steps; t-- > 0;) {
+      for (uint32_t l = 64; l-- > 0;) {
+        const uint32_t sym = (in[base + seg_value(t, l)] >> 7) & 0xFF;
+        const uint32_t f = h.freq[sym];
+        if (x[l] >= (f << (32 - kAnsPrecBits))) {  // x_max = ((L >> prec) << 16) * f
+          words.push_back((uint16_t)(x[l] & 0xFFFFu));
+          x[l] >>= 16;
+        }
+        x[l] = ((x[l] / f) << kAnsPrecBits) + (x[l] % f) + cum[sym];
+      }
+    }
+    std::reverse(words.begin(), words.end());
+    dir[s] = (uint32_t)pos;
+    const uint64_t bytes = 256 + ((words.size() * 2 + 3) & ~3ull);
+    if (pos + bytes > cap) return 0;
+    memcpy(out + pos, x, 256);
+    if (!words.empty()) memcpy(out + pos + 256, words.data(), words.size() * 2);
+    if (words.size() & 1) memset(out + pos + 256 + words.size() * 2, 0, 2);
+    pos += bytes;
+  }
+  dir[n_seg] = (uint32_t)pos;
+  memcpy(out, &h, sizeof h);
+  memset(out + kAnsHeaderBytes + n, 0, off_dir - kAnsHeaderBytes - n);
+  memcpy(out + off_dir, dir.data(), 4ull * (n_seg + 1));
+  return pos;
+}
+
+bool ans_decode(const uint8_t* in, uint16_t* out, uint32_t n) {
+  AnsHeader h;
+  memcpy(&h, in, sizeof h);
+  if (h.magic != kAnsMagic || h.n_values != n || n % 512) return false;
+  uint32_t cum[257];
+  cum[0] = 0;
+  for (int s = 0; s < 256; ++s) cum[s + 1] = cum[s] + h.freq[s];
+  if (cum[256] != kM) return false;
+  std::vector<uint8_t> slot_sym(kM);
+  for (int s = 0; s < 256; ++s)
+    for (uint32_t k = cum[s]; k < cum[s + 1]; ++k) slot_sym[k] = (uint8_t)s;
+  const uint8_t* sm = in + kAnsHeaderBytes;
+  const uint32_t* dir = reinterpret_cast<const uint32_t*>(in + h.off_dir);
+  for (uint32_t s = 0; s < h.n_seg; ++s) {
+    const uint32_t base = s * kAnsSegValues;
+    const uint32_t steps = std::min(kAnsSegValues, n - base) / 64u;
+    uint32_t x[64];
+    memcpy(x, in + dir[s], 256);
+    const uint16_t* w = reinterpret_cast<const uint16_t*>(in + dir[s] + 256);
+    const uint64_t nw = (dir[s + 1] - dir[s] - 256) / 2;
+    uint64_t wp = 0;
+    for (uint32_t t = 0; t < steps; ++t) {
+      for (uint32_t l = 0; l < 64; ++l) {
+        const uint32_t slot = x[l] & (kM - 1);
+        const uint32_t sym = slot_sym[slot];
+        x[l] = h.freq[sym] * (x[l] >> kAnsPrecBits) + slot - cum[sym];
+        if (x[l] < kAnsLowBound) {
+          if (wp >= nw) return false;
+          x[l] = (x[l] << 16) | w[wp++];
+        }
+        const uint32_t v = base + seg_value(t, l);
+        const uint32_t b = sm[v];
+        out[v] = (uint16_t)(((b & 0x80u) << 8) | (sym << 7) | (b & 0x7Fu));
+      }
+    }
+    for (uint32_t l = 0; l < 64; ++l)
+      if (x[l] != kAnsLowBound) return false;  // every lane must end where the encoder began
+  }
+  return true;
+}
+
+}  // namespace ogkm

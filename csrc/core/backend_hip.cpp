@@ -271,6 +271,14 @@ class HipBackend : public Backend {
     return Status::OK;
   }
 
+  Status unpack_ans_stream(int, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values, uint64_t,
+                           void* s, uint32_t workgroups, uint64_t dst_stride) override {
+    HIPCHK(launch_ans_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s,
+                             dst_stride));
+    launches_++;
+    return Status::OK;
+  }
+
   Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {
     HIPCHK(launch_dgemm(a, mode, (hipStream_t)s));
     launches_++;

@@ -255,7 +255,10 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_
       uint8_t* dst = out + head + c * slot;
       uint64_t e = 0;
       uint32_t kind = 0;
-      if (cnt % 8 == 0 && fmt == PackFormat::BF11_STRICT) {
+      if (fmt == PackFormat::ANS) {
+        e = cnt % 512 == 0 ? ans_encode(in + lo, cnt, dst, (uint64_t)cnt * 2) : 0;
+        kind = e ? 3 : 0;
+      } else if (cnt % 8 == 0 && fmt == PackFormat::BF11_STRICT) {
         e = bf11_encode(in + lo, cnt, dst, (uint64_t)cnt * 2);
         kind = e ? 2 : 0;
       } else if (cnt % 8 == 0 && fmt == PackFormat::BF11) {
@@ -273,7 +276,7 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_
           }
         }
       }
-      if (!e && cnt % 8 == 0 && fmt != PackFormat::BF11_STRICT) {
+      if (!e && cnt % 8 == 0 && fmt != PackFormat::BF11_STRICT && fmt != PackFormat::ANS) {
         e = bf12_encode(in + lo, cnt, dst, (uint64_t)cnt * 2);
         kind = e ? 1 : 0;
       }
@@ -302,7 +305,7 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_
     table[c].offset = off;
     off = (off + bytes[c] + 255) & ~255ull;
   }
-  Bf12StreamHeader h{kBf12StreamMagic, (uint32_t)nch, chunk_values, 0, n, off};
+  Bf12StreamHeader h{kBf12StreamMagic, (uint32_t)nch, chunk_values, (uint32_t)fmt, n, off};
   memset(out, 0, head);
   memcpy(out, &h, sizeof h);
   memcpy(out + sizeof h, table.data(), nch * sizeof(Bf12StreamChunk));
@@ -316,7 +319,9 @@ bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n, uint64_t dst_
   const Bf12StreamChunk* t = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof h);
   for (uint32_t c = 0; c < h.nchunks; ++c) {
     uint16_t* dst = out + (uint64_t)c * (dst_stride ? dst_stride : h.chunk_values);
-    if (t[c].encoded == 2) {
+    if (t[c].encoded == 3) {
+      if (!ans_decode(stream + t[c].offset, dst, t[c].n_values)) return false;
+    } else if (t[c].encoded == 2) {
       if (!bf11_decode(stream + t[c].offset, dst, t[c].n_values)) return false;
     } else if (t[c].encoded == 1) {
       if (!bf12_decode(stream + t[c].offset, dst, t[c].n_values)) return false;

@@ -1,6 +1,7 @@
 // SQ/CQ ring implementation.
 #include "ogkm/ring.hpp"
 
+#include <algorithm>
 #include <thread>
 
 #include "ogkm/config.hpp"
@@ -66,6 +67,25 @@ FenceRef Ring::submit_locked() {
     auto f = std::make_shared<Fence>();
     f->done.store(true);
     return f;
+  }
+  // Hoist the fence waits of every run of copy-like SQEs (COPY / DECODE /
+  // WAIT_FENCE / NOP) to the front of the run, so the run becomes ONE
+  // copy-kernel launch instead of one launch per wait (each launch boundary is
+  // tens of microseconds of idle link). Waiting earlier is conservative: it
+  // can only delay a copy that did not need to wait. No wait can depend on a
+  // copy of this submission (its fence does not exist until the end).
+  auto copy_like = [](SqeOp op) {
+    return op == SqeOp::COPY || op == SqeOp::DECODE_BF12 || op == SqeOp::WAIT_FENCE || op == SqeOp::NOP;
+  };
+  for (auto it = sq_.begin(); it != sq_.end();) {
+    if (!copy_like(it->second.op)) {
+      ++it;
+      continue;
+    }
+    auto end = it;
+    while (end != sq_.end() && copy_like(end->second.op)) ++end;
+    std::stable_partition(it, end, [](const std::pair<uint64_t, Sqe>& e) { return e.second.op == SqeOp::WAIT_FENCE; });
+    it = end;
   }
   Runtime* rt = Runtime::get();
   Status st = err_;
@@ -148,11 +168,12 @@ FenceRef Ring::submit_locked() {
     } else {
       cqe_status = (int32_t)st;
     }
-    last = e.first;
+    last = std::max(last, e.first);
     done.emplace_back(e.first, Cqe{s.user_data, e.first, cqe_status});
   }
   flush();
   sq_.clear();
+  std::sort(done.begin(), done.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
   if (st == Status::OK) st = be_->signal(dev_, sem_, last, stream_);
   if (st != Status::OK) {
     if (err_ == Status::OK) err_ = st;

@@ -100,6 +100,12 @@ class Backend {
   // Chunk c lands at dst + c * dst_stride values (0 = contiguous).
   virtual Status unpack_bf12_stream(int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
                                     uint64_t n_values, void* stream, uint32_t workgroups, uint64_t dst_stride = 0) = 0;
+  // Same for an ANS stream (ANS1 / raw chunks, k_ans_unpack). The default serves
+  // backends whose stream unpack decodes every chunk kind (the fake CPU one).
+  virtual Status unpack_ans_stream(int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
+                                   uint64_t n_values, void* stream, uint32_t workgroups, uint64_t dst_stride = 0) {
+    return unpack_bf12_stream(dev, src, dst, nchunks, chunk_values, n_values, stream, workgroups, dst_stride);
+  }
   // Decode GEMM (ogkm/dgemm.hpp): split-K partials, then the fused epilogue.
   virtual Status dgemm(int dev, const DGemmArgs& a, int mode, void* stream) = 0;
   virtual Status dgemm_reduce(int dev, const DGemmReduceArgs& a, void* stream) = 0;

@@ -113,6 +113,41 @@ bool bf11_decode(const uint8_t* in, uint16_t* out, uint32_t n_values);
 // BF11 block, exceptions included (the decode-GEMM fragment path).
 void bf11_decode_group(const uint8_t* in, uint32_t v, uint16_t* out512);
 
+// ANS1: entropy-coded exponents (interleaved rANS), sign|mantissa bytes raw.
+// BF11's fixed-width codes spend ~3.1 bits on an exponent whose entropy is
+// ~2.55 bits for weight-like (bell-shaped) data; rANS gets within ~0.01 bit of
+// the entropy, so a value costs ~8 + 2.56 bits + segment overhead (~0.1 bit).
+// Exponent-only modelling (like DFloat11-style codecs): no assumption about the
+// mantissa. A chunk (<= 1 Mi values, a multiple of 512) holds:
+//   [0, 1024)              AnsHeader (u16 freq[256] at byte 512: the chunk's
+//                          exponent histogram normalised to 2^12)
+//   [1024, 1024 + n)       sign|mantissa plane
+//   off_dir (4-aligned)    u32 seg_off[n_seg + 1] (offsets from the chunk start)
+//   segment s (4-aligned)  u32 state[64] + u16 words[] (renormalisation stream)
+// A segment is 32 Ki values decoded by ONE wave: at step t lane l decodes
+// value ((t / 8) * 64 + l) * 8 + t % 8 of the segment (so each lane assembles
+// one 16-B fragment every 8 steps). rANS: 32-bit state in [2^16, 2^32), 12-bit
+// precision, 16-bit renormalisation; the words of a segment are consumed in
+// (step, lane) order - a wave finds each lane's word with a ballot prefix.
+constexpr uint32_t kAnsMagic = 0x31534E41;  // "ANS1"
+constexpr uint32_t kAnsHeaderBytes = 1024;
+constexpr uint32_t kAnsSegValues = 32768;
+constexpr uint32_t kAnsPrecBits = 12;
+constexpr uint32_t kAnsLowBound = 1u << 16;
+struct AnsHeader {
+  uint32_t magic;
+  uint32_t n_values;
+  uint32_t n_seg;
+  uint32_t off_dir;
+  uint32_t reserved[124];
+  uint16_t freq[256];
+};
+static_assert(sizeof(AnsHeader) == kAnsHeaderBytes, "ANS header is 1 KB");
+// Encode n_values bf16 (a multiple of 512, <= 1 Mi) as an ANS1 chunk; 0 when
+// it does not fit `cap` (the caller stores the chunk raw).
+uint64_t ans_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);
+bool ans_decode(const uint8_t* in, uint16_t* out, uint32_t n_values);
+
 // Encode n_values bf16 (n_values even) into `out` (capacity `cap` bytes).
 // Returns the encoded size, or 0 when the block does not compress into `cap`.
 uint64_t bf12_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);
@@ -143,8 +178,9 @@ struct Bf12StreamChunk {
   uint32_t encoded;  // 0 = raw bf16, 1 = BF12 block, 2 = BF11 block
 };
 // BF11_STRICT: BF11 or raw only (streams read by the decode GEMM, which decodes
-// those two chunk kinds in registers).
-enum class PackFormat : uint32_t { BF12 = 1, BF11 = 2, BF11_STRICT = 3 };
+// those two chunk kinds in registers). ANS: ANS1 or raw chunks (encoded = 3),
+// unpacked by k_ans_unpack.
+enum class PackFormat : uint32_t { BF12 = 1, BF11 = 2, BF11_STRICT = 3, ANS = 4 };
 static_assert(sizeof(Bf12StreamHeader) == 32 && sizeof(Bf12StreamChunk) == 16, "stream layout");
 inline uint64_t bf12_stream_head_bytes(uint64_t nchunks) { return (32 + 16 * nchunks + 255) & ~255ull; }
 inline uint64_t bf12_pack_bound(uint64_t n_values, uint32_t chunk_values) {

@@ -56,6 +56,10 @@ hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgr
 // launch, one work item per 32768-value tile of every chunk.
 hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
                               uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0);
+// Unpack an ANS stream (ANS1 or raw chunks, codec.hpp) in device memory into
+// bf16 (csrc/kernels/ans_kernels.hip): one wave per 32 Ki-value rANS segment.
+hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
+                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0);
 
 // Decode GEMM (csrc/kernels/decode_gemm.hip); argument structs in ogkm/dgemm.hpp.
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);

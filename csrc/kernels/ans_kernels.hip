@@ -1,0 +1,167 @@
+// k_ans_unpack: HBM -> HBM unpack of an ANS stream (codec.hpp "ANS1" chunks,
+// interleaved rANS over the exponents, raw sign|mantissa plane) into bf16.
+//
+// Work item = 4 consecutive 32 Ki-value segments of one chunk, one per wave of
+// a 256-thread workgroup. The workgroup first expands the chunk's 256-entry
+// frequency table into a 4096-slot decode table in LDS (16 KB: slot ->
+// exponent | freq << 8 | (slot - cum) << 20; one wave-scan for the cumulative
+// counts, 16 slots per thread). Then every lane runs its own rANS state:
+//   slot lookup (LDS) -> state update -> renormalise if below 2^16.
+// Renormalisation words of a segment are consumed in (step, lane) order: a
+// ballot gives each needing lane its rank, and the word is fetched from a
+// 3-register window of the segment's word stream (192 words in use + 128
+// prefetched) with ds_bpermute - no LDS staging of the stream, so the table is
+// the only LDS a workgroup holds and many workgroups share a CU to hide the
+// serial per-lane dependency. Every 8 steps a lane owns 8 consecutive values
+// and writes one coalesced 16-B store (1 KB per wave).
+#include <hip/hip_runtime.h>
+
+#include "ogkm/codec.hpp"
+#include "ogkm/kernels.hpp"
+
+namespace ogkm {
+
+namespace {
+
+typedef unsigned int au32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int au32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kAnsThreads = 256;
+constexpr uint32_t kAnsSegsPerItem = kAnsThreads / 64;
+constexpr uint32_t kAnsSlots = 1u << kAnsPrecBits;
+
+__device__ __forceinline__ uint32_t ans_mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t ans_bperm(uint32_t lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lane << 2), (int)v);
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(kAnsThreads)
+    k_ans_unpack(const uint8_t* __restrict__ stream, uint16_t* __restrict__ out, uint64_t dst_stride,
+                 uint32_t items_per_chunk, uint64_t total_items) {
+  __shared__ uint32_t tab[kAnsSlots];
+  __shared__ uint32_t cum[257];
+  __shared__ uint32_t wsum[kAnsSegsPerItem];
+  const Bf12StreamChunk* table = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof(Bf12StreamHeader));
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
+    const uint64_t c = item / items_per_chunk;
+    const uint32_t sub = (uint32_t)(item - c * items_per_chunk);
+    const Bf12StreamChunk ch = table[c];  // uniform: scalar loads
+    const uint8_t* blk = stream + ch.offset;
+    uint16_t* dst = out + c * dst_stride;
+    const uint32_t v_lo = sub * kAnsSegsPerItem * kAnsSegValues;
+    if (v_lo >= ch.n_values) continue;  // uniform across the workgroup
+    if (ch.encoded != 3) {              // raw chunk: plain copy of this item's range
+      const uint32_t v_hi = ch.n_values - v_lo < kAnsSegsPerItem * kAnsSegValues
+                                ? ch.n_values : v_lo + kAnsSegsPerItem * kAnsSegValues;
+      const uint16_t* src = reinterpret_cast<const uint16_t*>(blk);
+      const uint32_t g_lo = v_lo / 8, g_hi = v_hi / 8;
+      for (uint32_t g = g_lo + threadIdx.x; g < g_hi; g += kAnsThreads)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const au32x4*>(src) + g),
+                                    reinterpret_cast<au32x4*>(dst) + g);
+      for (uint32_t k = g_hi * 8 + threadIdx.x; k < v_hi; k += kAnsThreads) dst[k] = src[k];
+      continue;
+    }
+    const AnsHeader* h = reinterpret_cast<const AnsHeader*>(blk);
+    __syncthreads();  // the previous item's table readers are done
+    // cumulative frequencies: thread t owns symbol t (blockDim == 256 symbols)
+    uint32_t s = h->freq[threadIdx.x];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(s, d, 64);
+      if (lane >= (uint32_t)d) s += y;
+    }
+    if (lane == 63u) wsum[wave] = s;
+    __syncthreads();
+    uint32_t add = 0;
+    for (uint32_t w = 0; w < wave; ++w) add += wsum[w];
+    cum[threadIdx.x + 1] = s + add;
+    if (threadIdx.x == 0) cum[0] = 0;
+    __syncthreads();
+    {  // decode table: thread t fills slots [16 t, 16 t + 16)
+      const uint32_t k0 = threadIdx.x * (kAnsSlots / kAnsThreads);
+      uint32_t lo = 0, hi = 256;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cum[mid] <= k0) lo = mid; else hi = mid;
+      }
+      uint32_t sym = lo;
+      for (uint32_t k = k0; k < k0 + kAnsSlots / kAnsThreads; ++k) {
+        while (cum[sym + 1] <= k) ++sym;
+        tab[k] = sym | ((cum[sym + 1] - cum[sym]) << 8) | ((k - cum[sym]) << 20);
+      }
+    }
+    __syncthreads();
+    const uint32_t seg = sub * kAnsSegsPerItem + wave;
+    if (seg >= h->n_seg) continue;  // wave-uniform (the next barrier is at the next item's start)
+    const uint32_t* dir = reinterpret_cast<const uint32_t*>(blk + h->off_dir);
+    const uint32_t off = dir[seg], end = dir[seg + 1];
+    const uint32_t npairs = (end - off - 256u) / 4u;  // word pairs (the encoder pads to an even count)
+    uint32_t x = reinterpret_cast<const uint32_t*>(blk + off)[lane];
+    const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(blk + off + 256u);
+    // word window: W0 = words [wb, wb + 128), W1 = the next 128, W2 = prefetch
+    uint32_t W0 = lane < npairs ? wsrc[lane] : 0u;
+    uint32_t W1 = 64u + lane < npairs ? wsrc[64u + lane] : 0u;
+    uint32_t W2 = 128u + lane < npairs ? wsrc[128u + lane] : 0u;
+    uint32_t wb = 0, wp = 0;
+    const uint32_t base = seg * kAnsSegValues;
+    const uint32_t nv = ch.n_values - base < kAnsSegValues ? ch.n_values - base : kAnsSegValues;
+    const uint32_t groups = nv / 512u;
+    const uint8_t* smp = blk + kAnsHeaderBytes;
+    au32x2 smn = __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + base + lane * 8u));
+    for (uint32_t g = 0; g < groups; ++g) {
+      const uint32_t v0 = base + (g * 64u + lane) * 8u;
+      const au32x2 sm = smn;
+      if (g + 1 < groups) smn = __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + v0 + 512u));
+      au32x4 o = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t t = tab[x & (kAnsSlots - 1u)];
+        x = ((t >> 8) & 0xFFFu) * (x >> kAnsPrecBits) + (t >> 20);
+        const bool need = x < kAnsLowBound;
+        const uint64_t m = __ballot(need);
+        if (m) {  // wave-uniform
+          const uint32_t rel = wp - wb + ans_mbcnt(m);  // < 192
+          const uint32_t a = ans_bperm((rel >> 1) & 63u, W0), b = ans_bperm((rel >> 1) & 63u, W1);
+          const uint32_t pr = rel < 128u ? a : b;
+          const uint32_t word = (rel & 1u) ? (pr >> 16) : (pr & 0xFFFFu);
+          if (need) x = (x << 16) | word;
+          wp += (uint32_t)__builtin_popcountll(m);
+          if (wp - wb >= 128u) {
+            W0 = W1;
+            W1 = W2;
+            wb += 128u;
+            const uint32_t q = (wb + 256u) / 2u + lane;
+            W2 = q < npairs ? wsrc[q] : 0u;
+          }
+        }
+        const uint32_t byte = (sm[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        const uint32_t val = ((byte & 0x80u) << 8) | ((t & 0xFFu) << 7) | (byte & 0x7Fu);
+        o[j >> 1] |= val << (16 * (j & 1));
+      }
+      __builtin_nontemporal_store(o, reinterpret_cast<au32x4*>(dst + v0));
+    }
+  }
+}
+
+hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
+                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride) {
+  if (nchunks == 0) return hipSuccess;
+  if (chunk_values < 8192 || (chunk_values & (chunk_values - 1)) || chunk_values > (1u << 20))
+    return hipErrorInvalidValue;
+  const uint32_t segs = (chunk_values + kAnsSegValues - 1) / kAnsSegValues;
+  const uint32_t per_chunk = (segs + kAnsSegsPerItem - 1) / kAnsSegsPerItem;
+  const uint64_t total = (uint64_t)nchunks * per_chunk;
+  const uint64_t grid = workgroups && workgroups < total ? workgroups : total;
+  hipLaunchKernelGGL(k_ans_unpack, dim3((uint32_t)grid), dim3(kAnsThreads), 0, s, (const uint8_t*)stream,
+                     (uint16_t*)dst, dst_stride ? dst_stride : (uint64_t)chunk_values, per_chunk, total);
+  return hipGetLastError();
+}
+
+}  // namespace ogkm

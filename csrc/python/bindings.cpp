@@ -607,6 +607,14 @@ PYBIND11_MODULE(_ogkm, m) {
           "bf12_unpack");
   }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("nchunks"), py::arg("chunk_values"),
      py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0, py::arg("dst_stride") = 0);
+  // Same for ANS streams (k_ans_unpack).
+  m.def("ans_unpack", [](int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
+                         uint64_t n_values, uint64_t stream, uint32_t workgroups, uint64_t dst_stride) {
+    check(rt()->be()->unpack_ans_stream(dev, src, dst, nchunks, chunk_values, n_values, (void*)stream, workgroups,
+                                        dst_stride),
+          "ans_unpack");
+  }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("nchunks"), py::arg("chunk_values"),
+     py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0, py::arg("dst_stride") = 0);
   // Decode GEMM + fused epilogue in one call: out = epi(X . W^T) (ops/dgemm.py).
   m.def("dgemm_plan", [](uint32_t N, uint32_t K, uint32_t target_units) {
     uint32_t ks, kl;

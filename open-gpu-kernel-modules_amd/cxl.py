@@ -112,9 +112,12 @@ def p2p_caps(device: int = 0) -> dict:
     }
 
 
-def measure_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 5, node: Optional[int] = None) -> dict:
+def measure_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 5, node: Optional[int] = None,
+                      barrier=None) -> dict:
     """HBM<->CXL GB/s through the CXL ring (HIP copy kernels). Records the measured
-    per-link bandwidth in the runtime's CXL info (replacing the fork's constant)."""
+    per-link bandwidth in the runtime's CXL info (replacing the fork's constant).
+    ``barrier``: called before each timed direction, so that N processes (one per
+    GPU) measure concurrently and the sum of their rates is the node aggregate."""
     import torch
 
     buf = CxlBuffer.allocate(nbytes, node=node if node is not None else (get_info()["numa_nodes"] or [None])[0])
@@ -123,6 +126,8 @@ def measure_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 5, no
     res = {}
     for name, d in (("cxl_to_gpu", DIR_CXL_TO_GPU), ("gpu_to_cxl", DIR_GPU_TO_CXL)):
         wait(buf.dma(dst.data_ptr(), device, 0, nbytes, d))
+        if barrier is not None:
+            barrier()
         t0 = time.perf_counter()
         tid = 0
         for _ in range(iters):

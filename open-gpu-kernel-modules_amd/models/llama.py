@@ -82,23 +82,57 @@ class LayerLayout:
     """Byte offsets of one TP shard's GEMM weights inside a layer buffer (bf16,
     4 KB aligned). Every matrix is stored in the decode GEMM's fragment order
     (ops/dgemm.py: 16x32 MFMA A-tiles), so the kernel streams it - raw or
-    BF11-packed - with one coalesced 1 KB wave access per tile. The RMSNorm
-    weights live in a separate small resident buffer (TieredLlama.norms)."""
+    packed - with one coalesced 1 KB wave access per tile. The RMSNorm weights
+    live in a separate small resident buffer (TieredLlama.norms).
+
+    The FFN matrices are cut into row parts no larger than the attention
+    matrices (``unit_bytes``): gate/up part p = [gate rows r0:r1; up rows r0:r1]
+    (its SiLU-mul epilogue yields FFN columns r0:r1), down part q = output rows
+    n0:n1. Every part is its own streamed unit, so the HBM held by in-flight
+    streaming slots (and the bf16 staging buffer of staged formats) is sized by
+    the largest part, not by the ~1 GB gate/up matrix."""
 
     shapes: dict = field(default_factory=dict)
     offsets: dict = field(default_factory=dict)
+    roles: dict = field(default_factory=dict)   # "wqkv" | "wo" | "wgu" | "wd" -> its part names
+    rows: dict = field(default_factory=dict)    # part name -> (r0, r1) of its role's output rows
     nbytes: int = 0
 
     @staticmethod
-    def build(cfg: LlamaConfig, world: int) -> "LayerLayout":
+    def _nparts(rows: int, total_bytes: int, target: int) -> int:
+        tiles = rows // 16
+        for p in range(1, tiles + 1):
+            if tiles % p == 0 and total_bytes // p <= target:
+                return p
+        return tiles
+
+    @staticmethod
+    def build(cfg: LlamaConfig, world: int, unit_bytes: Optional[int] = None) -> "LayerLayout":
         hd = cfg.head_dim
         hq, hkv, f = cfg.n_heads // world, cfg.n_kv_heads // world, cfg.ffn_dim // world
         L = LayerLayout()
-        for name, shape in (("wqkv", ((hq + 2 * hkv) * hd, cfg.dim)), ("wo", (cfg.dim, hq * hd)),
-                            ("wgu", (2 * f, cfg.dim)), ("wd", (cfg.dim, f))):
+
+        def add(role, name, shape, r0, r1):
             L.shapes[name] = shape
             L.offsets[name] = L.nbytes
+            L.rows[name] = (r0, r1)
+            L.roles.setdefault(role, []).append(name)
             L.nbytes += _al(math.prod(shape) * 2)
+
+        nqkv = (hq + 2 * hkv) * hd
+        add("wqkv", "wqkv", (nqkv, cfg.dim), 0, nqkv)
+        add("wo", "wo", (cfg.dim, hq * hd), 0, cfg.dim)
+        if unit_bytes is None:
+            env = os.environ.get("OGKM_UNIT_MB")
+            unit_bytes = int(float(env) * 2**20) if env else max(nqkv * cfg.dim, cfg.dim * hq * hd) * 2
+        p = LayerLayout._nparts(f, 2 * f * cfg.dim * 2, unit_bytes)
+        per = f // p
+        for j in range(p):
+            add("wgu", f"wgu.{j}", (2 * per, cfg.dim), j * per, (j + 1) * per)
+        q = LayerLayout._nparts(cfg.dim, cfg.dim * f * 2, unit_bytes)
+        per = cfg.dim // q
+        for j in range(q):
+            add("wd", f"wd.{j}", (per, f), j * per, (j + 1) * per)
         return L
 
 
@@ -120,6 +154,7 @@ class TieredLlama:
         self.layout = LayerLayout.build(cfg, tp_world)
         hd = cfg.head_dim
         self.hq, self.hkv = cfg.n_heads // tp_world, cfg.n_kv_heads // tp_world
+        self.f_local = cfg.ffn_dim // tp_world
         self.vocab_local = cfg.vocab // tp_world
         # ---- footprint and budget
         self.layer_bytes = self.layout.nbytes
@@ -145,17 +180,17 @@ class TieredLlama:
         # right before its layer runs (carved out of the same HBM budget).
         # "bf16": raw weights; with ``packed`` the runtime keeps streamed host
         # copies BF12 and decodes them inside the H2D copy kernel.
-        if weight_format not in ("bf11", "bf12", "bf16"):
-            raise ValueError("weight_format must be 'bf11', 'bf12' or 'bf16'")
+        if weight_format not in ("bf11", "bf12", "ans", "bf16"):
+            raise ValueError("weight_format must be 'bf11', 'bf12', 'ans' or 'bf16'")
         self.wfmt = weight_format
-        self.wpacked = weight_format in ("bf11", "bf12")   # weights rest packed in every tier
+        self.wpacked = weight_format in ("bf11", "bf12", "ans")   # weights rest packed in every tier
         self.packed = packed and weight_format == "bf16"
-        self.staged = weight_format == "bf12"
+        self.staged = weight_format in ("bf12", "ans")
         self.packfmt = "bf11s" if weight_format == "bf11" else weight_format
         self.stage_bytes = (chunks(max(math.prod(sh) * 2 for sh in self.layout.shapes.values()) + (1 << 20))
                             if self.staged else 0)
         self.arena_bytes = self.budget - self.stage_bytes
-        if kv_format == "bf11":
+        if kv_format != "bf16":
             self.arena_bytes -= chunks(self.kv_layer_bytes)  # the per-layer KV scratch
         lib.init_device(device, self.arena_bytes)
         self.pinfo: dict = {}
@@ -169,19 +204,19 @@ class TieredLlama:
         # head) row block of ctx x hd values), decode tokens in a raw tail; per
         # layer the prefix is unpacked (k_bf12_unpack, strided into row blocks of
         # T x hd) into one [2, B, hkv, T, hd] scratch that attention reads.
-        if kv_format not in ("bf16", "bf11"):
-            raise ValueError("kv_format must be 'bf16' or 'bf11'")
+        if kv_format not in ("bf16", "bf11", "ans"):
+            raise ValueError("kv_format must be 'bf16', 'bf11' or 'ans'")
         cv = context * hd
-        if kv_format == "bf11" and (cv & (cv - 1) or cv < 8192 or cv > (1 << 20)):
-            raise ValueError("kv_format='bf11' needs context * head_dim to be a power of two in [8 Ki, 1 Mi]")
+        if kv_format != "bf16" and (cv & (cv - 1) or cv < 8192 or cv > (1 << 20)):
+            raise ValueError("packed kv_format needs context * head_dim to be a power of two in [8 Ki, 1 Mi]")
         self.kv_format = kv_format
         self.tail = self.T - context
         self.kv_tail_bytes = cfg.n_layers * 2 * batch * self.hkv * self.tail * hd * 2
-        self.kv_scratch_bytes = self.kv_layer_bytes if kv_format == "bf11" else 0
+        self.kv_scratch_bytes = self.kv_layer_bytes if kv_format != "bf16" else 0
         self.kv_streams, self.kv_infos, self.kv_slot = [], [], 0
-        if kv_format == "bf11":
+        if kv_format != "bf16":
             for i, full in enumerate(self._gen_prefill()):
-                st, inf = bf12.pack(full, chunk_values=cv, fmt="bf11")
+                st, inf = bf12.pack(full, chunk_values=cv, fmt=kv_format)
                 self.kv_streams.append(st)
                 self.kv_infos.append(inf)
                 del full
@@ -216,9 +251,15 @@ class TieredLlama:
         # prefetched, unit u-1 may still be read by queued kernels).
         slot = max([chunks(b) for b in self.res_part.values()] + [chunks(b) for b in self.res_head_part])
         self.slot_bytes = slot
+        # The prefetch window must cover the longest resident stretch (~2 layers
+        # of compute) or the link idles behind it: at least OGKM_WINDOW_MB in flight.
+        # (Capped at a quarter of the arena left after the KV cache: small models.)
         layer_cost = sum(chunks(b) for b in self.res_part.values())
         head_cost = sum(chunks(b) for b in self.res_head_part)
         fixed = chunks(self.kv_resident_bytes + self.norm_bytes)
+        window_min = int(float(os.environ.get("OGKM_WINDOW_MB", "384")) * 2**20)
+        lookahead_arg = lookahead
+        lookahead = max(lookahead, min(-(-window_min // slot), max(0, self.arena_bytes - fixed) // (4 * slot)))
         runahead = int(os.environ.get("OGKM_RUNAHEAD", "1"))
         staging = (lookahead + 1 + runahead) * slot
         if self.arena_bytes - fixed - staging < slot:  # tiny budgets: no room for the run-ahead slot
@@ -232,10 +273,11 @@ class TieredLlama:
         self.head_resident = left >= head_cost
         # spread resident layers evenly so streaming continues behind them
         self.resident = [((i + 1) * n_res) // cfg.n_layers > (i * n_res) // cfg.n_layers for i in range(cfg.n_layers)]
-        self.lookahead = lookahead
-        self.window_bytes = lookahead * slot
         self.streamed_bytes = (sum(self.res_layer_bytes for r in self.resident if not r)
                                + (0 if self.head_resident else self.res_head_bytes))
+        # a window that wraps around a small streamed set would evict units before their use
+        self.lookahead = min(lookahead, max(lookahead_arg, self.streamed_bytes // (8 * slot)))
+        self.window_bytes = self.lookahead * slot
         # ---- where streamed tensors rest: host DRAM, or split host DRAM / CXL.mem
         # (three-tier: HBM + host + CXL). Streamed tensors are interleaved over
         # the two so every step reads both pools (capacity tiering; both cross
@@ -430,10 +472,16 @@ class TieredLlama:
         del wo
         wg = torch.empty(cfg.ffn_dim, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
         wu = torch.empty(cfg.ffn_dim, cfg.dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-        put("wgu", tpmod.shard_gate_up(wg, wu, self.rank, self.world))
+        wg, wu = tpmod.shard_rows(wg, self.rank, self.world), tpmod.shard_rows(wu, self.rank, self.world)
+        for name in L.roles["wgu"]:
+            r0, r1 = L.rows[name]
+            put(name, torch.cat([wg[r0:r1], wu[r0:r1]], 0))
         del wg, wu
         wd = torch.empty(cfg.dim, cfg.ffn_dim, dtype=torch.bfloat16, device=dev).normal_(0, std, generator=g)
-        put("wd", tpmod.shard_cols(wd, self.rank, self.world))
+        wd = tpmod.shard_cols(wd, self.rank, self.world)
+        for name in L.roles["wd"]:
+            r0, r1 = L.rows[name]
+            put(name, wd[r0:r1])
         del wd
         return flat
 
@@ -466,7 +514,7 @@ class TieredLlama:
     def _rope_append(self, i: int, pos: int, kv_layer: torch.Tensor, qkv: torch.Tensor) -> torch.Tensor:
         """RoPE on q/k + append k/v at pos (into the cache / scratch and the
         packed cache's raw tail) in one fused kernel; returns rotated q."""
-        tail = self.kv_tail_t[i] if self.kv_format == "bf11" else None
+        tail = self.kv_tail_t[i] if self.kv_format != "bf16" else None
         return fused.rope_kv(qkv, self.cos[pos], self.sin[pos], kv_layer, pos, self.hq, self.hkv, tail=tail,
                              tail_pos=pos - self.ctx, device_index=self.dev)
 
@@ -512,6 +560,11 @@ class TieredLlama:
         key ("layer", i, name), ("head", j) or ("head",) for the whole LM head."""
         if key == ("head",):
             return torch.cat([self.host_matrix(("head", j)) for j in range(len(self.head_rows))])
+        if key[0] == "layer" and key[2] not in self.layout.shapes:  # a whole role: reassemble its parts
+            mats = [self.host_matrix(("layer", key[1], n)) for n in self.layout.roles[key[2]]]
+            if key[2] == "wgu":
+                return torch.cat([m[:m.shape[0] // 2] for m in mats] + [m[m.shape[0] // 2:] for m in mats])
+            return torch.cat(mats)
         n, k = self._unit_shape(key)
         return dgemm.frag_unpermute(self.host_weights(key)[:n * k], n, k)
 
@@ -535,12 +588,12 @@ class TieredLlama:
     def _use(self, key):
         """Fault one unit in (lease) and return (lease or None, its WeightRef).
         bf11: the GEMM reads the packed stream in place (the lease is held until
-        it is enqueued). bf12: the stream is unpacked into the staging buffer on
-        the compute stream and the lease is released right away (the ring reuses
-        the chunks only after the unpack has read them)."""
+        it is enqueued). bf12 / ans: the stream is unpacked into the staging
+        buffer on the compute stream and the lease is released right away (the
+        ring reuses the chunks only after the unpack has read them)."""
         pin = self._pinned.get(key)
         if pin is not None:  # resident tensor: long-lived lease taken at init, refs cached
-            return None, pin
+            return None, (self._unstage(key, pin.ptr) if self.staged else pin)
         acct = self.byte_trace is not None
         if acct:
             b0 = lib.stats()["bytes_xfer_htd"]
@@ -552,19 +605,24 @@ class TieredLlama:
         if acct:  # H2D bytes submitted while servicing this tensor (prefetch window + its own faults)
             self.byte_trace[key] = self.byte_trace.get(key, 0) + lib.stats()["bytes_xfer_htd"] - b0
         lease.wait(0 if self.fake else None)
-        if self.staged:
-            bf12.unpack_into(self.stage, lease.dptr, self.pinfo[key], self.dev, 0 if self.fake else None)
-            lease.release(0 if self.fake else None)
-            return None, self._ref(key, self.stage.data_ptr(), dgemm.MODE_RAW)
         mode = self.pmode.get(key, dgemm.MODE_RAW)
         refs = self._ref(key, lease.dptr, mode)
-        if self._is_resident(key) and not self.staged:
+        if self._is_resident(key):
             # Planned-resident tensors keep their lease (and so their HBM chunks)
             # for the model's lifetime: later uses cost no runtime call.
             self._pinned[key] = refs
             self._pin_leases.append(lease)
-            return None, refs
+            return None, (self._unstage(key, lease.dptr) if self.staged else refs)
+        if self.staged:
+            st = self._unstage(key, lease.dptr)
+            lease.release(0 if self.fake else None)
+            return None, st
         return lease, refs
+
+    def _unstage(self, key, packed_ptr: int) -> "dgemm.WeightRef":
+        """Unpack a packed unit into the bf16 staging buffer (compute stream)."""
+        bf12.unpack_into(self.stage, packed_ptr, self.pinfo[key], self.dev, 0 if self.fake else None)
+        return self._ref(key, self.stage.data_ptr(), dgemm.MODE_RAW)
 
     def _ref(self, key, ptr: int, mode: int) -> "dgemm.WeightRef":
         shift = (self.pinfo[key].chunk_values.bit_length() - 1) if key in self.pinfo else 20
@@ -600,12 +658,13 @@ class TieredLlama:
             x = self._row_parallel(a, w, x)
             self._done(lease)
             h = fused.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps, device_index=dv)
-            lease, w = self._use(("layer", i, "wgu"))
-            g = dgemm.linear(h, w, "silu_mul", device_index=dv)
-            self._done(lease)
-            lease, w = self._use(("layer", i, "wd"))
-            x = self._row_parallel(g, w, x)
-            self._done(lease)
+            g = torch.empty(B, self.f_local, dtype=torch.bfloat16, device=x.device)
+            for name in self.layout.roles["wgu"]:
+                r0, r1 = self.layout.rows[name]
+                lease, w = self._use(("layer", i, name))
+                dgemm.linear(h, w, "silu_mul", out=g[:, r0:r1], device_index=dv)
+                self._done(lease)
+            x = self._down(i, g, x)
         x = fused.rms_norm(x, self.final_norm, cfg.norm_eps, device_index=dv)
         logits = torch.empty(B, self.vocab_local, dtype=torch.bfloat16, device=x.device)
         for j, (r0, r1) in enumerate(self.head_rows):
@@ -625,6 +684,21 @@ class TieredLlama:
             return dgemm.linear(a, w, "resid", resid=x, out=x, device_index=self.dev)
         o = dgemm.linear(a, w, device_index=self.dev)
         return x + tpmod.row_parallel_reduce(o)
+
+    def _down(self, i: int, g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        """x + g @ Wd^T over the down projection's row parts (and TP ranks). One
+        rank: each part's residual add is fused into its GEMM epilogue, in place
+        on x[:, n0:n1]; else the parts fill one partial sum for one all-reduce."""
+        o = x if self.world == 1 else torch.empty_like(x)
+        for name in self.layout.roles["wd"]:
+            n0, n1 = self.layout.rows[name]
+            lease, w = self._use(("layer", i, name))
+            if self.world == 1:
+                dgemm.linear(g, w, "resid", resid=x[:, n0:n1], out=x[:, n0:n1], device_index=self.dev)
+            else:
+                dgemm.linear(g, w, out=o[:, n0:n1], device_index=self.dev)
+            self._done(lease)
+        return x if self.world == 1 else x + tpmod.row_parallel_reduce(o)
 
     def reset(self, position: Optional[int] = None) -> None:
         self.pos = self.ctx if position is None else position
@@ -650,7 +724,7 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
     cos, sin = model.cos[pos], model.sin[pos]
     norms = model.norm_w.float().cpu().to(dev)
     for i in range(cfg.n_layers):
-        w = {n: model.host_matrix(("layer", i, n)).float().to(dev) for n in model.parts}
+        w = {n: model.host_matrix(("layer", i, n)).float().to(dev) for n in model.layout.roles}
         h = D.rms_norm(x, norms[2 * i], cfg.norm_eps)
         qkv = h @ w["wqkv"].t()
         q = qkv[:, :model.hq * hd].view(B, model.hq, hd)

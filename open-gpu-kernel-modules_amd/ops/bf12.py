@@ -16,9 +16,12 @@ each one of
     values that escape it, ~11 bits/value (~0.69x) for weight-like data;
   * BF12: sign|mantissa bytes + 4-bit exponent codes relative to a per-chunk
     base, 12 bits/value (0.75x);
+  * ANS1 ("ans"): sign|mantissa bytes + the exponents entropy-coded with
+    interleaved rANS (one wave decodes 32 Ki values; csrc/kernels/ans_kernels.hip),
+    ~10.65 bits/value (~0.667x) for weight-like data;
   * raw bf16 (incompressible chunks / odd tails).
-All carry an exception list for exponents outside their code space, so every
-bf16 bit pattern round-trips.
+BF11/BF12 carry an exception list for exponents outside their code space and
+ANS codes every exponent, so every bf16 bit pattern round-trips.
 """
 from __future__ import annotations
 
@@ -41,6 +44,7 @@ class PackedInfo:
     nbytes: int          # stream size
     nchunks: int
     chunk_values: int
+    fmt: int = 0         # PackFormat the stream was packed with (4 = ANS)
 
     @property
     def ratio(self) -> float:
@@ -51,7 +55,8 @@ def _threads() -> int:
     return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
 
 
-FORMATS = {"bf12": 1, "bf11": 2, "bf11s": 3}  # bf11s: BF11-or-raw chunks (decode-GEMM weights)
+FORMATS = {"bf12": 1, "bf11": 2, "bf11s": 3, "ans": 4}  # bf11s: BF11-or-raw chunks (decode-GEMM weights)
+FMT_ANS = 4
 
 
 def pack(t: torch.Tensor, chunk_values: int = CHUNK_VALUES, out: torch.Tensor | None = None, fmt: str = "bf11"
@@ -72,10 +77,10 @@ def pack(t: torch.Tensor, chunk_values: int = CHUNK_VALUES, out: torch.Tensor | 
 def info_of(stream_head: torch.Tensor) -> PackedInfo:
     """Parse a stream header (the first 32 bytes, CPU tensor or bytes)."""
     raw = bytes(stream_head[:HEADER.size].cpu().numpy()) if isinstance(stream_head, torch.Tensor) else stream_head
-    magic, nch, cv, _r, n, nbytes = HEADER.unpack(raw[:HEADER.size])
+    magic, nch, cv, fmt, n, nbytes = HEADER.unpack(raw[:HEADER.size])
     if magic != MAGIC:
         raise ValueError("not a BF12 stream")
-    return PackedInfo(n, nbytes, nch, cv)
+    return PackedInfo(n, nbytes, nch, cv, fmt)
 
 
 def unpack_host(stream: torch.Tensor, info: PackedInfo) -> torch.Tensor:
@@ -100,13 +105,13 @@ def unpack_into(dst: torch.Tensor, src_ptr: int, info: PackedInfo, device: int =
         raise ValueError("dst must be bf16 with room for the unpacked chunks")
     if stream is None:
         stream = int(torch.cuda.current_stream(device).cuda_stream) if dst.is_cuda else 0
-    lib.bf12_unpack(device, src_ptr, dst.data_ptr(), info.nchunks, info.chunk_values, info.n_values, stream,
-                    workgroups, dst_stride)
+    fn = lib.ans_unpack if info.fmt == FMT_ANS else lib.bf12_unpack
+    fn(device, src_ptr, dst.data_ptr(), info.nchunks, info.chunk_values, info.n_values, stream, workgroups, dst_stride)
     return dst
 
 
 def chunk_kinds(stream: torch.Tensor) -> set:
-    """Chunk encodings present in a (CPU) stream: 0 raw, 1 BF12, 2 BF11."""
+    """Chunk encodings present in a (CPU) stream: 0 raw, 1 BF12, 2 BF11, 3 ANS1."""
     info = info_of(stream[:64])
     table = stream[32:32 + 16 * info.nchunks].view(torch.int32).view(-1, 4)
     return set(int(k) for k in table[:, 3].unique().tolist())

@@ -50,3 +50,40 @@ def test_bf11_property_roundtrip(n, std, chunk, seed):
     g = torch.Generator().manual_seed(seed)
     ref = (torch.randn(n, generator=g) * std).to(torch.bfloat16)
     _roundtrip(ref, "bf11", chunk)
+
+
+@pytest.mark.parametrize("std", [0.02, 1.0, 1e-3])
+def test_ans_ratio_and_exactness_gaussian(std):
+    """ANS1 (rANS-coded exponents) round-trips and beats BF11 by its entropy margin."""
+    torch.manual_seed(1)
+    ref = (torch.randn(3 << 20) * std).to(torch.bfloat16)
+    ia = _roundtrip(ref, "ans")
+    i11 = _roundtrip(ref, "bf11")
+    assert ia.ratio < 0.675 and ia.ratio < i11.ratio - 0.02, (ia.ratio, i11.ratio)
+    assert bf12.chunk_kinds(bf12.pack(ref, fmt="ans")[0]) == {3}
+
+
+def test_ans_specials_constant_incompressible_and_tails():
+    torch.manual_seed(3)
+    ref = (torch.randn(1 << 20) * 0.02).to(torch.bfloat16)
+    specials = torch.tensor([0.0, -0.0, float("inf"), float("-inf"), float("nan"), 3.0e38, 1e-40, -2.5, 1.0],
+                            dtype=torch.bfloat16)
+    for t in range(32):  # rare exponents in every segment (12-bit frequency floor)
+        ref[t * 32768 + 100:t * 32768 + 109] = specials
+    _roundtrip(ref, "ans")
+    _roundtrip(torch.zeros(1 << 16, dtype=torch.bfloat16), "ans")          # one symbol
+    _roundtrip(torch.full((1 << 16,), 0.5, dtype=torch.bfloat16), "ans")   # one symbol
+    rnd = torch.randint(-32768, 32767, (1 << 20,), dtype=torch.int16).view(torch.bfloat16)
+    assert _roundtrip(rnd, "ans").ratio <= 1.001                           # raw fallback
+    tail = (torch.randn((1 << 20) + 1000) * 0.02).to(torch.bfloat16)       # last chunk not % 512: raw
+    info = _roundtrip(tail, "ans")
+    assert bf12.chunk_kinds(bf12.pack(tail, fmt="ans")[0]) == {0, 3} and info.ratio < 0.68
+
+
+@settings(max_examples=30, deadline=None)
+@given(n=st.integers(1, 80).map(lambda k: 512 * k), std=st.sampled_from([0.02, 1.0, 1e-30, 1e30]),
+       chunk=st.sampled_from([8192, 32768, 1 << 20]), seed=st.integers(0, 2**31 - 1))
+def test_ans_property_roundtrip(n, std, chunk, seed):
+    g = torch.Generator().manual_seed(seed)
+    ref = (torch.randn(n, generator=g) * std).to(torch.bfloat16)
+    _roundtrip(ref, "ans", chunk)

@@ -256,8 +256,8 @@ def test_bf12_decode_bandwidth(gpu_rt):
     b.free()
 
 
-@pytest.mark.parametrize("fmt,max_ratio", [("bf12", 0.78), ("bf11", 0.71)])
-def test_bf12_stream_unpack_hbm_bit_exact_and_fast(gpu_rt, fmt, max_ratio):
+@pytest.mark.parametrize("fmt,max_ratio,min_gbps", [("bf12", 0.78, 1000), ("bf11", 0.71, 1000), ("ans", 0.69, 400)])
+def test_bf12_stream_unpack_hbm_bit_exact_and_fast(gpu_rt, fmt, max_ratio, min_gbps):
     """k_bf12_unpack (HBM-resident packed weights -> bf16 staging) reproduces every
     bit and runs at HBM speed (a 70B layer is ~1.7 GB of bf16), for BF12 and
     BF11 chunks (the kernel dispatches per chunk)."""
@@ -269,7 +269,8 @@ def test_bf12_stream_unpack_hbm_bit_exact_and_fast(gpu_rt, fmt, max_ratio):
                             dtype=torch.bfloat16)
     ref[:len(specials)] = specials
     ref[123457:123457 + len(specials)] = specials
-    # exceptions in several tiles + a chunk of uniformly random bits (stored raw / BF12)
+    # exceptions in several tiles + a chunk of uniformly random bits (stored raw / BF12; ANS: every
+    # exponent is a symbol, the random chunk is stored raw)
     ref[(5 << 20) + 17] = torch.tensor(1e30, dtype=torch.bfloat16)
     ref[(9 << 20) + 40000] = torch.tensor(-1e-30, dtype=torch.bfloat16)
     ref[(12 << 20):(13 << 20)] = torch.randint(-32768, 32767, (1 << 20,), dtype=torch.int16).view(torch.bfloat16)
@@ -292,4 +293,4 @@ def test_bf12_stream_unpack_hbm_bit_exact_and_fast(gpu_rt, fmt, max_ratio):
     dt = (time.perf_counter() - t0) / iters
     gbps = n * 2 / dt / 1e9
     print(f"{fmt} HBM unpack: {gbps:.0f} GB/s of bf16 written ({(info.nbytes + 2 * n) / dt / 1e9:.0f} GB/s HBM traffic)")
-    assert gbps > 1000
+    assert gbps > min_gbps

@@ -88,7 +88,7 @@ def test_streaming_matches_plan_hbm_packed(fake_rt, fmt, ratio):
 def test_bf12_weights_bit_identical_to_bf16(fake_rt):
     cfg = llama.CONFIGS["tiny"]
     out = {}
-    for fmt in ("bf16", "bf12", "bf11"):
+    for fmt in ("bf16", "bf12", "bf11", "ans"):
         m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=4, oversub=1.5, lookahead=1, seed=9,
                               weight_format=fmt)
         m.keep_logits = True
@@ -99,7 +99,7 @@ def test_bf12_weights_bit_identical_to_bf16(fake_rt):
             logs.append(m.last_logits.clone())
         out[fmt] = logs
         m.close()
-    for fmt in ("bf12", "bf11"):
+    for fmt in ("bf12", "bf11", "ans"):
         for a, b in zip(out["bf16"], out[fmt]):
             assert torch.equal(a, b)
 
@@ -172,7 +172,7 @@ def test_bf11_kv_cache_bit_identical_to_bf16(fake_rt):
     context: logits are bit-identical to the raw cache, and it rests smaller."""
     cfg = llama.CONFIGS["tiny"]
     out, res = {}, {}
-    for fmt in ("bf16", "bf11"):
+    for fmt in ("bf16", "bf11", "ans"):
         m = llama.TieredLlama(cfg, batch=2, context=128, max_new_tokens=4, oversub=1.2, lookahead=1, seed=9,
                               kv_format=fmt)
         m.keep_logits = True
@@ -184,6 +184,7 @@ def test_bf11_kv_cache_bit_identical_to_bf16(fake_rt):
         out[fmt] = logs
         res[fmt] = m.kv_resident_bytes
         m.close()
-    for a, b in zip(out["bf16"], out["bf11"]):
-        assert torch.equal(a, b)
-    assert res["bf11"] < 0.8 * res["bf16"]
+    for fmt in ("bf11", "ans"):
+        for a, b in zip(out["bf16"], out[fmt]):
+            assert torch.equal(a, b)
+    assert res["ans"] < res["bf11"] < 0.8 * res["bf16"]

@@ -14,7 +14,7 @@ from ogkm.models import llama
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("weight_format,kv_format", [("bf11", "bf11"), ("bf16", "bf16"), ("bf12", "bf16")])
+@pytest.mark.parametrize("weight_format,kv_format", [("bf11", "bf11"), ("bf16", "bf16"), ("bf12", "bf16"), ("ans", "ans")])
 def test_tiny_decode_matches_fp32_reference_gpu(gpu_rt, weight_format, kv_format):
     cfg = llama.CONFIGS["tiny"]
     m = llama.TieredLlama(cfg, batch=3, context=128, max_new_tokens=4, oversub=1.5, lookahead=1, seed=5,
@@ -35,7 +35,7 @@ def test_tiny_decode_matches_fp32_reference_gpu(gpu_rt, weight_format, kv_format
 def test_formats_bit_identical_gpu(gpu_rt):
     cfg = llama.CONFIGS["small"]
     outs = {}
-    for wf, kf in (("bf16", "bf16"), ("bf11", "bf11")):
+    for wf, kf in (("bf16", "bf16"), ("bf11", "bf11"), ("ans", "ans")):
         m = llama.TieredLlama(cfg, batch=4, context=128, max_new_tokens=4, oversub=2.0, lookahead=1, seed=7,
                               weight_format=wf, kv_format=kf)
         m.keep_logits = True
@@ -47,5 +47,6 @@ def test_formats_bit_identical_gpu(gpu_rt):
         torch.cuda.synchronize()
         outs[wf] = logs
         m.close()
-    for a, b in zip(outs["bf16"], outs["bf11"]):
-        assert torch.equal(a, b)
+    for fmt in ("bf11", "ans"):
+        for a, b in zip(outs["bf16"], outs[fmt]):
+            assert torch.equal(a, b)
