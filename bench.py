@@ -17,11 +17,14 @@ streams only its shard over its own PCIe link.
 One step = one decode token for every sequence (weights streamed, KV appended,
 greedy sampling). ``value`` = global tokens/s = batch * K / max-over-ranks time.
 
-Weights rest losslessly packed (BF11, ~0.69x, bit-exact bf16 after unpack) in
-every tier and are unpacked into a bf16 staging buffer right before each layer
-runs; the oversubscription ratio and HBM budget are computed on the logical bf16
-footprint (weights + KV + embedding + head), and the staging buffer is carved out
-of that budget. ``--weights bf16`` runs the raw-weight path for comparison.
+Weights rest losslessly packed (rANS over the exponents, ~0.66x, bit-exact
+bf16 after unpack) in every tier and are unpacked per matrix into a bf16 staging
+buffer right before it is used (the KV prefix likewise, per layer); the
+oversubscription ratio and HBM budget are computed on the logical bf16 footprint
+(weights + KV + embedding + head), and the staging buffers are carved out of that
+budget. Streamed matrices cross PCIe on SDMA (the runtime's default ring engine),
+so the compute kernels run at full speed beside them. ``--weights bf11`` (decoded
+in the GEMM's registers) and ``--weights bf16`` run the other paths.
 
 Also reported (aux): HBM<->host and HBM<->CXL GB/s measured through the runtime's
 rings (the CXL pool is an emulated NUMA node when the box has no CXL device).
@@ -54,13 +57,13 @@ def parse():
     ap.add_argument("--lookahead", type=int, default=int(os.environ.get("OGKM_LOOKAHEAD", "1")),
                     help="streamed tensors in flight beyond the one in use (each costs a staging slot of HBM)")
     ap.add_argument("--no-aux", action="store_true", help="skip the HBM<->host/CXL bandwidth probe")
-    ap.add_argument("--weights", choices=("bf11", "bf12", "ans", "bf16"), default="bf11",
+    ap.add_argument("--weights", choices=("bf11", "bf12", "ans", "bf16"), default="ans",
                     help="bf11/ans/bf12: weights rest losslessly packed (~0.70x / ~0.67x / 0.75x) in every tier (HBM "
                          "included); bf11 is decoded in the GEMM's registers, ans/bf12 unpacked per matrix into a "
                          "bf16 staging buffer; bf16: raw weights")
     ap.add_argument("--no-packed", action="store_true",
                     help="with --weights bf16: raw host copies instead of BF12 copies decoded in the H2D kernel")
-    ap.add_argument("--kv-format", choices=("bf11", "ans", "bf16"), default="bf11",
+    ap.add_argument("--kv-format", choices=("bf11", "ans", "bf16"), default="ans",
                     help="bf11: the prefilled KV context rests losslessly packed in HBM (unpacked per layer into a "
                          "one-layer scratch), decode tokens raw; bf16: raw KV cache")
     ap.add_argument("--tiers", choices=("host", "host+cxl"), default="host",
@@ -233,6 +236,7 @@ def main() -> None:
                 "managed_footprint_gb_per_gpu": round(plan["footprint_gb"], 2),
                 "resident_layers": plan["resident_layers"],
                 "streamed_layers": plan["streamed_layers"],
+                "extra_resident_units": plan["extra_resident_units"],
                 "streamed_gb_per_step_per_gpu": round(plan["streamed_gb_per_step"], 2),
                 "weight_format": plan["weight_format"],
                 "host_copy_format": (f"{plan['weight_format']}-lossless" if plan["weight_format"] != "bf16"

@@ -5,8 +5,13 @@
 // * Host / CXL tiers: memfd pages registered with hipHostRegister (IOMMU-correct
 //   device mapping, identity address) - never raw physical addresses (fixes the
 //   reference's SKIP_IOMMU_MAPPING memdesc, p2p_cxl.c:167-217).
-// * Copies: hand-written copy kernels on side streams (engine 0) or SDMA via
-//   hipMemcpyAsync (engine 1, comparator only).
+// * Copies: SDMA via hipMemcpyAsync on the ring's side stream (engine 1, the
+//   default for PCIe / xGMI copies) or hand-written copy kernels (engine 0;
+//   engine 2 = HBM<->HBM, always kernels). Measured under the 70B decode
+//   (profiles/r1_copy_engine_interference.md): while a 16-WG copy kernel pulls
+//   host memory over PCIe, the HBM-bound compute kernels on the other stream
+//   run 3-7x slower (k_dgemm 42 -> 155 us, k_ans_unpack 114 -> 306 us); with
+//   SDMA they run at their unloaded speed and the step is link-bound.
 // * Completion: k_signal system-scope release into host-coherent memory;
 //   GPU-side waits with hipStreamWaitValue64 / hipStreamWaitEvent.
 #include <hip/hip_runtime.h>

@@ -56,7 +56,7 @@ namespace ogkm {
   X(host_budget_mb, 0, "host-tier arena limit in MB (0 = pin budget)")                               \
   /* channels / ring */                                                                              \
   X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \
-  X(copy_engine, 0, "0=HIP copy kernels 1=SDMA (hipMemcpyAsync) comparator")                         \
+  X(copy_engine, 1, "PCIe/xGMI ring copies: 1=SDMA (hipMemcpyAsync, default) 0=HIP copy kernels")       \
   X(copy_workgroups, 16, "workgroups per copy-kernel launch (CU budget; 16 saturate PCIe, more starve HBM-bound compute)") \
   X(copy_piece_kb, 64, "bytes per copy work item (KB)")                                              \
   X(decode_workgroups, 256, "workgroups per fused copy+BF12-decode launch")                           \

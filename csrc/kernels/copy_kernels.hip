@@ -12,6 +12,10 @@
 //    (vs one CE LAUNCH_DMA per contiguous run in the reference,
 //    uvm_va_block.c:4278-4326). Each wave keeps 4 dwordx4 loads in flight
 //    before storing (HBM/PCIe latency hiding without LDS).
+//  * PCIe-bound ring copies default to SDMA (config copy_engine=1): a copy kernel
+//    reading host memory slows concurrent HBM-bound kernels 3-7x (measured,
+//    profiles/r1_copy_engine_interference.md). These kernels serve HBM<->HBM
+//    copies, page gather/scatter, the fused copy+decode path and copy_engine=0.
 //  * Small batches pass their descriptors by value in the kernarg segment
 //    (scalar loads, no extra upload); big batches read them from device memory.
 #include <hip/hip_runtime.h>

@@ -381,7 +381,26 @@ __global__ void __launch_bounds__(256) k_dgemm_reduce(DGemmReduceArgs a) {
   if (i >= (uint64_t)a.M * q) return;
   const uint32_t m = (uint32_t)(i / q), n = (uint32_t)(i - (uint64_t)m * q) * 4u;
   f32x4_t s = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
-  for (uint32_t k = 0; k < a.ksplit; ++k) {
+  // Batches of 8 split rows: all loads of a batch are issued before the first
+  // add (8 requests in flight per lane instead of one dependent load per split;
+  // the wd shapes run 64 splits). Summation order is unchanged (k ascending).
+  constexpr uint32_t kB = 8;
+  uint32_t k = 0;
+  for (; k + kB <= a.ksplit; k += kB) {
+    f32x4_t v[kB], w[kB];
+#pragma unroll
+    for (uint32_t j = 0; j < kB; ++j) {
+      const float* row = a.part + ((uint64_t)(k + j) * a.M + m) * a.N;
+      v[j] = *reinterpret_cast<const f32x4_t*>(row + n);
+      if (a.epi == DGEMM_EPI_SILU_MUL) w[j] = *reinterpret_cast<const f32x4_t*>(row + nout + n);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kB; ++j) {
+      s += v[j];
+      if (a.epi == DGEMM_EPI_SILU_MUL) u += w[j];
+    }
+  }
+  for (; k < a.ksplit; ++k) {
     const float* row = a.part + ((uint64_t)k * a.M + m) * a.N;
     s += *reinterpret_cast<const f32x4_t*>(row + n);
     if (a.epi == DGEMM_EPI_SILU_MUL) u += *reinterpret_cast<const f32x4_t*>(row + nout + n);
