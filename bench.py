@@ -22,8 +22,9 @@ bf16 after unpack) in every tier and are unpacked per matrix into a bf16 staging
 buffer right before it is used (the KV prefix likewise, per layer); the
 oversubscription ratio and HBM budget are computed on the logical bf16 footprint
 (weights + KV + embedding + head), and the staging buffers are carved out of that
-budget. Streamed matrices cross PCIe on SDMA (the runtime's default ring engine),
-so the compute kernels run at full speed beside them. ``--weights bf11`` (decoded
+budget. Streamed matrices cross PCIe through hipMemcpyAsync on the migration
+ring's side stream (the runtime's default engine), so the compute kernels run at
+full speed beside them. ``--weights bf11`` (decoded
 in the GEMM's registers) and ``--weights bf16`` run the other paths.
 
 Also reported (aux): HBM<->host and HBM<->CXL GB/s measured through the runtime's

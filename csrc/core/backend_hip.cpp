@@ -5,13 +5,14 @@
 // * Host / CXL tiers: memfd pages registered with hipHostRegister (IOMMU-correct
 //   device mapping, identity address) - never raw physical addresses (fixes the
 //   reference's SKIP_IOMMU_MAPPING memdesc, p2p_cxl.c:167-217).
-// * Copies: SDMA via hipMemcpyAsync on the ring's side stream (engine 1, the
-//   default for PCIe / xGMI copies) or hand-written copy kernels (engine 0;
-//   engine 2 = HBM<->HBM, always kernels). Measured under the 70B decode
-//   (profiles/r1_copy_engine_interference.md): while a 16-WG copy kernel pulls
+// * Copies: hipMemcpyAsync on the ring's side stream (engine 1, the default for
+//   PCIe / xGMI copies; the kernel trace shows it as the runtime's
+//   __amd_rocclr_copyBuffer) or our hand-written copy kernels (engine 0;
+//   engine 2 = HBM<->HBM, always ours). Measured under the 70B decode
+//   (profiles/r1_copy_engine_interference.md): while our 16-WG copy kernel pulls
 //   host memory over PCIe, the HBM-bound compute kernels on the other stream
 //   run 3-7x slower (k_dgemm 42 -> 155 us, k_ans_unpack 114 -> 306 us); with
-//   SDMA they run at their unloaded speed and the step is link-bound.
+//   engine 1 they run at their unloaded speed and the step is link-bound.
 // * Completion: k_signal system-scope release into host-coherent memory;
 //   GPU-side waits with hipStreamWaitValue64 / hipStreamWaitEvent.
 #include <hip/hip_runtime.h>
@@ -243,7 +244,8 @@ class HipBackend : public Backend {
       inl.piece_start[cnt] = ps;
       // HBM<->HBM copies are not PCIe bound: give them the whole chip.
       uint32_t g = hbm_only ? (wgs * 16 > 2048 ? 2048 : wgs * 16) : wgs;
-      HIPCHK(launch_batch_copy(nullptr, nullptr, &inl, (uint32_t)cnt, ps, piece, g, (hipStream_t)s));
+      HIPCHK(launch_batch_copy(nullptr, nullptr, &inl, (uint32_t)cnt, ps, piece, g, (hipStream_t)s,
+                                config().copy_nt_loads != 0));
       launches_++;
     }
     return Status::OK;

@@ -56,9 +56,10 @@ namespace ogkm {
   X(host_budget_mb, 0, "host-tier arena limit in MB (0 = pin budget)")                               \
   /* channels / ring */                                                                              \
   X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \
-  X(copy_engine, 1, "PCIe/xGMI ring copies: 1=SDMA (hipMemcpyAsync, default) 0=HIP copy kernels")       \
+  X(copy_engine, 1, "PCIe/xGMI ring copies: 1=hipMemcpyAsync (default) 0=our HIP copy kernels")       \
   X(copy_workgroups, 16, "workgroups per copy-kernel launch (CU budget; 16 saturate PCIe, more starve HBM-bound compute)") \
   X(copy_piece_kb, 64, "bytes per copy work item (KB)")                                              \
+  X(copy_nt_loads, 1, "copy kernels: non-temporal source loads (0 = plain loads)")                      \
   X(decode_workgroups, 256, "workgroups per fused copy+BF12-decode launch")                           \
   X(peer_copy, 1, "0=phys 1=virt peer addressing")                                                   \
   /* misc UVM knobs */                                                                               \

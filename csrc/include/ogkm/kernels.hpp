@@ -33,7 +33,7 @@ struct KInlineDescs {   // passed by value as a kernel argument for small batche
 // batches) or null with `inl` used. piece_bytes must be a multiple of 4096.
 hipError_t launch_batch_copy(const KCopyDesc* d_descs, const uint64_t* d_piece_start, const KInlineDescs* inl,
                              uint32_t n, uint64_t total_pieces, uint32_t piece_bytes, uint32_t workgroups,
-                             hipStream_t s);
+                             hipStream_t s, bool nt_loads = true);
 hipError_t launch_gather_pages(uint64_t base, uint64_t contig, const uint32_t* d_idx, uint32_t npages,
                                uint32_t page_bytes, bool scatter, uint32_t workgroups, hipStream_t s);
 hipError_t launch_memset32(uint64_t dst, uint32_t pattern, uint64_t bytes, hipStream_t s);

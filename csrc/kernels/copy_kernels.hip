@@ -12,9 +12,10 @@
 //    (vs one CE LAUNCH_DMA per contiguous run in the reference,
 //    uvm_va_block.c:4278-4326). Each wave keeps 4 dwordx4 loads in flight
 //    before storing (HBM/PCIe latency hiding without LDS).
-//  * PCIe-bound ring copies default to SDMA (config copy_engine=1): a copy kernel
-//    reading host memory slows concurrent HBM-bound kernels 3-7x (measured,
-//    profiles/r1_copy_engine_interference.md). These kernels serve HBM<->HBM
+//  * PCIe-bound ring copies default to hipMemcpyAsync (config copy_engine=1):
+//    this kernel reading host memory slows concurrent HBM-bound kernels 3-7x
+//    (2.5x less with plain instead of non-temporal loads, copy_nt_loads=0;
+//    measured, profiles/r1_copy_engine_interference.md). These kernels serve HBM<->HBM
 //    copies, page gather/scatter, the fused copy+decode path and copy_engine=0.
 //  * Small batches pass their descriptors by value in the kernarg segment
 //    (scalar loads, no extra upload); big batches read them from device memory.
@@ -30,6 +31,9 @@ constexpr int kThreads = 256;
 constexpr int kUnroll = 4;
 
 // Copy `len` bytes with 256 threads. Fast path: 16-B aligned src/dst.
+// NT_LOAD: non-temporal source loads (config copy_nt_loads); stores are always
+// non-temporal.
+template <bool NT_LOAD = true>
 __device__ __forceinline__ void copy_span(uint64_t dst, uint64_t src, uint64_t len) {
   const int t = threadIdx.x;
   if (((dst | src) & 15) == 0) {
@@ -40,11 +44,11 @@ __device__ __forceinline__ void copy_span(uint64_t dst, uint64_t src, uint64_t l
     for (; i + (kUnroll - 1) * kThreads < n16; i += kUnroll * kThreads) {
       u32x4 v[kUnroll];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = __builtin_nontemporal_load(s + i + u * kThreads);
+      for (int u = 0; u < kUnroll; ++u) v[u] = NT_LOAD ? __builtin_nontemporal_load(s + i + u * kThreads) : s[i + u * kThreads];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) __builtin_nontemporal_store(v[u], d + i + u * kThreads);
     }
-    for (; i < n16; i += kThreads) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+    for (; i < n16; i += kThreads) __builtin_nontemporal_store(NT_LOAD ? __builtin_nontemporal_load(s + i) : s[i], d + i);
     uint64_t tail = n16 << 4;
     for (uint64_t b = tail + t; b < len; b += kThreads)
       reinterpret_cast<uint8_t*>(dst)[b] = reinterpret_cast<const uint8_t*>(src)[b];
@@ -61,7 +65,7 @@ __device__ __forceinline__ void copy_span(uint64_t dst, uint64_t src, uint64_t l
   }
 }
 
-template <bool INLINE>
+template <bool INLINE, bool NT_LOAD>
 __global__ void __launch_bounds__(kThreads)
     k_batch_copy(const KCopyDesc* __restrict__ descs, const uint64_t* __restrict__ piece_start, KInlineDescs inl,
                  uint32_t n, uint64_t total_pieces, uint32_t piece_bytes) {
@@ -92,25 +96,31 @@ __global__ void __launch_bounds__(kThreads)
     uint64_t off = (p - ps_i) * (uint64_t)piece_bytes;
     uint64_t len = d.bytes - off;
     if (len > piece_bytes) len = piece_bytes;
-    copy_span(d.dst + off, d.src + off, len);
+    copy_span<NT_LOAD>(d.dst + off, d.src + off, len);
     __syncthreads();
   }
 }
 
 hipError_t launch_batch_copy(const KCopyDesc* d_descs, const uint64_t* d_piece_start, const KInlineDescs* inl,
                              uint32_t n, uint64_t total_pieces, uint32_t piece_bytes, uint32_t workgroups,
-                             hipStream_t s) {
+                             hipStream_t s, bool nt_loads) {
   if (n == 0 || total_pieces == 0) return hipSuccess;
   uint32_t grid = (uint32_t)(total_pieces < workgroups ? total_pieces : workgroups);
   if (grid == 0) grid = 1;
-  if (inl) {
-    hipLaunchKernelGGL(k_batch_copy<true>, dim3(grid), dim3(kThreads), 0, s, nullptr, nullptr, *inl, n,
+  KInlineDescs dummy;
+  const KInlineDescs& d = inl ? *inl : dummy;
+  if (inl && nt_loads)
+    hipLaunchKernelGGL((k_batch_copy<true, true>), dim3(grid), dim3(kThreads), 0, s, nullptr, nullptr, d, n,
                        total_pieces, piece_bytes);
-  } else {
-    KInlineDescs dummy;
-    hipLaunchKernelGGL(k_batch_copy<false>, dim3(grid), dim3(kThreads), 0, s, d_descs, d_piece_start, dummy, n,
+  else if (inl)
+    hipLaunchKernelGGL((k_batch_copy<true, false>), dim3(grid), dim3(kThreads), 0, s, nullptr, nullptr, d, n,
                        total_pieces, piece_bytes);
-  }
+  else if (nt_loads)
+    hipLaunchKernelGGL((k_batch_copy<false, true>), dim3(grid), dim3(kThreads), 0, s, d_descs, d_piece_start, d,
+                       n, total_pieces, piece_bytes);
+  else
+    hipLaunchKernelGGL((k_batch_copy<false, false>), dim3(grid), dim3(kThreads), 0, s, d_descs, d_piece_start, d,
+                       n, total_pieces, piece_bytes);
   return hipGetLastError();
 }
 

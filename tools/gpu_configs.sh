@@ -1,4 +1,5 @@
-# North-star configs beyond the headline: 405B tp8 shard (simulated) on three tiers, 70B three-tier, lookahead 1.
+# North-star configs beyond the headline: 405B tp8 shard (simulated) on three tiers, 70B three-tier,
+# 8B HBM-resident allocator baseline (config 2).
 set -o pipefail
 mkdir -p gpurun_out
 : > gpurun_out/configs.log
@@ -9,4 +10,4 @@ run() {
 }
 run python bench.py --model llama3-405b --simulate-tp 8 --tiers host+cxl --steps 3 --warmup 1 --no-aux
 run python bench.py --tiers host+cxl --steps 3 --warmup 1 --no-aux
-run env OGKM_LOOKAHEAD=1 python bench.py --steps 3 --warmup 1 --no-aux
+run python bench.py --model llama3-8b --oversub 1.0 --steps 5 --warmup 2 --no-aux
