@@ -58,13 +58,13 @@ def parse():
     ap.add_argument("--lookahead", type=int, default=int(os.environ.get("OGKM_LOOKAHEAD", "1")),
                     help="streamed tensors in flight beyond the one in use (each costs a staging slot of HBM)")
     ap.add_argument("--no-aux", action="store_true", help="skip the HBM<->host/CXL bandwidth probe")
-    ap.add_argument("--weights", choices=("bf11", "bf12", "ans", "bf16"), default="ans",
+    ap.add_argument("--weights", choices=("auto", "bf11", "bf12", "ans", "bf16"), default="auto",
                     help="bf11/ans/bf12: weights rest losslessly packed (~0.70x / ~0.67x / 0.75x) in every tier (HBM "
                          "included); bf11 is decoded in the GEMM's registers, ans/bf12 unpacked per matrix into a "
                          "bf16 staging buffer; bf16: raw weights")
     ap.add_argument("--no-packed", action="store_true",
                     help="with --weights bf16: raw host copies instead of BF12 copies decoded in the H2D kernel")
-    ap.add_argument("--kv-format", choices=("bf11", "ans", "bf16"), default="ans",
+    ap.add_argument("--kv-format", choices=("auto", "bf11", "ans", "bf16"), default="auto",
                     help="bf11: the prefilled KV context rests losslessly packed in HBM (unpacked per layer into a "
                          "one-layer scratch), decode tokens raw; bf16: raw KV cache")
     ap.add_argument("--tiers", choices=("host", "host+cxl"), default="host",
@@ -139,6 +139,13 @@ def probe_all_ranks(dev: int, rank: int) -> dict:
 
 def main() -> None:
     a = parse()
+    # auto: packed (rANS) resting formats when part of the model streams - every
+    # byte saved is a byte off PCIe; raw bf16 when everything is HBM-resident
+    # (oversub <= 1), where packing would only add unpack work (8B: 2902 vs 925 tok/s).
+    if a.weights == "auto":
+        a.weights = "ans" if a.oversub > 1.0 else "bf16"
+    if a.kv_format == "auto":
+        a.kv_format = "ans" if a.oversub > 1.0 else "bf16"
     import torch
 
     from ogkm import rt
