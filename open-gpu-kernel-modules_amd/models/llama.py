@@ -124,7 +124,13 @@ class LayerLayout:
         add("wo", "wo", (cfg.dim, hq * hd), 0, cfg.dim)
         if unit_bytes is None:
             env = os.environ.get("OGKM_UNIT_MB")
-            unit_bytes = int(float(env) * 2**20) if env else max(nqkv * cfg.dim, cfg.dim * hq * hd) * 2
+            # Floor (OGKM_UNIT_MIN_MB, default 128 MB): every unit costs fixed host
+            # work (lease, unpack, GEMM + reduce launches), so small TP shards keep
+            # whole matrices as units instead of ~16 MB slivers (70B tp8: 4 units
+            # per layer instead of 13).
+            floor = int(float(os.environ.get("OGKM_UNIT_MIN_MB", "128")) * 2**20)
+            unit_bytes = (int(float(env) * 2**20) if env
+                          else max(max(nqkv * cfg.dim, cfg.dim * hq * hd) * 2, floor))
         p = LayerLayout._nparts(f, 2 * f * cfg.dim * 2, unit_bytes)
         per = f // p
         for j in range(p):

@@ -18,6 +18,9 @@ if str(ROOT) not in sys.path:
     sys.path.insert(0, str(ROOT))
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# Test models are tiny: no unit-size floor, so their FFN matrices still split
+# into several streamed row parts (the multi-part path stays covered).
+os.environ.setdefault("OGKM_UNIT_MIN_MB", "0")
 
 import ogkm  # noqa: E402  (builds/loads the native core)
 from ogkm import rt  # noqa: E402
