@@ -391,27 +391,11 @@ class TieredLlama:
         self._pin_leases: list = []
         self.keep_logits = False   # tests: keep the full-vocab logits of the last step
         self.last_logits = None
-        if not self.fake and os.environ.get("OGKM_WARM_STREAM", "1") != "0":
-            self._warm_stream()
         self.init_seconds = time.perf_counter() - t0
         if verbose:
             self.describe()
 
     # ------------------------------------------------------------------ setup
-    def _warm_stream(self) -> None:
-        """Load-time pass of every streamed unit through the ring (host tier ->
-        HBM slot, then released): the copy path's first-use costs (runtime
-        lookups of each registered host segment, first evictions) are paid while
-        loading instead of in the first decode steps (405B three-tier: the
-        first steps ran 16 s each without it)."""
-        for key in self.stream_seq:
-            b = self._buf(key)
-            b.prefetch(rt.Loc.gpu(self.dev))
-            lease = b.acquire(self.dev, rt.READ)
-            lease.wait(None)
-            lease.release(None)
-        torch.cuda.synchronize(self.dev)
-
     def describe(self) -> dict:
         d = {
             "model": self.cfg.name, "tp": f"{self.rank}/{self.world}", "batch": self.B, "context": self.ctx,
