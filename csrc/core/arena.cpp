@@ -89,7 +89,7 @@ void ChunkArena::lru_push_tail(uint32_t i, uint8_t list) {
 }
 
 // ------------------------------------------------------------ allocation
-Status ChunkArena::alloc(uint32_t n, Block* owner, int64_t hint, uint32_t* first) {
+Status ChunkArena::alloc(uint32_t n, Block* owner, int64_t hint, uint32_t* first, bool pin) {
   if (n == 0) return Status::INVALID_ARGUMENT;
   std::lock_guard<OrderedMutex> g(m_);
   int64_t pick = -1;
@@ -117,10 +117,11 @@ Status ChunkArena::alloc(uint32_t n, Block* owner, int64_t hint, uint32_t* first
     ChunkInfo& c = chunks_[pick + i];
     c.state = ChunkState::ALLOCATED;
     c.owner = owner;
-    c.pin_count = 0;
+    c.pin_count = pin ? 1 : 0;
     c.last_use = ++clock_;
     lru_push_tail((uint32_t)pick + i, 1);
   }
+  if (pin) st_.pinned += (uint64_t)n << kBlockShift;
   st_.allocated += (uint64_t)n << kBlockShift;
   st_.peak = std::max(st_.peak, st_.allocated);
   st_.allocs += n;
@@ -235,17 +236,18 @@ void ChunkArena::evicted(uint32_t i) {
   st_.evictions++;
 }
 
-void ChunkArena::commit(const Reservation& r) {
+void ChunkArena::commit(const Reservation& r, bool pin) {
   std::lock_guard<OrderedMutex> g(m_);
   for (uint32_t i = 0; i < r.n; ++i) {
     ChunkInfo& c = chunks_[r.first + i];
     RT_ASSERT_RELEASE(c.state == ChunkState::RESERVED);
     c.state = ChunkState::ALLOCATED;
     c.owner = nullptr;
-    c.pin_count = 0;
+    c.pin_count = pin ? 1 : 0;
     c.last_use = ++clock_;
     lru_push_tail((uint32_t)r.first + i, 1);
   }
+  if (pin) st_.pinned += (uint64_t)r.n << kBlockShift;
   st_.allocated += (uint64_t)r.n << kBlockShift;
   st_.peak = std::max(st_.peak, st_.allocated);
   st_.allocs += r.n;
@@ -275,6 +277,7 @@ void ChunkArena::free(uint32_t first, uint32_t n) {
     ChunkInfo& c = chunks_[k];
     RT_ASSERT_RELEASE(c.state == ChunkState::ALLOCATED);
     lru_remove(k);
+    if (c.pin_count) st_.pinned -= kBlockSize;
     c.state = ChunkState::FREE;
     c.owner = nullptr;
     c.pin_count = 0;
@@ -327,11 +330,17 @@ void ChunkArena::add_reuse_fence(uint32_t i, const FenceRef& f) {
   chunks_[i].reuse_fence.add(f);
 }
 
-Tracker ChunkArena::take_reuse_fence(uint32_t i) {
+// Every writer of a chunk waits for the chunk's reuse fence; the fence stays
+// (completed fences are pruned) because one chunk can receive several writers
+// on different rings - e.g. a D2D relocation of resident pages plus the H2D copy
+// of the missing ones. Consuming the fence on the first writer let the second
+// overwrite data the previous owner's kernels were still reading (the corrupt
+// ANS chunks / ~47 s decoder spin of the 70B tp8 shard,
+// profiles/r2_corrupt_chunk_hunt.md).
+Tracker ChunkArena::reuse_fence(uint32_t i) {
   std::lock_guard<OrderedMutex> g(m_);
-  Tracker t = chunks_[i].reuse_fence;
-  chunks_[i].reuse_fence.clear();
-  return t;
+  chunks_[i].reuse_fence.prune();
+  return chunks_[i].reuse_fence;
 }
 
 ChunkArena::Stats ChunkArena::stats() {

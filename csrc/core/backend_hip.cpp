@@ -281,9 +281,16 @@ class HipBackend : public Backend {
   Status unpack_ans_stream(int, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values, uint64_t,
                            void* s, uint32_t workgroups, uint64_t dst_stride) override {
     HIPCHK(launch_ans_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s,
-                             dst_stride));
+                             dst_stride, decode_err()));
     launches_++;
     return Status::OK;
+  }
+
+  void decode_errors(uint64_t out[4], bool reset) override {
+    uint64_t* e = decode_err();
+    for (int i = 0; i < 4; ++i) out[i] = e ? __atomic_load_n(e + i, __ATOMIC_ACQUIRE) : 0;
+    if (e && reset)
+      for (int i = 0; i < 4; ++i) __atomic_store_n(e + i, 0ull, __ATOMIC_RELEASE);
   }
 
   Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {
@@ -427,7 +434,21 @@ class HipBackend : public Backend {
     }
   }
 
+  // Host-coherent corrupt-chunk record shared by every decoder launch (lazy).
+  uint64_t* decode_err() {
+    std::call_once(dec_err_once_, [this] {
+      void* p = nullptr;
+      if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable) == hipSuccess) {
+        memset(p, 0, 64);
+        dec_err_ = (uint64_t*)p;
+      }
+    });
+    return dec_err_;
+  }
+
   int ndev_;
+  std::once_flag dec_err_once_;
+  uint64_t* dec_err_ = nullptr;
   std::string last_err_;
   std::mutex ev_m_, df_m_, reg_m_;
   std::map<uint64_t, uint64_t> regs_;  // host registrations: base -> bytes

@@ -58,7 +58,7 @@ Loc Runtime::demotion_target(const Loc& from) {
   return Loc{Tier::HOST, -1};  // nowhere to go
 }
 
-Status Runtime::alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* first) {
+Status Runtime::alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* first, Block* owner, bool pin) {
   if (a->loc().is_gpu()) {
     int64_t left = inject_.alloc_fail_after.load();
     if (left == 0) {
@@ -70,7 +70,7 @@ Status Runtime::alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* 
     Tools::get().inc(Counter::InjectedErrors);
     return Status::INJECTED_ERROR;
   }
-  Status st = a->alloc(n, nullptr, hint, first);
+  Status st = a->alloc(n, owner, hint, first, pin);
   if (st == Status::OK && !a->loc().is_gpu()) {
     st = static_cast<HostArena*>(a)->ensure_registered(*first, n);
     if (st != Status::OK) a->free(*first, n);
@@ -79,7 +79,7 @@ Status Runtime::alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* 
 }
 
 // Reserve n contiguous chunks, evicting victims (no block lock may be held).
-Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r) {
+Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool pin) {
   if (a->loc().is_gpu() && !config().global_oversubscription) return Status::NO_MEMORY;
   if (a->loc().is_gpu() && inject_.alloc_fail_after.load() == 0) {
     Tools::get().inc(Counter::InjectedErrors);
@@ -101,7 +101,7 @@ Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r) {
       return st;
     }
   }
-  a->commit(*r);
+  a->commit(*r, pin);
   Tools::get().inc(Counter::AllocRetries);
   return Status::OK;
 }
@@ -127,14 +127,13 @@ Status Runtime::populate(Ctx& c, Block* b, Loc dst, int64_t hint, Residency** ou
   ChunkArena* a = arena_for(dst);
   if (!a) return Status::INVALID_ARGUMENT;
   uint32_t chunk = 0;
-  Status st = alloc_chunks(a, 1, hint, &chunk);
+  Status st = alloc_chunks(a, 1, hint, &chunk, b);
   if (st == Status::NO_MEMORY) {
     c.need_arena = a;
     c.need_n = 1;
     return Status::MORE_PROCESSING_REQUIRED;
   }
   if (st != Status::OK) return st;
-  a->set_owner(chunk, b);
   Residency& r = b->get_or_add(dst);
   r.arena = a;
   r.chunk = chunk;
@@ -189,7 +188,7 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
   }
   // The writer waits for readers of the destination chunk's previous contents
   // and for pending writes into this block issued on other rings.
-  Tracker reuse = to->arena->take_reuse_fence((uint32_t)to->chunk);
+  Tracker reuse = to->arena->reuse_fence((uint32_t)to->chunk);
   Tracker pend = b->tracker;
   pend.prune();
   if (!ring) {
@@ -269,7 +268,7 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
 static Status zero_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* to, const PageMask& pages) {
   if (pages.empty()) return Status::OK;
   if (!to->loc.is_gpu()) {
-    Tracker reuse = to->arena->take_reuse_fence((uint32_t)to->chunk);
+    Tracker reuse = to->arena->reuse_fence((uint32_t)to->chunk);
     reuse.wait();
     pages.for_each_run([&](uint32_t p, uint32_t n) {
       memset((void*)page_addr(to->arena, to->chunk, p), 0, (uint64_t)n << kPageShift);
@@ -277,7 +276,14 @@ static Status zero_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* to, 
     return Status::OK;
   }
   Ring* ring = rt->ring(to->loc.id, RingKind::CPU_TO_GPU);
-  Tracker reuse = to->arena->take_reuse_fence((uint32_t)to->chunk);
+  if (log_level() >= LogLevel::DEBUG) {
+    std::string where;
+    for (auto& x : b->res) where += " " + x.loc.str() + ":" + std::to_string(x.resident.count());
+    RT_DBG("GPU zero-fill: range %llu '%s' block %llu pages %u (first %u) residencies%s",
+           (unsigned long long)b->range->id, b->range->name.c_str(), (unsigned long long)b->index, pages.count(),
+           pages.next_set(0), where.c_str());
+  }
+  Tracker reuse = to->arena->reuse_fence((uint32_t)to->chunk);
   for (auto& f : reuse.fences()) {
     if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
     Sqe w;
@@ -490,14 +496,15 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
     if (f) t.block->tracker.add(f);
     if (t.block->unpublished) t.block->unpublished--;
   }
-  for (auto& u : c.chunk_uses) {
-    FenceRef f = fence_of(u.ring);
-    if (f) u.arena->add_reuse_fence(u.chunk, f);
+  // Every reader's fence lands on its chunk before any chunk is freed: a chunk
+  // read on two rings must not be handed out between the two fences.
+  for (auto& u : c.chunk_uses)
+    if (FenceRef f = fence_of(u.ring)) u.arena->add_reuse_fence(u.chunk, f);
+  for (auto& u : c.chunk_uses)
     if (u.free_after) {
       u.arena->unpin(u.chunk);
       u.arena->free(u.chunk, 1);
     }
-  }
   for (auto& iv : c.invals) {
     bool bad = false;
     for (auto& t : c.touched)
@@ -784,13 +791,17 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
     if (in_place) first = c0;
   }
   if (!in_place) {
+    // The fresh extent stays pinned until the end of this call: its chunks have
+    // no owner until each block takes its chunk, and an unpinned owner-less
+    // chunk is a free eviction victim for a concurrent reserve() (two blocks
+    // would end up sharing one HBM chunk).
     uint32_t f = 0;
-    st = alloc_chunks(ga, n, -1, &f);
+    st = alloc_chunks(ga, n, -1, &f, nullptr, true);
     if (st == Status::OK) {
       first = f;
     } else if (st == Status::NO_MEMORY) {
       Reservation rv;
-      st = ensure_capacity(ga, n, &rv);
+      st = ensure_capacity(ga, n, &rv, true);
       first = rv.first;
     }
     if (st != Status::OK) return st;
@@ -869,15 +880,17 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
       c.need_arena = nullptr;
     }
   }
-  // Chunks of the extent that were never handed to a block (error path) go back.
-  if (st != Status::OK && !in_place) {
-    for (uint32_t k = 0; k < n; ++k) {
-      Block* b = r->block(b0 + k);
-      bool used = false;
-      for (Block* d : done)
-        if (d == b) used = true;
-      if (!used && ga->owner((uint32_t)(first + k)) == nullptr) ga->free((uint32_t)(first + k), 1);
-    }
+  if (!in_place) {
+    for (uint32_t k = 0; k < n; ++k) ga->unpin((uint32_t)(first + k));
+    // Chunks of the extent that were never handed to a block (error path) go back.
+    if (st != Status::OK)
+      for (uint32_t k = 0; k < n; ++k) {
+        Block* b = r->block(b0 + k);
+        bool used = false;
+        for (Block* d : done)
+          if (d == b) used = true;
+        if (!used && ga->owner((uint32_t)(first + k)) == nullptr) ga->free((uint32_t)(first + k), 1);
+      }
   }
   Status fs = finish_ctx(c, out);
   if (st == Status::OK) st = fs;

@@ -477,7 +477,7 @@ Status Runtime::write_compressed(Range* r, uint64_t off, const void* src, uint64
   if (src_dev >= 0) {
     stage = host_arena(Tier::HOST, host_node_);
     if (!stage) return Status::NO_MEMORY;
-    Status st = alloc_chunks(stage, (uint32_t)std::min<uint64_t>(batch, nb), -1, &stage_first);
+    Status st = alloc_chunks(stage, (uint32_t)std::min<uint64_t>(batch, nb), -1, &stage_first, nullptr, true);
     if (st != Status::OK) return st;
   }
   Status result = Status::OK;
@@ -516,7 +516,7 @@ Status Runtime::write_compressed(Range* r, uint64_t off, const void* src, uint64
           st = populate(c, b, d, -1, &dst[k]);
           if (st == Status::OK) {
             b->tracker.wait();
-            Tracker rf = dst[k]->arena->take_reuse_fence((uint32_t)dst[k]->chunk);
+            Tracker rf = dst[k]->arena->reuse_fence((uint32_t)dst[k]->chunk);
             rf.wait();
           }
         }
@@ -638,7 +638,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
           if (src_dev < 0) {
             Tracker t = b->tracker;
             t.wait();
-            Tracker rf = to->arena->take_reuse_fence((uint32_t)to->chunk);
+            Tracker rf = to->arena->reuse_fence((uint32_t)to->chunk);
             rf.wait();
             memcpy((void*)dst_addr, s, end - pos);
           } else {
@@ -646,7 +646,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
             Ring* rg = stage.is_gpu() ? (stage.id == src_dev ? ring(src_dev, RingKind::GPU_INTERNAL)
                                                             : ring(src_dev, RingKind::GPU_TO_GPU))
                                       : ring(src_dev, RingKind::GPU_TO_CPU);
-            Tracker rf = to->arena->take_reuse_fence((uint32_t)to->chunk);
+            Tracker rf = to->arena->reuse_fence((uint32_t)to->chunk);
             rf.merge(b->tracker);
             for (auto& f : rf.fences()) {
               Sqe w;
@@ -714,7 +714,7 @@ Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_
     if (encoded) {
       scratch_arena = host_arena(Tier::HOST, host_node_);
       uint32_t tmp;
-      Status st = scratch_arena ? alloc_chunks(scratch_arena, 1, -1, &tmp) : Status::NO_MEMORY;
+      Status st = scratch_arena ? alloc_chunks(scratch_arena, 1, -1, &tmp, nullptr, true) : Status::NO_MEMORY;
       if (st != Status::OK) return st;
       decoded = *encoded;
       decoded.arena = scratch_arena;
@@ -765,7 +765,7 @@ Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_
           // GPU -> pageable host: bounce through a pinned host chunk.
           HostArena* ha = host_arena(Tier::HOST, host_node_);
           uint32_t tmp;
-          Status st = ha ? alloc_chunks(ha, 1, -1, &tmp) : Status::NO_MEMORY;
+          Status st = ha ? alloc_chunks(ha, 1, -1, &tmp, nullptr, true) : Status::NO_MEMORY;
           if (st != Status::OK) return st;
           rg = ring(d, RingKind::GPU_TO_CPU);
           Sqe s;

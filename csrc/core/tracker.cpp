@@ -23,8 +23,16 @@ bool Fence::query() {
 Status Fence::wait() {
   if (done.load(std::memory_order_acquire)) return Status::OK;
   Status s = Status::OK;
+  uint64_t t0 = now_ns();
   if (be && event) s = be->event_sync(event);
+  uint64_t t1 = now_ns();
   if (s == Status::OK && ring) s = ring->wait_seq(seq);
+  uint64_t t2 = now_ns();
+  if (t2 - t0 > 1000000000ull)
+    RT_WARN("slow fence wait: event_sync %.1f ms, ring wait %.1f ms (ring %s/%d seq %llu completed %llu submitted %llu)",
+            (t1 - t0) / 1e6, (t2 - t1) / 1e6, ring ? ring_kind_str(ring->kind()) : "-", ring ? ring->dev() : -1,
+            (unsigned long long)seq, (unsigned long long)(ring ? ring->completed_seq() : 0),
+            (unsigned long long)(ring ? ring->submitted_seq() : 0));
   if (s == Status::OK) done.store(true, std::memory_order_release);
   return s;
 }
@@ -89,8 +97,17 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
   for (auto& f : fences_) {
     if (f->done.load(std::memory_order_relaxed)) continue;
     Status s;
+    uint64_t t0 = now_ns();
+    bool had_event = f->event != nullptr;
+    bool ev_done = had_event && be->event_query(f->event);
     if (f->event) s = be->stream_wait_event(stream, f->event);
     else s = f->wait();
+    uint64_t dt = now_ns() - t0;
+    if (dt > 20000000ull)  // a GPU-side dependency should cost microseconds of host time
+      RT_WARN("slow gpu_wait: %.1f ms event=%d event_done=%d ring=%s seq=%llu completed=%llu submitted=%llu",
+              dt / 1e6, (int)had_event, (int)ev_done, f->ring ? ring_kind_str(f->ring->kind()) : "-",
+              (unsigned long long)f->seq, (unsigned long long)(f->ring ? f->ring->completed_seq() : 0),
+              (unsigned long long)(f->ring ? f->ring->submitted_seq() : 0));
     if (s != Status::OK) return s;
   }
   return Status::OK;

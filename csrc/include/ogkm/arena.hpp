@@ -66,10 +66,12 @@ class ChunkArena {
   int64_t chunk_of(uint64_t addr) const;
 
   // Contiguous allocation of n chunks without eviction. `hint` = preferred first chunk.
-  Status alloc(uint32_t n, Block* owner_for_all, int64_t hint, uint32_t* first);
+  // `pin`: the chunks come back pinned (never eviction victims) so a caller that
+  // hands them to their owners later cannot lose them to a concurrent reserve().
+  Status alloc(uint32_t n, Block* owner_for_all, int64_t hint, uint32_t* first, bool pin = false);
   // Reserve a window of n contiguous chunks, possibly containing evictable chunks.
   Status reserve(uint32_t n, Reservation* r);
-  void commit(const Reservation& r);                // window -> ALLOCATED (owners set later)
+  void commit(const Reservation& r, bool pin = false);  // window -> ALLOCATED (owners set later)
   void cancel(const Reservation& r);                // give the window back
   void free(uint32_t first, uint32_t n);
   void set_owner(uint32_t i, Block* b);
@@ -88,7 +90,7 @@ class ChunkArena {
   void unpin(uint32_t i);
   bool pinned(uint32_t i);
   void add_reuse_fence(uint32_t i, const FenceRef& f);
-  Tracker take_reuse_fence(uint32_t i);             // moves the fence out (for the next writer)
+  Tracker reuse_fence(uint32_t i);                  // what the next writer must wait for (not consumed)
 
   struct Stats {
     uint64_t capacity = 0, allocated = 0, peak = 0, pinned = 0, evictions = 0, allocs = 0, frees = 0,

@@ -106,6 +106,13 @@ class Backend {
                                    uint64_t n_values, void* stream, uint32_t workgroups, uint64_t dst_stride = 0) {
     return unpack_bf12_stream(dev, src, dst, nchunks, chunk_values, n_values, stream, workgroups, dst_stride);
   }
+  // Corrupt packed chunks seen by the device decoders since the last reset:
+  // out = {count, stream address, chunk index, detail}. Decoders zero-fill such
+  // chunks and report them here instead of decoding garbage.
+  virtual void decode_errors(uint64_t out[4], bool reset) {
+    for (int i = 0; i < 4; ++i) out[i] = 0;
+    (void)reset;
+  }
   // Decode GEMM (ogkm/dgemm.hpp): split-K partials, then the fused epilogue.
   virtual Status dgemm(int dev, const DGemmArgs& a, int mode, void* stream) = 0;
   virtual Status dgemm_reduce(int dev, const DGemmReduceArgs& a, void* stream) = 0;

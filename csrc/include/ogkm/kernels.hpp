@@ -58,8 +58,9 @@ hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, u
                               uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0);
 // Unpack an ANS stream (ANS1 or raw chunks, codec.hpp) in device memory into
 // bf16 (csrc/kernels/ans_kernels.hip): one wave per 32 Ki-value rANS segment.
+// err: optional host-coherent {count, stream, chunk, freq sum} record of corrupt chunks.
 hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
-                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0);
+                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0, uint64_t* err = nullptr);
 
 // Decode GEMM (csrc/kernels/decode_gemm.hip); argument structs in ogkm/dgemm.hpp.
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);

@@ -224,8 +224,10 @@ class Runtime {
   Status make_resident(Ctx& c, Block* b, const PageMask& pages, Loc dst, bool read_dup, Cause cause);
   Status populate(Ctx& c, Block* b, Loc dst, int64_t chunk_hint, Residency** out);
   Status evict_chunk(ChunkArena* a, uint32_t chunk);
-  Status ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r);
-  Status alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* first);
+  Status ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool pin = false);
+  // owner / pin are applied atomically with the allocation (see ChunkArena::alloc).
+  Status alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* first, Block* owner = nullptr,
+                      bool pin = false);
   Loc demotion_target(const Loc& from);
   void cpu_map_block(Block* b);  // refresh CPU view protections
   void stable_map_block(Block* b);

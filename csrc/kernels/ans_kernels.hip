@@ -40,9 +40,13 @@ __device__ __forceinline__ uint32_t ans_bperm(uint32_t lane, uint32_t v) {
 
 }  // namespace
 
+// err (host-coherent, may be null): {count, stream, chunk, freq sum} of corrupt
+// ANS chunks - a frequency table that does not sum to 2^kAnsPrecBits (data that
+// is not a valid stream: a race or a wrong pointer upstream). Such a chunk is
+// zero-filled and reported instead of being decoded.
 __global__ void __launch_bounds__(kAnsThreads)
     k_ans_unpack(const uint8_t* __restrict__ stream, uint16_t* __restrict__ out, uint64_t dst_stride,
-                 uint32_t items_per_chunk, uint64_t total_items) {
+                 uint32_t items_per_chunk, uint64_t total_items, uint64_t* __restrict__ err) {
   __shared__ uint32_t tab[kAnsSlots];
   __shared__ uint32_t cum[257];
   __shared__ uint32_t wsum[kAnsSegsPerItem];
@@ -84,6 +88,19 @@ __global__ void __launch_bounds__(kAnsThreads)
     cum[threadIdx.x + 1] = s + add;
     if (threadIdx.x == 0) cum[0] = 0;
     __syncthreads();
+    if (cum[256] != kAnsSlots) {  // not an ANS chunk: report + zero-fill (workgroup-uniform)
+      if (threadIdx.x == 0 && err) {
+        if (__hip_atomic_fetch_add(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+          __hip_atomic_store(err + 1, (uint64_t)stream, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(err + 2, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(err + 3, (uint64_t)cum[256], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      const uint32_t v_hi = ch.n_values - v_lo < kAnsSegsPerItem * kAnsSegValues
+                                ? ch.n_values : v_lo + kAnsSegsPerItem * kAnsSegValues;
+      for (uint32_t k = v_lo + threadIdx.x; k < v_hi; k += kAnsThreads) dst[k] = 0;
+      continue;
+    }
     {  // decode table: thread t fills slots [16 t, 16 t + 16)
       const uint32_t k0 = threadIdx.x * (kAnsSlots / kAnsThreads);
       uint32_t lo = 0, hi = 256;
@@ -93,7 +110,7 @@ __global__ void __launch_bounds__(kAnsThreads)
       }
       uint32_t sym = lo;
       for (uint32_t k = k0; k < k0 + kAnsSlots / kAnsThreads; ++k) {
-        while (cum[sym + 1] <= k) ++sym;
+        while (sym < 255u && cum[sym + 1] <= k) ++sym;
         tab[k] = sym | ((cum[sym + 1] - cum[sym]) << 8) | ((k - cum[sym]) << 20);
       }
     }
@@ -151,7 +168,7 @@ __global__ void __launch_bounds__(kAnsThreads)
 }
 
 hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
-                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride) {
+                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride, uint64_t* err) {
   if (nchunks == 0) return hipSuccess;
   if (chunk_values < 8192 || (chunk_values & (chunk_values - 1)) || chunk_values > (1u << 20))
     return hipErrorInvalidValue;
@@ -160,7 +177,7 @@ hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, ui
   const uint64_t total = (uint64_t)nchunks * per_chunk;
   const uint64_t grid = workgroups && workgroups < total ? workgroups : total;
   hipLaunchKernelGGL(k_ans_unpack, dim3((uint32_t)grid), dim3(kAnsThreads), 0, s, (const uint8_t*)stream,
-                     (uint16_t*)dst, dst_stride ? dst_stride : (uint64_t)chunk_values, per_chunk, total);
+                     (uint16_t*)dst, dst_stride ? dst_stride : (uint64_t)chunk_values, per_chunk, total, err);
   return hipGetLastError();
 }
 

@@ -281,15 +281,17 @@ PYBIND11_MODULE(_ogkm, m) {
     d["pending"] = l->ready.size();
     return d;
   });
-  m.def("lease_wait", [](uint64_t lid, uint64_t stream) {
+  // on_stream: GPU-side dependency of `stream` (0 = the null stream) on the
+  // lease's copies - the host never blocks. Otherwise the host waits.
+  m.def("lease_wait", [](uint64_t lid, uint64_t stream, bool on_stream) {
     Lease* l = rt()->lease_by_id(lid);
     if (!l) throw StatusError("unknown lease");
-    if (stream) check(l->ready.gpu_wait(rt()->be(), (void*)stream), "lease gpu_wait");
+    if (on_stream) check(l->ready.gpu_wait(rt()->be(), (void*)stream), "lease gpu_wait");
     else {
       py::gil_scoped_release nogil;
       check(l->ready.wait(), "lease wait");
     }
-  });
+  }, py::arg("lease"), py::arg("stream"), py::arg("on_stream") = false);
   m.def("release", [](uint64_t lid, uint64_t stream) {
     Lease* l = rt()->lease_by_id(lid);
     if (!l) throw StatusError("unknown lease");
@@ -615,6 +617,16 @@ PYBIND11_MODULE(_ogkm, m) {
           "ans_unpack");
   }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("nchunks"), py::arg("chunk_values"),
      py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0, py::arg("dst_stride") = 0);
+  m.def("decode_errors", [](bool reset) {
+    uint64_t e[4];
+    rt()->be()->decode_errors(e, reset);
+    py::dict d;
+    d["count"] = e[0];
+    d["stream"] = e[1];
+    d["chunk"] = e[2];
+    d["detail"] = e[3];
+    return d;
+  }, py::arg("reset") = false);
   // Decode GEMM + fused epilogue in one call: out = epi(X . W^T) (ops/dgemm.py).
   m.def("dgemm_plan", [](uint32_t N, uint32_t K, uint32_t target_units) {
     uint32_t ks, kl;

@@ -39,6 +39,9 @@ from ..ops.memory import managed_embedding
 from ..parallel import comm, tp as tpmod
 
 ALIGN = 4096
+# Diagnostics: the host waits for every streamed unit's copies (instead of a
+# GPU-side stream dependency).
+_HOST_LEASE_WAIT = os.environ.get("OGKM_HOST_LEASE_WAIT", "0") != "0"
 
 
 @dataclass(frozen=True)
@@ -387,6 +390,7 @@ class TieredLlama:
         self._inflight: list = []   # prefetched, not yet consumed
         self._views: dict = {}
         self.byte_trace = None     # diagnostics: {key: H2D bytes submitted around its use}
+        self.use_trace = None      # diagnostics: [(key, acquire s, wait s)] per streamed use
         self._pinned: dict = {}    # resident tensors: key -> weight refs (leased for the model's lifetime)
         self._pin_leases: list = []
         self.keep_logits = False   # tests: keep the full-vocab logits of the last step
@@ -629,10 +633,14 @@ class TieredLlama:
             if self._inflight and self._inflight[0] == key:
                 self._inflight.pop(0)
             self._prefetch_ahead()
+        t_a = time.perf_counter()
         lease = self._buf(key).acquire(self.dev, rt.READ)
         if acct:  # H2D bytes submitted while servicing this tensor (prefetch window + its own faults)
             self.byte_trace[key] = self.byte_trace.get(key, 0) + lib.stats()["bytes_xfer_htd"] - b0
-        lease.wait(0 if self.fake else None)
+        t_w = time.perf_counter()
+        lease.wait(0 if (self.fake or _HOST_LEASE_WAIT) else None)
+        if self.use_trace is not None:
+            self.use_trace.append((key, t_w - t_a, time.perf_counter() - t_w))
         mode = self.pmode.get(key, dgemm.MODE_RAW)
         refs = self._ref(key, lease.dptr, mode)
         if self._is_resident(key):

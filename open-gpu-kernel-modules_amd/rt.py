@@ -196,7 +196,19 @@ class Lease:
         self._released = False
 
     def wait(self, stream: Optional[int] = None) -> None:
-        lib.lease_wait(self.id, current_stream_handle(self.proc) if stream is None else stream)
+        """Make the lease's data usable. ``stream=None``: the current stream of the
+        lease's GPU waits for the migration GPU-side (the host does not block,
+        also when that is the null stream); ``stream=<handle>``: that stream
+        waits; ``stream=0``: the host waits (CPU leases, fake backend, tests)."""
+        if self.proc == CPU or lib.backend_name() == "fake":
+            lib.lease_wait(self.id, 0, False)
+        elif stream is None:
+            lib.lease_wait(self.id, current_stream_handle(self.proc), True)
+        else:
+            lib.lease_wait(self.id, int(stream), bool(stream))
+
+    def wait_host(self) -> None:
+        lib.lease_wait(self.id, 0, False)
 
     def tensor(self, shape, dtype):
         dev = "cpu" if self.proc == CPU or lib.backend_name() == "fake" else "cuda"

@@ -2,6 +2,7 @@
 // reference's in-module UVM tests: uvm_pmm_test.c, uvm_range_tree_test.c,
 // uvm_channel_test.c, uvm_lock_test.c). Built with g++ and run under
 // AddressSanitizer + UBSan and under ThreadSanitizer by tests/test_native.py.
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -248,6 +249,92 @@ static void test_runtime_end_to_end() {
   Runtime::shutdown();
 }
 
+// A chunk's reuse fence must survive its first writer: a second writer on
+// another ring (D2D relocation + H2D fill of one extent) still has to wait for
+// the previous owner's readers (round-2 corrupt-chunk bug).
+static void test_reuse_fence_not_consumed() {
+  Runtime* rt = Runtime::init("fake", 1, 64ull << 20);
+  TestArena a(8);
+  uint32_t f;
+  CHECK(a.alloc(1, nullptr, -1, &f) == Status::OK);
+  Ring* ring = rt->ring(0, RingKind::CPU_TO_GPU);
+  auto pending = std::make_shared<Fence>();
+  pending->ring = ring;
+  pending->seq = ring->pushed_seq() + 1000;  // never completes during the test
+  a.add_reuse_fence(f, pending);
+  CHECK(a.reuse_fence(f).size() == 1);
+  CHECK(a.reuse_fence(f).size() == 1);  // still there for the next writer
+  auto done = std::make_shared<Fence>();
+  done->done.store(true);
+  a.add_reuse_fence(f, done);  // completed fences are never kept
+  CHECK(a.reuse_fence(f).size() == 1);
+  a.free(f, 1);
+  Runtime::shutdown();
+}
+
+// Concurrent extent placement vs eviction on a small arena: no HBM chunk may
+// ever back two blocks (owner-less unpinned extent chunks were
+// eviction victims of a concurrent reserve()).
+static void test_no_shared_chunks_under_concurrency() {
+  Runtime* rt = Runtime::init("fake", 1, 64ull << 20);
+  lockcheck::set_enabled(true);
+  CHECK(rt->init_device(0, 24ull << 20) == Status::OK);  // 12 chunks
+  std::vector<Range*> rs;
+  for (int i = 0; i < 6; ++i) {
+    Range* r = nullptr;
+    CHECK(rt->malloc_managed(8ull << 20, 0, "c" + std::to_string(i), &r) == Status::OK);
+    std::vector<uint8_t> data(8ull << 20, (uint8_t)(0x40 + i));
+    CHECK(rt->write(r, 0, data.data(), data.size(), -1) == Status::OK);
+    rs.push_back(r);
+  }
+  std::atomic<int> bad{0}, shared{0};
+  std::atomic<bool> stop{false};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 3; ++t)
+    th.emplace_back([&, t] {
+      for (int k = 0; k < 40; ++k) {
+        const size_t idx = (t * 2 + k) % rs.size();
+        Range* r = rs[idx];
+        Lease* l = nullptr;
+        Status s = rt->acquire(r, 0, r->size, 0, Access::READ, &l);
+        if (s != Status::OK) continue;  // BUSY / NO_MEMORY under contention is fine
+        const uint8_t want = (uint8_t)(0x40 + idx);
+        if (l->ready.wait() != Status::OK) bad++;
+        else if (((uint8_t*)l->dptr)[0] != want || ((uint8_t*)l->dptr)[r->size - 1] != want)
+          bad++;
+        rt->release(l, nullptr);
+      }
+    });
+  std::thread checker([&] {
+    while (!stop.load()) {
+      std::vector<std::pair<ChunkArena*, int64_t>> seen;
+      for (Range* r : rs)
+        for (auto& bp : r->blocks) {
+          std::lock_guard<OrderedMutex> g(bp->lock);
+          for (auto& x : bp->res)
+            if (x.loc.is_gpu() && x.chunk >= 0) seen.emplace_back(x.arena, x.chunk);
+        }
+      std::sort(seen.begin(), seen.end());
+      if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) shared++;
+      std::this_thread::yield();
+    }
+  });
+  for (auto& x : th) x.join();
+  stop.store(true);
+  checker.join();
+  CHECK(bad.load() == 0);
+  CHECK(shared.load() == 0);
+  CHECK(rt->dev(0).hbm->check().empty());
+  for (int i = 0; i < (int)rs.size(); ++i) {
+    std::vector<uint8_t> back(rs[i]->size);
+    CHECK(rt->read(rs[i], 0, back.data(), back.size(), -1) == Status::OK);
+    CHECK(back.front() == (uint8_t)(0x40 + i) && back.back() == (uint8_t)(0x40 + i));
+  }
+  for (Range* r : rs) CHECK(rt->free_range(r) == Status::OK);
+  CHECK(lockcheck::violations() == 0);
+  Runtime::shutdown();
+}
+
 int main() {
   RUN(test_pagemask);
   RUN(test_arena_alloc_reserve);
@@ -256,6 +343,8 @@ int main() {
   RUN(test_codec_bf11);
   RUN(test_lockcheck);
   RUN(test_runtime_end_to_end);
+  RUN(test_reuse_fence_not_consumed);
+  RUN(test_no_shared_chunks_under_concurrency);
   if (g_fail) {
     fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

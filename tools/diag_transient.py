@@ -24,7 +24,26 @@ def main():
     ap.add_argument("--simulate-tp", type=int, default=1)
     ap.add_argument("--tiers", default="host")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--weights", default="ans")
+    ap.add_argument("--verify", action="store_true", help="checksum every unpacked unit against its host copy")
+    ap.add_argument("--kv-format", default="ans")
+    ap.add_argument("--dump-every", type=float, default=0.0,
+                    help="dump every thread's Python stack every N s while a step runs (finds where a stall waits)")
+    ap.add_argument("--dump-file", default="gpurun_out/stall_stacks.txt")
     a = ap.parse_args()
+    import faulthandler
+    import gc
+
+    gc_t = {}
+
+    def gc_cb(phase, info):  # a long cyclic-GC pause (finalizers) would show up here
+        if phase == "start":
+            gc_t["t"] = time.perf_counter()
+        else:
+            dt = time.perf_counter() - gc_t.get("t", time.perf_counter())
+            if dt > 0.01:
+                print(f"  gc gen{info['generation']} took {dt * 1e3:.1f} ms", flush=True)
+    gc.callbacks.append(gc_cb)
     import importlib
 
     import torch
@@ -42,20 +61,71 @@ def main():
         lib.cxl_rediscover(other[0], "/sys")
     cfg = llama.CONFIGS[a.model]
     m = llama.TieredLlama(cfg, batch=64, context=1024, max_new_tokens=a.steps + 3, oversub=2.0, device=0,
-                          tp_rank=0, tp_world=a.simulate_tp, seed=1234, lookahead=1, weight_format="ans",
-                          tiers=a.tiers, kv_format="ans")
+                          tp_rank=0, tp_world=a.simulate_tp, seed=1234, lookahead=1, weight_format=a.weights,
+                          tiers=a.tiers, kv_format=a.kv_format)
     tok = torch.randint(0, cfg.vocab, (64,)).cuda()
+    unstaged = {}  # packed stream address -> unit (this step)
+    orig_unstage = m._unstage
+    ref_sum, seen = {}, []
+    if a.verify:
+        # checksum of every unit's packed stream as stored on the host
+        for key in m.order:
+            n = m.pinfo[key].nbytes // 4 * 4
+            ref_sum[key] = int(m._buf(key).read(nbytes=n).view(torch.int32).sum(dtype=torch.int64))
+        print(f"reference checksums of {len(ref_sum)} units", flush=True)
+
+    def unstage(key, ptr):
+        unstaged[ptr] = key
+        if a.verify:  # checksum of what the unpack is about to read, in stream order (no host sync)
+            n = m.pinfo[key].nbytes // 4 * 4
+            v = rt._tensor_from_ptr(ptr, (n // 4,), torch.int32, "cuda", 0)
+            seen.append((key, ptr, v.sum(dtype=torch.int64)))
+        return orig_unstage(key, ptr)
+    m._unstage = unstage
     for i in range(a.steps):
         s0 = lib.stats()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        if a.dump_every > 0:
+            dump = open(a.dump_file, "a")
+            dump.write(f"==== step {i}\n")
+            dump.flush()
+            faulthandler.dump_traceback_later(a.dump_every, repeat=True, file=dump)
+        m.use_trace = []
+        unstaged.clear()
         tok = m.step(tok)
+        t_enq = time.perf_counter() - t0
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if a.dump_every > 0:
+            faulthandler.cancel_dump_traceback_later()
+            dump.close()
+        print(f"step {i}: host enqueue {t_enq * 1e3:.1f} ms", flush=True)
+        slow = sorted(m.use_trace, key=lambda u: -(u[1] + u[2]))[:8]
+        print("  slowest uses (key, acquire ms, wait ms):",
+              [(u[0], round(u[1] * 1e3, 1), round(u[2] * 1e3, 1)) for u in slow], flush=True)
         s1 = lib.stats()
         d = {k: s1[k] - s0[k] for k in KEYS if k in s1}
         gb = {k: round(v / 1e9, 2) if "bytes" in k else v for k, v in d.items()}
         print(f"step {i}: {dt * 1e3:.1f} ms {gb}", flush=True)
+        if a.verify:
+            bad = [(k, p, int(t)) for k, p, t in seen if int(t) != ref_sum[k]]
+            print(f"  verify: {len(seen)} unpacks, {len(bad)} saw wrong packed bytes", flush=True)
+            for k, p, t in bad[:6]:
+                n = m.pinfo[k].nbytes // 4 * 4
+                now = int(rt._tensor_from_ptr(p, (n // 4,), torch.int32, "cuda", 0).sum(dtype=torch.int64))
+                res = [m._buf(k).residency(o) for o in range(0, m._buf(k).size, 2 << 20)]
+                gpu_pages = [sum(r["pages"] for r in x["resident_on"] if r["tier"] == "gpu") for x in res]
+                print(f"    {k} ptr {p:#x} saw {t} ref {ref_sum[k]} now {now} (fixed later: {now == ref_sum[k]}) "
+                      f"gpu pages/block {gpu_pages}", flush=True)
+            seen.clear()
+        err = lib.decode_errors(True)
+        if err["count"]:
+            where = [f"kv layer {j}" for j in range(cfg.n_layers)
+                     if m.kv_lease.dptr + j * m.kv_slot == err["stream"]] if m.kv_format != "bf16" else []
+            where += [unstaged.get(err["stream"], "?")]
+            print(f"  CORRUPT packed chunks: {err['count']} first stream {err['stream']:#x} chunk {err['chunk']} "
+                  f"freq sum {err['detail']} {where}", flush=True)
 
 
 if __name__ == "__main__":
