@@ -10,9 +10,15 @@ available offline), synthetic prefilled KV cache of ``--context`` tokens, greedy
 decode of ``--batch`` sequences. Every weight and the KV cache are runtime-managed;
 the per-GPU HBM arena is capped at (managed footprint / oversub), so half the
 model lives in host DRAM and streams through the migration ring every step.
-With N GPUs the model is tensor-parallel over N ranks (one process per GPU,
-RCCL over xGMI): the global batch is fixed (strong scaling) and each rank
-streams only its shard over its own PCIe link.
+With N GPUs (one process per GPU, RCCL over xGMI; each process's runtime
+manages only its own GPU and rests its host tier on that GPU's NUMA node) the
+global batch is fixed (strong scaling) and ``--parallel`` picks how the model is
+split:
+  * ``tp`` (default): Megatron tensor parallelism - each rank streams only its
+    1/N of every layer over its own PCIe link, 2 all-reduces per layer;
+  * ``shards`` (config 4, peermem-style P2P shards): each rank owns 1/N of every
+    unit (preferred on its GPU / streamed from its host DRAM), units are
+    all-gathered over xGMI before use, each rank decodes B/N sequences.
 
 One step = one decode token for every sequence (weights streamed, KV appended,
 greedy sampling). ``value`` = global tokens/s = batch * K / max-over-ranks time.
@@ -73,6 +79,13 @@ def parse():
     ap.add_argument("--simulate-tp", type=int, default=0,
                     help="single-process run of TP rank 0 of N (per-GPU shard of an N-GPU job; collectives "
                          "skipped, numerics not meaningful) - for configs larger than the box, e.g. 405B tp8")
+    ap.add_argument("--parallel", choices=("tp", "shards"), default="tp",
+                    help="multi-GPU split: tensor parallel, or peer-shard weights all-gathered over xGMI")
+    ap.add_argument("--backend", choices=("hip", "fake"), default="hip",
+                    help="fake: CPU-only runtime (fake GPUs, gloo) - rehearses the multi-rank path without a GPU")
+    ap.add_argument("--fake-hbm-mb", type=int, default=1024)
+    ap.add_argument("--dump-logits", default="",
+                    help="write the last step's logits [global batch, vocab] (fp32) to this file (rank 0)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -153,15 +166,25 @@ def main() -> None:
     from ogkm.models import llama
     from ogkm.parallel import comm
 
-    e = comm.init()
+    fake = a.backend == "fake"
+    e = comm.init("gloo" if fake else None)
     if e.world != a.gpus and e.world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={e.world}")
     dev = e.local_rank
-    torch.cuda.set_device(dev)
+    if not fake:
+        torch.cuda.set_device(dev)
     world = e.world
     cfg = llama.CONFIGS[a.model]
-    # The emulated CXL pool: the NUMA node that is not the GPU's (a remote memory node).
-    rt.init("hip", host_budget_mb=0)
+    # One process per GPU: this runtime manages only its own GPU (rings, fault
+    # buffer and HBM arena on no other device), and its host tier sits on that
+    # GPU's NUMA node.
+    if fake:
+        rt.init("fake", fake_devices=max(world, 1), fake_hbm_mb=a.fake_hbm_mb, host_budget_mb=4096,
+                local_devices=1 << dev, fake_numa_nodes=2 if world > 1 else 1)
+        a.no_aux = True
+    else:
+        rt.init("hip", host_budget_mb=0, local_devices=1 << dev)
+    # The emulated CXL pool: a NUMA node that is not this GPU's (a remote memory node).
     gpu_node = lib.device_numa_node(dev)
     nodes = sorted({int(p.name[4:]) for p in Path("/sys/devices/system/node").glob("node[0-9]*")})
     other = [n for n in nodes if n != gpu_node]
@@ -176,32 +199,45 @@ def main() -> None:
     model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 3,
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
                               seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
-                              weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac, kv_format=a.kv_format)
+                              weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac, kv_format=a.kv_format,
+                              parallel=a.parallel)
     plan = model.describe()
     init_s = time.perf_counter() - t_init
     g = torch.Generator(device="cpu").manual_seed(42)
-    tok = torch.randint(0, cfg.vocab, (a.batch,), generator=g).to(f"cuda:{dev}")
+    tok = torch.randint(0, cfg.vocab, (a.batch,), generator=g)
+    tok = tok[model.b0:model.b0 + model.B]  # shards: this rank's sequences (tp: all of them)
+    if not fake:
+        tok = tok.to(f"cuda:{dev}")
+    if a.dump_logits:
+        model.keep_logits = True
+
+    def sync():
+        if not fake:
+            torch.cuda.synchronize()
     for _ in range(a.warmup):
         tok = model.step(tok)
     lib.reset_counters()
     if a.verbose:
         model.byte_trace = {}
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         tok = model.step(tok)
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
     s = lib.stats()
+    host_nodes = comm.all_gather_objects(lib.host_node())
+    if a.dump_logits and e.rank == 0:
+        torch.save(model.last_logits.float().cpu(), a.dump_logits)
     if a.verbose:
         # host enqueue time of one step (no sync inside) vs its synchronized time
-        torch.cuda.synchronize()
+        sync()
         h0 = time.perf_counter()
         tok = model.step(tok)
         h1 = time.perf_counter()
-        torch.cuda.synchronize()
+        sync()
         h2 = time.perf_counter()
         if e.rank == 0:
             print(f"[ogkm] one step: host enqueue {1e3 * (h1 - h0):.1f} ms, synchronized {1e3 * (h2 - h0):.1f} ms",
@@ -217,8 +253,11 @@ def main() -> None:
     if e.rank == 0:
         name = {"llama3-70b": "Llama-3-70B", "llama3-405b": "Llama-3-405B", "llama3-8b": "Llama-3-8B"}.get(a.model,
                                                                                                         a.model)
+        metric = f"tokens/sec {name} {a.oversub:g}x oversubscribe"
+        if sim:  # one shard of an N-GPU job on one GPU: an upper bound, not a measured N-GPU rate
+            metric += f" (tp{a.simulate_tp} rank-0 shard simulated on 1 GPU, collectives skipped)"
         out = {
-            "metric": f"tokens/sec {name} {a.oversub:g}x oversubscribe",
+            "metric": metric,
             "value": round(value, 3),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -234,12 +273,18 @@ def main() -> None:
                 "model": a.model,
                 "global_batch": a.batch,
                 "seq_len": a.context,
-                "parallelism": f"tp{a.simulate_tp}-rank0-simulated" if sim else f"tp{world}",
+                "parallelism": (f"tp{a.simulate_tp}-rank0-simulated" if sim
+                                else f"{'shards' if a.parallel == 'shards' else 'tp'}{world}"),
+                "backend": a.backend,
+                "rank_host_numa_nodes": host_nodes,
                 "tiers": plan["tiers"],
                 "kv_format": plan["kv_format"],
                 "kv_resident_gb_per_gpu": round(plan["kv_resident_gb"], 2),
                 "cxl_streamed_gb_per_step_per_gpu": round(plan["cxl_streamed_gb_per_step"], 2),
                 "oversubscription": round(plan["oversubscription"], 3),
+                # resting (packed) bytes of every managed range / HBM budget: the
+                # physical oversubscription, vs the logical bf16 one above
+                "physical_oversubscription": round(plan["physical_oversubscription"], 3),
                 "hbm_budget_gb_per_gpu": round(plan["hbm_budget_gb"], 2),
                 "managed_footprint_gb_per_gpu": round(plan["footprint_gb"], 2),
                 "resident_layers": plan["resident_layers"],

@@ -18,6 +18,7 @@
 #include <thread>
 
 #include "ogkm/backend.hpp"
+#include "ogkm/config.hpp"
 #include "ogkm/codec.hpp"
 
 namespace ogkm {
@@ -93,7 +94,13 @@ class FakeBackend : public Backend {
   const char* name() const override { return "fake"; }
   bool is_fake() const override { return true; }
   int device_count() override { return ndev_; }
-  int device_numa_node(int) override { return 0; }
+  // Like a two-socket node: GPUs 0..n/2-1 on node 0, the rest on node 1 (with
+  // fake_numa_nodes = 2), so per-rank host-tier placement is testable on a CPU.
+  int device_numa_node(int d) override {
+    int64_t nodes = config().fake_numa_nodes;
+    if (nodes <= 1 || ndev_ <= 0 || d < 0) return 0;
+    return (int)((int64_t)d * nodes / ndev_);
+  }
   Status device_mem_info(int dev, size_t* f, size_t* t) override {
     if (dev < 0 || dev >= ndev_) return Status::INVALID_ARGUMENT;
     *t = hbm_;

@@ -154,6 +154,8 @@ void set_fatal(Status s, const char* why) {
 
 void clear_fatal_for_test() { g_status.store(0); }
 
+const char* fatal_reason() { return global_status() == Status::OK ? "" : g_fatal_why; }
+
 void assert_fail(const char* cond, const char* file, int line, bool release) {
   log_msg(LogLevel::ERROR, file, line, "assertion failed: %s", cond);
   if (release && config().release_asserts) set_fatal(Status::FATAL, cond);

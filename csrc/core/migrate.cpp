@@ -147,7 +147,8 @@ static Ring* ring_for(Runtime* rt, const Loc& s, const Loc& d) {
   if (s.is_gpu() && !d.is_gpu()) return rt->ring(s.id, RingKind::GPU_TO_CPU);
   if (s.is_gpu() && d.is_gpu()) return s.id == d.id ? rt->ring(s.id, RingKind::GPU_INTERNAL)
                                                     : rt->ring(s.id, RingKind::GPU_TO_GPU);
-  if (config().block_cpu_to_cpu_copy_with_ce && rt->ndev() > 0) return rt->ring(0, RingKind::CPU_TO_GPU);
+  if (config().block_cpu_to_cpu_copy_with_ce)
+    for (int d : rt->local_devices()) return rt->ring(d, RingKind::CPU_TO_GPU);
   return nullptr;
 }
 
@@ -918,7 +919,7 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
   if (global_status() != Status::OK) return global_status();
   if (quiesced_.load()) return Status::BUSY;
   if (!r || len == 0 || off + len > r->size) return Status::INVALID_ARGUMENT;
-  if (proc != kCpuProc && (proc < 0 || proc >= ndev())) return Status::INVALID_ARGUMENT;
+  if (proc != kCpuProc && !is_local(proc)) return Status::INVALID_ARGUMENT;
   auto L = std::make_unique<Lease>();
   L->range = r;
   L->offset = off;
@@ -1302,7 +1303,7 @@ Status Runtime::cpu_fault(uint64_t addr, bool write) {
 
 // ------------------------------------------------------------------ device faults
 size_t Runtime::poll_device_faults(int dev) {
-  if (dev < 0 || dev >= ndev()) return 0;
+  if (!is_local(dev)) return 0;
   DeviceFaultBuffer& fb = devs_[dev]->fault_buf;
   if (!fb.put) return 0;
   static std::mutex poll_m;  // the service thread and API callers drain one at a time

@@ -34,7 +34,15 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
   }
   Config& cfg = config();
   int nd = rt->be_->device_count();
-  rt->host_node_ = cfg.host_node >= 0 ? (int)cfg.host_node : (nd > 0 ? rt->be_->device_numa_node(0) : 0);
+  const uint64_t mask = (uint64_t)cfg.local_devices;
+  auto local = [&](int d) { return mask == 0 || ((mask >> d) & 1); };
+  // Host tier = the NUMA node of this process's (first) GPU: a rank on socket 1
+  // rests its streamed data in socket-1 DRAM.
+  int first_local = -1;
+  for (int d = 0; d < nd && first_local < 0; ++d)
+    if (local(d)) first_local = d;
+  rt->host_node_ = cfg.host_node >= 0 ? (int)cfg.host_node
+                                       : (first_local >= 0 ? rt->be_->device_numa_node(first_local) : 0);
   rt->cxl_topo_.discover((int)cfg.cxl_emulate_node);
   rt->cxl_ = std::make_unique<CxlRegistry>(rt->be_.get());
   rt->cxl_->init(system_ram_bytes() / 100 * (uint64_t)cfg.cxl_pin_budget_pct, (uint32_t)cfg.cxl_max_buffers,
@@ -43,6 +51,11 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
     auto dev = std::make_unique<Device>();
     dev->id = d;
     dev->numa = rt->be_->device_numa_node(d);
+    dev->local = local(d);
+    if (!dev->local) {
+      rt->devs_.push_back(std::move(dev));
+      continue;
+    }
     for (int k = 0; k < (int)RingKind::COUNT; ++k)
       dev->rings[k] = std::make_unique<Ring>(rt->be_.get(), d, (RingKind)k, (uint32_t)cfg.channel_num_gpfifo_entries);
     void* p = nullptr;
@@ -56,9 +69,16 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
   }
   g_rt.store(rt, std::memory_order_release);
   install_cpu_fault_handler();
-  RT_INFO("runtime up: backend=%s devices=%d host_node=%d cxl_nodes=%zu", rt->be_->name(), nd, rt->host_node_,
-          rt->cxl_topo_.info().numa_nodes.size());
+  RT_INFO("runtime up: backend=%s devices=%d local=0x%llx host_node=%d cxl_nodes=%zu", rt->be_->name(), nd,
+          (unsigned long long)mask, rt->host_node_, rt->cxl_topo_.info().numa_nodes.size());
   return rt;
+}
+
+std::vector<int> Runtime::local_devices() const {
+  std::vector<int> v;
+  for (auto& d : devs_)
+    if (d->local) v.push_back(d->id);
+  return v;
 }
 
 void Runtime::shutdown() {
@@ -98,7 +118,7 @@ Runtime::~Runtime() {
 
 // ------------------------------------------------------------------ tiers
 Status Runtime::init_device(int d, uint64_t budget) {
-  if (d < 0 || d >= ndev()) return Status::INVALID_ARGUMENT;
+  if (!is_local(d)) return Status::INVALID_ARGUMENT;
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
   if (devs_[d]->hbm && devs_[d]->hbm->outstanding_bytes()) return Status::BUSY;
   devs_[d]->hbm_live.store(nullptr);
@@ -130,7 +150,7 @@ HostArena* Runtime::host_arena(Tier t, int node) {
 
 ChunkArena* Runtime::arena_for(const Loc& l) {
   if (l.is_gpu()) {
-    if (l.id < 0 || l.id >= ndev()) return nullptr;
+    if (!is_local(l.id)) return nullptr;
     Device& d = *devs_[l.id];
     if (HbmArena* a = d.hbm_live.load(std::memory_order_acquire)) return a;
     // First touch of a GPU: create its arena with the default budget (once).
@@ -162,7 +182,7 @@ Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string&
   auto r = std::make_unique<Range>(&vs_, id, RangeType::MANAGED, size, flags, name);
   if (!(flags & RANGE_NO_CPU_VIEW) && !r->cpu_view) return Status::NO_MEMORY;
   if (flags & RANGE_STABLE_VA) {
-    if (stable_dev < 0 || stable_dev >= ndev()) return Status::INVALID_ARGUMENT;
+    if (!is_local(stable_dev)) return Status::INVALID_ARGUMENT;
     vg.unlock();
     ChunkArena* a = arena_for(Loc::gpu(stable_dev));
     vg.lock();
@@ -180,7 +200,7 @@ Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string&
 }
 
 Status Runtime::map_external(uint64_t ptr, uint64_t size, int dev, const std::string& name, Range** out) {
-  if (!ptr || !size || dev < 0 || dev >= ndev()) return Status::INVALID_ARGUMENT;
+  if (!ptr || !size || !is_local(dev)) return Status::INVALID_ARGUMENT;
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
   uint64_t id = vs_.next_range_id++;
   auto r = std::make_unique<Range>(&vs_, id, RangeType::EXTERNAL, size, RANGE_NO_CPU_VIEW, name);
@@ -192,7 +212,7 @@ Status Runtime::map_external(uint64_t ptr, uint64_t size, int dev, const std::st
 }
 
 Status Runtime::alloc_device_p2p(uint64_t size, int dev, const std::string& name, Range** out) {
-  if (!size || dev < 0 || dev >= ndev()) return Status::INVALID_ARGUMENT;
+  if (!size || !is_local(dev)) return Status::INVALID_ARGUMENT;
   void* p = nullptr;
   Status st = be_->hbm_alloc(dev, align_up(size, kBlockSize), &p);
   if (st != Status::OK) return st;
@@ -259,7 +279,7 @@ Status Runtime::mem_advise(Range* r, uint64_t off, uint64_t len, Advice a, Loc l
   if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
   if (a == Advice::SET_PREFERRED_LOCATION && !arena_for(loc)) return Status::INVALID_ARGUMENT;
   if ((a == Advice::SET_ACCESSED_BY || a == Advice::UNSET_ACCESSED_BY) &&
-      !(proc == kCpuProc || (proc >= 0 && proc < ndev())))
+      !(proc == kCpuProc || is_local(proc)))
     return Status::INVALID_ARGUMENT;
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
@@ -584,7 +604,7 @@ Status Runtime::write_compressed(Range* r, uint64_t off, const void* src, uint64
 }
 
 Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev) {
-  if (!r || off + bytes > r->size) return Status::INVALID_ARGUMENT;
+  if (!r || off + bytes > r->size || (src_dev >= 0 && !is_local(src_dev))) return Status::INVALID_ARGUMENT;
   if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
   if (bytes == 0) return Status::OK;
   if (r->flags & RANGE_COMPRESS_BF16) return write_compressed(r, off, src, bytes, src_dev);
@@ -693,7 +713,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
 }
 
 Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_dev) {
-  if (!r || off + bytes > r->size) return Status::INVALID_ARGUMENT;
+  if (!r || off + bytes > r->size || (dst_dev >= 0 && !is_local(dst_dev))) return Status::INVALID_ARGUMENT;
   if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   uint64_t pos = off;
@@ -860,7 +880,7 @@ Status Runtime::sync_all() {
 }
 
 Status Runtime::enable_peer(int a, int b) {
-  if (a < 0 || b < 0 || a >= ndev() || b >= ndev() || a == b) return Status::INVALID_ARGUMENT;
+  if (!is_local(a) || b < 0 || b >= ndev() || a == b) return Status::INVALID_ARGUMENT;
   Status st = be_->enable_peer(a, b);
   if (st != Status::OK) return st;
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
@@ -878,6 +898,7 @@ Status Runtime::start_fault_service(uint32_t poll_us) {
   if (!fs_threads_.empty()) return Status::OK;
   fs_stop_.store(false);
   for (int d = 0; d < ndev(); ++d) {
+    if (!is_local(d)) continue;
     fs_threads_.emplace_back([this, d, poll_us] {
       DeviceFaultBuffer& fb = devs_[d]->fault_buf;
       while (!fs_stop_.load(std::memory_order_acquire)) {
@@ -911,7 +932,7 @@ void Runtime::stop_fault_service() {
 Status Runtime::cxl_dma(uint64_t handle, uint64_t gpu_ptr, int dev, uint64_t cxl_off, uint64_t size, int dir,
                         bool async, uint64_t* tid) {
   if (global_status() != Status::OK) return global_status();
-  if (dev < 0 || dev >= ndev() || !gpu_ptr || size == 0) return Status::INVALID_ARGUMENT;
+  if (!is_local(dev) || !gpu_ptr || size == 0) return Status::INVALID_ARGUMENT;
   CxlBuffer buf;
   Status st = cxl_->lookup(handle, &buf);
   if (st != Status::OK) return st;
@@ -951,7 +972,7 @@ Status Runtime::cxl_dma(uint64_t handle, uint64_t gpu_ptr, int dev, uint64_t cxl
 
 Status Runtime::cxl_dma_wait(uint64_t tid) {
   int dev = (int)(tid >> 56);
-  if (dev < 0 || dev >= ndev()) return Status::INVALID_ARGUMENT;
+  if (!is_local(dev)) return Status::INVALID_ARGUMENT;
   return ring(dev, RingKind::CXL)->wait_seq(tid & ((1ull << 56) - 1));
 }
 

@@ -127,6 +127,7 @@ void log_msg(LogLevel l, const char* file, int line, const char* fmt, ...) __att
 Status global_status();
 void set_fatal(Status s, const char* why);
 void clear_fatal_for_test();
+const char* fatal_reason();  // why the sticky status was set ("" when OK)
 
 void assert_fail(const char* cond, const char* file, int line, bool release);
 #define RT_ASSERT_RELEASE(c) \

@@ -99,6 +99,10 @@ struct Lease {
 struct Device {
   int id = 0;
   int numa = 0;
+  // Managed by this process (config local_devices). One process per GPU keeps
+  // every other GPU non-local: no rings, fault buffer or arena are created on
+  // it (no contexts on the neighbours' GPUs).
+  bool local = true;
   std::unique_ptr<HbmArena> hbm;
   std::atomic<HbmArena*> hbm_live{nullptr};  // published `hbm` for lock-free readers (arena_for)
   std::unique_ptr<Ring> rings[(int)RingKind::COUNT];
@@ -136,6 +140,8 @@ class Runtime {
   Backend* be() { return be_.get(); }
   int ndev() const { return (int)devs_.size(); }
   Device& dev(int i) { return *devs_[i]; }
+  bool is_local(int d) const { return d >= 0 && d < (int)devs_.size() && devs_[d]->local; }
+  std::vector<int> local_devices() const;
   VaSpace& vs() { return vs_; }
   Injection& inject() { return inject_; }
   CxlTopology& cxl_topology() { return cxl_topo_; }
@@ -148,7 +154,8 @@ class Runtime {
   Status init_device(int d, uint64_t budget_bytes);   // (re)create the HBM arena of d
   HostArena* host_arena(Tier t, int node);            // created on first use
   ChunkArena* arena_for(const Loc& l);
-  Ring* ring(int dev, RingKind k) { return devs_[dev]->rings[(int)k].get(); }
+  // nullptr for a non-local device
+  Ring* ring(int dev, RingKind k) { return is_local(dev) ? devs_[dev]->rings[(int)k].get() : nullptr; }
 
   // ---- allocation / ranges (UvmMemMap + mmap analog)
   Status malloc_managed(uint64_t size, uint32_t flags, const std::string& name, Range** out, int stable_dev = 0);

@@ -38,6 +38,13 @@ Runtime* rt() {
   return r;
 }
 
+Ring* ring_of(int dev, int kind) {
+  if (kind < 0 || kind >= (int)RingKind::COUNT) throw StatusError("bad ring kind");
+  Ring* r = rt()->ring(dev, (RingKind)kind);
+  if (!r) throw StatusError("gpu " + std::to_string(dev) + " is not managed by this process (local_devices)");
+  return r;
+}
+
 Range* range(uint64_t id) {
   Range* r = rt()->range_by_id(id);
   if (!r) throw StatusError("unknown range id " + std::to_string(id));
@@ -153,10 +160,16 @@ PYBIND11_MODULE(_ogkm, m) {
   m.def("is_initialized", [] { return Runtime::get() != nullptr; });
   m.def("backend_name", [] { return std::string(rt()->be()->name()); });
   m.def("device_count", [] { return rt()->ndev(); });
+  m.def("local_devices", [] { return rt()->local_devices(); });
   m.def("host_node", [] { return rt()->host_node(); });
   m.def("device_numa_node", [](int d) { return rt()->dev(d).numa; });
   m.def("global_status", [] { return std::string(status_str(global_status())); });
   m.def("clear_fatal_for_test", [] { clear_fatal_for_test(); });
+  // Sticky fatal error raised outside the core (e.g. a failed / timed-out RCCL
+  // collective, parallel/comm.py): every later runtime entry point fails fast
+  // (uvm_global_set_fatal_error_impl, uvm_global.c:420-438).
+  m.def("set_fatal", [](const std::string& why) { set_fatal(Status::FATAL, why.c_str()); });
+  m.def("fatal_reason", [] { return std::string(fatal_reason()); });
   m.def("init_device", [](int d, uint64_t budget) { check(rt()->init_device(d, budget), "init_device"); });
   m.def("sync_all", [] {
     py::gil_scoped_release nogil;
@@ -425,6 +438,7 @@ PYBIND11_MODULE(_ogkm, m) {
     for (int g = 0; g < r->ndev(); ++g)
       for (int k = 0; k < (int)RingKind::COUNT; ++k) {
         Ring* rg = r->ring(g, (RingKind)k);
+        if (!rg) continue;
         py::dict x;
         x["dev"] = g;
         x["kind"] = ring_kind_str((RingKind)k);
@@ -466,19 +480,19 @@ PYBIND11_MODULE(_ogkm, m) {
   });
   m.def("ring_reap", [](int dev, int kind) {
     Cqe buf[256];
-    size_t n = rt()->ring(dev, (RingKind)kind)->reap(buf, 256);
+    size_t n = ring_of(dev, kind)->reap(buf, 256);
     std::vector<std::tuple<uint64_t, uint64_t, int>> out;
     for (size_t i = 0; i < n; ++i) out.emplace_back(buf[i].user_data, buf[i].seq, buf[i].status);
     return out;
   });
   m.def("ring_error", [](int dev, int kind) {
-    Ring* r = rt()->ring(dev, (RingKind)kind);
+    Ring* r = ring_of(dev, kind);
     return std::make_pair(std::string(status_str(r->error())), r->last_error_desc());
   });
-  m.def("ring_clear_error", [](int dev, int kind) { rt()->ring(dev, (RingKind)kind)->clear_error_for_test(); });
+  m.def("ring_clear_error", [](int dev, int kind) { ring_of(dev, kind)->clear_error_for_test(); });
   m.def("ring_copy", [](int dev, int kind, uint64_t dst, uint64_t src, uint64_t bytes, bool wait) {
     // Direct ring access (used by benchmarks and the CE-style tests).
-    Ring* r = rt()->ring(dev, (RingKind)kind);
+    Ring* r = ring_of(dev, kind);
     Sqe s;
     s.op = SqeOp::COPY;
     s.dst = dst;
@@ -493,7 +507,7 @@ PYBIND11_MODULE(_ogkm, m) {
     return seq;
   });
   m.def("ring_memset", [](int dev, int kind, uint64_t dst, uint32_t pattern, uint64_t bytes) {
-    Ring* r = rt()->ring(dev, (RingKind)kind);
+    Ring* r = ring_of(dev, kind);
     Sqe s;
     s.op = SqeOp::MEMSET;
     s.dst = dst;
@@ -505,7 +519,7 @@ PYBIND11_MODULE(_ogkm, m) {
   });
   m.def("ring_gather", [](int dev, uint64_t base, uint64_t contig, std::vector<uint32_t> idx, uint32_t page_bytes,
                           bool scatter) {
-    Ring* r = rt()->ring(dev, RingKind::GPU_INTERNAL);
+    Ring* r = ring_of(dev, (int)RingKind::GPU_INTERNAL);
     Sqe s;
     s.op = scatter ? SqeOp::SCATTER : SqeOp::GATHER;
     s.src = scatter ? contig : base;
@@ -516,7 +530,7 @@ PYBIND11_MODULE(_ogkm, m) {
     py::gil_scoped_release nogil;
     check(r->submit()->wait(), "ring_gather");
   });
-  m.def("ring_stream", [](int dev, int kind) { return (uint64_t)rt()->ring(dev, (RingKind)kind)->stream(); });
+  m.def("ring_stream", [](int dev, int kind) { return (uint64_t)ring_of(dev, kind)->stream(); });
 
   // ---- tools
   m.def("tools_create_queue", [](uint32_t entries, uint32_t mask, const std::string& shm) {

@@ -18,8 +18,20 @@ and the ring waits on the compute stream's release events before overwriting a
 chunk (SURVEY.md §7.3 minimum slice: malloc_managed + residency map + HBM budget
 + evict to host + software faults + decode tokens/s).
 
-Tensor parallelism (``tp_world`` > 1, one process per GPU, RCCL) shards every
-layer Megatron-style; each rank streams only its shard over its own PCIe link.
+Multi-GPU (one process per GPU, RCCL over xGMI), ``parallel=``:
+
+  * ``"tp"`` (default): Megatron tensor parallelism over ``tp_world`` ranks; each
+    rank streams only its 1/N of every layer over its own PCIe link and the
+    partial outputs are all-reduced (2 per layer).
+  * ``"shards"`` (north-star config 4, "peermem-style P2P shards"): every unit
+    (weight matrix / LM-head part, in its resting format) is cut into N byte
+    shards; rank r owns shard r (preferred on its GPU, or streamed from its host
+    DRAM at 2x oversubscription) and the whole unit is all-gathered over xGMI into
+    a transient HBM slot right before use, with look-ahead on a side stream
+    (parallel/shards.py UnitGather). Each rank decodes its own B/N sequences
+    with the full model (ZeRO-3-style inference). The reference's analogue is
+    data resident on one processor read by another through remote mapping /
+    read duplication (uvm_va_block.c:11660-11664, :5164).
 """
 from __future__ import annotations
 
@@ -150,7 +162,22 @@ class TieredLlama:
                  device: int = 0, tp_rank: int = 0, tp_world: int = 1, seed: int = 0, lookahead: int = 2,
                  hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
                  packed: bool = True, weight_format: str = "bf11", tiers: str = "host", cxl_frac: float = 0.5,
-                 kv_format: str = "bf16"):
+                 kv_format: str = "bf16", parallel: str = "tp"):
+        if parallel not in ("tp", "shards"):
+            raise ValueError("parallel must be 'tp' or 'shards'")
+        self.parallel = parallel
+        if parallel == "shards":
+            # Data parallel over sequences, weights sharded over ranks: the layer
+            # math is the single-GPU model (TP world 1) on B / N local sequences.
+            if batch % tp_world:
+                raise ValueError("shards: the global batch must be a multiple of the rank count")
+            self.srank, self.sworld = tp_rank, tp_world
+            self.B_global = batch
+            batch //= tp_world
+            self.b0 = self.srank * batch
+            tp_rank, tp_world = 0, 1
+        else:
+            self.srank, self.sworld, self.B_global, self.b0 = 0, 1, batch, 0
         assert cfg.n_heads % tp_world == 0 and cfg.n_kv_heads % tp_world == 0 and cfg.ffn_dim % tp_world == 0
         assert cfg.vocab % tp_world == 0
         self.cfg, self.B, self.ctx = cfg, batch, context
@@ -172,8 +199,8 @@ class TieredLlama:
         self.kv_layer_bytes = 2 * batch * self.hkv * self.T * hd * 2
         self.kv_bytes = cfg.n_layers * self.kv_layer_bytes
         self.norm_bytes = _al((2 * cfg.n_layers + 1) * cfg.dim * 2)
-        self.footprint = (self.embed_bytes + cfg.n_layers * self.layer_bytes + self.head_bytes + self.kv_bytes
-                          + self.norm_bytes)
+        self.footprint = (self.embed_bytes + (cfg.n_layers * self.layer_bytes + self.head_bytes) // self.sworld
+                          + self.kv_bytes + self.norm_bytes)
         self.oversub = oversub
         blk = 2 << 20
         budget = hbm_budget if hbm_budget is not None else int(self.footprint / oversub)
@@ -196,11 +223,22 @@ class TieredLlama:
         self.packed = packed and weight_format == "bf16"
         self.staged = weight_format in ("bf12", "ans")
         self.packfmt = "bf11s" if weight_format == "bf11" else weight_format
-        self.stage_bytes = (chunks(max(math.prod(sh) * 2 for sh in self.layout.shapes.values()) + (1 << 20))
-                            if self.staged else 0)
-        self.arena_bytes = self.budget - self.stage_bytes
+        unit_raw_max = max(math.prod(sh) * 2 for sh in self.layout.shapes.values())
+        self.stage_bytes = chunks(unit_raw_max + (1 << 20)) if self.staged else 0
+        # shards: the largest unit's shard (its resting stream is never bigger than
+        # the raw bf16 + chunk headers) and the all-gather slots that hold whole units
+        self.gather_depth = max(2, int(os.environ.get("OGKM_GATHER_DEPTH", "2")))
+        # resting-stream bound of a unit: raw bf16 + chunk headers (packed streams never exceed it)
+        stream_bound = unit_raw_max + 8192 + ((unit_raw_max >> 21) + 1) * 1024
+        self.shard_max = _al(-(-stream_bound // self.sworld)) if self.sworld > 1 else 0
+        self.gather_bytes = chunks(self.gather_depth * self.sworld * self.shard_max) if self.sworld > 1 else 0
+        self.arena_bytes = self.budget - self.stage_bytes - self.gather_bytes
         if kv_format != "bf16":
             self.arena_bytes -= chunks(self.kv_layer_bytes)  # the per-layer KV scratch
+        if self.arena_bytes <= 0:
+            raise ValueError(f"HBM budget {self.budget / 2**30:.2f} GiB does not cover the unpack staging "
+                             f"({self.stage_bytes / 2**30:.2f} GiB) and all-gather slots "
+                             f"({self.gather_bytes / 2**30:.2f} GiB): lower the oversubscription")
         lib.init_device(device, self.arena_bytes)
         self.pinfo: dict = {}
         self.pmode: dict = {}
@@ -252,6 +290,12 @@ class TieredLlama:
         else:
             self.res_part = {n: _al(b) for n, b in part_raw.items()}
             self.res_head_part = [_al((r1 - r0) * cfg.dim * 2) for r0, r1 in self.head_rows]
+        if self.sworld > 1:
+            # every rank rests 1/N of each unit: plan (and stream) shard bytes
+            self.full_part, self.full_head_part = dict(self.res_part), list(self.res_head_part)
+            shard = lambda b: min(self.shard_max, _al(-(-b // self.sworld)))  # noqa: E731
+            self.res_part = {n: shard(b) for n, b in self.res_part.items()}
+            self.res_head_part = [shard(b) for b in self.res_head_part]
         self.res_layer_bytes = sum(self.res_part.values())
         self.res_head_bytes = sum(self.res_head_part)
         # ---- residency plan (in resting bytes: packed or raw)
@@ -395,6 +439,11 @@ class TieredLlama:
         self._pin_leases: list = []
         self.keep_logits = False   # tests: keep the full-vocab logits of the last step
         self.last_logits = None
+        self.gather = None
+        if self.sworld > 1:
+            from ..parallel.shards import UnitGather
+            self.gather = UnitGather(self.order, self._buf, self._unit_bytes, self.sworld, self.gather_depth,
+                                     device=self.tdev, dev_index=device)
         self.init_seconds = time.perf_counter() - t0
         if verbose:
             self.describe()
@@ -402,7 +451,9 @@ class TieredLlama:
     # ------------------------------------------------------------------ setup
     def describe(self) -> dict:
         d = {
-            "model": self.cfg.name, "tp": f"{self.rank}/{self.world}", "batch": self.B, "context": self.ctx,
+            "model": self.cfg.name, "tp": f"{self.rank}/{self.world}", "parallel": self.parallel,
+            "shard": f"{self.srank}/{self.sworld}", "batch": self.B, "global_batch": self.B_global,
+            "gather_gb": self.gather_bytes / 1e9, "context": self.ctx,
             "footprint_gb": self.footprint / 1e9, "hbm_budget_gb": self.budget / 1e9,
             "oversubscription": self.footprint / self.budget, "kv_gb": self.kv_bytes / 1e9,
             "layer_gb": self.layer_bytes / 1e9, "resident_layers": sum(self.resident),
@@ -416,6 +467,13 @@ class TieredLlama:
             "cxl_streamed_gb_per_step": self.cxl_streamed_bytes / 1e9,
             "stream_slot_gb": self.slot_bytes / 1e9, "head_parts": len(self.head_rows),
         }
+        if getattr(self, "ubuf", None) and getattr(self, "kv", None) is not None:
+            # what the runtime really holds (packed where packed) per HBM byte
+            resting = sum(b.size for b in self.ubuf.values()) + self.kv.size + self.embed.size
+            d["resting_gb"] = resting / 1e9
+            d["physical_oversubscription"] = resting / self.budget
+        else:
+            d["physical_oversubscription"] = d["oversubscription"]
         if self.verbose and self.rank == 0:
             print("[ogkm] plan:", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}, flush=True)
         return d
@@ -463,6 +521,24 @@ class TieredLlama:
     def _alloc_unit(self, key, data: torch.Tensor, info, gpu, host) -> None:
         name = "-".join(str(x) for x in key)
         resident = self._is_resident(key)
+        if self.sworld > 1:
+            # bytes [r S, (r+1) S) of the unit's resting stream (zero padded)
+            S = self._unit_bytes(key)
+            raw = data.reshape(-1).contiguous().cpu().view(torch.uint8)
+            part = torch.zeros(S, dtype=torch.uint8)
+            lo = min(raw.numel(), self.srank * S)
+            hi = min(raw.numel(), lo + S)
+            part[:hi - lo] = raw[lo:hi]
+            if raw.numel() > self.sworld * S:
+                raise ValueError(f"unit {key} does not fit {self.sworld} shards of {S} bytes")
+            b = rt.malloc_managed(S, name, cpu_view=False)
+            if info is not None:
+                self.pinfo[key] = info
+                self.pmode[key] = dgemm.packed_mode(data) if not self.staged else dgemm.MODE_RAW
+            self._place(b, resident, gpu, self.rest_loc.get(key, host))
+            b.write(part)
+            self.ubuf[key] = b
+            return
         if info is not None:
             b = rt.malloc_managed(info.nbytes, name, cpu_view=False)
             self.pinfo[key] = info
@@ -525,10 +601,10 @@ class TieredLlama:
         g = torch.Generator(device=self.tdev).manual_seed(self._seed + 7919)
         h0 = self.rank * self.hkv
         for _ in range(cfg.n_layers):
-            full = torch.empty(2, self.B, cfg.n_kv_heads, self.ctx, cfg.head_dim, dtype=torch.bfloat16,
+            full = torch.empty(2, self.B_global, cfg.n_kv_heads, self.ctx, cfg.head_dim, dtype=torch.bfloat16,
                                device=self.tdev)
             full.normal_(0.0, 1.0, generator=g)
-            yield full[:, :, h0:h0 + self.hkv].contiguous()
+            yield full[:, self.b0:self.b0 + self.B, h0:h0 + self.hkv].contiguous()
             del full
 
     def _kv_layer(self, i: int, pos: int) -> torch.Tensor:
@@ -623,6 +699,8 @@ class TieredLlama:
         it is enqueued). bf12 / ans: the stream is unpacked into the staging
         buffer on the compute stream and the lease is released right away (the
         ring reuses the chunks only after the unpack has read them)."""
+        if self.gather is not None:
+            return self._use_gathered(key)
         pin = self._pinned.get(key)
         if pin is not None:  # resident tensor: long-lived lease taken at init, refs cached
             return None, (self._unstage(key, pin.ptr) if self.staged else pin)
@@ -655,6 +733,21 @@ class TieredLlama:
             return None, st
         return lease, refs
 
+    def _use_gathered(self, key):
+        """shards: fault this rank's shard in (the runtime prefetches streamed
+        shards ahead on the ring), all-gather the whole unit over RCCL (issued
+        ahead on the gather stream) and return its WeightRef in the gather slot."""
+        if not self._is_resident(key):
+            if self._inflight and self._inflight[0] == key:
+                self._inflight.pop(0)
+            self._prefetch_ahead()
+        full = self.gather.get(key)
+        if self.staged:
+            ref = self._unstage(key, full.data_ptr())
+            self.gather.done(key)
+            return None, ref
+        return ("gather", key), self._ref(key, full.data_ptr(), self.pmode.get(key, dgemm.MODE_RAW))
+
     def _unstage(self, key, packed_ptr: int) -> "dgemm.WeightRef":
         """Unpack a packed unit into the bf16 staging buffer (compute stream)."""
         bf12.unpack_into(self.stage, packed_ptr, self.pinfo[key], self.dev, 0 if self.fake else None)
@@ -666,7 +759,9 @@ class TieredLlama:
         return dgemm.WeightRef(ptr, 0, n, k, mode, shift)
 
     def _done(self, lease) -> None:
-        if lease is not None:
+        if isinstance(lease, tuple):  # a gather slot read by the kernels just enqueued
+            self.gather.done(lease[1])
+        elif lease is not None:
             lease.release(0 if self.fake else None)
 
     # ------------------------------------------------------------------ decode
@@ -708,7 +803,8 @@ class TieredLlama:
             dgemm.linear(x, w, out=logits[:, r0:r1], device_index=dv)
             self._done(lease)
         if self.keep_logits:
-            self.last_logits = comm.all_gather_cat(logits.float(), dim=-1)
+            # tp: vocab shards of every sequence; shards: every rank's own sequences
+            self.last_logits = comm.all_gather_cat(logits.float(), dim=0 if self.sworld > 1 else -1)
         nxt = tpmod.vocab_parallel_argmax(logits, self.rank, self.world)
         self.pos += 1
         return nxt
@@ -740,6 +836,8 @@ class TieredLlama:
         self.pos = self.ctx if position is None else position
 
     def close(self) -> None:
+        if self.gather is not None:
+            self.gather.drain()
         self.kv_lease.release(0 if self.fake else None)
         for lease in self._pin_leases:
             lease.release(0 if self.fake else None)

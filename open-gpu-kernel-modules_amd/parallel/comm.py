@@ -13,12 +13,41 @@ on the compute stream without extra host synchronisation.
 from __future__ import annotations
 
 import datetime
+import functools
 import os
 from dataclasses import dataclass
 from typing import Optional
 
 import torch
 import torch.distributed as dist
+
+
+class CollectiveError(RuntimeError):
+    """A collective failed or timed out; the runtime's status is now FATAL."""
+
+
+def _fatal_on_error(fn):
+    """Collective failures (peer lost, RCCL error, timeout) become the runtime's
+    sticky fatal status - the analogue of a channel error setting the global
+    fatal error (uvm_channel.c:2080-2112, uvm_global.c:420-438): every later
+    runtime call then fails fast instead of hanging on a dead peer."""
+
+    @functools.wraps(fn)
+    def wrapper(*a, **kw):
+        try:
+            return fn(*a, **kw)
+        except CollectiveError:
+            raise
+        except Exception as e:  # noqa: BLE001 - any backend error is fatal for the job
+            why = f"collective {fn.__name__} failed on rank {env().rank}: {type(e).__name__}: {e}"
+            try:
+                from .._native import lib
+                if lib.is_initialized():
+                    lib.set_fatal(why[:200])
+            except Exception:
+                pass
+            raise CollectiveError(why) from e
+    return wrapper
 
 
 @dataclass
@@ -53,6 +82,9 @@ def init(backend: Optional[str] = None, timeout_s: int = 600) -> DistEnv:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     if backend == "nccl":
+        # RCCL errors / timeouts are raised in the waiting thread (and abort the
+        # communicator) instead of hanging the job.
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s),
                                 device_id=torch.device("cuda", local))
@@ -73,6 +105,7 @@ def shutdown() -> None:
     _ENV = None
 
 
+@_fatal_on_error
 def barrier() -> None:
     e = env()
     if e.is_dist:
@@ -82,12 +115,14 @@ def barrier() -> None:
             dist.barrier()
 
 
+@_fatal_on_error
 def all_reduce_(t: torch.Tensor) -> torch.Tensor:
     if env().is_dist:
         dist.all_reduce(t)
     return t
 
 
+@_fatal_on_error
 def all_gather_cat(t: torch.Tensor, dim: int = 0) -> torch.Tensor:
     e = env()
     if not e.is_dist:
@@ -97,6 +132,21 @@ def all_gather_cat(t: torch.Tensor, dim: int = 0) -> torch.Tensor:
     return torch.cat(out, dim=dim)
 
 
+@_fatal_on_error
+def all_gather_into(out: torch.Tensor, shard: torch.Tensor) -> torch.Tensor:
+    """out = concat of every rank's ``shard`` (equal sizes), in rank order. RCCL:
+    one all_gather_into_tensor on the current stream (the host does not wait)."""
+    e = env()
+    if not e.is_dist:
+        out[:shard.numel()].copy_(shard.reshape(-1))
+    elif e.backend == "nccl":
+        dist.all_gather_into_tensor(out, shard)
+    else:
+        dist.all_gather(list(out.chunk(e.world)), shard.clone())
+    return out
+
+
+@_fatal_on_error
 def reduce_scatter_(out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
     e = env()
     if not e.is_dist:
@@ -106,6 +156,18 @@ def reduce_scatter_(out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
     return out
 
 
+@_fatal_on_error
+def all_gather_objects(obj) -> list:
+    """One picklable object per rank, in rank order (host-side metadata only)."""
+    e = env()
+    if not e.is_dist:
+        return [obj]
+    out = [None] * e.world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+@_fatal_on_error
 def max_over_ranks(x: float) -> float:
     """Max of a host scalar over ranks (timing: the job is as slow as its slowest rank)."""
     e = env()
@@ -124,6 +186,7 @@ class Bucketer:
     def __init__(self, bucket_bytes: int = 64 << 20):
         self.bucket_bytes = bucket_bytes
 
+    @_fatal_on_error
     def all_reduce(self, tensors: list[torch.Tensor]) -> None:
         if not env().is_dist or not tensors:
             return

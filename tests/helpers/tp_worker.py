@@ -1,7 +1,9 @@
-"""Worker for the multi-process tensor-parallel test (gloo, fake backend).
+"""Worker for the multi-process model tests (gloo, fake backend): tensor
+parallel (PARALLEL=tp) or peer-shard weights (PARALLEL=shards).
 
-Launched by torch.distributed.run; prints one JSON line per rank with the
-logits of each decode step, for comparison with the single-process run."""
+Launched by torch.distributed.run; rank 0 prints one JSON line with the logits
+of each decode step (all sequences, full vocab), for comparison with the
+single-process run."""
 import json
 import os
 import sys
@@ -13,20 +15,26 @@ import torch  # noqa: E402
 import ogkm  # noqa: E402,F401
 from ogkm import rt  # noqa: E402
 from ogkm.models import llama  # noqa: E402
+from ogkm._native import lib  # noqa: E402
 from ogkm.parallel import comm  # noqa: E402
 
 
 def main():
     e = comm.init("gloo")
     rt.init("fake", fake_devices=1, fake_hbm_mb=512, host_budget_mb=2048)
-    cfg = llama.CONFIGS["tiny"]
-    m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=4, oversub=1.2, lookahead=1,
-                          tp_rank=e.rank, tp_world=e.world, seed=5)
+    par = os.environ.get("PARALLEL", "tp")
+    batch = int(os.environ.get("BATCH", "2"))
+    oversub = float(os.environ.get("OVERSUB", "1.2"))
+    cfg = llama.CONFIGS[os.environ.get("MODEL", "tiny")]
+    m = llama.TieredLlama(cfg, batch=batch, context=8, max_new_tokens=4, oversub=oversub, lookahead=1,
+                          tp_rank=e.rank, tp_world=e.world, seed=5, parallel=par)
     m.keep_logits = True
     out = []
     for s in range(3):  # fixed input schedule: comparisons do not depend on near-tie argmax
-        tok = m.step(torch.tensor([3 + s, 11 + s]))
+        glob = torch.tensor([3 + s + 8 * j for j in range(batch)])
+        tok = m.step(glob[m.b0:m.b0 + m.B])
         out.append({"tokens": tok.tolist(), "logits": m.last_logits[:, :64].tolist()})
+    out.append({"host_node": lib.host_node(), "gathers": m.gather.stats["gathers"] if m.gather else 0})
     if e.rank == 0:
         print("TPRESULT " + json.dumps(out), flush=True)
     m.close()

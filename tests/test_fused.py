@@ -43,8 +43,8 @@ def _check_rope_kv(gpu):
     assert cd[:, :, :, pos + 1:].abs().sum() == 0 and cd[:, :, :, :pos].abs().sum() == 0
 
 
-def _check_attention(gpu, length):
-    B, hq, hkv, hd, T = 2, 16, 2, 128, 700
+def _check_attention(gpu, length, hq=16, hkv=2):
+    B, hd, T = 2, 128, 700
     q = torch.randn(B, hq, hd).to(torch.bfloat16)
     cache = torch.randn(2, B, hkv, T, hd).to(torch.bfloat16)
     want = D.gqa_decode_attention(q.float(), cache[0].float(), cache[1].float(), length)
@@ -80,3 +80,18 @@ def test_rope_kv_gpu(gpu_rt):
 @pytest.mark.parametrize("length", [1, 255, 256, 257, 700])
 def test_attention_gpu(gpu_rt, length):
     _check_attention(True, length)
+
+
+# The GQA group shapes every tp8 rank of Llama-3 70B (8 q heads : 1 kv head) and
+# 405B (16 : 1) runs.
+@pytest.mark.parametrize("hq,hkv", [(8, 1), (16, 1)])
+@pytest.mark.parametrize("length", [1, 700])
+def test_attention_one_kv_head_cpu(fake_rt, hq, hkv, length):
+    _check_attention(False, length, hq, hkv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hq,hkv", [(8, 1), (16, 1)])
+@pytest.mark.parametrize("length", [1, 255, 256, 257, 700])
+def test_attention_one_kv_head_gpu(gpu_rt, hq, hkv, length):
+    _check_attention(True, length, hq, hkv)

@@ -294,3 +294,35 @@ def test_bf12_stream_unpack_hbm_bit_exact_and_fast(gpu_rt, fmt, max_ratio, min_g
     gbps = n * 2 / dt / 1e9
     print(f"{fmt} HBM unpack: {gbps:.0f} GB/s of bf16 written ({(info.nbytes + 2 * n) / dt / 1e9:.0f} GB/s HBM traffic)")
     assert gbps > min_gbps
+
+
+def test_ans_unpack_reports_corrupt_chunk(gpu_rt):
+    """A chunk whose ANS frequency table is not a valid distribution (zeroed here)
+    is zero-filled and reported through lib.decode_errors() - the decoder never
+    spins on it (before round 2 such a chunk cost a ~47 s decode-table scan)."""
+    import struct
+
+    from ogkm._native import lib
+    from ogkm.ops import bf12
+
+    n = 3 << 20
+    ref = (torch.randn(n) * 0.02).to(torch.bfloat16)
+    stream, info = bf12.pack(ref, fmt="ans")
+    assert bf12.chunk_kinds(stream) == {3}
+    off = struct.unpack_from("<Q", bytes(stream[32 + 16:32 + 24].numpy()))[0]  # chunk 1 payload
+    bad = stream.clone()
+    bad[off + 512:off + 1024] = 0  # u16 freq[256]
+    src = bad.cuda()
+    dst = torch.full((n,), 7.0, dtype=torch.bfloat16, device="cuda")
+    lib.decode_errors(True)
+    t0 = time.perf_counter()
+    bf12.unpack_into(dst, src.data_ptr(), info, 0)
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 5.0
+    err = lib.decode_errors(True)
+    assert err["count"] >= 1 and err["stream"] == src.data_ptr() and err["chunk"] == 1 and err["detail"] == 0
+    got = dst.view(torch.int16).cpu()
+    cv = info.chunk_values
+    assert torch.equal(got[:cv], ref.view(torch.int16)[:cv])
+    assert torch.equal(got[2 * cv:], ref.view(torch.int16)[2 * cv:])
+    assert (got[cv:2 * cv] == 0).all()

@@ -242,3 +242,21 @@ def test_external_and_device_p2p_ranges(fake_rt):
     assert x.residency(0)["resident_on"][0] == {"tier": "gpu", "id": 1, "pages": 512, "chunk": -1}
     x.free()
     e.free()
+
+
+def test_ring_gather_scatter_memset_cpu(fake_rt):
+    """Page-list pack/unpack and memset SQEs through a ring (fake backend)."""
+    import torch
+
+    src = torch.arange(64 * 1024, dtype=torch.int32)
+    dst = torch.zeros(16 * 1024, dtype=torch.int32)
+    idx = [3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59]
+    lib.ring_gather(0, src.data_ptr(), dst.data_ptr(), idx, 4096, False)
+    assert torch.equal(dst, torch.cat([src[i * 1024:(i + 1) * 1024] for i in idx]))
+    back = torch.zeros_like(src)
+    lib.ring_gather(0, back.data_ptr(), dst.data_ptr(), idx, 4096, True)
+    for i in idx:
+        assert torch.equal(back[i * 1024:(i + 1) * 1024], src[i * 1024:(i + 1) * 1024])
+    m = torch.empty(1 << 16, dtype=torch.int32)
+    lib.ring_memset(0, 4, m.data_ptr(), 0x7F7F7F7F, m.numel() * 4)
+    assert bool((m == 0x7F7F7F7F).all())

@@ -112,25 +112,50 @@ def _free_port() -> int:
     return p
 
 
-def test_tensor_parallel_two_ranks_matches_single(fake_rt):
-    cfg = llama.CONFIGS["tiny"]
-    m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=4, oversub=1.2, lookahead=1, seed=5)
+def _single_run(batch: int = 2, oversub: float = 1.2, model: str = "tiny"):
+    cfg = llama.CONFIGS[model]
+    m = llama.TieredLlama(cfg, batch=batch, context=8, max_new_tokens=4, oversub=oversub, lookahead=1, seed=5)
     m.keep_logits = True
     single = []
     for s in range(3):
-        tok = m.step(torch.tensor([3 + s, 11 + s]))
+        tok = m.step(torch.tensor([3 + s + 8 * j for j in range(batch)]))
         single.append((tok.tolist(), m.last_logits[:, :64].clone()))
     m.close()
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    return single
+
+
+def _multi_run(nproc: int, parallel: str, batch: int = 2, oversub: float = 1.2, model: str = "tiny"):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", PARALLEL=parallel, BATCH=str(batch),
+               OVERSUB=str(oversub), MODEL=model)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "tests/helpers/tp_worker.py")]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     line = [l for l in r.stdout.splitlines() if l.startswith("TPRESULT ")]
     assert line, r.stdout[-2000:] + r.stderr[-4000:]
-    tp = json.loads(line[0][len("TPRESULT "):])
-    assert len(tp) == 3
+    return json.loads(line[0][len("TPRESULT "):])
+
+
+def test_tensor_parallel_two_ranks_matches_single(fake_rt):
+    single = _single_run()
+    tp = _multi_run(2, "tp")
+    assert len(tp) == 4
     for (tok1, log1), step in zip(single, tp):
         torch.testing.assert_close(torch.tensor(step["logits"]), log1, atol=0.05, rtol=0.05)
+
+
+def test_peer_shards_two_ranks_matches_single(fake_rt):
+    """Config 4 ("peermem-style P2P shards"): each rank owns half of every unit,
+    units are all-gathered before use and each rank decodes its own sequences
+    with the full model - the same math as one GPU, at 2x oversubscription of the
+    per-rank shard footprint."""
+    lib.shutdown()
+    rt.init("fake", fake_devices=1, fake_hbm_mb=512, lock_check=1, host_budget_mb=2048)
+    single = _single_run(batch=4, oversub=2.0, model="small")
+    sh = _multi_run(2, "shards", batch=4, oversub=2.0, model="small")
+    assert len(sh) == 4 and sh[-1]["gathers"] > 0
+    for (tok1, log1), step in zip(single, sh):
+        torch.testing.assert_close(torch.tensor(step["logits"]), log1, atol=1e-3, rtol=1e-3)
+        assert step["tokens"] == tok1[:2]  # rank 0's own sequences
 
 
 def test_three_tier_host_and_cxl_streaming(fake_rt):

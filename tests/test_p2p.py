@@ -133,3 +133,28 @@ def test_ipc_cross_process(fake_rt):
     reg.put()
     c.close()
     b.free()
+
+
+def test_collective_timeout_sets_sticky_fatal():
+    """A collective that fails (here: a peer that never joins, caught by the
+    process-group timeout) raises comm.CollectiveError and sets the runtime's
+    sticky FATAL status, so later runtime calls fail fast."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "tests/helpers/comm_fault_worker.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    line = [l for l in r.stdout.splitlines() if l.startswith("COMMFAULT ")]
+    assert line, r.stdout[-2000:] + r.stderr[-3000:]
+    out = json.loads(line[0][len("COMMFAULT "):])
+    assert out["raised"] and out["status"] == "FATAL" and "all_reduce_" in out["reason"]
+    assert out["malloc_after"] != "ok" and "FATAL" in out["malloc_after"]
