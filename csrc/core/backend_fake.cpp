@@ -251,6 +251,12 @@ class FakeBackend : public Backend {
     });
     return Status::OK;
   }
+  // The fake "SDMA engine": the ring worker's own thread does the copy.
+  bool dma_supported(int) override { return true; }
+  Status dma_copy(int, const CopyDesc* d, size_t n, int) override {
+    for (size_t i = 0; i < n; ++i) memmove((void*)d[i].dst, (const void*)d[i].src, d[i].bytes);
+    return Status::OK;
+  }
   Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s, uint32_t) override {
     std::vector<DecodeDesc> v(d, d + n);
     run(s, [v] {

@@ -27,9 +27,21 @@ Ring::Ring(Backend* be, int dev, RingKind kind, uint32_t entries) : be_(be), dev
     err_ = Status::NO_MEMORY;
     RT_ERR("ring %s/%d init failed", ring_kind_str(kind), dev);
   }
+  // PCIe / xGMI rings run their copies on a copy engine (SDMA) when there is one.
+  dma_ = config().copy_engine == 3 && kind != RingKind::GPU_INTERNAL && kind != RingKind::MEMOPS &&
+         be_->dma_supported(dev) && err_ == Status::OK;
+  if (dma_) worker_ = std::thread([this] { worker(); });
 }
 
 Ring::~Ring() {
+  if (dma_) {
+    {
+      std::lock_guard<std::mutex> g(wm_);
+      stop_ = true;
+    }
+    wcv_.notify_all();
+    worker_.join();
+  }
   if (stream_) {
     be_->stream_sync(stream_);
     last_fence_.reset();
@@ -61,6 +73,131 @@ FenceRef Ring::submit() {
   return submit_locked();
 }
 
+FenceRef Ring::submit_dma_locked() {
+  Runtime* rt = Runtime::get();
+  Batch b;
+  uint64_t last = 0;
+  for (auto& e : sq_) {
+    Sqe& s = e.second;
+    int32_t cqe_status = 0;
+    if (s.op == SqeOp::COPY && rt && rt->inject().copy_drop.load() > 0 && rt->inject().copy_drop.fetch_sub(1) > 0) {
+      // Simulated link error (uvm_volta_ce.c:137-138 analog): dropped + reported.
+      Tools::get().inc(Counter::InjectedErrors);
+      cqe_status = (int32_t)Status::INJECTED_ERROR;
+      if (err_ == Status::OK) {
+        err_ = Status::INJECTED_ERROR;
+        err_desc_ = std::string(s.file) + ":" + std::to_string(s.line) + " " + s.desc;
+      }
+    } else if (err_ != Status::OK) {
+      cqe_status = (int32_t)err_.load();
+    } else {
+      b.ops.push_back(std::move(s));
+    }
+    last = std::max(last, e.first);
+    inflight_.emplace_back(e.first, Cqe{s.user_data, e.first, cqe_status});
+  }
+  sq_.clear();
+  b.last = last;
+  if (err_ == Status::OK) {
+    Tools::get().inc(Counter::CopyKernelLaunches);  // one engine submission per batch
+    {
+      std::lock_guard<std::mutex> g(wm_);
+      work_.push_back(std::move(b));
+    }
+    wcv_.notify_one();
+  } else {
+    // Robust-channel style: a failed ring never leaves CPU waiters hanging.
+    __atomic_store_n(sem_, std::max(last, completed_seq()), __ATOMIC_RELEASE);
+    RT_ERR("ring %s/%d error %s at %s", ring_kind_str(kind_), dev_, status_str(err_), err_desc_.c_str());
+    tools_event(ToolsEventType::RingError, Cause::User, Loc::gpu(dev_), Loc::gpu(dev_), dev_, 0, 0, 0);
+  }
+  submitted_ = last;
+  batches_++;
+  Tools::get().inc(Counter::RingSubmissions);
+  auto f = std::make_shared<Fence>();
+  f->be = be_;
+  f->dev = dev_;
+  f->ring = this;
+  f->seq = last;
+  last_fence_ = f;
+  return f;
+}
+
+// DMA ring worker: batches complete in submission order.
+void Ring::worker() {
+  for (;;) {
+    Batch b;
+    {
+      std::unique_lock<std::mutex> g(wm_);
+      wcv_.wait(g, [&] { return stop_ || !work_.empty(); });
+      if (work_.empty()) return;  // stop_ with nothing left
+      b = std::move(work_.front());
+      work_.pop_front();
+    }
+    Status st = err_ == Status::OK ? run_batch(b) : err_.load();
+    if (st != Status::OK && err_ == Status::OK) {
+      err_ = st;
+      RT_ERR("ring %s/%d batch up to seq %llu failed: %s (%s)", ring_kind_str(kind_), dev_,
+             (unsigned long long)b.last, status_str(st), be_->last_error().c_str());
+      if (st != Status::INJECTED_ERROR) set_fatal(st, "DMA ring batch failed");
+    }
+    // Publish even on error (robust channel): waiters then see err_.
+    __atomic_store_n(sem_, b.last, __ATOMIC_RELEASE);
+  }
+}
+
+Status Ring::run_batch(Batch& b) {
+  std::vector<CopyDesc> copies;
+  Status st = Status::OK;
+  auto flush = [&] {
+    if (st == Status::OK && !copies.empty()) st = be_->dma_copy(dev_, copies.data(), copies.size(), (int)kind_);
+    copies.clear();
+  };
+  bool stream_used = false;
+  for (auto& s : b.ops) {
+    if (st != Status::OK) break;
+    switch (s.op) {
+      case SqeOp::COPY:
+        if (!copies.empty() && copies.back().dst + copies.back().bytes == s.dst &&
+            copies.back().src + copies.back().bytes == s.src)
+          copies.back().bytes += s.bytes;
+        else
+          copies.push_back(CopyDesc{s.dst, s.src, s.bytes});
+        break;
+      case SqeOp::WAIT_FENCE:
+        // Dependencies are waited for where the copies are issued: here, on
+        // the host, before the engine starts (events of compute streams, other
+        // rings' tracking values).
+        flush();
+        if (st == Status::OK && s.wait && !s.wait->done.load(std::memory_order_acquire)) st = s.wait->wait();
+        break;
+      case SqeOp::NOP:
+        break;
+      default: {
+        // Kernel SQEs (memset, fused decode, page gather / scatter) run on the
+        // side stream, in order with the copies around them.
+        flush();
+        if (st != Status::OK) break;
+        if (s.op == SqeOp::MEMSET) st = be_->memset32(dev_, s.dst, s.pattern, s.bytes, stream_);
+        else if (s.op == SqeOp::DECODE_BF12) {
+          DecodeDesc d{s.src, s.dst, (uint32_t)(s.bytes / 2)};
+          st = be_->decode_bf12(dev_, &d, 1, stream_);
+        } else {
+          PageListDesc d{s.op == SqeOp::GATHER ? s.src : s.dst, s.op == SqeOp::GATHER ? s.dst : s.src, s.idx.data(),
+                         (uint32_t)s.idx.size(), s.page_bytes};
+          st = s.op == SqeOp::GATHER ? be_->gather_pages(dev_, d, stream_) : be_->scatter_pages(dev_, d, stream_);
+        }
+        if (st == Status::OK) st = be_->stream_sync(stream_);
+        stream_used = true;
+        break;
+      }
+    }
+  }
+  flush();
+  (void)stream_used;
+  return st;
+}
+
 FenceRef Ring::submit_locked() {
   if (sq_.empty()) {
     if (last_fence_) return last_fence_;
@@ -68,6 +205,7 @@ FenceRef Ring::submit_locked() {
     f->done.store(true);
     return f;
   }
+  if (dma_) return submit_dma_locked();
   // Hoist the fence waits of every run of copy-like SQEs (COPY / DECODE /
   // WAIT_FENCE / NOP) to the front of the run, so the run becomes ONE
   // copy-kernel launch instead of one launch per wait (each launch boundary is
@@ -152,6 +290,8 @@ FenceRef Ring::submit_locked() {
           flush();
           if (st == Status::OK && s.wait && !s.wait->done.load()) {
             if (s.wait->event) st = be_->stream_wait_event(stream_, s.wait->event);
+            else if (s.wait->ring && s.wait->ring->is_dma())
+              st = be_->wait_value(stream_, s.wait->ring->semaphore(), s.wait->seq);
             else st = s.wait->wait();
           }
           break;

@@ -57,10 +57,11 @@ void Tracker::add(const FenceRef& f) {
   if (!f || f->done.load(std::memory_order_relaxed)) return;
   for (auto& x : fences_)
     if (x == f) return;
-  // Keep only the newest fence per ring: ring fences complete in order.
+  // Keep only the newest fence per ring: ring fences complete in order (DMA
+  // ring fences carry no event; stream ring fences always carry one).
   if (f->ring) {
     for (auto& x : fences_)
-      if (x->ring == f->ring && x->event && f->event) {
+      if (x->ring == f->ring && (x->event != nullptr) == (f->event != nullptr)) {
         if (x->seq <= f->seq) x = f;
         return;
       }
@@ -101,6 +102,7 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
     bool had_event = f->event != nullptr;
     bool ev_done = had_event && be->event_query(f->event);
     if (f->event) s = be->stream_wait_event(stream, f->event);
+    else if (f->ring && f->ring->is_dma()) s = be->wait_value(stream, f->ring->semaphore(), f->seq);
     else s = f->wait();
     uint64_t dt = now_ns() - t0;
     if (dt > 20000000ull)  // a GPU-side dependency should cost microseconds of host time

@@ -90,9 +90,17 @@ class Backend {
   virtual Status stream_wait_event(void* stream, void* e) = 0;
 
   // ---- work submission (ordered on `stream`)
-  // engine: 0 = copy kernel with the PCIe CU budget, 1 = SDMA, 2 = copy kernel
-  // with the whole chip (HBM<->HBM).
+  // engine: 0 = copy kernel with the PCIe CU budget, 1 = hipMemcpyAsync, 2 = copy
+  // kernel with the whole chip (HBM<->HBM).
   virtual Status copy_batch(int dev, const CopyDesc* d, size_t n, void* stream, int engine) = 0;
+  // ---- DMA copy engines (SDMA), driven from a ring's worker thread: no CU, no
+  // stream. `channel` picks the engine (one per ring kind and direction).
+  // dma_copy returns once every copy of the batch has completed.
+  virtual bool dma_supported(int dev) { (void)dev; return false; }
+  virtual Status dma_copy(int dev, const CopyDesc* d, size_t n, int channel) {
+    (void)dev; (void)d; (void)n; (void)channel;
+    return Status::NOT_SUPPORTED;
+  }
   // workgroups = 0: config().decode_workgroups (sized for H2D streaming); HBM->HBM
   // unpacking passes a full-chip grid.
   virtual Status decode_bf12(int dev, const DecodeDesc* d, size_t n, void* stream, uint32_t workgroups = 0) = 0;

@@ -58,7 +58,7 @@ namespace ogkm {
   X(host_budget_mb, 0, "host-tier arena limit in MB (0 = pin budget)")                               \
   /* channels / ring */                                                                              \
   X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \
-  X(copy_engine, 1, "PCIe/xGMI ring copies: 1=hipMemcpyAsync (default) 0=our HIP copy kernels")       \
+  X(copy_engine, 3, "PCIe/xGMI ring copies: 3=SDMA engines driven by the ring's worker (default) 1=hipMemcpyAsync 0=our CU copy kernels") \
   X(copy_workgroups, 16, "workgroups per copy-kernel launch (CU budget; 16 saturate PCIe, more starve HBM-bound compute)") \
   X(copy_piece_kb, 64, "bytes per copy work item (KB)")                                              \
   X(copy_nt_loads, 1, "copy kernels: non-temporal source loads (0 = plain loads)")                      \

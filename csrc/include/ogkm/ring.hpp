@@ -13,11 +13,23 @@
 //     its push description (file:line + text, uvm_push.c:169) so a ring error
 //     can name the work that failed (uvm_channel.c:2080-2112);
 //   * errors are sticky per ring and propagate to the runtime's fatal status.
+//
+// DMA rings (copy_engine 3: CPU_TO_GPU, GPU_TO_CPU, GPU_TO_GPU, CXL when the
+// backend has copy engines): submit() hands the batch to the ring's worker
+// thread, which waits for the batch's fence dependencies, runs its copies on
+// the ring's SDMA engine (Backend::dma_copy - no CU, no stream), its rare
+// kernel SQEs (memset, fused decode, gather/scatter) on the side stream, and
+// then publishes the tracking value with a release store. GPU consumers wait
+// on that value GPU-side (hipStreamWaitValue64), so the fences of a DMA ring
+// carry no event.
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ogkm/backend.hpp"
@@ -82,9 +94,18 @@ class Ring {
   RingKind kind() const { return kind_; }
   uint64_t batches() const { return batches_; }
   std::string last_error_desc();
+  bool is_dma() const { return dma_; }
+  uint64_t* semaphore() const { return sem_; }
 
  private:
+  struct Batch {
+    std::vector<Sqe> ops;   // in submission order (WAIT_FENCE included)
+    uint64_t last = 0;      // tracking value published when the batch is done
+  };
   FenceRef submit_locked();
+  FenceRef submit_dma_locked();
+  void worker();
+  Status run_batch(Batch& b);
   Backend* be_;
   int dev_;
   RingKind kind_;
@@ -100,6 +121,13 @@ class Ring {
   FenceRef last_fence_;
   std::atomic<Status> err_{Status::OK};
   std::string err_desc_;
+  // DMA mode
+  bool dma_ = false;
+  std::thread worker_;
+  std::mutex wm_;
+  std::condition_variable wcv_;
+  std::deque<Batch> work_;
+  bool stop_ = false;
 };
 
 }  // namespace ogkm

@@ -35,6 +35,7 @@ Multi-GPU (one process per GPU, RCCL over xGMI), ``parallel=``:
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import time
@@ -432,6 +433,14 @@ class TieredLlama:
         self.stream_seq = [k for k in self.order if not self._is_resident(k)]
         self._pf_next = 0           # next index in stream_seq to prefetch (cyclic)
         self._inflight: list = []   # prefetched, not yet consumed
+        # Bounded run-ahead: compute events of streamed units enqueued but maybe
+        # not yet run. Leases wait GPU-side, so without a bound the host would
+        # prefetch a whole step ahead and the ring would evict (and wait on)
+        # chunks whose readers are still queued - the copies then serialise
+        # behind compute and the link idles. The host waits for the unit
+        # ``max_ahead`` streamed units back instead (OGKM_MAX_AHEAD).
+        self._ahead = collections.deque()
+        self.max_ahead = int(os.environ.get("OGKM_MAX_AHEAD", "0")) or (self.lookahead + runahead)
         self._views: dict = {}
         self.byte_trace = None     # diagnostics: {key: H2D bytes submitted around its use}
         self.use_trace = None      # diagnostics: [(key, acquire s, wait s)] per streamed use
@@ -730,8 +739,20 @@ class TieredLlama:
         if self.staged:
             st = self._unstage(key, lease.dptr)
             lease.release(0 if self.fake else None)
+            self._mark_consumed()
             return None, st
         return lease, refs
+
+    def _mark_consumed(self) -> None:
+        """A streamed unit's readers are enqueued: remember where the compute
+        stream is, then keep the host at most max_ahead streamed units ahead."""
+        if self.fake:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        self._ahead.append(ev)
+        while len(self._ahead) > self.max_ahead:
+            self._ahead.popleft().synchronize()
 
     def _use_gathered(self, key):
         """shards: fault this rank's shard in (the runtime prefetches streamed
@@ -745,6 +766,7 @@ class TieredLlama:
         if self.staged:
             ref = self._unstage(key, full.data_ptr())
             self.gather.done(key)
+            self._mark_consumed()
             return None, ref
         return ("gather", key), self._ref(key, full.data_ptr(), self.pmode.get(key, dgemm.MODE_RAW))
 
@@ -761,8 +783,10 @@ class TieredLlama:
     def _done(self, lease) -> None:
         if isinstance(lease, tuple):  # a gather slot read by the kernels just enqueued
             self.gather.done(lease[1])
+            self._mark_consumed()
         elif lease is not None:
             lease.release(0 if self.fake else None)
+            self._mark_consumed()
 
     # ------------------------------------------------------------------ decode
     @torch.no_grad()
