@@ -131,11 +131,23 @@ class HipBackend : public Backend {
     ad.location.id = dev;
     ad.flags = hipMemAccessFlagsProtReadWrite;
     HIPCHK(hipMemSetAccess(va, bytes, &ad, 1));
+    std::lock_guard<std::mutex> g(reg_m_);
+    vmm_maps_[(uint64_t)va] = {bytes, dev};
     return Status::OK;
   }
   Status vmm_unmap(void* va, size_t bytes) override {
     HIPCHK(hipMemUnmap(va, bytes));
+    std::lock_guard<std::mutex> g(reg_m_);
+    vmm_maps_.erase((uint64_t)va);
     return Status::OK;
+  }
+  // Device of the VMM mapping that contains `a` (-1 = none).
+  int vmm_dev(uint64_t a) {
+    std::lock_guard<std::mutex> g(reg_m_);
+    auto it = vmm_maps_.upper_bound(a);
+    if (it == vmm_maps_.begin()) return -1;
+    --it;
+    return a < it->first + it->second.first ? it->second.second : -1;
   }
 
   Status host_register(void* p, size_t bytes) override {
@@ -299,6 +311,11 @@ class HipBackend : public Backend {
       }
     }
     hsa_signal_store_relaxed(sig, (hsa_signal_value_t)pieces.size());
+    if (log_level() >= LogLevel::DEBUG)
+      for (auto& pc : pieces)
+        RT_DBG("dma_copy dev %d ch %d: %p (agent %llx) <- %p (agent %llx) %zu B [cpu agent %llx]", dev, channel,
+               pc.dst, (unsigned long long)pc.da.handle, pc.src, (unsigned long long)pc.sa.handle, pc.len,
+               (unsigned long long)dd.cpu.handle);
     for (auto& pc : pieces) {
       const bool h2d = pc.sa.handle == dd.cpu.handle, d2h = pc.da.handle == dd.cpu.handle;
       uint32_t mask = h2d ? dd.h2d : (d2h ? dd.d2h : dd.d2d);
@@ -569,6 +586,8 @@ class HipBackend : public Backend {
     memset(&info, 0, sizeof info);
     info.size = sizeof info;
     if (hsa_amd_pointer_info(p, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS) return false;
+    RT_DBG("dma_resolve %p: type %d agentBase %p hostBase %p size %zu", p, (int)info.type, info.agentBaseAddress,
+           info.hostBaseAddress, info.sizeInBytes);
     switch (info.type) {
       case HSA_EXT_POINTER_TYPE_HSA:
       case HSA_EXT_POINTER_TYPE_HSA_VMEM:
@@ -584,6 +603,20 @@ class HipBackend : public Backend {
         *out = (char*)info.agentBaseAddress + ((char*)p - (char*)info.hostBaseAddress);
         return true;
       default:
+        // Host memory registered through HIP's SVM path is not in ROCr's
+        // allocation map: it is system memory mapped at the same address.
+        if (reg_room((uint64_t)p)) {
+          *agent = dd.cpu;
+          *out = p;
+          return true;
+        }
+        // HBM mapped through the VMM API at an alias VA (stable-VA arenas) is
+        // not in that map either: the GPU VA is what the SDMA engine uses.
+        if (int d = vmm_dev((uint64_t)p); d >= 0 && d < (int)dma_.size()) {
+          *agent = dma_[d].gpu;
+          *out = p;
+          return true;
+        }
         return false;
     }
   }
@@ -609,6 +642,7 @@ class HipBackend : public Backend {
   std::string last_err_;
   std::mutex ev_m_, df_m_, reg_m_;
   std::map<uint64_t, uint64_t> regs_;  // host registrations: base -> bytes
+  std::map<uint64_t, std::pair<uint64_t, int>> vmm_maps_;  // VMM mappings: va -> (bytes, device)
   std::vector<void*> free_events_[64];
   std::map<void*, int> ev_dev_;
   std::map<void*, void*> ipc_base_;  // opened IPC pointer -> mapped allocation base

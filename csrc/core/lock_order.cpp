@@ -1,6 +1,8 @@
 // Lock-order checker (uvm_lock.c:75-145 semantics).
 #include "ogkm/lock_order.hpp"
 
+#include <cstdlib>
+
 #include "ogkm/common.hpp"
 #include "ogkm/config.hpp"
 
@@ -47,6 +49,8 @@ void on_acquire(LockOrder o, bool trylock) {
       int worst = 31 - __builtin_clz(deeper_or_equal);
       RT_ERR("lock order violation: acquiring %s while holding %s", lock_order_name(o),
              lock_order_name((LockOrder)worst));
+      static const bool abort_on = getenv("RT_LOCKCHECK_ABORT") != nullptr;  // debugging: stop at the culprit
+      if (abort_on) abort();
     }
   }
   t_held |= bit;

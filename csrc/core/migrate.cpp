@@ -213,17 +213,11 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
   }
   for (auto& f : reuse.fences()) {
     if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
-    Sqe w;
-    w.op = SqeOp::WAIT_FENCE;
-    w.wait = f;
-    ring->push(std::move(w));
+    ring->push_wait(f);
   }
   for (auto& f : pend.fences()) {
     if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
-    Sqe w;
-    w.op = SqeOp::WAIT_FENCE;
-    w.wait = f;
-    ring->push(std::move(w));
+    ring->push_wait(f);
   }
   if (from->fmt == 1) {
     // Encoded source: one fused copy+decode of the whole block into HBM, or a
@@ -260,6 +254,9 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
   c.use_ring(ring);
   c.touched.push_back({ring, b});
   b->unpublished++;
+  // The pages count as resident from now on: another thread that sources them
+  // before this operation publishes its fence must still wait for the copy.
+  b->tracker.add(ring_fence(ring, ring->pushed_seq()));
   c.chunk_uses.push_back({ring, from->arena, (uint32_t)from->chunk, false});
   tools_event(ToolsEventType::Migration, c.cause, from->loc, to->loc, to->loc.is_gpu() ? to->loc.id : kCpuProc,
               b->range->addr() + b->block_offset(), bytes, b->range->id, t0, 0, ring->pushed_seq());
@@ -287,10 +284,7 @@ static Status zero_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* to, 
   Tracker reuse = to->arena->reuse_fence((uint32_t)to->chunk);
   for (auto& f : reuse.fences()) {
     if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
-    Sqe w;
-    w.op = SqeOp::WAIT_FENCE;
-    w.wait = f;
-    ring->push(std::move(w));
+    ring->push_wait(f);
   }
   pages.for_each_run([&](uint32_t p, uint32_t n) {
     Sqe s;
@@ -305,6 +299,7 @@ static Status zero_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* to, 
   c.use_ring(ring);
   c.touched.push_back({ring, b});
   b->unpublished++;
+  b->tracker.add(ring_fence(ring, ring->pushed_seq()));
   return Status::OK;
 }
 
@@ -359,10 +354,13 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
   // Keep a range's blocks adjacent in the destination arena.
   if (b->index > 0) {
     Block* prev = b->range->block(b->index - 1);
-    // Reading the neighbour's residency without its lock is a heuristic only.
-    if (prev)
+    // A hint only: skip it when the neighbour is busy (trylock keeps the lock
+    // order - two block locks are never waited for at once).
+    if (prev && prev->lock.try_lock()) {
       for (auto& r : prev->res)
         if (r.loc == dst && r.chunk >= 0) hint = r.chunk + 1;
+      prev->lock.unlock();
+    }
   }
   Status st = populate(c, b, dst, hint, &to);
   if (st != Status::OK) return st;
@@ -512,12 +510,20 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
       if (t.block == iv.b && std::find(failed.begin(), failed.end(), t.ring) != failed.end()) bad = true;
     std::lock_guard<OrderedMutex> g(iv.b->lock);
     std::vector<Loc> empty;
+    // Only pages the destination still holds retire their other copies: a
+    // concurrent operation may have revoked (migrated away) some of them since
+    // the copy was queued, and then the source is the copy that must stay.
+    PageMask pages = iv.pages;
+    if (!bad) {
+      Residency* d = iv.b->find(iv.dst);
+      pages = d ? (pages & d->resident) : PageMask{};
+    }
     for (auto& r : iv.b->res) {
       bool is_dst = r.loc == iv.dst;
       if (bad ? !is_dst : is_dst) continue;  // failed copy: the destination is what becomes invalid
-      if (!r.resident.intersects(iv.pages)) continue;
+      if (!r.resident.intersects(pages)) continue;
       if (!bad) Tools::get().inc(Counter::Revocations);
-      r.resident = r.resident.andnot(iv.pages);
+      r.resident = r.resident.andnot(pages);
       if (r.resident.empty()) empty.push_back(r.loc);
     }
     for (auto& l : empty) release_residency_now(iv.b, l);
@@ -761,6 +767,21 @@ Status Runtime::evict_range(Range* r, Loc from) {
 // and resident pages are relocated D2D. With a lease, chunks are pinned.
 Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
                                     Lease* L, Tracker* out, Cause cause) {
+  // An extent found in place can lose a block to a concurrent eviction between
+  // the check and the copies (its chunk may already back another block): the
+  // placement then starts over and relocates the span into a fresh extent.
+  Status st = Status::OK;
+  for (int round = 0; round < 8; ++round) {
+    bool conflict = false;
+    st = place_extent(r, off, len, gpu, read_dup, L, out, cause, &conflict);
+    if (!conflict) return st;
+    Tools::get().inc(Counter::AllocRetries);
+  }
+  return st;
+}
+
+Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
+                             Lease* L, Tracker* out, Cause cause, bool* conflict) {
   Loc dst = Loc::gpu(gpu);
   ChunkArena* ga = arena_for(dst);
   if (!ga) return Status::INVALID_ARGUMENT;
@@ -808,6 +829,14 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
     if (st != Status::OK) return st;
   }
   std::vector<Block*> done;
+  // Extent chunks handed to their block: from then on the block owns (and may
+  // drop) the chunk, so the allocation pin is released at hand-over, under the
+  // block lock; chunks never handed over are freed (still pinned) at the end.
+  std::vector<uint8_t> handed(n, 0);
+  auto hand_over = [&](uint32_t k) {
+    handed[k] = 1;
+    ga->unpin((uint32_t)(first + k));
+  };
   for (uint32_t k = 0; k < n && st == Status::OK; ++k) {
     Block* b = r->block(b0 + k);
     uint32_t target = (uint32_t)(first + k);
@@ -815,7 +844,11 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
       {
         std::lock_guard<OrderedMutex> g(b->lock);
         Residency* x = b->find(dst);
-        if (x && x->chunk != (int64_t)target && b->lease_pins) {
+        if (in_place && (!x || x->chunk != (int64_t)target)) {
+          // Evicted since the in-place check: `target` is not ours any more.
+          *conflict = true;
+          st = Status::BUSY;
+        } else if (x && x->chunk != (int64_t)target && b->lease_pins) {
           st = Status::BUSY;  // another lease pins this block's chunk: it cannot move
         } else if (x && x->chunk != (int64_t)target) {
           // Relocate: copy the resident pages into the new extent (D2D).
@@ -839,6 +872,9 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
             if (!queued) x->arena->free((uint32_t)x->chunk, 1);
             x->chunk = target;
             x->arena = ga;
+            hand_over(k);
+          } else {
+            ga->set_owner(target, nullptr);
           }
         } else if (!x) {
           ga->set_owner(target, b);
@@ -846,6 +882,7 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
           nr.arena = ga;
           nr.chunk = target;
           nr.resident.zero();
+          if (!in_place) hand_over(k);
         }
         if (st == Status::OK) {
           PageMask want = pages_of(b0 + k);
@@ -881,18 +918,9 @@ Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gp
       c.need_arena = nullptr;
     }
   }
-  if (!in_place) {
-    for (uint32_t k = 0; k < n; ++k) ga->unpin((uint32_t)(first + k));
-    // Chunks of the extent that were never handed to a block (error path) go back.
-    if (st != Status::OK)
-      for (uint32_t k = 0; k < n; ++k) {
-        Block* b = r->block(b0 + k);
-        bool used = false;
-        for (Block* d : done)
-          if (d == b) used = true;
-        if (!used && ga->owner((uint32_t)(first + k)) == nullptr) ga->free((uint32_t)(first + k), 1);
-      }
-  }
+  if (!in_place)
+    for (uint32_t k = 0; k < n; ++k)
+      if (!handed[k]) ga->free((uint32_t)(first + k), 1);  // error path: never handed over
   Status fs = finish_ctx(c, out);
   if (st == Status::OK) st = fs;
   if (st != Status::OK) {

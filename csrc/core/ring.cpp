@@ -50,6 +50,17 @@ Ring::~Ring() {
   if (sem_) be_->host_free_coherent(sem_);
 }
 
+void Ring::push_wait(const FenceRef& f) {
+  if (!f || f->ring == this || f->done.load(std::memory_order_relaxed)) return;
+  // A tracking-value fence of another ring must be submitted before anything
+  // waits on it (never from inside a submission: two ring locks at once).
+  if (f->ring && !f->event && f->seq > f->ring->submitted_seq()) f->ring->submit();
+  Sqe w;
+  w.op = SqeOp::WAIT_FENCE;
+  w.wait = f;
+  push(std::move(w));
+}
+
 uint64_t Ring::push(Sqe&& s) {
   std::unique_lock<OrderedMutex> g(m_);
   // SQ full (GPFIFO full): submit, then wait for the oldest in-flight entries.
@@ -147,54 +158,76 @@ void Ring::worker() {
 }
 
 Status Ring::run_batch(Batch& b) {
+  // Copies go to the engine (synchronously, from this thread); kernel SQEs
+  // (fused decode, memset, page gather / scatter) go to the side stream
+  // asynchronously - consecutive decodes as ONE launch - so a decode overlaps
+  // the engine copies after it. The stream is drained before an engine copy
+  // that follows kernels (the copy may read their output) and at batch end.
   std::vector<CopyDesc> copies;
+  std::vector<DecodeDesc> decodes;
   Status st = Status::OK;
-  auto flush = [&] {
-    if (st == Status::OK && !copies.empty()) st = be_->dma_copy(dev_, copies.data(), copies.size(), (int)kind_);
+  bool kernels_pending = false;
+  auto drain = [&] {
+    if (st == Status::OK && kernels_pending) st = be_->stream_sync(stream_);
+    kernels_pending = false;
+  };
+  auto flush_decodes = [&] {
+    if (st == Status::OK && !decodes.empty()) {
+      st = be_->decode_bf12(dev_, decodes.data(), decodes.size(), stream_);
+      kernels_pending = true;
+    }
+    decodes.clear();
+  };
+  auto flush_copies = [&] {
+    if (!copies.empty()) {
+      drain();
+      if (st == Status::OK) st = be_->dma_copy(dev_, copies.data(), copies.size(), (int)kind_);
+    }
     copies.clear();
   };
-  bool stream_used = false;
   for (auto& s : b.ops) {
     if (st != Status::OK) break;
     switch (s.op) {
       case SqeOp::COPY:
+        flush_decodes();
         if (!copies.empty() && copies.back().dst + copies.back().bytes == s.dst &&
             copies.back().src + copies.back().bytes == s.src)
           copies.back().bytes += s.bytes;
         else
           copies.push_back(CopyDesc{s.dst, s.src, s.bytes});
         break;
+      case SqeOp::DECODE_BF12:
+        flush_copies();
+        decodes.push_back(DecodeDesc{s.src, s.dst, (uint32_t)(s.bytes / 2)});
+        break;
       case SqeOp::WAIT_FENCE:
-        // Dependencies are waited for where the copies are issued: here, on
-        // the host, before the engine starts (events of compute streams, other
-        // rings' tracking values).
-        flush();
+        // Dependencies are waited for where the work is issued: here, on the
+        // host, before the engine / stream is handed anything after the wait.
+        flush_decodes();
+        flush_copies();
         if (st == Status::OK && s.wait && !s.wait->done.load(std::memory_order_acquire)) st = s.wait->wait();
         break;
       case SqeOp::NOP:
         break;
       default: {
-        // Kernel SQEs (memset, fused decode, page gather / scatter) run on the
-        // side stream, in order with the copies around them.
-        flush();
+        flush_decodes();
+        flush_copies();
         if (st != Status::OK) break;
-        if (s.op == SqeOp::MEMSET) st = be_->memset32(dev_, s.dst, s.pattern, s.bytes, stream_);
-        else if (s.op == SqeOp::DECODE_BF12) {
-          DecodeDesc d{s.src, s.dst, (uint32_t)(s.bytes / 2)};
-          st = be_->decode_bf12(dev_, &d, 1, stream_);
+        if (s.op == SqeOp::MEMSET) {
+          st = be_->memset32(dev_, s.dst, s.pattern, s.bytes, stream_);
         } else {
           PageListDesc d{s.op == SqeOp::GATHER ? s.src : s.dst, s.op == SqeOp::GATHER ? s.dst : s.src, s.idx.data(),
                          (uint32_t)s.idx.size(), s.page_bytes};
           st = s.op == SqeOp::GATHER ? be_->gather_pages(dev_, d, stream_) : be_->scatter_pages(dev_, d, stream_);
         }
-        if (st == Status::OK) st = be_->stream_sync(stream_);
-        stream_used = true;
+        kernels_pending = true;
         break;
       }
     }
   }
-  flush();
-  (void)stream_used;
+  flush_decodes();
+  flush_copies();
+  drain();
   return st;
 }
 
@@ -290,7 +323,8 @@ FenceRef Ring::submit_locked() {
           flush();
           if (st == Status::OK && s.wait && !s.wait->done.load()) {
             if (s.wait->event) st = be_->stream_wait_event(stream_, s.wait->event);
-            else if (s.wait->ring && s.wait->ring->is_dma())
+            else if (s.wait->ring && s.wait->ring != this)
+              // tracking-value fence (its ring was submitted when the wait was pushed)
               st = be_->wait_value(stream_, s.wait->ring->semaphore(), s.wait->seq);
             else st = s.wait->wait();
           }

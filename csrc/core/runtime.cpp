@@ -4,9 +4,7 @@
 #include "ogkm/runtime.hpp"
 #include "ogkm/codec.hpp"
 
-#include <signal.h>
 #include <sys/mman.h>
-#include <ucontext.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -69,6 +67,7 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
   }
   g_rt.store(rt, std::memory_order_release);
   install_cpu_fault_handler();
+  start_cpu_fault_service();
   RT_INFO("runtime up: backend=%s devices=%d local=0x%llx host_node=%d cxl_nodes=%zu", rt->be_->name(), nd,
           (unsigned long long)mask, rt->host_node_, rt->cxl_topo_.info().numa_nodes.size());
   return rt;
@@ -88,6 +87,7 @@ void Runtime::shutdown() {
 }
 
 Runtime::~Runtime() {
+  stop_cpu_fault_service();
   stop_fault_service();
   for (auto& d : devs_)
     for (auto& r : d->rings)
@@ -193,7 +193,10 @@ Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string&
     r->dev_va = va;
     r->stable_dev = stable_dev;
   }
-  if (r->cpu_view) vs_.tree[r->addr()] = r.get();
+  if (r->cpu_view) {
+    vs_.tree[r->addr()] = r.get();
+    cpu_views_add(r->addr(), r->cpu_view_bytes);  // the SIGSEGV handler's lock-free index
+  }
   *out = r.get();
   vs_.ranges[id] = std::move(r);
   return Status::OK;
@@ -249,7 +252,10 @@ Status Runtime::free_range(Range* r) {
     auto& v = r->group->ranges;
     v.erase(std::remove(v.begin(), v.end(), r), v.end());
   }
-  if (r->cpu_view) vs_.tree.erase(r->addr());
+  if (r->cpu_view) {
+    cpu_views_remove(r->addr());
+    vs_.tree.erase(r->addr());
+  }
   {
     std::lock_guard<std::mutex> g(dev_tables_m_);
     auto t = dev_tables_.find(r->id);
@@ -668,12 +674,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
                                       : ring(src_dev, RingKind::GPU_TO_CPU);
             Tracker rf = to->arena->reuse_fence((uint32_t)to->chunk);
             rf.merge(b->tracker);
-            for (auto& f : rf.fences()) {
-              Sqe w;
-              w.op = SqeOp::WAIT_FENCE;
-              w.wait = f;
-              rg->push(std::move(w));
-            }
+            for (auto& f : rf.fences()) rg->push_wait(f);
             Sqe cp;
             cp.op = SqeOp::COPY;
             cp.dst = dst_addr;
@@ -1208,41 +1209,6 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
     }
   }
   return Status::OK;
-}
-
-// ------------------------------------------------------------------ SIGSEGV
-static struct sigaction g_prev_segv;
-static std::atomic<bool> g_handler_installed{false};
-
-static void segv_handler(int sig, siginfo_t* si, void* uc) {
-  Runtime* rt = Runtime::get();
-  uint64_t addr = (uint64_t)si->si_addr;
-  bool write = false;
-#if defined(__x86_64__)
-  write = (((ucontext_t*)uc)->uc_mcontext.gregs[REG_ERR] & 2) != 0;
-#endif
-  if (rt && rt->cpu_fault(addr, write) == Status::OK) return;
-  if (g_prev_segv.sa_flags & SA_SIGINFO) {
-    if (g_prev_segv.sa_sigaction) {
-      g_prev_segv.sa_sigaction(sig, si, uc);
-      return;
-    }
-  } else if (g_prev_segv.sa_handler != SIG_DFL && g_prev_segv.sa_handler != SIG_IGN) {
-    g_prev_segv.sa_handler(sig);
-    return;
-  }
-  signal(SIGSEGV, SIG_DFL);  // re-fault with the default action
-}
-
-void install_cpu_fault_handler() {
-  bool expected = false;
-  if (!g_handler_installed.compare_exchange_strong(expected, true)) return;
-  struct sigaction sa;
-  memset(&sa, 0, sizeof sa);
-  sa.sa_sigaction = segv_handler;
-  sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
-  sigemptyset(&sa.sa_mask);
-  sigaction(SIGSEGV, &sa, &g_prev_segv);
 }
 
 }  // namespace ogkm

@@ -53,6 +53,14 @@ FenceRef fence_record(Backend* be, int dev, void* stream, Ring* ring, uint64_t s
   return f;
 }
 
+FenceRef ring_fence(Ring* ring, uint64_t seq) {
+  auto f = std::make_shared<Fence>();
+  f->ring = ring;
+  f->seq = seq;
+  f->dev = ring->dev();
+  return f;
+}
+
 void Tracker::add(const FenceRef& f) {
   if (!f || f->done.load(std::memory_order_relaxed)) return;
   for (auto& x : fences_)
@@ -102,7 +110,12 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
     bool had_event = f->event != nullptr;
     bool ev_done = had_event && be->event_query(f->event);
     if (f->event) s = be->stream_wait_event(stream, f->event);
-    else if (f->ring && f->ring->is_dma()) s = be->wait_value(stream, f->ring->semaphore(), f->seq);
+    else if (f->ring) {
+      // Tracking-value fence: make sure the ring work is submitted, then let
+      // the stream wait for the ring's semaphore GPU-side.
+      if (f->seq > f->ring->submitted_seq()) f->ring->submit();
+      s = be->wait_value(stream, f->ring->semaphore(), f->seq);
+    }
     else s = f->wait();
     uint64_t dt = now_ns() - t0;
     if (dt > 20000000ull)  // a GPU-side dependency should cost microseconds of host time

@@ -39,6 +39,17 @@ Residency& Block::get_or_add(const Loc& l) {
 void Block::drop(const Loc& l) {
   for (size_t i = 0; i < res.size(); ++i)
     if (res[i].loc == l) {
+      // The chunk is about to be freed or handed to another block: a CPU view
+      // that still maps it must lose the mapping first, or a concurrent CPU
+      // access would read (or write) the chunk's next owner.
+      if (cpu_arena && cpu_arena == res[i].arena && cpu_chunk == res[i].chunk && range->cpu_view) {
+        mmap(range->cpu_view + block_offset(), kBlockSize, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE,
+             -1, 0);
+        cpu_arena = nullptr;
+        cpu_chunk = -1;
+        cpu_ro.zero();
+        cpu_rw.zero();
+      }
       res.erase(res.begin() + i);
       return;
     }

@@ -78,6 +78,8 @@ class Ring {
   ~Ring();
   // Append an SQE. Returns its sequence number (tracking value).
   uint64_t push(Sqe&& s);
+  // Append a WAIT_FENCE on `f` (skipped for this ring's own / completed fences).
+  void push_wait(const FenceRef& f);
   // Submit everything pushed so far; returns the fence of the last batch
   // (an already-completed fence if nothing was pending).
   FenceRef submit();
@@ -115,7 +117,7 @@ class Ring {
   OrderedMutex m_{LockOrder::RING};
   std::deque<std::pair<uint64_t, Sqe>> sq_;   // pushed, not yet submitted
   std::deque<std::pair<uint64_t, Cqe>> inflight_;  // submitted, not yet reaped
-  uint64_t next_seq_ = 1;
+  std::atomic<uint64_t> next_seq_{1};  // read lock-free by pushed_seq()
   std::atomic<uint64_t> submitted_{0};  // read lock-free by wait_seq
   uint64_t batches_ = 0;
   FenceRef last_fence_;

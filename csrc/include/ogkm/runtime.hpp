@@ -244,6 +244,8 @@ class Runtime {
   Tracker published_tracker(Block* b);  // tracker once all queued copies into b published their fences
   Status gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
                              Lease* L, Tracker* out, Cause cause);
+  Status place_extent(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup, Lease* L,
+                      Tracker* out, Cause cause, bool* conflict);
   Status queue_copy(Ctx& c, Block* b, Residency* from, Residency* to, const PageMask& pages);
   void update_device_table(Block* b);
 
@@ -321,7 +323,13 @@ enum class ThrashHint { NONE = 0, THROTTLE = 1, PIN = 2 };
 ThrashHint thrash_on_migration(Block* b, int dst_slot, uint64_t now);
 bool thrash_pinned(Block* b, uint64_t now);
 
-// SIGSEGV handler installation for CPU faults on managed CPU views.
+// CPU faults on managed CPU views (csrc/core/cpu_fault.cpp): an
+// async-signal-safe SIGSEGV handler posts the fault to a service thread.
 void install_cpu_fault_handler();
+void start_cpu_fault_service();
+void stop_cpu_fault_service();
+void cpu_views_add(uint64_t start, uint64_t bytes);
+void cpu_views_remove(uint64_t start);
+void cpu_fault_stats(uint64_t* serviced, uint64_t* passed_on);
 
 }  // namespace ogkm

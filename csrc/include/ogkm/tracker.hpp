@@ -35,6 +35,10 @@ using FenceRef = std::shared_ptr<Fence>;
 
 // Records an event on `stream` and wraps it in a fence.
 FenceRef fence_record(Backend* be, int dev, void* stream, Ring* ring = nullptr, uint64_t seq = 0);
+// A fence on ring work by tracking value alone (no event): valid as soon as the
+// SQE is pushed, before the ring is submitted - waiting on it submits the ring;
+// GPU-side waits use the ring's tracking semaphore.
+FenceRef ring_fence(Ring* ring, uint64_t seq);
 
 class Tracker {
  public:

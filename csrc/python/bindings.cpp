@@ -406,6 +406,10 @@ PYBIND11_MODULE(_ogkm, m) {
     py::dict d;
     for (int c = 0; c < (int)Counter::NumCounters; ++c) d[counter_name((Counter)c)] = Tools::get().counter((Counter)c);
     d["lock_violations"] = lockcheck::violations();
+    uint64_t cf_serviced = 0, cf_passed = 0;
+    cpu_fault_stats(&cf_serviced, &cf_passed);
+    d["cpu_faults_serviced"] = cf_serviced;  // by the CPU-fault service thread
+    d["cpu_faults_passed_on"] = cf_passed;   // not ours: chained to the previous handler
     py::list arenas;
     for (int g = 0; g < r->ndev(); ++g) {
       if (!r->dev(g).hbm) continue;

@@ -306,16 +306,23 @@ static void test_no_shared_chunks_under_concurrency() {
       }
     });
   std::thread checker([&] {
+    // A consistent snapshot: every block locked at once (trylock, all or none -
+    // two block locks are never waited for together).
+    std::vector<Block*> all;
+    for (Range* r : rs)
+      for (auto& bp : r->blocks) all.push_back(bp.get());
     while (!stop.load()) {
-      std::vector<std::pair<ChunkArena*, int64_t>> seen;
-      for (Range* r : rs)
-        for (auto& bp : r->blocks) {
-          std::lock_guard<OrderedMutex> g(bp->lock);
-          for (auto& x : bp->res)
+      size_t got = 0;
+      while (got < all.size() && all[got]->lock.try_lock()) ++got;
+      if (got == all.size()) {
+        std::vector<std::pair<ChunkArena*, int64_t>> seen;
+        for (Block* b : all)
+          for (auto& x : b->res)
             if (x.loc.is_gpu() && x.chunk >= 0) seen.emplace_back(x.arena, x.chunk);
-        }
-      std::sort(seen.begin(), seen.end());
-      if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) shared++;
+        std::sort(seen.begin(), seen.end());
+        if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) shared++;
+      }
+      for (size_t i = 0; i < got; ++i) all[i]->lock.unlock();
       std::this_thread::yield();
     }
   });
@@ -324,7 +331,11 @@ static void test_no_shared_chunks_under_concurrency() {
   checker.join();
   CHECK(bad.load() == 0);
   CHECK(shared.load() == 0);
-  CHECK(rt->dev(0).hbm->check().empty());
+  {
+    std::string why = rt->dev(0).hbm->check();
+    if (!why.empty()) fprintf(stderr, "hbm check: %s\n", why.c_str());
+    CHECK(why.empty());
+  }
   for (int i = 0; i < (int)rs.size(); ++i) {
     std::vector<uint8_t> back(rs[i]->size);
     CHECK(rt->read(rs[i], 0, back.data(), back.size(), -1) == Status::OK);
@@ -332,6 +343,82 @@ static void test_no_shared_chunks_under_concurrency() {
   }
   for (Range* r : rs) CHECK(rt->free_range(r) == Status::OK);
   CHECK(lockcheck::violations() == 0);
+  Runtime::shutdown();
+}
+
+// Reads a managed CPU view. Not TSan-instrumented: TSan keeps no shadow for the
+// view's PROT_NONE reservation (later mprotect'ed page by page by the runtime),
+// so an instrumented access would fault inside TSan itself.
+__attribute__((no_sanitize("thread"), noinline)) static uint32_t view_read(const uint32_t* p) {
+  return *(const volatile uint32_t*)p;
+}
+
+// Many threads touch the CPU views of managed ranges (SIGSEGV -> service
+// thread -> cpu_fault) while other threads lease the same ranges on a fake GPU
+// and migrate them back and forth. Under TSan this also checks that the signal
+// handler does nothing signal-unsafe (TSan reports malloc / locks in handlers).
+static void test_cpu_faults_concurrent() {
+  Runtime* rt = Runtime::init("fake", 1, 64ull << 20);
+  CHECK(rt->init_device(0, 16ull << 20) == Status::OK);
+  const int nr = 4;
+  const uint64_t sz = 4ull << 20;
+  std::vector<Range*> rs;
+  for (int i = 0; i < nr; ++i) {
+    Range* r = nullptr;
+    CHECK(rt->malloc_managed(sz, 0, "cf" + std::to_string(i), &r) == Status::OK);
+    std::vector<uint32_t> data(sz / 4);
+    for (size_t k = 0; k < data.size(); ++k) data[k] = (uint32_t)(i * 0x1000000 + k);
+    CHECK(rt->write(r, 0, data.data(), sz, -1) == Status::OK);
+    rs.push_back(r);
+  }
+  // Move every range to the GPU first: the views lose their mappings, so the
+  // readers' first touches fault.
+  for (int i = 0; i < nr; ++i) {
+    Lease* l = nullptr;
+    CHECK(rt->acquire(rs[i], 0, sz, 0, Access::WRITE, &l) == Status::OK);
+    if (!l) continue;
+    l->ready.wait();
+    rt->release(l, nullptr);
+  }
+  std::atomic<int> bad{0};
+  std::atomic<bool> stop{false};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 6; ++t)
+    th.emplace_back([&, t] {  // CPU readers through the views (real page faults)
+      for (int k = 0; k < 300; ++k) {
+        int i = (t + k) % nr;
+        const uint32_t* v = (const uint32_t*)rs[i]->addr();
+        size_t idx = ((size_t)k * 7919 + t * 104729) % (sz / 4);
+        uint32_t got = view_read(v + idx);
+        if (got != (uint32_t)(i * 0x1000000 + idx)) {
+          if (bad++ < 4)
+            fprintf(stderr, "cpu-fault test: range %d idx %zu read %08x want %08x\n", i, idx, got,
+                    (uint32_t)(i * 0x1000000 + idx));
+        }
+      }
+    });
+  std::thread gpu([&] {  // a GPU user pulling the ranges into (tiny) HBM and out again
+    for (int k = 0; !stop.load() && k < 200; ++k) {
+      Lease* l = nullptr;
+      Range* r = rs[k % nr];
+      // WRITE: the GPU copy becomes the only one, the CPU views lose their mapping
+      if (rt->acquire(r, 0, sz, 0, Access::WRITE, &l) != Status::OK) continue;
+      l->ready.wait();
+      rt->release(l, nullptr);
+      Tracker t;
+      rt->prefetch(r, 0, sz, rt->cpu_loc(), &t);
+      t.wait();
+    }
+  });
+  for (auto& x : th) x.join();
+  stop.store(true);
+  gpu.join();
+  CHECK(bad.load() == 0);
+  uint64_t serviced = 0, passed = 0;
+  cpu_fault_stats(&serviced, &passed);
+  CHECK(serviced > 0);
+  CHECK(passed == 0);
+  for (Range* r : rs) CHECK(rt->free_range(r) == Status::OK);
   Runtime::shutdown();
 }
 
@@ -345,6 +432,7 @@ int main() {
   RUN(test_runtime_end_to_end);
   RUN(test_reuse_fence_not_consumed);
   RUN(test_no_shared_chunks_under_concurrency);
+  RUN(test_cpu_faults_concurrent);
   if (g_fail) {
     fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

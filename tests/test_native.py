@@ -61,7 +61,7 @@ def _run(exe: Path, env_extra: dict) -> None:
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
 def test_core_asan_ubsan():
     exe = _build("asan", ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
-    _run(exe, {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "UBSAN_OPTIONS": "print_stacktrace=1",
+    _run(exe, {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:allow_user_segv_handler=1", "UBSAN_OPTIONS": "print_stacktrace=1",
                "RT_LOG": "error"})
 
 
