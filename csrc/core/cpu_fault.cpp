@@ -262,3 +262,34 @@ void install_cpu_fault_handler() {
 }
 
 }  // namespace ogkm
+
+namespace ogkm {
+
+// Host-side producer of the device fault-buffer protocol (ogkm/fault_abi.hpp).
+bool fault_buf_produce(FaultBufHeader* h, DeviceFaultRecord* recs, uint32_t entries, DeviceFaultRecord rec,
+                       bool may_drop) {
+  if (may_drop && __atomic_load_n(&h->put, __ATOMIC_RELAXED) - __atomic_load_n(&h->get, __ATOMIC_ACQUIRE) >= entries) {
+    __atomic_fetch_add(&h->overflow, 1u, __ATOMIC_RELAXED);
+    return false;
+  }
+  const uint32_t p = __atomic_fetch_add(&h->put, 1u, __ATOMIC_RELAXED);
+  auto t0 = std::chrono::steady_clock::now();
+  while (p - __atomic_load_n(&h->get, __ATOMIC_ACQUIRE) >= entries) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+      __atomic_fetch_add(&h->overflow, 1u, __ATOMIC_RELAXED);  // overwrite: the old record counts as lost
+      break;
+    }
+    std::this_thread::yield();
+  }
+  DeviceFaultRecord* slot = &recs[p & (entries - 1)];
+  slot->range_id = rec.range_id;
+  slot->block = rec.block;
+  slot->page = rec.page;
+  slot->access = rec.access;
+  slot->kind = rec.kind;
+  slot->proc = rec.proc;
+  __atomic_store_n(&slot->seq, p + 1, __ATOMIC_RELEASE);
+  return true;
+}
+
+}  // namespace ogkm

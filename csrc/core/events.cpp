@@ -129,7 +129,10 @@ const char* counter_name(Counter c) {
                             "alloc_retries",
                             "injected_errors",
                             "decoded_bytes",
-                            "encoded_bytes"};
+                            "encoded_bytes",
+                            "table_shootdowns",
+                            "fault_replays",
+                            "fault_records_consumed"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -308,6 +308,7 @@ static void drop_residency(Runtime::Ctx& c, Block* b, const Loc& l) {
   Residency* r = b->find(l);
   if (!r) return;
   if (r->chunk >= 0) {
+    Runtime::get()->shootdown(b, r);
     bool queued = false;
     for (auto& u : c.chunk_uses)
       if (u.arena == r->arena && u.chunk == (uint32_t)r->chunk) {
@@ -465,6 +466,7 @@ static void release_residency_now(Block* b, const Loc& l) {
   Residency* r = b->find(l);
   if (!r) return;
   if (r->chunk >= 0) {
+    Runtime::get()->shootdown(b, r);
     for (auto& f : b->tracker.fences()) r->arena->add_reuse_fence((uint32_t)r->chunk, f);
     r->arena->free((uint32_t)r->chunk, 1);
   }
@@ -593,6 +595,7 @@ Status Runtime::evict_chunk(ChunkArena* a, uint32_t i) {
       // Detach the chunk from the block; the arena keeps it reserved for the
       // evicting allocator, fenced on the copy-out.
       Tracker pend = b->tracker;
+      shootdown(b, r);
       b->drop(from);
       c.cpu_refresh.push_back(b);
       for (auto& f : pend.fences()) a->add_reuse_fence(i, f);
@@ -860,6 +863,7 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
           tmp.chunk = target;
           st = copy_pages(this, c, b, x, &tmp, x->resident);
           if (st == Status::OK) {
+            shootdown(b, x);
             bool queued = false;
             for (auto& u : c.chunk_uses)
               if (u.arena == x->arena && u.chunk == (uint32_t)x->chunk && !u.free_after) {
@@ -1330,36 +1334,76 @@ Status Runtime::cpu_fault(uint64_t addr, bool write) {
 }
 
 // ------------------------------------------------------------------ device faults
+size_t Runtime::drain_fault_records(int dev, std::vector<DeviceFaultRecord>* out, size_t max) {
+  if (!is_local(dev)) return 0;
+  DeviceFaultBuffer& fb = devs_[dev]->fault_buf;
+  if (!fb.hdr) return 0;
+  FaultBufHeader* h = fb.hdr;
+  uint32_t ov = __atomic_load_n(&h->overflow, __ATOMIC_RELAXED);
+  if (ov != fb.overflow_seen) {
+    uint32_t lost = ov - fb.overflow_seen;
+    fb.overflow_seen = ov;
+    fb.overflows += lost;
+    tools_event(ToolsEventType::FaultBufferOverflow, Cause::User, Loc{}, Loc{}, dev, 0, lost, 0);
+  }
+  uint32_t get = __atomic_load_n(&h->get, __ATOMIC_RELAXED);  // only the host writes GET
+  const uint32_t put = __atomic_load_n(&h->put, __ATOMIC_ACQUIRE);
+  size_t n = 0;
+  uint64_t lost = 0;
+  while (get != put && n < max) {
+    const DeviceFaultRecord* rec = &fb.recs[get & (fb.entries - 1)];
+    // A reserved slot becomes valid when its producer stores the sequence
+    // number; a producer between the two steps is waited for briefly, else the
+    // rest is left for the next poll (GET stops at the first unpublished slot).
+    // A later lap's seq means a producer that gave up waiting overwrote it.
+    int state = 0;  // 1 valid, 2 overwritten
+    for (int spin = 0; spin < 20000 && !state; ++spin) {
+      uint32_t seq = __atomic_load_n(&rec->seq, __ATOMIC_ACQUIRE);
+      if (seq == get + 1) state = 1;
+      else if ((int32_t)(seq - (get + 1)) > 0) state = 2;
+      else if (spin > 64) std::this_thread::yield();
+    }
+    if (!state) break;
+    if (state == 1) {
+      DeviceFaultRecord copy = *rec;
+      if (__atomic_load_n(&rec->seq, __ATOMIC_ACQUIRE) == get + 1) out->push_back(copy);
+      else ++lost;
+    } else {
+      ++lost;
+    }
+    ++get;
+    ++n;
+  }
+  (void)lost;  // an overwriting producer already counted it in hdr->overflow
+  __atomic_store_n(&h->get, get, __ATOMIC_RELEASE);  // hands the slots back to producers
+  Tools::get().inc(Counter::FaultRecordsConsumed, n);
+  return n;
+}
+
 size_t Runtime::poll_device_faults(int dev) {
   if (!is_local(dev)) return 0;
   DeviceFaultBuffer& fb = devs_[dev]->fault_buf;
-  if (!fb.put) return 0;
-  static std::mutex poll_m;  // the service thread and API callers drain one at a time
-  std::unique_lock<std::mutex> pg(poll_m);
-  uint32_t put = __atomic_load_n(fb.put, __ATOMIC_ACQUIRE);
-  uint32_t n = std::min(put, fb.entries);
-  if (put > fb.entries) {
-    fb.overflows += put - fb.entries;
-    tools_event(ToolsEventType::FaultBufferOverflow, Cause::User, Loc{}, Loc{}, dev, 0, put - fb.entries, 0);
-  }
+  if (!fb.hdr) return 0;
+  std::unique_lock<std::mutex> pg(poll_m_);  // the service thread and API callers drain one at a time
+  std::vector<DeviceFaultRecord> recs;
+  size_t n = drain_fault_records(dev, &recs, fb.entries);
   std::vector<FaultEntry> faults;
   std::vector<std::pair<uint64_t, uint32_t>> remote_hits;
-  for (uint32_t i = 0; i < n; ++i) {
-    const DeviceFaultRecord& rec = fb.recs[i];
+  for (const DeviceFaultRecord& rec : recs) {
     if (rec.kind == 1) {
       remote_hits.emplace_back(rec.range_id, rec.block);
       continue;
     }
     FaultEntry f;
     f.range_id = rec.range_id;
-    f.offset = ((uint64_t)rec.block << kBlockShift) + ((uint64_t)rec.page << kPageShift);
-    f.bytes = kPageSize;
+    const bool whole = rec.page == kFaultWholeBlock;  // a gate needs the whole block in HBM
+    f.offset = ((uint64_t)rec.block << kBlockShift) + (whole ? 0 : ((uint64_t)rec.page << kPageShift));
+    f.bytes = whole ? kBlockSize : kPageSize;
     f.proc = (int)rec.proc;
     f.access = rec.access == 2 ? Access::WRITE : Access::READ;
     faults.push_back(f);
   }
-  __atomic_store_n(fb.put, 0u, __ATOMIC_RELEASE);
-  pg.unlock();
+  Tools::get().inc(Counter::GpuPageFaultCount, faults.size());
   // Access counters (uvm_gpu_access_counters.c:1617): migrate hot remote blocks.
   int64_t mig = config().perf_access_counter_migration_enable;
   if (!remote_hits.empty()) {
@@ -1372,6 +1416,8 @@ size_t Runtime::poll_device_faults(int dev) {
         Block* b = r->block(h.second);
         std::lock_guard<OrderedMutex> g(b->lock);
         Tools::get().inc(Counter::AccessCounterNotifications);
+        tools_event(ToolsEventType::AccessCounter, Cause::AccessCounters, Loc{}, Loc::gpu(dev), dev,
+                    r->addr() + b->block_offset(), kBlockSize, r->id);
         uint32_t& cnt = b->counters.remote_hits[dev];
         if (++cnt >= (uint64_t)config().perf_access_counter_threshold) {
           cnt = 0;
@@ -1391,6 +1437,24 @@ size_t Runtime::poll_device_faults(int dev) {
     Tracker t;
     service_faults(faults, &t);
     t.wait();
+    // The batch has landed: publish the new residency to the device tables
+    // (entries stay 0 while copies are in flight), then replay - kernels
+    // stalled in k_fault_gate re-check and proceed (BATCH_FLUSH policy).
+    {
+      std::shared_lock<OrderedRWLock> vg(vs_.lock);
+      for (auto& f : faults) {
+        Range* r = vs_.by_id_locked(f.range_id);
+        if (!r || f.block >= r->nblocks) continue;
+        Block* b = r->block(f.block);
+        published_tracker(b).wait();
+        std::lock_guard<OrderedMutex> g(b->lock);
+        b->tracker.prune();
+        update_device_table(b);
+      }
+    }
+    __atomic_fetch_add(&fb.hdr->replay, 1, __ATOMIC_RELEASE);
+    Tools::get().inc(Counter::FaultReplays);
+    tools_event(ToolsEventType::GpuFaultReplay, Cause::User, Loc{}, Loc::gpu(dev), dev, 0, faults.size(), 0);
   }
   return n;
 }

@@ -57,10 +57,12 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
     for (int k = 0; k < (int)RingKind::COUNT; ++k)
       dev->rings[k] = std::make_unique<Ring>(rt->be_.get(), d, (RingKind)k, (uint32_t)cfg.channel_num_gpfifo_entries);
     void* p = nullptr;
-    const uint32_t entries = (uint32_t)cfg.perf_fault_batch_count * 16;
-    if (rt->be_->host_alloc_coherent(64 + (size_t)entries * sizeof(DeviceFaultRecord), &p) == Status::OK) {
-      dev->fault_buf.put = (uint32_t*)p;
-      dev->fault_buf.recs = (DeviceFaultRecord*)((char*)p + 64);
+    uint32_t entries = 64;  // power of two >= 16 fault batches
+    while (entries < (uint32_t)cfg.perf_fault_batch_count * 16) entries <<= 1;
+    if (rt->be_->host_alloc_coherent(sizeof(FaultBufHeader) + (size_t)entries * sizeof(DeviceFaultRecord), &p) ==
+        Status::OK) {
+      dev->fault_buf.hdr = (FaultBufHeader*)p;
+      dev->fault_buf.recs = (DeviceFaultRecord*)((char*)p + sizeof(FaultBufHeader));
       dev->fault_buf.entries = entries;
     }
     rt->devs_.push_back(std::move(dev));
@@ -109,7 +111,7 @@ Runtime::~Runtime() {
   cxl_.reset();
   for (auto& d : devs_) {
     for (auto& r : d->rings) r.reset();
-    if (d->fault_buf.put) be_->host_free_coherent(d->fault_buf.put);
+    if (d->fault_buf.hdr) be_->host_free_coherent(d->fault_buf.hdr);
     d->hbm_live.store(nullptr);
     d->hbm.reset();
   }
@@ -445,6 +447,30 @@ void Runtime::stable_map_block(Block* b) {
   }
 }
 
+void Runtime::register_table_stream(int dev, void* stream, bool on) {
+  if (dev < 0 || dev >= kMaxGpus) return;
+  std::lock_guard<std::mutex> g(dev_tables_m_);
+  auto& v = table_streams_[dev];
+  auto it = std::find(v.begin(), v.end(), stream);
+  if (on && it == v.end()) v.push_back(stream);
+  if (!on && it != v.end()) v.erase(it);
+}
+
+void Runtime::shootdown(Block* b, Residency* r) {
+  if (!r || !r->loc.is_gpu() || r->chunk < 0) return;
+  std::lock_guard<std::mutex> g(dev_tables_m_);
+  auto it = dev_tables_.find(b->range->id);
+  if (it == dev_tables_.end() || it->second->dev != r->loc.id) return;
+  uint64_t* e = &it->second->entries[2 * b->index];
+  uint64_t addr = r->arena->chunk_addr((uint32_t)r->chunk);
+  if (__atomic_load_n(e, __ATOMIC_RELAXED) != addr) return;
+  __atomic_store_n(e, 0, __ATOMIC_RELEASE);
+  // Kernels already queued on a table stream may have read the old entry.
+  for (void* s : table_streams_[r->loc.id])
+    if (FenceRef f = fence_record(be_.get(), r->loc.id, s)) r->arena->add_reuse_fence((uint32_t)r->chunk, f);
+  Tools::get().inc(Counter::TableShootdowns);
+}
+
 void Runtime::update_device_table(Block* b) {
   std::lock_guard<std::mutex> g(dev_tables_m_);
   auto it = dev_tables_.find(b->range->id);
@@ -477,7 +503,8 @@ Status Runtime::device_table(Range* r, DeviceResidencyTable** out) {
     if (st != Status::OK) return st;
     t->entries = (uint64_t*)p;
     t->nblocks = r->nblocks;
-    t->dev = 0;
+    std::vector<int> loc = local_devices();
+    t->dev = loc.empty() ? 0 : loc.front();  // the table describes this process's GPU
     *out = t.get();
     dev_tables_[r->id] = std::move(t);
   }
@@ -903,9 +930,11 @@ Status Runtime::start_fault_service(uint32_t poll_us) {
     fs_threads_.emplace_back([this, d, poll_us] {
       DeviceFaultBuffer& fb = devs_[d]->fault_buf;
       while (!fs_stop_.load(std::memory_order_acquire)) {
-        // Top half: cheap check of the device-written put index.
-        uint32_t put = fb.put ? __atomic_load_n(fb.put, __ATOMIC_ACQUIRE) : 0;
-        if (put == 0) {
+        // Top half: cheap check of the device-advanced PUT against GET.
+        bool pending = fb.hdr && (__atomic_load_n(&fb.hdr->put, __ATOMIC_ACQUIRE) !=
+                                      __atomic_load_n(&fb.hdr->get, __ATOMIC_RELAXED) ||
+                                  __atomic_load_n(&fb.hdr->overflow, __ATOMIC_RELAXED) != fb.overflow_seen);
+        if (!pending) {
           std::this_thread::sleep_for(std::chrono::microseconds(poll_us ? poll_us : 50));
           continue;
         }

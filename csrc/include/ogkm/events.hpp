@@ -173,6 +173,9 @@ enum class Counter : int {
   InjectedErrors,
   DecodedBytes,     // raw bytes produced by the fused BF12 copy+decode
   EncodedBytes,     // raw bytes stored BF12-packed in host / CXL tiers
+  TableShootdowns,  // device residency-table entries cleared before their chunk was released
+  FaultReplays,     // replay tokens issued after serviced device-fault batches
+  FaultRecordsConsumed,  // device fault-buffer records consumed from GET
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -14,6 +14,7 @@
 #include <cstdint>
 
 #include "ogkm/dgemm.hpp"
+#include "ogkm/fault_abi.hpp"
 
 namespace ogkm {
 
@@ -71,15 +72,37 @@ hipError_t launch_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, uin
 hipError_t launch_rope_kv(const RopeKvArgs& a, hipStream_t s);
 hipError_t launch_attn_decode(AttnArgs a, hipStream_t s);
 
+// Device fault buffer (GET/PUT ring, ogkm/fault_abi.hpp) as kernels see it.
+struct KFaultBuf {
+  FaultBufHeader* hdr;
+  DeviceFaultRecord* recs;
+  uint32_t entries;   // power of two
+};
+
 // Gather `nrows` rows (row_bytes each) of a managed table through its device
 // residency table; misses read zero and are recorded as faults, remote hits are
 // recorded as access-counter notifications.
-struct KFaultBuf {
-  uint32_t* put;
-  void* recs;       // DeviceFaultRecord[entries]
-  uint32_t entries;
-};
 hipError_t launch_managed_gather(const uint64_t* table, uint64_t range_id, const int64_t* rows, uint32_t nrows,
                                  uint32_t row_bytes, void* out, KFaultBuf fb, uint32_t proc, hipStream_t s);
+
+// Fault gate (replayable-fault stall + replay): one wave checks blocks
+// [b0, b0 + nblocks) of a range in its device residency table; every block not
+// resident in HBM is recorded as a fault and the wave waits for the host's
+// replay token (re-recording every ~1 ms), then re-checks. Work queued behind
+// the gate on the stream runs once every block is resident. status[0]: 0 =
+// resolved, 2 = cancelled after `timeout_us` (the kernel always exits);
+// status[1] = number of replays the gate waited for.
+hipError_t launch_fault_gate(const uint64_t* table, uint64_t range_id, uint32_t b0, uint32_t nblocks, KFaultBuf fb,
+                             uint32_t proc, uint32_t access, uint32_t timeout_us, uint32_t* status, hipStream_t s);
+
+// Table-indirect fetch: copy [off, off + bytes) of a range into `out`, block by
+// block through the device residency table (HBM entry, else the remote entry).
+// Meant to run behind a fault gate on a registered table stream.
+hipError_t launch_table_fetch(const uint64_t* table, uint64_t off, uint64_t bytes, void* out, uint32_t workgroups,
+                              hipStream_t s);
+
+// Fault-buffer stress producer (tests): `waves` x 64 lanes append
+// `per_lane` records each, retrying while the ring is full (bounded).
+hipError_t launch_fault_stress(KFaultBuf fb, uint32_t waves, uint32_t per_lane, uint32_t* gave_up, hipStream_t s);
 
 }  // namespace ogkm

@@ -21,6 +21,7 @@
 #include "ogkm/config.hpp"
 #include "ogkm/cxl.hpp"
 #include "ogkm/events.hpp"
+#include "ogkm/fault_abi.hpp"
 #include "ogkm/ring.hpp"
 #include "ogkm/tracker.hpp"
 #include "ogkm/va_space.hpp"
@@ -52,27 +53,15 @@ struct FaultEntry {
   bool duplicate = false;
 };
 
-// Device-recorded miss / access-counter record (written by HIP kernels into
-// host-coherent memory; layout shared with csrc/kernels/*.hip).
-struct DeviceFaultRecord {
-  uint64_t range_id;
-  uint32_t block;
-  uint16_t page;
-  uint8_t access;   // 1 read 2 write
-  uint8_t kind;     // 0 miss (fault), 1 remote access (access counter)
-  uint32_t proc;
-  uint32_t pad;
-};
-static_assert(sizeof(DeviceFaultRecord) == 24, "device fault record layout");
-
-// Replayable fault buffer analog (uvm_gpu_replayable_faults.c:844-988): a
-// ring in host-coherent memory that device code appends to with atomics.
+// Device fault buffer: GET/PUT ring of DeviceFaultRecord (ogkm/fault_abi.hpp)
+// in host-coherent memory, appended to by kernels (k_managed_gather,
+// k_fault_gate) and drained by the fault-service thread.
 struct DeviceFaultBuffer {
-  uint32_t* put = nullptr;      // device-incremented
-  uint32_t get = 0;
-  uint32_t entries = 0;
+  FaultBufHeader* hdr = nullptr;
   DeviceFaultRecord* recs = nullptr;
-  uint64_t overflows = 0;
+  uint32_t entries = 0;       // power of two
+  uint64_t overflows = 0;     // records producers dropped on a full ring (host total)
+  uint32_t overflow_seen = 0; // last value of hdr->overflow accounted for
 };
 
 // Per-range device residency table (2 entries per block: hbm address, remote
@@ -183,7 +172,16 @@ class Runtime {
   Lease* lease_by_id(uint64_t id);
   Status cpu_fault(uint64_t addr, bool write);        // SIGSEGV path
   size_t poll_device_faults(int dev);                  // service device-recorded faults
+  // Consume up to `max` published records from GET (no servicing).
+  size_t drain_fault_records(int dev, std::vector<DeviceFaultRecord>* out, size_t max);
   Status device_table(Range* r, DeviceResidencyTable** out);
+  // Streams whose kernels resolve addresses through device residency tables
+  // (k_managed_gather, table-indirect fetches). Before an HBM chunk listed in a
+  // table is released, its entry is cleared and an event is recorded on every
+  // such stream of the device into the chunk's reuse fence: a kernel that read
+  // the old entry finishes before the chunk is overwritten (the TLB-shootdown
+  // + membar step of unmapping, uvm_va_block.c unmap + tlb_invalidate).
+  void register_table_stream(int dev, void* stream, bool on);
 
   // ---- data movement helpers
   Status write(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev);
@@ -248,6 +246,7 @@ class Runtime {
                       Tracker* out, Cause cause, bool* conflict);
   Status queue_copy(Ctx& c, Block* b, Residency* from, Residency* to, const PageMask& pages);
   void update_device_table(Block* b);
+  void shootdown(Block* b, Residency* r);  // block lock held; before r's GPU chunk is released
 
   std::atomic<bool> quiesced_{false};
   std::atomic<uint64_t> cxl_transfers_{0};
@@ -265,6 +264,8 @@ class Runtime {
   int host_node_ = 0;
   std::unordered_map<uint64_t, std::unique_ptr<DeviceResidencyTable>> dev_tables_;
   std::mutex dev_tables_m_;
+  std::vector<void*> table_streams_[kMaxGpus];  // guarded by dev_tables_m_
+  std::mutex poll_m_;  // fault-buffer consumers drain one at a time
   std::unordered_map<uint64_t, std::pair<Ring*, uint64_t>> cxl_pending_;
   std::mutex cxl_m_;
   std::vector<std::thread> fs_threads_;

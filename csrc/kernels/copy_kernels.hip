@@ -181,21 +181,46 @@ hipError_t launch_signal(uint64_t* host_addr, uint64_t value, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- fault buffer
+// Producer side of the GET/PUT fault ring (ogkm/fault_abi.hpp): drop on a
+// full ring at first look (may_drop), else reserve a slot with one atomic add
+// on PUT, wait (bounded, ~1 s) for the host to consume the slot's previous lap,
+// fill the record and publish it by storing seq = slot + 1 with release
+// semantics at system scope. All stores are vector stores.
+__device__ bool fb_append(KFaultBuf fb, uint64_t range_id, uint32_t block, uint32_t page, uint32_t access,
+                          uint32_t kind, uint32_t proc, bool may_drop = true) {
+  FaultBufHeader* h = fb.hdr;
+  if (may_drop && __hip_atomic_load(&h->put, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) -
+                          __hip_atomic_load(&h->get, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >=
+                      fb.entries) {
+    __hip_atomic_fetch_add(&h->overflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return false;
+  }
+  const uint32_t p = __hip_atomic_fetch_add(&h->put, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t t0 = wall_clock64();
+  while (p - __hip_atomic_load(&h->get, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= fb.entries) {
+    if (wall_clock64() - t0 > 100000000ull) {  // 1 s: overwrite, the older record counts as lost
+      __hip_atomic_fetch_add(&h->overflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  DeviceFaultRecord* r = fb.recs + (p & (fb.entries - 1));
+  r->range_id = range_id;
+  r->block = block;
+  r->page = (uint16_t)page;
+  r->access = (uint8_t)access;
+  r->kind = (uint8_t)kind;
+  r->proc = proc;
+  __hip_atomic_store(&r->seq, p + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return true;
+}
+
 // Device-side residency check + gather. table[2*b] = HBM address of block b (0 if
 // not resident on this GPU), table[2*b+1] = remote (host/CXL) address. One
 // workgroup per row; lane 0 resolves the source and records misses / remote
 // accesses into the fault buffer (software replayable-fault + access-counter
 // producer).
-struct DevFaultRec {
-  uint64_t range_id;
-  uint32_t block;
-  uint16_t page;
-  uint8_t access;
-  uint8_t kind;
-  uint32_t proc;
-  uint32_t pad;
-};
-
 __global__ void __launch_bounds__(kThreads)
     k_managed_gather(const uint64_t* __restrict__ table, uint64_t range_id, const int64_t* __restrict__ rows,
                      uint32_t nrows, uint32_t row_bytes, uint8_t* __restrict__ out, KFaultBuf fb, uint32_t proc) {
@@ -205,23 +230,10 @@ __global__ void __launch_bounds__(kThreads)
       uint64_t off = (uint64_t)rows[r] * row_bytes;
       uint64_t b = off >> 21;
       uint64_t in_blk = off & ((1ull << 21) - 1);
-      uint64_t hbm = __hip_atomic_load(table + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      uint64_t rem = __hip_atomic_load(table + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint64_t hbm = __hip_atomic_load(table + 2 * b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint64_t rem = __hip_atomic_load(table + 2 * b + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
       uint64_t src = hbm ? hbm + in_blk : (rem ? rem + in_blk : 0);
-      if (!hbm && fb.put) {
-        uint32_t slot = __hip_atomic_fetch_add(fb.put, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (slot < fb.entries) {
-          DevFaultRec rec;
-          rec.range_id = range_id;
-          rec.block = (uint32_t)b;
-          rec.page = (uint16_t)(in_blk >> 12);
-          rec.access = 1;
-          rec.kind = rem ? 1 : 0;
-          rec.proc = proc;
-          rec.pad = 0;
-          reinterpret_cast<DevFaultRec*>(fb.recs)[slot] = rec;
-        }
-      }
+      if (!hbm && fb.hdr) fb_append(fb, range_id, (uint32_t)b, (uint32_t)(in_blk >> 12), 1, rem ? 1 : 0, proc);
       s_src = src;
     }
     __syncthreads();
@@ -243,6 +255,116 @@ hipError_t launch_managed_gather(const uint64_t* table, uint64_t range_id, const
   uint32_t grid = nrows < 1024 ? nrows : 1024;
   hipLaunchKernelGGL(k_managed_gather, dim3(grid), dim3(kThreads), 0, s, table, range_id, rows, nrows, row_bytes,
                      reinterpret_cast<uint8_t*>(out), fb, proc);
+  return hipGetLastError();
+}
+
+// One wave. The wall clock (100 MHz constant counter) bounds every wait, so
+// the kernel exits even if the host never services the faults.
+__global__ void __launch_bounds__(64)
+    k_fault_gate(const uint64_t* __restrict__ table, uint64_t range_id, uint32_t b0, uint32_t nblocks, KFaultBuf fb,
+                 uint32_t proc, uint32_t access, uint64_t timeout_ticks, uint32_t* status) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t t0 = wall_clock64();
+  uint32_t replays = 0;
+  for (;;) {
+    const uint64_t token = __hip_atomic_load(&fb.hdr->replay, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    int miss = 0;
+    for (uint32_t b = b0 + lane; b < b0 + nblocks; b += 64) {
+      uint64_t hbm = __hip_atomic_load(table + 2 * (uint64_t)b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (!hbm) {
+        miss = 1;
+        fb_append(fb, range_id, b, kFaultWholeBlock, access, 0, proc);
+      }
+    }
+    if (!__any(miss)) {
+      if (lane == 0) {
+        status[0] = 0;
+        status[1] = replays;
+      }
+      return;
+    }
+    // Stall until the host replays (or ~1 ms passes: re-record, a record may
+    // have been dropped on a full ring), bounded by the timeout.
+    const uint64_t t_rec = wall_clock64();
+    for (;;) {
+      __builtin_amdgcn_s_sleep(32);
+      uint64_t now = wall_clock64();
+      if (now - t0 > timeout_ticks) {
+        if (lane == 0) {
+          status[0] = 2;
+          status[1] = replays;
+        }
+        return;
+      }
+      if (__hip_atomic_load(&fb.hdr->replay, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != token) {
+        ++replays;
+        break;
+      }
+      if (now - t_rec > 100000) break;  // 1 ms at 100 MHz
+    }
+  }
+}
+
+hipError_t launch_fault_gate(const uint64_t* table, uint64_t range_id, uint32_t b0, uint32_t nblocks, KFaultBuf fb,
+                             uint32_t proc, uint32_t access, uint32_t timeout_us, uint32_t* status, hipStream_t s) {
+  if (!fb.hdr || !table || !status) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fault_gate, dim3(1), dim3(64), 0, s, table, range_id, b0, nblocks, fb, proc, access,
+                     (uint64_t)timeout_us * 100, status);
+  return hipGetLastError();
+}
+
+// Table-indirect copy: work item = (block, 64 KB piece); source resolved per
+// block from the residency table at run time.
+__global__ void __launch_bounds__(kThreads)
+    k_table_fetch(const uint64_t* __restrict__ table, uint64_t off, uint64_t bytes, uint8_t* __restrict__ out) {
+  constexpr uint64_t kPiece = 64 << 10;
+  const uint64_t npieces = (bytes + kPiece - 1) / kPiece;
+  for (uint64_t p = blockIdx.x; p < npieces; p += gridDim.x) {
+    uint64_t o = off + p * kPiece;
+    uint64_t len = bytes - p * kPiece < kPiece ? bytes - p * kPiece : kPiece;
+    // a piece never crosses a block when off is 64 KB aligned; split otherwise
+    while (len) {
+      uint64_t b = o >> 21, in_blk = o & ((1ull << 21) - 1);
+      uint64_t n = (1ull << 21) - in_blk < len ? (1ull << 21) - in_blk : len;
+      uint64_t hbm = __hip_atomic_load(table + 2 * b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint64_t base = hbm ? hbm : __hip_atomic_load(table + 2 * b + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint64_t dst = reinterpret_cast<uint64_t>(out) + (o - off);
+      if (base) {
+        copy_span(dst, base + in_blk, n);
+      } else {
+        for (uint64_t k = threadIdx.x * 4; k < n; k += kThreads * 4) *reinterpret_cast<uint32_t*>(dst + k) = 0;
+      }
+      o += n;
+      len -= n;
+    }
+  }
+}
+
+hipError_t launch_table_fetch(const uint64_t* table, uint64_t off, uint64_t bytes, void* out, uint32_t workgroups,
+                              hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  if ((off | bytes | reinterpret_cast<uint64_t>(out)) & 3) return hipErrorInvalidValue;
+  uint64_t pieces = (bytes + (64 << 10) - 1) / (64 << 10);
+  uint32_t grid = pieces < workgroups ? (uint32_t)pieces : workgroups;
+  hipLaunchKernelGGL(k_table_fetch, dim3(grid), dim3(kThreads), 0, s, table, off, bytes,
+                     reinterpret_cast<uint8_t*>(out));
+  return hipGetLastError();
+}
+
+// Every lane appends per_lane records (block = global lane id, page = i),
+// never dropping: each append waits for ring space (the host drains).
+__global__ void __launch_bounds__(64) k_fault_stress(KFaultBuf fb, uint32_t per_lane, uint32_t* gave_up) {
+  const uint32_t id = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t ov0 = __hip_atomic_load(&fb.hdr->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (uint32_t i = 0; i < per_lane; ++i) fb_append(fb, 7, id, i, 1, 0, id, false);
+  // a bounded wait that expired shows up as an overflow
+  if (__hip_atomic_load(&fb.hdr->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != ov0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(gave_up, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t launch_fault_stress(KFaultBuf fb, uint32_t waves, uint32_t per_lane, uint32_t* gave_up, hipStream_t s) {
+  if (!fb.hdr || !gave_up || waves == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fault_stress, dim3(waves), dim3(64), 0, s, fb, per_lane, gave_up);
   return hipGetLastError();
 }
 

@@ -353,11 +353,80 @@ PYBIND11_MODULE(_ogkm, m) {
     DeviceResidencyTable* t;
     check(r->device_table(rg, &t), "device_table");
     DeviceFaultBuffer& fb = r->dev(dev).fault_buf;
-    KFaultBuf kfb{fb.put, fb.recs, fb.entries};
+    KFaultBuf kfb{fb.hdr, fb.recs, fb.entries};
     hipError_t e = launch_managed_gather(t->entries, rg->id, (const int64_t*)rows_dptr, nrows, row_bytes,
                                          (void*)out_dptr, kfb, (uint32_t)dev, (hipStream_t)stream);
     if (e != hipSuccess) throw StatusError(std::string("managed_gather launch: ") + hipGetErrorString(e));
   });
+  // Fault gate: a one-wave kernel that stalls the stream until blocks covering
+  // [off, off+len) of the range are HBM-resident (records faults, waits for the
+  // replay token). status_dptr: device uint32[2] {0 ok / 2 cancelled, replays}.
+  m.def("fault_gate", [](uint64_t id, uint64_t off, uint64_t len, int dev, uint64_t stream, uint64_t status_dptr,
+                         uint32_t timeout_ms, bool write) {
+    Runtime* r = rt();
+    if (r->be()->is_fake()) throw StatusError("fault_gate needs the HIP backend");
+    Range* rg = range(id);
+    if (len == 0 || off + len > rg->size || !status_dptr) throw StatusError("fault_gate: bad span");
+    DeviceResidencyTable* t;
+    check(r->device_table(rg, &t), "device_table");
+    if (t->dev != dev) throw StatusError("fault_gate: the range's device table belongs to another GPU");
+    DeviceFaultBuffer& fb = r->dev(dev).fault_buf;
+    KFaultBuf kfb{fb.hdr, fb.recs, fb.entries};
+    uint32_t b0 = (uint32_t)(off >> kBlockShift), b1 = (uint32_t)((off + len - 1) >> kBlockShift);
+    hipError_t e = launch_fault_gate(t->entries, rg->id, b0, b1 - b0 + 1, kfb, (uint32_t)dev, write ? 2 : 1,
+                                     timeout_ms * 1000u, (uint32_t*)status_dptr, (hipStream_t)stream);
+    if (e != hipSuccess) throw StatusError(std::string("fault_gate launch: ") + hipGetErrorString(e));
+  }, py::arg("id"), py::arg("off"), py::arg("len"), py::arg("dev"), py::arg("stream"), py::arg("status_dptr"),
+     py::arg("timeout_ms") = 5000, py::arg("write") = false);
+  m.def("table_fetch", [](uint64_t id, uint64_t off, uint64_t len, uint64_t out_dptr, int dev, uint64_t stream) {
+    Runtime* r = rt();
+    if (r->be()->is_fake()) throw StatusError("table_fetch needs the HIP backend");
+    Range* rg = range(id);
+    if (len == 0 || off + len > rg->size || !out_dptr) throw StatusError("table_fetch: bad span");
+    DeviceResidencyTable* t;
+    check(r->device_table(rg, &t), "device_table");
+    if (t->dev != dev) throw StatusError("table_fetch: the range's device table belongs to another GPU");
+    hipError_t e = launch_table_fetch(t->entries, off, len, (void*)out_dptr, 64, (hipStream_t)stream);
+    if (e != hipSuccess) throw StatusError(std::string("table_fetch launch: ") + hipGetErrorString(e));
+  });
+  m.def("register_table_stream", [](int dev, uint64_t stream, bool on) {
+    rt()->register_table_stream(dev, (void*)stream, on);
+  }, py::arg("dev"), py::arg("stream"), py::arg("on") = true);
+  m.def("fault_stress", [](int dev, uint32_t waves, uint32_t per_lane, uint64_t gave_up_dptr, uint64_t stream) {
+    Runtime* r = rt();
+    if (r->be()->is_fake()) throw StatusError("fault_stress needs the HIP backend");
+    DeviceFaultBuffer& fb = r->dev(dev).fault_buf;
+    KFaultBuf kfb{fb.hdr, fb.recs, fb.entries};
+    hipError_t e = launch_fault_stress(kfb, waves, per_lane, (uint32_t*)gave_up_dptr, (hipStream_t)stream);
+    if (e != hipSuccess) throw StatusError(std::string("fault_stress launch: ") + hipGetErrorString(e));
+  });
+  // Host-side producer (the device protocol): fake backend / tests.
+  m.def("inject_device_faults", [](int dev, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint32_t,
+                                                                         uint32_t, uint32_t>>& recs) {
+    DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
+    size_t ok = 0;
+    for (auto& t : recs) {
+      DeviceFaultRecord r{};
+      r.range_id = std::get<0>(t);
+      r.block = std::get<1>(t);
+      r.page = (uint16_t)std::get<2>(t);
+      r.access = (uint8_t)std::get<3>(t);
+      r.kind = (uint8_t)std::get<4>(t);
+      r.proc = std::get<5>(t);
+      ok += fault_buf_produce(fb.hdr, fb.recs, fb.entries, r);
+    }
+    return ok;
+  });
+  m.def("drain_fault_records", [](int dev, size_t max) {
+    std::vector<DeviceFaultRecord> v;
+    {
+      py::gil_scoped_release nogil;
+      rt()->drain_fault_records(dev, &v, max);
+    }
+    py::list out;
+    for (auto& r : v) out.append(py::make_tuple(r.range_id, r.block, r.page, r.access, r.kind, r.proc));
+    return out;
+  }, py::arg("dev"), py::arg("max") = (size_t)1 << 20);
 
   // ---- data
   m.def("write", [](uint64_t id, uint64_t off, uint64_t ptr, uint64_t bytes, int src_dev) {
@@ -710,7 +779,15 @@ PYBIND11_MODULE(_ogkm, m) {
   });
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
-    return py::make_tuple((uint64_t)fb.put, (uint64_t)fb.recs, fb.entries, fb.overflows);
+    py::dict d;
+    d["header"] = (uint64_t)fb.hdr;
+    d["records"] = (uint64_t)fb.recs;
+    d["entries"] = fb.entries;
+    d["overflows"] = fb.overflows;
+    d["put"] = fb.hdr ? __atomic_load_n(&fb.hdr->put, __ATOMIC_ACQUIRE) : 0;
+    d["get"] = fb.hdr ? __atomic_load_n(&fb.hdr->get, __ATOMIC_ACQUIRE) : 0;
+    d["replay"] = fb.hdr ? __atomic_load_n(&fb.hdr->replay, __ATOMIC_ACQUIRE) : 0;
+    return d;
   });
 
   // ---- lock checker

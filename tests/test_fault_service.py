@@ -15,18 +15,10 @@ from ogkm._native import lib
 MB = 1 << 20
 
 
-class Rec(ctypes.Structure):
-    _fields_ = [("range_id", ctypes.c_uint64), ("block", ctypes.c_uint32), ("page", ctypes.c_uint16),
-                ("access", ctypes.c_uint8), ("kind", ctypes.c_uint8), ("proc", ctypes.c_uint32),
-                ("pad", ctypes.c_uint32)]
-
-
 def _inject(records):
-    put_addr, recs_addr, entries, _ = lib.fault_buffer_info(0)
-    arr = (Rec * entries).from_address(recs_addr)
-    for i, r in enumerate(records):
-        arr[i] = r
-    ctypes.c_uint32.from_address(put_addr).value = len(records)
+    """Append records with the device producer protocol (CAS on PUT, release-
+    published sequence numbers): (range_id, block, page, access, kind, proc)."""
+    assert lib.inject_device_faults(0, records) == len(records)
 
 
 def _wait(pred, timeout=10.0):
@@ -39,11 +31,10 @@ def _wait(pred, timeout=10.0):
 
 
 def test_fault_records_serviced_by_thread(fake_rt):
-    assert ctypes.sizeof(Rec) == 24
     b = rt.malloc_managed(4 * MB, "faults")
     b.write(torch.ones(4 * MB, dtype=torch.uint8))
     lib.start_fault_service(100)
-    _inject([Rec(b.id, 1, 7, 1, 0, 0, 0), Rec(b.id, 1, 7, 1, 0, 0, 0), Rec(b.id, 0, 3, 2, 0, 0, 0)])
+    _inject([(b.id, 1, 7, 1, 0, 0), (b.id, 1, 7, 1, 0, 0), (b.id, 0, 3, 2, 0, 0)])
     assert _wait(lambda: lib.fault_service_batches() >= 1)
     assert _wait(lambda: any(r["tier"] == "gpu" for r in b.residency(2 * MB)["resident_on"]))
     s = lib.stats()
@@ -59,7 +50,7 @@ def test_access_counters_migrate_hot_block(fake_rt):
     b.set_accessed_by(0)
     b.write(torch.ones(4 * MB, dtype=torch.uint8))
     # remote-access notifications (kind=1) for block 1 only
-    _inject([Rec(b.id, 1, p, 1, 1, 0, 0) for p in range(4)])
+    _inject([(b.id, 1, p, 1, 1, 0) for p in range(4)])
     lib.poll_device_faults(0)
     s = lib.stats()
     assert s["access_counter_notifications"] == 4
@@ -70,12 +61,67 @@ def test_access_counters_migrate_hot_block(fake_rt):
 
 
 def test_fault_buffer_overflow_is_counted(fake_rt):
-    put_addr, _, entries, _ = lib.fault_buffer_info(0)
-    ctypes.c_uint32.from_address(put_addr).value = entries + 10  # device wrote past the end
+    info = lib.fault_buffer_info(0)
+    n = info["entries"]
+    b = rt.malloc_managed(2 * MB, "ov")
     from ogkm import tools
 
     q = tools.EventQueue(events=["FaultBufferOverflow"])
+    # a full ring drops (and counts) what does not fit; nothing is overwritten
+    assert lib.inject_device_faults(0, [(b.id, 0, p % 512, 1, 0, 0) for p in range(n + 10)]) == n
     lib.poll_device_faults(0)
-    assert lib.fault_buffer_info(0)[3] == 10
+    info = lib.fault_buffer_info(0)
+    assert info["overflows"] == 10 and info["get"] == info["put"]
     assert any(e["type"] == "FaultBufferOverflow" for e in q.read_dicts())
     q.close()
+    b.free()
+
+
+def test_get_put_ring_concurrent_producers_lose_nothing(fake_rt):
+    """Producers append while the host drains: every record arrives exactly
+    once, in slot order per producer, across many wraps of the ring."""
+    import threading
+
+    n_prod, per = 4, 3 * lib.fault_buffer_info(0)["entries"]
+    got = []
+    stop = threading.Event()
+
+    def drain():
+        while not stop.is_set() or lib.fault_buffer_info(0)["put"] != lib.fault_buffer_info(0)["get"]:
+            got.extend(lib.drain_fault_records(0))
+
+    def produce(k):
+        i = 0
+        while i < per:
+            if lib.inject_device_faults(0, [(99, k, i % 512, 1, 0, i)]):
+                i += 1
+
+    d = threading.Thread(target=drain)
+    d.start()
+    ps = [threading.Thread(target=produce, args=(k,)) for k in range(n_prod)]
+    for t in ps:
+        t.start()
+    for t in ps:
+        t.join()
+    stop.set()
+    d.join()
+    assert len(got) == n_prod * per
+    for k in range(n_prod):
+        mine = [r[5] for r in got if r[1] == k]
+        assert mine == list(range(per))
+
+
+def test_replay_token_and_table_after_service(fake_rt):
+    """A serviced batch bumps the replay token after its copies landed and the
+    device residency table shows the block in HBM."""
+    b = rt.malloc_managed(4 * MB, "rp")
+    b.write(torch.ones(4 * MB, dtype=torch.uint8))
+    table = lib.device_table(b.id)
+    r0 = lib.fault_buffer_info(0)["replay"]
+    _inject([(b.id, 1, 0xFFFF, 1, 0, 0)])  # whole block (what k_fault_gate records)
+    lib.poll_device_faults(0)
+    assert lib.fault_buffer_info(0)["replay"] == r0 + 1
+    hbm = ctypes.c_uint64.from_address(table + 16).value
+    assert hbm != 0
+    assert lib.stats()["fault_replays"] >= 1
+    b.free()

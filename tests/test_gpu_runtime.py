@@ -123,7 +123,7 @@ def test_ring_copy_bandwidth_h2d(gpu_rt):
     l.release()
     gbps = n / dt / 1e9
     print(f"acquire 1 GiB H2D: {gbps:.1f} GB/s")
-    assert gbps > 35
+    assert gbps > 50  # SDMA engine: ~56.8 GB/s on the box (profiles/r2_probe_sdma.txt)
     b.free()
 
 
