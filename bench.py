@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--fake-hbm-mb", type=int, default=1024)
     ap.add_argument("--dump-logits", default="",
                     help="write the last step's logits [global batch, vocab] (fp32) to this file (rank 0)")
+    ap.add_argument("--planner", choices=("static", "off"), default="static",
+                    help="off: no residency plan - every weight prefers HBM, nothing is pinned, the runtime's "
+                         "LRU / prefetch / eviction decide residency")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -200,7 +203,7 @@ def main() -> None:
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
                               seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
                               weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac, kv_format=a.kv_format,
-                              parallel=a.parallel)
+                              parallel=a.parallel, planner=a.planner)
     plan = model.describe()
     init_s = time.perf_counter() - t_init
     g = torch.Generator(device="cpu").manual_seed(42)
@@ -254,6 +257,8 @@ def main() -> None:
         name = {"llama3-70b": "Llama-3-70B", "llama3-405b": "Llama-3-405B", "llama3-8b": "Llama-3-8B"}.get(a.model,
                                                                                                         a.model)
         metric = f"tokens/sec {name} {a.oversub:g}x oversubscribe"
+        if a.planner == "off":
+            metric += " (planner off: runtime LRU residency)"
         if sim:  # one shard of an N-GPU job on one GPU: an upper bound, not a measured N-GPU rate
             metric += f" (tp{a.simulate_tp} rank-0 shard simulated on 1 GPU, collectives skipped)"
         out = {
@@ -276,6 +281,7 @@ def main() -> None:
                 "parallelism": (f"tp{a.simulate_tp}-rank0-simulated" if sim
                                 else f"{'shards' if a.parallel == 'shards' else 'tp'}{world}"),
                 "backend": a.backend,
+                "planner": a.planner,
                 "rank_host_numa_nodes": host_nodes,
                 "tiers": plan["tiers"],
                 "kv_format": plan["kv_format"],

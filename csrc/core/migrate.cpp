@@ -539,7 +539,15 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
     update_device_table(b);
     if (b->range->dev_va) stable_map_block(b);
   }
+  // The context is spent; what the caller still needs for its retry (the
+  // arena to evict from on MORE_PROCESSING_REQUIRED) survives the reset.
+  ChunkArena* need_arena = c.need_arena;
+  uint32_t need_n = c.need_n;
+  Cause cause = c.cause;
   c = Ctx{};
+  c.need_arena = need_arena;
+  c.need_n = need_n;
+  c.cause = cause;
   return result;
 }
 
@@ -847,8 +855,9 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
       {
         std::lock_guard<OrderedMutex> g(b->lock);
         Residency* x = b->find(dst);
-        if (in_place && (!x || x->chunk != (int64_t)target)) {
-          // Evicted since the in-place check: `target` is not ours any more.
+        if ((in_place || handed[k]) && (!x || x->chunk != (int64_t)target)) {
+          // Evicted since the in-place check (or since it was handed over, on a
+          // MORE_PROCESSING_REQUIRED retry): `target` is not ours any more.
           *conflict = true;
           st = Status::BUSY;
         } else if (x && x->chunk != (int64_t)target && b->lease_pins) {

@@ -163,9 +163,16 @@ class TieredLlama:
                  device: int = 0, tp_rank: int = 0, tp_world: int = 1, seed: int = 0, lookahead: int = 2,
                  hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
                  packed: bool = True, weight_format: str = "bf11", tiers: str = "host", cxl_frac: float = 0.5,
-                 kv_format: str = "bf16", parallel: str = "tp"):
+                 kv_format: str = "bf16", parallel: str = "tp", planner: str = "static"):
         if parallel not in ("tp", "shards"):
             raise ValueError("parallel must be 'tp' or 'shards'")
+        # planner "static": the plan below picks resident layers and pins them
+        # with lifetime leases. "off": no plan - every weight prefers HBM, none
+        # is pinned, each use is a lease (software fault) and the runtime's LRU,
+        # prefetch and eviction decide what stays resident.
+        if planner not in ("static", "off"):
+            raise ValueError("planner must be 'static' or 'off'")
+        self.planner = planner
         self.parallel = parallel
         if parallel == "shards":
             # Data parallel over sequences, weights sharded over ranks: the layer
@@ -323,8 +330,10 @@ class TieredLlama:
             raise ValueError(f"HBM budget {self.budget/2**30:.1f} GiB too small for KV + staging "
                              f"({(fixed + staging + self.stage_bytes)/2**30:.1f} GiB)")
         n_res = max(0, min(cfg.n_layers, avail // layer_cost - int(os.environ.get("OGKM_RESIDENT_MARGIN", "0"))))
+        if planner == "off":
+            n_res, avail = 0, 0
         left = avail - n_res * layer_cost
-        self.head_resident = left >= head_cost
+        self.head_resident = left >= head_cost and planner == "static"
         if self.head_resident:
             left -= head_cost
         # spread resident layers evenly so streaming continues behind them
@@ -461,6 +470,7 @@ class TieredLlama:
     def describe(self) -> dict:
         d = {
             "model": self.cfg.name, "tp": f"{self.rank}/{self.world}", "parallel": self.parallel,
+            "planner": self.planner,
             "shard": f"{self.srank}/{self.sworld}", "batch": self.B, "global_batch": self.B_global,
             "gather_gb": self.gather_bytes / 1e9, "context": self.ctx,
             "footprint_gb": self.footprint / 1e9, "hbm_budget_gb": self.budget / 1e9,
@@ -544,7 +554,7 @@ class TieredLlama:
             if info is not None:
                 self.pinfo[key] = info
                 self.pmode[key] = dgemm.packed_mode(data) if not self.staged else dgemm.MODE_RAW
-            self._place(b, resident, gpu, self.rest_loc.get(key, host))
+            self._place(b, resident, gpu, self.rest_loc.get(key, host), self.planner)
             b.write(part)
             self.ubuf[key] = b
             return
@@ -554,13 +564,18 @@ class TieredLlama:
             self.pmode[key] = dgemm.packed_mode(data) if not self.staged else dgemm.MODE_RAW
         else:
             b = rt.malloc_managed(data.numel() * 2, name, packed_bf16=self.packed and not resident)
-        self._place(b, resident, gpu, self.rest_loc.get(key, host))
+        self._place(b, resident, gpu, self.rest_loc.get(key, host), self.planner)
         b.write(data)
         self.ubuf[key] = b
 
     @staticmethod
-    def _place(b, resident: bool, gpu, host) -> None:
-        if resident:
+    def _place(b, resident: bool, gpu, host, planner: str = "static") -> None:
+        if planner == "off":
+            # no plan: HBM preferred, read-duplicated (an eviction drops the HBM
+            # copy, the host copy stays) - residency is the runtime's decision
+            b.set_preferred_location(gpu)
+            b.set_read_mostly(True)
+        elif resident:
             b.set_preferred_location(gpu)
         else:
             b.set_preferred_location(host)

@@ -422,6 +422,33 @@ static void test_cpu_faults_concurrent() {
   Runtime::shutdown();
 }
 
+
+// Writes into ranges that prefer HBM while HBM is oversubscribed (the
+// planner-off model init): each write stages on the host, then migrates to the
+// GPU, evicting earlier ranges.
+static void test_write_preferred_gpu_oversubscribed() {
+  Runtime* rt = Runtime::init("fake", 1, 64ull << 20);
+  CHECK(rt->init_device(0, 16ull << 20) == Status::OK);
+  std::vector<Range*> rs;
+  for (int i = 0; i < 10; ++i) {
+    Range* r = nullptr;
+    CHECK(rt->malloc_managed((3ull << 20) + 4096 * i, 0, "pg" + std::to_string(i), &r) == Status::OK);
+    CHECK(rt->mem_advise(r, 0, r->size, Advice::SET_PREFERRED_LOCATION, Loc::gpu(0), 0) == Status::OK);
+    CHECK(rt->mem_advise(r, 0, r->size, Advice::SET_READ_MOSTLY, Loc{}, 0) == Status::OK);
+    std::vector<uint8_t> data(r->size, (uint8_t)(0x30 + i));
+    CHECK(rt->write(r, 0, data.data(), data.size(), -1) == Status::OK);
+    rs.push_back(r);
+  }
+  for (int i = 0; i < 10; ++i) {
+    std::vector<uint8_t> back(rs[i]->size);
+    CHECK(rt->read(rs[i], 0, back.data(), back.size(), -1) == Status::OK);
+    CHECK(back.front() == (uint8_t)(0x30 + i) && back.back() == (uint8_t)(0x30 + i));
+  }
+  CHECK(rt->dev(0).hbm->check().empty());
+  for (Range* r : rs) CHECK(rt->free_range(r) == Status::OK);
+  Runtime::shutdown();
+}
+
 int main() {
   RUN(test_pagemask);
   RUN(test_arena_alloc_reserve);
@@ -433,6 +460,7 @@ int main() {
   RUN(test_reuse_fence_not_consumed);
   RUN(test_no_shared_chunks_under_concurrency);
   RUN(test_cpu_faults_concurrent);
+  RUN(test_write_preferred_gpu_oversubscribed);
   if (g_fail) {
     fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

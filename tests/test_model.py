@@ -213,3 +213,31 @@ def test_bf11_kv_cache_bit_identical_to_bf16(fake_rt):
         for a, b in zip(out["bf16"], out[fmt]):
             assert torch.equal(a, b)
     assert res["ans"] < res["bf11"] < 0.8 * res["bf16"]
+
+
+def test_planner_off_matches_static_plan(fake_rt):
+    """planner='off': no resident plan, no lifetime pins - every unit prefers
+    HBM and the runtime's LRU evicts under 2x oversubscription. Logits equal the
+    planned run's, and the runtime (not the plan) did the evicting."""
+    lib.shutdown()
+    rt.init("fake", fake_devices=1, fake_hbm_mb=512, lock_check=1, host_budget_mb=1024)
+    cfg = llama.CONFIGS["small"]
+    out = {}
+    for planner in ("static", "off"):
+        m = llama.TieredLlama(cfg, batch=2, context=8, max_new_tokens=4, oversub=2.0, lookahead=1, seed=3,
+                              weight_format="ans", planner=planner)
+        m.keep_logits = True
+        if planner == "off":
+            assert m.describe()["resident_layers"] == 0 and not m._pin_leases
+        lib.reset_counters()
+        logs = []
+        for s in range(3):
+            m.step(torch.tensor([5, 7]) + s)
+            logs.append(m.last_logits.clone())
+        out[planner] = (logs, lib.stats()["evictions"])
+        if planner == "off":
+            assert not m._pin_leases   # nothing pinned for the model's lifetime
+        m.close()
+    for a, b in zip(out["static"][0], out["off"][0]):
+        assert torch.equal(a, b)
+    assert out["off"][1] > 0
