@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--planner", choices=("static", "off"), default="static",
                     help="off: no residency plan - every weight prefers HBM, nothing is pinned, the runtime's "
                          "LRU / prefetch / eviction decide residency")
+    ap.add_argument("--allocator", action="store_true",
+                    help="route torch CUDA allocations through the runtime's HBM arena (pluggable allocator)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -170,6 +172,12 @@ def main() -> None:
     from ogkm.parallel import comm
 
     fake = a.backend == "fake"
+    if a.allocator and not fake:
+        # config 2: torch tensors share the runtime's HBM arena. Swapped in
+        # before torch initialises its caching allocator (and before any CUDA
+        # tensor exists); allocations resolve once the runtime is up.
+        from ogkm import allocator
+        allocator.enable()
     e = comm.init("gloo" if fake else None)
     if e.world != a.gpus and e.world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={e.world}")
@@ -282,6 +290,7 @@ def main() -> None:
                                 else f"{'shards' if a.parallel == 'shards' else 'tp'}{world}"),
                 "backend": a.backend,
                 "planner": a.planner,
+                "torch_allocator": "ogkm-arena" if a.allocator else "torch-caching",
                 "rank_host_numa_nodes": host_nodes,
                 "tiers": plan["tiers"],
                 "kv_format": plan["kv_format"],

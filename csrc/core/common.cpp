@@ -156,8 +156,15 @@ void clear_fatal_for_test() { g_status.store(0); }
 
 const char* fatal_reason() { return global_status() == Status::OK ? "" : g_fatal_why; }
 
+#if defined(__SANITIZE_ADDRESS__) || defined(__SANITIZE_THREAD__)
+extern "C" void __sanitizer_print_stack_trace();
+#endif
+
 void assert_fail(const char* cond, const char* file, int line, bool release) {
   log_msg(LogLevel::ERROR, file, line, "assertion failed: %s", cond);
+#if defined(__SANITIZE_ADDRESS__) || defined(__SANITIZE_THREAD__)
+  __sanitizer_print_stack_trace();  // sanitizer test builds: where the broken invariant was hit
+#endif
   if (release && config().release_asserts) set_fatal(Status::FATAL, cond);
 #ifdef OGKM_DEBUG
   if (!release) abort();

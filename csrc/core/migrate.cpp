@@ -501,11 +501,11 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
   // read on two rings must not be handed out between the two fences.
   for (auto& u : c.chunk_uses)
     if (FenceRef f = fence_of(u.ring)) u.arena->add_reuse_fence(u.chunk, f);
+  // Freed while still pinned (free() drops the pin in the same critical
+  // section): an unpin first would let a concurrent reserve() take the
+  // owner-less chunk as an eviction victim before the free.
   for (auto& u : c.chunk_uses)
-    if (u.free_after) {
-      u.arena->unpin(u.chunk);
-      u.arena->free(u.chunk, 1);
-    }
+    if (u.free_after) u.arena->free(u.chunk, 1);
   for (auto& iv : c.invals) {
     bool bad = false;
     for (auto& t : c.touched)

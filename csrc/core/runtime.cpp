@@ -88,7 +88,10 @@ void Runtime::shutdown() {
   delete rt;
 }
 
+void torch_alloc_reset();
+
 Runtime::~Runtime() {
+  torch_alloc_reset();
   stop_cpu_fault_service();
   stop_fault_service();
   for (auto& d : devs_)

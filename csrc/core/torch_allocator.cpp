@@ -6,6 +6,17 @@
 //     2 MB arena chunks (a slab per class, chunks returned when empty);
 //   * size  > 1 MB: a contiguous extent of 2 MB chunks, evicting cold managed
 //     data through the arena's reservation protocol when the budget is full.
+//
+// Stream ordering (the caching-allocator contract torch expects, and what the
+// reference's PMM gets from its trackers, uvm_pmm_gpu.c free-with-tracker):
+//   * free(ptr, stream) records a fence on the freeing stream; the memory is
+//     reusable at once, but every later user waits for that fence GPU-side;
+//   * alloc(size, stream) makes the allocating stream wait (hipStreamWaitEvent,
+//     no host stall) for the fences of the slot / chunks it hands out - the
+//     previous tensor's kernels and any ring copy that last touched the chunk.
+//   * chunks are taken from the arena already pinned and returned while still
+//     pinned (one critical section each): an allocator chunk is never an
+//     eviction victim, and never visible to reserve() between two steps.
 // The C entry points ogkm_torch_alloc / ogkm_torch_free are what
 // CUDAPluggableAllocator dlsym()s.
 #include <mutex>
@@ -21,10 +32,15 @@ namespace {
 constexpr uint64_t kMinClass = 512;
 constexpr int kNumClasses = 12;  // 512 B .. 1 MB
 
+struct Slot {
+  uint32_t index;
+  Tracker fence;  // uses of the previous tensor in this slot
+};
+
 struct Slab {
   uint32_t chunk;
   uint32_t used = 0;
-  std::vector<uint32_t> free_slots;
+  std::vector<Slot> free_slots;
 };
 
 struct DevAlloc {
@@ -37,7 +53,7 @@ struct DevAlloc {
     uint64_t size;
   };
   std::unordered_map<uint64_t, Entry> live;
-  uint64_t allocated = 0, peak = 0, nallocs = 0;
+  uint64_t allocated = 0, peak = 0, nallocs = 0, stream_waits = 0;
 };
 
 std::mutex g_m;
@@ -57,11 +73,28 @@ int class_of(uint64_t size) {
   return -1;
 }
 
+// n pinned chunks from the arena (evicting cold managed data if needed).
+bool take_chunks(Runtime* rt, ChunkArena* a, uint32_t n, uint32_t* first) {
+  if (rt->alloc_chunks(a, n, -1, first, nullptr, true) == Status::OK) return true;
+  Reservation r;
+  if (rt->ensure_capacity(a, n, &r, true) != Status::OK) return false;
+  *first = (uint32_t)r.first;
+  return true;
+}
+
+// The allocating stream waits for everything that last used the memory.
+void order_after(Runtime* rt, DevAlloc* da, Tracker t, void* stream) {
+  t.prune();
+  if (t.empty()) return;
+  if (t.gpu_wait(rt->be(), stream) != Status::OK) t.wait();
+  da->stream_waits++;
+}
+
 }  // namespace
 
-void* torch_alloc(size_t size, int device) {
+void* torch_alloc(size_t size, int device, void* stream) {
   Runtime* rt = Runtime::get();
-  if (!rt || device < 0 || device >= rt->ndev()) return nullptr;
+  if (!rt || !rt->is_local(device)) return nullptr;
   ChunkArena* a = rt->arena_for(Loc::gpu(device));
   if (!a) return nullptr;
   if (size == 0) size = 1;
@@ -72,41 +105,39 @@ void* torch_alloc(size_t size, int device) {
   if (cls >= 0) {
     uint64_t csz = kMinClass << cls;
     Slab* s = nullptr;
-    for (auto& x : da->slabs[cls])
-      if (!x.free_slots.empty()) {
+    // A slot whose previous tensor is done beats one still in flight.
+    for (int pass = 0; pass < 2 && !s; ++pass)
+      for (auto& x : da->slabs[cls]) {
+        if (x.free_slots.empty()) continue;
+        if (pass == 0 && !x.free_slots.back().fence.query()) continue;
         s = &x;
         break;
       }
     if (!s) {
       uint32_t ch;
-      if (rt->alloc_chunks(a, 1, -1, &ch) != Status::OK) {
-        Reservation r;
-        if (rt->ensure_capacity(a, 1, &r) != Status::OK) return nullptr;
-        ch = (uint32_t)r.first;
-      }
-      a->pin(ch);  // allocator chunks are never eviction victims
+      if (!take_chunks(rt, a, 1, &ch)) return nullptr;
+      order_after(rt, da, a->reuse_fence(ch), stream);
       Slab ns;
       ns.chunk = ch;
       uint32_t nslots = (uint32_t)(kBlockSize / csz);
-      for (uint32_t i = nslots; i-- > 0;) ns.free_slots.push_back(i);
+      for (uint32_t i = nslots; i-- > 0;) ns.free_slots.push_back(Slot{i, Tracker{}});
       da->slabs[cls].push_back(std::move(ns));
       s = &da->slabs[cls].back();
     }
-    uint32_t slot = s->free_slots.back();
+    Slot slot = std::move(s->free_slots.back());
     s->free_slots.pop_back();
     s->used++;
-    addr = a->chunk_addr(s->chunk) + (uint64_t)slot * csz;
+    order_after(rt, da, slot.fence, stream);
+    addr = a->chunk_addr(s->chunk) + (uint64_t)slot.index * csz;
     da->live[addr] = DevAlloc::Entry{cls, s->chunk, 0, csz};
     da->allocated += csz;
   } else {
     uint32_t n = (uint32_t)((size + kBlockSize - 1) >> kBlockShift);
     uint32_t first;
-    if (rt->alloc_chunks(a, n, -1, &first) != Status::OK) {
-      Reservation r;
-      if (rt->ensure_capacity(a, n, &r) != Status::OK) return nullptr;
-      first = (uint32_t)r.first;
-    }
-    for (uint32_t i = 0; i < n; ++i) a->pin(first + i);
+    if (!take_chunks(rt, a, n, &first)) return nullptr;
+    Tracker t;
+    for (uint32_t i = 0; i < n; ++i) t.merge(a->reuse_fence(first + i));
+    order_after(rt, da, t, stream);
     addr = a->chunk_addr(first);
     da->live[addr] = DevAlloc::Entry{-1, first, n, (uint64_t)n << kBlockShift};
     da->allocated += (uint64_t)n << kBlockShift;
@@ -116,11 +147,13 @@ void* torch_alloc(size_t size, int device) {
   return (void*)addr;
 }
 
-void torch_free(void* p, int device) {
+void torch_free(void* p, int device, void* stream) {
   Runtime* rt = Runtime::get();
-  if (!rt || !p || device < 0 || device >= rt->ndev()) return;
+  if (!rt || !p || !rt->is_local(device)) return;
   ChunkArena* a = rt->arena_for(Loc::gpu(device));
   DevAlloc* da = dev_alloc(device);
+  // The freeing stream's queued work may still use the memory.
+  FenceRef f = fence_record(rt->be(), device, stream);
   std::lock_guard<std::mutex> g(da->m);
   auto it = da->live.find((uint64_t)p);
   if (it == da->live.end()) return;
@@ -128,17 +161,21 @@ void torch_free(void* p, int device) {
   da->live.erase(it);
   da->allocated -= e.size;
   if (e.cls < 0) {
-    for (uint32_t i = 0; i < e.n; ++i) a->unpin(e.chunk + i);
-    a->free(e.chunk, e.n);
+    for (uint32_t i = 0; i < e.n; ++i)
+      if (f) a->add_reuse_fence(e.chunk + i, f);
+    a->free(e.chunk, e.n);  // still pinned: free() drops the pin atomically
     return;
   }
   auto& slabs = da->slabs[e.cls];
   for (size_t i = 0; i < slabs.size(); ++i) {
     if (slabs[i].chunk != e.chunk) continue;
     uint64_t csz = kMinClass << e.cls;
-    slabs[i].free_slots.push_back((uint32_t)(((uint64_t)p - a->chunk_addr(e.chunk)) / csz));
+    Slot slot{(uint32_t)(((uint64_t)p - a->chunk_addr(e.chunk)) / csz), Tracker{}};
+    if (f) slot.fence.add(f);
+    slabs[i].free_slots.push_back(std::move(slot));
     if (--slabs[i].used == 0) {
-      a->unpin(e.chunk);
+      for (auto& s : slabs[i].free_slots)
+        for (auto& x : s.fence.fences()) a->add_reuse_fence(e.chunk, x);
       a->free(e.chunk, 1);
       slabs.erase(slabs.begin() + i);
     }
@@ -146,22 +183,30 @@ void torch_free(void* p, int device) {
   }
 }
 
-void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs) {
+// Runtime teardown: forget every slab / live entry (their fences reference
+// the backend being destroyed). Tensors still alive after shutdown dangle, as
+// any device memory does once its context is gone.
+void torch_alloc_reset() {
+  std::lock_guard<std::mutex> g(g_m);
+  g_devs.clear();
+}
+
+void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits) {
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);
   *allocated = da->allocated;
   *peak = da->peak;
   *nallocs = da->nallocs;
+  *stream_waits = da->stream_waits;
 }
 
 }  // namespace ogkm
 
 extern "C" {
-__attribute__((visibility("default"))) void* ogkm_torch_alloc(size_t size, int device, void* /*stream*/) {
-  return ogkm::torch_alloc(size, device);
+__attribute__((visibility("default"))) void* ogkm_torch_alloc(size_t size, int device, void* stream) {
+  return ogkm::torch_alloc(size, device, stream);
 }
-__attribute__((visibility("default"))) void ogkm_torch_free(void* ptr, size_t /*size*/, int device,
-                                                            void* /*stream*/) {
-  ogkm::torch_free(ptr, device);
+__attribute__((visibility("default"))) void ogkm_torch_free(void* ptr, size_t /*size*/, int device, void* stream) {
+  ogkm::torch_free(ptr, device, stream);
 }
 }

@@ -17,9 +17,9 @@ namespace py = pybind11;
 using namespace ogkm;
 
 namespace ogkm {
-void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs);
-void* torch_alloc(size_t size, int device);
-void torch_free(void* p, int device);
+void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits);
+void* torch_alloc(size_t size, int device, void* stream);
+void torch_free(void* p, int device, void* stream);
 }  // namespace ogkm
 
 namespace {
@@ -492,8 +492,8 @@ PYBIND11_MODULE(_ogkm, m) {
       a["evictions"] = s.evictions;
       a["free_chunks"] = r->dev(g).hbm->free_chunks();
       a["largest_free_run"] = r->dev(g).hbm->largest_free_run();
-      uint64_t al, pk, na;
-      torch_alloc_stats(g, &al, &pk, &na);
+      uint64_t al, pk, na, sw;
+      torch_alloc_stats(g, &al, &pk, &na, &sw);
       a["torch_allocated"] = al;
       a["torch_peak"] = pk;
       arenas.append(a);
@@ -951,11 +951,14 @@ PYBIND11_MODULE(_ogkm, m) {
   m.def("free_coherent", [](uint64_t p) { rt()->be()->host_free_coherent((void*)p); });
 
   // ---- torch pluggable allocator (in-process use / tests)
-  m.def("torch_alloc", [](uint64_t size, int dev) { return (uint64_t)torch_alloc(size, dev); });
-  m.def("torch_free", [](uint64_t p, int dev) { torch_free((void*)p, dev); });
+  m.def("torch_alloc", [](uint64_t size, int dev, uint64_t stream) {
+    return (uint64_t)torch_alloc(size, dev, (void*)stream);
+  }, py::arg("size"), py::arg("dev"), py::arg("stream") = 0);
+  m.def("torch_free", [](uint64_t p, int dev, uint64_t stream) { torch_free((void*)p, dev, (void*)stream); },
+        py::arg("ptr"), py::arg("dev"), py::arg("stream") = 0);
   m.def("torch_alloc_stats", [](int dev) {
-    uint64_t a, p, n;
-    torch_alloc_stats(dev, &a, &p, &n);
-    return py::make_tuple(a, p, n);
+    uint64_t a, p, n, w;
+    torch_alloc_stats(dev, &a, &p, &n, &w);
+    return py::make_tuple(a, p, n, w);
   });
 }

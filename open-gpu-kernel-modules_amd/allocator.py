@@ -4,6 +4,10 @@
 ``ogkm_torch_alloc`` / ``ogkm_torch_free`` (csrc/core/torch_allocator.cpp), so
 model tensors and managed ranges share one HBM budget (north-star config 2:
 "allocator baseline"). Must be called before the first CUDA allocation.
+
+Frees are stream-ordered: the freeing stream's fence guards the memory, and
+the next allocation of it makes its own stream wait for that fence GPU-side
+(csrc/core/torch_allocator.cpp).
 """
 from __future__ import annotations
 
@@ -28,5 +32,5 @@ def enabled() -> bool:
 
 
 def stats(device: int = 0) -> dict:
-    a, p, n = lib.torch_alloc_stats(device)
-    return {"allocated": a, "peak": p, "allocs": n}
+    a, p, n, w = lib.torch_alloc_stats(device)
+    return {"allocated": a, "peak": p, "allocs": n, "stream_waits": w}

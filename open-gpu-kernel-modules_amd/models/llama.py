@@ -247,7 +247,18 @@ class TieredLlama:
             raise ValueError(f"HBM budget {self.budget / 2**30:.2f} GiB does not cover the unpack staging "
                              f"({self.stage_bytes / 2**30:.2f} GiB) and all-gather slots "
                              f"({self.gather_bytes / 2**30:.2f} GiB): lower the oversubscription")
-        lib.init_device(device, self.arena_bytes)
+        # With the pluggable allocator (config 2) torch tensors - staging,
+        # KV scratch, activations - come out of the same HBM arena: the arena is
+        # the whole budget and the plan keeps 256 MB of it for activations.
+        self.torch_in_arena = False
+        if not self.fake:
+            from .. import allocator as _alloc
+            self.torch_in_arena = _alloc.enabled()
+        if self.torch_in_arena:
+            lib.init_device(device, self.budget)
+            self.arena_bytes -= 256 << 20
+        else:
+            lib.init_device(device, self.arena_bytes)
         self.pinfo: dict = {}
         self.pmode: dict = {}
         gpu = rt.Loc.gpu(device)

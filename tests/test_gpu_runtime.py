@@ -211,6 +211,29 @@ def test_pluggable_allocator_subprocess():
     assert "ALLOC_OK" in r.stdout, r.stdout + r.stderr
 
 
+def test_allocator_free_on_busy_stream_is_stream_ordered(gpu_rt):
+    """Free while the freeing stream is still busy writing the memory, then
+    reallocate it on another stream: the new owner's write must land after the
+    old one (the allocating stream waits GPU-side for the free's fence)."""
+    n = 64 * MB
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    p = lib.torch_alloc(n, 0, s1.cuda_stream)
+    old = rt._tensor_from_ptr(p, (n // 4,), torch.int32, "cuda", 0)
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(200_000_000)     # keep s1 busy (~100 ms)
+        old.fill_(1)
+    lib.torch_free(p, 0, s1.cuda_stream)   # s1 has not run the fill yet
+    q = lib.torch_alloc(n, 0, s2.cuda_stream)
+    assert q == p                          # the same HBM comes back at once
+    new = rt._tensor_from_ptr(q, (n // 4,), torch.int32, "cuda", 0)
+    with torch.cuda.stream(s2):
+        new.fill_(2)
+    torch.cuda.synchronize()
+    assert bool((new == 2).all())          # not overwritten by the old owner's late fill
+    assert lib.torch_alloc_stats(0)[3] >= 1
+    lib.torch_free(q, 0, s2.cuda_stream)
+
+
 def test_bf12_packed_stream_is_bit_exact(gpu_rt):
     """Fused H2D copy + BF12 decode kernel reproduces every bf16 bit pattern."""
     n = 5 * (1 << 20) + 4096  # 2.5 blocks, partial last block

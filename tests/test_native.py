@@ -14,7 +14,7 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 CORE = [p for p in sorted((ROOT / "csrc" / "core").glob("*.cpp"))
-        if p.name not in ("backend_hip.cpp", "torch_allocator.cpp")]
+        if p.name not in ("backend_hip.cpp",)]
 
 
 def _build(kind: str, flags: list[str]) -> Path:
