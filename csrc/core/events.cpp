@@ -10,28 +10,30 @@
 namespace ogkm {
 
 // ------------------------------------------------------------- perf bus
+// Copy-on-write subscriber list: notify() (hot: every migration and fault
+// group) reads a snapshot without copying callbacks or holding the mutex.
 int PerfEventBus::subscribe(PerfEvent e, Cb cb) {
   std::lock_guard<std::mutex> g(m_);
   int t = next_++;
-  subs_.push_back({t, e, std::move(cb)});
+  auto v = std::make_shared<std::vector<Sub>>(subs_ ? *subs_ : std::vector<Sub>{});
+  v->push_back({t, e, std::move(cb)});
+  std::atomic_store(&subs_, std::shared_ptr<const std::vector<Sub>>(std::move(v)));
   return t;
 }
 
 void PerfEventBus::unsubscribe(int token) {
   std::lock_guard<std::mutex> g(m_);
-  subs_.erase(std::remove_if(subs_.begin(), subs_.end(), [&](const Sub& s) { return s.token == token; }),
-              subs_.end());
+  if (!subs_) return;
+  auto v = std::make_shared<std::vector<Sub>>(*subs_);
+  v->erase(std::remove_if(v->begin(), v->end(), [&](const Sub& s) { return s.token == token; }), v->end());
+  std::atomic_store(&subs_, std::shared_ptr<const std::vector<Sub>>(std::move(v)));
 }
 
 void PerfEventBus::notify(const PerfEventData& d) {
-  std::vector<Cb> cbs;
-  {
-    std::lock_guard<std::mutex> g(m_);
-    if (subs_.empty()) return;
-    for (auto& s : subs_)
-      if (s.e == d.type) cbs.push_back(s.cb);
-  }
-  for (auto& cb : cbs) cb(d);
+  std::shared_ptr<const std::vector<Sub>> v = std::atomic_load(&subs_);
+  if (!v) return;
+  for (const Sub& s : *v)
+    if (s.e == d.type) s.cb(d);
 }
 
 // ------------------------------------------------------------- event queue

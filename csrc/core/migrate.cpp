@@ -18,6 +18,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <shared_mutex>
@@ -406,11 +407,10 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
     }
     to->resident |= missing;
   }
+  bool moved = false;
   if (!read_dup) {
-    bool moved = false;
     for (auto& r : b->res)
       if (!(r.loc == dst) && r.resident.intersects(pages)) moved = true;
-    if (moved && cause != Cause::Eviction) thrash_on_migration(b, dst.slot(), now_ns());
     if (copied) {
       // Sources stay valid until the replacing copies are submitted (finish_ctx).
       c.invals.push_back(Ctx::Inval{b, dst, pages});
@@ -443,8 +443,14 @@ done:
   if (Residency* t = b->find(dst)) touch_residency(b, t, cause == Cause::Prefetch);
   b->last_access_ns = now_ns();
   c.cpu_refresh.push_back(b);
-  Tools::get().bus().notify(PerfEventData{PerfEvent::MIGRATION, b->range->id, b->index, Loc{}, dst, 0,
-                                          (uint64_t)pages.count() << kPageShift, (int)cause, 0, 0, false});
+  {
+    // Perf modules (thrashing) see every migration through the bus.
+    PerfEventData ev{PerfEvent::MIGRATION, b->range->id, b->index, Loc{}, dst, 0,
+                     (uint64_t)pages.count() << kPageShift, (int)cause, 0, 0, false};
+    ev.moved = moved;
+    ev.block = b;
+    Tools::get().bus().notify(ev);
+  }
   return Status::OK;
 }
 
@@ -1212,7 +1218,7 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
   c.cause = Cause::User;
   Status result = Status::OK;
   size_t i = 0;
-  uint32_t throttled = 0;
+  uint64_t nap_until = 0;
   while (i < faults.size()) {
     // Group: same (range, block, proc)
     size_t j = i;
@@ -1239,16 +1245,47 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
     for (int attempt = 0; attempt < 8; ++attempt) {
       {
         std::lock_guard<OrderedMutex> g(b->lock);
-        b->faults_by_proc[proc == kCpuProc ? kMaxGpus : proc]++;
+        if (attempt == 0) {
+          PerfEventData fe{PerfEvent::FAULT, r->id, b->index, Loc{}, proc_loc(proc), proc,
+                           (uint64_t)pages.count() << kPageShift, (int)Cause::User, pages.next_set(0),
+                           (uint32_t)pages.count(), acc == Access::WRITE};
+          fe.block = b;
+          Tools::get().bus().notify(fe);  // prefetch module: per-processor fault counts
+        }
         tools_event(proc == kCpuProc ? ToolsEventType::CpuFault : ToolsEventType::GpuFault, Cause::User, Loc{}, Loc{},
                     proc, r->addr() + b->block_offset(), (uint64_t)pages.count() << kPageShift, r->id);
         ResidencyDecision d = select_residency(this, b, proc, acc, pages);
-        if (d.map_remote) {
+        // THROTTLE (consumed as at uvm_va_block.c:12528): the processor naps on
+        // this block - map the closest copy remotely when it can reach it,
+        // else come back once the nap ends.
+        if (thrash_hint(b, proc_loc(proc).slot(), now_ns()) == ThrashHint::THROTTLE && !d.map_remote) {
+          Loc closest;
+          bool found = false;
+          for (auto& x : b->res)
+            if (x.resident.intersects(pages) && !x.loc.is_gpu()) {  // host / CXL: reachable by every processor
+              closest = x.loc;
+              found = true;
+              break;
+            }
+          Tools::get().inc(Counter::ThrottleEvents);
+          if (found && !(closest == proc_loc(proc))) {
+            d.dst = closest;
+            d.map_remote = true;
+            d.read_dup = false;
+            Tools::get().inc(Counter::MapRemote);
+            tools_event(ToolsEventType::MapRemote, Cause::Thrashing, closest, proc_loc(proc), proc,
+                        r->addr() + b->block_offset(), (uint64_t)pages.count() << kPageShift, r->id);
+          } else {
+            nap_until = b->thrash.throttle_until_ns;
+          }
+        }
+        if (nap_until) {
+          // serviced after the nap (below, outside the block lock)
+        } else if (d.map_remote) {
           // Keep in place; make sure the pages exist somewhere reachable.
           PageMask have = b->resident_anywhere();
           PageMask need = pages.andnot(have);
           if (!need.empty()) st = make_resident(c, b, need, d.dst, false, Cause::User);
-          if (b->thrash.detected) throttled++;
         } else {
           PageMask want = pages;
           Residency* y = b->find(d.dst);
@@ -1260,6 +1297,14 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
           }
           st = make_resident(c, b, want, d.dst, d.read_dup, Cause::User);
         }
+      }
+      if (nap_until) {
+        // The faulting processor naps (a CPU thread sleeps; a GPU's fault is
+        // replayed later): at most one nap per group, then it is serviced.
+        uint64_t now = now_ns();
+        if (nap_until > now) std::this_thread::sleep_for(std::chrono::nanoseconds(nap_until - now));
+        nap_until = 0;
+        continue;
       }
       if (st != Status::MORE_PROCESSING_REQUIRED) break;
       finish_ctx(c, out);
@@ -1273,7 +1318,6 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
       c.need_arena = nullptr;
     }
     if (st != Status::OK && result == Status::OK) result = st;
-    if (throttled > (uint32_t)config().perf_fault_max_throttle_per_service) break;
     i = j;
   }
   Status fs = finish_ctx(c, out);

@@ -172,12 +172,52 @@ ThrashHint thrash_on_migration(Block* b, int dst_slot, uint64_t now) {
         t.throttles = 0;
         h = ThrashHint::PIN;
         Tools::get().inc(Counter::PinEvents);
+      } else {
+        // The processor that just pulled the block in naps: its next faults
+        // on the block do not migrate it again until the nap ends.
+        t.throttle_until_ns = now + lapse * (uint64_t)std::max<int64_t>(1, config().perf_thrashing_nap);
+        t.throttle_slot = dst_slot;
+        if (!t.throttling)
+          tools_event(ToolsEventType::ThrottlingStart, Cause::Thrashing, Loc{}, Loc{}, dst_slot,
+                      b->range->addr() + b->block_offset(), kBlockSize, b->range->id);
+        t.throttling = true;
       }
     }
   }
   t.last_dst_slot = dst_slot;
   t.last_migration_ns = now;
   return h;
+}
+
+ThrashHint thrash_hint(Block* b, int slot, uint64_t now) {
+  ThrashState& t = b->thrash;
+  if (t.pinned_until_ns > now) return ThrashHint::PIN;
+  if (t.throttling && now >= t.throttle_until_ns) {
+    t.throttling = false;
+    tools_event(ToolsEventType::ThrottlingEnd, Cause::Thrashing, Loc{}, Loc{}, t.throttle_slot,
+                b->range->addr() + b->block_offset(), kBlockSize, b->range->id);
+  }
+  if (t.throttling && slot == t.throttle_slot) return ThrashHint::THROTTLE;
+  return ThrashHint::NONE;
+}
+
+// ---------------------------------------------------------------- perf modules
+// Thrashing module: consumes MIGRATION events (state update + hints on the
+// block); prefetch module: consumes FAULT events (per-processor fault counts
+// that gate the bitmap-tree prefetch). Callbacks run with the block lock held.
+std::vector<int> perf_modules_register(PerfEventBus& bus) {
+  std::vector<int> tok;
+  tok.push_back(bus.subscribe(PerfEvent::MIGRATION, [](const PerfEventData& d) {
+    auto* b = static_cast<Block*>(d.block);
+    if (!b || !d.moved || d.cause == (int)Cause::Eviction) return;
+    thrash_on_migration(b, d.dst.slot(), now_ns());
+  }));
+  tok.push_back(bus.subscribe(PerfEvent::FAULT, [](const PerfEventData& d) {
+    auto* b = static_cast<Block*>(d.block);
+    if (!b) return;
+    b->faults_by_proc[d.processor == kCpuProc ? kMaxGpus : d.processor]++;
+  }));
+  return tok;
 }
 
 bool thrash_pinned(Block* b, uint64_t now) { return b->thrash.pinned_until_ns > now; }

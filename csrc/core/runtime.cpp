@@ -67,6 +67,7 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
     }
     rt->devs_.push_back(std::move(dev));
   }
+  rt->perf_subs_ = perf_modules_register(Tools::get().bus());
   g_rt.store(rt, std::memory_order_release);
   install_cpu_fault_handler();
   start_cpu_fault_service();
@@ -92,6 +93,7 @@ void torch_alloc_reset();
 
 Runtime::~Runtime() {
   torch_alloc_reset();
+  for (int t : perf_subs_) Tools::get().bus().unsubscribe(t);
   stop_cpu_fault_service();
   stop_fault_service();
   for (auto& d : devs_)

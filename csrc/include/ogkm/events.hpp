@@ -46,6 +46,8 @@ struct PerfEventData {
   int cause = 0;
   uint32_t first_page = 0, npages = 0;
   bool is_write = false;
+  bool moved = false;      // MIGRATION: other copies were revoked (not a read duplicate)
+  void* block = nullptr;   // in-process subscribers: the Block (its lock is held by the notifier)
 };
 
 class PerfEventBus {
@@ -57,8 +59,8 @@ class PerfEventBus {
 
  private:
   struct Sub { int token; PerfEvent e; Cb cb; };
-  std::mutex m_;
-  std::vector<Sub> subs_;
+  std::mutex m_;  // writers
+  std::shared_ptr<const std::vector<Sub>> subs_;  // snapshot read by notify()
   int next_ = 1;
 };
 

@@ -273,6 +273,7 @@ class Runtime {
   std::atomic<uint64_t> fs_batches_{0};
   std::mutex fs_m_;
   OrderedMutex pm_{LockOrder::GLOBAL_PM};
+  std::vector<int> perf_subs_;  // perf-module subscriptions on the tools bus
 };
 
 // Per-operation migration context: rings used, blocks touched, chunks read by
@@ -322,6 +323,13 @@ PageMask prefetch_hint(const PageMask& resident_on_dst, const PageMask& faulted,
 // Thrashing hint (uvm_perf_thrashing.c:1615).
 enum class ThrashHint { NONE = 0, THROTTLE = 1, PIN = 2 };
 ThrashHint thrash_on_migration(Block* b, int dst_slot, uint64_t now);
+// Hint for a fault by processor slot `slot` on b at `now` (block lock held):
+// PIN while pinned, THROTTLE while `slot` naps; emits ThrottlingEnd once a nap
+// has expired.
+ThrashHint thrash_hint(Block* b, int slot, uint64_t now);
+// The perf modules (thrashing, prefetch) as PerfEventBus subscribers
+// (uvm_perf_events.c:56-94 registration); returns the subscription tokens.
+std::vector<int> perf_modules_register(PerfEventBus& bus);
 bool thrash_pinned(Block* b, uint64_t now);
 
 // CPU faults on managed CPU views (csrc/core/cpu_fault.cpp): an

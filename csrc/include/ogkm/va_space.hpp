@@ -50,6 +50,12 @@ struct ThrashState {
   uint64_t pinned_until_ns = 0;
   int last_dst_slot = -1;
   bool detected = false;
+  // THROTTLE (uvm_perf_thrashing.c:1535-1762 hints): the processor pulling the
+  // block back and forth naps - its faults on the block map remotely or wait -
+  // until throttle_until_ns.
+  uint64_t throttle_until_ns = 0;
+  int throttle_slot = -1;
+  bool throttling = false;  // ThrottlingStart emitted, ThrottlingEnd pending
 };
 
 // Software access counters (uvm_gpu_access_counters.c analog): remote accesses

@@ -4,6 +4,8 @@ demotion, prefetch / two-pass migrate, and the software fault batch service.
 Modelled on the reference's UVM_TEST_VA_RESIDENCY_INFO-driven tests."""
 from __future__ import annotations
 
+import time
+
 import pytest
 import torch
 
@@ -181,7 +183,7 @@ def test_prefetch_hint_bitmap_tree(fake_rt):
 def test_thrashing_detection_pins_block(fake_rt):
     lib.configure("perf_thrashing_threshold", 3)
     lib.configure("perf_thrashing_pin_threshold", 2)
-    lib.configure("perf_thrashing_lapse_usec", 10_000_000)
+    lib.configure("perf_thrashing_lapse_usec", 50_000)
     b = rt.malloc_managed(2 * MB, "th")
     b.write(torch.ones(2 * MB, dtype=torch.uint8))
     for i in range(8):
@@ -260,3 +262,37 @@ def test_ring_gather_scatter_memset_cpu(fake_rt):
     m = torch.empty(1 << 16, dtype=torch.int32)
     lib.ring_memset(0, 4, m.data_ptr(), 0x7F7F7F7F, m.numel() * 4)
     assert bool((m == 0x7F7F7F7F).all())
+
+
+def test_thrashing_throttle_then_pin_via_perf_bus(fake_rt):
+    """GPU0 <-> CPU write ping-pong on one block: the thrashing module (a perf
+    bus subscriber) detects it, throttles the processor that keeps pulling the
+    block - its next fault maps the host copy remotely instead of migrating -
+    ends the throttle after the nap, and finally pins the block
+    (uvm_perf_thrashing.c:1535-1762, consumed as at uvm_va_block.c:12528)."""
+    from ogkm import tools
+
+    lib.configure("perf_thrashing_threshold", 3)
+    lib.configure("perf_thrashing_pin_threshold", 4)
+    lib.configure("perf_thrashing_lapse_usec", 50_000)   # nap = 1 lapse = 50 ms
+    q = tools.EventQueue(events=["ThrashingDetected", "ThrottlingStart", "ThrottlingEnd", "MapRemote"])
+    b = rt.malloc_managed(2 * MB, "pp")
+    b.write(torch.ones(2 * MB, dtype=torch.uint8))
+    procs = [0, rt.CPU, 0, rt.CPU, 0]          # the 4th migration throttles the CPU, the 5th the GPU
+    for p in procs:
+        lib.service_faults([(b.id, 0, 4096, p, rt.WRITE)])
+    assert lib.stats()["thrashing_detected"] >= 1
+    # the GPU is napping: its fault on a page still on the host maps it remotely
+    mr0 = lib.stats()["map_remote"]
+    lib.service_faults([(b.id, 8 * 4096, 4096, 0, rt.READ)])
+    assert lib.stats()["map_remote"] == mr0 + 1
+    assert not any(r["tier"] == "gpu" and r["pages"] > 1 for r in b.residency(0)["resident_on"])
+    time.sleep(0.06)                           # the nap ends
+    for p in [rt.CPU, 0, rt.CPU, 0, rt.CPU, 0]:
+        lib.service_faults([(b.id, 0, 4096, p, rt.WRITE)])
+    ev = [e["type"] for e in q.read_dicts()]
+    q.close()
+    assert "ThrashingDetected" in ev and "ThrottlingStart" in ev and "MapRemote" in ev and "ThrottlingEnd" in ev
+    assert ev.index("ThrottlingStart") < ev.index("MapRemote") < ev.index("ThrottlingEnd")
+    assert lib.stats()["pin_events"] >= 1 and b.residency(0)["pinned"]
+    b.free()
