@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--planner", choices=("static", "off"), default="static",
                     help="off: no residency plan - every weight prefers HBM, nothing is pinned, the runtime's "
                          "LRU / prefetch / eviction decide residency")
+    ap.add_argument("--kv-tiering", action="store_true",
+                    help="KV prefixes as evictable per-layer units (resident with their layer, else streamed)")
     ap.add_argument("--allocator", action="store_true",
                     help="route torch CUDA allocations through the runtime's HBM arena (pluggable allocator)")
     ap.add_argument("--verbose", action="store_true")
@@ -211,7 +213,7 @@ def main() -> None:
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
                               seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
                               weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac, kv_format=a.kv_format,
-                              parallel=a.parallel, planner=a.planner)
+                              parallel=a.parallel, planner=a.planner, kv_tiering=a.kv_tiering)
     plan = model.describe()
     init_s = time.perf_counter() - t_init
     g = torch.Generator(device="cpu").manual_seed(42)
@@ -290,6 +292,7 @@ def main() -> None:
                                 else f"{'shards' if a.parallel == 'shards' else 'tp'}{world}"),
                 "backend": a.backend,
                 "planner": a.planner,
+                "kv_tiering": a.kv_tiering,
                 "torch_allocator": "ogkm-arena" if a.allocator else "torch-caching",
                 "rank_host_numa_nodes": host_nodes,
                 "tiers": plan["tiers"],

@@ -163,7 +163,8 @@ class TieredLlama:
                  device: int = 0, tp_rank: int = 0, tp_world: int = 1, seed: int = 0, lookahead: int = 2,
                  hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
                  packed: bool = True, weight_format: str = "bf11", tiers: str = "host", cxl_frac: float = 0.5,
-                 kv_format: str = "bf16", parallel: str = "tp", planner: str = "static"):
+                 kv_format: str = "bf16", parallel: str = "tp", planner: str = "static",
+                 kv_tiering: bool = False):
         if parallel not in ("tp", "shards"):
             raise ValueError("parallel must be 'tp' or 'shards'")
         # planner "static": the plan below picks resident layers and pins them
@@ -241,7 +242,14 @@ class TieredLlama:
         self.shard_max = _al(-(-stream_bound // self.sworld)) if self.sworld > 1 else 0
         self.gather_bytes = chunks(self.gather_depth * self.sworld * self.shard_max) if self.sworld > 1 else 0
         self.arena_bytes = self.budget - self.stage_bytes - self.gather_bytes
-        if kv_format != "bf16":
+        # KV tiering: each layer's prefilled context is a managed
+        # unit like a weight matrix - resident with its layer or streamed (and
+        # evicted) past the budget, prefetched layer-ahead; decode tokens go to a
+        # small always-resident tail. Per layer, prefix + tail are assembled in
+        # one [2, B, hkv, T, hd] scratch that attention reads.
+        self.kv_tier = bool(kv_tiering)
+        self.kv_split = kv_format != "bf16" or self.kv_tier
+        if self.kv_split:
             self.arena_bytes -= chunks(self.kv_layer_bytes)  # the per-layer KV scratch
         if self.arena_bytes <= 0:
             raise ValueError(f"HBM budget {self.budget / 2**30:.2f} GiB does not cover the unpack staging "
@@ -278,8 +286,9 @@ class TieredLlama:
         self.kv_format = kv_format
         self.tail = self.T - context
         self.kv_tail_bytes = cfg.n_layers * 2 * batch * self.hkv * self.tail * hd * 2
-        self.kv_scratch_bytes = self.kv_layer_bytes if kv_format != "bf16" else 0
+        self.kv_scratch_bytes = self.kv_layer_bytes if self.kv_split else 0
         self.kv_streams, self.kv_infos, self.kv_slot = [], [], 0
+        self.kv_prefix_bytes = 2 * batch * self.hkv * context * hd * 2  # raw bf16 prefix of one layer
         if kv_format != "bf16":
             for i, full in enumerate(self._gen_prefill()):
                 st, inf = bf12.pack(full, chunk_values=cv, fmt=kv_format)
@@ -290,6 +299,12 @@ class TieredLlama:
             self.kv_resident_bytes = cfg.n_layers * self.kv_slot + _al(self.kv_tail_bytes)
         else:
             self.kv_resident_bytes = _al(self.kv_bytes)
+        if self.kv_tier:
+            # prefixes leave the resident range: they are units now
+            self.kv_unit_bytes = self.kv_slot if kv_format != "bf16" else _al(self.kv_prefix_bytes)
+            self.kv_resident_bytes = _al(self.kv_tail_bytes)
+        else:
+            self.kv_unit_bytes = 0
         # ---- streamed units: each layer's four matrices and the LM head split
         # into row parts no larger than the largest matrix. Streaming per unit
         # (not per layer) keeps the HBM reserved for in-flight streaming at a
@@ -321,12 +336,13 @@ class TieredLlama:
         # Streaming slots: the unit in use + `lookahead` prefetched + one
         # run-ahead slot (the host runs ahead of the GPU: when unit u+lookahead is
         # prefetched, unit u-1 may still be read by queued kernels).
-        slot = max([chunks(b) for b in self.res_part.values()] + [chunks(b) for b in self.res_head_part])
+        slot = max([chunks(b) for b in self.res_part.values()] + [chunks(b) for b in self.res_head_part]
+                   + [chunks(self.kv_unit_bytes)])
         self.slot_bytes = slot
         # The prefetch window must cover the longest resident stretch (~2 layers
         # of compute) or the link idles behind it: at least OGKM_WINDOW_MB in flight.
         # (Capped at a quarter of the arena left after the KV cache: small models.)
-        layer_cost = sum(chunks(b) for b in self.res_part.values())
+        layer_cost = sum(chunks(b) for b in self.res_part.values()) + chunks(self.kv_unit_bytes)
         head_cost = sum(chunks(b) for b in self.res_head_part)
         fixed = chunks(self.kv_resident_bytes + self.norm_bytes)
         window_min = int(float(os.environ.get("OGKM_WINDOW_MB", "384")) * 2**20)
@@ -365,7 +381,7 @@ class TieredLlama:
                     if cost <= left:
                         self.extra_resident.add(key)
                         left -= cost
-        self.streamed_bytes = (sum(self.res_layer_bytes for r in self.resident if not r)
+        self.streamed_bytes = (sum(self.res_layer_bytes + self.kv_unit_bytes for r in self.resident if not r)
                                - sum(self.res_part[k[2]] for k in self.extra_resident)
                                + (0 if self.head_resident else self.res_head_bytes))
         # a window that wraps around a small streamed set would evict units before their use
@@ -378,7 +394,8 @@ class TieredLlama:
         if tiers not in ("host", "host+cxl"):
             raise ValueError("tiers must be 'host' or 'host+cxl'")
         self.tiers = tiers
-        self.order = ([("layer", i, n) for i in range(cfg.n_layers) for n in self.parts]
+        self.order = ([k for i in range(cfg.n_layers) for n in self.parts
+                       for k in ([("layer", i, n)] + ([("kv", i)] if self.kv_tier and n == self.parts[0] else []))]
                       + [("head", j) for j in range(len(self.head_rows))])
         streamed_keys = [k for k in self.order if not self._is_resident(k)]
         self.rest_loc = {}
@@ -417,6 +434,17 @@ class TieredLlama:
             else:
                 self._alloc_unit(("head", j), part, None, gpu, host)
         del head
+        if self.kv_tier:
+            gen = None if kv_format != "bf16" else self._gen_prefill()
+            for i in range(cfg.n_layers):
+                key = ("kv", i)
+                data = self.kv_streams[i] if kv_format != "bf16" else next(gen).reshape(-1).view(torch.uint8)
+                b = rt.malloc_managed(self.kv_unit_bytes, f"kv-{i}", cpu_view=False)
+                self._place(b, self._is_resident(key), gpu, self.rest_loc.get(key, host), self.planner)
+                b.write(data)
+                self.ubuf[key] = b
+                del data
+            self.kv_streams = []
         self.embed.write(self._gen_embed())
         if not self.fake:
             torch.cuda.synchronize(self.dev)
@@ -425,7 +453,7 @@ class TieredLlama:
         # RMSNorm weights of every layer + the final norm (after the KV cache)
         self.kv.write(torch.ones((2 * cfg.n_layers + 1) * cfg.dim, dtype=torch.bfloat16),
                       offset=self.kv_resident_bytes)
-        for i, st in enumerate(self.kv_streams):
+        for i, st in enumerate(self.kv_streams):  # (tiering: written to the KV units above)
             self.kv.write(st, offset=i * self.kv_slot)
         self.kv_streams = []
         self.cos, self.sin = D.rope_tables(hd, self.T, cfg.rope_theta, self.tdev)
@@ -436,7 +464,7 @@ class TieredLlama:
         self.norm_w = rt._tensor_from_ptr(self.kv_lease.dptr + self.kv_resident_bytes, (2 * cfg.n_layers + 1, cfg.dim),
                                           torch.bfloat16, tdev, device)
         self.final_norm = self.norm_w[2 * cfg.n_layers]
-        if kv_format == "bf16":
+        if not self.kv_split:
             kv = self.kv_lease.tensor((cfg.n_layers, 2, batch, self.hkv, self.T, hd), torch.bfloat16)
             for i, full in enumerate(self._gen_prefill()):
                 kv[i, :, :, :, :context].copy_(full)
@@ -444,7 +472,8 @@ class TieredLlama:
             self.kv_t = kv
         else:
             self.kv_t = None
-            self.kv_tail_t = rt._tensor_from_ptr(self.kv_lease.dptr + cfg.n_layers * self.kv_slot,
+            tail_off = 0 if self.kv_tier else cfg.n_layers * self.kv_slot
+            self.kv_tail_t = rt._tensor_from_ptr(self.kv_lease.dptr + tail_off,
                                                  (cfg.n_layers, 2, batch, self.hkv, max(self.tail, 1), hd),
                                                  torch.bfloat16, tdev, device)
             self.kv_scratch = torch.empty(2, batch, self.hkv, self.T, hd, dtype=torch.bfloat16, device=self.tdev)
@@ -466,12 +495,13 @@ class TieredLlama:
         self.use_trace = None      # diagnostics: [(key, acquire s, wait s)] per streamed use
         self._pinned: dict = {}    # resident tensors: key -> weight refs (leased for the model's lifetime)
         self._pin_leases: list = []
+        self._kv_pinned: dict = {}  # kv tiering: resident layers' prefix pointers
         self.keep_logits = False   # tests: keep the full-vocab logits of the last step
         self.last_logits = None
         self.gather = None
         if self.sworld > 1:
             from ..parallel.shards import UnitGather
-            self.gather = UnitGather(self.order, self._buf, self._unit_bytes, self.sworld, self.gather_depth,
+            self.gather = UnitGather([k for k in self.order if k[0] != "kv"], self._buf, self._unit_bytes, self.sworld, self.gather_depth,
                                      device=self.tdev, dev_index=device)
         self.init_seconds = time.perf_counter() - t0
         if verbose:
@@ -481,7 +511,7 @@ class TieredLlama:
     def describe(self) -> dict:
         d = {
             "model": self.cfg.name, "tp": f"{self.rank}/{self.world}", "parallel": self.parallel,
-            "planner": self.planner,
+            "planner": self.planner, "kv_tiering": self.kv_tier,
             "shard": f"{self.srank}/{self.sworld}", "batch": self.B, "global_batch": self.B_global,
             "gather_gb": self.gather_bytes / 1e9, "context": self.ctx,
             "footprint_gb": self.footprint / 1e9, "hbm_budget_gb": self.budget / 1e9,
@@ -511,12 +541,16 @@ class TieredLlama:
     def _is_resident(self, key) -> bool:
         if key[0] == "layer":
             return self.resident[key[1]] or key in self.extra_resident
+        if key[0] == "kv":
+            return self.resident[key[1]]
         return self.head_resident
 
     def _buf(self, key) -> "rt.ManagedBuffer":
         return self.ubuf[key]
 
     def _unit_bytes(self, key) -> int:
+        if key[0] == "kv":
+            return self.kv_unit_bytes
         return self.res_part[key[2]] if key[0] == "layer" else self.res_head_part[key[1]]
 
     def _unit_shape(self, key) -> tuple:
@@ -644,11 +678,21 @@ class TieredLlama:
 
     def _kv_layer(self, i: int, pos: int) -> torch.Tensor:
         """Layer i's KV cache as [2, B, hkv, T, hd], valid for positions < pos."""
-        if self.kv_format == "bf16":
+        if not self.kv_split:
             return self.kv_t[i]
         sc = self.kv_scratch
-        bf12.unpack_into(sc, self.kv_lease.dptr + i * self.kv_slot, self.kv_infos[i], self.dev,
-                         0 if self.fake else None, dst_stride=self.T * self.cfg.head_dim)
+        lease, ptr = self._kv_prefix(i) if self.kv_tier else (None, self.kv_lease.dptr + i * self.kv_slot)
+        if self.kv_format != "bf16":
+            bf12.unpack_into(sc, ptr, self.kv_infos[i], self.dev, 0 if self.fake else None,
+                             dst_stride=self.T * self.cfg.head_dim)
+        else:
+            hd = self.cfg.head_dim
+            pre = rt._tensor_from_ptr(ptr, (2, self.B, self.hkv, self.ctx, hd), torch.bfloat16,
+                                      "cpu" if self.fake else "cuda", self.dev)
+            sc[:, :, :, :self.ctx].copy_(pre)
+        if lease is not None:  # the prefix's readers are enqueued: the unit may be evicted behind them
+            lease.release(0 if self.fake else None)
+            self._mark_consumed()
         t = pos - self.ctx
         if t > 0:
             sc[:, :, :, self.ctx:pos].copy_(self.kv_tail_t[i, :, :, :, :t])
@@ -657,19 +701,24 @@ class TieredLlama:
     def _rope_append(self, i: int, pos: int, kv_layer: torch.Tensor, qkv: torch.Tensor) -> torch.Tensor:
         """RoPE on q/k + append k/v at pos (into the cache / scratch and the
         packed cache's raw tail) in one fused kernel; returns rotated q."""
-        tail = self.kv_tail_t[i] if self.kv_format != "bf16" else None
+        tail = self.kv_tail_t[i] if self.kv_split else None
         return fused.rope_kv(qkv, self.cos[pos], self.sin[pos], kv_layer, pos, self.hq, self.hkv, tail=tail,
                              tail_pos=pos - self.ctx, device_index=self.dev)
 
     def host_kv(self, i: int) -> torch.Tensor:
         """Layer i's KV cache [2, B, hkv, T, hd] on the host (reference numerics)."""
-        if self.kv_format == "bf16":
-            return self.kv_t[i].cpu()
+        if not self.kv_split:
+            return self.kv_t[i].to("cpu", copy=True)
         if not self.fake:
             torch.cuda.synchronize(self.dev)
-        raw = self.kv.read(offset=i * self.kv_slot, nbytes=self.kv_infos[i].nbytes)
+        src, off = (self.ubuf[("kv", i)], 0) if self.kv_tier else (self.kv, i * self.kv_slot)
         out = torch.zeros(2, self.B, self.hkv, self.T, self.cfg.head_dim, dtype=torch.bfloat16)
-        pre = bf12.unpack_host(raw, self.kv_infos[i]).view(2, self.B, self.hkv, self.ctx, self.cfg.head_dim)
+        if self.kv_format != "bf16":
+            raw = src.read(offset=off, nbytes=self.kv_infos[i].nbytes)
+            pre = bf12.unpack_host(raw, self.kv_infos[i]).view(2, self.B, self.hkv, self.ctx, self.cfg.head_dim)
+        else:
+            raw = src.read(offset=off, nbytes=self.kv_prefix_bytes)
+            pre = raw.view(torch.bfloat16).view(2, self.B, self.hkv, self.ctx, self.cfg.head_dim)
         out[:, :, :, :self.ctx] = pre
         out[:, :, :, self.ctx:] = self.kv_tail_t[i, :, :, :, :self.tail].cpu()
         return out
@@ -768,6 +817,25 @@ class TieredLlama:
             self._mark_consumed()
             return None, st
         return lease, refs
+
+    def _kv_prefix(self, i: int):
+        """Fault layer i's KV prefix unit in: (lease or None, device pointer).
+        Resident layers keep theirs leased for the model's lifetime."""
+        key = ("kv", i)
+        ptr = self._kv_pinned.get(i)
+        if ptr is not None:
+            return None, ptr
+        if not self._is_resident(key):
+            if self._inflight and self._inflight[0] == key:
+                self._inflight.pop(0)
+            self._prefetch_ahead()
+        lease = self._buf(key).acquire(self.dev, rt.READ)
+        lease.wait(0 if (self.fake or _HOST_LEASE_WAIT) else None)
+        if self._is_resident(key):
+            self._kv_pinned[i] = lease.dptr
+            self._pin_leases.append(lease)
+            return None, lease.dptr
+        return lease, lease.dptr
 
     def _mark_consumed(self) -> None:
         """A streamed unit's readers are enqueued: remember where the compute
@@ -891,7 +959,7 @@ class TieredLlama:
         self.kv_lease.release(0 if self.fake else None)
         for lease in self._pin_leases:
             lease.release(0 if self.fake else None)
-        self._pin_leases, self._pinned = [], {}
+        self._pin_leases, self._pinned, self._kv_pinned = [], {}, {}
         lib.sync_all()
         for b in [self.embed, self.kv] + list(self.ubuf.values()):
             b.free()

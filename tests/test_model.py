@@ -241,3 +241,32 @@ def test_planner_off_matches_static_plan(fake_rt):
     for a, b in zip(out["static"][0], out["off"][0]):
         assert torch.equal(a, b)
     assert out["off"][1] > 0
+
+
+@pytest.mark.parametrize("kv_format", ["bf16", "ans"])
+def test_kv_tiering_bit_identical_to_resident_kv(fake_rt, kv_format):
+    """KV tiering: each layer's prefilled KV is a managed unit that streams with
+    its layer (evicted past the budget, prefetched ahead); logits are
+    bit-identical to the resident-KV run and KV units really were streamed."""
+    lib.shutdown()
+    rt.init("fake", fake_devices=1, fake_hbm_mb=512, lock_check=1, host_budget_mb=1024)
+    cfg = llama.CONFIGS["tiny"]
+    out = {}
+    for tier in (False, True):
+        m = llama.TieredLlama(cfg, batch=2, context=128, max_new_tokens=4, oversub=2.0, lookahead=1, seed=11,
+                              kv_format=kv_format, weight_format="bf16", kv_tiering=tier)
+        m.keep_logits = True
+        logs = []
+        for s in range(3):
+            m.step(torch.tensor([3, 9]) + s)
+            logs.append(m.last_logits.clone())
+        if tier:
+            streamed_kv = [k for k in m.stream_seq if k[0] == "kv"]
+            assert streamed_kv, "some KV prefixes must stream at 2x oversubscription"
+            assert m.describe()["kv_tiering"]
+            for i in range(cfg.n_layers):   # the host view of the tiered cache matches the resident one
+                assert torch.equal(m.host_kv(i), out[False][1][i])
+        out[tier] = (logs, [m.host_kv(i) for i in range(cfg.n_layers)])
+        m.close()
+    for a, b in zip(out[False][0], out[True][0]):
+        assert torch.equal(a, b)

@@ -50,3 +50,30 @@ def test_formats_bit_identical_gpu(gpu_rt):
     for fmt in ("bf11", "ans"):
         for a, b in zip(outs["bf16"], outs[fmt]):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("kv_format", ["bf16", "ans"])
+def test_kv_tiering_matches_fp32_reference_and_resident_kv_gpu(gpu_rt, kv_format):
+    """KV prefixes as streamed per-layer units on the GPU: logits match the fp32
+    reference and are bit-identical to the resident-KV run."""
+    cfg = llama.CONFIGS["small"]
+    outs = {}
+    for tier in (False, True):
+        m = llama.TieredLlama(cfg, batch=4, context=128, max_new_tokens=4, oversub=2.0, lookahead=1, seed=13,
+                              weight_format="ans", kv_format=kv_format, kv_tiering=tier)
+        m.keep_logits = True
+        tok = torch.tensor([5, 17, 900, 33], device="cuda")
+        logs = []
+        for _ in range(3):
+            ref = llama.reference_step(cfg, m, tok.cpu(), m.pos).cpu() if tier else None
+            tok = m.step(tok)
+            torch.cuda.synchronize()
+            logs.append(m.last_logits.cpu())
+            if tier:
+                torch.testing.assert_close(logs[-1], ref, atol=0.05, rtol=0.05)
+        if tier:
+            assert any(k[0] == "kv" for k in m.stream_seq)
+        outs[tier] = logs
+        m.close()
+    for a, b in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)
