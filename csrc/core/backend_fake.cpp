@@ -300,6 +300,14 @@ class FakeBackend : public Backend {
     });
     return Status::OK;
   }
+  Status page_copy(int, uint64_t dst_base, uint64_t src_base, const uint32_t* idx, uint32_t npages,
+                   void* s) override {
+    std::vector<uint32_t> v(idx, idx + npages);
+    run(s, [dst_base, src_base, v] {
+      for (uint32_t p : v) memcpy((char*)dst_base + ((uint64_t)p << 12), (char*)src_base + ((uint64_t)p << 12), 4096);
+    });
+    return Status::OK;
+  }
   Status scatter_pages(int, const PageListDesc& d, void* s) override {
     std::vector<uint32_t> idx(d.idx, d.idx + d.npages);
     PageListDesc dd = d;

@@ -22,6 +22,7 @@
 //   streaming read (tools/probe_sdma.hip, profiles/r2_copy_engines.md) SDMA costs
 //   the reader 1.06x, our 16-WG CU copy kernel 2.86x, at the same 56.8 GB/s.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
@@ -414,6 +415,24 @@ class HipBackend : public Backend {
     return Status::OK;
   }
   Status gather_pages(int dev, const PageListDesc& d, void* s) override { return page_list(dev, d, s, false); }
+  void range_push(const char* name) override { roctxRangePushA(name); }
+  void range_pop() override { roctxRangePop(); }
+  void mark(const char* name) override { roctxMarkA(name); }
+  Status stream_check(void* s) override {
+    hipError_t e = hipStreamQuery((hipStream_t)s);
+    if (e == hipSuccess || e == hipErrorNotReady) return Status::OK;
+    last_err_ = std::string("stream: ") + hipGetErrorString(e);
+    return Status::IO_ERROR;
+  }
+  Status page_copy(int, uint64_t dst_base, uint64_t src_base, const uint32_t* idx, uint32_t npages,
+                   void* s) override {
+    if (npages > 512) return Status::INVALID_ARGUMENT;
+    KPageList pl;
+    for (uint32_t i = 0; i < npages; ++i) pl.idx[i] = (uint16_t)idx[i];
+    uint32_t wgs = (uint32_t)config().copy_workgroups;
+    HIPCHK(launch_page_copy(dst_base, src_base, pl, npages, wgs ? wgs : 16, (hipStream_t)s));
+    return Status::OK;
+  }
   Status scatter_pages(int dev, const PageListDesc& d, void* s) override { return page_list(dev, d, s, true); }
   Status memset32(int, uint64_t dst, uint32_t pat, size_t bytes, void* s) override {
     HIPCHK(launch_memset32(dst, pat, bytes, (hipStream_t)s));

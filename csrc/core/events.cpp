@@ -134,7 +134,8 @@ const char* counter_name(Counter c) {
                             "encoded_bytes",
                             "table_shootdowns",
                             "fault_replays",
-                            "fault_records_consumed"};
+                            "fault_records_consumed",
+                            "page_list_copies"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -236,6 +236,23 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
       to->fmt = 1;
       to->enc_bytes = from->enc_bytes;
     }
+  } else if (pages.runs() >= (uint32_t)std::max<int64_t>(2, config().copy_page_list_min_runs)) {
+    // Fragmented mask: one page-list kernel (LDS-staged) instead of one copy
+    // per run - the staged pack of uvm_va_block.c:4278-4326 / 3673-3860.
+    Sqe s;
+    s.op = SqeOp::PAGE_COPY;
+    s.dst = page_addr(to->arena, to->chunk, 0);
+    s.src = page_addr(from->arena, from->chunk, 0);
+    s.bytes = (uint64_t)pages.count() << kPageShift;
+    s.idx.reserve(pages.count());
+    pages.for_each_run([&](uint32_t p, uint32_t n) {
+      for (uint32_t k = 0; k < n; ++k) s.idx.push_back(p + k);
+    });
+    s.user_data = b->range->id;
+    s.file = __FILE__;
+    s.line = __LINE__;
+    ring->push(std::move(s));
+    Tools::get().inc(Counter::PageListCopies);
   } else {
     pages.for_each_run([&](uint32_t p, uint32_t n) {
       Sqe s;
@@ -560,6 +577,7 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
 // ------------------------------------------------------------------ eviction
 // Evict chunk `i` of arena `a` (EVICTING state). No block lock may be held.
 Status Runtime::evict_chunk(ChunkArena* a, uint32_t i) {
+  TraceRange tr(be_.get(), "ogkm:evict_chunk");
   if (inject_.evict_fail.load() > 0 && inject_.evict_fail.fetch_sub(1) > 0) {
     Tools::get().inc(Counter::InjectedErrors);
     return Status::INJECTED_ERROR;
@@ -653,8 +671,12 @@ Status Runtime::prefetch(Range* r, uint64_t off, uint64_t len, Loc dst, Tracker*
   if (!r || off + len > r->size || len == 0) return Status::INVALID_ARGUMENT;
   if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
   if (!arena_for(dst)) return Status::INVALID_ARGUMENT;
+  TraceRange tr(be_.get(), "ogkm:prefetch");
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   if (r->group && !r->group->migratable) return Status::BUSY;
+  if (cause == Cause::Prefetch || cause == Cause::ApiMigrate)
+    tools_event(ToolsEventType::Prefetch, cause, Loc{}, dst, dst.is_gpu() ? dst.id : kCpuProc, r->addr() + off, len,
+                r->id);
   if (dst.is_gpu()) {
     // GPU destinations are laid out as one contiguous extent so a later
     // acquire() finds the span in place (no relocation).
@@ -963,6 +985,7 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
 
 // ------------------------------------------------------------------ leases
 Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out) {
+  TraceRange tr(be_.get(), "ogkm:acquire");
   if (global_status() != Status::OK) return global_status();
   if (quiesced_.load()) return Status::BUSY;
   if (!r || len == 0 || off + len > r->size) return Status::INVALID_ARGUMENT;
@@ -1184,6 +1207,7 @@ Lease* Runtime::lease_by_id(uint64_t id) {
 // with thrashing hints, residency selection and prefetch expansion.
 Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
   if (faults.empty()) return Status::OK;
+  TraceRange tr(be_.get(), "ogkm:service_faults");
   if (global_status() != Status::OK) return global_status();
   Tools::get().inc(Counter::FaultBatches);
   for (auto& f : faults) {
@@ -1330,6 +1354,7 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
 
 // ------------------------------------------------------------------ CPU faults
 Status Runtime::cpu_fault(uint64_t addr, bool write) {
+  TraceRange tr(be_.get(), "ogkm:cpu_fault");
   Range* r = nullptr;
   {
     std::shared_lock<OrderedRWLock> vg(vs_.lock);
@@ -1435,8 +1460,10 @@ size_t Runtime::drain_fault_records(int dev, std::vector<DeviceFaultRecord>* out
 
 size_t Runtime::poll_device_faults(int dev) {
   if (!is_local(dev)) return 0;
+  TraceRange tr(be_.get(), "ogkm:device_fault_batch");
   DeviceFaultBuffer& fb = devs_[dev]->fault_buf;
   if (!fb.hdr) return 0;
+  refresh_device_tables();
   std::unique_lock<std::mutex> pg(poll_m_);  // the service thread and API callers drain one at a time
   std::vector<DeviceFaultRecord> recs;
   size_t n = drain_fault_records(dev, &recs, fb.entries);

@@ -215,6 +215,8 @@ Status Ring::run_batch(Batch& b) {
         if (st != Status::OK) break;
         if (s.op == SqeOp::MEMSET) {
           st = be_->memset32(dev_, s.dst, s.pattern, s.bytes, stream_);
+        } else if (s.op == SqeOp::PAGE_COPY) {
+          st = be_->page_copy(dev_, s.dst, s.src, s.idx.data(), (uint32_t)s.idx.size(), stream_);
         } else {
           PageListDesc d{s.op == SqeOp::GATHER ? s.src : s.dst, s.op == SqeOp::GATHER ? s.dst : s.src, s.idx.data(),
                          (uint32_t)s.idx.size(), s.page_bytes};
@@ -319,6 +321,10 @@ FenceRef Ring::submit_locked() {
           flush();
           if (st == Status::OK) st = be_->memset32(dev_, s.dst, s.pattern, s.bytes, stream_);
           break;
+        case SqeOp::PAGE_COPY:
+          flush();
+          if (st == Status::OK) st = be_->page_copy(dev_, s.dst, s.src, s.idx.data(), (uint32_t)s.idx.size(), stream_);
+          break;
         case SqeOp::WAIT_FENCE:
           flush();
           if (st == Status::OK && s.wait && !s.wait->done.load()) {
@@ -374,15 +380,43 @@ Status Ring::wait_seq(uint64_t seq) {
     if (++spins > 64) std::this_thread::yield();
     if (spins > (1ull << 34)) return Status::TIMEOUT;
   }
+  return check_errors();
+}
+
+Status Ring::check_errors() {
+  if (err_ != Status::OK) return err_;
+  Status st = Status::OK;
+  Runtime* rt = Runtime::get();
+  bool injected = false;
+  if (rt && rt->inject().async_copy_error.load() > 0 && rt->inject().async_copy_error.fetch_sub(1) > 0) {
+    Tools::get().inc(Counter::InjectedErrors);
+    st = Status::INJECTED_ERROR;
+    injected = true;
+  } else if (!dma_ && stream_) {
+    st = be_->stream_check(stream_);
+  }
+  if (st == Status::OK) return Status::OK;
+  Status expected = Status::OK;
+  if (err_.compare_exchange_strong(expected, st)) {
+    RT_ERR("ring %s/%d: work failed after submission: %s (%s)", ring_kind_str(kind_), dev_, status_str(st),
+           injected ? "injected" : be_->last_error().c_str());
+    tools_event(ToolsEventType::RingError, Cause::User, Loc::gpu(dev_), Loc::gpu(dev_), dev_, 0, 0, 0);
+    if (!injected) set_fatal(st, "ring work failed after submission");
+  }
   return err_;
 }
 
 size_t Ring::reap(Cqe* out, size_t max) {
   std::lock_guard<OrderedMutex> g(m_);
   uint64_t c = completed_seq();
+  // Completed entries are checked before they are retired: a failure after
+  // submission is attributed to the CQEs that complete with it.
+  Status post = (!inflight_.empty() && inflight_.front().first <= c) ? check_errors() : Status::OK;
   size_t n = 0;
   while (!inflight_.empty() && inflight_.front().first <= c && n < max) {
-    out[n++] = inflight_.front().second;
+    out[n] = inflight_.front().second;
+    if (post != Status::OK && out[n].status == 0) out[n].status = (int32_t)post;
+    ++n;
     inflight_.pop_front();
   }
   Tools::get().inc(Counter::RingCompletions, n);

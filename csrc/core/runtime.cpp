@@ -490,8 +490,37 @@ void Runtime::update_device_table(Block* b) {
     }
   }
   bool pending = b->unpublished > 0 || !b->tracker.query();
-  __atomic_store_n(&t->entries[2 * b->index], pending ? 0 : hbm, __ATOMIC_RELEASE);
+  uint64_t old = __atomic_load_n(&t->entries[2 * b->index], __ATOMIC_RELAXED);
+  uint64_t now = pending ? 0 : hbm;
+  // Copies still in flight: the entry is published once they land
+  // (refresh_device_tables, run by the fault-service poll and sync points).
+  if (pending && (hbm || rem)) table_pending_.emplace_back(b->range->id, b->index);
+  if ((old == 0) != (now == 0))
+    // The GPU's view of the block switches between one 2 MB mapping and
+    // per-page (remote / absent) access: the PageSizeChange event of uvm_tools.
+    tools_event(ToolsEventType::PageSizeChange, Cause::User, Loc{}, Loc::gpu(t->dev), t->dev,
+                b->range->addr() + b->block_offset(), now ? kBlockSize : kPageSize, b->range->id);
+  __atomic_store_n(&t->entries[2 * b->index], now, __ATOMIC_RELEASE);
   __atomic_store_n(&t->entries[2 * b->index + 1], pending ? 0 : rem, __ATOMIC_RELEASE);
+}
+
+void Runtime::refresh_device_tables() {
+  std::vector<std::pair<uint64_t, uint64_t>> todo;
+  {
+    std::lock_guard<std::mutex> g(dev_tables_m_);
+    if (table_pending_.empty()) return;
+    todo.swap(table_pending_);
+  }
+  std::sort(todo.begin(), todo.end());
+  todo.erase(std::unique(todo.begin(), todo.end()), todo.end());
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  for (auto& [rid, bi] : todo) {
+    Range* r = vs_.by_id_locked(rid);
+    if (!r || bi >= r->nblocks) continue;
+    Block* b = r->block(bi);
+    std::lock_guard<OrderedMutex> g(b->lock);
+    update_device_table(b);  // re-queues itself while still pending
+  }
 }
 
 Status Runtime::device_table(Range* r, DeviceResidencyTable** out) {
@@ -909,6 +938,7 @@ Status Runtime::sync_all() {
       Status s = f->wait();
       if (s != Status::OK && st == Status::OK) st = s;
     }
+  refresh_device_tables();
   return st;
 }
 
@@ -935,6 +965,7 @@ Status Runtime::start_fault_service(uint32_t poll_us) {
     fs_threads_.emplace_back([this, d, poll_us] {
       DeviceFaultBuffer& fb = devs_[d]->fault_buf;
       while (!fs_stop_.load(std::memory_order_acquire)) {
+        refresh_device_tables();
         // Top half: cheap check of the device-advanced PUT against GET.
         bool pending = fb.hdr && (__atomic_load_n(&fb.hdr->put, __ATOMIC_ACQUIRE) !=
                                       __atomic_load_n(&fb.hdr->get, __ATOMIC_RELAXED) ||

@@ -131,6 +131,19 @@ class Backend {
   virtual Status attn_decode(int dev, const AttnArgs& a, void* stream) = 0;
   virtual Status gather_pages(int dev, const PageListDesc& d, void* stream) = 0;
   virtual Status scatter_pages(int dev, const PageListDesc& d, void* stream) = 0;
+  // Asynchronous error state of a stream after its work completed (a kernel or
+  // copy that faulted): OK while fine or still running.
+  virtual Status stream_check(void* stream) { (void)stream; return Status::OK; }
+  // Profiler annotations (roctx ranges / marks on the HIP backend):
+  // rocprofv3 --marker-trace shows them on the CPU timeline.
+  virtual void range_push(const char* name) { (void)name; }
+  virtual void range_pop() {}
+  virtual void mark(const char* name) { (void)name; }
+  // Scattered 4 KiB pages of one block (npages <= 512): page idx[i] of src_base
+  // -> page idx[i] of dst_base (k_page_copy_lds; the index list travels in the
+  // kernel arguments).
+  virtual Status page_copy(int dev, uint64_t dst_base, uint64_t src_base, const uint32_t* idx, uint32_t npages,
+                           void* stream) = 0;
   virtual Status memset32(int dev, uint64_t dst, uint32_t pattern, size_t bytes, void* stream) = 0;
   // Write `value` to *addr (host-coherent) once all prior work on `stream` is done,
   // with system-scope release (the tracking-semaphore release of uvm_channel.c:1484-1580).

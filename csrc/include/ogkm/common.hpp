@@ -104,6 +104,16 @@ struct PageMask {
       p = next_set(e);
     }
   }
+  // Number of maximal runs of set pages (rising edges of the 512-bit mask).
+  uint32_t runs() const {
+    uint32_t r = 0;
+    uint64_t carry = 0;  // bit 63 of the previous word
+    for (int i = 0; i < 8; ++i) {
+      r += __builtin_popcountll(w[i] & ~((w[i] << 1) | carry));
+      carry = w[i] >> 63;
+    }
+    return r;
+  }
   static PageMask all() { PageMask m; m.fill(); return m; }
   static PageMask range(uint32_t first, uint32_t n) { PageMask m; m.set_range(first, n); return m; }
 };

@@ -62,6 +62,8 @@ namespace ogkm {
   X(copy_workgroups, 16, "workgroups per copy-kernel launch (CU budget; 16 saturate PCIe, more starve HBM-bound compute)") \
   X(copy_piece_kb, 64, "bytes per copy work item (KB)")                                              \
   X(copy_nt_loads, 1, "copy kernels: non-temporal source loads (0 = plain loads)")                      \
+  X(trace_ranges, 1, "emit roctx ranges around runtime operations (fault batches, migrations, evictions)") \
+  X(copy_page_list_min_runs, 4, "a block copy with at least this many page runs is one LDS-staged page-list kernel") \
   X(decode_workgroups, 256, "workgroups per fused copy+BF12-decode launch")                           \
   X(peer_copy, 1, "0=phys 1=virt peer addressing")                                                   \
   /* misc UVM knobs */                                                                               \

@@ -178,6 +178,7 @@ enum class Counter : int {
   TableShootdowns,  // device residency-table entries cleared before their chunk was released
   FaultReplays,     // replay tokens issued after serviced device-fault batches
   FaultRecordsConsumed,  // device fault-buffer records consumed from GET
+  PageListCopies,   // fragmented block copies issued as one page-list kernel
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -38,6 +38,13 @@ hipError_t launch_batch_copy(const KCopyDesc* d_descs, const uint64_t* d_piece_s
 hipError_t launch_gather_pages(uint64_t base, uint64_t contig, const uint32_t* d_idx, uint32_t npages,
                                uint32_t page_bytes, bool scatter, uint32_t workgroups, hipStream_t s);
 hipError_t launch_memset32(uint64_t dst, uint32_t pattern, uint64_t bytes, hipStream_t s);
+// Page-list copy of one 2 MB block's scattered 4 KiB pages, staged through LDS
+// with global_load_lds (16 pages = 64 KiB in flight per workgroup).
+struct KPageList {
+  uint16_t idx[512];
+};
+hipError_t launch_page_copy(uint64_t dst_base, uint64_t src_base, const KPageList& pl, uint32_t npages,
+                            uint32_t workgroups, hipStream_t s);
 hipError_t launch_signal(uint64_t* host_addr, uint64_t value, hipStream_t s);
 
 // Fused copy + BF12 decode of up to kInlineDescs encoded blocks (codec.hpp).

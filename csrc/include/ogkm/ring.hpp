@@ -51,7 +51,9 @@ enum class RingKind : int {
 const char* ring_kind_str(RingKind k);
 
 // DECODE_BF12: fused copy + decode of an encoded block (dst = raw bf16, bytes = 2 * values).
-enum class SqeOp : uint8_t { COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP, DECODE_BF12 };
+// PAGE_COPY: scattered pages of one block, page idx[i] of src -> page idx[i] of
+// dst (one LDS-staged kernel instead of one copy per run).
+enum class SqeOp : uint8_t { COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP, DECODE_BF12, PAGE_COPY };
 
 struct Sqe {
   SqeOp op = SqeOp::NOP;
@@ -89,6 +91,11 @@ class Ring {
   uint64_t pushed_seq() const { return next_seq_ - 1; }
   Status wait_seq(uint64_t seq);
   size_t reap(Cqe* out, size_t max);
+  // Post-completion error check (uvm_channel.c:2047-2112 channel error
+  // detection): a copy or kernel that failed AFTER submission - a faulting
+  // kernel, an ECC / link error - marks the ring failed; the CQEs retired
+  // since carry the status and fence waits return it.
+  Status check_errors();
   Status error() const { return err_; }
   void clear_error_for_test();
   void* stream() const { return stream_; }

@@ -105,6 +105,7 @@ struct Injection {
   std::atomic<uint64_t> peer_link_down{0};     // bit g: peer link of GPU g down
   std::atomic<int64_t> populate_error{0};      // next N populates fail
   std::atomic<int64_t> host_alloc_error{0};    // next N host chunk allocs fail
+  std::atomic<int64_t> async_copy_error{0};     // next N ring completions report a post-submission failure
 };
 
 struct ResidencyInfo {   // UVM_TEST_VA_RESIDENCY_INFO analog (uvm_test_ioctl.h:626-674)
@@ -182,6 +183,7 @@ class Runtime {
   // the old entry finishes before the chunk is overwritten (the TLB-shootdown
   // + membar step of unmapping, uvm_va_block.c unmap + tlb_invalidate).
   void register_table_stream(int dev, void* stream, bool on);
+  void refresh_device_tables();  // publish entries whose copies have landed since
 
   // ---- data movement helpers
   Status write(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev);
@@ -265,6 +267,7 @@ class Runtime {
   std::unordered_map<uint64_t, std::unique_ptr<DeviceResidencyTable>> dev_tables_;
   std::mutex dev_tables_m_;
   std::vector<void*> table_streams_[kMaxGpus];  // guarded by dev_tables_m_
+  std::vector<std::pair<uint64_t, uint64_t>> table_pending_;  // (range, block) entries awaiting copies
   std::mutex poll_m_;  // fault-buffer consumers drain one at a time
   std::unordered_map<uint64_t, std::pair<Ring*, uint64_t>> cxl_pending_;
   std::mutex cxl_m_;
@@ -274,6 +277,19 @@ class Runtime {
   std::mutex fs_m_;
   OrderedMutex pm_{LockOrder::GLOBAL_PM};
   std::vector<int> perf_subs_;  // perf-module subscriptions on the tools bus
+};
+
+// Scoped profiler range around a runtime operation (no-op on the fake backend).
+struct TraceRange {
+  Backend* be;
+  explicit TraceRange(Backend* b, const char* name) : be(config().trace_ranges ? b : nullptr) {
+    if (be) be->range_push(name);
+  }
+  ~TraceRange() {
+    if (be) be->range_pop();
+  }
+  TraceRange(const TraceRange&) = delete;
+  TraceRange& operator=(const TraceRange&) = delete;
 };
 
 // Per-operation migration context: rings used, blocks touched, chunks read by

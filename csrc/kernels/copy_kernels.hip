@@ -145,6 +145,42 @@ hipError_t launch_gather_pages(uint64_t base, uint64_t contig, const uint32_t* d
   return hipGetLastError();
 }
 
+// Scattered pages of one block: every workgroup stages up to kStagePages pages
+// (4 KiB = 256 lanes x 16 B each) global -> LDS with global_load_lds (no VGPR
+// round trip, all of them in flight at once - what hides the PCIe latency of a
+// host-resident source), then writes them out with non-temporal 16-B stores.
+// The LDS image is lane-linear per wave (each wave-instruction fills 1 KiB).
+constexpr uint32_t kStagePages = 16;  // 64 KiB of the 160 KiB LDS
+
+__global__ void __launch_bounds__(kThreads)
+    k_page_copy_lds(uint64_t dst_base, uint64_t src_base, KPageList pl, uint32_t npages) {
+  __shared__ u32x4 stage[kStagePages * kThreads];
+  const uint32_t t = threadIdx.x, wave = t >> 6;
+  for (uint32_t first = blockIdx.x * kStagePages; first < npages; first += gridDim.x * kStagePages) {
+    const uint32_t n = npages - first < kStagePages ? npages - first : kStagePages;
+    for (uint32_t j = 0; j < n; ++j) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(src_base + ((uint64_t)pl.idx[first + j] << 12)) + t;
+      __builtin_amdgcn_global_load_lds(src, &stage[j * kThreads + wave * 64], 16, 0, 0);
+    }
+    __syncthreads();  // vmcnt(0): every staged page has landed in LDS
+    for (uint32_t j = 0; j < n; ++j) {
+      u32x4* dst = reinterpret_cast<u32x4*>(dst_base + ((uint64_t)pl.idx[first + j] << 12)) + t;
+      __builtin_nontemporal_store(stage[j * kThreads + t], dst);
+    }
+    __syncthreads();  // the stage is rewritten by the next round
+  }
+}
+
+hipError_t launch_page_copy(uint64_t dst_base, uint64_t src_base, const KPageList& pl, uint32_t npages,
+                            uint32_t workgroups, hipStream_t s) {
+  if (npages == 0) return hipSuccess;
+  if (npages > 512 || ((dst_base | src_base) & 4095)) return hipErrorInvalidValue;
+  uint32_t grid = (npages + kStagePages - 1) / kStagePages;
+  if (grid > workgroups) grid = workgroups;
+  hipLaunchKernelGGL(k_page_copy_lds, dim3(grid), dim3(kThreads), 0, s, dst_base, src_base, pl, npages);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(kThreads) k_memset32(uint32_t* __restrict__ dst, uint32_t pattern, uint64_t n4) {
   u32x4 v = {pattern, pattern, pattern, pattern};
   uint64_t n16 = n4 >> 2;

@@ -812,6 +812,32 @@ PYBIND11_MODULE(_ogkm, m) {
     return lockcheck::violations() - before;
   });
 
+  // ---- tools: process memory access (UVM_TOOLS_READ/WRITE_PROCESS_MEMORY,
+  // uvm_tools.c:2591,2601): read / write managed memory by virtual address
+  // wherever its valid copy lives (no migration of the data for the tool).
+  m.def("tools_read_process_memory", [](uint64_t addr, uint64_t nbytes) {
+    Runtime* r = rt();
+    Range* rg = r->find_range(addr);
+    if (!rg || addr + nbytes > rg->addr() + rg->size) throw StatusError("read_process_memory: not managed memory");
+    std::string buf(nbytes, '\0');
+    {
+      py::gil_scoped_release nogil;
+      check(r->read(rg, addr - rg->addr(), buf.data(), nbytes, -1), "read_process_memory");
+    }
+    return py::bytes(buf);
+  });
+  m.def("tools_write_process_memory", [](uint64_t addr, py::bytes data) {
+    Runtime* r = rt();
+    std::string buf = data;
+    Range* rg = r->find_range(addr);
+    if (!rg || addr + buf.size() > rg->addr() + rg->size) throw StatusError("write_process_memory: not managed memory");
+    py::gil_scoped_release nogil;
+    check(r->write(rg, addr - rg->addr(), buf.data(), buf.size(), -1), "write_process_memory");
+  });
+  m.def("range_push", [](const std::string& name) { rt()->be()->range_push(name.c_str()); });
+  m.def("range_pop", [] { rt()->be()->range_pop(); });
+  m.def("mark", [](const std::string& name) { rt()->be()->mark(name.c_str()); });
+
   // ---- injection
   m.def("inject", [](const std::string& kind, int64_t v) {
     Injection& in = rt()->inject();
@@ -821,6 +847,7 @@ PYBIND11_MODULE(_ogkm, m) {
     else if (kind == "peer_link_down") in.peer_link_down.store((uint64_t)v);
     else if (kind == "populate_error") in.populate_error.store(v);
     else if (kind == "host_alloc_error") in.host_alloc_error.store(v);
+    else if (kind == "async_copy_error") in.async_copy_error.store(v);
     else throw StatusError("unknown injection " + kind);
   });
 

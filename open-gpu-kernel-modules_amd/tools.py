@@ -94,3 +94,32 @@ def prometheus_text(prefix: str = "ogkm") -> str:
             lines.append(f'{prefix}_arena_{key}{{arena="{a["name"]}"}} {a[key]}')
     lines.append(f"{prefix}_lock_violations {s['lock_violations']}")
     return "\n".join(lines) + "\n"
+
+
+def read_process_memory(addr: int, nbytes: int) -> bytes:
+    """Read managed memory at a virtual address wherever its valid copy lives
+    (UVM_TOOLS_READ_PROCESS_MEMORY, uvm_tools.c:2591)."""
+    return lib.tools_read_process_memory(addr, nbytes)
+
+
+def write_process_memory(addr: int, data: bytes) -> None:
+    """Write managed memory at a virtual address (UVM_TOOLS_WRITE_PROCESS_MEMORY,
+    uvm_tools.c:2601); other copies of the written pages are invalidated."""
+    lib.tools_write_process_memory(addr, bytes(data))
+
+
+class trace_range:
+    """``with tools.trace_range("step"):`` - a roctx range around Python code
+    (shown by ``rocprofv3 --marker-trace``); the runtime wraps its own fault
+    batches, migrations, evictions and leases the same way (config trace_ranges)."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        lib.range_push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        lib.range_pop()
+        return False

@@ -108,3 +108,32 @@ def test_config_env_override(tmp_path):
     env = dict(os.environ, RT_PERF_PREFETCH_THRESHOLD="77")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert out.stdout.strip().endswith("77"), out.stderr
+
+
+def test_tools_process_memory_read_write(fake_rt):
+    """Read / write managed memory by address wherever it lives (host, HBM)."""
+    b = rt.malloc_managed(4 * MB, "pm")
+    ref = torch.arange(MB, dtype=torch.int32)
+    b.write(ref)
+    b.migrate("gpu:0", 2 * MB, 2 * MB)                 # second half lives in HBM
+    got = tools.read_process_memory(b.addr + 2 * MB - 8, 16)
+    assert torch.equal(torch.frombuffer(bytearray(got), dtype=torch.int32), ref[MB // 2 - 2:MB // 2 + 2])
+    tools.write_process_memory(b.addr + 3 * MB, torch.tensor([7, 8], dtype=torch.int32).numpy().tobytes())
+    back = b.read().view(torch.int32)
+    assert back[(3 * MB) // 4].item() == 7 and back[(3 * MB) // 4 + 1].item() == 8
+    b.free()
+
+
+def test_tools_prefetch_and_page_size_change_events(fake_rt):
+    q = tools.EventQueue(events=["Prefetch", "PageSizeChange"])
+    b = rt.malloc_managed(4 * MB, "ev")
+    b.write(torch.ones(4 * MB, dtype=torch.uint8))
+    lib.device_table(b.id)                               # the GPU view of the range
+    b.prefetch("gpu:0").wait()
+    lib.poll_device_faults(0)
+    b.migrate("host:0")
+    types = [e["type"] for e in q.read_dicts()]
+    q.close()
+    assert "Prefetch" in types
+    assert types.count("PageSizeChange") >= 2            # 2 MB mapping on, then off
+    b.free()

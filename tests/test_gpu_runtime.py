@@ -349,3 +349,22 @@ def test_ans_unpack_reports_corrupt_chunk(gpu_rt):
     assert torch.equal(got[:cv], ref.view(torch.int16)[:cv])
     assert torch.equal(got[2 * cv:], ref.view(torch.int16)[2 * cv:])
     assert (got[cv:2 * cv] == 0).all()
+
+
+def test_fragmented_block_copy_page_list_kernel_gpu(gpu_rt):
+    """Scattered pages of a host block -> HBM through one k_page_copy_lds
+    launch (global_load_lds staging), bit-exact."""
+    lib.configure("perf_prefetch_enable", 0)
+    b = rt.malloc_managed(4 * MB, "frag")
+    ref = _rand_bytes(4 * MB, seed=3)
+    b.write(ref)
+    pages = [p for p in range(1024) if p % 5 in (0, 2)]
+    lib.service_faults([(b.id, p * 4096, 4096, 0, rt.READ) for p in pages])
+    assert lib.stats()["page_list_copies"] >= 2          # one per block
+    l = b.acquire(0, rt.READ)
+    l.wait()
+    t = l.tensor((4 * MB,), torch.uint8)
+    torch.cuda.synchronize()
+    assert torch.equal(t.cpu(), ref)
+    l.release()
+    b.free()

@@ -296,3 +296,24 @@ def test_thrashing_throttle_then_pin_via_perf_bus(fake_rt):
     assert ev.index("ThrottlingStart") < ev.index("MapRemote") < ev.index("ThrottlingEnd")
     assert lib.stats()["pin_events"] >= 1 and b.residency(0)["pinned"]
     b.free()
+
+
+def test_fragmented_block_copy_is_one_page_list_kernel(fake_rt):
+    """A block whose faulted pages form many runs moves with one page-list
+    copy (the LDS-staged k_page_copy_lds on a GPU) instead of one copy per run,
+    and the data is exact."""
+    lib.configure("perf_prefetch_enable", 0)
+    b = rt.malloc_managed(2 * MB, "frag")
+    ref = torch.randint(0, 256, (2 * MB,), dtype=torch.uint8)
+    b.write(ref)
+    pages = list(range(0, 512, 3))            # 171 single-page runs
+    lib.service_faults([(b.id, p * 4096, 4096, 0, rt.READ) for p in pages])
+    s = lib.stats()
+    assert s["page_list_copies"] == 1
+    gpu = [r for r in b.residency(0)["resident_on"] if r["tier"] == "gpu"]
+    assert gpu and gpu[0]["pages"] == len(pages)
+    l = b.acquire(0, rt.READ)                  # the rest comes in; every byte matches
+    l.wait()
+    assert torch.equal(l.tensor((2 * MB,), torch.uint8).clone(), ref)
+    l.release()
+    b.free()

@@ -65,6 +65,30 @@ def test_copy_drop_injection_reports_error(fake_rt):
     assert int(b.read().min()) == 1
 
 
+def test_failure_after_submission_is_caught_at_completion(fake_rt):
+    """A copy that fails after it was submitted (ECC / link error, faulting
+    kernel) is caught when its completion is checked: the fence wait returns the
+    error, the CQE retired with it carries the status, the ring records it
+    (uvm_channel.c:2047-2112 channel error detection)."""
+    from ogkm import tools
+
+    q = tools.EventQueue(events=["RingError"])
+    b = rt.malloc_managed(2 * MB, "late")
+    b.write(torch.ones(2 * MB, dtype=torch.uint8))
+    lib.ring_reap(0, CPU_TO_GPU)
+    lib.inject("async_copy_error", 1)
+    with pytest.raises(rt.RuntimeStatusError, match="INJECTED_ERROR"):
+        b.migrate("gpu:0")
+    cqes = lib.ring_reap(0, CPU_TO_GPU)
+    assert any(st != 0 for _, _, st in cqes)
+    assert lib.ring_error(0, CPU_TO_GPU)[0] == "INJECTED_ERROR"
+    assert any(e["type"] == "RingError" for e in q.read_dicts())
+    q.close()
+    lib.ring_clear_error(0, CPU_TO_GPU)
+    b.migrate("gpu:0")
+    assert int(b.read().min()) == 1
+
+
 def test_alloc_fail_after_and_recovery(fake_rt):
     lib.init_device(0, 32 * MB)
     lib.inject("alloc_fail_after", 0)

@@ -99,7 +99,8 @@ def build(debug: bool = False, jobs: int | None = None, verbose: bool = False) -
         return out
     link = [str(ROCM / "bin" / "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out)]
     link += [str(o) for o in sorted(objs)]
-    link += [f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64", "-lhsa-runtime64", "-lnuma",
+    link += [f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64", "-lhsa-runtime64",
+             "-lrocprofiler-sdk-roctx", "-lnuma",
              "-lpthread"]
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:
