@@ -99,9 +99,16 @@ std::atomic<bool> g_service_stop{false};
 // destroy a joinable std::thread (std::terminate) in static destructors.
 std::thread* g_service = nullptr;
 
+// Bottom half: every posted fault is serviced in ONE batch (one
+// service_faults call: coalescing, one copy submission, one wait), then the
+// faulting threads are woken - the batch service of
+// uvm_gpu_replayable_faults.c:2906 applied to CPU faults.
 void service_loop() {
   g_service_tid.store((pid_t)syscall(SYS_gettid));
   int seen = 0;
+  std::vector<FaultSlot*> batch;
+  std::vector<std::pair<uint64_t, bool>> req;
+  std::vector<Status> res;
   while (!g_service_stop.load(std::memory_order_acquire)) {
     int now = g_posted.load(std::memory_order_acquire);
     if (now == seen) {
@@ -109,14 +116,24 @@ void service_loop() {
       continue;
     }
     seen = now;
-    for (auto& s : g_slots) {
-      if (s.state.load(std::memory_order_acquire) != SLOT_POSTED) continue;
-      Runtime* rt = Runtime::get();
-      Status st = rt ? rt->cpu_fault(s.addr, s.write != 0) : Status::NOT_FOUND;
+    batch.clear();
+    req.clear();
+    for (auto& s : g_slots)
+      if (s.state.load(std::memory_order_acquire) == SLOT_POSTED) {
+        batch.push_back(&s);
+        req.emplace_back(s.addr, s.write != 0);
+      }
+    if (batch.empty()) continue;
+    Runtime* rt = Runtime::get();
+    res.assign(batch.size(), Status::NOT_FOUND);
+    if (rt) rt->cpu_fault_batch(req, &res);
+    for (size_t k = 0; k < batch.size(); ++k) {
+      FaultSlot& s = *batch[k];
+      Status st = res[k];
       // BUSY: a GPU lease pins the only copy (the GPU may be writing it); the
       // CPU access waits for the release, like a CPU fault on a block whose GPU
       // mapping cannot be revoked yet (uvm_va_space.c:2540-2590 retries).
-      for (int tries = 0; st == Status::BUSY && tries < 20000; ++tries) {
+      for (int tries = 0; rt && st == Status::BUSY && tries < 20000; ++tries) {
         std::this_thread::sleep_for(std::chrono::microseconds(tries < 100 ? 20 : 500));
         st = rt->cpu_fault(s.addr, s.write != 0);
       }

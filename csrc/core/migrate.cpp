@@ -1353,6 +1353,52 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
 }
 
 // ------------------------------------------------------------------ CPU faults
+void Runtime::cpu_fault_batch(const std::vector<std::pair<uint64_t, bool>>& faults, std::vector<Status>* out) {
+  out->assign(faults.size(), Status::NOT_FOUND);
+  if (faults.size() == 1) {
+    (*out)[0] = cpu_fault(faults[0].first, faults[0].second);
+    return;
+  }
+  TraceRange tr(be_.get(), "ogkm:cpu_fault_batch");
+  std::vector<FaultEntry> fe;
+  std::vector<Range*> ranges(faults.size(), nullptr);
+  {
+    std::shared_lock<OrderedRWLock> vg(vs_.lock);
+    for (size_t i = 0; i < faults.size(); ++i) {
+      Range* r = vs_.find_locked(faults[i].first);
+      if (!r || r->type != RangeType::MANAGED) continue;
+      uint64_t off = faults[i].first - r->addr();
+      if (off >= r->cpu_view_bytes) continue;
+      if (off >= align_up(r->size, kPageSize)) {
+        (*out)[i] = Status::INVALID_ARGUMENT;
+        continue;
+      }
+      ranges[i] = r;
+      FaultEntry f;
+      f.range_id = r->id;
+      f.offset = align_down(off, kPageSize);
+      f.bytes = kPageSize;
+      f.proc = kCpuProc;
+      f.access = faults[i].second ? Access::WRITE : Access::READ;
+      f.ts_ns = now_ns();
+      fe.push_back(f);
+    }
+  }
+  Tools::get().inc(Counter::CpuPageFaultCount, fe.size());
+  Tracker t;
+  Status st = fe.empty() ? Status::OK : service_faults(fe, &t);
+  t.wait();
+  for (size_t i = 0; i < faults.size(); ++i) {
+    if (!ranges[i]) continue;
+    if (st != Status::OK) {
+      (*out)[i] = cpu_fault(faults[i].first, faults[i].second);  // per-fault path (retries, BUSY)
+      continue;
+    }
+    // Map (and, for writes, collapse duplicates) exactly as the single path does.
+    (*out)[i] = cpu_fault_finish(ranges[i], faults[i].first, faults[i].second);
+  }
+}
+
 Status Runtime::cpu_fault(uint64_t addr, bool write) {
   TraceRange tr(be_.get(), "ogkm:cpu_fault");
   Range* r = nullptr;
@@ -1375,6 +1421,14 @@ Status Runtime::cpu_fault(uint64_t addr, bool write) {
   Tracker t;
   Status st = service_faults(f, &t);
   t.wait();
+  Status ms = cpu_fault_finish(r, addr, write);
+  return st != Status::OK ? st : ms;
+}
+
+// After servicing: wait for every copy into the block, collapse duplicates of a
+// written page, map the CPU view (block lock held only here).
+Status Runtime::cpu_fault_finish(Range* r, uint64_t addr, bool write) {
+  uint64_t off = addr - r->addr();
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   Block* b = r->block(off >> kBlockShift);
   // Concurrent faults (e.g. a multi-threaded memcpy over the CPU view) may still
@@ -1408,7 +1462,7 @@ Status Runtime::cpu_fault(uint64_t addr, bool write) {
   cpu_map_block(b);
   update_device_table(b);
   if (r->dev_va) stable_map_block(b);
-  return st;
+  return Status::OK;
 }
 
 // ------------------------------------------------------------------ device faults

@@ -172,6 +172,9 @@ class Runtime {
   Status release(Lease* l, void* stream);  // consumer's last use recorded on `stream`
   Lease* lease_by_id(uint64_t id);
   Status cpu_fault(uint64_t addr, bool write);        // SIGSEGV path
+  // Several CPU faults (addr, write) serviced as one batch; out[i] per fault.
+  void cpu_fault_batch(const std::vector<std::pair<uint64_t, bool>>& faults, std::vector<Status>* out);
+  Status cpu_fault_finish(Range* r, uint64_t addr, bool write);
   size_t poll_device_faults(int dev);                  // service device-recorded faults
   // Consume up to `max` published records from GET (no servicing).
   size_t drain_fault_records(int dev, std::vector<DeviceFaultRecord>* out, size_t max);
