@@ -4,6 +4,7 @@
 // which executes CE memcopy/memset methods on CPU addresses.
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -348,6 +349,25 @@ class FakeBackend : public Backend {
     *fd = fcntl(a->fd, F_DUPFD_CLOEXEC, 0);
     return *fd < 0 ? Status::IO_ERROR : Status::OK;
   }
+  Status import_dmabuf(int, int fd, void** ptr, size_t* bytes) override {
+    struct stat stt;
+    if (fstat(fd, &stt) != 0 || stt.st_size <= 0) return Status::INVALID_ARGUMENT;
+    void* p = mmap(nullptr, (size_t)stt.st_size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (p == MAP_FAILED) return Status::IO_ERROR;
+    std::lock_guard<std::mutex> g(m_);
+    imports_[p] = (size_t)stt.st_size;
+    *ptr = p;
+    *bytes = (size_t)stt.st_size;
+    return Status::OK;
+  }
+  Status unimport_dmabuf(void* ptr) override {
+    std::lock_guard<std::mutex> g(m_);
+    auto it = imports_.find(ptr);
+    if (it == imports_.end()) return Status::INVALID_ARGUMENT;
+    munmap(ptr, it->second);
+    imports_.erase(it);
+    return Status::OK;
+  }
   // Handle = "fake:<pid>:<fd>:<offset>:<alloc bytes>"; another process opens the
   // allocation's memfd through /proc/<pid>/fd (hipIpcGetMemHandle analog).
   Status ipc_handle(void* p, std::string* h) override {
@@ -408,6 +428,7 @@ class FakeBackend : public Backend {
   std::map<void*, size_t> coherent_;
   std::map<uint64_t, FakeAlloc> allocs_;                        // base -> memfd
   std::map<uint64_t, std::pair<uint64_t, size_t>> opened_;      // ipc ptr -> (map base, bytes)
+  std::map<void*, size_t> imports_;                             // imported dma-buf mappings
 };
 
 }  // namespace

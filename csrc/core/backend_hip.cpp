@@ -479,6 +479,27 @@ class HipBackend : public Backend {
     }
     return Status::OK;
   }
+  Status import_dmabuf(int dev, int fd, void** ptr, size_t* bytes) override {
+    dma_init();
+    if (dev < 0 || dev >= (int)dma_.size() || !dma_[dev].ok) {
+      last_err_ = "import_dmabuf: no HSA agent for the device";
+      return Status::NOT_SUPPORTED;
+    }
+    hsa_agent_t ag = dma_[dev].gpu;
+    size_t sz = 0;
+    void* p = nullptr;
+    hsa_status_t s = hsa_amd_interop_map_buffer(1, &ag, (hsa_handle_t)fd, 0, &sz, &p, nullptr, nullptr);
+    if (s != HSA_STATUS_SUCCESS) {
+      last_err_ = "hsa_amd_interop_map_buffer failed";
+      return Status::IO_ERROR;
+    }
+    *ptr = p;
+    *bytes = sz;
+    return Status::OK;
+  }
+  Status unimport_dmabuf(void* ptr) override {
+    return hsa_amd_interop_unmap_buffer(ptr) == HSA_STATUS_SUCCESS ? Status::OK : Status::IO_ERROR;
+  }
   // Handle = hipIpcMemHandle_t of the containing allocation + 8-byte offset of
   // `p` inside it (arena chunks live inside one slab allocation).
   Status ipc_handle(void* p, std::string* h) override {

@@ -668,6 +668,7 @@ Status Runtime::evict_chunk(ChunkArena* a, uint32_t i) {
 // ------------------------------------------------------------------ prefetch / migrate
 Status Runtime::prefetch(Range* r, uint64_t off, uint64_t len, Loc dst, Tracker* out, Cause cause) {
   if (global_status() != Status::OK) return global_status();
+  if (quiesced_.load()) return Status::BUSY;  // checkpoint in progress: residency is frozen
   if (!r || off + len > r->size || len == 0) return Status::INVALID_ARGUMENT;
   if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
   if (!arena_for(dst)) return Status::INVALID_ARGUMENT;
@@ -1139,6 +1140,21 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
         L->dptr = ra->chunk_addr((uint32_t)first) + (off - (b0 << kBlockShift));
         for (Block* b : L->blocks) L->ready.merge(published_tracker(b));
         Tools::get().inc(Counter::MapRemote, n);
+        // Software access counters on real traffic: a remote lease is the GPU
+        // reading the block over the link; hot blocks are promoted (their next
+        // decision migrates them to the GPU).
+        const int64_t thr = std::max<int64_t>(1, config().perf_access_counter_threshold);
+        for (Block* b : L->blocks) {
+          std::lock_guard<OrderedMutex> g(b->lock);
+          Tools::get().inc(Counter::AccessCounterNotifications);
+          tools_event(ToolsEventType::AccessCounter, Cause::AccessCounters, Loc{}, Loc::gpu(proc), proc,
+                      r->addr() + b->block_offset(), kBlockSize, r->id);
+          uint32_t& cnt = b->counters.remote_hits[proc];
+          if (++cnt >= (uint64_t)thr) {
+            cnt = 0;
+            if (config().perf_access_counter_migration_enable) b->counters.promote[proc] = true;
+          }
+        }
       } else {
         for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
         for (Block* b : L->blocks) {

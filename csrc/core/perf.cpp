@@ -92,6 +92,14 @@ ResidencyDecision select_residency(Runtime* rt, Block* b, int proc, Access acces
     return d;
   }
   int pbit = proc == kCpuProc ? kCpuProc : proc;
+  bool& hot = b->counters.promote[proc == kCpuProc ? kMaxGpus : proc];
+  if (hot && proc != kCpuProc) {
+    // Access counters found the remote mapping hot: migrate it here.
+    hot = false;
+    Tools::get().inc(Counter::AccessCounterMigrations);
+    d.dst = me;
+    return d;
+  }
   if (((pol.accessed_by >> pbit) & 1) && accessible(rt, closest, proc)) {
     d.dst = closest;
     d.map_remote = !(closest == me);

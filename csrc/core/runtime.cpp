@@ -672,6 +672,7 @@ Status Runtime::write_compressed(Range* r, uint64_t off, const void* src, uint64
 
 Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, int src_dev) {
   if (!r || off + bytes > r->size || (src_dev >= 0 && !is_local(src_dev))) return Status::INVALID_ARGUMENT;
+  if (quiesced_.load()) return Status::BUSY;  // checkpoint in progress
   if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
   if (bytes == 0) return Status::OK;
   if (r->flags & RANGE_COMPRESS_BF16) return write_compressed(r, off, src, bytes, src_dev);
@@ -1076,7 +1077,13 @@ template <class T> bool rd(std::istream& i, T* v) { return (bool)i.read((char*)v
 // per-location page masks, policy, and thrash pin state; optionally the data.
 Status Runtime::checkpoint_save(const std::string& path, bool with_data) {
   bool was_quiesced = quiesced_.load();
-  if (!was_quiesced) quiesce();
+  if (!was_quiesced) {
+    Status qs = quiesce();
+    if (qs != Status::OK) {  // in-flight work failed: the saved map would not match memory
+      resume();
+      return qs;
+    }
+  }
   std::ofstream o(path, std::ios::binary);
   if (!o) {
     if (!was_quiesced) resume();

@@ -158,6 +158,13 @@ class Backend {
 
   // ---- export (dma-buf for NICs / importers; IPC for peer processes)
   virtual Status export_dmabuf(void* p, size_t bytes, int* fd, uint64_t* offset) = 0;
+  // Importer side of a dma-buf (a third-party exporter, or our own export in
+  // another process): map the fd into device `dev`'s address space.
+  virtual Status import_dmabuf(int dev, int fd, void** ptr, size_t* bytes) {
+    (void)dev; (void)fd; (void)ptr; (void)bytes;
+    return Status::NOT_SUPPORTED;
+  }
+  virtual Status unimport_dmabuf(void* ptr) { (void)ptr; return Status::NOT_SUPPORTED; }
   virtual Status ipc_handle(void* p, std::string* handle) = 0;
   virtual Status ipc_open(const std::string& handle, void** p) = 0;
   virtual void ipc_close(void* p) = 0;

@@ -62,6 +62,9 @@ struct ThrashState {
 // per accessing processor to this 2 MB region.
 struct AccessCounterState {
   uint32_t remote_hits[kMaxGpus + 1] = {0};
+  // Hot for this processor: its next residency decision migrates the block to
+  // it instead of mapping remotely (uvm_gpu_access_counters.c:1617,1704).
+  bool promote[kMaxGpus + 1] = {false};
 };
 
 struct Residency {

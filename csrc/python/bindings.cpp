@@ -957,6 +957,13 @@ PYBIND11_MODULE(_ogkm, m) {
     check(rt()->be()->export_dmabuf((void*)ptr, size, &fd, &off), "export_dmabuf");
     return std::make_pair(fd, off);
   });
+  m.def("import_dmabuf", [](int dev, int fd) {
+    void* p = nullptr;
+    size_t n = 0;
+    check(rt()->be()->import_dmabuf(dev, fd, &p, &n), "import_dmabuf");
+    return std::make_pair((uint64_t)p, (uint64_t)n);
+  });
+  m.def("unimport_dmabuf", [](uint64_t ptr) { check(rt()->be()->unimport_dmabuf((void*)ptr), "unimport_dmabuf"); });
   m.def("ipc_handle", [](uint64_t ptr) {
     std::string h;
     check(rt()->be()->ipc_handle((void*)ptr, &h), "ipc_handle");

@@ -240,3 +240,33 @@ def default_client() -> PeerMemClient:
     if _default is None:
         _default = PeerMemClient()
     return _default
+
+
+class DmabufImport:
+    """Importer side of a dma-buf fd (from ``export_dmabuf`` here or in another
+    process, or a third-party exporter): the buffer mapped into a GPU's address
+    space (``hsa_amd_interop_map_buffer``). ``tensor()`` views it; ``close()``
+    unmaps. The consumer half of the peer-memory contract (nvidia-peermem's
+    importer role, kernel-open/nvidia-peermem/nvidia-peermem.c)."""
+
+    def __init__(self, fd: int, device: int = 0):
+        self.fd = fd
+        self.device = device
+        self.ptr, self.nbytes = lib.import_dmabuf(device, fd)
+
+    def tensor(self, shape, dtype, offset: int = 0):
+        from .rt import _tensor_from_ptr
+        dev = "cpu" if lib.backend_name() == "fake" else "cuda"
+        return _tensor_from_ptr(self.ptr + offset, shape, dtype, dev, self.device)
+
+    def close(self) -> None:
+        if self.ptr:
+            lib.unimport_dmabuf(self.ptr)
+            self.ptr = 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False

@@ -125,3 +125,26 @@ def test_replay_token_and_table_after_service(fake_rt):
     assert hbm != 0
     assert lib.stats()["fault_replays"] >= 1
     b.free()
+
+
+def test_access_counters_on_remote_leases_promote_hot_block(fake_rt):
+    """Remote (zero-copy) leases are real GPU traffic to host memory: they feed
+    the software access counters, and a block that crosses the threshold is
+    migrated to the GPU on its next use instead of being mapped remotely."""
+    lib.configure("perf_access_counter_threshold", 4)
+    b = rt.malloc_managed(4 * MB, "remote-hot")
+    b.set_preferred_location("host:0")
+    b.set_accessed_by(0)
+    b.write(torch.ones(4 * MB, dtype=torch.uint8))
+    for _ in range(4):
+        l = b.acquire(0, rt.READ)
+        assert l.remote
+        l.release()
+    s = lib.stats()
+    assert s["access_counter_notifications"] == 8            # 4 leases x 2 blocks
+    l = b.acquire(0, rt.READ)
+    assert not l.remote                                      # promoted: migrated to HBM
+    l.release()
+    assert lib.stats()["access_counter_migrations"] >= 2
+    assert all(any(r["tier"] == "gpu" for r in b.residency(o)["resident_on"]) for o in (0, 2 * MB))
+    b.free()

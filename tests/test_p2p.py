@@ -158,3 +158,52 @@ def test_collective_timeout_sets_sticky_fatal():
     out = json.loads(line[0][len("COMMFAULT "):])
     assert out["raised"] and out["status"] == "FATAL" and "all_reduce_" in out["reason"]
     assert out["malloc_after"] != "ok" and "FATAL" in out["malloc_after"]
+
+
+_IMPORTER = textwrap.dedent("""
+    import sys, torch
+    sys.path.insert(0, sys.argv[4])
+    import ogkm
+    from ogkm import rt, p2p
+    backend = sys.argv[3]
+    if backend == "fake":
+        rt.init("fake", fake_devices=1, fake_hbm_mb=64)
+    else:
+        rt.init("hip", hbm_budget={0: 1 << 30})
+    fd, off = int(sys.argv[1]), int(sys.argv[2])
+    with p2p.DmabufImport(fd, 0) as imp:
+        t = imp.tensor((1 << 18,), torch.int32, offset=off)
+        ok = bool((t[:1000] == torch.arange(1000, dtype=torch.int32, device=t.device)).all())
+        t[5] = -77                                   # write through the importer's mapping
+        if backend != "fake":
+            torch.cuda.synchronize()
+    print("IMPORT_OK" if ok else "IMPORT_BAD", flush=True)
+""")
+
+
+def _dmabuf_round_trip(backend):
+    b = rt.alloc_device_p2p(4 * MB, 0, "exp")
+    info = lib.range_info(b.id)
+    dev = "cpu" if backend == "fake" else "cuda"
+    src = rt._tensor_from_ptr(info["ext_ptr"], (MB,), torch.int32, dev, 0)
+    src.copy_(torch.arange(MB, dtype=torch.int32, device=dev))
+    if backend != "fake":
+        torch.cuda.synchronize()
+    fd, off = lib.export_dmabuf(info["ext_ptr"], 4 * MB)
+    r = subprocess.run([sys.executable, "-c", _IMPORTER, str(fd), str(off), backend, ROOT], pass_fds=(fd,),
+                       capture_output=True, text=True, timeout=240)
+    os.close(fd)
+    assert r.returncode == 0 and "IMPORT_OK" in r.stdout, r.stdout + r.stderr[-2000:]
+    assert int(src[5]) == -77                      # the importer's write is visible to the exporter
+    b.free()
+
+
+def test_dmabuf_import_cross_process(fake_rt):
+    """Exporter (this process) -> dma-buf fd -> importer (another process) maps
+    it, reads the exporter's data and writes back through its mapping."""
+    _dmabuf_round_trip("fake")
+
+
+@pytest.mark.gpu
+def test_dmabuf_import_cross_process_gpu(gpu_rt):
+    _dmabuf_round_trip("hip")

@@ -82,6 +82,7 @@ def main():
             seen.append((key, ptr, v.sum(dtype=torch.int64)))
         return orig_unstage(key, ptr)
     m._unstage = unstage
+    times = []
     for i in range(a.steps):
         s0 = lib.stats()
         torch.cuda.synchronize()
@@ -108,6 +109,7 @@ def main():
         d = {k: s1[k] - s0[k] for k in KEYS if k in s1}
         gb = {k: round(v / 1e9, 2) if "bytes" in k else v for k, v in d.items()}
         print(f"step {i}: {dt * 1e3:.1f} ms {gb}", flush=True)
+        times.append(dt)
         if a.verify:
             bad = [(k, p, int(t)) for k, p, t in seen if int(t) != ref_sum[k]]
             print(f"  verify: {len(seen)} unpacks, {len(bad)} saw wrong packed bytes", flush=True)
@@ -126,6 +128,16 @@ def main():
             where += [unstaged.get(err["stream"], "?")]
             print(f"  CORRUPT packed chunks: {err['count']} first stream {err['stream']:#x} chunk {err['chunk']} "
                   f"freq sum {err['detail']} {where}", flush=True)
+
+    # Regression guard for the one-time ~47 s stall of round 1 (reuse fences
+    # consumed by the first writer, profiles/r2_corrupt_chunk_hunt.md): no early
+    # step may take more than 3x the steady (last) step.
+    if len(times) >= 3:
+        steady = times[-1]
+        worst = max(times[:-1])
+        print(f"transient check: worst early step {worst * 1e3:.1f} ms, steady {steady * 1e3:.1f} ms", flush=True)
+        if worst > 3 * steady:
+            raise SystemExit(f"transient stall: an early step took {worst / steady:.1f}x the steady step")
 
 
 if __name__ == "__main__":
