@@ -245,8 +245,10 @@ def default_client() -> PeerMemClient:
 class DmabufImport:
     """Importer side of a dma-buf fd (from ``export_dmabuf`` here or in another
     process, or a third-party exporter): the buffer mapped into a GPU's address
-    space (``hsa_amd_interop_map_buffer``). ``tensor()`` views it; ``close()``
-    unmaps. The consumer half of the peer-memory contract (nvidia-peermem's
+    space (``hsa_amd_interop_map_buffer``). ``tensor()`` views it for kernels;
+    the mapping is device-visible only (the HIP runtime does not track it, so
+    hipMemcpy / ``.cpu()`` cannot read it - use kernels or the runtime's ring
+    copies). ``close()`` unmaps. The consumer half of the peer-memory contract (nvidia-peermem's
     importer role, kernel-open/nvidia-peermem/nvidia-peermem.c)."""
 
     def __init__(self, fd: int, device: int = 0):
