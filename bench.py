@@ -28,9 +28,9 @@ bf16 after unpack) in every tier and are unpacked per matrix into a bf16 staging
 buffer right before it is used (the KV prefix likewise, per layer); the
 oversubscription ratio and HBM budget are computed on the logical bf16 footprint
 (weights + KV + embedding + head), and the staging buffers are carved out of that
-budget. Streamed matrices cross PCIe through hipMemcpyAsync on the migration
-ring's side stream (the runtime's default engine), so the compute kernels run at
-full speed beside them. ``--weights bf11`` (decoded
+budget. Streamed matrices cross PCIe on the SDMA engines (the runtime's default
+ring engine, copy_engine=3: ROCr hsa_amd_memory_async_copy_on_engine driven by
+the ring worker), so no CU copy kernel competes with the compute kernels. ``--weights bf11`` (decoded
 in the GEMM's registers) and ``--weights bf16`` run the other paths.
 
 Also reported (aux): HBM<->host and HBM<->CXL GB/s measured through the runtime's
@@ -101,8 +101,9 @@ PROBE_KEYS = ("host_to_hbm", "hbm_to_host", "cxl_to_hbm", "hbm_to_cxl")
 
 
 def bandwidth_probe(dev: int, barrier, nbytes: int = 1 << 30) -> tuple[dict, dict]:
-    """HBM<->host and HBM<->CXL GB/s through the runtime (HIP copy kernels on the
-    rings). Every rank runs it at once (``barrier`` before each timed direction),
+    """HBM<->host and HBM<->CXL GB/s through the runtime's migration rings
+    (``lib.ring_copy``: the ring's configured engine, SDMA by default). Every
+    rank runs it at once (``barrier`` before each timed direction),
     so with N GPUs the sum over ranks is the node's aggregate HBM<->host/CXL rate
     (BASELINE metric: "HBM<->CXL GB/s at 1/2/4/8 GPU"). Returns (rates, info)."""
     import torch

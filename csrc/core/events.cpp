@@ -135,7 +135,9 @@ const char* counter_name(Counter c) {
                             "table_shootdowns",
                             "fault_replays",
                             "fault_records_consumed",
-                            "page_list_copies"};
+                            "page_list_copies",
+                            "vmm_remaps",
+                            "vmm_errors"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -965,6 +965,14 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
       if (!handed[k]) ga->free((uint32_t)(first + k), 1);  // error path: never handed over
   Status fs = finish_ctx(c, out);
   if (st == Status::OK) st = fs;
+  if (r->dev_va) {
+    // A stable VA follows every block to its (possibly relocated) chunk: a
+    // relocation queues no invalidation, so finish_ctx does not remap it.
+    for (Block* b : done) {
+      std::lock_guard<OrderedMutex> g(b->lock);
+      stable_map_block(b);
+    }
+  }
   if (st != Status::OK) {
     if (L) {
       for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);

@@ -444,11 +444,22 @@ void Runtime::stable_map_block(Block* b) {
   int64_t want = (g && g->chunk >= 0) ? g->chunk : -1;
   if (want == b->stable_chunk) return;
   char* va = (char*)r->dev_va + b->block_offset();
-  if (b->stable_chunk >= 0) be_->vmm_unmap(va, kBlockSize);
+  Tools::get().inc(Counter::VmmRemaps);
+  if (b->stable_chunk >= 0 && be_->vmm_unmap(va, kBlockSize) != Status::OK) {
+    Tools::get().inc(Counter::VmmErrors);
+    RT_ERR("stable VA unmap of range %llu block %llu failed: %s", (unsigned long long)r->id,
+           (unsigned long long)b->index, be_->last_error().c_str());
+  }
   b->stable_chunk = -1;
   if (want >= 0) {
     HbmArena* ha = static_cast<HbmArena*>(g->arena);
-    if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) b->stable_chunk = want;
+    if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) {
+      b->stable_chunk = want;
+    } else {
+      Tools::get().inc(Counter::VmmErrors);
+      RT_ERR("stable VA map of range %llu block %llu to chunk %lld failed: %s", (unsigned long long)r->id,
+             (unsigned long long)b->index, (long long)want, be_->last_error().c_str());
+    }
   }
 }
 

@@ -17,6 +17,20 @@
 //   * chunks are taken from the arena already pinned and returned while still
 //     pinned (one critical section each): an allocator chunk is never an
 //     eviction victim, and never visible to reserve() between two steps.
+//
+// Managed mode (torch_alloc_managed_min_mb > 0, hbm_provider=1): allocations at
+// least that large are not arena extents but managed ranges with a stable device
+// VA (HIP VMM): the tensor's pointer never changes while its 2 MB blocks move.
+// Such a tensor is "active" (leased: resident in HBM, pinned) from allocation
+// until torch_park(); a parked tensor is an ordinary preferred-GPU managed range
+// that the arena LRU may evict to host DRAM under pressure (its VA is unmapped),
+// and torch_unpark() makes it resident again at the same VA (the stream waits
+// GPU-side for the copies). Torch tensors thereby oversubscribe HBM - the
+// cudaMallocManaged + cudaMemPrefetchAsync pattern the reference serves with
+// uvm_migrate.c, with explicit park points instead of replayable GPU faults
+// (a kernel touching a parked, evicted tensor would hit an unmapped VA).
+// Frees of managed tensors are deferred until the freeing stream's fence
+// completes (no host stall in free).
 // The C entry points ogkm_torch_alloc / ogkm_torch_free are what
 // CUDAPluggableAllocator dlsym()s.
 #include <mutex>
@@ -53,7 +67,15 @@ struct DevAlloc {
     uint64_t size;
   };
   std::unordered_map<uint64_t, Entry> live;
+  struct Managed {
+    Range* r;
+    Lease* lease;      // nullptr while parked
+    uint64_t size;
+  };
+  std::unordered_map<uint64_t, Managed> managed;   // stable VA -> range
+  std::vector<std::pair<Range*, Tracker>> deferred;  // freed, waiting for their stream fence
   uint64_t allocated = 0, peak = 0, nallocs = 0, stream_waits = 0;
+  uint64_t managed_bytes = 0, parks = 0, unparks = 0;
 };
 
 std::mutex g_m;
@@ -90,6 +112,52 @@ void order_after(Runtime* rt, DevAlloc* da, Tracker t, void* stream) {
   da->stream_waits++;
 }
 
+// Free managed ranges whose last uses have completed (da->m held).
+void reap_deferred(Runtime* rt, DevAlloc* da) {
+  for (size_t i = 0; i < da->deferred.size();) {
+    if (!da->deferred[i].second.query()) {
+      ++i;
+      continue;
+    }
+    rt->free_range(da->deferred[i].first);
+    da->deferred[i] = std::move(da->deferred.back());
+    da->deferred.pop_back();
+  }
+}
+
+// Lease the whole range on `device` (resident in HBM at its stable VA, pinned)
+// and make `stream` wait for the copies that bring it there.
+Status lease_on(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, void* stream) {
+  Lease* L = nullptr;
+  Status st = rt->acquire(m.r, 0, m.size, device, Access::WRITE, &L);
+  if (st != Status::OK) return st;
+  if (L->remote) {  // thrashing / accessed-by chose a zero-copy mapping: the stable VA would not map it
+    rt->release(L, stream);
+    return Status::BUSY;
+  }
+  order_after(rt, da, L->ready, stream);
+  m.lease = L;
+  return Status::OK;
+}
+
+void* managed_alloc(Runtime* rt, DevAlloc* da, size_t size, int device, void* stream) {
+  Range* r = nullptr;
+  uint64_t bytes = align_up((uint64_t)size, kBlockSize);
+  if (rt->malloc_managed(bytes, RANGE_STABLE_VA | RANGE_NO_CPU_VIEW, "torch", &r, device) != Status::OK)
+    return nullptr;
+  rt->mem_advise(r, 0, bytes, Advice::SET_PREFERRED_LOCATION, Loc::gpu(device), device);
+  DevAlloc::Managed m{r, nullptr, bytes};
+  if (lease_on(rt, da, m, device, stream) != Status::OK) {
+    rt->free_range(r);
+    return nullptr;
+  }
+  uint64_t addr = (uint64_t)r->dev_va;
+  da->managed[addr] = m;
+  da->managed_bytes += bytes;
+  da->allocated += bytes;
+  return (void*)addr;
+}
+
 }  // namespace
 
 void* torch_alloc(size_t size, int device, void* stream) {
@@ -101,6 +169,16 @@ void* torch_alloc(size_t size, int device, void* stream) {
   DevAlloc* da = dev_alloc(device);
   int cls = class_of(size);
   std::lock_guard<std::mutex> g(da->m);
+  if (!da->deferred.empty()) reap_deferred(rt, da);
+  const int64_t mmin = config().torch_alloc_managed_min_mb;
+  if (mmin > 0 && size >= ((uint64_t)mmin << 20) && static_cast<HbmArena*>(a)->vmm()) {
+    void* p = managed_alloc(rt, da, size, device, stream);
+    if (p) {
+      da->nallocs++;
+      da->peak = std::max(da->peak, da->allocated);
+    }
+    return p;
+  }
   uint64_t addr = 0;
   if (cls >= 0) {
     uint64_t csz = kMinClass << cls;
@@ -155,6 +233,19 @@ void torch_free(void* p, int device, void* stream) {
   // The freeing stream's queued work may still use the memory.
   FenceRef f = fence_record(rt->be(), device, stream);
   std::lock_guard<std::mutex> g(da->m);
+  auto mt = da->managed.find((uint64_t)p);
+  if (mt != da->managed.end()) {
+    DevAlloc::Managed m = mt->second;
+    da->managed.erase(mt);
+    da->allocated -= m.size;
+    da->managed_bytes -= m.size;
+    if (m.lease) rt->release(m.lease, stream);
+    Tracker t;
+    if (f) t.add(f);
+    da->deferred.emplace_back(m.r, std::move(t));
+    reap_deferred(rt, da);
+    return;
+  }
   auto it = da->live.find((uint64_t)p);
   if (it == da->live.end()) return;
   DevAlloc::Entry e = it->second;
@@ -189,6 +280,45 @@ void torch_free(void* p, int device, void* stream) {
 void torch_alloc_reset() {
   std::lock_guard<std::mutex> g(g_m);
   g_devs.clear();
+}
+
+// Park / unpark a managed tensor (see the header comment). Returns NOT_FOUND
+// for a pointer that is not a managed allocation's base.
+Status torch_park(void* p, int device, void* stream) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  auto it = da->managed.find((uint64_t)p);
+  if (it == da->managed.end()) return Status::NOT_FOUND;
+  if (!it->second.lease) return Status::OK;
+  Status st = rt->release(it->second.lease, stream);  // the stream's queued uses fence the eviction
+  it->second.lease = nullptr;
+  da->parks++;
+  return st;
+}
+
+Status torch_unpark(void* p, int device, void* stream) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  auto it = da->managed.find((uint64_t)p);
+  if (it == da->managed.end()) return Status::NOT_FOUND;
+  if (it->second.lease) return Status::OK;
+  Status st = lease_on(rt, da, it->second, device, stream);
+  if (st == Status::OK) da->unparks++;
+  return st;
+}
+
+// (active, parked bytes, parks, unparks) of the managed tensors.
+void torch_managed_stats(int device, uint64_t* active, uint64_t* parked, uint64_t* parks, uint64_t* unparks) {
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  *active = *parked = 0;
+  for (auto& kv : da->managed) (kv.second.lease ? *active : *parked) += kv.second.size;
+  *parks = da->parks;
+  *unparks = da->unparks;
 }
 
 void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits) {

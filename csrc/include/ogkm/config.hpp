@@ -52,6 +52,7 @@ namespace ogkm {
   X(perf_pma_batch_nonpinned_order, 6, "log2 of chunks evicted per batch")                           \
   X(hbm_budget_mb, 0, "per-GPU HBM budget for the arena in MB (0 = 90% of free)")                   \
   X(hbm_provider, 0, "0=slab (one hipMalloc) 1=vmm (hipMemCreate handles, enables stable VA)")       \
+  X(torch_alloc_managed_min_mb, 0, "pluggable allocator: allocations >= this many MB are evictable stable-VA managed ranges (0 = off; needs hbm_provider=1)") \
   X(host_node, -1, "NUMA node for the host tier (-1 = NUMA node of the first local GPU)")             \
   X(local_devices, 0, "bitmask of the GPUs this process manages (0 = all; one process per GPU: 1<<rank)") \
   X(fake_numa_nodes, 1, "fake backend: NUMA nodes the fake GPUs are spread over (GPU d on node d*n/ndev)") \

@@ -179,6 +179,8 @@ enum class Counter : int {
   FaultReplays,     // replay tokens issued after serviced device-fault batches
   FaultRecordsConsumed,  // device fault-buffer records consumed from GET
   PageListCopies,   // fragmented block copies issued as one page-list kernel
+  VmmRemaps,        // stable-VA block remaps (unmap / map of a 2 MB VMM handle)
+  VmmErrors,        // failed stable-VA unmaps / maps
   NumCounters
 };
 const char* counter_name(Counter c);

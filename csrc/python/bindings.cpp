@@ -20,6 +20,9 @@ namespace ogkm {
 void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits);
 void* torch_alloc(size_t size, int device, void* stream);
 void torch_free(void* p, int device, void* stream);
+Status torch_park(void* p, int device, void* stream);
+Status torch_unpark(void* p, int device, void* stream);
+void torch_managed_stats(int device, uint64_t* active, uint64_t* parked, uint64_t* parks, uint64_t* unparks);
 }  // namespace ogkm
 
 namespace {
@@ -990,6 +993,22 @@ PYBIND11_MODULE(_ogkm, m) {
   }, py::arg("size"), py::arg("dev"), py::arg("stream") = 0);
   m.def("torch_free", [](uint64_t p, int dev, uint64_t stream) { torch_free((void*)p, dev, (void*)stream); },
         py::arg("ptr"), py::arg("dev"), py::arg("stream") = 0);
+  m.def("torch_park", [](uint64_t p, int dev, uint64_t stream) {
+    check(torch_park((void*)p, dev, (void*)stream), "torch_park");
+  }, py::arg("ptr"), py::arg("dev"), py::arg("stream") = 0);
+  m.def("torch_unpark", [](uint64_t p, int dev, uint64_t stream) {
+    check(torch_unpark((void*)p, dev, (void*)stream), "torch_unpark");
+  }, py::arg("ptr"), py::arg("dev"), py::arg("stream") = 0);
+  m.def("torch_managed_stats", [](int dev) {
+    uint64_t a, p, np, nu;
+    torch_managed_stats(dev, &a, &p, &np, &nu);
+    py::dict d;
+    d["active_bytes"] = a;
+    d["parked_bytes"] = p;
+    d["parks"] = np;
+    d["unparks"] = nu;
+    return d;
+  });
   m.def("torch_alloc_stats", [](int dev) {
     uint64_t a, p, n, w;
     torch_alloc_stats(dev, &a, &p, &n, &w);

@@ -8,19 +8,37 @@ model tensors and managed ranges share one HBM budget (north-star config 2:
 Frees are stream-ordered: the freeing stream's fence guards the memory, and
 the next allocation of it makes its own stream wait for that fence GPU-side
 (csrc/core/torch_allocator.cpp).
+
+Managed mode (``enable(managed_min_mb=N)``): allocations of at least N MB are
+runtime-managed ranges at a stable device VA (HIP VMM), so torch tensors
+oversubscribe HBM. A tensor is active (resident, pinned) until :func:`park`;
+parked tensors are evictable by the arena LRU (to host DRAM) and
+:func:`unpark` brings them back at the same address, the current stream waiting
+GPU-side for the copies - the cudaMallocManaged + cudaMemPrefetchAsync pattern
+(reference: uvm_migrate.c) with explicit park points, since a kernel touching
+an evicted tensor would hit an unmapped VA (no replayable faults without XNACK).
 """
 from __future__ import annotations
+
+import contextlib
 
 from ._native import SO_PATH, lib
 
 _enabled = False
 
 
-def enable() -> None:
+def enable(managed_min_mb: int = 0) -> None:
+    """Route torch CUDA allocations through the runtime. ``managed_min_mb`` > 0
+    turns on managed mode for allocations of at least that many MB (call before
+    the runtime creates its HBM arena: it selects the VMM arena provider)."""
     global _enabled
     if _enabled:
         return
     import torch
+
+    if managed_min_mb > 0:
+        lib.configure("hbm_provider", 1)
+        lib.configure("torch_alloc_managed_min_mb", int(managed_min_mb))
 
     alloc = torch.cuda.memory.CUDAPluggableAllocator(str(SO_PATH), "ogkm_torch_alloc", "ogkm_torch_free")
     torch.cuda.memory.change_current_allocator(alloc)
@@ -34,3 +52,44 @@ def enabled() -> bool:
 def stats(device: int = 0) -> dict:
     a, p, n, w = lib.torch_alloc_stats(device)
     return {"allocated": a, "peak": p, "allocs": n, "stream_waits": w}
+
+
+def _base(t) -> tuple[int, int]:
+    """(allocation base pointer, device) of a CUDA tensor."""
+    return t.untyped_storage().data_ptr(), t.device.index or 0
+
+
+def _stream(dev: int) -> int:
+    import torch
+
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def park(*tensors) -> None:
+    """Mark managed tensors evictable; their queued uses on the current stream
+    fence any eviction. Do not touch a parked tensor before :func:`unpark`."""
+    for t in tensors:
+        p, d = _base(t)
+        lib.torch_park(p, d, _stream(d))
+
+
+def unpark(*tensors) -> None:
+    """Make parked tensors resident again (same addresses); the current stream
+    waits GPU-side for the copies, the host does not."""
+    for t in tensors:
+        p, d = _base(t)
+        lib.torch_unpark(p, d, _stream(d))
+
+
+@contextlib.contextmanager
+def parked(*tensors):
+    """``with parked(a, b): ...`` - a and b may be evicted inside the block."""
+    park(*tensors)
+    try:
+        yield
+    finally:
+        unpark(*tensors)
+
+
+def managed_stats(device: int = 0) -> dict:
+    return lib.torch_managed_stats(device)

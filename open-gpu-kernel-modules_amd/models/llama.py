@@ -503,9 +503,39 @@ class TieredLlama:
             from ..parallel.shards import UnitGather
             self.gather = UnitGather([k for k in self.order if k[0] != "kv"], self._buf, self._unit_bytes, self.sworld, self.gather_depth,
                                      device=self.tdev, dev_index=device)
+        self._settle()
         self.init_seconds = time.perf_counter() - t0
         if verbose:
             self.describe()
+
+    def _settle(self) -> None:
+        """Bring the residency to its steady state before the first step: the
+        planned-resident units take their lifetime leases now (the load's
+        writes may have left some of them in host DRAM, evicted by later
+        writes) and the first streaming window is prefetched - so step 0 costs
+        what every later step does instead of paying the layout's convergence
+        (70B tp8 shard: step 0 was 1.86x a steady step)."""
+        if self.gather is None:
+            for key in self.order:
+                if self._is_resident(key) and key not in self._pinned and \
+                        not (key[0] == "kv" and key[1] in self._kv_pinned):
+                    self._pin_resident(key)
+        self._prefetch_ahead()
+        if not self.fake:
+            torch.cuda.synchronize(self.dev)
+
+    def _pin_resident(self, key):
+        """Lifetime lease of a planned-resident unit: later uses cost no
+        runtime call. Returns its WeightRef (a KV prefix: its device pointer)."""
+        lease = self._buf(key).acquire(self.dev, rt.READ)
+        lease.wait(0 if (self.fake or _HOST_LEASE_WAIT) else None)
+        self._pin_leases.append(lease)
+        if key[0] == "kv":
+            self._kv_pinned[key[1]] = lease.dptr
+            return lease.dptr
+        refs = self._ref(key, lease.dptr, self.pmode.get(key, dgemm.MODE_RAW))
+        self._pinned[key] = refs
+        return refs
 
     # ------------------------------------------------------------------ setup
     def describe(self) -> dict:
@@ -786,6 +816,8 @@ class TieredLlama:
         if self.gather is not None:
             return self._use_gathered(key)
         pin = self._pinned.get(key)
+        if pin is None and self._is_resident(key):
+            pin = self._pin_resident(key)
         if pin is not None:  # resident tensor: long-lived lease taken at init, refs cached
             return None, (self._unstage(key, pin.ptr) if self.staged else pin)
         acct = self.byte_trace is not None
@@ -805,12 +837,6 @@ class TieredLlama:
             self.use_trace.append((key, t_w - t_a, time.perf_counter() - t_w))
         mode = self.pmode.get(key, dgemm.MODE_RAW)
         refs = self._ref(key, lease.dptr, mode)
-        if self._is_resident(key):
-            # Planned-resident tensors keep their lease (and so their HBM chunks)
-            # for the model's lifetime: later uses cost no runtime call.
-            self._pinned[key] = refs
-            self._pin_leases.append(lease)
-            return None, (self._unstage(key, lease.dptr) if self.staged else refs)
         if self.staged:
             st = self._unstage(key, lease.dptr)
             lease.release(0 if self.fake else None)
@@ -823,6 +849,8 @@ class TieredLlama:
         Resident layers keep theirs leased for the model's lifetime."""
         key = ("kv", i)
         ptr = self._kv_pinned.get(i)
+        if ptr is None and self._is_resident(key):
+            ptr = self._pin_resident(key)
         if ptr is not None:
             return None, ptr
         if not self._is_resident(key):
@@ -831,10 +859,6 @@ class TieredLlama:
             self._prefetch_ahead()
         lease = self._buf(key).acquire(self.dev, rt.READ)
         lease.wait(0 if (self.fake or _HOST_LEASE_WAIT) else None)
-        if self._is_resident(key):
-            self._kv_pinned[i] = lease.dptr
-            self._pin_leases.append(lease)
-            return None, lease.dptr
         return lease, lease.dptr
 
     def _mark_consumed(self) -> None:

@@ -56,10 +56,11 @@ class DistEnv:
     world: int = 1
     local_rank: int = 0
     backend: str = "none"
+    forced: bool = False  # a one-rank process group (OGKM_DIST_FORCE=1): collectives still run
 
     @property
     def is_dist(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.forced
 
 
 _ENV: Optional[DistEnv] = None
@@ -67,14 +68,18 @@ _ENV: Optional[DistEnv] = None
 
 def init(backend: Optional[str] = None, timeout_s: int = 600) -> DistEnv:
     """Initialise from torchrun-style env vars (RANK / WORLD_SIZE / LOCAL_RANK /
-    MASTER_ADDR / MASTER_PORT). Single-process runs get a trivial env."""
+    MASTER_ADDR / MASTER_PORT). Single-process runs get a trivial env, unless
+    ``OGKM_DIST_FORCE=1``: then a one-rank process group is created and every
+    collective really runs (RCCL on a single GPU - the multi-GPU code path,
+    stream interplay included, exercised on a one-GPU box)."""
     global _ENV
     if _ENV is not None:
         return _ENV
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if world <= 1:
+    forced = world == 1 and os.environ.get("OGKM_DIST_FORCE", "0") == "1"
+    if world <= 1 and not forced:
         _ENV = DistEnv(0, 1, 0, "none")
         return _ENV
     if backend is None:
@@ -90,7 +95,7 @@ def init(backend: Optional[str] = None, timeout_s: int = 600) -> DistEnv:
                                 device_id=torch.device("cuda", local))
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-    _ENV = DistEnv(rank, world, local, backend)
+    _ENV = DistEnv(rank, world, local, backend, forced)
     return _ENV
 
 

@@ -117,7 +117,7 @@ class ShardGatherPipeline:
         self.s = shards
         self.depth = max(1, depth)
         e = comm.env()
-        self.dist = e.is_dist and shards.world > 1
+        self.dist = e.is_dist and (shards.world > 1 or e.forced)
         self.cuda = device is not None and device.type == "cuda"
         self.device = device or torch.device("cpu")
         self.full = [torch.empty(shards.max_full_numel, dtype=shards.dtype, device=self.device)
@@ -276,7 +276,7 @@ class UnitGather:
         return True
 
     def _gather(self, out: torch.Tensor, shard: torch.Tensor) -> None:
-        if self.world > 1:
+        if self.world > 1 or comm.env().forced:
             comm.all_gather_into(out, shard)  # RCCL: the current (side) stream waits, not the host
         else:
             out[:shard.numel()].copy_(shard)

@@ -1,0 +1,119 @@
+"""Pluggable-allocator managed mode: torch allocations as evictable stable-VA
+managed ranges (csrc/core/torch_allocator.cpp). On the fake backend the stable
+VA is a CPU mapping of the fake HBM chunk, so contents are checked through it.
+Parity target: cudaMallocManaged memory oversubscribing the GPU
+(kernel-open/nvidia-uvm/uvm_migrate.c:882 prefetch, uvm_pmm_gpu.c eviction)."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from ogkm import rt
+from ogkm._native import RuntimeStatusError, lib
+
+MB = 1 << 20
+
+
+def _write(ptr: int, arr: np.ndarray) -> None:
+    ctypes.memmove(ptr, arr.ctypes.data, arr.nbytes)
+
+
+def _read(ptr: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.int32)
+    ctypes.memmove(out.ctypes.data, ptr, out.nbytes)
+    return out
+
+
+@pytest.fixture
+def managed_rt(fake_rt):
+    lib.configure("hbm_provider", 1)
+    lib.configure("torch_alloc_managed_min_mb", 4)
+    lib.init_device(0, 32 * MB)  # 16 chunks of fake HBM
+    yield fake_rt
+
+
+def test_managed_tensors_oversubscribe_and_keep_their_address(managed_rt):
+    n = 8 * MB
+    ptrs, refs = [], []
+    for i in range(3):  # 3 x 8 MB active fits in 32 MB
+        p = lib.torch_alloc(n, 0)
+        ref = np.arange(n // 4, dtype=np.int32) * (i + 3)
+        _write(p, ref)
+        lib.torch_park(p, 0)
+        ptrs.append(p)
+        refs.append(ref)
+    # 3 more tensors: 48 MB of tensors on a 32 MB arena - parked ones are evicted
+    for i in range(3, 6):
+        p = lib.torch_alloc(n, 0)
+        ref = np.full(n // 4, i, dtype=np.int32)
+        _write(p, ref)
+        lib.torch_park(p, 0)
+        ptrs.append(p)
+        refs.append(ref)
+    st = lib.torch_managed_stats(0)
+    assert st["parked_bytes"] == 6 * n and st["active_bytes"] == 0
+    assert lib.stats()["evictions"] > 0
+    # every tensor comes back at its own address with its own contents
+    for p, ref in zip(ptrs, refs):
+        lib.torch_unpark(p, 0)
+        assert np.array_equal(_read(p, n // 4), ref)
+        lib.torch_park(p, 0)
+    assert lib.torch_managed_stats(0)["unparks"] == 6
+    for p in ptrs:
+        lib.torch_free(p, 0)
+    rt.sync()
+    lib.torch_alloc(1 * MB, 0)  # any allocation reaps deferred frees
+    assert lib.torch_managed_stats(0)["parked_bytes"] == 0
+
+
+def test_active_tensors_are_never_evicted(managed_rt):
+    n = 8 * MB
+    a = lib.torch_alloc(n, 0)
+    _write(a, np.full(n // 4, 7, dtype=np.int32))
+    parked = [lib.torch_alloc(n, 0) for _ in range(3)]
+    for p in parked:
+        lib.torch_park(p, 0)
+    # a stays active while 3 more active tensors push every parked one out
+    active = [lib.torch_alloc(n, 0) for _ in range(3)]
+    assert all(active)
+    assert np.array_equal(_read(a, n // 4), np.full(n // 4, 7, dtype=np.int32))
+    assert lib.torch_managed_stats(0)["active_bytes"] == 4 * n
+    # 32 MB of active tensors fill the arena: nothing evictable is left
+    assert lib.torch_alloc(n, 0) == 0
+    with pytest.raises(RuntimeStatusError):
+        lib.torch_unpark(parked[0], 0)
+    for p in [a] + parked + active:
+        lib.torch_free(p, 0)
+
+
+def test_small_allocations_stay_arena_extents(managed_rt):
+    p = lib.torch_alloc(1 * MB, 0)
+    assert lib.torch_managed_stats(0)["active_bytes"] == 0
+    with pytest.raises(RuntimeStatusError):
+        lib.torch_park(p, 0)  # not a managed allocation
+    lib.torch_free(p, 0)
+
+
+def test_partially_evicted_tensor_relocates_under_its_address(managed_rt):
+    """Only part of a parked tensor is evicted; unpark relocates the resident
+    part into a fresh extent (D2D) and faults the rest back: the stable VA must
+    follow every block to its new chunk."""
+    n = 8 * MB
+    b = lib.torch_alloc(16 * MB, 0)     # chunks 0-7, active
+    a = lib.torch_alloc(n, 0)           # chunks 8-11
+    ref = np.arange(n // 4, dtype=np.int32) ^ 0x5A5A
+    _write(a, ref)
+    lib.torch_park(a, 0)
+    c = lib.torch_alloc(12 * MB, 0)     # 6 contiguous chunks: 12-15 + two of a's
+    assert c and lib.stats()["evictions"] >= 1
+    info = lib.torch_managed_stats(0)
+    assert info["parked_bytes"] == n
+    lib.torch_free(b, 0)
+    rt.sync()
+    lib.torch_alloc(4096, 0)            # reaps b's deferred free
+    lib.torch_unpark(a, 0)
+    assert np.array_equal(_read(a, n // 4), ref)
+    for p in (a, c):
+        lib.torch_free(p, 0)

@@ -26,10 +26,12 @@ def _port() -> int:
     return p
 
 
-def _bench(tmp_path, nproc: int, extra: list) -> tuple[dict, torch.Tensor]:
-    dump = str(tmp_path / f"logits_{nproc}_{'_'.join(extra)}.pt")
+def _bench(tmp_path, nproc: int, extra: list, force_dist: bool = False) -> tuple[dict, torch.Tensor]:
+    dump = str(tmp_path / f"logits_{nproc}_{int(force_dist)}_{'_'.join(extra)}.pt")
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", OGKM_UNIT_MIN_MB="0")
-    if nproc == 1:
+    if force_dist:
+        env["OGKM_DIST_FORCE"] = "1"
+    if nproc == 1 and not force_dist:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py")]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -62,3 +64,13 @@ def test_bench_four_ranks(single, tmp_path, parallel):
     else:
         # row-parallel partial sums are reduced in a different order
         torch.testing.assert_close(logits, ref, atol=0.05, rtol=0.05)
+
+
+@pytest.mark.parametrize("parallel", ["tp", "shards"])
+def test_bench_forced_one_rank_group(single, tmp_path, parallel):
+    """OGKM_DIST_FORCE=1: a one-rank process group in which every collective
+    still runs (the GPU twin is tests/test_gpu_rccl.py) - bit-identical."""
+    _, ref = single
+    out, logits = _bench(tmp_path, 1, ["--parallel", parallel], force_dist=True)
+    assert out["n_gpus"] == 1
+    assert torch.equal(logits, ref)
