@@ -142,6 +142,28 @@ class HipBackend : public Backend {
     vmm_maps_.erase((uint64_t)va);
     return Status::OK;
   }
+  // Heavyweight translation flush provoked from user space: mapping a 4 KB SVM
+  // page on the GPU and revoking it again runs the KFD SVM unmap path, which
+  // flushes the process's GPU TLBs (VMM unmap / map on gfx950 here does not:
+  // tools/probe_vmm_tlb.hip, 100/100 stale reads without, 99/100 right with).
+  Status tlb_flush(int dev) override {
+    dma_init();
+    if (dev < 0 || dev >= (int)dma_.size() || !dma_[dev].gpu.handle) return Status::NOT_SUPPORTED;
+    std::lock_guard<std::mutex> g(flush_m_);
+    if (!flush_page_) {
+      flush_page_ = aligned_alloc(4096, 4096);
+      if (!flush_page_) return Status::NO_MEMORY;
+      memset(flush_page_, 0, 4096);
+    }
+    hsa_amd_svm_attribute_pair_t on{HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE_IN_PLACE, dma_[dev].gpu.handle};
+    hsa_amd_svm_attribute_pair_t off{HSA_AMD_SVM_ATTRIB_AGENT_NO_ACCESS, dma_[dev].gpu.handle};
+    if (hsa_amd_svm_attributes_set(flush_page_, 4096, &on, 1) != HSA_STATUS_SUCCESS ||
+        hsa_amd_svm_attributes_set(flush_page_, 4096, &off, 1) != HSA_STATUS_SUCCESS) {
+      last_err_ = "hsa_amd_svm_attributes_set (TLB flush) failed";
+      return Status::IO_ERROR;
+    }
+    return Status::OK;
+  }
   // Device of the VMM mapping that contains `a` (-1 = none).
   int vmm_dev(uint64_t a) {
     std::lock_guard<std::mutex> g(reg_m_);
@@ -572,7 +594,7 @@ class HipBackend : public Backend {
   void dma_init() {
     std::call_once(dma_once_, [this] {
       dma_.assign(ndev_, DmaDev{});
-      if (config().copy_engine != 3 || hsa_init() != HSA_STATUS_SUCCESS) return;
+      if (hsa_init() != HSA_STATUS_SUCCESS) return;  // agents are resolved for every engine choice
       std::vector<hsa_agent_t> agents;
       if (hsa_iterate_agents(dma_agent_cb, &agents) != HSA_STATUS_SUCCESS) return;
       hsa_agent_t cpu{0};
@@ -602,7 +624,7 @@ class HipBackend : public Backend {
             if (hsa_amd_memory_copy_engine_status(dd.gpu, cpu, &m) == HSA_STATUS_SUCCESS) dd.h2d = m;
             if (hsa_amd_memory_copy_engine_status(cpu, dd.gpu, &m) == HSA_STATUS_SUCCESS) dd.d2h = m;
             dd.d2d = dd.h2d | dd.d2h;
-            dd.ok = cpu.handle && dd.h2d && dd.d2h;
+            dd.ok = config().copy_engine == 3 && cpu.handle && dd.h2d && dd.d2h;
           }
       }
     });
@@ -683,6 +705,8 @@ class HipBackend : public Backend {
   std::mutex ev_m_, df_m_, reg_m_;
   std::map<uint64_t, uint64_t> regs_;  // host registrations: base -> bytes
   std::map<uint64_t, std::pair<uint64_t, int>> vmm_maps_;  // VMM mappings: va -> (bytes, device)
+  std::mutex flush_m_;
+  void* flush_page_ = nullptr;  // the SVM page toggled by tlb_flush (never freed: process lifetime)
   std::vector<void*> free_events_[64];
   std::map<void*, int> ev_dev_;
   std::map<void*, void*> ipc_base_;  // opened IPC pointer -> mapped allocation base

@@ -137,7 +137,8 @@ const char* counter_name(Counter c) {
                             "fault_records_consumed",
                             "page_list_copies",
                             "vmm_remaps",
-                            "vmm_errors"};
+                            "vmm_errors",
+                            "tlb_flushes"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

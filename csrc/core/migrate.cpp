@@ -562,6 +562,7 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
     update_device_table(b);
     if (b->range->dev_va) stable_map_block(b);
   }
+  if (tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
   // The context is spent; what the caller still needs for its retry (the
   // arena to evict from on MORE_PROCESSING_REQUIRED) survives the reset.
   ChunkArena* need_arena = c.need_arena;
@@ -972,6 +973,7 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
       std::lock_guard<OrderedMutex> g(b->lock);
       stable_map_block(b);
     }
+    if (tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
   }
   if (st != Status::OK) {
     if (L) {

@@ -455,10 +455,24 @@ void Runtime::stable_map_block(Block* b) {
     HbmArena* ha = static_cast<HbmArena*>(g->arena);
     if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) {
       b->stable_chunk = want;
+      tlb_dirty_.fetch_or(1u << r->stable_dev);
     } else {
       Tools::get().inc(Counter::VmmErrors);
       RT_ERR("stable VA map of range %llu block %llu to chunk %lld failed: %s", (unsigned long long)r->id,
              (unsigned long long)b->index, (long long)want, be_->last_error().c_str());
+    }
+  }
+}
+
+void Runtime::flush_translations() {
+  uint32_t m = tlb_dirty_.exchange(0);
+  for (int d = 0; m; ++d, m >>= 1) {
+    if (!(m & 1)) continue;
+    if (be_->tlb_flush(d) != Status::OK) {
+      Tools::get().inc(Counter::VmmErrors);
+      RT_ERR("GPU %d translation flush after stable-VA remaps failed: %s", d, be_->last_error().c_str());
+    } else {
+      Tools::get().inc(Counter::TlbFlushes);
     }
   }
 }

@@ -70,6 +70,14 @@ class Backend {
   virtual void va_free(void* va, size_t bytes) = 0;
   virtual Status vmm_map(void* va, size_t bytes, uint64_t handle, int dev) = 0;
   virtual Status vmm_unmap(void* va, size_t bytes) = 0;
+  // Invalidate the process's cached GPU translations on `dev`. Needed after a
+  // VA that was mapped to one handle is mapped to another: on this driver stack
+  // (gfx950) hipMemUnmap / hipMemMap leave the old translation live, so the VA
+  // keeps reading the previous chunk (tools/probe_vmm_tlb.hip).
+  virtual Status tlb_flush(int dev) {
+    (void)dev;
+    return Status::OK;
+  }
 
   // ---- host memory pinning (device-visible at the same address)
   virtual Status host_register(void* p, size_t bytes) = 0;

@@ -180,7 +180,8 @@ enum class Counter : int {
   FaultRecordsConsumed,  // device fault-buffer records consumed from GET
   PageListCopies,   // fragmented block copies issued as one page-list kernel
   VmmRemaps,        // stable-VA block remaps (unmap / map of a 2 MB VMM handle)
-  VmmErrors,        // failed stable-VA unmaps / maps
+  VmmErrors,        // failed stable-VA unmaps / maps / translation flushes
+  TlbFlushes,       // GPU translation flushes after stable-VA remaps
   NumCounters
 };
 const char* counter_name(Counter c);

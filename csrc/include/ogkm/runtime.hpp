@@ -241,6 +241,10 @@ class Runtime {
   Loc demotion_target(const Loc& from);
   void cpu_map_block(Block* b);  // refresh CPU view protections
   void stable_map_block(Block* b);
+  // Flush GPU translations of devices whose stable VAs were remapped since the
+  // last flush (before any consumer of the new mapping can run).
+  void flush_translations();
+  std::atomic<uint32_t> tlb_dirty_{0};  // bit d: device d has remapped stable VAs
   Status finish_ctx(Ctx& c, Tracker* out);
   void drop_copy(Ctx& c, Block* b, const Loc& l);  // release a residency (block lock held)
   void touch_residency(Block* b, Residency* r, bool prefetched = false);  // LRU bump (preferred / prefetch aware)
