@@ -521,6 +521,15 @@ class TieredLlama:
                         not (key[0] == "kv" and key[1] in self._kv_pinned):
                     self._pin_resident(key)
         self._prefetch_ahead()
+        if os.environ.get("OGKM_WARM_STEP", "1") != "0":
+            # One warm-up decode at load, then the position rewinds (the next
+            # step rewrites the same KV slot): kernels are loaded, the compute
+            # path's torch allocations are pooled and the streaming cursor sits
+            # where every later step finds it - what a serving engine's start-up
+            # warm-up does. Step 0 of a run then costs what step 1 does.
+            tok = torch.zeros(self.B, dtype=torch.int64, device=self.tdev)
+            self.step(tok)
+            self.reset(self.ctx)
         if not self.fake:
             torch.cuda.synchronize(self.dev)
 
