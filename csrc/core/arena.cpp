@@ -467,6 +467,11 @@ HostArena::HostArena(Backend* be, Tier tier, int node, uint64_t capacity)
     init_chunks(0, 0);
     return;
   }
+  // Ask for transparent huge pages on the tier (honoured when shmem THP is
+  // "advise"/"always"): fewer TLB entries for the DMA engines and the GPU's
+  // remote reads, 2 MB pin granularity. hugetlbfs is not used: a
+  // memfd past the reserved huge-page pool would SIGBUS on first touch.
+  thp_advised_ = madvise(view_, bytes_, MADV_HUGEPAGE) == 0;
   // Bind the pages of this tier to its NUMA node (CXL.mem nodes are CPU-less
   // NUMA nodes). Shared (shmem) mappings keep the policy on the object.
   if (node >= 0 && node < 64) {

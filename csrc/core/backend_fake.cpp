@@ -21,6 +21,7 @@
 #include "ogkm/backend.hpp"
 #include "ogkm/config.hpp"
 #include "ogkm/codec.hpp"
+#include "ogkm/runtime.hpp"
 
 namespace ogkm {
 
@@ -145,6 +146,18 @@ class FakeBackend : public Backend {
     if (dev >= 0 && dev < ndev_) used_[dev] -= bytes;
   }
 
+  // Fake RAS counters: tests raise them through Injection (ecc_ue / ecc_ce / link_ue).
+  Status device_health(int dev, Health* out) override {
+    if (dev < 0 || dev >= ndev_) return Status::INVALID_ARGUMENT;
+    Runtime* rt = Runtime::get();
+    *out = Health{};
+    out->source = "fake";
+    out->ue = rt ? rt->inject().ecc_ue.load() : 0;
+    out->ce = rt ? rt->inject().ecc_ce.load() : 0;
+    out->link_ue = rt ? rt->inject().link_ue.load() : 0;
+    out->link_ce = 0;
+    return Status::OK;
+  }
   bool vmm_supported(int) override { return true; }
   Status vmm_create(int dev, size_t bytes, uint64_t* h) override {
     if (used_[dev] + bytes > hbm_) return Status::NO_MEMORY;

@@ -21,6 +21,7 @@
 //   on the completion signal. No CU is used: measured beside a 2 GB HBM
 //   streaming read (tools/probe_sdma.hip, profiles/r2_copy_engines.md) SDMA costs
 //   the reader 1.06x, our 16-WG CU copy kernel 2.86x, at the same 56.8 GB/s.
+#include <dirent.h>
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <hsa/hsa.h>
@@ -72,6 +73,39 @@ class HipBackend : public Backend {
     if (fscanf(f, "%d", &n) != 1) n = 0;
     fclose(f);
     return n < 0 ? 0 : n;
+  }
+  // amdgpu RAS counters under the GPU's PCI device: ras/<block>_err_count
+  // files hold "ue: N" / "ce: N" lines.
+  Status device_health(int dev, Health* out) override {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) return Status::INVALID_ARGUMENT;
+    for (char* p = bus; *p; ++p) *p = (char)tolower(*p);
+    std::string dir = std::string("/sys/bus/pci/devices/") + bus + "/ras";
+    DIR* d = opendir(dir.c_str());
+    if (!d) return Status::NOT_SUPPORTED;
+    *out = Health{};
+    out->source = dir;
+    while (dirent* e = readdir(d)) {
+      std::string n = e->d_name;
+      if (n.size() < 11 || n.compare(n.size() - 10, 10, "_err_count") != 0) continue;
+      FILE* f = fopen((dir + "/" + n).c_str(), "r");
+      if (!f) continue;
+      long long ue = -1, ce = -1;
+      char line[128];
+      while (fgets(line, sizeof line, f)) {
+        long long v;
+        if (sscanf(line, "ue: %lld", &v) == 1) ue = v;
+        else if (sscanf(line, "ce: %lld", &v) == 1) ce = v;
+      }
+      fclose(f);
+      bool link = n.rfind("xgmi", 0) == 0 || n.find("wafl") != std::string::npos || n.find("pcs") != std::string::npos;
+      int64_t& U = link ? out->link_ue : out->ue;
+      int64_t& C = link ? out->link_ce : out->ce;
+      if (ue >= 0) U = (U < 0 ? 0 : U) + ue;
+      if (ce >= 0) C = (C < 0 ? 0 : C) + ce;
+    }
+    closedir(d);
+    return Status::OK;
   }
   Status device_mem_info(int dev, size_t* f, size_t* t) override {
     HIPCHK(hipSetDevice(dev));

@@ -164,6 +164,35 @@ void CxlRegistry::init(uint64_t pin_budget, uint32_t max_buffers, uint64_t max_b
   gens_.assign(max_buffers, 1);
 }
 
+// Backing of the mapping that contains `addr` (/proc/self/smaps): the kernel
+// page size (hugetlbfs mappings report 2 MB / 1 GB) and the bytes of it mapped
+// by transparent huge pages. Huge-page pinning is then a property
+// that is measured, not a label guessed from the buffer's alignment.
+static void backing_of(uint64_t addr, uint64_t* kernel_page, uint64_t* thp_bytes) {
+  *kernel_page = kPageSize;
+  *thp_bytes = 0;
+  FILE* f = fopen("/proc/self/smaps", "r");
+  if (!f) return;
+  char line[512];
+  bool in = false;
+  while (fgets(line, sizeof line, f)) {
+    unsigned long lo = 0, hi = 0;
+    char c = 0;
+    if (sscanf(line, "%lx-%lx %c", &lo, &hi, &c) == 3 && strchr(line, '-') < strchr(line, ' ')) {
+      if (in) break;  // past the mapping
+      in = addr >= lo && addr < hi;
+      continue;
+    }
+    if (!in) continue;
+    unsigned long kb = 0;
+    if (sscanf(line, "KernelPageSize: %lu kB", &kb) == 1) *kernel_page = (uint64_t)kb << 10;
+    else if (sscanf(line, "AnonHugePages: %lu kB", &kb) == 1 || sscanf(line, "ShmemPmdMapped: %lu kB", &kb) == 1 ||
+             sscanf(line, "FilePmdMapped: %lu kB", &kb) == 1)
+      *thp_bytes += (uint64_t)kb << 10;
+  }
+  fclose(f);
+}
+
 Status CxlRegistry::register_buffer(uint64_t base, uint64_t size, int version, uint64_t* handle) {
   if (!base || size == 0 || version < 1 || version > 3) return Status::INVALID_ARGUMENT;
   if (base + size < base) return Status::INVALID_ARGUMENT;  // overflow
@@ -188,6 +217,8 @@ Status CxlRegistry::register_buffer(uint64_t base, uint64_t size, int version, u
   // 2 MB extents when the buffer is 2 MB aligned in address and size (A4, with
   // the page counting done in base pages, not in huge pages).
   b.page_size = ((base | size) & (kBlockSize - 1)) == 0 ? kBlockSize : kPageSize;
+  backing_of(base, &b.backing_page, &b.thp_bytes);
+  if (b.backing_page > kBlockSize && b.page_size == kBlockSize) b.page_size = kBlockSize;  // 1 GB pages: 2 MB extents
   int node = -1;
   if (get_mempolicy(&node, nullptr, 0, (void*)base, MPOL_F_NODE | MPOL_F_ADDR) != 0) node = -1;
   b.numa_node = node;
@@ -202,8 +233,9 @@ Status CxlRegistry::register_buffer(uint64_t base, uint64_t size, int version, u
   b.handle = ((uint64_t)gens_[slot] << 32) | (uint64_t)(slot + 1);
   slots_[slot] = b;
   *handle = b.handle;
-  RT_INFO("cxl: registered buffer %#llx size %llu ver %d page %llu node %d", (unsigned long long)base,
-          (unsigned long long)size, version, (unsigned long long)b.page_size, node);
+  RT_INFO("cxl: registered buffer %#llx size %llu ver %d page %llu (backing %llu, thp %llu B) node %d",
+          (unsigned long long)base, (unsigned long long)size, version, (unsigned long long)b.page_size,
+          (unsigned long long)b.backing_page, (unsigned long long)b.thp_bytes, node);
   return Status::OK;
 }
 

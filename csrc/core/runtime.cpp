@@ -65,6 +65,8 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
       dev->fault_buf.recs = (DeviceFaultRecord*)((char*)p + sizeof(FaultBufHeader));
       dev->fault_buf.entries = entries;
     }
+    dev->health_ok = rt->be_->device_health(d, &dev->health0) == Status::OK;
+    dev->health = dev->health0;
     rt->devs_.push_back(std::move(dev));
   }
   rt->perf_subs_ = perf_modules_register(Tools::get().bus());
@@ -955,6 +957,35 @@ Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
   return Status::OK;
 }
 
+Status Runtime::check_health(int dev, bool force) {
+  if (!is_local(dev)) return Status::INVALID_ARGUMENT;
+  Device& d = *devs_[dev];
+  std::lock_guard<std::mutex> g(d.health_m);
+  uint64_t now = now_ns();
+  if (!force && now - d.health_checked_ns < 20ull * 1000 * 1000) return global_status();
+  d.health_checked_ns = now;
+  Backend::Health h;
+  if (be_->device_health(dev, &h) != Status::OK) return global_status();
+  if (!d.health_ok) {  // counters appeared after init: take them as the baseline
+    d.health0 = h;
+    d.health_ok = true;
+  }
+  d.health = h;
+  auto grew = [](int64_t now_v, int64_t base) { return now_v >= 0 && now_v > (base < 0 ? 0 : base); };
+  const char* why = grew(h.ue, d.health0.ue) ? "uncorrectable ECC error"
+                    : grew(h.link_ue, d.health0.link_ue) ? "uncorrectable xGMI link error" : nullptr;
+  if (why && global_status() == Status::OK) {
+    char msg[160];
+    snprintf(msg, sizeof msg, "GPU %d: %s (ue %lld, link ue %lld since init)", dev, why,
+             (long long)(h.ue - std::max<int64_t>(0, d.health0.ue)),
+             (long long)(h.link_ue - std::max<int64_t>(0, d.health0.link_ue)));
+    RT_ERR("%s", msg);
+    tools_event(ToolsEventType::FatalFault, Cause::User, Loc::gpu(dev), Loc::gpu(dev), dev, 0, 0, 0);
+    set_fatal(Status::FATAL, msg);
+  }
+  return global_status();
+}
+
 Status Runtime::sync_all() {
   Status st = Status::OK;
   for (auto& d : devs_)
@@ -965,6 +996,10 @@ Status Runtime::sync_all() {
       if (s != Status::OK && st == Status::OK) st = s;
     }
   refresh_device_tables();
+  // Completed work is only trusted once the GPU reports no new uncorrectable
+  // error (the post-push ECC check of uvm_gpu.c:1328-1354).
+  for (auto& d : devs_)
+    if (d->local && check_health(d->id) != Status::OK && st == Status::OK) st = global_status();
   return st;
 }
 
@@ -997,6 +1032,7 @@ Status Runtime::start_fault_service(uint32_t poll_us) {
                                       __atomic_load_n(&fb.hdr->get, __ATOMIC_RELAXED) ||
                                   __atomic_load_n(&fb.hdr->overflow, __ATOMIC_RELAXED) != fb.overflow_seen);
         if (!pending) {
+          check_health(d);  // rate-limited: one sysfs scan per 20 ms at most
           std::this_thread::sleep_for(std::chrono::microseconds(poll_us ? poll_us : 50));
           continue;
         }

@@ -160,6 +160,7 @@ class HostArena : public ChunkArena {
   Status ensure_registered(uint32_t first, uint32_t n);
   Status init_status() const { return init_; }
   bool numa_bound() const { return numa_bound_; }
+  bool thp_advised() const { return thp_advised_; }
 
  private:
   Backend* be_;
@@ -170,6 +171,7 @@ class HostArena : public ChunkArena {
   std::vector<uint8_t> seg_registered_;  // per 1 GB segment
   std::mutex seg_m_;
   bool numa_bound_ = false;
+  bool thp_advised_ = false;
   Status init_ = Status::OK;
 };
 

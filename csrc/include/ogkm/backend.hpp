@@ -70,6 +70,19 @@ class Backend {
   virtual void va_free(void* va, size_t bytes) = 0;
   virtual Status vmm_map(void* va, size_t bytes, uint64_t handle, int dev) = 0;
   virtual Status vmm_unmap(void* va, size_t bytes) = 0;
+  // RAS error counters of a GPU (ECC of HBM / on-chip SRAM and xGMI link
+  // errors): the analog of the reference's ECC error notifier and NVLink error
+  // checks (uvm_gpu.c:1328-1354, 2087-2104). -1 = not reported by the platform.
+  struct Health {
+    int64_t ue = -1, ce = -1;            // uncorrectable / correctable, all blocks but xGMI
+    int64_t link_ue = -1, link_ce = -1;  // xGMI (WAFL / PCS) link errors
+    std::string source;                  // where the counters were read
+  };
+  virtual Status device_health(int dev, Health* out) {
+    (void)dev;
+    (void)out;
+    return Status::NOT_SUPPORTED;
+  }
   // Invalidate the process's cached GPU translations on `dev`. Needed after a
   // VA that was mapped to one handle is mapped to another: on this driver stack
   // (gfx950) hipMemUnmap / hipMemMap leave the old translation live, so the VA

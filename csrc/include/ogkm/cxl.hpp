@@ -91,7 +91,9 @@ struct CxlBuffer {
   uint64_t base = 0;
   uint64_t size = 0;
   int version = 0;
-  uint64_t page_size = 0;   // 4 KB or 2 MB
+  uint64_t page_size = 0;   // 4 KB or 2 MB: the extent granularity
+  uint64_t backing_page = 0;  // kernel page size backing the buffer (hugetlbfs: 2 MB / 1 GB)
+  uint64_t thp_bytes = 0;     // bytes mapped by transparent huge pages at registration
   std::vector<CxlExtent> extents;
   uint32_t page_refs = 0;   // outstanding pages() users
   bool registered_with_device = false;

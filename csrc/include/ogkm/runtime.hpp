@@ -96,6 +96,12 @@ struct Device {
   std::atomic<HbmArena*> hbm_live{nullptr};  // published `hbm` for lock-free readers (arena_for)
   std::unique_ptr<Ring> rings[(int)RingKind::COUNT];
   DeviceFaultBuffer fault_buf;
+  // RAS counters at init (the baseline) and the last check: an uncorrectable
+  // error past the baseline makes the runtime FATAL (uvm_gpu.c:1328-1354).
+  Backend::Health health0, health;
+  bool health_ok = false;           // the platform reports RAS counters
+  uint64_t health_checked_ns = 0;
+  std::mutex health_m;
 };
 
 struct Injection {
@@ -106,6 +112,7 @@ struct Injection {
   std::atomic<int64_t> populate_error{0};      // next N populates fail
   std::atomic<int64_t> host_alloc_error{0};    // next N host chunk allocs fail
   std::atomic<int64_t> async_copy_error{0};     // next N ring completions report a post-submission failure
+  std::atomic<int64_t> ecc_ue{0}, ecc_ce{0}, link_ue{0};  // fake backend RAS counters
 };
 
 struct ResidencyInfo {   // UVM_TEST_VA_RESIDENCY_INFO analog (uvm_test_ioctl.h:626-674)
@@ -208,6 +215,11 @@ class Runtime {
   Status resume();
   Status checkpoint_save(const std::string& path, bool with_data);
   Status checkpoint_load(const std::string& path, bool with_data, std::vector<uint64_t>* new_range_ids);
+
+  // ---- GPU health (ECC / xGMI link errors, rate-limited sysfs reads)
+  // OK, or FATAL once an uncorrectable error appeared since init. `force`
+  // skips the rate limit (min_interval_ms).
+  Status check_health(int dev, bool force = false);
 
   // ---- peers
   Status enable_peer(int a, int b);

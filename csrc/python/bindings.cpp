@@ -529,6 +529,31 @@ PYBIND11_MODULE(_ogkm, m) {
     d["global_status"] = status_str(global_status());
     return d;
   });
+  m.def("device_health", [](int dev) {
+    Status st = rt()->check_health(dev, true);
+    Device& d = rt()->dev(dev);
+    std::lock_guard<std::mutex> g(d.health_m);
+    auto h2d = [](const Backend::Health& h) {
+      py::dict x;
+      x["ue"] = h.ue;
+      x["ce"] = h.ce;
+      x["link_ue"] = h.link_ue;
+      x["link_ce"] = h.link_ce;
+      x["source"] = h.source;
+      return x;
+    };
+    py::dict out;
+    out["reported"] = d.health_ok;
+    out["baseline"] = h2d(d.health0);
+    out["now"] = h2d(d.health);
+    out["status"] = status_str(st);
+    return out;
+  });
+  m.def("inject_ras", [](int64_t ue, int64_t ce, int64_t link_ue) {
+    rt()->inject().ecc_ue.store(ue);
+    rt()->inject().ecc_ce.store(ce);
+    rt()->inject().link_ue.store(link_ue);
+  });
   m.def("reset_counters", [] { Tools::get().reset_counters(); });
   m.def("arena_stats", [](int tier, int id) {
     ChunkArena* a = rt()->arena_for(make_loc(tier, id));
@@ -547,6 +572,11 @@ PYBIND11_MODULE(_ogkm, m) {
     d["free_chunks"] = a->free_chunks();
     d["nchunks"] = a->nchunks();
     d["base"] = a->base();
+    if (!a->loc().is_gpu()) {
+      auto* h = static_cast<HostArena*>(a);
+      d["numa_bound"] = h->numa_bound();
+      d["thp_advised"] = h->thp_advised();
+    }
     return d;
   });
   m.def("arena_check", [](int tier, int id) {
@@ -902,6 +932,8 @@ PYBIND11_MODULE(_ogkm, m) {
     d["size"] = b.size;
     d["version"] = b.version;
     d["page_size"] = b.page_size;
+    d["backing_page"] = b.backing_page;
+    d["thp_bytes"] = b.thp_bytes;
     d["numa_node"] = b.numa_node;
     d["page_refs"] = b.page_refs;
     return d;

@@ -17,6 +17,7 @@ pool (config ``cxl_emulate_node``) - results are then labelled ``emulated``.
 from __future__ import annotations
 
 import ctypes
+import os
 import ctypes.util
 import mmap
 import time
@@ -99,16 +100,37 @@ def _mbind(addr: int, size: int, node: int) -> None:
     mbind(addr, size, MPOL_BIND, ctypes.byref(mask), 64, 0)
 
 
-def p2p_caps(device: int = 0) -> dict:
-    """CXL reachability of a GPU (the P2P caps CXL bit the fork declares but never sets)."""
+def numa_distances(node: int, sysfs: str = "/sys") -> dict:
+    """SLIT distances from NUMA ``node`` to every node ({node: distance}), from
+    ``<sysfs>/devices/system/node/node<N>/distance`` ({} when unreadable)."""
+    base = os.path.join(sysfs, "devices", "system", "node")
+    try:
+        nodes = sorted(int(d[4:]) for d in os.listdir(base) if d.startswith("node") and d[4:].isdigit())
+        with open(os.path.join(base, f"node{node}", "distance")) as f:
+            dist = [int(x) for x in f.read().split()]
+    except (OSError, ValueError):
+        return {}
+    return {n: d for n, d in zip(nodes, dist)}
+
+
+def p2p_caps(device: int = 0, sysfs: str = "/sys") -> dict:
+    """CXL reachability of a GPU (the P2P caps CXL bit the fork declares but
+    never sets, kern_bus_ctrl.c:769-774): per CXL node, the NUMA distance from the
+    GPU's own node (the CPU-side hop a GPU<->CXL DMA crosses) and the nearest node."""
     info = lib.cxl_info()
+    gnode = lib.device_numa_node(device) if device < lib.device_count() else -1
+    dist = numa_distances(gnode, sysfs) if gnode >= 0 else {}
+    cxl_dist = {n: dist.get(n, -1) for n in info["numa_nodes"]}
+    reachable = [n for n, d in cxl_dist.items() if d >= 0]
     return {
         "cxl_supported": bool(info["memory_expander"]),
         "cxl_link_up": bool(info["link_up"]),
         "emulated": bool(info["emulated"]),
         "connectivity": "CXL" if info["memory_expander"] else "NONE",
-        "gpu_numa_node": lib.device_numa_node(device) if device < lib.device_count() else -1,
+        "gpu_numa_node": gnode,
         "cxl_numa_nodes": info["numa_nodes"],
+        "cxl_numa_distance": cxl_dist,
+        "nearest_cxl_node": min(reachable, key=lambda n: (cxl_dist[n], n)) if reachable else -1,
     }
 
 

@@ -21,6 +21,7 @@ def _fake_sysfs(tmp_path, with_cxl_bus=True):
         d.mkdir(parents=True)
         (d / "cpulist").write_text(cpus + "\n")
         (d / "meminfo").write_text(f"Node {nid} MemTotal:       {kb} kB\n")
+        (d / "distance").write_text({0: "10 32 20", 1: "32 10 40", 2: "20 40 10"}[nid] + "\n")
     if with_cxl_bus:
         port = tmp_path / "bus" / "cxl" / "devices" / "port0"
         mem = tmp_path / "bus" / "cxl" / "devices" / "mem0"
@@ -40,7 +41,11 @@ def test_topology_from_sysfs(fake_rt, tmp_path):
     assert info["memory_expander"] and info["link_up"] and not info["emulated"]
     assert info["cxl_version"] == 2  # Gen5 link
     assert any(d["name"] == "mem0" and d["numa_node"] == 2 for d in info["devices"])
-    assert cxl.p2p_caps(0)["connectivity"] == "CXL"
+    caps = cxl.p2p_caps(0, str(root))
+    assert caps["connectivity"] == "CXL"
+    # fake GPU 0 sits on node 0: the CXL node is 20 away (SLIT)
+    assert caps["gpu_numa_node"] == 0 and caps["cxl_numa_distance"] == {2: 20} and caps["nearest_cxl_node"] == 2
+    assert cxl.numa_distances(1, str(root)) == {0: 32, 1: 10, 2: 40}
 
 
 def test_emulated_node(fake_rt, tmp_path):
@@ -69,7 +74,9 @@ def test_register_validation_and_unregister(fake_rt):
     assert h >> 32 >= 1 and (h & 0xFFFFFFFF) >= 1   # opaque generation-checked handle
     with pytest.raises(rt.RuntimeStatusError, match="BUSY"):
         lib.cxl_register(base + 4 * MB, 4 * MB, 2)  # overlap
-    assert lib.cxl_buffer(h)["page_size"] in (4096, 2 * MB)
+    info = lib.cxl_buffer(h)
+    assert info["page_size"] in (4096, 2 * MB)
+    assert info["backing_page"] >= 4096  # measured from /proc/self/smaps (hugetlbfs reports 2 MB / 1 GB)
     lib.cxl_unregister(h)
     with pytest.raises(rt.RuntimeStatusError, match="NOT_FOUND"):
         lib.cxl_unregister(h)               # stale handle

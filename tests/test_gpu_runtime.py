@@ -195,6 +195,21 @@ def test_stable_va_vmm(gpu_rt):
     b.free()
 
 
+def test_device_health_reports_ras_counters(gpu_rt):
+    """ECC / xGMI RAS counters of the real GPU (amdgpu sysfs ras/*_err_count):
+    baselined at init, and a healthy box stays OK after a migration round trip."""
+    buf = rt.malloc_managed(8 * MB, "health")
+    buf.write(torch.arange(2 * MB, dtype=torch.int32))
+    buf.migrate("gpu:0")
+    buf.migrate("host")
+    h = lib.device_health(0)
+    print("device_health", h)
+    assert h["status"] == "OK"
+    if h["reported"]:
+        assert h["now"]["source"].endswith("/ras") and h["now"]["ue"] >= 0
+    buf.free()
+
+
 def test_pluggable_allocator_subprocess():
     code = (
         "import sys; sys.path.insert(0, %r)\n"

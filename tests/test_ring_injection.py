@@ -154,3 +154,19 @@ def test_quiesce_blocks_new_faults(fake_rt):
 def test_lock_checker_detects_inversion(fake_rt):
     assert lib.lock_check_self_test() == 1
     lib.reset_lock_violations()  # the fixture asserts zero afterwards
+
+
+def test_ecc_uncorrectable_error_is_fatal(fake_rt):
+    """RAS counters are baselined at init; correctable errors are reported only,
+    a new uncorrectable (ECC or xGMI link) error makes the runtime FATAL - the
+    reference's ECC notifier check after pushes (uvm_gpu.c:1328-1354)."""
+    h = lib.device_health(0)
+    assert h["reported"] and h["status"] == "OK" and h["now"]["source"] == "fake"
+    lib.inject_ras(0, 5, 0)            # correctable: counted, not fatal
+    h = lib.device_health(0)
+    assert h["now"]["ce"] == 5 and h["status"] == "OK"
+    lib.inject_ras(0, 5, 1)            # one uncorrectable xGMI link error
+    assert lib.device_health(0)["status"] == "FATAL"
+    assert "xGMI" in lib.fatal_reason()
+    with pytest.raises(Exception):
+        rt.malloc_managed(1 << 20, "after-ecc")  # every later operation fails fast
