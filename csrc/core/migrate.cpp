@@ -1549,9 +1549,27 @@ size_t Runtime::poll_device_faults(int dev) {
   size_t n = drain_fault_records(dev, &recs, fb.entries);
   std::vector<FaultEntry> faults;
   std::vector<std::pair<uint64_t, uint32_t>> remote_hits;
+  // Per-channel attribution (record.proc = dev | channel << 16) and the
+  // precise cancel of faults no service can satisfy.
+  std::vector<std::pair<uint16_t, int>> per_channel;  // (channel, 0 fault / 1 remote / 2 fatal)
   for (const DeviceFaultRecord& rec : recs) {
+    const uint16_t ch = (uint16_t)(rec.proc >> 16);
     if (rec.kind == 1) {
       remote_hits.emplace_back(rec.range_id, rec.block);
+      if (ch) per_channel.emplace_back(ch, 1);
+      continue;
+    }
+    bool valid;
+    {
+      std::shared_lock<OrderedRWLock> vg(vs_.lock);
+      Range* r = vs_.by_id_locked(rec.range_id);
+      valid = r && r->type == RangeType::MANAGED && rec.block < r->nblocks;
+    }
+    if (!valid) {
+      // A fault on a freed range / past its end: fatal for the faulting
+      // channel, not serviced (the kernel's gate times out or is cancelled).
+      if (ch) per_channel.emplace_back(ch, 2);
+      tools_event(ToolsEventType::FatalFault, Cause::User, Loc{}, Loc::gpu(dev), dev, 0, 0, rec.range_id);
       continue;
     }
     FaultEntry f;
@@ -1559,9 +1577,24 @@ size_t Runtime::poll_device_faults(int dev) {
     const bool whole = rec.page == kFaultWholeBlock;  // a gate needs the whole block in HBM
     f.offset = ((uint64_t)rec.block << kBlockShift) + (whole ? 0 : ((uint64_t)rec.page << kPageShift));
     f.bytes = whole ? kBlockSize : kPageSize;
-    f.proc = (int)rec.proc;
+    f.proc = (int)(rec.proc & 0xffff);
+    f.channel = ch;
     f.access = rec.access == 2 ? Access::WRITE : Access::READ;
     faults.push_back(f);
+    if (ch) per_channel.emplace_back(ch, 0);
+  }
+  if (!per_channel.empty()) {
+    std::lock_guard<std::mutex> g(channels_m_);
+    for (auto& pc : per_channel) {
+      if (pc.first > channels_.size() || !channels_[pc.first - 1].id) continue;
+      Channel& c = channels_[pc.first - 1];
+      if (pc.second == 0) c.faults++;
+      else if (pc.second == 1) c.remote_accesses++;
+      else {
+        c.fatal_faults++;
+        c.error = Status::INVALID_ARGUMENT;
+      }
+    }
   }
   Tools::get().inc(Counter::GpuPageFaultCount, faults.size());
   // Access counters (uvm_gpu_access_counters.c:1617): migrate hot remote blocks.

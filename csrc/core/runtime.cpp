@@ -957,6 +957,44 @@ Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
   return Status::OK;
 }
 
+uint16_t Runtime::register_channel(int dev, void* stream, const std::string& name) {
+  if (!is_local(dev)) return 0;
+  std::lock_guard<std::mutex> g(channels_m_);
+  for (auto& c : channels_)
+    if (c.id && c.dev == dev && c.stream == stream) return c.id;
+  size_t slot = 0;
+  while (slot < channels_.size() && channels_[slot].id) ++slot;
+  if (slot >= 0xffff) return 0;
+  if (slot == channels_.size()) channels_.emplace_back();
+  Channel c;
+  c.id = (uint16_t)(slot + 1);
+  c.dev = dev;
+  c.stream = stream;
+  c.name = name;
+  channels_[slot] = c;
+  return c.id;
+}
+
+void Runtime::unregister_channel(uint16_t id) {
+  std::lock_guard<std::mutex> g(channels_m_);
+  if (id && id <= channels_.size()) channels_[id - 1] = Channel{};
+}
+
+uint32_t Runtime::fault_client(int dev, void* stream) {
+  std::lock_guard<std::mutex> g(channels_m_);
+  for (auto& c : channels_)
+    if (c.id && c.dev == dev && c.stream == stream) return (uint32_t)dev | ((uint32_t)c.id << 16);
+  return (uint32_t)dev;
+}
+
+std::vector<Runtime::Channel> Runtime::channels() {
+  std::lock_guard<std::mutex> g(channels_m_);
+  std::vector<Channel> v;
+  for (auto& c : channels_)
+    if (c.id) v.push_back(c);
+  return v;
+}
+
 Status Runtime::check_health(int dev, bool force) {
   if (!is_local(dev)) return Status::INVALID_ARGUMENT;
   Device& d = *devs_[dev];

@@ -45,6 +45,7 @@ struct FaultEntry {
   uint64_t offset = 0;
   uint64_t bytes = 0;
   int proc = 0;             // GPU id or kCpuProc
+  uint16_t channel = 0;     // user channel of the faulting kernel (0 = none)
   Access access = Access::READ;
   uint64_t ts_ns = 0;
   // filled by preprocessing
@@ -216,6 +217,26 @@ class Runtime {
   Status checkpoint_save(const std::string& path, bool with_data);
   Status checkpoint_load(const std::string& path, bool with_data, std::vector<uint64_t>* new_range_ids);
 
+  // ---- user channels (uvm_user_channel.c / the channel+TSG attribution of
+  // uvm_gpu_replayable_faults.c): a stream registered as a channel gets the
+  // device faults of kernels it runs attributed to it (the producers encode
+  // dev | channel << 16 in the record's proc field). A fault that cannot be
+  // serviced (freed range, address past its end) is fatal for its channel only:
+  // the channel is marked errored (the precise-cancel target), the runtime and
+  // other channels carry on.
+  struct Channel {
+    uint16_t id = 0;
+    int dev = 0;
+    void* stream = nullptr;
+    std::string name;
+    uint64_t faults = 0, remote_accesses = 0, fatal_faults = 0;
+    Status error = Status::OK;
+  };
+  uint16_t register_channel(int dev, void* stream, const std::string& name);
+  void unregister_channel(uint16_t id);
+  uint32_t fault_client(int dev, void* stream);  // the proc value a producer on `stream` records
+  std::vector<Channel> channels();
+
   // ---- GPU health (ECC / xGMI link errors, rate-limited sysfs reads)
   // OK, or FATAL once an uncorrectable error appeared since init. `force`
   // skips the rate limit (min_interval_ms).
@@ -296,6 +317,8 @@ class Runtime {
   std::mutex fs_m_;
   OrderedMutex pm_{LockOrder::GLOBAL_PM};
   std::vector<int> perf_subs_;  // perf-module subscriptions on the tools bus
+  std::mutex channels_m_;
+  std::vector<Channel> channels_;  // slot id - 1 (id 0 = no channel); unregistered slots keep id 0
 };
 
 // Scoped profiler range around a runtime operation (no-op on the fake backend).

@@ -358,7 +358,8 @@ PYBIND11_MODULE(_ogkm, m) {
     DeviceFaultBuffer& fb = r->dev(dev).fault_buf;
     KFaultBuf kfb{fb.hdr, fb.recs, fb.entries};
     hipError_t e = launch_managed_gather(t->entries, rg->id, (const int64_t*)rows_dptr, nrows, row_bytes,
-                                         (void*)out_dptr, kfb, (uint32_t)dev, (hipStream_t)stream);
+                                         (void*)out_dptr, kfb, r->fault_client(dev, (void*)stream),
+                                         (hipStream_t)stream);
     if (e != hipSuccess) throw StatusError(std::string("managed_gather launch: ") + hipGetErrorString(e));
   });
   // Fault gate: a one-wave kernel that stalls the stream until blocks covering
@@ -376,7 +377,8 @@ PYBIND11_MODULE(_ogkm, m) {
     DeviceFaultBuffer& fb = r->dev(dev).fault_buf;
     KFaultBuf kfb{fb.hdr, fb.recs, fb.entries};
     uint32_t b0 = (uint32_t)(off >> kBlockShift), b1 = (uint32_t)((off + len - 1) >> kBlockShift);
-    hipError_t e = launch_fault_gate(t->entries, rg->id, b0, b1 - b0 + 1, kfb, (uint32_t)dev, write ? 2 : 1,
+    hipError_t e = launch_fault_gate(t->entries, rg->id, b0, b1 - b0 + 1, kfb, r->fault_client(dev, (void*)stream),
+                                     write ? 2 : 1,
                                      timeout_ms * 1000u, (uint32_t*)status_dptr, (hipStream_t)stream);
     if (e != hipSuccess) throw StatusError(std::string("fault_gate launch: ") + hipGetErrorString(e));
   }, py::arg("id"), py::arg("off"), py::arg("len"), py::arg("dev"), py::arg("stream"), py::arg("status_dptr"),
@@ -402,6 +404,29 @@ PYBIND11_MODULE(_ogkm, m) {
     KFaultBuf kfb{fb.hdr, fb.recs, fb.entries};
     hipError_t e = launch_fault_stress(kfb, waves, per_lane, (uint32_t*)gave_up_dptr, (hipStream_t)stream);
     if (e != hipSuccess) throw StatusError(std::string("fault_stress launch: ") + hipGetErrorString(e));
+  });
+  m.def("register_channel", [](int dev, uint64_t stream, const std::string& name) {
+    uint16_t id = rt()->register_channel(dev, (void*)stream, name);
+    if (!id) throw StatusError("register_channel: not a local GPU or no channel slot left");
+    return id;
+  }, py::arg("dev"), py::arg("stream"), py::arg("name") = "");
+  m.def("unregister_channel", [](uint16_t id) { rt()->unregister_channel(id); });
+  m.def("fault_client", [](int dev, uint64_t stream) { return rt()->fault_client(dev, (void*)stream); });
+  m.def("channels", [] {
+    py::list out;
+    for (auto& c : rt()->channels()) {
+      py::dict d;
+      d["id"] = c.id;
+      d["dev"] = c.dev;
+      d["stream"] = (uint64_t)c.stream;
+      d["name"] = c.name;
+      d["faults"] = c.faults;
+      d["remote_accesses"] = c.remote_accesses;
+      d["fatal_faults"] = c.fatal_faults;
+      d["error"] = status_str(c.error);
+      out.append(d);
+    }
+    return out;
   });
   // Host-side producer (the device protocol): fake backend / tests.
   m.def("inject_device_faults", [](int dev, const std::vector<std::tuple<uint64_t, uint32_t, uint32_t, uint32_t,

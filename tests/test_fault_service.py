@@ -148,3 +148,32 @@ def test_access_counters_on_remote_leases_promote_hot_block(fake_rt):
     assert lib.stats()["access_counter_migrations"] >= 2
     assert all(any(r["tier"] == "gpu" for r in b.residency(o)["resident_on"]) for o in (0, 2 * MB))
     b.free()
+
+
+def test_user_channel_attribution_and_fatal_cancel(fake_rt):
+    """Faults carry their channel (proc = dev | channel << 16, what the HIP
+    producers record for a registered stream): per-channel counts, and a fault on
+    a freed range is fatal for its channel only (uvm_user_channel.c +
+    precise cancel, uvm_gpu_replayable_faults.c:2495-2875)."""
+    b = rt.malloc_managed(4 * MB, "chan")
+    b.write(torch.ones(4 * MB, dtype=torch.uint8))
+    a_id = lib.register_channel(0, 0x1000, "decode")
+    b_id = lib.register_channel(0, 0x2000, "prefill")
+    assert lib.register_channel(0, 0x1000, "again") == a_id  # one channel per stream
+    assert lib.fault_client(0, 0x1000) == a_id << 16 and lib.fault_client(0, 0x3000) == 0
+    gone = rt.malloc_managed(2 * MB, "gone")
+    gone_id = gone.id
+    gone.free()
+    _inject([(b.id, 0, 1, 1, 0, a_id << 16), (b.id, 1, 2, 1, 0, a_id << 16),
+             (b.id, 1, 0, 1, 1, b_id << 16),          # remote access (access counter)
+             (gone_id, 0, 0, 1, 0, b_id << 16)])      # fault on a freed range
+    lib.poll_device_faults(0)
+    ch = {c["name"]: c for c in lib.channels()}
+    assert ch["decode"]["faults"] == 2 and ch["decode"]["error"] == "OK"
+    assert ch["prefill"]["remote_accesses"] == 1 and ch["prefill"]["fatal_faults"] == 1
+    assert ch["prefill"]["error"] != "OK"
+    assert lib.global_status() == "OK"                 # the runtime carries on
+    assert any(r["tier"] == "gpu" for r in b.residency(0)["resident_on"])
+    lib.unregister_channel(b_id)
+    assert [c["name"] for c in lib.channels()] == ["decode"]
+    b.free()

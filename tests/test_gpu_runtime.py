@@ -160,6 +160,26 @@ def test_managed_gather_records_faults(gpu_rt):
     b.free()
 
 
+def test_managed_gather_faults_attributed_to_channel(gpu_rt):
+    """A stream registered as a user channel: the records k_managed_gather
+    writes from it carry the channel, the service counts them per channel."""
+    rows, dim = 1024, 1024
+    b = rt.malloc_managed(rows * dim * 2, "emb-ch")
+    b.write(torch.randn(rows, dim, dtype=torch.bfloat16))
+    s = torch.cuda.Stream()
+    cid = lib.register_channel(0, s.cuda_stream, "gather-stream")
+    idx = torch.tensor([1, 2, 3], dtype=torch.int64, device="cuda")
+    out = torch.empty(3, dim, dtype=torch.bfloat16, device="cuda")
+    torch.cuda.synchronize()
+    lib.managed_gather(b.id, idx.data_ptr(), 3, dim * 2, out.data_ptr(), 0, s.cuda_stream)
+    s.synchronize()
+    assert lib.poll_device_faults(0) == 3
+    ch = [c for c in lib.channels() if c["id"] == cid][0]
+    assert ch["remote_accesses"] == 3 and ch["error"] == "OK"
+    lib.unregister_channel(cid)
+    b.free()
+
+
 def test_cxl_dma_roundtrip(gpu_rt):
     from ogkm import cxl
 
