@@ -26,6 +26,7 @@ void ChunkArena::init_chunks(uint64_t base, uint32_t n) {
   if (n) free_runs_[0] = n;
   st_ = Stats{};
   st_.capacity = (uint64_t)n << kBlockShift;
+  active_limit_ = (uint32_t)((uint64_t)n * (uint64_t)std::max<int64_t>(0, config().perf_workingset_active_pct) / 100);
 }
 
 int64_t ChunkArena::chunk_of(uint64_t addr) const {
@@ -148,12 +149,15 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
     // then chunks whose data prefers this tier.
     // Within a list, the oldest few candidates compete on recency (prefetched
     // chunks carry a recency bonus and lose to genuinely cold data).
-    for (int list : {1, 2, 3}) {
+    // Workingset-protected (active) chunks go only when nothing inactive is left.
+    for (int pass = 0; pass < 6; ++pass) {
+      const int list = 1 + pass % 3;
+      const bool allow_active = pass >= 3;
       int32_t best = -1;
       int scanned = 0;
       for (int32_t i = head_[list]; i >= 0 && scanned < 64; i = chunks_[i].next) {
         ChunkInfo& c = chunks_[i];
-        if (c.state != ChunkState::ALLOCATED || c.pin_count != 0) continue;
+        if (c.state != ChunkState::ALLOCATED || c.pin_count != 0 || (c.active && !allow_active)) continue;
         ++scanned;
         if (best < 0 || c.last_use < chunks_[best].last_use) best = i;
       }
@@ -181,7 +185,7 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
   auto cost_of = [&](uint32_t i) -> uint64_t {
     const ChunkInfo& c = chunks_[i];
     if (c.state == ChunkState::FREE) return 0;
-    return c.last_use + (c.list == 3 ? (1ull << 62) : 0);
+    return c.last_use + (c.list == 3 ? (1ull << 62) : 0) + (c.active ? (1ull << 61) : 0);
   };
   for (uint32_t i = 0; i < nchunks_; ++i) {
     ChunkInfo& c = chunks_[i];
@@ -232,6 +236,7 @@ void ChunkArena::evicted(uint32_t i) {
   RT_ASSERT_RELEASE(c.state == ChunkState::EVICTING);
   c.state = ChunkState::RESERVED;
   c.owner = nullptr;
+  deactivate(c);
   st_.allocated -= kBlockSize;
   st_.evictions++;
 }
@@ -282,6 +287,7 @@ void ChunkArena::free(uint32_t first, uint32_t n) {
     c.owner = nullptr;
     c.pin_count = 0;
     c.zeroed = false;
+    deactivate(c);
   }
   add_run(first, n);
   st_.allocated -= (uint64_t)n << kBlockShift;
@@ -298,13 +304,26 @@ Block* ChunkArena::owner(uint32_t i) {
   return chunks_[i].owner;
 }
 
-void ChunkArena::touch(uint32_t i, bool has_data, bool preferred, bool prefetched) {
+void ChunkArena::touch(uint32_t i, bool has_data, bool preferred, bool prefetched, uint64_t refault_key,
+                       uint64_t evicted_at) {
   std::lock_guard<OrderedMutex> g(m_);
   ChunkInfo& c = chunks_[i];
   if (c.state != ChunkState::ALLOCATED) return;
   c.last_use = ++clock_ + (prefetched ? kPrefetchBoost : 0);
   // A chunk keeps its preferred status until it loses its data.
   bool pref = has_data && (preferred || c.list == 3);
+  if (!has_data) {
+    deactivate(c);
+  } else if (refault_key && preferred && !c.active && st_.active + (st_.pinned >> kBlockShift) < active_limit_) {
+    // (pinned chunks - leased / allocator memory - count against the protected share)
+    const uint64_t distance = st_.evictions > evicted_at ? st_.evictions - evicted_at : 0;
+    const uint64_t ws = distance + nchunks_;  // estimated cyclic working set, in chunks
+    const uint64_t h = (refault_key * 0x9E3779B97F4A7C15ull) >> 44;  // 20-bit bucket
+    if (h * ws < ((uint64_t)active_limit_ << 20)) {
+      c.active = true;
+      st_.active++;
+    }
+  }
   lru_remove(i);
   lru_push_tail(i, !has_data ? 1 : (pref ? 3 : 2));
 }

@@ -112,7 +112,9 @@ Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool 
 void Runtime::touch_residency(Block* b, Residency* r, bool prefetched) {
   if (!r || r->chunk < 0) return;
   bool pref = b->policy.has_preferred && b->policy.preferred == r->loc;
-  r->arena->touch((uint32_t)r->chunk, !r->resident.empty(), pref, prefetched);
+  const bool refault = r->loc.is_gpu() && b->gpu_evictions > 0;
+  r->arena->touch((uint32_t)r->chunk, !r->resident.empty(), pref, prefetched, refault ? b->range->id + 1 : 0,
+                  b->gpu_evicted_at);
 }
 
 // Populate: give block b a chunk at location dst (block lock held).
@@ -629,6 +631,10 @@ Status Runtime::evict_chunk(ChunkArena* a, uint32_t i) {
       // evicting allocator, fenced on the copy-out.
       Tracker pend = b->tracker;
       shootdown(b, r);
+      if (from.is_gpu()) {
+        b->gpu_evictions++;
+        b->gpu_evicted_at = a->evictions();
+      }
       b->drop(from);
       c.cpu_refresh.push_back(b);
       for (auto& f : pend.fences()) a->add_reuse_fence(i, f);

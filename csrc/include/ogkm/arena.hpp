@@ -40,6 +40,7 @@ struct ChunkInfo {
   ChunkState state = ChunkState::FREE;
   uint8_t list = 0;      // 0 none, 1 unused, 2 used, 3 used + preferred here
   bool zeroed = false;
+  bool active = false;   // workingset-protected (a refaulted block's data): evicted after every inactive chunk
   uint32_t pin_count = 0;
   Block* owner = nullptr;
   int32_t prev = -1, next = -1;  // LRU links
@@ -85,7 +86,24 @@ class ChunkArena {
   // `prefetched`: the data was brought in ahead of its use - it ranks as newer than
   // every chunk that has actually been used until its first access (otherwise a
   // layer-ahead prefetch would be the LRU victim of the next prefetch).
-  void touch(uint32_t i, bool has_data, bool preferred = false, bool prefetched = false);
+  // `refault`: the owner block's data was evicted from this tier before and is
+  // back - with `preferred`, the chunk joins the protected active set while that
+  // set is below perf_workingset_active_pct of the arena (the refault-distance
+  // workingset idea: a cyclic scan larger than the arena keeps a stable subset
+  // resident instead of evicting every block just before its next use).
+  //
+  // Admission is spread over the scan: the refault distance (evictions since
+  // the block left, + the arena size) estimates the cyclic working set W, and a
+  // unit (`refault_key`, e.g. its range id - a unit is all in or all out) is
+  // admitted when its hash falls in the first active_limit / W of the hash
+  // space, so resident units interleave with streamed ones over the cycle (the
+  // link keeps streaming behind them) instead of forming one long stretch.
+  void touch(uint32_t i, bool has_data, bool preferred = false, bool prefetched = false, uint64_t refault_key = 0,
+             uint64_t evicted_at = 0);
+  uint64_t evictions() {
+    std::lock_guard<OrderedMutex> g(m_);
+    return st_.evictions;
+  }
   void pin(uint32_t i);
   void unpin(uint32_t i);
   bool pinned(uint32_t i);
@@ -94,7 +112,7 @@ class ChunkArena {
 
   struct Stats {
     uint64_t capacity = 0, allocated = 0, peak = 0, pinned = 0, evictions = 0, allocs = 0, frees = 0,
-             used_list = 0, unused_list = 0, reservations = 0;
+             used_list = 0, unused_list = 0, reservations = 0, active = 0;
   };
   Stats stats();
   uint32_t free_chunks();
@@ -122,6 +140,13 @@ class ChunkArena {
   std::map<uint32_t, uint32_t> free_runs_;  // start -> len
   int32_t head_[4] = {-1, -1, -1, -1}, tail_[4] = {-1, -1, -1, -1};
   uint64_t clock_ = 0;
+  uint32_t active_limit_ = 0;
+  void deactivate(ChunkInfo& c) {
+    if (c.active) {
+      c.active = false;
+      st_.active--;
+    }
+  }
   Stats st_;
 };
 

@@ -94,6 +94,8 @@ class Block {
   int64_t cpu_chunk = -1;
   int64_t stable_chunk = -1;   // HBM chunk VMM-mapped at the stable device VA (-1 = none)
   uint32_t lease_pins = 0;
+  uint32_t gpu_evictions = 0;  // times an HBM copy of this block was evicted (refault detection)
+  uint64_t gpu_evicted_at = 0; // the HBM arena's eviction count when it last was (refault distance)
   uint32_t user_pins = 0;      // range-group / explicit pins (non-migratable)
   uint64_t last_access_ns = 0;
   uint32_t faults_by_proc[kMaxGpus + 1] = {0};

@@ -594,6 +594,7 @@ PYBIND11_MODULE(_ogkm, m) {
     d["frees"] = s.frees;
     d["used_list"] = s.used_list;
     d["unused_list"] = s.unused_list;
+    d["active"] = s.active;
     d["free_chunks"] = a->free_chunks();
     d["nchunks"] = a->nchunks();
     d["base"] = a->base();

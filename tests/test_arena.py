@@ -124,3 +124,41 @@ def test_random_stress_consistency(fake_rt):
     for b, _ in live.values():
         b.free()
     assert lib.arena_stats(0, 0)["allocated"] == 0
+
+
+def _cyclic_htd_bytes(active_pct: int) -> int:
+    """H2D bytes of the last of 4 cyclic passes over 8 x 8 MB GPU-preferred,
+    read-mostly ranges (64 MB) on a 32 MB arena - the access pattern of a model
+    streamed in layer order with no residency plan (bench --planner off)."""
+    lib.configure("perf_workingset_active_pct", active_pct)
+    lib.init_device(0, 32 * MB)
+    bufs = []
+    for i in range(8):
+        b = rt.malloc_managed(8 * MB, f"cyc{i}")
+        b.set_preferred_location("gpu:0")
+        b.set_read_mostly(True)
+        b.write(torch.full((8 * MB,), i, dtype=torch.uint8))
+        bufs.append(b)
+    last = 0
+    for p in range(4):
+        s0 = lib.stats()["bytes_xfer_htd"]
+        for b in bufs:
+            lease = b.acquire(0, rt.READ)
+            lease.wait(0)
+            lease.release(0)
+        last = lib.stats()["bytes_xfer_htd"] - s0
+    active = lib.arena_stats(0, 0)["active"]
+    for b in bufs:
+        b.free()
+    return last, active
+
+
+def test_workingset_protects_refaulted_blocks_under_cyclic_scan(fake_rt):
+    """Plain LRU evicts every block just before its next use in a cyclic scan
+    larger than HBM (every pass streams all 64 MB); protecting refaulted
+    GPU-preferred blocks keeps a stable subset resident."""
+    lru, lru_active = _cyclic_htd_bytes(0)
+    ws, ws_active = _cyclic_htd_bytes(50)
+    assert lru_active == 0 and lru == 64 * MB
+    assert 0 < ws_active <= 8                     # 50% of 16 chunks
+    assert ws <= 48 * MB, (ws, lru)               # at least 2 of 8 ranges stay resident
