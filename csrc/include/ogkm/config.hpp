@@ -50,7 +50,7 @@ namespace ogkm {
   /* physical memory managers */                                                                     \
   X(global_oversubscription, 1, "allow eviction from HBM under pressure")                            \
   X(perf_pma_batch_nonpinned_order, 6, "log2 of chunks evicted per batch")                           \
-  X(perf_workingset_active_pct, 90, "HBM chunks of refaulted GPU-preferred blocks (plus pinned chunks) protected from eviction, percent of the arena (0 = plain LRU)") \
+  X(perf_workingset_active_pct, 95, "HBM chunks of refaulted GPU-preferred blocks (plus pinned chunks) protected from eviction, percent of the arena (0 = plain LRU)") \
   X(hbm_budget_mb, 0, "per-GPU HBM budget for the arena in MB (0 = 90% of free)")                   \
   X(hbm_provider, 0, "0=slab (one hipMalloc) 1=vmm (hipMemCreate handles, enables stable VA)")       \
   X(torch_alloc_managed_min_mb, 0, "pluggable allocator: allocations >= this many MB are evictable stable-VA managed ranges (0 = off; needs hbm_provider=1)") \
