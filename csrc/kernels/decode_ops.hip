@@ -206,6 +206,174 @@ __global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a) {
   }
 }
 
+// Wave-split decode attention on the matrix cores (the default for hd 64 / 128).
+// The workgroup's 256 tokens are four independent 64-token runs, one per wave:
+// no block-wide barrier sits between the phases, and LDS holds only the
+// probabilities and the four wave partials (24 KB for a group of 8 - the lane-
+// per-token kernel above needs 56 KB: 2 workgroups per CU).
+//  * Q.K is a [64 tokens x hd] . [hd x 16 heads] GEMM per wave on
+//    v_mfma_f32_16x16x32_bf16: the A fragment of a 16-token tile is one 16 B
+//    load per lane straight from the K rows (lane l: token l&15, dims
+//    8(l>>4)..+8 of the 32-dim step - every load a fully used 1 KB wave
+//    access), B is the query group (heads padded to 16), and all 16 (hd 128)
+//    K fragments are in flight before the first MFMA.
+//  * D lands as lane l = head l&15, tokens 4(l>>4)+r of each tile: the softmax
+//    max / sum over a head's 64 tokens is a 16-value local reduction plus two
+//    xor shuffles for ALL heads at once (the lane-per-token kernel shuffles per
+//    head).
+//  * P.V (contraction over tokens, V rows are dim-contiguous) stays on the
+//    vector ALUs: half a wave per token, 4 dims per lane, p broadcast from LDS.
+// The four wave partials are merged (log-sum-exp) into the split partial the
+// combine kernel reads (same part_o / part_ml layout as k_attn_decode).
+typedef __bf16 attn_bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float attn_f32x4_t __attribute__((ext_vector_type(4)));
+
+template <int HD, int G>
+__global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
+  constexpr int KS = HD / 32;         // 32-dim MFMA steps
+  constexpr int DPV = HD / 32;        // p.v dims per lane
+  constexpr int PU = G <= 4 ? 8 : G <= 8 ? 4 : 2;
+  static_assert((HD == 64 || HD == 128) && G <= 16, "shape");
+  extern __shared__ float smem[];
+  const uint32_t g = a.hq / a.hkv;    // <= G
+  float* ps = smem;                   // [4 waves][g][64] scores -> probabilities
+  float* po = smem + 4 * g * 64;      // [4 waves][g][HD] unnormalised outputs
+  __shared__ float wm[4][G], wl[4][G];
+  const uint32_t split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t wt0 = split * kAttnSplit + wave * 64;
+  const int32_t wn = (int32_t)a.len - (int32_t)wt0 < 64 ? (int32_t)a.len - (int32_t)wt0 : 64;
+  float* wps = ps + wave * g * 64;
+  float* wpo = po + wave * g * HD;
+  if (wn <= 0) {  // this wave's tokens are past the context: an empty partial
+    for (uint32_t e = lane; e < g * HD; e += 64) wpo[e] = 0.f;
+    if (lane < g) {
+      wm[wave][lane] = -INFINITY;
+      wl[wave][lane] = 0.f;
+    }
+  } else {
+    const uint16_t* kbase = a.cache + ((uint64_t)b * a.hkv + kvh) * (uint64_t)a.T * HD;
+    const uint16_t* vbase = a.cache + (((uint64_t)a.B + b) * a.hkv + kvh) * (uint64_t)a.T * HD;
+    const uint32_t col = lane & 15, quad = lane >> 4;
+    // B fragments: the query group, head `col` (zero past the group)
+    uint4 qb[KS];
+    const uint16_t* qr = a.q + ((uint64_t)b * a.hq + kvh * g + (col < g ? col : 0)) * HD + 8 * quad;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      qb[k] = *reinterpret_cast<const uint4*>(qr + 32 * k);
+      if (col >= g) qb[k] = uint4{0u, 0u, 0u, 0u};
+    }
+    // A fragments: 4 token tiles x KS dim steps, all loads issued up front
+    // (rows past the context are clamped to the last one and masked below)
+    uint4 ka[4][KS];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int32_t tok = t * 16 + (int32_t)col;
+      const uint32_t row = wt0 + (uint32_t)(tok < wn ? tok : wn - 1);
+      const uint16_t* kr = kbase + (uint64_t)row * HD + 8 * quad;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) ka[t][k] = *reinterpret_cast<const uint4*>(kr + 32 * k);
+    }
+    attn_f32x4_t sc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sc[t] = attn_f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+        sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(attn_bf16x8_t, ka[t][k]),
+                                                        __builtin_bit_cast(attn_bf16x8_t, qb[k]), sc[t], 0, 0, 0);
+    }
+    // softmax partials: lane = head col, tokens t*16 + 4*quad + r
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int32_t tok = t * 16 + 4 * (int32_t)quad + r;
+        const float v = tok < wn ? sc[t][r] * a.scale : -INFINITY;
+        sc[t][r] = v;
+        m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __expf(sc[t][r] - m);  // masked tokens: exp(-inf) = 0
+        l += p;
+        if (col < g) wps[col * 64 + t * 16 + 4 * quad + r] = p;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (quad == 0 && col < g) {
+      wm[wave][col] = m;
+      wl[wave][col] = l;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // P.V: half a wave per token, DPV dims per lane
+    const uint32_t half = lane >> 5, d0 = (lane & 31) * DPV;
+    float o[G][DPV];
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int j = 0; j < DPV; ++j) o[h][j] = 0.f;
+#pragma unroll PU
+    for (int32_t t = (int32_t)half; t < wn; t += 2) {
+      const uint16_t* vr = vbase + (uint64_t)(wt0 + t) * HD + d0;
+      float vf[DPV];
+      if constexpr (DPV == 4) {
+        const uint2 w = *reinterpret_cast<const uint2*>(vr);
+        vf[0] = dbf((uint16_t)w.x);
+        vf[1] = dbf((uint16_t)(w.x >> 16));
+        vf[2] = dbf((uint16_t)w.y);
+        vf[3] = dbf((uint16_t)(w.y >> 16));
+      } else {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(vr);
+        vf[0] = dbf((uint16_t)w);
+        vf[1] = dbf((uint16_t)(w >> 16));
+      }
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        const float p = (uint32_t)h < g ? wps[h * 64 + t] : 0.f;
+#pragma unroll
+        for (int j = 0; j < DPV; ++j) o[h][j] += p * vf[j];
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+#pragma unroll
+      for (int j = 0; j < DPV; ++j) {
+        const float x = o[h][j] + __shfl_xor(o[h][j], 32, 64);
+        if (half == 0 && (uint32_t)h < g) wpo[h * HD + d0 + j] = x;
+      }
+    }
+  }
+  __syncthreads();
+  // merge the four wave partials into this split's partial
+  for (uint32_t e = threadIdx.x; e < g * HD; e += 256) {
+    const uint32_t h = e / HD, d = e - h * HD;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, wm[w][h]);
+    float acc = 0.f, l = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = wm[w][h] == -INFINITY ? 0.f : __expf(wm[w][h] - M);
+      acc += f * po[(w * g + h) * HD + d];
+      l += f * wl[w][h];
+    }
+    const uint64_t row = ((uint64_t)b * a.hq + kvh * g + h) * a.nsplit + split;
+    a.part_o[row * HD + d] = acc;
+    if (d == 0) {
+      a.part_ml[row * 2] = M;
+      a.part_ml[row * 2 + 1] = l;
+    }
+  }
+}
+
 // One workgroup of hd threads per (b, q head): merge the splits.
 __global__ void k_attn_combine(AttnArgs a) {
   const uint32_t bh = blockIdx.x;  // b * hq + h
@@ -242,7 +410,25 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
       !a.len || a.len > a.T)
     return hipErrorInvalidValue;
   if (a.nsplit != (a.len + kAttnSplit - 1) / kAttnSplit) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_attn_decode, dim3(a.nsplit, a.hkv, a.B), dim3(256), 0, s, a);
+  const uint32_t g = a.hq / a.hkv;
+  const uint32_t gg = g <= 4 ? 4 : g <= 8 ? 8 : 16;
+  const dim3 grid(a.nsplit, a.hkv, a.B);
+  const size_t lds = (size_t)4 * g * (64 + a.hd) * sizeof(float);
+  if (a.hd == 128 || a.hd == 64) {
+#define OGKM_ATTN_WS(HD, L) hipLaunchKernelGGL((k_attn_decode_ws<HD, L>), grid, dim3(256), lds, s, a)
+    if (a.hd == 128) {
+      if (gg == 4) OGKM_ATTN_WS(128, 4);
+      else if (gg == 8) OGKM_ATTN_WS(128, 8);
+      else OGKM_ATTN_WS(128, 16);
+    } else {
+      if (gg == 4) OGKM_ATTN_WS(64, 4);
+      else if (gg == 8) OGKM_ATTN_WS(64, 8);
+      else OGKM_ATTN_WS(64, 16);
+    }
+#undef OGKM_ATTN_WS
+  } else {
+    hipLaunchKernelGGL(k_attn_decode, grid, dim3(256), 0, s, a);
+  }
   hipLaunchKernelGGL(k_attn_combine, dim3(a.B * a.hq), dim3(a.hd < 64 ? 64 : a.hd), 0, s, a);
   return hipGetLastError();
 }

@@ -43,8 +43,8 @@ def _check_rope_kv(gpu):
     assert cd[:, :, :, pos + 1:].abs().sum() == 0 and cd[:, :, :, :pos].abs().sum() == 0
 
 
-def _check_attention(gpu, length, hq=16, hkv=2):
-    B, hd, T = 2, 128, 700
+def _check_attention(gpu, length, hq=16, hkv=2, hd=128):
+    B, T = 2, 700
     q = torch.randn(B, hq, hd).to(torch.bfloat16)
     cache = torch.randn(2, B, hkv, T, hd).to(torch.bfloat16)
     want = D.gqa_decode_attention(q.float(), cache[0].float(), cache[1].float(), length)
@@ -95,3 +95,12 @@ def test_attention_one_kv_head_cpu(fake_rt, hq, hkv, length):
 @pytest.mark.parametrize("length", [1, 255, 256, 257, 700])
 def test_attention_one_kv_head_gpu(gpu_rt, hq, hkv, length):
     _check_attention(True, length, hq, hkv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (16, 4, 64), (8, 1, 64), (4, 4, 128), (12, 2, 128)])
+@pytest.mark.parametrize("length", [1, 63, 65, 700])
+def test_attention_group_shapes_gpu(gpu_rt, hq, hkv, hd, length):
+    """Every group-size / head-dim instantiation of the wave-split kernel
+    (group 1..16 rounded up to 4 / 8 / 16, hd 64 / 128), partial waves included."""
+    _check_attention(True, length, hq, hkv, hd)

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Decode-attention microbenchmark (k_attn_decode_ws + combine): one layer's KV
+at the bench shapes, time per call and effective KV-read bandwidth.
+    python tools/bench_attn.py"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import ogkm  # noqa: E402,F401
+from ogkm import rt  # noqa: E402
+from ogkm.ops import fused  # noqa: E402
+
+SHAPES = {  # name: (B, hq, hkv, hd, len)
+    "8b": (64, 32, 8, 128, 1025),
+    "70b": (64, 64, 8, 128, 1025),
+    "70b-tp8": (64, 8, 1, 128, 1025),
+    "405b-tp8": (64, 16, 1, 128, 1025),
+}
+
+
+def main() -> None:
+    rt.init("hip")
+    iters = int(os.environ.get("ITERS", "50"))
+    for name, (B, hq, hkv, hd, L) in SHAPES.items():
+        T = L
+        q = torch.randn(B, hq, hd, device="cuda").to(torch.bfloat16)
+        cache = torch.randn(2, B, hkv, T, hd, device="cuda").to(torch.bfloat16)
+        for _ in range(3):
+            fused.attention(q, cache, L)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fused.attention(q, cache, L)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / iters
+        gb = 2 * B * hkv * L * hd * 2 / 1e9
+        print(f"{name:9s} B={B} hq={hq} hkv={hkv} hd={hd} len={L}: {us:8.1f} us  KV {gb * 1e3:7.1f} MB  "
+              f"{gb / (us * 1e-6):7.0f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
