@@ -18,6 +18,8 @@ from ogkm import rt  # noqa: E402
 from ogkm.ops import bf12, dgemm  # noqa: E402
 
 SHAPES = ((10240, 8192), (8192, 8192), (57344, 8192), (8192, 28672))
+if os.environ.get("SHAPES"):  # e.g. "6144x4096,4096x4096,28672x4096,4096x14336" (Llama-3-8B)
+    SHAPES = tuple(tuple(int(v) for v in s.split("x")) for s in os.environ["SHAPES"].split(","))
 
 
 def timeit(fn, it=10):
