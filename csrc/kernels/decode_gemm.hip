@@ -421,91 +421,10 @@ __global__ void __launch_bounds__(256) k_dgemm_reduce(DGemmReduceArgs a) {
   *reinterpret_cast<u32x2_t*>(dst) = u32x2_t{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
 }
 
-// Raw-weight variant with one row tile per wave: a workgroup's 4 waves take 4
-// consecutive row tiles over the SAME K range, so their activation fragments
-// are the same addresses (served by the CU's L1 after the first wave) and, for
-// the same number of waves, the K range is split 4x less often - the f32
-// split-K partials (ksplit x M x N x 4 B, as many bytes as the weights
-// themselves for a 4096-row GEMM at 32 splits) shrink 4x. The wave issues U
-// weight fragments (1 KB each, non-temporal: read once) per step block.
-template <int U>
-__global__ void __launch_bounds__(256) k_dgemm_wg(DGemmArgs a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t unit = blockIdx.x;  // row block * ksplit + k split
-  if (unit >= a.row_blocks * a.ksplit) return;
-  const uint32_t rb = unit / a.ksplit, ks = unit - rb * a.ksplit;
-  const uint32_t rt = rb * 4u + wave;
-  if (rt >= (a.N >> 4)) return;  // wave-uniform: no barrier below
-  const uint32_t k_lo = ks * a.klen;
-  const uint32_t k_hi = k_lo + a.klen < a.K ? k_lo + a.klen : a.K;
-  const uint32_t kfr = a.K >> 5;
-  const uint32_t m_base = blockIdx.y * (kMTiles * 16);
-  const uint32_t h = lane >> 4;
-  const uint16_t* xrow[kMTiles];
-  bool mval[kMTiles];
-#pragma unroll
-  for (int mt = 0; mt < kMTiles; ++mt) {
-    const uint32_t m = m_base + mt * 16 + (lane & 15u);
-    mval[mt] = m < a.M;
-    xrow[mt] = a.x + (uint64_t)(mval[mt] ? m : 0) * a.ldx + 8u * h;
-  }
-  const uint16_t* wrow = reinterpret_cast<const uint16_t*>(a.w) + a.w_off + (uint64_t)rt * kfr * 512u + lane * 8u;
-  f32x4_t acc[kMTiles];
-#pragma unroll
-  for (int mt = 0; mt < kMTiles; ++mt) acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  uint32_t k = k_lo;
-  for (; k + 32 * U <= k_hi; k += 32 * U) {
-    const uint32_t kst = k >> 5;
-    u32x4_t wa[U];
-    u32x4_t xb[U][kMTiles];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      wa[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wrow + (uint64_t)(kst + u) * 512u));
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int mt = 0; mt < kMTiles; ++mt)
-        xb[u][mt] = mval[mt] ? *reinterpret_cast<const u32x4_t*>(xrow[mt] + k + 32 * u) : u32x4_t{0, 0, 0, 0};
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int mt = 0; mt < kMTiles; ++mt)
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wa[u]),
-                                                          __builtin_bit_cast(bf16x8_t, xb[u][mt]), acc[mt], 0, 0, 0);
-  }
-  for (; k < k_hi; k += 32) {
-    const u32x4_t wa = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wrow + (uint64_t)(k >> 5) * 512u));
-#pragma unroll
-    for (int mt = 0; mt < kMTiles; ++mt) {
-      const u32x4_t xb = mval[mt] ? *reinterpret_cast<const u32x4_t*>(xrow[mt] + k) : u32x4_t{0, 0, 0, 0};
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wa),
-                                                        __builtin_bit_cast(bf16x8_t, xb), acc[mt], 0, 0, 0);
-    }
-  }
-  // D layout (16x16x32): col = lane & 15 -> m, row = 4 (lane >> 4) + reg -> n.
-  const uint32_t n = rt * 16u + 4u * h;
-#pragma unroll
-  for (int mt = 0; mt < kMTiles; ++mt) {
-    const uint32_t m = m_base + mt * 16 + (lane & 15u);
-    if (m < a.M) *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[mt];
-  }
-}
-
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s) {
   if (a.N % 16 || a.K % 32 || a.klen % 32 || !a.ksplit || a.row_blocks != (a.N / 16 + kRowTiles - 1) / kRowTiles)
     return hipErrorInvalidValue;
   const uint32_t units = a.row_blocks * a.ksplit;
-  if (mode == DGEMM_W_RAW && a.wg_rows == 1) {
-    dim3 grid(units, (a.M + kMTiles * 16 - 1) / (kMTiles * 16));
-    if (a.unroll == 2)
-      hipLaunchKernelGGL((k_dgemm_wg<2>), grid, dim3(256), 0, s, a);
-    else if (a.unroll == 8)
-      hipLaunchKernelGGL((k_dgemm_wg<8>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((k_dgemm_wg<4>), grid, dim3(256), 0, s, a);
-    return hipGetLastError();
-  }
   dim3 grid((units + 3) / 4, (a.M + kMTiles * 16 - 1) / (kMTiles * 16));
   switch (mode) {
     case DGEMM_W_RAW:

@@ -790,14 +790,7 @@ PYBIND11_MODULE(_ogkm, m) {
     a.x = (const uint16_t*)x;
     a.part = (float*)part;
     a.M = M; a.N = N; a.K = K; a.ldx = ldx;
-    // Raw weights: one row tile per wave (a workgroup = 4 waves sharing the K
-    // range), so the same wave count needs 4x fewer K splits (OGKM_DGEMM_WG=1: on).
-    static const bool wg_env = [] {
-      const char* e = getenv("OGKM_DGEMM_WG");
-      return e && e[0] == '1';
-    }();
-    a.wg_rows = (mode == DGEMM_W_RAW && wg_env) ? 1 : 0;
-    dgemm_plan(N, K, a.wg_rows ? std::max<uint32_t>(1, target_units / 4) : target_units, &a.ksplit, &a.klen);
+    dgemm_plan(N, K, target_units, &a.ksplit, &a.klen);
     a.row_blocks = (N / 16 + 3) / 4;
     a.chunk_shift = chunk_shift;
     a.unroll = unroll;
