@@ -85,6 +85,7 @@ class HipBackend : public Backend {
     if (!d) return Status::NOT_SUPPORTED;
     *out = Health{};
     out->source = dir;
+    int parsed = 0;
     while (dirent* e = readdir(d)) {
       std::string n = e->d_name;
       if (n.size() < 11 || n.compare(n.size() - 10, 10, "_err_count") != 0) continue;
@@ -103,8 +104,13 @@ class HipBackend : public Backend {
       int64_t& C = link ? out->link_ce : out->ce;
       if (ue >= 0) U = (U < 0 ? 0 : U) + ue;
       if (ce >= 0) C = (C < 0 ? 0 : C) + ce;
+      parsed += (ue >= 0 || ce >= 0);
     }
     closedir(d);
+    if (!parsed) {  // the directory exists but no counter is readable (permissions, older kernel)
+      last_err_ = "no readable RAS counters under " + dir;
+      return Status::NOT_SUPPORTED;
+    }
     return Status::OK;
   }
   Status device_mem_info(int dev, size_t* f, size_t* t) override {

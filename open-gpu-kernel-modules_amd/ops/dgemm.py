@@ -23,7 +23,12 @@ from .._native import lib
 from . import bf12
 
 EPI = {"store": 0, "resid": 1, "silu_mul": 2}
-TARGET_UNITS = int(os.environ.get("OGKM_DGEMM_UNITS", "2048"))  # waves per GEMM (~8 per CU)
+# Waves per GEMM (~3 per CU): fewer K splits keep the f32 split-K partials
+# small - measured best at Llama-3 8B and 70B decode shapes (profiles/r2_dgemm_sweep.txt:
+# 768 -> 2.71 / 3.86 TB/s vs 2048 -> 2.19 / 3.45 TB/s).
+TARGET_UNITS = int(os.environ.get("OGKM_DGEMM_UNITS", "768"))
+# Packed (BF11) weights decode in registers - ALU-heavy, they need the waves:
+TARGET_UNITS_PACKED = int(os.environ.get("OGKM_DGEMM_UNITS_PACKED", "2048"))
 UNROLL = int(os.environ.get("OGKM_DGEMM_UNROLL", "0"))  # K steps per pipelined block (0 = kernel default)
 
 
@@ -101,13 +106,14 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     if epi == "resid":
         if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
             raise ValueError("dgemm.linear: resid must match out")
-    ks = _PLANS.get((w.n, w.k, TARGET_UNITS))
+    units = TARGET_UNITS if w.mode == MODE_RAW else TARGET_UNITS_PACKED
+    ks = _PLANS.get((w.n, w.k, units))
     if ks is None:
-        ks = _PLANS[(w.n, w.k, TARGET_UNITS)] = lib.dgemm_plan(w.n, w.k, TARGET_UNITS)[0]
+        ks = _PLANS[(w.n, w.k, units)] = lib.dgemm_plan(w.n, w.k, units)[0]
     ksplit = ks
     part = _WS.get(x.device, ksplit * m * w.n * 4)
     stream = int(torch.cuda.current_stream(device_index).cuda_stream) if x.is_cuda else 0
     lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), x.stride(0), m, w.n, w.k,
               part.data_ptr(), part.numel() * 4, EPI[epi], resid.data_ptr() if resid is not None else 0,
-              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), TARGET_UNITS, UNROLL)
+              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, UNROLL)
     return out
