@@ -61,6 +61,10 @@ def test_managed_tensors_oversubscribe_and_keep_their_address(managed_rt):
         assert np.array_equal(_read(p, n // 4), ref)
         lib.torch_park(p, 0)
     assert lib.torch_managed_stats(0)["unparks"] == 6
+    # every remap of a stable VA ends with a GPU translation flush (tools/probe_vmm_tlb.hip:
+    # unmap + map alone leaves stale translations on gfx950)
+    st = lib.stats()
+    assert st["vmm_remaps"] > 0 and st["tlb_flushes"] > 0 and st["vmm_errors"] == 0
     for p in ptrs:
         lib.torch_free(p, 0)
     rt.sync()
