@@ -19,6 +19,7 @@ struct DGemmArgs {
   uint32_t row_blocks;    // ceil(N / 64)
   uint32_t chunk_shift;   // packed: log2(stream chunk_values)
   uint32_t unroll;        // K steps per pipelined block (1, 2 or 4; 0 = default)
+  uint32_t lds_x;         // raw weights: 1 = row tile per wave, activations shared through LDS
 };
 // Weight source: raw bf16 fragments; a packed stream with BF11 and raw chunks;
 // a packed stream whose chunks are all BF11 (fast, phase-pipelined path).

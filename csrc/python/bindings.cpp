@@ -790,7 +790,14 @@ PYBIND11_MODULE(_ogkm, m) {
     a.x = (const uint16_t*)x;
     a.part = (float*)part;
     a.M = M; a.N = N; a.K = K; a.ldx = ldx;
-    dgemm_plan(N, K, target_units, &a.ksplit, &a.klen);
+    // Raw weights with LDS-shared activations: a workgroup of 4 waves per row
+    // block, so the same wave count needs 4x fewer K splits (OGKM_DGEMM_LDS).
+    static const int lds_env = [] {
+      const char* e = getenv("OGKM_DGEMM_LDS");
+      return e ? atoi(e) : 0;
+    }();
+    a.lds_x = (mode == DGEMM_W_RAW && lds_env) ? 1 : 0;
+    dgemm_plan(N, K, a.lds_x ? std::max<uint32_t>(1, target_units / 4) : target_units, &a.ksplit, &a.klen);
     a.row_blocks = (N / 16 + 3) / 4;
     a.chunk_shift = chunk_shift;
     a.unroll = unroll;
