@@ -781,7 +781,8 @@ PYBIND11_MODULE(_ogkm, m) {
   });
   m.def("dgemm", [](int dev, uint64_t stream, uint64_t w, uint64_t w_off, int mode, uint32_t chunk_shift,
                     uint64_t x, uint32_t ldx, uint32_t M, uint32_t N, uint32_t K, uint64_t part, uint64_t part_bytes,
-                    uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo, uint32_t target_units, uint32_t unroll) {
+                    uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo, uint32_t target_units, uint32_t unroll,
+                    int lds_x) {
     if (N % 16 || K % 32 || ldx % 8 || !M) throw StatusError("dgemm: N % 16, K % 32, ldx % 8 and M > 0 required");
     if (epi == DGEMM_EPI_SILU_MUL && (N % 32)) throw StatusError("dgemm: SILU_MUL needs N % 32 == 0");
     DGemmArgs a{};
@@ -792,11 +793,7 @@ PYBIND11_MODULE(_ogkm, m) {
     a.M = M; a.N = N; a.K = K; a.ldx = ldx;
     // Raw weights with LDS-shared activations: a workgroup of 4 waves per row
     // block, so the same wave count needs 4x fewer K splits (OGKM_DGEMM_LDS).
-    static const int lds_env = [] {
-      const char* e = getenv("OGKM_DGEMM_LDS");
-      return e ? atoi(e) : 0;
-    }();
-    a.lds_x = (mode == DGEMM_W_RAW && lds_env) ? 1 : 0;
+    a.lds_x = (mode == DGEMM_W_RAW && lds_x > 0) ? 1 : 0;
     dgemm_plan(N, K, a.lds_x ? std::max<uint32_t>(1, target_units / 4) : target_units, &a.ksplit, &a.klen);
     a.row_blocks = (N / 16 + 3) / 4;
     a.chunk_shift = chunk_shift;
@@ -813,7 +810,8 @@ PYBIND11_MODULE(_ogkm, m) {
     return a.ksplit;
   }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("w_off"), py::arg("mode"), py::arg("chunk_shift"),
      py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("part"), py::arg("part_bytes"),
-     py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("target_units") = 2048, py::arg("unroll") = 0);
+     py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("target_units") = 2048, py::arg("unroll") = 0,
+     py::arg("lds_x") = 0);
   // Fused decode-step ops (ops/fused.py).
   m.def("rmsnorm", [](int dev, uint64_t stream, uint64_t x, uint64_t w, uint64_t y, uint32_t rows, uint32_t dim,
                       uint32_t ldx, uint32_t ldy, float eps) {

@@ -29,6 +29,9 @@ EPI = {"store": 0, "resid": 1, "silu_mul": 2}
 TARGET_UNITS = int(os.environ.get("OGKM_DGEMM_UNITS", "768"))
 # Packed (BF11) weights decode in registers - ALU-heavy, they need the waves:
 TARGET_UNITS_PACKED = int(os.environ.get("OGKM_DGEMM_UNITS_PACKED", "2048"))
+# Raw weights: k_dgemm_lds (row tile per wave, activations shared in LDS, 4x
+# fewer K splits at equal waves) - +8% at 8B shapes, -2% at 70B: opt-in.
+LDS_X = int(os.environ.get("OGKM_DGEMM_LDS", "0"))
 UNROLL = int(os.environ.get("OGKM_DGEMM_UNROLL", "0"))  # K steps per pipelined block (0 = kernel default)
 
 
@@ -93,7 +96,7 @@ _PLANS: dict = {}
 
 
 def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tensor | None = None,
-           out: torch.Tensor | None = None, device_index: int = 0) -> torch.Tensor:
+           out: torch.Tensor | None = None, device_index: int = 0, lds: int | None = None) -> torch.Tensor:
     """x: [M, K] bf16 (row stride % 8 == 0). Returns out [M, N] (silu_mul: [M, N/2])."""
     if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1 or x.shape[1] != w.k:
         raise ValueError("dgemm.linear: x must be a row-major bf16 [M, K] view")
@@ -106,7 +109,10 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     if epi == "resid":
         if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
             raise ValueError("dgemm.linear: resid must match out")
+    lds = LDS_X if lds is None else int(lds)
     units = TARGET_UNITS if w.mode == MODE_RAW else TARGET_UNITS_PACKED
+    if lds and w.mode == MODE_RAW:
+        units *= 2  # waves; the kernel runs 4 per K split
     ks = _PLANS.get((w.n, w.k, units))
     if ks is None:
         ks = _PLANS[(w.n, w.k, units)] = lib.dgemm_plan(w.n, w.k, units)[0]
@@ -115,5 +121,5 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     stream = int(torch.cuda.current_stream(device_index).cuda_stream) if x.is_cuda else 0
     lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), x.stride(0), m, w.n, w.k,
               part.data_ptr(), part.numel() * 4, EPI[epi], resid.data_ptr() if resid is not None else 0,
-              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, UNROLL)
+              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, UNROLL, lds)
     return out

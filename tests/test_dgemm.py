@@ -82,10 +82,13 @@ def test_dgemm_cpu_strided_x_and_inplace_resid(fake_rt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("packed", [False, True, "generic"])
+@pytest.mark.parametrize("packed", [False, True, "generic", "lds"])
 @pytest.mark.parametrize("epi", ["store", "resid", "silu_mul"])
 @pytest.mark.parametrize("m", [1, 7, 64, 80])
 def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m):
+    """packed="lds": raw weights through k_dgemm_lds (activations shared in LDS)."""
+    lds = packed == "lds"
+    packed = False if lds else packed
     n, k = 320, 1024
     w = _weights(n, k, 5)
     x = (torch.randn(m, k) * 0.5).to(torch.bfloat16)
@@ -93,7 +96,7 @@ def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m):
     buf, ref_w = _place(w, packed, "cuda")
     xd = x.cuda()
     rd = resid.cuda() if epi == "resid" else None
-    out = dgemm.linear(xd, ref_w, epi, resid=rd)
+    out = dgemm.linear(xd, ref_w, epi, resid=rd, lds=int(lds))
     torch.cuda.synchronize()
     want = _ref(x, w, epi, resid)
     torch.testing.assert_close(out.float().cpu(), want, atol=2e-2, rtol=2e-2)
