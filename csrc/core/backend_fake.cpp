@@ -279,8 +279,10 @@ class FakeBackend : public Backend {
     return Status::OK;
   }
   Status unpack_bf12_stream(int, uint64_t src, uint64_t dst, uint32_t, uint32_t, uint64_t n, void* s,
-                            uint32_t, uint64_t dst_stride) override {
-    run(s, [src, dst, n, dst_stride] { bf12_unpack((const uint8_t*)src, (uint16_t*)dst, n, dst_stride); });
+                            uint32_t, uint64_t dst_stride, uint32_t row_shift) override {
+    run(s, [src, dst, n, dst_stride, row_shift] {
+      bf12_unpack((const uint8_t*)src, (uint16_t*)dst, n, dst_stride, row_shift);
+    });
     return Status::OK;
   }
   Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {

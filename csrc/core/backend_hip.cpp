@@ -418,17 +418,17 @@ class HipBackend : public Backend {
   }
 
   Status unpack_bf12_stream(int, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values, uint64_t,
-                            void* s, uint32_t workgroups, uint64_t dst_stride) override {
+                            void* s, uint32_t workgroups, uint64_t dst_stride, uint32_t row_shift) override {
     HIPCHK(launch_bf12_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s,
-                              dst_stride));
+                              dst_stride, row_shift));
     launches_++;
     return Status::OK;
   }
 
   Status unpack_ans_stream(int, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values, uint64_t,
-                           void* s, uint32_t workgroups, uint64_t dst_stride) override {
+                           void* s, uint32_t workgroups, uint64_t dst_stride, uint32_t row_shift) override {
     HIPCHK(launch_ans_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s,
-                             dst_stride, decode_err()));
+                             dst_stride, decode_err(), row_shift));
     launches_++;
     return Status::OK;
   }

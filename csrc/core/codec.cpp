@@ -312,13 +312,14 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n, uint32_t chunk_values, uint8_
   return off;
 }
 
-bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n, uint64_t dst_stride) {
+bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n, uint64_t dst_stride, uint32_t row_shift) {
   Bf12StreamHeader h;
   memcpy(&h, stream, sizeof h);
   if (h.magic != kBf12StreamMagic || h.n_values != n) return false;
   const Bf12StreamChunk* t = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof h);
   for (uint32_t c = 0; c < h.nchunks; ++c) {
-    uint16_t* dst = out + (uint64_t)c * (dst_stride ? dst_stride : h.chunk_values);
+    const uint64_t stride = dst_stride ? dst_stride : h.chunk_values;
+    uint16_t* dst = out + ((uint64_t)c >> row_shift) * stride + ((uint64_t)c & ((1ull << row_shift) - 1)) * h.chunk_values;
     if (t[c].encoded == 3) {
       if (!ans_decode(stream + t[c].offset, dst, t[c].n_values)) return false;
     } else if (t[c].encoded == 2) {

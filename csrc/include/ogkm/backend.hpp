@@ -126,14 +126,18 @@ class Backend {
   // unpacking passes a full-chip grid.
   virtual Status decode_bf12(int dev, const DecodeDesc* d, size_t n, void* stream, uint32_t workgroups = 0) = 0;
   // Unpack a device-resident BF12 stream (codec.hpp) of n_values into bf16 at dst.
-  // Chunk c lands at dst + c * dst_stride values (0 = contiguous).
+  // Chunk c lands at dst + (c >> row_shift) * dst_stride + (c mod 2^row_shift) *
+  // chunk_values values (dst_stride 0 = contiguous).
   virtual Status unpack_bf12_stream(int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
-                                    uint64_t n_values, void* stream, uint32_t workgroups, uint64_t dst_stride = 0) = 0;
+                                    uint64_t n_values, void* stream, uint32_t workgroups, uint64_t dst_stride = 0,
+                                    uint32_t row_shift = 0) = 0;
   // Same for an ANS stream (ANS1 / raw chunks, k_ans_unpack). The default serves
   // backends whose stream unpack decodes every chunk kind (the fake CPU one).
   virtual Status unpack_ans_stream(int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
-                                   uint64_t n_values, void* stream, uint32_t workgroups, uint64_t dst_stride = 0) {
-    return unpack_bf12_stream(dev, src, dst, nchunks, chunk_values, n_values, stream, workgroups, dst_stride);
+                                   uint64_t n_values, void* stream, uint32_t workgroups, uint64_t dst_stride = 0,
+                                   uint32_t row_shift = 0) {
+    return unpack_bf12_stream(dev, src, dst, nchunks, chunk_values, n_values, stream, workgroups, dst_stride,
+                              row_shift);
   }
   // Corrupt packed chunks seen by the device decoders since the last reset:
   // out = {count, stream address, chunk index, detail}. Decoders zero-fill such

@@ -194,6 +194,7 @@ uint64_t bf12_pack(const uint16_t* in, uint64_t n_values, uint32_t chunk_values,
                    unsigned threads, PackFormat fmt = PackFormat::BF12);
 // Reference unpack of a whole stream (CPU).
 // dst_stride: chunk c lands at out + c * dst_stride values (0 = contiguous).
-bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n_values, uint64_t dst_stride = 0);
+bool bf12_unpack(const uint8_t* stream, uint16_t* out, uint64_t n_values, uint64_t dst_stride = 0,
+                 uint32_t row_shift = 0);
 
 }  // namespace ogkm

@@ -62,13 +62,17 @@ hipError_t launch_bf12_decode(const KBf12Descs& inl, uint32_t n, uint32_t workgr
 // Unpack a whole BF12 stream (codec.hpp) that lives in device memory into bf16
 // at `dst` (chunk c at dst + c * dst_stride values; 0 = contiguous): one
 // launch, one work item per 32768-value tile of every chunk.
+// Destination of chunk c: (c >> row_shift) * dst_stride + (c & (2^row_shift - 1)) * chunk_values
+// (row_shift 0: c * dst_stride) - a row of 2^row_shift chunks, e.g. a KV row block
+// longer than the largest chunk, lands contiguously in a strided cache row.
 hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
-                              uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0);
+                              uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0, uint32_t row_shift = 0);
 // Unpack an ANS stream (ANS1 or raw chunks, codec.hpp) in device memory into
 // bf16 (csrc/kernels/ans_kernels.hip): one wave per 32 Ki-value rANS segment.
 // err: optional host-coherent {count, stream, chunk, freq sum} record of corrupt chunks.
 hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
-                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0, uint64_t* err = nullptr);
+                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0, uint64_t* err = nullptr,
+                             uint32_t row_shift = 0);
 
 // Decode GEMM (csrc/kernels/decode_gemm.hip); argument structs in ogkm/dgemm.hpp.
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);

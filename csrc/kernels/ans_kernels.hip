@@ -46,7 +46,8 @@ __device__ __forceinline__ uint32_t ans_bperm(uint32_t lane, uint32_t v) {
 // zero-filled and reported instead of being decoded.
 __global__ void __launch_bounds__(kAnsThreads)
     k_ans_unpack(const uint8_t* __restrict__ stream, uint16_t* __restrict__ out, uint64_t dst_stride,
-                 uint32_t items_per_chunk, uint64_t total_items, uint64_t* __restrict__ err) {
+                 uint32_t items_per_chunk, uint64_t total_items, uint64_t* __restrict__ err, uint32_t row_shift,
+                 uint32_t chunk_values) {
   __shared__ uint32_t tab[kAnsSlots];
   __shared__ uint32_t cum[257];
   __shared__ uint32_t wsum[kAnsSegsPerItem];
@@ -58,7 +59,7 @@ __global__ void __launch_bounds__(kAnsThreads)
     const uint32_t sub = (uint32_t)(item - c * items_per_chunk);
     const Bf12StreamChunk ch = table[c];  // uniform: scalar loads
     const uint8_t* blk = stream + ch.offset;
-    uint16_t* dst = out + c * dst_stride;
+    uint16_t* dst = out + (c >> row_shift) * dst_stride + (c & ((1ull << row_shift) - 1)) * chunk_values;
     const uint32_t v_lo = sub * kAnsSegsPerItem * kAnsSegValues;
     if (v_lo >= ch.n_values) continue;  // uniform across the workgroup
     if (ch.encoded != 3) {              // raw chunk: plain copy of this item's range
@@ -168,7 +169,8 @@ __global__ void __launch_bounds__(kAnsThreads)
 }
 
 hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
-                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride, uint64_t* err) {
+                             uint32_t workgroups, hipStream_t s, uint64_t dst_stride, uint64_t* err,
+                             uint32_t row_shift) {
   if (nchunks == 0) return hipSuccess;
   if (chunk_values < 8192 || (chunk_values & (chunk_values - 1)) || chunk_values > (1u << 20))
     return hipErrorInvalidValue;
@@ -177,7 +179,8 @@ hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, ui
   const uint64_t total = (uint64_t)nchunks * per_chunk;
   const uint64_t grid = workgroups && workgroups < total ? workgroups : total;
   hipLaunchKernelGGL(k_ans_unpack, dim3((uint32_t)grid), dim3(kAnsThreads), 0, s, (const uint8_t*)stream,
-                     (uint16_t*)dst, dst_stride ? dst_stride : (uint64_t)chunk_values, per_chunk, total, err);
+                     (uint16_t*)dst, dst_stride ? dst_stride : (uint64_t)chunk_values, per_chunk, total, err, row_shift,
+                     chunk_values);
   return hipGetLastError();
 }
 

@@ -236,7 +236,7 @@ __device__ __forceinline__ void bf11_decode_tile(const uint8_t* __restrict__ blk
 // one item per tile (a 70B layer is ~27k items, >> 256 CUs).
 __global__ void __launch_bounds__(kDecThreads)
     k_bf12_unpack(const uint8_t* __restrict__ stream, uint8_t* __restrict__ out, uint64_t dst_stride,
-                  uint32_t tile_shift, uint64_t total_items) {
+                  uint32_t tile_shift, uint64_t total_items, uint32_t row_shift, uint32_t chunk_values) {
   const Bf12StreamChunk* table = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof(Bf12StreamHeader));
   for (uint64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
     const uint64_t c = item >> tile_shift;
@@ -246,17 +246,18 @@ __global__ void __launch_bounds__(kDecThreads)
     if (lo >= ch.n_values) continue;     // uniform across the workgroup
     const uint32_t cnt = ch.n_values - lo < kBf12Tile ? ch.n_values - lo : kBf12Tile;
     const uint8_t* blk = stream + ch.offset;
-    u32x4* dst = reinterpret_cast<u32x4*>(out + (c * dst_stride + lo) * 2);
+    const uint64_t doff = (c >> row_shift) * dst_stride + (c & ((1ull << row_shift) - 1)) * chunk_values;
+    u32x4* dst = reinterpret_cast<u32x4*>(out + (doff + lo) * 2);
     if (!ch.encoded) {  // raw chunk: plain tile copy (cnt may have an odd tail)
       const u32x4* src = reinterpret_cast<const u32x4*>(blk + (uint64_t)lo * 2);
       for (uint32_t q = threadIdx.x; q < cnt / 8; q += kDecThreads) __builtin_nontemporal_store(src[q], dst + q);
       const uint16_t* s16 = reinterpret_cast<const uint16_t*>(blk) + lo;
-      uint16_t* d16 = reinterpret_cast<uint16_t*>(out) + c * dst_stride + lo;
+      uint16_t* d16 = reinterpret_cast<uint16_t*>(out) + doff + lo;
       for (uint32_t k = (cnt & ~7u) + threadIdx.x; k < cnt; k += kDecThreads) d16[k] = s16[k];
       continue;
     }
     if (ch.encoded == 2) {
-      bf11_decode_tile(blk, reinterpret_cast<uint16_t*>(out) + c * dst_stride, t);
+      bf11_decode_tile(blk, reinterpret_cast<uint16_t*>(out) + doff, t);
       continue;
     }
     const Bf12Header* h = reinterpret_cast<const Bf12Header*>(blk);
@@ -289,7 +290,7 @@ __global__ void __launch_bounds__(kDecThreads)
       __syncthreads();  // workgroup-scope ordering: the patch lands after the bulk store
       const Bf12Exception* exc =
           reinterpret_cast<const Bf12Exception*>(blk + kBf12HeaderBytes + n + n / 2);
-      uint16_t* d16 = reinterpret_cast<uint16_t*>(out) + c * dst_stride;
+      uint16_t* d16 = reinterpret_cast<uint16_t*>(out) + doff;
       for (uint32_t k = e0 + threadIdx.x; k < e1; k += kDecThreads) {
         Bf12Exception ex = exc[k];
         d16[ex.index] = ex.bits;
@@ -299,7 +300,7 @@ __global__ void __launch_bounds__(kDecThreads)
 }
 
 hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
-                              uint32_t workgroups, hipStream_t s, uint64_t dst_stride) {
+                              uint32_t workgroups, hipStream_t s, uint64_t dst_stride, uint32_t row_shift) {
   if (nchunks == 0) return hipSuccess;
   if (chunk_values < 8192 || (chunk_values & (chunk_values - 1)) || chunk_values > kBf12Tile * kBf12MaxTiles)
     return hipErrorInvalidValue;
@@ -308,7 +309,8 @@ hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, u
   uint64_t total = (uint64_t)nchunks << shift;
   uint64_t grid = workgroups && workgroups < total ? workgroups : total;
   hipLaunchKernelGGL(k_bf12_unpack, dim3((uint32_t)grid), dim3(kDecThreads), 0, s, (const uint8_t*)stream,
-                     (uint8_t*)dst, dst_stride ? dst_stride : (uint64_t)chunk_values, shift, total);
+                     (uint8_t*)dst, dst_stride ? dst_stride : (uint64_t)chunk_values, shift, total, row_shift,
+                     chunk_values);
   return hipGetLastError();
 }
 

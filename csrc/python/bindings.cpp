@@ -749,20 +749,22 @@ PYBIND11_MODULE(_ogkm, m) {
   });
   // Unpack a stream resident on device `dev` into `dst` on `stream` (k_bf12_unpack).
   m.def("bf12_unpack", [](int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
-                          uint64_t n_values, uint64_t stream, uint32_t workgroups, uint64_t dst_stride) {
+                          uint64_t n_values, uint64_t stream, uint32_t workgroups, uint64_t dst_stride,
+                          uint32_t row_shift) {
     check(rt()->be()->unpack_bf12_stream(dev, src, dst, nchunks, chunk_values, n_values, (void*)stream, workgroups,
-                                         dst_stride),
+                                         dst_stride, row_shift),
           "bf12_unpack");
   }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("nchunks"), py::arg("chunk_values"),
-     py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0, py::arg("dst_stride") = 0);
+     py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0, py::arg("dst_stride") = 0, py::arg("row_shift") = 0);
   // Same for ANS streams (k_ans_unpack).
   m.def("ans_unpack", [](int dev, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values,
-                         uint64_t n_values, uint64_t stream, uint32_t workgroups, uint64_t dst_stride) {
+                         uint64_t n_values, uint64_t stream, uint32_t workgroups, uint64_t dst_stride,
+                          uint32_t row_shift) {
     check(rt()->be()->unpack_ans_stream(dev, src, dst, nchunks, chunk_values, n_values, (void*)stream, workgroups,
-                                        dst_stride),
+                                        dst_stride, row_shift),
           "ans_unpack");
   }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("nchunks"), py::arg("chunk_values"),
-     py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0, py::arg("dst_stride") = 0);
+     py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0, py::arg("dst_stride") = 0, py::arg("row_shift") = 0);
   m.def("decode_errors", [](bool reset) {
     uint64_t e[4];
     rt()->be()->decode_errors(e, reset);

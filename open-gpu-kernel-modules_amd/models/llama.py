@@ -280,9 +280,14 @@ class TieredLlama:
         # T x hd) into one [2, B, hkv, T, hd] scratch that attention reads.
         if kv_format not in ("bf16", "bf11", "ans"):
             raise ValueError("kv_format must be 'bf16', 'bf11' or 'ans'")
-        cv = context * hd
-        if kv_format != "bf16" and (cv & (cv - 1) or cv < 8192 or cv > (1 << 20)):
-            raise ValueError("packed kv_format needs context * head_dim to be a power of two in [8 Ki, 1 Mi]")
+        # One (k|v, b, head) row block of the prefilled context = ctx * hd values:
+        # one codec chunk, or 2^n chunks of 1 Mi (the largest chunk) for long
+        # contexts, unpacked contiguously into the strided cache row.
+        rowv = context * hd
+        if kv_format != "bf16" and (rowv & (rowv - 1) or rowv < 8192):
+            raise ValueError("packed kv_format needs context * head_dim to be a power of two >= 8 Ki")
+        cv = min(rowv, 1 << 20)
+        self.kv_row_chunks = rowv // cv
         self.kv_format = kv_format
         self.tail = self.T - context
         self.kv_tail_bytes = cfg.n_layers * 2 * batch * self.hkv * self.tail * hd * 2
@@ -723,7 +728,7 @@ class TieredLlama:
         lease, ptr = self._kv_prefix(i) if self.kv_tier else (None, self.kv_lease.dptr + i * self.kv_slot)
         if self.kv_format != "bf16":
             bf12.unpack_into(sc, ptr, self.kv_infos[i], self.dev, 0 if self.fake else None,
-                             dst_stride=self.T * self.cfg.head_dim)
+                             dst_stride=self.T * self.cfg.head_dim, row_chunks=self.kv_row_chunks)
         else:
             hd = self.cfg.head_dim
             pre = rt._tensor_from_ptr(ptr, (2, self.B, self.hkv, self.ctx, hd), torch.bfloat16,

@@ -92,21 +92,27 @@ def unpack_host(stream: torch.Tensor, info: PackedInfo) -> torch.Tensor:
 
 
 def unpack_into(dst: torch.Tensor, src_ptr: int, info: PackedInfo, device: int = 0, stream: int | None = None,
-                workgroups: int = 0, dst_stride: int = 0) -> torch.Tensor:
+                workgroups: int = 0, dst_stride: int = 0, row_chunks: int = 1) -> torch.Tensor:
     """Unpack the stream at device address ``src_ptr`` into ``dst`` (bf16) on
     ``stream`` (default: the current torch stream of ``device``). ``dst_stride``:
-    chunk c lands at element c * dst_stride (0 = contiguous), e.g. KV row blocks
-    into a cache with room for more tokens per row."""
-    need = info.n_values if not dst_stride else (info.nchunks - 1) * dst_stride + (
-        info.n_values - (info.nchunks - 1) * info.chunk_values)
-    if dst_stride and dst_stride < info.chunk_values:
-        raise ValueError("dst_stride must be >= chunk_values")
+    rows of ``row_chunks`` consecutive chunks (a power of two) land at element
+    row * dst_stride (0 = contiguous), e.g. KV row blocks into a cache with room
+    for more tokens per row - a row longer than the largest chunk (1 Mi values)
+    is several chunks."""
+    if row_chunks < 1 or row_chunks & (row_chunks - 1):
+        raise ValueError("row_chunks must be a power of two")
+    row = row_chunks * info.chunk_values
+    rows = -(-info.nchunks // row_chunks)
+    need = info.n_values if not dst_stride else (rows - 1) * dst_stride + (info.n_values - (rows - 1) * row)
+    if dst_stride and dst_stride < row:
+        raise ValueError("dst_stride must be >= row_chunks * chunk_values")
     if dst.dtype != torch.bfloat16 or dst.numel() < need:
         raise ValueError("dst must be bf16 with room for the unpacked chunks")
     if stream is None:
         stream = int(torch.cuda.current_stream(device).cuda_stream) if dst.is_cuda else 0
     fn = lib.ans_unpack if info.fmt == FMT_ANS else lib.bf12_unpack
-    fn(device, src_ptr, dst.data_ptr(), info.nchunks, info.chunk_values, info.n_values, stream, workgroups, dst_stride)
+    fn(device, src_ptr, dst.data_ptr(), info.nchunks, info.chunk_values, info.n_values, stream, workgroups, dst_stride,
+       row_chunks.bit_length() - 1)
     return dst
 
 

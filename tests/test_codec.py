@@ -87,3 +87,33 @@ def test_ans_property_roundtrip(n, std, chunk, seed):
     g = torch.Generator().manual_seed(seed)
     ref = (torch.randn(n, generator=g) * std).to(torch.bfloat16)
     _roundtrip(ref, "ans", chunk)
+
+
+def _strided_rows_case(dev: str, fmt: str):
+    """Rows of 4 chunks (a KV row block longer than the largest chunk) unpacked
+    into a strided cache: row r lands at r * stride, its chunks back to back."""
+    from ogkm.ops import bf12
+
+    cv, rows, stride = 8192, 3, 4 * 8192 + 1000
+    src = (torch.randn(rows, 4 * cv) * 0.7).to(torch.bfloat16)
+    st, info = bf12.pack(src.reshape(-1), chunk_values=cv, fmt=fmt)
+    assert info.nchunks == rows * 4
+    dst = torch.full((rows * stride,), -7.0, dtype=torch.bfloat16, device=dev)
+    s = st.to(dev)
+    bf12.unpack_into(dst, s.data_ptr(), info, 0, 0 if dev == "cpu" else None, dst_stride=stride, row_chunks=4)
+    if dev != "cpu":
+        torch.cuda.synchronize()
+    got = dst.cpu().view(rows, stride)
+    assert torch.equal(got[:, :4 * cv].view(torch.int16), src.view(torch.int16))
+    assert bool((got[:, 4 * cv:] == -7.0).all())  # the tail room is untouched
+
+
+@pytest.mark.parametrize("fmt", ["bf11", "ans"])
+def test_unpack_rows_of_chunks_into_strided_cache_cpu(fake_rt, fmt):
+    _strided_rows_case("cpu", fmt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["bf11", "bf12", "ans"])
+def test_unpack_rows_of_chunks_into_strided_cache_gpu(gpu_rt, fmt):
+    _strided_rows_case("cuda", fmt)

@@ -270,3 +270,23 @@ def test_kv_tiering_bit_identical_to_resident_kv(fake_rt, kv_format):
         m.close()
     for a, b in zip(out[False][0], out[True][0]):
         assert torch.equal(a, b)
+
+
+def test_long_context_packed_kv_rows_of_chunks(fake_rt):
+    """A context whose (k|v, b, head) row block exceeds the largest codec chunk
+    (ctx * hd = 2 Mi values = 2 chunks) still rests packed and decodes the exact
+    bf16 context (the unpack lands each row's chunks back to back in the cache)."""
+    lib.shutdown()
+    rt.init("fake", fake_devices=1, fake_hbm_mb=512, host_budget_mb=2048)
+    cfg = llama.CONFIGS["tiny"]
+    ctx = (2 << 20) // cfg.head_dim
+    out = {}
+    for fmt in ("bf16", "ans"):
+        m = llama.TieredLlama(cfg, batch=1, context=ctx, max_new_tokens=3, oversub=1.0, lookahead=1, seed=4,
+                              kv_format=fmt, weight_format="bf16")
+        assert fmt == "bf16" or m.kv_row_chunks == 2
+        m.keep_logits = True
+        m.step(torch.tensor([3]))
+        out[fmt] = m.last_logits.clone()
+        m.close()
+    assert torch.equal(out["bf16"], out["ans"])
