@@ -104,10 +104,21 @@ bool take_chunks(Runtime* rt, ChunkArena* a, uint32_t n, uint32_t* first) {
   return true;
 }
 
-// The allocating stream waits for everything that last used the memory.
+// The allocating stream waits for everything that last used the memory -
+// except the uses queued on that same stream, which stream order already puts
+// before anything the new owner enqueues (the caching-allocator rule: reuse on
+// the freeing stream costs no wait).
 void order_after(Runtime* rt, DevAlloc* da, Tracker t, void* stream) {
   t.prune();
   if (t.empty()) return;
+  bool foreign = false;
+  for (auto& f : t.fences())
+    if (f->ring || f->stream != stream) foreign = true;
+  if (!foreign) return;
+  Tracker other;
+  for (auto& f : t.fences())
+    if (f->ring || f->stream != stream) other.add(f);
+  t = std::move(other);
   if (t.gpu_wait(rt->be(), stream) != Status::OK) t.wait();
   da->stream_waits++;
 }

@@ -43,6 +43,7 @@ FenceRef fence_record(Backend* be, int dev, void* stream, Ring* ring, uint64_t s
   f->dev = dev;
   f->ring = ring;
   f->seq = seq;
+  f->stream = stream;
   f->event = be->event_create(dev);
   if (!f->event || be->event_record(f->event, stream) != Status::OK) {
     // Could not record: degrade to a ring-only fence (or completed).

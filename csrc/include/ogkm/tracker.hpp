@@ -26,6 +26,7 @@ struct Fence {
   Ring* ring = nullptr;    // ring whose work this fence retires (may be null)
   uint64_t seq = 0;        // ring tracking value
   int dev = -1;
+  void* stream = nullptr;  // stream the event was recorded on (fence_record)
   std::atomic<bool> done{false};
   ~Fence();
   bool query();

@@ -304,6 +304,28 @@ def test_allocator_free_on_busy_stream_is_stream_ordered(gpu_rt):
     lib.torch_free(q, 0, s2.cuda_stream)
 
 
+def test_allocator_same_stream_reuse_needs_no_wait(gpu_rt):
+    """Freed and reallocated on the same stream: stream order already serialises
+    the old and new owner, so no GPU-side wait is queued (and the data is right)."""
+    n = 64 * MB
+    s1 = torch.cuda.Stream()
+    p = lib.torch_alloc(n, 0, s1.cuda_stream)
+    old = rt._tensor_from_ptr(p, (n // 4,), torch.int32, "cuda", 0)
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(100_000_000)
+        old.fill_(1)
+    waits0 = lib.torch_alloc_stats(0)[3]
+    lib.torch_free(p, 0, s1.cuda_stream)
+    q = lib.torch_alloc(n, 0, s1.cuda_stream)
+    assert q == p and lib.torch_alloc_stats(0)[3] == waits0
+    new = rt._tensor_from_ptr(q, (n // 4,), torch.int32, "cuda", 0)
+    with torch.cuda.stream(s1):
+        new.fill_(2)
+    torch.cuda.synchronize()
+    assert bool((new == 2).all())
+    lib.torch_free(q, 0, s1.cuda_stream)
+
+
 def test_bf12_packed_stream_is_bit_exact(gpu_rt):
     """Fused H2D copy + BF12 decode kernel reproduces every bf16 bit pattern."""
     n = 5 * (1 << 20) + 4096  # 2.5 blocks, partial last block
