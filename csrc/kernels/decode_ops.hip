@@ -263,25 +263,31 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
       qb[k] = *reinterpret_cast<const uint4*>(qr + 32 * k);
       if (col >= g) qb[k] = uint4{0u, 0u, 0u, 0u};
     }
-    // A fragments: 4 token tiles x KS dim steps, all loads issued up front
-    // (rows past the context are clamped to the last one and masked below)
-    uint4 ka[4][KS];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int32_t tok = t * 16 + (int32_t)col;
-      const uint32_t row = wt0 + (uint32_t)(tok < wn ? tok : wn - 1);
-      const uint16_t* kr = kbase + (uint64_t)row * HD + 8 * quad;
-#pragma unroll
-      for (int k = 0; k < KS; ++k) ka[t][k] = *reinterpret_cast<const uint4*>(kr + 32 * k);
-    }
+    // A fragments: 4 token tiles x KS dim steps, two tiles' loads in flight at a
+    // time for big groups (the P.V accumulators need the registers), all four
+    // for small ones (rows past the context are clamped and masked below)
+    constexpr int TH = 2;
     attn_f32x4_t sc[4];
+#pragma unroll 1
+    for (int t0 = 0; t0 < 4; t0 += TH) {
+      uint4 ka[TH][KS];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      sc[t] = attn_f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < TH; ++t) {
+        const int32_t tok = (t0 + t) * 16 + (int32_t)col;
+        const uint32_t row = wt0 + (uint32_t)(tok < wn ? tok : wn - 1);
+        const uint16_t* kr = kbase + (uint64_t)row * HD + 8 * quad;
 #pragma unroll
-      for (int k = 0; k < KS; ++k)
-        sc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(attn_bf16x8_t, ka[t][k]),
-                                                        __builtin_bit_cast(attn_bf16x8_t, qb[k]), sc[t], 0, 0, 0);
+        for (int k = 0; k < KS; ++k) ka[t][k] = *reinterpret_cast<const uint4*>(kr + 32 * k);
+      }
+#pragma unroll
+      for (int t = 0; t < TH; ++t) {
+        attn_f32x4_t acc = attn_f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(attn_bf16x8_t, ka[t][k]),
+                                                        __builtin_bit_cast(attn_bf16x8_t, qb[k]), acc, 0, 0, 0);
+        sc[t0 + t] = acc;
+      }
     }
     // softmax partials: lane = head col, tokens t*16 + 4*quad + r
     float m = -INFINITY;
