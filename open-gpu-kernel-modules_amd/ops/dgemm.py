@@ -30,8 +30,11 @@ TARGET_UNITS = int(os.environ.get("OGKM_DGEMM_UNITS", "768"))
 # Packed (BF11) weights decode in registers - ALU-heavy, they need the waves:
 TARGET_UNITS_PACKED = int(os.environ.get("OGKM_DGEMM_UNITS_PACKED", "2048"))
 # Raw weights: k_dgemm_lds (row tile per wave, activations shared in LDS, 4x
-# fewer K splits at equal waves) - +8% at 8B shapes, -2% at 70B: opt-in.
-LDS_X = int(os.environ.get("OGKM_DGEMM_LDS", "0"))
+# fewer K splits at equal waves) wins when N is small (few row blocks, many
+# splits: 8-13% at N <= 8192) and loses on tall matrices (57344 x 8192: +20%),
+# measured per shape (profiles/r2_dgemm_sweep.txt). -1 = auto (N <= 8192), 0 off, 1 on.
+LDS_X = int(os.environ.get("OGKM_DGEMM_LDS", "-1"))
+LDS_MAX_N = 8192
 UNROLL = int(os.environ.get("OGKM_DGEMM_UNROLL", "0"))  # K steps per pipelined block (0 = kernel default)
 
 
@@ -110,6 +113,8 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
         if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
             raise ValueError("dgemm.linear: resid must match out")
     lds = LDS_X if lds is None else int(lds)
+    if lds < 0:
+        lds = int(w.mode == MODE_RAW and w.n <= LDS_MAX_N)
     units = TARGET_UNITS if w.mode == MODE_RAW else TARGET_UNITS_PACKED
     if lds and w.mode == MODE_RAW:
         units *= 2  # waves; the kernel runs 4 per K split

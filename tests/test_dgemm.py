@@ -96,7 +96,7 @@ def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m):
     buf, ref_w = _place(w, packed, "cuda")
     xd = x.cuda()
     rd = resid.cuda() if epi == "resid" else None
-    out = dgemm.linear(xd, ref_w, epi, resid=rd, lds=int(lds))
+    out = dgemm.linear(xd, ref_w, epi, resid=rd, lds=int(lds))  # raw: the 4-row-tile kernel unless "lds"
     torch.cuda.synchronize()
     want = _ref(x, w, epi, resid)
     torch.testing.assert_close(out.float().cpu(), want, atol=2e-2, rtol=2e-2)
