@@ -145,34 +145,17 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
       return Status::OK;
     }
   if (n == 1) {
-    // Victim order: unused list head, then used LRU head (uvm_pmm_gpu.c:1460-1500),
-    // then chunks whose data prefers this tier.
-    // Within a list, the oldest few candidates compete on recency (prefetched
-    // chunks carry a recency bonus and lose to genuinely cold data).
-    // Workingset-protected (active) chunks go only when nothing inactive is left.
-    for (int pass = 0; pass < 6; ++pass) {
-      const int list = 1 + pass % 3;
-      const bool allow_active = pass >= 3;
-      int32_t best = -1;
-      int scanned = 0;
-      for (int32_t i = head_[list]; i >= 0 && scanned < 64; i = chunks_[i].next) {
-        ChunkInfo& c = chunks_[i];
-        if (c.state != ChunkState::ALLOCATED || c.pin_count != 0 || (c.active && !allow_active)) continue;
-        ++scanned;
-        if (best < 0 || c.last_use < chunks_[best].last_use) best = i;
-      }
-      if (best >= 0) {
-        ChunkInfo& c = chunks_[best];
-        lru_remove((uint32_t)best);
-        c.state = ChunkState::EVICTING;
-        r->first = best;
-        r->n = 1;
-        r->victims = {(uint32_t)best};
-        st_.reservations++;
-        return Status::OK;
-      }
-    }
-    return Status::NO_MEMORY;
+    int32_t best = pick_victim_locked();
+    if (best < 0) return Status::NO_MEMORY;
+    ChunkInfo& c = chunks_[best];
+    lru_remove((uint32_t)best);
+    c.state = ChunkState::EVICTING;
+    r->first = best;
+    r->n = 1;
+    r->victims = {(uint32_t)best};
+    r->list.clear();
+    st_.reservations++;
+    return Status::OK;
   }
   // Sliding window over [0, nchunks): every chunk must be FREE or evictable;
   // minimise the newest last_use in the window (evict the coldest data).
@@ -230,6 +213,70 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
   return Status::OK;
 }
 
+// Victim order: unused list head, then used LRU head (uvm_pmm_gpu.c:1460-1500),
+// then chunks whose data prefers this tier.
+// Within a list, the oldest few candidates compete on recency (prefetched
+// chunks carry a recency bonus and lose to genuinely cold data).
+// Workingset-protected (active) chunks go only when nothing inactive is left.
+int32_t ChunkArena::pick_victim_locked() {
+  for (int pass = 0; pass < 6; ++pass) {
+    const int list = 1 + pass % 3;
+    const bool allow_active = pass >= 3;
+    int32_t best = -1;
+    int scanned = 0;
+    for (int32_t i = head_[list]; i >= 0 && scanned < 64; i = chunks_[i].next) {
+      ChunkInfo& c = chunks_[i];
+      if (c.state != ChunkState::ALLOCATED || c.pin_count != 0 || (c.active && !allow_active)) continue;
+      ++scanned;
+      if (best < 0 || c.last_use < chunks_[best].last_use) best = i;
+    }
+    if (best >= 0) return best;
+  }
+  return -1;
+}
+
+Status ChunkArena::reserve_scattered(uint32_t n, Reservation* r) {
+  std::lock_guard<OrderedMutex> g(m_);
+  if (n == 0 || n > nchunks_) return Status::NO_MEMORY;
+  r->first = -1;
+  r->n = n;
+  r->victims.clear();
+  r->list.clear();
+  r->list.reserve(n);
+  while (r->list.size() < n && !free_runs_.empty()) {
+    uint32_t k = free_runs_.begin()->first;
+    take_run(k, 1);
+    chunks_[k].state = ChunkState::RESERVED;
+    r->list.push_back(k);
+  }
+  while (r->list.size() < n) {
+    int32_t v = pick_victim_locked();
+    if (v < 0) break;
+    lru_remove((uint32_t)v);
+    chunks_[v].state = ChunkState::EVICTING;
+    r->list.push_back((uint32_t)v);
+    r->victims.push_back((uint32_t)v);
+  }
+  if (r->list.size() < n) {  // not enough evictable memory: give everything back
+    for (uint32_t k : r->list) {
+      ChunkInfo& c = chunks_[k];
+      if (c.state == ChunkState::RESERVED) {
+        c.state = ChunkState::FREE;
+        add_run(k, 1);
+      } else {
+        c.state = ChunkState::ALLOCATED;
+        lru_push_tail(k, 2);
+      }
+    }
+    r->list.clear();
+    r->victims.clear();
+    r->n = 0;
+    return Status::NO_MEMORY;
+  }
+  st_.reservations++;
+  return Status::OK;
+}
+
 void ChunkArena::evicted(uint32_t i) {
   std::lock_guard<OrderedMutex> g(m_);
   ChunkInfo& c = chunks_[i];
@@ -243,15 +290,15 @@ void ChunkArena::evicted(uint32_t i) {
 
 void ChunkArena::commit(const Reservation& r, bool pin) {
   std::lock_guard<OrderedMutex> g(m_);
-  for (uint32_t i = 0; i < r.n; ++i) {
-    ChunkInfo& c = chunks_[r.first + i];
+  r.for_each([&](uint32_t k) {
+    ChunkInfo& c = chunks_[k];
     RT_ASSERT_RELEASE(c.state == ChunkState::RESERVED);
     c.state = ChunkState::ALLOCATED;
     c.owner = nullptr;
     c.pin_count = pin ? 1 : 0;
     c.last_use = ++clock_;
-    lru_push_tail((uint32_t)r.first + i, 1);
-  }
+    lru_push_tail(k, 1);
+  });
   if (pin) st_.pinned += (uint64_t)r.n << kBlockShift;
   st_.allocated += (uint64_t)r.n << kBlockShift;
   st_.peak = std::max(st_.peak, st_.allocated);
@@ -260,8 +307,7 @@ void ChunkArena::commit(const Reservation& r, bool pin) {
 
 void ChunkArena::cancel(const Reservation& r) {
   std::lock_guard<OrderedMutex> g(m_);
-  for (uint32_t i = 0; i < r.n; ++i) {
-    uint32_t k = (uint32_t)r.first + i;
+  r.for_each([&](uint32_t k) {
     ChunkInfo& c = chunks_[k];
     if (c.state == ChunkState::RESERVED) {
       c.state = ChunkState::FREE;
@@ -272,7 +318,7 @@ void ChunkArena::cancel(const Reservation& r) {
       c.state = ChunkState::ALLOCATED;
       lru_push_tail(k, 2);
     }
-  }
+  });
 }
 
 void ChunkArena::free(uint32_t first, uint32_t n) {
@@ -450,6 +496,7 @@ HbmArena::HbmArena(Backend* be, int dev, uint64_t budget, int provider)
     return;
   }
   init_chunks((uint64_t)slab_, n);
+  stable_owner.assign(n, nullptr);
   RT_INFO("HBM arena gpu%d: %u x 2MB chunks at %p (%s)", dev, n, slab_, handles_.empty() ? "slab" : "vmm");
 }
 

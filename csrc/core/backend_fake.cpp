@@ -16,6 +16,7 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <chrono>
 #include <thread>
 
 #include "ogkm/backend.hpp"
@@ -268,6 +269,7 @@ class FakeBackend : public Backend {
   // The fake "SDMA engine": the ring worker's own thread does the copy.
   bool dma_supported(int) override { return true; }
   Status dma_copy(int, const CopyDesc* d, size_t n, int) override {
+    if (int64_t us = config().fake_dma_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(us));
     for (size_t i = 0; i < n; ++i) memmove((void*)d[i].dst, (const void*)d[i].src, d[i].bytes);
     return Status::OK;
   }

@@ -88,12 +88,10 @@ Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool 
   }
   Status st = a->reserve(n, r);
   if (st != Status::OK) return st;
-  for (uint32_t v : r->victims) {
-    Status es = evict_chunk(a, v);
-    if (es != Status::OK) {
-      a->cancel(*r);
-      return es;
-    }
+  Status es = evict_batch(a, r->victims);
+  if (es != Status::OK) {
+    a->cancel(*r);
+    return es;
   }
   if (!a->loc().is_gpu()) {
     st = static_cast<HostArena*>(a)->ensure_registered((uint32_t)r->first, r->n);
@@ -420,7 +418,7 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
       if (left.empty()) break;
     }
     // Never-populated pages are zero-filled (uvm_va_block.c:2863).
-    if (!left.empty()) {
+    if (!left.empty() && !(b->range->flags & RANGE_NO_ZERO_FILL)) {
       st = zero_pages(this, c, b, to, left);
       if (st != Status::OK) return st;
     }
@@ -564,112 +562,166 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
     update_device_table(b);
     if (b->range->dev_va) stable_map_block(b);
   }
-  if (tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
+  // A caller that remaps several groups flushes once at its end (place_stable).
+  if (!c.defer_flush && tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
   // The context is spent; what the caller still needs for its retry (the
   // arena to evict from on MORE_PROCESSING_REQUIRED) survives the reset.
   ChunkArena* need_arena = c.need_arena;
   uint32_t need_n = c.need_n;
   Cause cause = c.cause;
+  bool defer = c.defer_flush;
   c = Ctx{};
   c.need_arena = need_arena;
   c.need_n = need_n;
   c.cause = cause;
+  c.defer_flush = defer;
   return result;
 }
 
 // ------------------------------------------------------------------ eviction
-// Evict chunk `i` of arena `a` (EVICTING state). No block lock may be held.
-Status Runtime::evict_chunk(ChunkArena* a, uint32_t i) {
-  TraceRange tr(be_.get(), "ogkm:evict_chunk");
+// Detach EVICTING chunk `i` of arena `a` from its owner block, queueing the
+// copy-out of the pages only it holds into context `c` (no block lock may be
+// held on entry). *detached is set when the chunk no longer belongs to a block
+// (then its reuse fence must cover c's copies, see seal_evictions). Returns
+// MORE_PROCESSING_REQUIRED with c.need_* set when the demotion tier is full.
+Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
+  *detached = false;
   if (inject_.evict_fail.load() > 0 && inject_.evict_fail.fetch_sub(1) > 0) {
     Tools::get().inc(Counter::InjectedErrors);
     return Status::INJECTED_ERROR;
   }
   Block* b = a->owner(i);
   if (!b) {
-    a->evicted(i);
+    *detached = true;
     return Status::OK;
   }
+  std::lock_guard<OrderedMutex> g(b->lock);
+  Residency* r = nullptr;
+  for (auto& x : b->res)
+    if (x.arena == a && x.chunk == (int64_t)i) r = &x;
+  if (!r) {
+    *detached = true;
+    return Status::OK;
+  }
+  if (b->lease_pins || b->user_pins) return Status::BUSY;
+  PageMask others;
+  for (auto& x : b->res)
+    if (&x != r) others |= x.resident;
+  PageMask only_here = r->resident.andnot(others);
+  Loc from = r->loc;
+  uint64_t bytes = (uint64_t)r->resident.count() << kPageShift;
+  if (!only_here.empty()) {
+    Loc dst = demotion_target(from);
+    // Honour a host/CXL preferred location for evicted HBM data.
+    if (from.is_gpu() && b->policy.has_preferred && !b->policy.preferred.is_gpu()) dst = b->policy.preferred;
+    if (dst.id < 0) return Status::NO_MEMORY;
+    Residency* to = nullptr;
+    Status st = populate(c, b, dst, -1, &to);
+    if (st != Status::OK) return st;
+    r = nullptr;
+    for (auto& x : b->res)
+      if (x.arena == a && x.chunk == (int64_t)i) r = &x;
+    st = copy_pages(this, c, b, r, to, only_here);
+    if (st != Status::OK) return st;
+    to->resident |= only_here;
+    c.cpu_refresh.push_back(b);
+  }
+  // Detach the chunk from the block; the arena keeps it reserved for the
+  // evicting allocator, fenced on the copy-out.
+  Tracker pend = b->tracker;
+  shootdown(b, r);
+  if (from.is_gpu()) {
+    b->gpu_evictions++;
+    b->gpu_evicted_at = a->evictions();
+    // Users of the stable VA's mapping of this chunk (see Block::stable_users).
+    if (b->range->dev_va && b->stable_chunk.load() == (int64_t)i) {
+      std::lock_guard<std::mutex> sg(stable_m_);
+      b->stable_users.merge(pend);
+    }
+  }
+  b->drop(from);
+  c.cpu_refresh.push_back(b);
+  for (auto& f : pend.fences()) a->add_reuse_fence(i, f);
+  *detached = true;
+  Tools::get().inc(Counter::Evictions);
+  Tools::get().inc(Counter::EvictedBytes, bytes);
+  tools_event(ToolsEventType::Eviction, Cause::Eviction, from, demotion_target(from), kCpuProc,
+              b->range->addr() + b->block_offset(), bytes, b->range->id);
+  Tools::get().bus().notify(PerfEventData{PerfEvent::MIGRATION, b->range->id, b->index, from, demotion_target(from),
+                                          kCpuProc, bytes, (int)Cause::Eviction});
+  return Status::OK;
+}
+
+// Submit the copy-outs of context `c` (ONE submission per ring for every
+// victim) and hand the detached chunks to the reserver: each victim's reuse
+// fence covers the copies that read it; the chunks are not freed.
+void Runtime::seal_evictions(Ctx& c, ChunkArena* a, const std::vector<uint32_t>& victims) {
+  std::vector<std::pair<Ring*, FenceRef>> fs;
+  for (Ring* rr : c.rings) fs.emplace_back(rr, rr->submit());
+  for (uint32_t i : victims)
+    for (auto& f : fs) a->add_reuse_fence(i, f.second);
+  for (auto& u : c.chunk_uses)
+    if (u.arena == a && std::find(victims.begin(), victims.end(), u.chunk) != victims.end())
+      u.arena = nullptr;  // an evicted chunk is not freed
+  c.chunk_uses.erase(std::remove_if(c.chunk_uses.begin(), c.chunk_uses.end(),
+                                    [](const Ctx::ChunkUse& u) { return u.arena == nullptr; }),
+                     c.chunk_uses.end());
+  for (uint32_t i : victims) a->evicted(i);
+  c.defer_flush = true;  // evictions only unmap stable VAs: nothing to flush
+  finish_ctx(c, nullptr);
+}
+
+// Evict chunk `i` of arena `a` (EVICTING state). No block lock may be held.
+Status Runtime::evict_chunk(ChunkArena* a, uint32_t i) { return evict_batch(a, {i}); }
+
+// Evict a set of EVICTING chunks with one copy-out submission per ring
+// (uvm_pmm_gpu.c evict_root_chunk, batched the way pick_root_chunk_to_evict's
+// callers free a PMA batch). Victims whose owner is pinned are left EVICTING
+// (the caller's cancel() gives them back) and BUSY is returned.
+Status Runtime::evict_batch(ChunkArena* a, const std::vector<uint32_t>& victims) {
+  if (victims.empty()) return Status::OK;
+  TraceRange tr(be_.get(), "ogkm:evict_batch");
   Ctx c;
   c.cause = Cause::Eviction;
-  Status st = Status::OK;
-  for (int attempt = 0; attempt < 4; ++attempt) {
-    {
-      std::lock_guard<OrderedMutex> g(b->lock);
-      Residency* r = nullptr;
-      for (auto& x : b->res)
-        if (x.arena == a && x.chunk == (int64_t)i) r = &x;
-      if (!r) {
-        a->evicted(i);
-        return Status::OK;
-      }
-      if (b->lease_pins || b->user_pins) return Status::BUSY;
-      PageMask others;
-      for (auto& x : b->res)
-        if (&x != r) others |= x.resident;
-      PageMask only_here = r->resident.andnot(others);
-      Loc from = r->loc;
-      uint64_t bytes = (uint64_t)r->resident.count() << kPageShift;
-      if (!only_here.empty()) {
-        Loc dst = demotion_target(from);
-        // Honour a host/CXL preferred location for evicted HBM data.
-        if (from.is_gpu() && b->policy.has_preferred && !b->policy.preferred.is_gpu()) dst = b->policy.preferred;
-        if (dst.id < 0) return Status::NO_MEMORY;
-        Residency* to = nullptr;
-        st = populate(c, b, dst, -1, &to);
-        if (st == Status::MORE_PROCESSING_REQUIRED) goto retry;
-        if (st != Status::OK) return st;
-        r = nullptr;
-        for (auto& x : b->res)
-          if (x.arena == a && x.chunk == (int64_t)i) r = &x;
-        st = copy_pages(this, c, b, r, to, only_here);
-        if (st != Status::OK) return st;
-        to->resident |= only_here;
-        c.cpu_refresh.push_back(b);
-      }
-      // Detach the chunk from the block; the arena keeps it reserved for the
-      // evicting allocator, fenced on the copy-out.
-      Tracker pend = b->tracker;
-      shootdown(b, r);
-      if (from.is_gpu()) {
-        b->gpu_evictions++;
-        b->gpu_evicted_at = a->evictions();
-      }
-      b->drop(from);
-      c.cpu_refresh.push_back(b);
-      for (auto& f : pend.fences()) a->add_reuse_fence(i, f);
-      Tools::get().inc(Counter::Evictions);
-      Tools::get().inc(Counter::EvictedBytes, bytes);
-      tools_event(ToolsEventType::Eviction, Cause::Eviction, from, demotion_target(from), kCpuProc,
-                  b->range->addr() + b->block_offset(), bytes, b->range->id);
-      Tools::get().bus().notify(PerfEventData{PerfEvent::MIGRATION, b->range->id, b->index, from,
-                                              demotion_target(from), kCpuProc, bytes, (int)Cause::Eviction});
+  std::vector<uint32_t> sealed;
+  Status result = Status::OK;
+  int retries = 0;
+  for (size_t k = 0; k < victims.size() && result == Status::OK;) {
+    bool detached = false;
+    Status st = evict_one(c, a, victims[k], &detached);
+    if (st == Status::OK) {
+      if (detached) sealed.push_back(victims[k]);
+      ++k;
+      retries = 0;
+      continue;
     }
-    // Fences for the copy-out are published by finish_ctx; the chunk itself
-    // is handed to the reserver (evicted), not freed.
-    {
-      std::vector<std::pair<Ring*, FenceRef>> fs;
-      for (Ring* rr : c.rings) fs.emplace_back(rr, rr->submit());
-      for (auto& f : fs) a->add_reuse_fence(i, f.second);
-      for (auto& u : c.chunk_uses)
-        if (u.arena == a && u.chunk == i) u.arena = nullptr;  // the evicted chunk is not freed
-      c.chunk_uses.erase(std::remove_if(c.chunk_uses.begin(), c.chunk_uses.end(),
-                                        [](const Ctx::ChunkUse& u) { return u.arena == nullptr; }),
-                         c.chunk_uses.end());
-      a->evicted(i);
-      finish_ctx(c, nullptr);
+    ChunkArena* na = c.need_arena;
+    uint32_t nn = c.need_n ? c.need_n : 1;
+    // Submit what is queued before waiting for anything.
+    seal_evictions(c, a, sealed);
+    sealed.clear();
+    c = Ctx{};
+    c.cause = Cause::Eviction;
+    if (st != Status::MORE_PROCESSING_REQUIRED || ++retries > 4) {
+      result = st == Status::MORE_PROCESSING_REQUIRED ? Status::NO_MEMORY : st;
+      break;
     }
-    return Status::OK;
-  retry:
-    if (c.need_arena) {
-      Reservation rr;
-      Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
-      if (es != Status::OK) return es;
-      c.need_arena->free((uint32_t)rr.first, rr.n);
-      c.need_arena = nullptr;
+    // The demotion tier is full: make room there (a deeper eviction), retry.
+    if (!na) na = arena_for(demotion_target(a->loc()));
+    if (!na) {
+      result = Status::NO_MEMORY;
+      break;
     }
+    Reservation rr;
+    Status es = ensure_capacity(na, nn, &rr);
+    if (es != Status::OK) {
+      result = es;
+      break;
+    }
+    na->free((uint32_t)rr.first, rr.n);
   }
-  return Status::NO_MEMORY;
+  seal_evictions(c, a, sealed);
+  return result;
 }
 
 // ------------------------------------------------------------------ prefetch / migrate
@@ -814,6 +866,9 @@ Status Runtime::evict_range(Range* r, Loc from) {
 // and resident pages are relocated D2D. With a lease, chunks are pinned.
 Status Runtime::gpu_extent_resident(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
                                     Lease* L, Tracker* out, Cause cause) {
+  // A stable-VA range on its own GPU is addressed through its VMM mapping: no
+  // contiguous extent (and no relocation) is ever needed.
+  if (r->dev_va && gpu == r->stable_dev) return place_stable(r, off, len, gpu, read_dup, L, out, cause);
   // An extent found in place can lose a block to a concurrent eviction between
   // the check and the copies (its chunk may already back another block): the
   // placement then starts over and relocates the span into a fresh extent.
@@ -996,6 +1051,168 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
   if (L) {
     for (Block* b : L->blocks) L->ready.merge(published_tracker(b));
     L->dptr = ga->chunk_addr((uint32_t)first) + (off - (b0 << kBlockShift));
+  }
+  return Status::OK;
+}
+
+// Stable-VA placement. Blocks go in groups of `stable_batch_blocks`: for each
+// group the missing blocks get chunks (a block's previous chunk when it is free
+// again - then its VMM mapping is still right and no remap is needed - else any
+// free chunk, else LRU victims evicted as ONE copy-out batch), their H2D copies
+// are queued as ONE submission that waits only for that group's copy-outs, and
+// their VAs are remapped while the copies run. Consecutive groups therefore
+// overlap D2H (evictions) and H2D (fills) on the two SDMA engines; one
+// translation flush covers every remap of the call.
+Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
+                             Lease* L, Tracker* out, Cause cause) {
+  TraceRange tr(be_.get(), "ogkm:place_stable");
+  Loc dst = Loc::gpu(gpu);
+  ChunkArena* ga = arena_for(dst);
+  if (!ga) return Status::INVALID_ARGUMENT;
+  const uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
+  auto pages_of = [&](uint64_t bi) {
+    uint64_t lo = std::max(off, bi << kBlockShift) - (bi << kBlockShift);
+    uint64_t hi = std::min(off + len, (bi + 1) << kBlockShift) - (bi << kBlockShift);
+    uint32_t p0 = (uint32_t)(lo >> kPageShift), p1 = (uint32_t)((hi + kPageSize - 1) >> kPageShift);
+    return PageMask::range(p0, p1 - p0);
+  };
+  const uint64_t group = (uint64_t)std::max<int64_t>(1, config().stable_batch_blocks);
+  std::lock_guard<OrderedMutex> placement(r->place_lock);
+  Status st = Status::OK;
+  std::vector<Block*> leased;  // blocks this call pinned for L (undone on failure)
+  for (uint64_t g0 = b0; g0 <= b1 && st == Status::OK; g0 += group) {
+    const uint64_t g1 = std::min(b1, g0 + group - 1);
+    // 1) blocks of the group without an HBM residency, and the chunk each had last
+    std::vector<uint64_t> need;
+    std::vector<int64_t> hints;
+    for (uint64_t bi = g0; bi <= g1; ++bi) {
+      Block* b = r->block(bi);
+      std::lock_guard<OrderedMutex> g(b->lock);
+      if (!b->find(dst)) {
+        need.push_back(bi);
+        hints.push_back(b->stable_chunk.load());
+      }
+    }
+    // 2) chunks for them (pinned until handed to their block)
+    std::vector<uint32_t> chunks;
+    for (size_t k = 0; k < need.size(); ++k) {
+      uint32_t ch = 0;
+      if (alloc_chunks(ga, 1, hints[k], &ch, nullptr, true) != Status::OK) break;
+      chunks.push_back(ch);
+    }
+    if (chunks.size() < need.size()) {
+      Reservation rv;
+      const uint32_t m = (uint32_t)(need.size() - chunks.size());
+      if (ga->loc().is_gpu() && !config().global_oversubscription) st = Status::NO_MEMORY;
+      else if (inject_.alloc_fail_after.load() == 0) {
+        Tools::get().inc(Counter::InjectedErrors);
+        st = Status::NO_MEMORY;
+      } else {
+        st = ga->reserve_scattered(m, &rv);
+      }
+      if (st == Status::OK) {
+        st = evict_batch(ga, rv.victims);
+        if (st != Status::OK) ga->cancel(rv);
+      }
+      if (st == Status::OK) {
+        ga->commit(rv, true);
+        Tools::get().inc(Counter::AllocRetries);
+        chunks.insert(chunks.end(), rv.list.begin(), rv.list.end());
+      } else {
+        for (uint32_t ch : chunks) ga->free(ch, 1);
+        break;
+      }
+    }
+    // 3) hand chunks over, queue the fills of the group
+    Ctx c;
+    c.cause = cause;
+    c.defer_flush = true;
+    size_t next = 0;
+    for (uint64_t bi = g0; bi <= g1; ++bi) {
+      Block* b = r->block(bi);
+      for (int attempt = 0; attempt < 8; ++attempt) {
+        {
+          std::lock_guard<OrderedMutex> g(b->lock);
+          Residency* x = b->find(dst);
+          if (next < need.size() && need[next] == bi) {
+            uint32_t ch = chunks[next++];
+            if (x) {
+              ga->free(ch, 1);  // populated concurrently (a prefetch): keep theirs
+            } else {
+              ga->set_owner(ch, b);
+              Residency& nr = b->get_or_add(dst);
+              nr.arena = ga;
+              nr.chunk = ch;
+              nr.resident.zero();
+              ga->unpin(ch);
+            }
+          }
+          PageMask want = pages_of(bi);
+          const bool dup = read_dup.empty() ? b->policy.read_dup : read_dup[bi - b0];
+          Residency* y = b->find(dst);
+          // Fast path (the common case of a leased tensor that stayed resident):
+          // every page here, mapped at the stable VA, no other copy to revoke.
+          bool fast = y && want.andnot(y->resident).empty() && b->stable_chunk == y->chunk && !b->unpublished;
+          if (fast && !dup)
+            for (auto& o : b->res)
+              if (&o != y && o.resident.intersects(want)) fast = false;
+          if (!fast && config().perf_prefetch_enable) {
+            PageMask hint = prefetch_hint(y ? y->resident : PageMask{}, want, b->npages,
+                                          (uint32_t)config().perf_prefetch_threshold);
+            want |= (hint & b->resident_anywhere());
+          }
+          st = fast ? Status::OK : make_resident(c, b, want, dst, dup, cause);
+          if (st == Status::OK) {
+            y = b->find(dst);
+            touch_residency(b, y, cause == Cause::Prefetch && !L);
+            if (L) {
+              b->lease_pins++;
+              y->arena->pin((uint32_t)y->chunk);
+              L->pinned_chunks.emplace_back(y->arena, (uint32_t)y->chunk);
+              L->blocks.push_back(b);
+              leased.push_back(b);
+            }
+          }
+        }
+        if (st != Status::MORE_PROCESSING_REQUIRED) break;
+        finish_ctx(c, out);
+        Reservation rr;
+        Status es = ensure_capacity(c.need_arena, c.need_n, &rr);
+        if (es != Status::OK) {
+          st = es;
+          break;
+        }
+        c.need_arena->free((uint32_t)rr.first, rr.n);
+        c.need_arena = nullptr;
+      }
+      if (st != Status::OK) {
+        // chunks never handed over (error part-way through the group)
+        while (next < need.size()) ga->free(chunks[next++], 1);
+        break;
+      }
+    }
+    // 4) submit the group; finish_ctx remaps the group's VAs (no flush yet)
+    Status fs = finish_ctx(c, out);
+    if (st == Status::OK) st = fs;
+  }
+  // Blocks whose chunk did not change since they were last mapped are already
+  // right; every other one was remapped above: one flush before any use.
+  if (tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
+  if (st != Status::OK) {
+    if (L) {
+      for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);
+      for (Block* b : leased) {
+        std::lock_guard<OrderedMutex> g(b->lock);
+        b->lease_pins--;
+      }
+      L->pinned_chunks.clear();
+      L->blocks.clear();
+    }
+    return st;
+  }
+  if (L) {
+    for (Block* b : L->blocks) L->ready.merge(published_tracker(b));
+    L->dptr = (uint64_t)r->dev_va + off;
   }
   return Status::OK;
 }

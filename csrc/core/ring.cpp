@@ -117,8 +117,15 @@ FenceRef Ring::submit_dma_locked() {
     }
     wcv_.notify_one();
   } else {
-    // Robust-channel style: a failed ring never leaves CPU waiters hanging.
-    __atomic_store_n(sem_, std::max(last, completed_seq()), __ATOMIC_RELEASE);
+    // Robust-channel style: a failed ring never leaves CPU waiters hanging. The
+    // (empty) batch still goes through the worker, so the tracking value is
+    // published in submission order after the batches queued before it: a
+    // direct store here would race the worker's stores of smaller values.
+    {
+      std::lock_guard<std::mutex> g(wm_);
+      work_.push_back(std::move(b));
+    }
+    wcv_.notify_one();
     RT_ERR("ring %s/%d error %s at %s", ring_kind_str(kind_), dev_, status_str(err_), err_desc_.c_str());
     tools_event(ToolsEventType::RingError, Cause::User, Loc::gpu(dev_), Loc::gpu(dev_), dev_, 0, 0, 0);
   }
@@ -153,7 +160,7 @@ void Ring::worker() {
       if (st != Status::INJECTED_ERROR) set_fatal(st, "DMA ring batch failed");
     }
     // Publish even on error (robust channel): waiters then see err_.
-    __atomic_store_n(sem_, b.last, __ATOMIC_RELEASE);
+    publish(b.last);
   }
 }
 
@@ -358,7 +365,10 @@ FenceRef Ring::submit_locked() {
   if (st != Status::OK) {
     if (err_ == Status::OK) err_ = st;
     // Robust-channel style: mark the ring failed; CPU waiters must not hang.
-    __atomic_store_n(sem_, last, __ATOMIC_RELEASE);
+    // Signal kernels of earlier batches may still be queued on the stream:
+    // drain it first so none of them stores a smaller value afterwards.
+    (void)be_->stream_sync(stream_);
+    publish(last);
     RT_ERR("ring %s/%d error %s at %s", ring_kind_str(kind_), dev_, status_str(err_), err_desc_.c_str());
     if (err_ != Status::INJECTED_ERROR) set_fatal(err_, "ring submission failed");
     tools_event(ToolsEventType::RingError, Cause::User, Loc::gpu(dev_), Loc::gpu(dev_), dev_, 0, 0, 0);
@@ -369,6 +379,15 @@ FenceRef Ring::submit_locked() {
   Tools::get().inc(Counter::RingSubmissions);
   last_fence_ = fence_record(be_, dev_, stream_, this, last);
   return last_fence_;
+}
+
+// Monotonic release store of the tracking value (a waiter on seq s must never
+// see the value drop below s once it was published).
+void Ring::publish(uint64_t seq) {
+  if (!sem_) return;
+  uint64_t cur = __atomic_load_n(sem_, __ATOMIC_RELAXED);
+  while (cur < seq && !__atomic_compare_exchange_n(sem_, &cur, seq, true, __ATOMIC_RELEASE, __ATOMIC_RELAXED)) {
+  }
 }
 
 uint64_t Ring::completed_seq() { return sem_ ? __atomic_load_n(sem_, __ATOMIC_ACQUIRE) : 0; }

@@ -249,7 +249,10 @@ Status Runtime::free_range(Range* r) {
     Block* b = bp.get();
     std::lock_guard<OrderedMutex> g(b->lock);
     b->tracker.wait();
-    if (r->dev_va && b->stable_chunk >= 0) be_->vmm_unmap((char*)r->dev_va + b->block_offset(), kBlockSize);
+    if (r->dev_va && b->stable_chunk.load() >= 0) {
+      std::lock_guard<std::mutex> sg(stable_m_);
+      stable_unmap_locked(b);  // after the kernels still reading through the mapping
+    }
     for (auto& x : b->res)
       if (x.chunk >= 0) x.arena->free((uint32_t)x.chunk, 1);
     b->res.clear();
@@ -439,30 +442,66 @@ void Runtime::cpu_map_block(Block* b) {
   b->cpu_ro = ro;
 }
 
-void Runtime::stable_map_block(Block* b) {
+void Runtime::stable_unmap_locked(Block* b) {
+  const int64_t c = b->stable_chunk.load();
+  if (c < 0) return;
   Range* r = b->range;
-  if (!r->dev_va) return;
-  Residency* g = b->find(Loc::gpu(r->stable_dev));
-  int64_t want = (g && g->chunk >= 0) ? g->chunk : -1;
-  if (want == b->stable_chunk) return;
-  char* va = (char*)r->dev_va + b->block_offset();
+  if (b->stable_users.wait() != Status::OK)
+    RT_ERR("stable VA users of range %llu block %llu failed", (unsigned long long)r->id, (unsigned long long)b->index);
+  b->stable_users.clear();
   Tools::get().inc(Counter::VmmRemaps);
-  if (b->stable_chunk >= 0 && be_->vmm_unmap(va, kBlockSize) != Status::OK) {
+  if (be_->vmm_unmap((char*)r->dev_va + b->block_offset(), kBlockSize) != Status::OK) {
     Tools::get().inc(Counter::VmmErrors);
     RT_ERR("stable VA unmap of range %llu block %llu failed: %s", (unsigned long long)r->id,
            (unsigned long long)b->index, be_->last_error().c_str());
   }
-  b->stable_chunk = -1;
-  if (want >= 0) {
-    HbmArena* ha = static_cast<HbmArena*>(g->arena);
-    if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) {
-      b->stable_chunk = want;
-      tlb_dirty_.fetch_or(1u << r->stable_dev);
-    } else {
-      Tools::get().inc(Counter::VmmErrors);
-      RT_ERR("stable VA map of range %llu block %llu to chunk %lld failed: %s", (unsigned long long)r->id,
-             (unsigned long long)b->index, (long long)want, be_->last_error().c_str());
-    }
+  if (HbmArena* ha = devs_[r->stable_dev]->hbm.get())
+    if ((uint64_t)c < ha->stable_owner.size() && ha->stable_owner[c] == b) ha->stable_owner[c] = nullptr;
+  b->stable_chunk.store(-1);
+}
+
+// Point block b's stable VA at its HBM chunk (block lock held). Invariants:
+//  * a mapping is torn down only after the work that may use it finished
+//    (Block::stable_users);
+//  * an evicted block keeps its now-stale mapping until the block comes back
+//    (same chunk: nothing to do) or until another block's stable VA claims
+//    the chunk - HIP's VMM layer tracks one mapping per handle, so a handle is
+//    never mapped at two stable VAs at once (plus the arena's own view).
+void Runtime::stable_map_block(Block* b) {
+  Range* r = b->range;
+  if (!r->dev_va) return;
+  Residency* g = b->find(Loc::gpu(r->stable_dev));
+  const int64_t want = (g && g->chunk >= 0) ? g->chunk : -1;
+  if (want == b->stable_chunk.load()) return;
+  std::lock_guard<std::mutex> sg(stable_m_);
+  if (want == b->stable_chunk.load()) return;
+  if (want < 0) {
+    // Evicted: kernels enqueued before the last lease release may still read
+    // the VA. Unmap at once only when they are done (and not in lazy mode);
+    // otherwise the stale mapping stays - a stray access then reads whatever
+    // the chunk holds instead of faulting.
+    b->stable_users.merge(b->tracker);
+    if (config().stable_lazy_unmap || !b->stable_users.query()) return;
+    stable_unmap_locked(b);
+    return;
+  }
+  HbmArena* ha = static_cast<HbmArena*>(g->arena);
+  // The chunk's handle may still be mapped at another block's (stale) VA.
+  if ((uint64_t)want < ha->stable_owner.size()) {
+    Block* o = ha->stable_owner[want];
+    if (o && o != b) stable_unmap_locked(o);
+  }
+  stable_unmap_locked(b);  // b's own previous mapping (stale, another chunk)
+  char* va = (char*)r->dev_va + b->block_offset();
+  Tools::get().inc(Counter::VmmRemaps);
+  if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) {
+    b->stable_chunk.store(want);
+    if ((uint64_t)want < ha->stable_owner.size()) ha->stable_owner[want] = b;
+    tlb_dirty_.fetch_or(1u << r->stable_dev);
+  } else {
+    Tools::get().inc(Counter::VmmErrors);
+    RT_ERR("stable VA map of range %llu block %llu to chunk %lld failed: %s", (unsigned long long)r->id,
+           (unsigned long long)b->index, (long long)want, be_->last_error().c_str());
   }
 }
 
@@ -947,7 +986,7 @@ Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
   }
   out->read_dup = !dup.empty();
   if (!b->cpu_ro.empty() || !b->cpu_rw.empty()) out->mapped_on.push_back(kCpuProc);
-  if (b->stable_chunk >= 0) out->mapped_on.push_back(r->stable_dev);
+  if (b->stable_chunk.load() >= 0) out->mapped_on.push_back(r->stable_dev);
   if (b->lease_pins)
     for (auto& x : b->res)
       if (x.loc.is_gpu()) out->mapped_on.push_back(x.loc.id);

@@ -69,13 +69,24 @@ struct DevAlloc {
   std::unordered_map<uint64_t, Entry> live;
   struct Managed {
     Range* r;
-    Lease* lease;      // nullptr while parked
+    Lease* lease;      // nullptr while parked (no holds)
     uint64_t size;
+    uint32_t holds = 0;       // allocation hold + op holds (the lease lives while > 0)
+    bool alloc_hold = false;  // the allocation's own hold (dropped by park / the end of the allocating op)
+    bool read_mostly = false;
+    // Long-lived (parameters, buffers, caches): held by ops twice with at
+    // least torch_persistent_births allocations in between. Activations live
+    // for a few ops and get a new address every pass; the transparent mode's
+    // prefetcher keys its trace on persistent operands only.
+    bool persistent = false;
+    bool held_once = false;
+    uint64_t last_hold_birth = 0;
   };
   std::unordered_map<uint64_t, Managed> managed;   // stable VA -> range
   std::vector<std::pair<Range*, Tracker>> deferred;  // freed, waiting for their stream fence
   uint64_t allocated = 0, peak = 0, nallocs = 0, stream_waits = 0;
-  uint64_t managed_bytes = 0, parks = 0, unparks = 0;
+  uint64_t managed_bytes = 0, parks = 0, unparks = 0, op_holds = 0;
+  uint64_t births = 0;  // managed allocations so far (the persistence clock)
 };
 
 std::mutex g_m;
@@ -138,9 +149,9 @@ void reap_deferred(Runtime* rt, DevAlloc* da) {
 
 // Lease the whole range on `device` (resident in HBM at its stable VA, pinned)
 // and make `stream` wait for the copies that bring it there.
-Status lease_on(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, void* stream) {
+Status lease_on(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, void* stream, Access access) {
   Lease* L = nullptr;
-  Status st = rt->acquire(m.r, 0, m.size, device, Access::WRITE, &L);
+  Status st = rt->acquire(m.r, 0, m.size, device, access, &L);
   if (st != Status::OK) return st;
   if (L->remote) {  // thrashing / accessed-by chose a zero-copy mapping: the stable VA would not map it
     rt->release(L, stream);
@@ -154,15 +165,19 @@ Status lease_on(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, voi
 void* managed_alloc(Runtime* rt, DevAlloc* da, size_t size, int device, void* stream) {
   Range* r = nullptr;
   uint64_t bytes = align_up((uint64_t)size, kBlockSize);
-  if (rt->malloc_managed(bytes, RANGE_STABLE_VA | RANGE_NO_CPU_VIEW, "torch", &r, device) != Status::OK)
+  if (rt->malloc_managed(bytes, RANGE_STABLE_VA | RANGE_NO_CPU_VIEW | RANGE_NO_ZERO_FILL, "torch", &r, device) !=
+      Status::OK)
     return nullptr;
   rt->mem_advise(r, 0, bytes, Advice::SET_PREFERRED_LOCATION, Loc::gpu(device), device);
   DevAlloc::Managed m{r, nullptr, bytes};
-  if (lease_on(rt, da, m, device, stream) != Status::OK) {
+  m.holds = 1;
+  m.alloc_hold = true;
+  if (lease_on(rt, da, m, device, stream, Access::WRITE) != Status::OK) {
     rt->free_range(r);
     return nullptr;
   }
   uint64_t addr = (uint64_t)r->dev_va;
+  da->births++;
   da->managed[addr] = m;
   da->managed_bytes += bytes;
   da->allocated += bytes;
@@ -293,8 +308,33 @@ void torch_alloc_reset() {
   g_devs.clear();
 }
 
-// Park / unpark a managed tensor (see the header comment). Returns NOT_FOUND
-// for a pointer that is not a managed allocation's base.
+// Drop one hold of a managed tensor; the last one releases its lease (the
+// stream's queued uses fence any eviction). da->m held.
+Status drop_hold(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, void* stream) {
+  if (m.holds == 0) return Status::OK;
+  if (--m.holds > 0 || !m.lease) return Status::OK;
+  Status st = rt->release(m.lease, stream);
+  m.lease = nullptr;
+  da->parks++;
+  return st;
+}
+
+// Add one hold; the first one leases the tensor (resident at its VA, pinned;
+// the stream waits GPU-side for the copies). da->m held.
+Status add_hold(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, void* stream, Access access) {
+  if (m.holds++ > 0 && m.lease) return Status::OK;
+  Status st = lease_on(rt, da, m, device, stream, m.read_mostly && access == Access::READ ? Access::READ : access);
+  if (st != Status::OK) {
+    m.holds--;
+    return st;
+  }
+  da->unparks++;
+  return Status::OK;
+}
+
+// Park / unpark a managed tensor (see the header comment): park drops the
+// allocation's hold, unpark takes it again. Returns NOT_FOUND for a pointer
+// that is not a managed allocation's base.
 Status torch_park(void* p, int device, void* stream) {
   Runtime* rt = Runtime::get();
   if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
@@ -302,11 +342,9 @@ Status torch_park(void* p, int device, void* stream) {
   std::lock_guard<std::mutex> g(da->m);
   auto it = da->managed.find((uint64_t)p);
   if (it == da->managed.end()) return Status::NOT_FOUND;
-  if (!it->second.lease) return Status::OK;
-  Status st = rt->release(it->second.lease, stream);  // the stream's queued uses fence the eviction
-  it->second.lease = nullptr;
-  da->parks++;
-  return st;
+  if (!it->second.alloc_hold) return Status::OK;
+  it->second.alloc_hold = false;
+  return drop_hold(rt, da, it->second, stream);
 }
 
 Status torch_unpark(void* p, int device, void* stream) {
@@ -316,10 +354,145 @@ Status torch_unpark(void* p, int device, void* stream) {
   std::lock_guard<std::mutex> g(da->m);
   auto it = da->managed.find((uint64_t)p);
   if (it == da->managed.end()) return Status::NOT_FOUND;
-  if (it->second.lease) return Status::OK;
-  Status st = lease_on(rt, da, it->second, device, stream);
-  if (st == Status::OK) da->unparks++;
+  if (it->second.alloc_hold) return Status::OK;
+  Status st = add_hold(rt, da, it->second, device, stream, Access::WRITE);
+  if (st == Status::OK) it->second.alloc_hold = true;
   return st;
+}
+
+// Drop the allocation hold of every managed tensor of `device` (entering the
+// transparent mode: from then on only op holds keep tensors resident).
+void torch_park_all(int device, void* stream) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  for (auto& kv : da->managed) {
+    if (kv.second.alloc_hold) {
+      kv.second.alloc_hold = false;
+      (void)drop_hold(rt, da, kv.second, stream);
+    }
+  }
+}
+
+// Tensor-granular software faults for one dispatched op (the transparent mode,
+// open-gpu-kernel-modules_amd/managed.py): every managed storage the op reads
+// or writes gets an op hold - made resident at its stable VA, pinned, the
+// stream ordered after the copies - before the op is enqueued. Non-managed
+// pointers are ignored. Returns the pointers that were held (for op_end).
+// Reference: the fault -> service -> replay path of
+// uvm_gpu_replayable_faults.c:2906 at tensor granularity, with the operands
+// declared by the dispatcher instead of reported by the MMU.
+Status torch_op_begin(const std::vector<std::pair<uint64_t, bool>>& ptrs, int device, void* stream,
+                      std::vector<uint64_t>* held, std::vector<uint64_t>* persistent) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  if (da->managed.empty()) return Status::OK;
+  // Writers first: a tensor both read and written is leased for writing.
+  std::vector<std::pair<uint64_t, bool>> v;
+  for (auto& pw : ptrs) {
+    if (!da->managed.count(pw.first)) continue;
+    bool dup = false;
+    for (auto& x : v)
+      if (x.first == pw.first) {
+        x.second |= pw.second;
+        dup = true;
+      }
+    if (!dup) v.push_back(pw);
+  }
+  for (auto& pw : v) {
+    auto& m = da->managed[pw.first];
+    Status st = add_hold(rt, da, m, device, stream, pw.second ? Access::WRITE : Access::READ);
+    if (st != Status::OK) {
+      for (uint64_t p : *held) (void)drop_hold(rt, da, da->managed[p], stream);
+      held->clear();
+      return st;
+    }
+    held->push_back(pw.first);
+    if (m.held_once && da->births - m.last_hold_birth >= (uint64_t)std::max<int64_t>(1, config().torch_persistent_births))
+      m.persistent = true;
+    m.held_once = true;
+    m.last_hold_birth = da->births;
+    if (m.persistent) persistent->push_back(pw.first);
+    da->op_holds++;
+  }
+  return Status::OK;
+}
+
+// End of a dispatched op: drop the op holds of `held`, and the allocation hold
+// of every managed operand and output (from its first use as an operand on,
+// a tensor is resident only while an op holds it; a tensor never passed to an
+// op - a library workspace used behind the dispatcher's back - keeps its
+// allocation hold and is never evicted).
+Status torch_op_end(const std::vector<uint64_t>& held, const std::vector<uint64_t>& outs, int device, void* stream) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  Status res = Status::OK;
+  auto drop_alloc = [&](uint64_t p) {
+    auto it = da->managed.find(p);
+    if (it == da->managed.end() || !it->second.alloc_hold) return;
+    it->second.alloc_hold = false;
+    Status st = drop_hold(rt, da, it->second, stream);
+    if (res == Status::OK) res = st;
+  };
+  for (uint64_t p : outs) drop_alloc(p);
+  for (uint64_t p : held) drop_alloc(p);
+  for (uint64_t p : held) {
+    auto it = da->managed.find(p);
+    if (it == da->managed.end()) continue;  // freed inside the op (its free already released the lease)
+    Status st = drop_hold(rt, da, it->second, stream);
+    if (res == Status::OK) res = st;
+  }
+  return res;
+}
+
+// Keep host copies of a managed tensor when it is only read (READ_MOSTLY:
+// evicting a clean duplicate then costs no copy-out).
+Status torch_set_read_mostly(void* p, int device, bool on) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  auto it = da->managed.find((uint64_t)p);
+  if (it == da->managed.end()) return Status::NOT_FOUND;
+  it->second.read_mostly = on;
+  return rt->mem_advise(it->second.r, 0, it->second.size, on ? Advice::SET_READ_MOSTLY : Advice::UNSET_READ_MOSTLY,
+                        Loc::gpu(device), device);
+}
+
+// Layer-ahead prefetch of managed tensors not currently held: queue their
+// H2D copies (no lease, no stream wait; a later op hold finds them resident or
+// waits for the copies). Returns how many prefetches were queued.
+size_t torch_prefetch(const std::vector<uint64_t>& ptrs, int device) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return 0;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  size_t n = 0;
+  for (uint64_t p : ptrs) {
+    auto it = da->managed.find(p);
+    if (it == da->managed.end() || it->second.holds) continue;
+    Tracker t;
+    if (rt->prefetch(it->second.r, 0, it->second.size, Loc::gpu(device), &t, Cause::Prefetch) == Status::OK) ++n;
+  }
+  return n;
+}
+
+uint64_t torch_managed_size(void* p, int device) {
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  auto it = da->managed.find((uint64_t)p);
+  return it == da->managed.end() ? 0 : it->second.size;
+}
+
+bool torch_is_managed(void* p, int device) {
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  return da->managed.count((uint64_t)p) != 0;
 }
 
 // (active, parked bytes, parks, unparks) of the managed tensors.
@@ -327,7 +500,7 @@ void torch_managed_stats(int device, uint64_t* active, uint64_t* parked, uint64_
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);
   *active = *parked = 0;
-  for (auto& kv : da->managed) (kv.second.lease ? *active : *parked) += kv.second.size;
+  for (auto& kv : da->managed) (kv.second.holds ? *active : *parked) += kv.second.size;
   *parks = da->parks;
   *unparks = da->unparks;
 }

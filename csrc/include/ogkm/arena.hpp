@@ -52,6 +52,16 @@ struct Reservation {
   int64_t first = -1;
   uint32_t n = 0;
   std::vector<uint32_t> victims;  // chunks that must be evicted before commit
+  // Scattered reservation (reserve_scattered): exactly these chunks, in no
+  // particular order; empty = the contiguous window [first, first + n).
+  std::vector<uint32_t> list;
+  template <class F>
+  void for_each(F f) const {
+    if (!list.empty())
+      for (uint32_t k : list) f(k);
+    else
+      for (uint32_t i = 0; i < n; ++i) f((uint32_t)first + i);
+  }
 };
 
 class ChunkArena {
@@ -72,6 +82,10 @@ class ChunkArena {
   Status alloc(uint32_t n, Block* owner_for_all, int64_t hint, uint32_t* first, bool pin = false);
   // Reserve a window of n contiguous chunks, possibly containing evictable chunks.
   Status reserve(uint32_t n, Reservation* r);
+  // Reserve n chunks anywhere (stable-VA blocks are mapped one by one and need
+  // no contiguity): free chunks first, then victims in reserve(1)'s order.
+  // All or nothing.
+  Status reserve_scattered(uint32_t n, Reservation* r);
   void commit(const Reservation& r, bool pin = false);  // window -> ALLOCATED (owners set later)
   void cancel(const Reservation& r);                // give the window back
   void free(uint32_t first, uint32_t n);
@@ -130,6 +144,7 @@ class ChunkArena {
   uint32_t nchunks_ = 0;
 
  private:
+  int32_t pick_victim_locked();  // coldest evictable chunk (reserve(1) order), -1 = none
   void lru_remove(uint32_t i);
   void lru_push_tail(uint32_t i, uint8_t list);
   void take_run(uint32_t first, uint32_t n);  // remove [first,first+n) from free runs
@@ -160,6 +175,12 @@ class HbmArena : public ChunkArena {
   bool vmm() const { return !handles_.empty(); }
   uint64_t handle(uint32_t i) const { return handles_.empty() ? 0 : handles_[i]; }
   Status init_status() const { return init_; }
+  // Block whose stable VA currently maps chunk i's handle (besides the arena's
+  // own view), nullptr = none. At most one stable VA maps a handle at a time:
+  // HIP's VMM layer tracks one mapping per handle, so unmapping one of two
+  // stable VAs of a handle can tear down the other (tools/probe_vmm_multimap.hip).
+  // Guarded by Runtime::stable_m_.
+  std::vector<Block*> stable_owner;
 
  private:
   Backend* be_;

@@ -53,6 +53,9 @@ namespace ogkm {
   X(perf_workingset_active_pct, 95, "HBM chunks of refaulted GPU-preferred blocks (plus pinned chunks) protected from eviction, percent of the arena (0 = plain LRU)") \
   X(hbm_budget_mb, 0, "per-GPU HBM budget for the arena in MB (0 = 90% of free)")                   \
   X(hbm_provider, 0, "0=slab (one hipMalloc) 1=vmm (hipMemCreate handles, enables stable VA)")       \
+  X(stable_lazy_unmap, 0, "stable VAs of evicted blocks stay mapped to their old chunk until the block returns (saves the unmap; a stray access reads stale data instead of faulting)") \
+  X(stable_batch_blocks, 32, "stable-VA placement: 2 MB blocks per eviction / fill / remap group (pipelined)") \
+  X(torch_persistent_births, 64, "transparent mode: a managed tensor held twice with this many allocations in between is long-lived (keys the op-trace prefetcher)") \
   X(torch_alloc_managed_min_mb, 0, "pluggable allocator: allocations >= this many MB are evictable stable-VA managed ranges (0 = off; needs hbm_provider=1)") \
   X(host_node, -1, "NUMA node for the host tier (-1 = NUMA node of the first local GPU)")             \
   X(local_devices, 0, "bitmask of the GPUs this process manages (0 = all; one process per GPU: 1<<rank)") \
@@ -80,6 +83,7 @@ namespace ogkm {
   X(cxl_emulate_node, -1, "treat this NUMA node as CXL when no CXL hardware (-1 = off)")             \
   /* debug */                                                                                        \
   X(lock_check, 0, "enable the lock-order checker")                                                  \
+  X(fake_dma_delay_us, 0, "fake backend: microseconds every SDMA batch takes (ordering tests)")       \
   X(leak_check, 1, "track outstanding arena bytes")                                                  \
   X(release_asserts, 1, "release asserts set the sticky fatal error")                                \
   X(tools_queue_entries, 4096, "entries per tools event queue")

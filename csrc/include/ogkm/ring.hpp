@@ -115,6 +115,7 @@ class Ring {
   FenceRef submit_dma_locked();
   void worker();
   Status run_batch(Batch& b);
+  void publish(uint64_t seq);
   Backend* be_;
   int dev_;
   RingKind kind_;

@@ -267,6 +267,13 @@ class Runtime {
   Status make_resident(Ctx& c, Block* b, const PageMask& pages, Loc dst, bool read_dup, Cause cause);
   Status populate(Ctx& c, Block* b, Loc dst, int64_t chunk_hint, Residency** out);
   Status evict_chunk(ChunkArena* a, uint32_t chunk);
+  Status evict_batch(ChunkArena* a, const std::vector<uint32_t>& victims);
+  Status evict_one(Ctx& c, ChunkArena* a, uint32_t chunk, bool* detached);
+  void seal_evictions(Ctx& c, ChunkArena* a, const std::vector<uint32_t>& victims);
+  // GPU residency of a stable-VA range: any HBM chunk per block (the VA is
+  // mapped block by block), victims evicted in batches, one translation flush.
+  Status place_stable(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup, Lease* L,
+                      Tracker* out, Cause cause);
   Status ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool pin = false);
   // owner / pin are applied atomically with the allocation (see ChunkArena::alloc).
   Status alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* first, Block* owner = nullptr,
@@ -274,6 +281,9 @@ class Runtime {
   Loc demotion_target(const Loc& from);
   void cpu_map_block(Block* b);  // refresh CPU view protections
   void stable_map_block(Block* b);
+  // stable_m_ held: tear down b's stable-VA mapping after its users finished.
+  void stable_unmap_locked(Block* b);
+  std::mutex stable_m_;  // stable-VA mappings (Block::stable_chunk / stable_users, HbmArena::stable_owner)
   // Flush GPU translations of devices whose stable VAs were remapped since the
   // last flush (before any consumer of the new mapping can run).
   void flush_translations();
@@ -347,6 +357,7 @@ struct Runtime::Ctx {
   ChunkArena* need_arena = nullptr;   // set on MORE_PROCESSING_REQUIRED
   uint32_t need_n = 0;
   std::vector<std::pair<Ring*, Fence*>> waited;  // GPU-side waits already queued
+  bool defer_flush = false;           // finish_ctx leaves the translation flush to the caller
   // Migration invalidations are applied only once the copies that replace the
   // data were submitted successfully; a failed submission invalidates the
   // destination instead, so a link/copy error never loses the source.

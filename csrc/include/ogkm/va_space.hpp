@@ -92,7 +92,14 @@ class Block {
   PageMask cpu_ro, cpu_rw;     // CPU view protection state
   ChunkArena* cpu_arena = nullptr;  // host/CXL chunk currently mapped in the CPU window
   int64_t cpu_chunk = -1;
-  int64_t stable_chunk = -1;   // HBM chunk VMM-mapped at the stable device VA (-1 = none)
+  // HBM chunk VMM-mapped at the stable device VA (-1 = none). Written under
+  // Runtime::stable_m_ (a remap of another block may tear a stale mapping down).
+  std::atomic<int64_t> stable_chunk{-1};
+  // Work that may still access the stable VA through its current mapping (the
+  // block's tracker - copies and lease-release fences - when it was evicted):
+  // the mapping is torn down only once it completed (a kernel queued before the
+  // release would otherwise fault on an unmapped VA). Guarded by Runtime::stable_m_.
+  Tracker stable_users;
   uint32_t lease_pins = 0;
   uint32_t gpu_evictions = 0;  // times an HBM copy of this block was evicted (refault detection)
   uint64_t gpu_evicted_at = 0; // the HBM arena's eviction count when it last was (refault distance)
@@ -126,6 +133,10 @@ enum RangeFlags : uint32_t {
   // Contents are bf16 and read-only on GPUs: host / CXL copies are stored
   // BF12-packed (lossless) and decoded by the H2D copy kernel. Implies no CPU view.
   RANGE_COMPRESS_BF16 = 1u << 2,
+  // Never-populated pages need no zero-fill (torch allocations: the caller
+  // writes before it reads, as with any caching allocator). Saves a memset per
+  // fresh block - and keeps fresh-block fills kernel-free on the copy engines.
+  RANGE_NO_ZERO_FILL = 1u << 3,
 };
 
 class Range {

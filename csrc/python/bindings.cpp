@@ -23,6 +23,14 @@ void torch_free(void* p, int device, void* stream);
 Status torch_park(void* p, int device, void* stream);
 Status torch_unpark(void* p, int device, void* stream);
 void torch_managed_stats(int device, uint64_t* active, uint64_t* parked, uint64_t* parks, uint64_t* unparks);
+void torch_park_all(int device, void* stream);
+Status torch_op_begin(const std::vector<std::pair<uint64_t, bool>>& ptrs, int device, void* stream,
+                      std::vector<uint64_t>* held, std::vector<uint64_t>* persistent);
+Status torch_op_end(const std::vector<uint64_t>& held, const std::vector<uint64_t>& outs, int device, void* stream);
+Status torch_set_read_mostly(void* p, int device, bool on);
+bool torch_is_managed(void* p, int device);
+size_t torch_prefetch(const std::vector<uint64_t>& ptrs, int device);
+uint64_t torch_managed_size(void* p, int device);
 }  // namespace ogkm
 
 namespace {
@@ -663,6 +671,12 @@ PYBIND11_MODULE(_ogkm, m) {
     check(r->submit()->wait(), "ring_gather");
   });
   m.def("ring_stream", [](int dev, int kind) { return (uint64_t)ring_of(dev, kind)->stream(); });
+  m.def("ring_wait_seq", [](int dev, int kind, uint64_t seq) {
+    Ring* r = ring_of(dev, kind);
+    py::gil_scoped_release nogil;
+    return std::string(status_str(r->wait_seq(seq)));
+  });
+  m.def("ring_completed", [](int dev, int kind) { return ring_of(dev, kind)->completed_seq(); });
 
   // ---- tools
   m.def("tools_create_queue", [](uint32_t entries, uint32_t mask, const std::string& shm) {
@@ -1064,6 +1078,36 @@ PYBIND11_MODULE(_ogkm, m) {
   m.def("torch_unpark", [](uint64_t p, int dev, uint64_t stream) {
     check(torch_unpark((void*)p, dev, (void*)stream), "torch_unpark");
   }, py::arg("ptr"), py::arg("dev"), py::arg("stream") = 0);
+  m.def("torch_park_all", [](int dev, uint64_t stream) { torch_park_all(dev, (void*)stream); },
+        py::arg("dev"), py::arg("stream") = 0);
+  m.def("torch_op_begin", [](const std::vector<std::pair<uint64_t, bool>>& ptrs, int dev, uint64_t stream) {
+    std::vector<uint64_t> held, persistent;
+    Status st;
+    {
+      py::gil_scoped_release nogil;
+      st = torch_op_begin(ptrs, dev, (void*)stream, &held, &persistent);
+    }
+    check(st, "torch_op_begin");
+    return py::make_tuple(held, persistent);
+  });
+  m.def("torch_op_end", [](const std::vector<uint64_t>& held, const std::vector<uint64_t>& outs, int dev,
+                           uint64_t stream) {
+    Status st;
+    {
+      py::gil_scoped_release nogil;
+      st = torch_op_end(held, outs, dev, (void*)stream);
+    }
+    check(st, "torch_op_end");
+  });
+  m.def("torch_set_read_mostly", [](uint64_t p, int dev, bool on) {
+    check(torch_set_read_mostly((void*)p, dev, on), "torch_set_read_mostly");
+  });
+  m.def("torch_is_managed", [](uint64_t p, int dev) { return torch_is_managed((void*)p, dev); });
+  m.def("torch_prefetch", [](const std::vector<uint64_t>& ptrs, int dev) {
+    py::gil_scoped_release nogil;
+    return torch_prefetch(ptrs, dev);
+  });
+  m.def("torch_managed_size", [](uint64_t p, int dev) { return torch_managed_size((void*)p, dev); });
   m.def("torch_managed_stats", [](int dev) {
     uint64_t a, p, np, nu;
     torch_managed_stats(dev, &a, &p, &np, &nu);

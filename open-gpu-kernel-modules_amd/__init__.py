@@ -14,6 +14,7 @@ Layout
   tools        event queues + counters (UVM tools analog)
   checkpoint   residency-map checkpoint format
   allocator    PyTorch pluggable allocator on the HBM arena
+  managed      transparent mode: tensor-granular software faults for unmodified torch code
   p2p          peer-memory client: pinned exports, dma-buf, IPC (nvidia-peermem analog)
   ops/         HIP kernel entry points (copies, managed gather) + decode ops
   models/      Llama-3 decode engine with tiered (oversubscribed) weights
@@ -28,6 +29,7 @@ __version__ = "0.1.0"
 
 from . import _native  # noqa: E402,F401  (fails loudly if the native core is missing)
 from . import rt, tools, checkpoint, cxl, allocator, p2p  # noqa: E402,F401
+from .managed import managed  # noqa: E402,F401
 from . import utils, ops, parallel, models  # noqa: E402,F401
 
 # Register the importable alias "ogkm" for the package and every loaded submodule.

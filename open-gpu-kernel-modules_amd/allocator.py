@@ -91,5 +91,23 @@ def parked(*tensors):
         unpark(*tensors)
 
 
+def set_read_mostly(*tensors, on: bool = True) -> None:
+    """Managed tensors that are only read keep their host copy while resident
+    in HBM (READ_MOSTLY / read duplication): evicting them costs no copy-out."""
+    for t in tensors:
+        p, d = _base(t)
+        lib.torch_set_read_mostly(p, d, on)
+
+
+def is_managed(t) -> bool:
+    p, d = _base(t)
+    return lib.torch_is_managed(p, d)
+
+
+def park_all(device: int = 0) -> None:
+    """Drop the allocation hold of every managed tensor of ``device``."""
+    lib.torch_park_all(device, _stream(device))
+
+
 def managed_stats(device: int = 0) -> dict:
     return lib.torch_managed_stats(device)

@@ -1,0 +1,111 @@
+"""Worker for tests/test_managed_mode_gpu.py: a stock torch.nn transformer run
+either plainly (torch's own allocator, everything resident) or under
+``ogkm.managed()`` with its parameters oversubscribing the HBM arena; saves the
+outputs / gradients / updated parameters for a bitwise comparison.
+
+    python managed_mode_worker.py plain|managed OUT.pt [--lazy]
+"""
+from __future__ import annotations
+
+import os
+import resource
+import sys
+import time
+
+resource.setrlimit(resource.RLIMIT_CORE, (0, 0))  # a crash must not spend minutes writing a core
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+import torch  # noqa: E402
+
+D, FF, LAYERS, HEADS = 1024, 4096, 8, 16
+BATCH, SEQ = 4, 128
+ARENA_MB = 192
+
+
+def build():
+    torch.manual_seed(0)
+    layer = torch.nn.TransformerEncoderLayer(D, HEADS, FF, dropout=0.0, batch_first=True)
+    model = torch.nn.TransformerEncoder(layer, LAYERS, enable_nested_tensor=False)
+    x = torch.randn(BATCH, SEQ, D)
+    return model, x
+
+
+def run(model, x, log=False):
+    """Inference pass + one training step (forward, backward, SGD)."""
+    def say(m):
+        if log:
+            print(m, flush=True)
+    model.eval()
+    with torch.no_grad():
+        y_inf = model(x)
+    say("inference done")
+    model.train()
+    opt = torch.optim.SGD(model.parameters(), lr=1e-3)
+    y = model(x)
+    say("train forward done")
+    loss = y.float().pow(2).mean()
+    loss.backward()
+    say("backward done")
+    opt.step()
+    say("step done")
+    out = {"y_inf": y_inf, "loss": loss.detach()}
+    for name, p in model.named_parameters():
+        out["p." + name] = p.detach()
+        out["g." + name] = p.grad.detach()
+    return {k: v.cpu() for k, v in out.items()}
+
+
+def main() -> None:
+    which, path = sys.argv[1], sys.argv[2]
+    if which == "plain":
+        model, x = build()
+        res = run(model.cuda(), x.cuda())
+        torch.cuda.synchronize()
+        torch.save(res, path)
+        print("PLAIN_OK", len(res))
+        return
+    import faulthandler
+    import threading
+
+    import ogkm
+    from ogkm import allocator, rt
+
+    # Hang diagnostics (stderr): Python stacks after 60 s, ring progress every 10 s.
+    faulthandler.dump_traceback_later(60, exit=False)
+
+    def watchdog():
+        while True:
+            time.sleep(10)
+            try:
+                rings = [(r["kind"], r["submitted"], r["completed"]) for r in rt.stats()["rings"] if r["dev"] == 0]
+                print("WATCHDOG", round(time.perf_counter() - t0, 1), rings, file=sys.stderr, flush=True)
+            except Exception as e:  # noqa: BLE001
+                print("WATCHDOG error", e, file=sys.stderr, flush=True)
+
+    t0 = time.perf_counter()
+    threading.Thread(target=watchdog, daemon=True).start()
+
+    allocator.enable(managed_min_mb=1)
+    rt.init("hip", hbm_budget={0: ARENA_MB << 20}, stable_lazy_unmap=int("--lazy" in sys.argv))
+    model, x = build()
+    param_bytes = sum(p.numel() * p.element_size() for p in model.parameters())
+    mode = ogkm.managed()
+    t0 = time.perf_counter()
+    with mode:
+        model = model.cuda()
+        print("model on gpu", flush=True)
+        res = run(model, x.cuda(), log=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    torch.save(res, path)
+    st = rt.stats()
+    print("MANAGED_OK", {"param_mb": param_bytes >> 20, "arena_mb": ARENA_MB, "ops": mode.ops,
+                         "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches,
+                         "evictions": st["evictions"], "htd_mb": st["bytes_xfer_htd"] >> 20,
+                         "dth_mb": st["bytes_xfer_dth"] >> 20, "vmm_remaps": st["vmm_remaps"],
+                         "tlb_flushes": st["tlb_flushes"], "vmm_errors": st["vmm_errors"], "seconds": round(dt, 3)})
+
+
+if __name__ == "__main__":
+    main()

@@ -121,3 +121,87 @@ def test_partially_evicted_tensor_relocates_under_its_address(managed_rt):
     assert np.array_equal(_read(a, n // 4), ref)
     for p in (a, c):
         lib.torch_free(p, 0)
+
+
+def test_op_holds_make_operands_resident_and_evictable_after(managed_rt):
+    """The transparent mode's op protocol (torch_op_begin / torch_op_end): an
+    op's managed operands are resident (and pinned) between begin and end, the
+    outputs it allocated lose their allocation hold at end, and afterwards
+    every tensor is evictable - 6 x 8 MB cycled through a 32 MB arena."""
+    n = 8 * MB
+    ptrs, refs = [], []
+    for i in range(6):
+        p = lib.torch_alloc(n, 0)
+        ref = np.full(n // 4, 100 + i, dtype=np.int32)
+        _write(p, ref)
+        held, _ = lib.torch_op_begin([(p, True)], 0, 0)
+        assert held == [p]
+        lib.torch_op_end(held, [p], 0, 0)  # p is this op's output: its alloc hold goes too
+        ptrs.append(p)
+        refs.append(ref)
+    st = lib.torch_managed_stats(0)
+    assert st["active_bytes"] == 0 and st["parked_bytes"] == 6 * n
+    for rnd in range(2):
+        for i, p in enumerate(ptrs):
+            q = ptrs[(i + 1) % 6]
+            held, _ = lib.torch_op_begin([(p, False), (q, True), (12345, True)], 0, 0)  # non-managed ptr ignored
+            assert sorted(held) == sorted([p, q])
+            assert np.array_equal(_read(p, n // 4), refs[i])
+            assert lib.torch_managed_stats(0)["active_bytes"] == 2 * n
+            lib.torch_op_end(held, [], 0, 0)
+    assert lib.stats()["evictions"] > 6
+    for p in ptrs:
+        lib.torch_free(p, 0)
+
+
+def test_op_hold_nests_with_allocation_hold(managed_rt):
+    n = 8 * MB
+    p = lib.torch_alloc(n, 0)  # allocation hold
+    held, pers = lib.torch_op_begin([(p, False), (p, True)], 0, 0)  # duplicate operand: one hold
+    assert held == [p] and pers == []
+    lib.torch_op_end(held, [], 0, 0)
+    # its first use as an operand also ended its allocation hold
+    assert lib.torch_managed_stats(0)["active_bytes"] == 0
+    lib.configure("torch_persistent_births", 2)
+    tmp = [lib.torch_alloc(4 * MB, 0) for _ in range(2)]  # two allocations later ...
+    held, pers = lib.torch_op_begin([(p, False)], 0, 0)
+    assert pers == [p]  # ... the second hold marks p long-lived (a parameter, not an activation)
+    lib.torch_op_end(held, [], 0, 0)
+    q = tmp[0]
+    held, pers = lib.torch_op_begin([(q, False)], 0, 0)
+    lib.torch_op_end(held, [], 0, 0)
+    held, pers = lib.torch_op_begin([(q, False)], 0, 0)
+    assert pers == []  # held twice with no allocation in between: short-lived
+    lib.torch_op_end(held, [], 0, 0)
+    for t in tmp:
+        lib.torch_free(t, 0)
+    assert lib.torch_managed_size(p, 0) == n and lib.torch_is_managed(p, 0)
+    lib.torch_free(p, 0)
+
+
+@pytest.mark.parametrize("lazy", [0, 1])
+def test_stable_placement_batches_evictions(managed_rt, lazy):
+    """A stable-VA lease needs no contiguous extent: blocks take any chunk,
+    victims go out as one batch per group, and a block that returns to its old
+    chunk needs no remap (lazy unmap keeps the mapping)."""
+    lib.configure("stable_lazy_unmap", lazy)
+    lib.configure("stable_batch_blocks", 2)
+    try:
+        n = 12 * MB
+        a = lib.torch_alloc(n, 0)
+        _write(a, np.arange(n // 4, dtype=np.int32))
+        lib.torch_park(a, 0)
+        b = lib.torch_alloc(24 * MB, 0)  # 12 + 24 > 32: part of a is evicted
+        lib.torch_park(b, 0)
+        s0 = lib.stats()
+        lib.torch_unpark(a, 0)
+        assert np.array_equal(_read(a, n // 4), np.arange(n // 4, dtype=np.int32))
+        s1 = lib.stats()
+        assert s1["evictions"] > s0["evictions"]
+        assert s1["vmm_errors"] == 0
+        lib.torch_park(a, 0)
+        for p in (a, b):
+            lib.torch_free(p, 0)
+    finally:
+        lib.configure("stable_lazy_unmap", 0)
+        lib.configure("stable_batch_blocks", 32)

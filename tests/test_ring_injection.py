@@ -65,6 +65,35 @@ def test_copy_drop_injection_reports_error(fake_rt):
     assert int(b.read().min()) == 1
 
 
+def test_copy_drop_behind_queued_batch_never_hangs_waiters(fake_rt):
+    """A copy dropped while an earlier SDMA batch is still queued: the ring's
+    tracking value stays monotonic (the error batch is published in order after
+    the slow one), so waits on every sequence number return - the error, not a
+    hang (the direct store raced the worker's smaller stores)."""
+    import time
+
+    src = torch.ones(4 * MB, dtype=torch.uint8)
+    dst = torch.zeros(4 * MB, dtype=torch.uint8)
+    rt.configure(fake_dma_delay_us=200_000)
+    try:
+        s1 = lib.ring_copy(0, CPU_TO_GPU, dst.data_ptr(), src.data_ptr(), 2 * MB, False)
+        lib.inject("copy_drop", 1)
+        s2 = lib.ring_copy(0, CPU_TO_GPU, dst.data_ptr() + 2 * MB, src.data_ptr() + 2 * MB, 2 * MB, False)
+        assert s2 > s1
+        t0 = time.time()
+        assert lib.ring_wait_seq(0, CPU_TO_GPU, s2) == "INJECTED_ERROR"
+        assert lib.ring_wait_seq(0, CPU_TO_GPU, s1) == "INJECTED_ERROR"
+        assert time.time() - t0 < 5
+        # The value never moves backwards once published.
+        c = lib.ring_completed(0, CPU_TO_GPU)
+        assert c >= s2
+        time.sleep(0.3)
+        assert lib.ring_completed(0, CPU_TO_GPU) >= c
+    finally:
+        rt.configure(fake_dma_delay_us=0)
+        lib.ring_clear_error(0, CPU_TO_GPU)
+
+
 def test_failure_after_submission_is_caught_at_completion(fake_rt):
     """A copy that fails after it was submitted (ECC / link error, faulting
     kernel) is caught when its completion is checked: the fence wait returns the
