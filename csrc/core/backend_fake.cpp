@@ -347,6 +347,16 @@ class FakeBackend : public Backend {
     run(s, [addr, v] { __atomic_store_n(addr, v, __ATOMIC_RELEASE); });
     return Status::OK;
   }
+  Status debug_touch(void* s, uint64_t ptr, uint64_t bytes, uint32_t delay_us) override {
+    run(s, [ptr, bytes, delay_us] {
+      if (delay_us) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
+      for (uint64_t o = 0; o < bytes; o += 4096) {
+        volatile uint32_t* w = (volatile uint32_t*)(ptr + o);
+        *w = *w + 1;
+      }
+    });
+    return Status::OK;
+  }
   Status wait_value(void* s, uint64_t* addr, uint64_t v) override {
     auto f = [addr, v] {
       while (__atomic_load_n(addr, __ATOMIC_ACQUIRE) < v) std::this_thread::yield();

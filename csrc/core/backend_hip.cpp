@@ -40,6 +40,8 @@
 #include "ogkm/codec.hpp"
 #include "ogkm/config.hpp"
 #include "ogkm/kernels.hpp"
+#include "ogkm/events.hpp"
+#include "ogkm/runtime.hpp"
 
 namespace ogkm {
 
@@ -631,10 +633,29 @@ class HipBackend : public Backend {
     v->push_back(a);
     return HSA_STATUS_SUCCESS;
   }
+  // GPU memory faults (an illegal address, a page not mapped) reported by ROCr:
+  // log the faulting VA with what the runtime knows about it (which range /
+  // block / chunk), the attribution the reference prints for fatal faults.
+  static hsa_status_t fault_event_cb(const hsa_amd_event_t* e, void*) {
+    if (!e || e->event_type != HSA_AMD_GPU_MEMORY_FAULT_EVENT) return HSA_STATUS_SUCCESS;
+    const uint64_t va = e->memory_fault.virtual_address;
+    const uint32_t why = e->memory_fault.fault_reason_mask;
+    Runtime* rt = Runtime::get();
+    std::string what = rt ? rt->describe_device_address(va) : std::string("(no runtime)");
+    fprintf(stderr, "[ogkm FAULT] GPU memory fault at VA %#llx reason %#x%s%s%s: %s\n", (unsigned long long)va, why,
+            (why & HSA_AMD_MEMORY_FAULT_PAGE_NOT_PRESENT) ? " page-not-present" : "",
+            (why & HSA_AMD_MEMORY_FAULT_READ_ONLY) ? " read-only" : "",
+            (why & HSA_AMD_MEMORY_FAULT_IMPRECISE) ? " imprecise" : "", what.c_str());
+    fflush(stderr);
+    Tools::get().inc(Counter::VmmErrors);
+    return HSA_STATUS_SUCCESS;
+  }
+
   void dma_init() {
     std::call_once(dma_once_, [this] {
       dma_.assign(ndev_, DmaDev{});
       if (hsa_init() != HSA_STATUS_SUCCESS) return;  // agents are resolved for every engine choice
+      (void)hsa_amd_register_system_event_handler(fault_event_cb, nullptr);
       std::vector<hsa_agent_t> agents;
       if (hsa_iterate_agents(dma_agent_cb, &agents) != HSA_STATUS_SUCCESS) return;
       hsa_agent_t cpu{0};

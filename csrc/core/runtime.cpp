@@ -201,6 +201,7 @@ Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string&
     if (st != Status::OK) return st;
     r->dev_va = va;
     r->stable_dev = stable_dev;
+    vs_.dev_tree[(uint64_t)va] = r.get();
   }
   if (r->cpu_view) {
     vs_.tree[r->addr()] = r.get();
@@ -258,7 +259,10 @@ Status Runtime::free_range(Range* r) {
     b->res.clear();
     Tools::get().bus().notify(PerfEventData{PerfEvent::BLOCK_DESTROY, r->id, b->index});
   }
-  if (r->dev_va) be_->va_free(r->dev_va, r->cpu_view_bytes);
+  if (r->dev_va) {
+    vs_.dev_tree.erase((uint64_t)r->dev_va);
+    be_->va_free(r->dev_va, r->cpu_view_bytes);
+  }
   if (r->ext_owned && r->ext_ptr) be_->hbm_free(r->ext_dev, (void*)r->ext_ptr, align_up(r->size, kBlockSize));
   if (r->group) {
     auto& v = r->group->ranges;
@@ -503,6 +507,48 @@ void Runtime::stable_map_block(Block* b) {
     RT_ERR("stable VA map of range %llu block %llu to chunk %lld failed: %s", (unsigned long long)r->id,
            (unsigned long long)b->index, (long long)want, be_->last_error().c_str());
   }
+}
+
+// Everything the runtime knows about a device address - for GPU memory-fault
+// reports (the analog of the reference's fatal-fault reporting with the
+// faulting VA, uvm_gpu_replayable_faults.c:2495-2875). Called from a ROCr
+// thread: it only try-locks, so it never waits for a lock a stuck thread holds.
+std::string Runtime::describe_device_address(uint64_t va) {
+  char buf[512];
+  std::string out;
+  if (!vs_.lock.try_lock_shared()) return "(VA space busy)";
+  auto it = vs_.dev_tree.upper_bound(va);
+  if (it != vs_.dev_tree.begin()) {
+    --it;
+    Range* r = it->second;
+    if (va >= it->first && va < it->first + r->cpu_view_bytes) {
+      Block* b = r->block((va - it->first) >> kBlockShift);
+      snprintf(buf, sizeof buf, "stable VA of range %llu '%s' (%llu B) block %llu: stable_chunk %lld", (unsigned long long)r->id,
+               r->name.c_str(), (unsigned long long)r->size, (unsigned long long)b->index,
+               (long long)b->stable_chunk.load());
+      out = buf;
+      if (b->lock.try_lock()) {
+        for (auto& x : b->res) {
+          snprintf(buf, sizeof buf, "; resident %s chunk %lld pages %u", x.loc.str().c_str(), (long long)x.chunk,
+                   x.resident.count());
+          out += buf;
+        }
+        snprintf(buf, sizeof buf, "; lease_pins %u tracker %zu stable_users %zu", (unsigned)b->lease_pins,
+                 b->tracker.size(), b->stable_users.size());
+        out += buf;
+        b->lock.unlock();
+      }
+    }
+  }
+  for (auto& d : devs_) {
+    HbmArena* ha = d->hbm_live.load();
+    if (!ha || va < ha->base() || va >= ha->base() + ((uint64_t)ha->nchunks() << kBlockShift)) continue;
+    snprintf(buf, sizeof buf, "%sarena view of gpu %d chunk %lld", out.empty() ? "" : "; ", d->id,
+             (long long)ha->chunk_of(va));
+    out += buf;
+  }
+  vs_.lock.unlock_shared();
+  return out.empty() ? "(not a runtime address)" : out;
 }
 
 void Runtime::flush_translations() {

@@ -33,6 +33,7 @@
 // completes (no host stall in free).
 // The C entry points ogkm_torch_alloc / ogkm_torch_free are what
 // CUDAPluggableAllocator dlsym()s.
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -186,6 +187,22 @@ void* managed_alloc(Runtime* rt, DevAlloc* da, size_t size, int device, void* st
 
 }  // namespace
 
+// Out of arena memory: free every deferred managed range now (host-waiting
+// for the streams that last used them) - the caching-allocator move of freeing
+// its cache and synchronizing before reporting OOM. da->m held.
+static bool drain_deferred(Runtime* rt, DevAlloc* da) {
+  if (da->deferred.empty()) return false;
+  for (auto& d : da->deferred) {
+    (void)d.second.wait();
+    rt->free_range(d.first);
+  }
+  da->deferred.clear();
+  return true;
+}
+
+static void* torch_alloc_locked(Runtime* rt, ChunkArena* a, DevAlloc* da, size_t size, int device, void* stream);
+
+
 void* torch_alloc(size_t size, int device, void* stream) {
   Runtime* rt = Runtime::get();
   if (!rt || !rt->is_local(device)) return nullptr;
@@ -193,9 +210,16 @@ void* torch_alloc(size_t size, int device, void* stream) {
   if (!a) return nullptr;
   if (size == 0) size = 1;
   DevAlloc* da = dev_alloc(device);
-  int cls = class_of(size);
   std::lock_guard<std::mutex> g(da->m);
   if (!da->deferred.empty()) reap_deferred(rt, da);
+  void* p = torch_alloc_locked(rt, a, da, size, device, stream);
+  if (!p && drain_deferred(rt, da)) p = torch_alloc_locked(rt, a, da, size, device, stream);
+  return p;
+}
+
+
+static void* torch_alloc_locked(Runtime* rt, ChunkArena* a, DevAlloc* da, size_t size, int device, void* stream) {
+  int cls = class_of(size);
   const int64_t mmin = config().torch_alloc_managed_min_mb;
   if (mmin > 0 && size >= ((uint64_t)mmin << 20) && static_cast<HbmArena*>(a)->vmm()) {
     void* p = managed_alloc(rt, da, size, device, stream);
@@ -250,6 +274,7 @@ void* torch_alloc(size_t size, int device, void* stream) {
   da->peak = std::max(da->peak, da->allocated);
   return (void*)addr;
 }
+
 
 void torch_free(void* p, int device, void* stream) {
   Runtime* rt = Runtime::get();
@@ -518,7 +543,22 @@ void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t
 
 extern "C" {
 __attribute__((visibility("default"))) void* ogkm_torch_alloc(size_t size, int device, void* stream) {
-  return ogkm::torch_alloc(size, device, stream);
+  void* p = ogkm::torch_alloc(size, device, stream);
+  if (!p && size) {
+    // torch's pluggable-allocator path does not check for null: a null
+    // tensor would reach a kernel and fault the GPU. Fail loudly on the CPU.
+    ogkm::Runtime* rt = ogkm::Runtime::get();
+    ogkm::ChunkArena* a = rt ? rt->arena_for(ogkm::Loc::gpu(device)) : nullptr;
+    ogkm::ChunkArena::Stats st = a ? a->stats() : ogkm::ChunkArena::Stats{};
+    RT_ERR("torch allocation of %zu bytes on gpu %d failed: HBM arena %llu MB, allocated %llu MB, pinned %llu MB "
+           "(pinned = leased / held tensors + allocator slabs + tensors never used as an operand, e.g. library "
+           "workspaces). Raise the HBM budget or lower the working set of one op; aborting instead of returning "
+           "a null device pointer.",
+           size, device, (unsigned long long)(st.capacity >> 20), (unsigned long long)(st.allocated >> 20),
+           (unsigned long long)(st.pinned >> 20));
+    std::abort();
+  }
+  return p;
 }
 __attribute__((visibility("default"))) void ogkm_torch_free(void* ptr, size_t /*size*/, int device, void* stream) {
   ogkm::torch_free(ptr, device, stream);

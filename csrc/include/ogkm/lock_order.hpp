@@ -68,6 +68,11 @@ class OrderedRWLock {
   void unlock() { m_.unlock(); lockcheck::on_release(order_); }
   void lock_shared() { lockcheck::on_acquire(order_, false); m_.lock_shared(); }
   void unlock_shared() { m_.unlock_shared(); lockcheck::on_release(order_); }
+  bool try_lock_shared() {
+    if (!m_.try_lock_shared()) return false;
+    lockcheck::on_acquire(order_, true);
+    return true;
+  }
 
  private:
   std::shared_mutex m_;

@@ -287,6 +287,7 @@ class Runtime {
   // Flush GPU translations of devices whose stable VAs were remapped since the
   // last flush (before any consumer of the new mapping can run).
   void flush_translations();
+  std::string describe_device_address(uint64_t va);  // for GPU memory-fault reports
   std::atomic<uint32_t> tlb_dirty_{0};  // bit d: device d has remapped stable VAs
   Status finish_ctx(Ctx& c, Tracker* out);
   void drop_copy(Ctx& c, Block* b, const Loc& l);  // release a residency (block lock held)

@@ -181,6 +181,7 @@ class VaSpace {
   VaSpace() = default;
   OrderedRWLock lock{LockOrder::VA_SPACE};
   std::map<uint64_t, Range*> tree;  // cpu_view start -> range
+  std::map<uint64_t, Range*> dev_tree;  // stable device VA start -> range (RANGE_STABLE_VA)
   std::unordered_map<uint64_t, std::unique_ptr<Range>> ranges;
   std::unordered_map<uint64_t, std::unique_ptr<RangeGroup>> groups;
   uint64_t next_range_id = 1;

@@ -676,6 +676,15 @@ PYBIND11_MODULE(_ogkm, m) {
     py::gil_scoped_release nogil;
     return std::string(status_str(r->wait_seq(seq)));
   });
+  m.def("debug_stream_create", [](int dev) { return (uint64_t)rt()->be()->stream_create(dev, 0); });
+  m.def("debug_stream_destroy", [](uint64_t s) { rt()->be()->stream_destroy((void*)s); });
+  m.def("debug_stream_sync", [](uint64_t s) {
+    py::gil_scoped_release nogil;
+    rt()->be()->stream_sync((void*)s);
+  });
+  m.def("debug_touch", [](uint64_t s, uint64_t ptr, uint64_t bytes, uint32_t delay_us) {
+    check(rt()->be()->debug_touch((void*)s, ptr, bytes, delay_us), "debug_touch");
+  });
   m.def("ring_completed", [](int dev, int kind) { return ring_of(dev, kind)->completed_seq(); });
 
   // ---- tools

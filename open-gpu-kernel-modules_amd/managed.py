@@ -73,6 +73,12 @@ def _mode_class():
             self._recording = True
             self.ops = 0
             self.faulted_ops = 0
+            # OGKM_MODE_TRACE=N: remember the last N ops, printed when one fails.
+            import collections
+            import os
+
+            n = int(os.environ.get("OGKM_MODE_TRACE", "0"))
+            self._last = collections.deque(maxlen=n) if n > 0 else None
             self.prefetches = 0
 
         # ---------------------------------------------------------- mode
@@ -111,8 +117,17 @@ def _mode_class():
             stream = self._stream() if ptrs else 0
             held, persistent = lib.torch_op_begin(ptrs, self.device, stream) if ptrs else ((), ())
             self.ops += 1
+            if self._last is not None:
+                self._last.append((self.ops, func.__name__, len(held)))
             try:
                 out = func(*args, **kwargs)
+            except BaseException:
+                if self._last is not None:
+                    import sys
+
+                    print(f"ogkm.managed: op #{self.ops} {func.__name__} failed; previous ops: {list(self._last)}",
+                          file=sys.stderr, flush=True)
+                raise
             finally:
                 # Outputs the op allocated hold their allocation lease: drop it.
                 outs = []

@@ -1,0 +1,76 @@
+"""Adversarial stress of the stable-VA managed path on the fake backend
+("test with adversarial access patterns").
+
+Managed tensors cycle through an arena far smaller than them. Every "op"
+holds a random operand set (torch_op_begin), enqueues a lagging "kernel" on a
+fake stream that reads and writes every page of those operands through their
+stable VAs, and drops the holds (torch_op_end) - so the host runs far ahead of
+the stream, exactly like torch ahead of the GPU. Evictions, batch copy-outs,
+remaps (a block returning to another chunk), stale-mapping teardown and frees
+all happen while earlier kernels are still queued. The fake backend's VMM is
+real: an unmapped VA is PROT_NONE, so a mapping torn down before its last
+queued user ran crashes the worker (the GPU "illegal memory access").
+Runs in a subprocess so a crash fails the test instead of killing pytest."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r'''
+import random, sys
+sys.path.insert(0, %r)
+import ogkm
+from ogkm import rt
+from ogkm._native import lib
+MB = 1 << 20
+rt.init("fake", fake_devices=1, fake_hbm_mb=256)
+lib.configure("hbm_provider", 1)
+lib.configure("torch_alloc_managed_min_mb", 1)
+lib.configure("stable_lazy_unmap", %d)
+lib.configure("stable_batch_blocks", %d)
+lib.init_device(0, 24 * MB)  # 12 chunks
+s = lib.debug_stream_create(0)
+rng = random.Random(%d)
+live = []
+def alloc():
+    n = rng.choice([2, 4, 6]) * MB
+    held, _ = lib.torch_op_begin([], 0, s)
+    p = lib.torch_alloc(n, 0, s)
+    assert p, "alloc failed"
+    lib.debug_touch(s, p, n, 50)
+    lib.torch_op_end(held, [p], 0, s)
+    live.append((p, n))
+for _ in range(6):
+    alloc()
+for it in range(%d):
+    k = rng.randint(1, 2)
+    ops = rng.sample(live, k)
+    held, _ = lib.torch_op_begin([(p, rng.random() < 0.5) for p, _ in ops], 0, s)
+    for p, n in ops:
+        lib.debug_touch(s, p, n, rng.choice([0, 100, 400]))
+    lib.torch_op_end(held, [], 0, s)
+    r = rng.random()
+    if r < 0.1 and len(live) > 4:
+        p, n = live.pop(rng.randrange(len(live)))
+        lib.torch_free(p, 0, s)
+    elif r < 0.2:
+        alloc()
+lib.debug_stream_sync(s)
+st = rt.stats()
+print("STRESS_OK", st["evictions"], st["vmm_remaps"], st["tlb_flushes"], st["vmm_errors"])
+'''
+
+
+@pytest.mark.parametrize("lazy,batch,seed", [(0, 32, 1), (1, 32, 2), (0, 1, 3), (1, 2, 4)])
+def test_stable_va_stress_async_users(lazy, batch, seed):
+    code = WORKER % (ROOT, lazy, batch, seed, 300)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
+    assert "STRESS_OK" in r.stdout
+    ev, remaps, flushes, errors = map(int, r.stdout.split("STRESS_OK")[1].split()[:4])
+    assert ev > 50 and remaps > 0 and errors == 0, r.stdout
