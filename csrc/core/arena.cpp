@@ -496,7 +496,6 @@ HbmArena::HbmArena(Backend* be, int dev, uint64_t budget, int provider)
     return;
   }
   init_chunks((uint64_t)slab_, n);
-  stable_owner.assign(n, nullptr);
   RT_INFO("HBM arena gpu%d: %u x 2MB chunks at %p (%s)", dev, n, slab_, handles_.empty() ? "slab" : "vmm");
 }
 

@@ -190,12 +190,67 @@ class FakeBackend : public Backend {
   void va_free(void* va, size_t bytes) override { munmap(va, bytes); }
   Status vmm_map(void* va, size_t bytes, uint64_t h, int) override {
     void* m = mmap(va, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, (int)h, 0);
-    return m == MAP_FAILED ? Status::IO_ERROR : Status::OK;
+    if (m == MAP_FAILED) return Status::IO_ERROR;
+    std::lock_guard<std::mutex> g(race_m_);
+    vmaps_[(uint64_t)va] = {bytes, h};
+    return Status::OK;
   }
   Status vmm_unmap(void* va, size_t bytes) override {
     void* m = mmap(va, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
+    std::lock_guard<std::mutex> g(race_m_);
+    vmaps_.erase((uint64_t)va);
     return m == MAP_FAILED ? Status::IO_ERROR : Status::OK;
   }
+  // Race detector for tests (fake_race_check): the VMM handle behind an
+  // address, and the handles an in-flight engine copy reads / writes.
+  uint64_t handle_of(uint64_t a) {
+    auto it = vmaps_.upper_bound(a);
+    if (it == vmaps_.begin()) return 0;
+    --it;
+    return a < it->first + it->second.first ? it->second.second : 0;
+  }
+  void race_begin(const CopyDesc* d, size_t n, int64_t delta) {
+    if (!config().fake_race_check) return;
+    std::lock_guard<std::mutex> g(race_m_);
+    for (size_t i = 0; i < n; ++i) {
+      for (uint64_t o = 0; o < d[i].bytes; o += kBlockSize) {
+        uint64_t hw = handle_of(d[i].dst + o), hr = handle_of(d[i].src + o);
+        if (hw) busy_w_[hw] += delta;
+        if (hr) busy_r_[hr] += delta;
+        if ((hw && busy_k_[hw] > 0) || (hr && busy_kw_[hr] > 0)) {
+          races_++;
+          fprintf(stderr, "[fake RACE] engine copy %#llx <- %#llx (%s) while a kernel uses handle %llu\n",
+                  (unsigned long long)d[i].dst, (unsigned long long)d[i].src, delta > 0 ? "start" : "end",
+                  (unsigned long long)(hw && busy_k_[hw] > 0 ? hw : hr));
+        }
+      }
+    }
+  }
+  void race_kernel(uint64_t ptr, uint64_t bytes, bool write, int64_t delta) {
+    if (!config().fake_race_check) return;
+    std::lock_guard<std::mutex> g(race_m_);
+    for (uint64_t o = 0; o < bytes; o += kBlockSize)
+      if (uint64_t h = handle_of(ptr + o)) {
+        busy_k_[h] += delta;
+        if (write) busy_kw_[h] += delta;
+      }
+  }
+  void race_touch(uint64_t ptr, bool write) {
+    if (!config().fake_race_check) return;
+    std::lock_guard<std::mutex> g(race_m_);
+    uint64_t h = handle_of(ptr);
+    if (!h) return;
+    if (busy_w_[h] > 0 || (write && busy_r_[h] > 0)) {
+      races_++;
+      fprintf(stderr, "[fake RACE] kernel %s VA %#llx (handle %llu) while an engine copy %s it\n",
+              write ? "writes" : "reads", (unsigned long long)ptr, (unsigned long long)h,
+              busy_w_[h] > 0 ? "writes" : "reads");
+    }
+  }
+  std::mutex race_m_;
+  std::map<uint64_t, std::pair<uint64_t, uint64_t>> vmaps_;  // va -> (bytes, handle)
+  std::map<uint64_t, int64_t> busy_w_, busy_r_, busy_k_, busy_kw_;
+  std::atomic<uint64_t> races_{0};
 
   Status host_register(void*, size_t) override { return Status::OK; }
   void host_unregister(void*) override {}
@@ -269,8 +324,10 @@ class FakeBackend : public Backend {
   // The fake "SDMA engine": the ring worker's own thread does the copy.
   bool dma_supported(int) override { return true; }
   Status dma_copy(int, const CopyDesc* d, size_t n, int) override {
+    race_begin(d, n, 1);
     if (int64_t us = config().fake_dma_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(us));
     for (size_t i = 0; i < n; ++i) memmove((void*)d[i].dst, (const void*)d[i].src, d[i].bytes);
+    race_begin(d, n, -1);
     return Status::OK;
   }
   Status decode_bf12(int, const DecodeDesc* d, size_t n, void* s, uint32_t) override {
@@ -347,13 +404,19 @@ class FakeBackend : public Backend {
     run(s, [addr, v] { __atomic_store_n(addr, v, __ATOMIC_RELEASE); });
     return Status::OK;
   }
-  Status debug_touch(void* s, uint64_t ptr, uint64_t bytes, uint32_t delay_us) override {
-    run(s, [ptr, bytes, delay_us] {
+  Status debug_touch(void* s, uint64_t ptr, uint64_t bytes, uint32_t delay_us, bool write) override {
+    run(s, [this, ptr, bytes, delay_us, write] {
       if (delay_us) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
+      for (uint64_t o = 0; o < bytes; o += kBlockSize) race_touch(ptr + o, write);
+      race_kernel(ptr, bytes, write, 1);
+      uint32_t sum = 0;
       for (uint64_t o = 0; o < bytes; o += 4096) {
         volatile uint32_t* w = (volatile uint32_t*)(ptr + o);
-        *w = *w + 1;
+        if (write) *w = *w + 1;
+        else sum += *w;
       }
+      (void)sum;
+      race_kernel(ptr, bytes, write, -1);
     });
     return Status::OK;
   }

@@ -22,10 +22,12 @@
 //   streaming read (tools/probe_sdma.hip, profiles/r2_copy_engines.md) SDMA costs
 //   the reader 1.06x, our 16-WG CU copy kernel 2.86x, at the same 56.8 GB/s.
 #include <dirent.h>
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
+#include <amd_smi/amdsmi.h>
 
 #include <atomic>
 #include <cstdio>
@@ -76,42 +78,109 @@ class HipBackend : public Backend {
     fclose(f);
     return n < 0 ? 0 : n;
   }
-  // amdgpu RAS counters under the GPU's PCI device: ras/<block>_err_count
-  // files hold "ue: N" / "ce: N" lines.
+  // GPU RAS counters. Two sources, the first that reads wins:
+  //  1. amdgpu sysfs under the GPU's PCI device: ras/<block>_err_count (older
+  //     kernels) or ras/aca_<block> (ACA-based RAS, what gfx950 boxes expose),
+  //     each holding "ue: N" / "ce: N" (/ "de: N" deferred) lines;
+  //  2. amd-smi (libamd_smi, dlopen'ed): total ECC counts plus the XGMI_WAFL
+  //     block's counts.
+  // Neither readable -> NOT_SUPPORTED with the reason in last_error(); the
+  // runtime reports that as a condition instead of treating it as healthy.
   Status device_health(int dev, Health* out) override {
     char bus[64] = {0};
     if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) return Status::INVALID_ARGUMENT;
     for (char* p = bus; *p; ++p) *p = (char)tolower(*p);
+    std::string why;
+    if (ras_sysfs(bus, out, &why) == Status::OK) return Status::OK;
+    std::string why2;
+    if (ras_amdsmi(bus, out, &why2) == Status::OK) return Status::OK;
+    last_err_ = why + "; " + why2;
+    return Status::NOT_SUPPORTED;
+  }
+  Status ras_sysfs(const char* bus, Health* out, std::string* why) {
     std::string dir = std::string("/sys/bus/pci/devices/") + bus + "/ras";
     DIR* d = opendir(dir.c_str());
-    if (!d) return Status::NOT_SUPPORTED;
+    if (!d) {
+      *why = "no " + dir;
+      return Status::NOT_SUPPORTED;
+    }
     *out = Health{};
-    out->source = dir;
+    out->source = "sysfs:" + dir;
     int parsed = 0;
     while (dirent* e = readdir(d)) {
       std::string n = e->d_name;
-      if (n.size() < 11 || n.compare(n.size() - 10, 10, "_err_count") != 0) continue;
+      const bool legacy = n.size() > 10 && n.compare(n.size() - 10, 10, "_err_count") == 0;
+      const bool aca = n.rfind("aca_", 0) == 0;
+      if (!legacy && !aca) continue;
       FILE* f = fopen((dir + "/" + n).c_str(), "r");
       if (!f) continue;
-      long long ue = -1, ce = -1;
+      long long ue = -1, ce = -1, de = -1;
       char line[128];
       while (fgets(line, sizeof line, f)) {
         long long v;
         if (sscanf(line, "ue: %lld", &v) == 1) ue = v;
         else if (sscanf(line, "ce: %lld", &v) == 1) ce = v;
+        else if (sscanf(line, "de: %lld", &v) == 1) de = v;
       }
       fclose(f);
-      bool link = n.rfind("xgmi", 0) == 0 || n.find("wafl") != std::string::npos || n.find("pcs") != std::string::npos;
+      const std::string blk = aca ? n.substr(4) : n.substr(0, n.size() - 10);
+      bool link = blk.rfind("xgmi", 0) == 0 || blk.find("wafl") != std::string::npos || blk.find("pcs") != std::string::npos;
       int64_t& U = link ? out->link_ue : out->ue;
       int64_t& C = link ? out->link_ce : out->ce;
       if (ue >= 0) U = (U < 0 ? 0 : U) + ue;
-      if (ce >= 0) C = (C < 0 ? 0 : C) + ce;
+      if (ce >= 0 || de >= 0) C = (C < 0 ? 0 : C) + std::max(0ll, ce) + std::max(0ll, de);
       parsed += (ue >= 0 || ce >= 0);
     }
     closedir(d);
     if (!parsed) {  // the directory exists but no counter is readable (permissions, older kernel)
-      last_err_ = "no readable RAS counters under " + dir;
+      *why = "no readable RAS counters under " + dir;
       return Status::NOT_SUPPORTED;
+    }
+    return Status::OK;
+  }
+  Status ras_amdsmi(const char* bus, Health* out, std::string* why) {
+    using init_t = int (*)(uint64_t);
+    using handle_t = int (*)(amdsmi_bdf_t, amdsmi_processor_handle*);
+    using total_t = int (*)(amdsmi_processor_handle, amdsmi_error_count_t*);
+    using block_t = int (*)(amdsmi_processor_handle, amdsmi_gpu_block_t, amdsmi_error_count_t*);
+    static void* lib = dlopen("libamd_smi.so", RTLD_NOW | RTLD_LOCAL);
+    if (!lib) {
+      *why = "libamd_smi.so not loadable";
+      return Status::NOT_SUPPORTED;
+    }
+    static auto init = (init_t)dlsym(lib, "amdsmi_init");
+    static auto by_bdf = (handle_t)dlsym(lib, "amdsmi_get_processor_handle_from_bdf");
+    static auto total = (total_t)dlsym(lib, "amdsmi_get_gpu_total_ecc_count");
+    static auto block = (block_t)dlsym(lib, "amdsmi_get_gpu_ecc_count");
+    static int init_rc = init ? init(AMDSMI_INIT_AMD_GPUS) : -1;
+    if (!by_bdf || !total || init_rc != 0) {
+      *why = "amd-smi init failed (" + std::to_string(init_rc) + ")";
+      return Status::NOT_SUPPORTED;
+    }
+    unsigned dom = 0, b = 0, dv = 0, fn = 0;
+    if (sscanf(bus, "%x:%x:%x.%x", &dom, &b, &dv, &fn) != 4) return Status::INVALID_ARGUMENT;
+    amdsmi_bdf_t bdf{};
+    bdf.domain_number = dom;
+    bdf.bus_number = b;
+    bdf.device_number = dv;
+    bdf.function_number = fn;
+    amdsmi_processor_handle h = nullptr;
+    amdsmi_error_count_t ec{};
+    if (by_bdf(bdf, &h) != 0 || total(h, &ec) != 0) {
+      *why = std::string("amd-smi has no ECC counts for ") + bus;
+      return Status::NOT_SUPPORTED;
+    }
+    *out = Health{};
+    out->source = "amdsmi";
+    out->ue = (int64_t)ec.uncorrectable_count;
+    out->ce = (int64_t)(ec.correctable_count + ec.deferred_count);
+    amdsmi_error_count_t xe{};
+    if (block && block(h, AMDSMI_GPU_BLOCK_XGMI_WAFL, &xe) == 0) {
+      out->link_ue = (int64_t)xe.uncorrectable_count;
+      out->link_ce = (int64_t)xe.correctable_count;
+      // the total includes the link block: keep the two classes disjoint
+      out->ue = std::max<int64_t>(0, out->ue - out->link_ue);
+      out->ce = std::max<int64_t>(0, out->ce - out->link_ce);
     }
     return Status::OK;
   }

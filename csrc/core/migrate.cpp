@@ -417,7 +417,13 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
       left = left.andnot(from_here);
       if (left.empty()) break;
     }
-    // Never-populated pages are zero-filled (uvm_va_block.c:2863).
+    // Never-populated pages are zero-filled (uvm_va_block.c:2863). Without the
+    // fill (RANGE_NO_ZERO_FILL) nothing writes the chunk before its new owner
+    // does, so the owner must still wait for the chunk's previous users (an
+    // eviction copy-out may still be reading it): its reuse fence joins the
+    // block's tracker, which every lease's ready-tracker includes.
+    if (!left.empty() && (b->range->flags & RANGE_NO_ZERO_FILL) && to->chunk >= 0)
+      b->tracker.merge(to->arena->reuse_fence((uint32_t)to->chunk));
     if (!left.empty() && !(b->range->flags & RANGE_NO_ZERO_FILL)) {
       st = zero_pages(this, c, b, to, left);
       if (st != Status::OK) return st;
@@ -499,6 +505,7 @@ static void release_residency_now(Block* b, const Loc& l) {
 // Submit every ring used by the context, publish fences to blocks / chunks and
 // apply (or, on a failed submission, reverse) the deferred invalidations.
 Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
+  TraceRange tr(be_.get(), "ogkm:finish_ctx", 2);
   std::vector<std::pair<Ring*, FenceRef>> fences;
   std::vector<Ring*> failed;
   Status result = Status::OK;
@@ -585,6 +592,7 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
 // (then its reuse fence must cover c's copies, see seal_evictions). Returns
 // MORE_PROCESSING_REQUIRED with c.need_* set when the demotion tier is full.
 Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
+  TraceRange tr(be_.get(), "ogkm:evict_one", 2);
   *detached = false;
   if (inject_.evict_fail.load() > 0 && inject_.evict_fail.fetch_sub(1) > 0) {
     Tools::get().inc(Counter::InjectedErrors);
@@ -656,6 +664,7 @@ Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
 // victim) and hand the detached chunks to the reserver: each victim's reuse
 // fence covers the copies that read it; the chunks are not freed.
 void Runtime::seal_evictions(Ctx& c, ChunkArena* a, const std::vector<uint32_t>& victims) {
+  TraceRange tr(be_.get(), "ogkm:seal_evictions", 2);
   std::vector<std::pair<Ring*, FenceRef>> fs;
   for (Ring* rr : c.rings) fs.emplace_back(rr, rr->submit());
   for (uint32_t i : victims)
@@ -1055,14 +1064,18 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
   return Status::OK;
 }
 
-// Stable-VA placement. Blocks go in groups of `stable_batch_blocks`: for each
-// group the missing blocks get chunks (a block's previous chunk when it is free
-// again - then its VMM mapping is still right and no remap is needed - else any
-// free chunk, else LRU victims evicted as ONE copy-out batch), their H2D copies
-// are queued as ONE submission that waits only for that group's copy-outs, and
-// their VAs are remapped while the copies run. Consecutive groups therefore
-// overlap D2H (evictions) and H2D (fills) on the two SDMA engines; one
-// translation flush covers every remap of the call.
+// Stable-VA placement, in groups of `stable_batch_blocks` blocks and two
+// passes so the two SDMA directions overlap:
+//  A) for every group: the missing blocks get chunks - a block's previous
+//     chunk when it is free again (its VMM mapping is then still right: no
+//     remap), else any free chunk, else LRU victims evicted as ONE copy-out
+//     submission per group. The D2H engine starts on group 0 while the host
+//     evicts group 1. Blocks of the range that are already resident are
+//     pinned for the call, so a later group never evicts an earlier one.
+//  B) for every group: hand the chunks over and queue its fills as ONE H2D
+//     submission that waits only for that group's copy-outs (H2D of group g
+//     runs while D2H of group g+1 drains), then remap the group's VAs while
+//     the copies fly. One translation flush covers every remap of the call.
 Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
                              Lease* L, Tracker* out, Cause cause) {
   TraceRange tr(be_.get(), "ogkm:place_stable");
@@ -1079,32 +1092,41 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
   const uint64_t group = (uint64_t)std::max<int64_t>(1, config().stable_batch_blocks);
   std::lock_guard<OrderedMutex> placement(r->place_lock);
   Status st = Status::OK;
-  std::vector<Block*> leased;  // blocks this call pinned for L (undone on failure)
+  struct Group {
+    uint64_t g0, g1;
+    std::vector<uint64_t> need;   // blocks without an HBM residency
+    std::vector<uint32_t> chunks; // their chunks (pinned until handed over)
+    size_t used = 0;              // chunks handed over (or given back)
+  };
+  std::vector<Group> groups;
+  std::vector<uint32_t> kept;  // resident chunks of the range pinned for the call
+  // ---- pass A: chunks (and the copy-outs they cost) for every group
   for (uint64_t g0 = b0; g0 <= b1 && st == Status::OK; g0 += group) {
-    const uint64_t g1 = std::min(b1, g0 + group - 1);
-    // 1) blocks of the group without an HBM residency, and the chunk each had last
-    std::vector<uint64_t> need;
+    Group G{g0, std::min(b1, g0 + group - 1), {}, {}, 0};
     std::vector<int64_t> hints;
-    for (uint64_t bi = g0; bi <= g1; ++bi) {
+    for (uint64_t bi = G.g0; bi <= G.g1; ++bi) {
       Block* b = r->block(bi);
       std::lock_guard<OrderedMutex> g(b->lock);
-      if (!b->find(dst)) {
-        need.push_back(bi);
+      Residency* x = b->find(dst);
+      if (!x) {
+        G.need.push_back(bi);
         hints.push_back(b->stable_chunk.load());
+      } else if (x->chunk >= 0) {
+        ga->pin((uint32_t)x->chunk);
+        kept.push_back((uint32_t)x->chunk);
       }
     }
-    // 2) chunks for them (pinned until handed to their block)
-    std::vector<uint32_t> chunks;
-    for (size_t k = 0; k < need.size(); ++k) {
+    for (size_t k = 0; k < G.need.size(); ++k) {
       uint32_t ch = 0;
       if (alloc_chunks(ga, 1, hints[k], &ch, nullptr, true) != Status::OK) break;
-      chunks.push_back(ch);
+      G.chunks.push_back(ch);
     }
-    if (chunks.size() < need.size()) {
+    if (G.chunks.size() < G.need.size()) {
       Reservation rv;
-      const uint32_t m = (uint32_t)(need.size() - chunks.size());
-      if (ga->loc().is_gpu() && !config().global_oversubscription) st = Status::NO_MEMORY;
-      else if (inject_.alloc_fail_after.load() == 0) {
+      const uint32_t m = (uint32_t)(G.need.size() - G.chunks.size());
+      if (!config().global_oversubscription) {
+        st = Status::NO_MEMORY;
+      } else if (inject_.alloc_fail_after.load() == 0) {
         Tools::get().inc(Counter::InjectedErrors);
         st = Status::NO_MEMORY;
       } else {
@@ -1117,25 +1139,27 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
       if (st == Status::OK) {
         ga->commit(rv, true);
         Tools::get().inc(Counter::AllocRetries);
-        chunks.insert(chunks.end(), rv.list.begin(), rv.list.end());
-      } else {
-        for (uint32_t ch : chunks) ga->free(ch, 1);
-        break;
+        G.chunks.insert(G.chunks.end(), rv.list.begin(), rv.list.end());
       }
     }
-    // 3) hand chunks over, queue the fills of the group
+    groups.push_back(std::move(G));
+  }
+  // ---- pass B: hand over, fill and remap group by group
+  std::vector<Block*> leased;  // blocks this call pinned for L (undone on failure)
+  for (size_t gi = 0; gi < groups.size() && st == Status::OK; ++gi) {
+    Group& G = groups[gi];
+    TraceRange trf(be_.get(), "ogkm:fill_group", 2);
     Ctx c;
     c.cause = cause;
     c.defer_flush = true;
-    size_t next = 0;
-    for (uint64_t bi = g0; bi <= g1; ++bi) {
+    for (uint64_t bi = G.g0; bi <= G.g1 && st == Status::OK; ++bi) {
       Block* b = r->block(bi);
       for (int attempt = 0; attempt < 8; ++attempt) {
         {
           std::lock_guard<OrderedMutex> g(b->lock);
           Residency* x = b->find(dst);
-          if (next < need.size() && need[next] == bi) {
-            uint32_t ch = chunks[next++];
+          if (G.used < G.need.size() && G.need[G.used] == bi) {
+            uint32_t ch = G.chunks[G.used++];
             if (x) {
               ga->free(ch, 1);  // populated concurrently (a prefetch): keep theirs
             } else {
@@ -1185,16 +1209,15 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
         c.need_arena->free((uint32_t)rr.first, rr.n);
         c.need_arena = nullptr;
       }
-      if (st != Status::OK) {
-        // chunks never handed over (error part-way through the group)
-        while (next < need.size()) ga->free(chunks[next++], 1);
-        break;
-      }
     }
-    // 4) submit the group; finish_ctx remaps the group's VAs (no flush yet)
+    // submit the group; finish_ctx remaps the group's VAs (no flush yet)
     Status fs = finish_ctx(c, out);
     if (st == Status::OK) st = fs;
   }
+  // chunks never handed over (an error part-way) go back; call pins end
+  for (auto& G : groups)
+    while (G.used < G.chunks.size()) ga->free(G.chunks[G.used++], 1);
+  for (uint32_t ch : kept) ga->unpin(ch);
   // Blocks whose chunk did not change since they were last mapped are already
   // right; every other one was remapped above: one flush before any use.
   if (tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();

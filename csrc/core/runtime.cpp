@@ -67,6 +67,12 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
     }
     dev->health_ok = rt->be_->device_health(d, &dev->health0) == Status::OK;
     dev->health = dev->health0;
+    if (!dev->health_ok && !rt->be_->is_fake()) {
+      // Not silently "healthy": the condition is reported (stats, device_health()).
+      dev->health_reason = rt->be_->last_error();
+      RT_WARN("GPU %d: no readable RAS / ECC counters (%s): uncorrectable errors cannot be detected", d,
+              dev->health_reason.c_str());
+    }
     rt->devs_.push_back(std::move(dev));
   }
   rt->perf_subs_ = perf_modules_register(Tools::get().bus());
@@ -287,7 +293,12 @@ Status Runtime::free_range(Range* r) {
 
 Range* Runtime::find_range(uint64_t addr) {
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
-  return vs_.find_locked(addr);
+  if (Range* r = vs_.find_locked(addr)) return r;
+  // a stable device VA (RANGE_STABLE_VA ranges have one, often without a CPU view)
+  auto it = vs_.dev_tree.upper_bound(addr);
+  if (it == vs_.dev_tree.begin()) return nullptr;
+  --it;
+  return addr < it->first + it->second->cpu_view_bytes ? it->second : nullptr;
 }
 
 Range* Runtime::range_by_id(uint64_t id) {
@@ -459,21 +470,20 @@ void Runtime::stable_unmap_locked(Block* b) {
     RT_ERR("stable VA unmap of range %llu block %llu failed: %s", (unsigned long long)r->id,
            (unsigned long long)b->index, be_->last_error().c_str());
   }
-  if (HbmArena* ha = devs_[r->stable_dev]->hbm.get())
-    if ((uint64_t)c < ha->stable_owner.size() && ha->stable_owner[c] == b) ha->stable_owner[c] = nullptr;
   b->stable_chunk.store(-1);
 }
 
-// Point block b's stable VA at its HBM chunk (block lock held). Invariants:
-//  * a mapping is torn down only after the work that may use it finished
-//    (Block::stable_users);
-//  * an evicted block keeps its now-stale mapping until the block comes back
-//    (same chunk: nothing to do) or until another block's stable VA claims
-//    the chunk - HIP's VMM layer tracks one mapping per handle, so a handle is
-//    never mapped at two stable VAs at once (plus the arena's own view).
+// Point block b's stable VA at its HBM chunk (block lock held). A mapping is
+// torn down only after the work that may use it finished
+// (Block::stable_users); an evicted block keeps its now-stale mapping until it
+// comes back - to the same chunk (nothing to do: the hint in place_stable
+// prefers it) or to another one. A handle may then be mapped at several VAs at
+// once (the arena view, its block's VA, stale VAs of earlier owners), which
+// HIP's VMM layer handles (tools/probe_vmm_multimap.hip).
 void Runtime::stable_map_block(Block* b) {
   Range* r = b->range;
   if (!r->dev_va) return;
+  TraceRange tr(be_.get(), "ogkm:stable_map", 2);
   Residency* g = b->find(Loc::gpu(r->stable_dev));
   const int64_t want = (g && g->chunk >= 0) ? g->chunk : -1;
   if (want == b->stable_chunk.load()) return;
@@ -490,17 +500,11 @@ void Runtime::stable_map_block(Block* b) {
     return;
   }
   HbmArena* ha = static_cast<HbmArena*>(g->arena);
-  // The chunk's handle may still be mapped at another block's (stale) VA.
-  if ((uint64_t)want < ha->stable_owner.size()) {
-    Block* o = ha->stable_owner[want];
-    if (o && o != b) stable_unmap_locked(o);
-  }
   stable_unmap_locked(b);  // b's own previous mapping (stale, another chunk)
   char* va = (char*)r->dev_va + b->block_offset();
   Tools::get().inc(Counter::VmmRemaps);
   if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) {
     b->stable_chunk.store(want);
-    if ((uint64_t)want < ha->stable_owner.size()) ha->stable_owner[want] = b;
     tlb_dirty_.fetch_or(1u << r->stable_dev);
   } else {
     Tools::get().inc(Counter::VmmErrors);
@@ -1033,6 +1037,7 @@ Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
   out->read_dup = !dup.empty();
   if (!b->cpu_ro.empty() || !b->cpu_rw.empty()) out->mapped_on.push_back(kCpuProc);
   if (b->stable_chunk.load() >= 0) out->mapped_on.push_back(r->stable_dev);
+  out->stable_chunk = b->stable_chunk.load();
   if (b->lease_pins)
     for (auto& x : b->res)
       if (x.loc.is_gpu()) out->mapped_on.push_back(x.loc.id);
@@ -1088,7 +1093,11 @@ Status Runtime::check_health(int dev, bool force) {
   if (!force && now - d.health_checked_ns < 20ull * 1000 * 1000) return global_status();
   d.health_checked_ns = now;
   Backend::Health h;
-  if (be_->device_health(dev, &h) != Status::OK) return global_status();
+  if (be_->device_health(dev, &h) != Status::OK) {
+    d.health_reason = be_->last_error();
+    return global_status();
+  }
+  d.health_reason.clear();
   if (!d.health_ok) {  // counters appeared after init: take them as the baseline
     d.health0 = h;
     d.health_ok = true;

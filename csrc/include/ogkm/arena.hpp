@@ -175,12 +175,6 @@ class HbmArena : public ChunkArena {
   bool vmm() const { return !handles_.empty(); }
   uint64_t handle(uint32_t i) const { return handles_.empty() ? 0 : handles_[i]; }
   Status init_status() const { return init_; }
-  // Block whose stable VA currently maps chunk i's handle (besides the arena's
-  // own view), nullptr = none. At most one stable VA maps a handle at a time:
-  // HIP's VMM layer tracks one mapping per handle, so unmapping one of two
-  // stable VAs of a handle can tear down the other (tools/probe_vmm_multimap.hip).
-  // Guarded by Runtime::stable_m_.
-  std::vector<Block*> stable_owner;
 
  private:
   Backend* be_;

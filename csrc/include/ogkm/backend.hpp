@@ -176,9 +176,11 @@ class Backend {
   // Make `stream` wait until *addr >= value (GPU-side wait, no CPU involvement).
   virtual Status wait_value(void* stream, uint64_t* addr, uint64_t value) = 0;
   // Test hook (fake backend): a "kernel" on `stream` that sleeps delay_us and
-  // then reads and writes one word of every 4 KB page of [ptr, ptr+bytes) - an
-  // access through an unmapped VA is a SIGSEGV on the stream's thread.
-  virtual Status debug_touch(void* /*stream*/, uint64_t /*ptr*/, uint64_t /*bytes*/, uint32_t /*delay_us*/) {
+  // then reads (and with `write`, increments) one word of every 4 KB page of
+  // [ptr, ptr+bytes) - an access through an unmapped VA is a SIGSEGV on the
+  // stream's thread.
+  virtual Status debug_touch(void* /*stream*/, uint64_t /*ptr*/, uint64_t /*bytes*/, uint32_t /*delay_us*/,
+                             bool /*write*/) {
     return Status::NOT_SUPPORTED;
   }
 

@@ -83,6 +83,7 @@ namespace ogkm {
   X(cxl_emulate_node, -1, "treat this NUMA node as CXL when no CXL hardware (-1 = off)")             \
   /* debug */                                                                                        \
   X(lock_check, 0, "enable the lock-order checker")                                                  \
+  X(fake_race_check, 0, "fake backend: report kernels (debug_touch) that touch a chunk an engine copy is using") \
   X(fake_dma_delay_us, 0, "fake backend: microseconds every SDMA batch takes (ordering tests)")       \
   X(leak_check, 1, "track outstanding arena bytes")                                                  \
   X(release_asserts, 1, "release asserts set the sticky fatal error")                                \

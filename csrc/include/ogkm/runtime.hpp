@@ -101,6 +101,7 @@ struct Device {
   // error past the baseline makes the runtime FATAL (uvm_gpu.c:1328-1354).
   Backend::Health health0, health;
   bool health_ok = false;           // the platform reports RAS counters
+  std::string health_reason;        // why they are unreadable (empty when readable)
   uint64_t health_checked_ns = 0;
   std::mutex health_m;
 };
@@ -125,6 +126,7 @@ struct ResidencyInfo {   // UVM_TEST_VA_RESIDENCY_INFO analog (uvm_test_ioctl.h:
   bool read_dup = false;
   bool pinned = false;
   bool thrashing = false;
+  int64_t stable_chunk = -1;        // HBM chunk the stable VA maps (may be stale after an eviction)
   Policy policy;
 };
 
@@ -283,7 +285,7 @@ class Runtime {
   void stable_map_block(Block* b);
   // stable_m_ held: tear down b's stable-VA mapping after its users finished.
   void stable_unmap_locked(Block* b);
-  std::mutex stable_m_;  // stable-VA mappings (Block::stable_chunk / stable_users, HbmArena::stable_owner)
+  std::mutex stable_m_;  // stable-VA mappings (Block::stable_chunk / stable_users)
   // Flush GPU translations of devices whose stable VAs were remapped since the
   // last flush (before any consumer of the new mapping can run).
   void flush_translations();
@@ -333,9 +335,12 @@ class Runtime {
 };
 
 // Scoped profiler range around a runtime operation (no-op on the fake backend).
+// level 1: per operation (acquire, place, eviction batch); level 2 also per
+// block / phase (trace_ranges >= 2, for host-time profiles).
 struct TraceRange {
   Backend* be;
-  explicit TraceRange(Backend* b, const char* name) : be(config().trace_ranges ? b : nullptr) {
+  explicit TraceRange(Backend* b, const char* name, int level = 1)
+      : be(config().trace_ranges >= level ? b : nullptr) {
     if (be) be->range_push(name);
   }
   ~TraceRange() {

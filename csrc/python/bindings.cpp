@@ -504,6 +504,7 @@ PYBIND11_MODULE(_ogkm, m) {
     d["read_mostly"] = ri.policy.read_dup;
     d["preferred"] = ri.policy.has_preferred ? py::object(loc_dict(ri.policy.preferred)) : py::object(py::none());
     d["accessed_by"] = ri.policy.accessed_by;
+    d["stable_chunk"] = ri.stable_chunk;
     return d;
   });
   m.def("stats", [] {
@@ -528,6 +529,7 @@ PYBIND11_MODULE(_ogkm, m) {
       a["evictions"] = s.evictions;
       a["free_chunks"] = r->dev(g).hbm->free_chunks();
       a["largest_free_run"] = r->dev(g).hbm->largest_free_run();
+      a["base"] = r->dev(g).hbm->base();
       uint64_t al, pk, na, sw;
       torch_alloc_stats(g, &al, &pk, &na, &sw);
       a["torch_allocated"] = al;
@@ -577,6 +579,7 @@ PYBIND11_MODULE(_ogkm, m) {
     };
     py::dict out;
     out["reported"] = d.health_ok;
+    out["unreadable_reason"] = d.health_reason;
     out["baseline"] = h2d(d.health0);
     out["now"] = h2d(d.health);
     out["status"] = status_str(st);
@@ -682,9 +685,9 @@ PYBIND11_MODULE(_ogkm, m) {
     py::gil_scoped_release nogil;
     rt()->be()->stream_sync((void*)s);
   });
-  m.def("debug_touch", [](uint64_t s, uint64_t ptr, uint64_t bytes, uint32_t delay_us) {
-    check(rt()->be()->debug_touch((void*)s, ptr, bytes, delay_us), "debug_touch");
-  });
+  m.def("debug_touch", [](uint64_t s, uint64_t ptr, uint64_t bytes, uint32_t delay_us, bool write) {
+    check(rt()->be()->debug_touch((void*)s, ptr, bytes, delay_us, write), "debug_touch");
+  }, py::arg("stream"), py::arg("ptr"), py::arg("bytes"), py::arg("delay_us"), py::arg("write") = true);
   m.def("ring_completed", [](int dev, int kind) { return ring_of(dev, kind)->completed_seq(); });
 
   // ---- tools

@@ -9,8 +9,12 @@ the stream, exactly like torch ahead of the GPU. Evictions, batch copy-outs,
 remaps (a block returning to another chunk), stale-mapping teardown and frees
 all happen while earlier kernels are still queued. The fake backend's VMM is
 real: an unmapped VA is PROT_NONE, so a mapping torn down before its last
-queued user ran crashes the worker (the GPU "illegal memory access").
-Runs in a subprocess so a crash fails the test instead of killing pytest."""
+queued user ran crashes the worker (the GPU "illegal memory access"); every
+write is counted and checked at the end (a lost update = an ordering bug,
+e.g. a fresh chunk written before its previous owner's copy-out finished);
+and the fake backend's race detector reports any engine copy that overlaps a
+kernel on the same chunk. Runs in a subprocess so a crash fails the test
+instead of killing pytest."""
 from __future__ import annotations
 
 import os
@@ -22,7 +26,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 WORKER = r'''
-import random, sys
+import ctypes, random, sys
 sys.path.insert(0, %r)
 import ogkm
 from ogkm import rt
@@ -33,34 +37,56 @@ lib.configure("hbm_provider", 1)
 lib.configure("torch_alloc_managed_min_mb", 1)
 lib.configure("stable_lazy_unmap", %d)
 lib.configure("stable_batch_blocks", %d)
+lib.configure("fake_race_check", 1)  # engine copy vs kernel on one chunk -> "[fake RACE]" on stderr
 lib.init_device(0, 24 * MB)  # 12 chunks
 s = lib.debug_stream_create(0)
 rng = random.Random(%d)
 live = []
+touches = {}
 def alloc():
     n = rng.choice([2, 4, 6]) * MB
     held, _ = lib.torch_op_begin([], 0, s)
     p = lib.torch_alloc(n, 0, s)
     assert p, "alloc failed"
+    lib.debug_stream_sync(s)
+    ctypes.memset(p, 0, n)  # known start (torch ranges are not zero-filled)
     lib.debug_touch(s, p, n, 50)
     lib.torch_op_end(held, [p], 0, s)
     live.append((p, n))
+    touches[p] = 1
 for _ in range(6):
     alloc()
 for it in range(%d):
     k = rng.randint(1, 2)
     ops = rng.sample(live, k)
-    held, _ = lib.torch_op_begin([(p, rng.random() < 0.5) for p, _ in ops], 0, s)
-    for p, n in ops:
-        lib.debug_touch(s, p, n, rng.choice([0, 100, 400]))
+    ws = [rng.random() < 0.5 for _ in ops]
+    held, _ = lib.torch_op_begin([(p, w) for (p, _), w in zip(ops, ws)], 0, s)
+    for (p, n), w in zip(ops, ws):
+        # an operand declared read-only is only read (a read lease may keep
+        # host duplicates valid): only writers count
+        lib.debug_touch(s, p, n, rng.choice([0, 100, 400]), w)
+        touches[p] += int(w)
     lib.torch_op_end(held, [], 0, s)
     r = rng.random()
     if r < 0.1 and len(live) > 4:
         p, n = live.pop(rng.randrange(len(live)))
         lib.torch_free(p, 0, s)
+        del touches[p]
     elif r < 0.2:
         alloc()
 lib.debug_stream_sync(s)
+# Data check: every touch added 1 to the first word of every page of its
+# operands (no update may be lost to an eviction / fill / remap race).
+bad = 0
+for p, n in live:
+    held, _ = lib.torch_op_begin([(p, False)], 0, s)
+    lib.debug_stream_sync(s)
+    words = [ctypes.c_uint32.from_address(p + o).value for o in range(0, n, 4096)]
+    lib.torch_op_end(held, [], 0, s)
+    if set(words) != {touches[p]}:
+        bad += 1
+        print("DATA_MISMATCH", hex(p), n, touches[p], sorted(set(words))[:8])
+assert bad == 0, bad
 st = rt.stats()
 print("STRESS_OK", st["evictions"], st["vmm_remaps"], st["tlb_flushes"], st["vmm_errors"])
 '''
@@ -72,5 +98,6 @@ def test_stable_va_stress_async_users(lazy, batch, seed):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
     assert "STRESS_OK" in r.stdout
+    assert "[fake RACE]" not in r.stderr, r.stderr[-3000:]
     ev, remaps, flushes, errors = map(int, r.stdout.split("STRESS_OK")[1].split()[:4])
     assert ev > 50 and remaps > 0 and errors == 0, r.stdout

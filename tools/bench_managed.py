@@ -31,6 +31,7 @@ def main() -> None:
     ap.add_argument("--sync-phases", action="store_true", help="synchronize after each phase (per-phase times)")
     ap.add_argument("--lazy-unmap", action="store_true")
     ap.add_argument("--batch-blocks", type=int, default=32)
+    ap.add_argument("--trace-level", type=int, default=1)
     a = ap.parse_args()
 
     import torch
@@ -39,7 +40,7 @@ def main() -> None:
 
     allocator.enable(managed_min_mb=4)
     rt.init("hip", hbm_budget={0: a.arena_mb << 20}, stable_lazy_unmap=int(a.lazy_unmap),
-            stable_batch_blocks=a.batch_blocks, perf_workingset_active_pct=0)
+            stable_batch_blocks=a.batch_blocks, perf_workingset_active_pct=0, trace_ranges=a.trace_level)
     n = a.mb << 20
     xs = []
     for i in range(a.tensors):

@@ -15,9 +15,8 @@ step() {  # step <name> <seconds> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc $rc)"; exit $rc; fi
 }
 step mode_test 400 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_managed_mode_gpu.py
-step bm_park_eager 150 python tools/bench_managed.py --tensors 8 --mb 256 --arena-mb 1024 --iters 2
-step bm_park_lazy 150 python tools/bench_managed.py --tensors 8 --mb 256 --arena-mb 1024 --iters 2 --lazy-unmap
+step health 200 python -u -m pytest -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_runtime.py -k "health"
 step bm_dispatch 150 python tools/bench_managed.py --tensors 8 --mb 256 --arena-mb 1024 --iters 2 --mode dispatch
 step bm_dispatch64 150 python tools/bench_managed.py --tensors 8 --mb 64 --arena-mb 256 --iters 4 --mode dispatch
-step alloc_tests 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_runtime.py -k "allocator or managed"
-for f in bm_park_eager bm_park_lazy bm_dispatch bm_dispatch64; do tail -1 gpurun_out/r3/$f.log; done
+grep -h "MANAGED_OK\|device_health" gpurun_out/r3/mode_test.log gpurun_out/r3/health.log | head -5
+for f in bm_dispatch bm_dispatch64; do tail -1 gpurun_out/r3/$f.log; done
