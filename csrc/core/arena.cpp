@@ -102,6 +102,23 @@ Status ChunkArena::alloc(uint32_t n, Block* owner, int64_t hint, uint32_t* first
       if (it->first <= hint && hint + n <= (int64_t)it->first + it->second) pick = hint;
     }
   }
+  if (pick < 0 && n == 1 && hint < 0) {
+    // A single chunk: prefer one nobody is still using. A chunk freed a moment
+    // ago usually still has a queued reader (the H2D fill that drained it); a
+    // writer handed that chunk would wait for that copy - e.g. an eviction
+    // copy-out serialised behind the previous fill. Idle chunks keep the two
+    // copy directions overlapping.
+    int scanned = 0;
+    for (auto it = free_runs_.begin(); it != free_runs_.end() && scanned < 32 && pick < 0; ++it) {
+      for (uint32_t k = 0; k < it->second && scanned < 32; ++k, ++scanned) {
+        Tracker& t = chunks_[it->first + k].reuse_fence;
+        if (t.query()) {
+          pick = it->first + k;
+          break;
+        }
+      }
+    }
+  }
   if (pick < 0) {
     // Best fit: smallest run that holds n chunks (limits fragmentation).
     uint32_t best = UINT32_MAX;

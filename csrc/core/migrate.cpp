@@ -1089,7 +1089,10 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
     uint32_t p0 = (uint32_t)(lo >> kPageShift), p1 = (uint32_t)((hi + kPageSize - 1) >> kPageShift);
     return PageMask::range(p0, p1 - p0);
   };
-  const uint64_t group = (uint64_t)std::max<int64_t>(1, config().stable_batch_blocks);
+  // At least ~4 groups per call (so a tensor's own D2H and H2D overlap), of
+  // 4 .. stable_batch_blocks blocks.
+  const uint64_t cap = (uint64_t)std::max<int64_t>(1, config().stable_batch_blocks);
+  const uint64_t group = std::min(cap, std::max<uint64_t>(std::min<uint64_t>(4, cap), (b1 - b0 + 1 + 3) / 4));
   std::lock_guard<OrderedMutex> placement(r->place_lock);
   Status st = Status::OK;
   struct Group {

@@ -75,19 +75,19 @@ struct DevAlloc {
     uint32_t holds = 0;       // allocation hold + op holds (the lease lives while > 0)
     bool alloc_hold = false;  // the allocation's own hold (dropped by park / the end of the allocating op)
     bool read_mostly = false;
-    // Long-lived (parameters, buffers, caches): held by ops twice with at
-    // least torch_persistent_births allocations in between. Activations live
-    // for a few ops and get a new address every pass; the transparent mode's
-    // prefetcher keys its trace on persistent operands only.
+    // Long-lived (parameters, buffers, caches): held by two ops at least
+    // torch_persistent_ops ops apart. Activations are consumed within a few ops
+    // and get a new address every pass; the transparent mode's prefetcher keys
+    // its trace on persistent operands only.
     bool persistent = false;
     bool held_once = false;
-    uint64_t last_hold_birth = 0;
+    uint64_t last_hold_op = 0;
   };
   std::unordered_map<uint64_t, Managed> managed;   // stable VA -> range
   std::vector<std::pair<Range*, Tracker>> deferred;  // freed, waiting for their stream fence
   uint64_t allocated = 0, peak = 0, nallocs = 0, stream_waits = 0;
   uint64_t managed_bytes = 0, parks = 0, unparks = 0, op_holds = 0;
-  uint64_t births = 0;  // managed allocations so far (the persistence clock)
+  uint64_t op_seq = 0;  // dispatched ops that held managed operands (the persistence clock)
 };
 
 std::mutex g_m;
@@ -178,7 +178,6 @@ void* managed_alloc(Runtime* rt, DevAlloc* da, size_t size, int device, void* st
     return nullptr;
   }
   uint64_t addr = (uint64_t)r->dev_va;
-  da->births++;
   da->managed[addr] = m;
   da->managed_bytes += bytes;
   da->allocated += bytes;
@@ -427,6 +426,7 @@ Status torch_op_begin(const std::vector<std::pair<uint64_t, bool>>& ptrs, int de
       }
     if (!dup) v.push_back(pw);
   }
+  if (!v.empty()) da->op_seq++;
   for (auto& pw : v) {
     auto& m = da->managed[pw.first];
     Status st = add_hold(rt, da, m, device, stream, pw.second ? Access::WRITE : Access::READ);
@@ -436,10 +436,10 @@ Status torch_op_begin(const std::vector<std::pair<uint64_t, bool>>& ptrs, int de
       return st;
     }
     held->push_back(pw.first);
-    if (m.held_once && da->births - m.last_hold_birth >= (uint64_t)std::max<int64_t>(1, config().torch_persistent_births))
+    if (m.held_once && da->op_seq - m.last_hold_op >= (uint64_t)std::max<int64_t>(1, config().torch_persistent_ops))
       m.persistent = true;
     m.held_once = true;
-    m.last_hold_birth = da->births;
+    m.last_hold_op = da->op_seq;
     if (m.persistent) persistent->push_back(pw.first);
     da->op_holds++;
   }

@@ -162,16 +162,20 @@ def test_op_hold_nests_with_allocation_hold(managed_rt):
     lib.torch_op_end(held, [], 0, 0)
     # its first use as an operand also ended its allocation hold
     assert lib.torch_managed_stats(0)["active_bytes"] == 0
-    lib.configure("torch_persistent_births", 2)
-    tmp = [lib.torch_alloc(4 * MB, 0) for _ in range(2)]  # two allocations later ...
+    lib.configure("torch_persistent_ops", 3)
+    tmp = [lib.torch_alloc(4 * MB, 0) for _ in range(3)]
+    for t in tmp:  # three other ops later ...
+        h, _ = lib.torch_op_begin([(t, False)], 0, 0)
+        lib.torch_op_end(h, [], 0, 0)
     held, pers = lib.torch_op_begin([(p, False)], 0, 0)
     assert pers == [p]  # ... the second hold marks p long-lived (a parameter, not an activation)
     lib.torch_op_end(held, [], 0, 0)
-    q = tmp[0]
+    q = lib.torch_alloc(4 * MB, 0)
+    tmp.append(q)
     held, pers = lib.torch_op_begin([(q, False)], 0, 0)
     lib.torch_op_end(held, [], 0, 0)
     held, pers = lib.torch_op_begin([(q, False)], 0, 0)
-    assert pers == []  # held twice with no allocation in between: short-lived
+    assert pers == []  # held by consecutive ops: short-lived (an activation)
     lib.torch_op_end(held, [], 0, 0)
     for t in tmp:
         lib.torch_free(t, 0)
