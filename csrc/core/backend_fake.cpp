@@ -314,7 +314,9 @@ class FakeBackend : public Backend {
     if (s) ((FakeStream*)s)->enqueue(std::move(f));
     else f();
   }
-  Status copy_batch(int, const CopyDesc* d, size_t n, void* s, int) override {
+  Status copy_batch(int dev, const CopyDesc* d, size_t n, void* s, int engine) override {
+    if (engine == 4)  // k_peer_push stand-in: counted per source device
+      for (size_t i = 0; i < n; ++i) __atomic_fetch_add(&push_bytes_[dev & 31], d[i].bytes, __ATOMIC_RELAXED);
     std::vector<CopyDesc> v(d, d + n);
     run(s, [v] {
       for (auto& c : v) memmove((void*)c.dst, (const void*)c.src, c.bytes);
@@ -323,7 +325,25 @@ class FakeBackend : public Backend {
   }
   // The fake "SDMA engine": the ring worker's own thread does the copy.
   bool dma_supported(int) override { return true; }
-  Status dma_copy(int, const CopyDesc* d, size_t n, int) override {
+  // Synthetic SDMA topology: engine 0 host->GPU, engine 1 GPU->host, and two
+  // xGMI engines per peer pair that differ between destinations (engines 2..7).
+  uint32_t copy_engine_mask(int dst_dev, int src_dev) override {
+    if (src_dev < 0) return dst_dev >= 0 && dst_dev < ndev_ ? 0x1u : 0;
+    if (src_dev >= ndev_) return 0;
+    if (dst_dev < 0) return 0x2u;
+    if (dst_dev == src_dev || dst_dev >= ndev_) return 0;
+    return (1u << (2 + dst_dev % 6)) | (1u << (2 + (dst_dev + 3) % 6));
+  }
+  void engine_bytes(int dev, uint64_t out[32]) override {
+    for (int i = 0; i < 32; ++i)
+      out[i] = i < 31 ? __atomic_load_n(&eng_bytes_[dev & 31][i], __ATOMIC_RELAXED)
+                      : __atomic_load_n(&push_bytes_[dev & 31], __ATOMIC_RELAXED);  // slot 31: k_peer_push bytes
+  }
+  Status dma_copy(int dev, const CopyDesc* d, size_t n, int channel) override {
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t e = d[i].engine ? d[i].engine : (1u << (channel % 2));
+      __atomic_fetch_add(&eng_bytes_[dev & 31][__builtin_ctz(e) % 31], d[i].bytes, __ATOMIC_RELAXED);
+    }
     race_begin(d, n, 1);
     if (int64_t us = config().fake_dma_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(us));
     for (size_t i = 0; i < n; ++i) memmove((void*)d[i].dst, (const void*)d[i].src, d[i].bytes);
@@ -346,6 +366,10 @@ class FakeBackend : public Backend {
   }
   Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {
     run(s, [a, mode] { dgemm_cpu(a, mode != DGEMM_W_RAW); });
+    return Status::OK;
+  }
+  Status dgemm_fused(int, const DGemmFusedArgs& a, void* s) override {
+    run(s, [a] { dgemm_fused_cpu(a); });
     return Status::OK;
   }
   Status dgemm_reduce(int, const DGemmReduceArgs& a, void* s) override {
@@ -519,6 +543,8 @@ class FakeBackend : public Backend {
   std::map<uint64_t, FakeAlloc> allocs_;                        // base -> memfd
   std::map<uint64_t, std::pair<uint64_t, size_t>> opened_;      // ipc ptr -> (map base, bytes)
   std::map<void*, size_t> imports_;                             // imported dma-buf mappings
+  uint64_t eng_bytes_[32][31] = {};                             // per device, per synthetic SDMA engine
+  uint64_t push_bytes_[32] = {};                                // k_peer_push stand-in bytes per source device
 };
 
 }  // namespace

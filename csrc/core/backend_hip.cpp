@@ -384,6 +384,23 @@ class HipBackend : public Backend {
     }
     uint32_t piece = (uint32_t)(config().copy_piece_kb * 1024);
     if (piece < 4096) piece = 4096;
+    if (engine == 4) {  // k_peer_push: the source GPU writes the peer's HBM, bounded CU budget
+      const uint32_t pw = config().peer_push_wgs > 0 ? (uint32_t)config().peer_push_wgs : 64;
+      for (size_t base = 0; base < n; base += kInlineDescs) {
+        size_t cnt = n - base < (size_t)kInlineDescs ? n - base : (size_t)kInlineDescs;
+        KInlineDescs inl;
+        uint64_t ps = 0;
+        for (size_t i = 0; i < cnt; ++i) {
+          inl.d[i] = KCopyDesc{d[base + i].dst, d[base + i].src, d[base + i].bytes};
+          inl.piece_start[i] = ps;
+          ps += (d[base + i].bytes + piece - 1) / piece;
+        }
+        inl.piece_start[cnt] = ps;
+        HIPCHK(launch_peer_push(inl, (uint32_t)cnt, ps, piece, pw, (hipStream_t)s));
+        launches_++;
+      }
+      return Status::OK;
+    }
     uint32_t wgs = (uint32_t)config().copy_workgroups;
     if (wgs == 0) wgs = 64;
     for (size_t base = 0; base < n; base += kInlineDescs) {
@@ -422,7 +439,7 @@ class HipBackend : public Backend {
       last_err_ = "hsa_signal_create failed";
       return Status::NO_MEMORY;
     }
-    struct Piece { void* dst; hsa_agent_t da; const void* src; hsa_agent_t sa; size_t len; };
+    struct Piece { void* dst; hsa_agent_t da; const void* src; hsa_agent_t sa; size_t len; uint32_t engine; };
     std::vector<Piece> pieces;
     pieces.reserve(n);
     for (size_t i = 0; i < n; ++i) {
@@ -438,6 +455,7 @@ class HipBackend : public Backend {
           return Status::INVALID_ARGUMENT;
         }
         pc.len = len;
+        pc.engine = d[i].engine;
         pieces.push_back(pc);
         dst += len;
         src += len;
@@ -452,8 +470,10 @@ class HipBackend : public Backend {
                (unsigned long long)dd.cpu.handle);
     for (auto& pc : pieces) {
       const bool h2d = pc.sa.handle == dd.cpu.handle, d2h = pc.da.handle == dd.cpu.handle;
-      uint32_t mask = h2d ? dd.h2d : (d2h ? dd.d2h : dd.d2d);
-      hsa_amd_sdma_engine_id_t eng = (hsa_amd_sdma_engine_id_t)pick_engine(mask, channel);
+      uint32_t mask = h2d ? dd.h2d : (d2h ? dd.d2h : peer_mask(dd, pc.da));
+      uint32_t e = (pc.engine && (pc.engine & mask)) ? pc.engine : pick_engine(mask, channel);
+      hsa_amd_sdma_engine_id_t eng = (hsa_amd_sdma_engine_id_t)e;
+      __atomic_fetch_add(&dd.eng_bytes[__builtin_ctz(e)], (uint64_t)pc.len, __ATOMIC_RELAXED);
       hsa_status_t st = hsa_amd_memory_async_copy_on_engine(pc.dst, pc.da, pc.src, pc.sa, pc.len, 0, nullptr, sig,
                                                             eng, true);
       if (st != HSA_STATUS_SUCCESS) {
@@ -513,6 +533,11 @@ class HipBackend : public Backend {
 
   Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {
     HIPCHK(launch_dgemm(a, mode, (hipStream_t)s));
+    launches_++;
+    return Status::OK;
+  }
+  Status dgemm_fused(int, const DGemmFusedArgs& a, void* s) override {
+    HIPCHK(launch_dgemm_fused(a, (hipStream_t)s));
     launches_++;
     return Status::OK;
   }
@@ -695,8 +720,16 @@ class HipBackend : public Backend {
   struct DmaDev {
     bool ok = false;
     hsa_agent_t gpu{0}, cpu{0};
-    uint32_t h2d = 0, d2h = 0, d2d = 0;
+    uint32_t h2d = 0, d2h = 0;
+    uint32_t peer[kMaxGpus] = {};     // engines copying this GPU -> GPU e (hsa_amd_memory_copy_engine_status(e, this))
+    uint64_t eng_bytes[32] = {};      // bytes per SDMA engine (atomic adds)
   };
+  // Engines for a copy from dd's GPU into the HBM of the GPU owning agent `dst`.
+  uint32_t peer_mask(const DmaDev& dd, hsa_agent_t dst) {
+    for (size_t e = 0; e < dma_.size(); ++e)
+      if (dma_[e].gpu.handle == dst.handle) return dd.peer[e] ? dd.peer[e] : dd.h2d | dd.d2h;
+    return dd.h2d | dd.d2h;
+  }
   static hsa_status_t dma_agent_cb(hsa_agent_t a, void* data) {
     auto* v = (std::vector<hsa_agent_t>*)data;
     v->push_back(a);
@@ -753,11 +786,30 @@ class HipBackend : public Backend {
             uint32_t m = 0;
             if (hsa_amd_memory_copy_engine_status(dd.gpu, cpu, &m) == HSA_STATUS_SUCCESS) dd.h2d = m;
             if (hsa_amd_memory_copy_engine_status(cpu, dd.gpu, &m) == HSA_STATUS_SUCCESS) dd.d2h = m;
-            dd.d2d = dd.h2d | dd.d2h;
             dd.ok = config().copy_engine == 3 && cpu.handle && dd.h2d && dd.d2h;
           }
       }
+      // Per GPU pair (xGMI peers): the engines of the source that reach the
+      // destination - not the host-direction masks (uvm_gpu.c:2332-2388).
+      for (int a = 0; a < ndev_ && a < kMaxGpus; ++a)
+        for (int b = 0; b < ndev_ && b < kMaxGpus; ++b) {
+          if (a == b || !dma_[a].gpu.handle || !dma_[b].gpu.handle) continue;
+          uint32_t m = 0;
+          if (hsa_amd_memory_copy_engine_status(dma_[b].gpu, dma_[a].gpu, &m) == HSA_STATUS_SUCCESS) dma_[a].peer[b] = m;
+        }
     });
+  }
+  uint32_t copy_engine_mask(int dst_dev, int src_dev) override {
+    dma_init();
+    if (src_dev < 0) return dst_dev >= 0 && dst_dev < (int)dma_.size() ? dma_[dst_dev].h2d : 0;
+    if (src_dev >= (int)dma_.size()) return 0;
+    if (dst_dev < 0) return dma_[src_dev].d2h;
+    return dst_dev < kMaxGpus && dst_dev != src_dev ? dma_[src_dev].peer[dst_dev] : 0;
+  }
+  void engine_bytes(int dev, uint64_t out[32]) override {
+    dma_init();
+    for (int i = 0; i < 32; ++i)
+      out[i] = dev >= 0 && dev < (int)dma_.size() ? __atomic_load_n(&dma_[dev].eng_bytes[i], __ATOMIC_RELAXED) : 0;
   }
   // The ring kinds get distinct engines so H2D, D2H, CXL and peer traffic never
   // queue behind each other: channel k -> the k-th available engine of the mask.

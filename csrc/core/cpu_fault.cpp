@@ -23,6 +23,7 @@
 #include <linux/futex.h>
 #include <signal.h>
 #include <sys/syscall.h>
+#include <time.h>
 #include <ucontext.h>
 #include <unistd.h>
 
@@ -77,27 +78,48 @@ bool in_view(uint64_t a) {
 
 // ---------------------------------------------------------------- fault slots
 constexpr int kSlots = 256;
-enum : int { SLOT_FREE = 0, SLOT_CLAIMED = 1, SLOT_POSTED = 2, SLOT_DONE = 3 };
+// FREE -> CLAIMED (handler) -> POSTED (handler) -> SERVICING (service thread,
+// CAS) -> DONE (service) -> FREE (handler). A BUSY slot goes SERVICING -> POSTED
+// again with a not-before time, so it is retried in a LATER batch and never
+// holds up the other posted faults.
+enum : int { SLOT_FREE = 0, SLOT_CLAIMED = 1, SLOT_POSTED = 2, SLOT_SERVICING = 3, SLOT_DONE = 4 };
 struct alignas(64) FaultSlot {
   std::atomic<int> state{SLOT_FREE};
   uint64_t addr = 0;
   int write = 0;
   int result = 0;
+  // service thread only
+  uint64_t retry_at_ns = 0;
+  int busy_tries = 0;
 };
 FaultSlot g_slots[kSlots];
 std::atomic<int> g_posted{0};  // futex word of the service thread: number of posts ever made
 std::atomic<bool> g_service_up{false};
 std::atomic<pid_t> g_service_tid{0};
 std::atomic<uint64_t> g_serviced{0}, g_passed_on{0};
+constexpr int kBusyTries = 20000;  // ~10 s of BUSY retries (20 us, then 500 us apart)
 
-long futex(std::atomic<int>* w, int op, int val) {
-  return syscall(SYS_futex, reinterpret_cast<int*>(w), op, val, nullptr, nullptr, 0);
+long futex(std::atomic<int>* w, int op, int val, const struct timespec* ts = nullptr) {
+  return syscall(SYS_futex, reinterpret_cast<int*>(w), op, val, ts, nullptr, 0);
+}
+
+uint64_t mono_ns() {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
 }
 
 std::atomic<bool> g_service_stop{false};
 // Heap-held so a process that exits without shutting the runtime down does not
 // destroy a joinable std::thread (std::terminate) in static destructors.
 std::thread* g_service = nullptr;
+
+void complete(FaultSlot& s, Status st) {
+  s.result = (int)st;
+  g_serviced.fetch_add(1, std::memory_order_relaxed);
+  s.state.store(SLOT_DONE, std::memory_order_release);
+  futex(&s.state, FUTEX_WAKE_PRIVATE, 1);
+}
 
 // Bottom half: every posted fault is serviced in ONE batch (one
 // service_faults call: coalescing, one copy submission, one wait), then the
@@ -106,41 +128,67 @@ std::thread* g_service = nullptr;
 void service_loop() {
   g_service_tid.store((pid_t)syscall(SYS_gettid));
   int seen = 0;
+  uint64_t next_retry = 0;  // earliest not-before time of a BUSY slot (0 = none)
   std::vector<FaultSlot*> batch;
   std::vector<std::pair<uint64_t, bool>> req;
   std::vector<Status> res;
   while (!g_service_stop.load(std::memory_order_acquire)) {
     int now = g_posted.load(std::memory_order_acquire);
-    if (now == seen) {
-      futex(&g_posted, FUTEX_WAIT_PRIVATE, seen);
+    const uint64_t t = mono_ns();
+    if (now == seen && (!next_retry || t < next_retry)) {
+      if (next_retry) {
+        struct timespec ts{0, (long)std::min<uint64_t>(next_retry - t, 1000000)};
+        futex(&g_posted, FUTEX_WAIT_PRIVATE, seen, &ts);
+      } else {
+        futex(&g_posted, FUTEX_WAIT_PRIVATE, seen);
+      }
       continue;
     }
     seen = now;
+    next_retry = 0;
     batch.clear();
     req.clear();
-    for (auto& s : g_slots)
-      if (s.state.load(std::memory_order_acquire) == SLOT_POSTED) {
-        batch.push_back(&s);
-        req.emplace_back(s.addr, s.write != 0);
+    for (auto& s : g_slots) {
+      if (s.state.load(std::memory_order_acquire) != SLOT_POSTED) continue;
+      if (s.busy_tries && s.retry_at_ns > t) {
+        next_retry = next_retry ? std::min(next_retry, s.retry_at_ns) : s.retry_at_ns;
+        continue;
       }
+      int expect = SLOT_POSTED;  // the handler may take a slot back once the service is down
+      if (!s.state.compare_exchange_strong(expect, SLOT_SERVICING, std::memory_order_acq_rel)) continue;
+      batch.push_back(&s);
+      req.emplace_back(s.addr, s.write != 0);
+    }
     if (batch.empty()) continue;
     Runtime* rt = Runtime::get();
     res.assign(batch.size(), Status::NOT_FOUND);
     if (rt) rt->cpu_fault_batch(req, &res);
+    const uint64_t t1 = mono_ns();
     for (size_t k = 0; k < batch.size(); ++k) {
       FaultSlot& s = *batch[k];
       Status st = res[k];
       // BUSY: a GPU lease pins the only copy (the GPU may be writing it); the
       // CPU access waits for the release, like a CPU fault on a block whose GPU
-      // mapping cannot be revoked yet (uvm_va_space.c:2540-2590 retries).
-      for (int tries = 0; rt && st == Status::BUSY && tries < 20000; ++tries) {
-        std::this_thread::sleep_for(std::chrono::microseconds(tries < 100 ? 20 : 500));
-        st = rt->cpu_fault(s.addr, s.write != 0);
+      // mapping cannot be revoked yet (uvm_va_space.c:2540-2590 retries) - in a
+      // later batch, so the rest of this one completes now.
+      if (rt && st == Status::BUSY && s.busy_tries < kBusyTries) {
+        s.retry_at_ns = t1 + (s.busy_tries < 100 ? 20000ull : 500000ull);
+        s.busy_tries++;
+        next_retry = next_retry ? std::min(next_retry, s.retry_at_ns) : s.retry_at_ns;
+        s.state.store(SLOT_POSTED, std::memory_order_release);
+        continue;
       }
-      s.result = (int)st;
-      g_serviced.fetch_add(1, std::memory_order_relaxed);
-      s.state.store(SLOT_DONE, std::memory_order_release);
-      futex(&s.state, FUTEX_WAKE_PRIVATE, 1);
+      s.busy_tries = 0;
+      complete(s, st);
+    }
+  }
+  // Stopping: complete every fault still posted (NOT_FOUND -> the handler passes
+  // it on) so no faulting thread sleeps forever on its slot.
+  for (auto& s : g_slots) {
+    int expect = SLOT_POSTED;
+    if (s.state.compare_exchange_strong(expect, SLOT_SERVICING, std::memory_order_acq_rel)) {
+      s.busy_tries = 0;
+      complete(s, Status::NOT_FOUND);
     }
   }
 }
@@ -194,7 +242,22 @@ void segv_handler(int sig, siginfo_t* si, void* uc) {
   slot->state.store(SLOT_POSTED, std::memory_order_release);
   g_posted.fetch_add(1, std::memory_order_acq_rel);
   futex(&g_posted, FUTEX_WAKE_PRIVATE, 1);
-  while (slot->state.load(std::memory_order_acquire) != SLOT_DONE) futex(&slot->state, FUTEX_WAIT_PRIVATE, SLOT_POSTED);
+  // Bounded sleeps: if the service stopped after this thread passed the
+  // g_service_up check (and after its final sweep), take the slot back and pass
+  // the fault on instead of sleeping forever.
+  for (;;) {
+    int st = slot->state.load(std::memory_order_acquire);
+    if (st == SLOT_DONE) break;
+    struct timespec ts{0, 20 * 1000 * 1000};
+    futex(&slot->state, FUTEX_WAIT_PRIVATE, st, &ts);
+    if (!g_service_up.load(std::memory_order_acquire) && !g_service_tid.load()) {
+      int expect = SLOT_POSTED;
+      if (slot->state.compare_exchange_strong(expect, SLOT_FREE, std::memory_order_acq_rel)) {
+        pass_on(sig, si, uc);
+        return;
+      }
+    }
+  }
   int result = slot->result;
   slot->state.store(SLOT_FREE, std::memory_order_release);
   if (result != (int)Status::OK) pass_on(sig, si, uc);

@@ -5,6 +5,8 @@
 #include <numaif.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -52,8 +54,27 @@ static int version_from_speed(const std::string& s) {
   return 0;
 }
 
-void CxlTopology::discover(int emulate_node, const std::string& root) {
+void CxlTopology::discover(int emulate_node, const std::string& root, uint64_t emulate_mask) {
   info_ = CxlInfo{};
+  node_ids_.clear();
+  distances_.clear();
+  {
+    // SLIT: node<N>/distance lists the distances to every online node in
+    // ascending node-id order.
+    std::string nodes = root + "/devices/system/node";
+    for (auto& name : list_dir(nodes))
+      if (name.rfind("node", 0) == 0 && name.size() > 4 && isdigit((unsigned char)name[4]))
+        node_ids_.push_back(atoi(name.c_str() + 4));
+    std::sort(node_ids_.begin(), node_ids_.end());
+    for (int nid : node_ids_) {
+      std::istringstream in(read_line(nodes + "/node" + std::to_string(nid) + "/distance"));
+      std::vector<int> row;
+      int v;
+      while (in >> v) row.push_back(v);
+      if (row.size() != node_ids_.size()) row.assign(node_ids_.size(), -1);
+      distances_.push_back(row);
+    }
+  }
   // 1) CXL memory devices on the cxl bus.
   std::string bus = root + "/bus/cxl/devices";
   for (auto& name : list_dir(bus)) {
@@ -103,16 +124,20 @@ void CxlTopology::discover(int emulate_node, const std::string& root) {
       info_.devices.push_back(d);
     }
   }
-  // 3) Emulation: an ordinary NUMA node stands in for a CXL pool (no CXL hardware).
-  if (info_.numa_nodes.empty() && emulate_node >= 0) {
+  // 3) Emulation: ordinary NUMA nodes stand in for CXL pools (no CXL hardware).
+  if (emulate_node >= 0 && emulate_node < 64) emulate_mask |= 1ull << emulate_node;
+  if (info_.numa_nodes.empty() && emulate_mask) {
     info_.emulated = true;
-    info_.numa_nodes.push_back(emulate_node);
-    CxlDevice d;
-    d.name = "emulated-node" + std::to_string(emulate_node);
-    d.numa_node = emulate_node;
-    d.link_up = true;
-    d.version = 2;
-    info_.devices.push_back(d);
+    for (int nid = 0; nid < 64; ++nid) {
+      if (!((emulate_mask >> nid) & 1)) continue;
+      info_.numa_nodes.push_back(nid);
+      CxlDevice d;
+      d.name = "emulated-node" + std::to_string(nid);
+      d.numa_node = nid;
+      d.link_up = true;
+      d.version = 2;
+      info_.devices.push_back(d);
+    }
   }
   info_.num_devices = (uint32_t)info_.devices.size();
   info_.max_links = info_.num_devices;
@@ -121,6 +146,26 @@ void CxlTopology::discover(int emulate_node, const std::string& root) {
   info_.link_up = info_.link_mask != 0;
   info_.memory_expander = !info_.numa_nodes.empty() || !info_.devices.empty();
   for (auto& d : info_.devices) info_.cxl_version = std::max<uint32_t>(info_.cxl_version, (uint32_t)d.version);
+}
+
+int CxlTopology::distance(int from, int to) const {
+  size_t i = std::find(node_ids_.begin(), node_ids_.end(), from) - node_ids_.begin();
+  size_t j = std::find(node_ids_.begin(), node_ids_.end(), to) - node_ids_.begin();
+  if (i >= node_ids_.size() || j >= node_ids_.size()) return -1;
+  return distances_[i][j];
+}
+
+int CxlTopology::nearest_node(int from) const {
+  int best = first_node(), best_d = -1;
+  for (int n : info_.numa_nodes) {
+    int d = distance(from, n);
+    if (d < 0) continue;
+    if (best_d < 0 || d < best_d || (d == best_d && n < best)) {
+      best = n;
+      best_d = d;
+    }
+  }
+  return best;
 }
 
 bool CxlTopology::is_cxl_node(int nid) const {

@@ -138,7 +138,8 @@ const char* counter_name(Counter c) {
                             "page_list_copies",
                             "vmm_remaps",
                             "vmm_errors",
-                            "tlb_flushes"};
+                            "tlb_flushes",
+                            "faults_cancelled"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

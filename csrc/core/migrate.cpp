@@ -53,7 +53,11 @@ Loc Runtime::demotion_target(const Loc& from) {
     return cpu_loc();
   }
   if (from.tier == Tier::HOST) {
-    int n = cxl_topo_.first_node();
+    // The CXL pool nearest the host node the data leaves (SLIT distance), as
+    // block_select_node_residency picks the node closest to the processor
+    // (uvm_va_block.c:11714-11760): with one runtime per GPU, each rank's host
+    // tier is its GPU's socket, so every rank demotes to its own socket's pool.
+    int n = cxl_topo_.nearest_node(from.id);
     if (n >= 0) return Loc::cxl(n);
   }
   return Loc{Tier::HOST, -1};  // nowhere to go
@@ -263,6 +267,7 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
       s.user_data = b->range->id;
       s.file = __FILE__;
       s.line = __LINE__;
+      if (from->loc.is_gpu() && to->loc.is_gpu() && from->loc.id != to->loc.id) s.dst_dev = to->loc.id;
       if (log_level() >= LogLevel::DEBUG)
         s.desc = "range " + std::to_string(b->range->id) + " block " + std::to_string(b->index) + " " +
                  from->loc.str() + "->" + to->loc.str();
@@ -1536,6 +1541,7 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
     if (!r || faults[i].block >= r->nblocks || r->type != RangeType::MANAGED) {
       result = Status::INVALID_ARGUMENT;  // fatal fault: cancelled
       tools_event(ToolsEventType::FatalFault, Cause::User, Loc{}, Loc{}, proc, faults[i].offset, 0, faults[i].range_id);
+      for (size_t k = i; k < j; ++k) faults[k].status = Status::INVALID_ARGUMENT;
       i = j;
       continue;
     }
@@ -1617,6 +1623,7 @@ Status Runtime::service_faults(std::vector<FaultEntry>& faults, Tracker* out) {
       c.need_arena = nullptr;
     }
     if (st != Status::OK && result == Status::OK) result = st;
+    for (size_t k = i; k < j; ++k) faults[k].status = st;
     i = j;
   }
   Status fs = finish_ctx(c, out);
@@ -1875,10 +1882,23 @@ size_t Runtime::poll_device_faults(int dev) {
         Tools::get().inc(Counter::AccessCounterMigrations);
     }
   }
+  // Precise cancel (cancel_faults_precise, uvm_gpu_replayable_faults.c:2863):
+  // channels whose faults cannot be serviced are marked errored and their
+  // gates released with kGateCancelled instead of being replayed blindly.
+  std::vector<std::pair<uint16_t, Status>> cancel;
+  for (auto& pc : per_channel)
+    if (pc.second == 2) cancel.emplace_back(pc.first, Status::INVALID_ARGUMENT);
   if (!faults.empty()) {
     Tracker t;
-    service_faults(faults, &t);
-    t.wait();
+    Status sst = service_faults(faults, &t);
+    Status wst = t.wait();
+    for (auto& f : faults) {
+      Status fst = f.status != Status::OK ? f.status : wst;
+      if (fst != Status::OK) cancel.emplace_back(f.channel, fst);
+    }
+    if (sst != Status::OK)
+      RT_WARN("device fault batch on GPU %d: service failed (%s), %zu fault(s) cancelled", dev, status_str(sst),
+              cancel.size());
     // The batch has landed: publish the new residency to the device tables
     // (entries stay 0 while copies are in flight), then replay - kernels
     // stalled in k_fault_gate re-check and proceed (BATCH_FLUSH policy).
@@ -1894,6 +1914,30 @@ size_t Runtime::poll_device_faults(int dev) {
         update_device_table(b);
       }
     }
+  }
+  if (!cancel.empty()) {
+    // Mark the channels errored, then bump their cancel words BEFORE the replay
+    // token: a woken gate sees the cancel, never a bare replay of a fault that
+    // will not be serviced.
+    std::sort(cancel.begin(), cancel.end(),
+              [](const std::pair<uint16_t, Status>& a, const std::pair<uint16_t, Status>& b) { return a.first < b.first; });
+    uint16_t last = 0xffff;
+    for (auto& cc : cancel) {
+      if (cc.first == last) continue;
+      last = cc.first;
+      {
+        std::lock_guard<std::mutex> g(channels_m_);
+        if (cc.first && cc.first <= channels_.size() && channels_[cc.first - 1].id) {
+          Channel& ch = channels_[cc.first - 1];
+          if (ch.error == Status::OK) ch.error = cc.second;
+          ch.cancelled_faults++;
+        }
+      }
+      __atomic_fetch_add(&fb.hdr->cancel[cc.first % kFaultCancelSlots], 1u, __ATOMIC_RELEASE);
+      Tools::get().inc(Counter::FaultsCancelled);
+    }
+  }
+  if (!faults.empty() || !cancel.empty()) {
     __atomic_fetch_add(&fb.hdr->replay, 1, __ATOMIC_RELEASE);
     Tools::get().inc(Counter::FaultReplays);
     tools_event(ToolsEventType::GpuFaultReplay, Cause::User, Loc{}, Loc::gpu(dev), dev, 0, faults.size(), 0);

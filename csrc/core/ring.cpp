@@ -29,7 +29,8 @@ Ring::Ring(Backend* be, int dev, RingKind kind, uint32_t entries) : be_(be), dev
   }
   // PCIe / xGMI rings run their copies on a copy engine (SDMA) when there is one.
   dma_ = config().copy_engine == 3 && kind != RingKind::GPU_INTERNAL && kind != RingKind::MEMOPS &&
-         be_->dma_supported(dev) && err_ == Status::OK;
+         !(kind == RingKind::GPU_TO_GPU && config().peer_copy_engine == 0) && be_->dma_supported(dev) &&
+         err_ == Status::OK;
   if (dma_) worker_ = std::thread([this] { worker(); });
 }
 
@@ -164,6 +165,36 @@ void Ring::worker() {
   }
 }
 
+std::vector<CopyDesc> split_over_engines(const std::vector<CopyDesc>& in, uint32_t mask, uint64_t min_piece,
+                                         uint32_t* rot) {
+  std::vector<uint32_t> engs;
+  for (int b = 0; b < 32; ++b)
+    if ((mask >> b) & 1) engs.push_back(1u << b);
+  std::vector<CopyDesc> out;
+  if (engs.empty()) {
+    out = in;
+    return out;
+  }
+  constexpr uint64_t kAlign = 64 << 10;
+  for (const CopyDesc& c : in) {
+    uint64_t k = min_piece ? c.bytes / min_piece : 1;
+    if (k > engs.size()) k = engs.size();
+    if (k < 2) {
+      CopyDesc d = c;
+      d.engine = engs[(*rot)++ % engs.size()];
+      out.push_back(d);
+      continue;
+    }
+    uint64_t piece = (c.bytes / k + kAlign - 1) / kAlign * kAlign;
+    for (uint64_t off = 0; off < c.bytes; off += piece) {
+      CopyDesc d{c.dst + off, c.src + off, std::min(piece, c.bytes - off)};
+      d.engine = engs[(*rot)++ % engs.size()];
+      out.push_back(d);
+    }
+  }
+  return out;
+}
+
 Status Ring::run_batch(Batch& b) {
   // Copies go to the engine (synchronously, from this thread); kernel SQEs
   // (fused decode, memset, page gather / scatter) go to the side stream
@@ -171,6 +202,7 @@ Status Ring::run_batch(Batch& b) {
   // the engine copies after it. The stream is drained before an engine copy
   // that follows kernels (the copy may read their output) and at batch end.
   std::vector<CopyDesc> copies;
+  std::vector<int> copy_dst;  // GPU_TO_GPU: the peer each copy writes
   std::vector<DecodeDesc> decodes;
   Status st = Status::OK;
   bool kernels_pending = false;
@@ -188,9 +220,28 @@ Status Ring::run_batch(Batch& b) {
   auto flush_copies = [&] {
     if (!copies.empty()) {
       drain();
+      if (kind_ == RingKind::GPU_TO_GPU) {
+        // xGMI peer copies, pushed by this (source) GPU: large copies split over
+        // every SDMA engine of the (peer, source) pair, each piece on its own
+        // engine - the per-link split the reference does with one CE channel per
+        // peer (uvm_va_block.c:3390-3460, uvm_channel.c peer pools).
+        std::vector<CopyDesc> split;
+        const uint64_t min_piece = (uint64_t)std::max<int64_t>(1, config().peer_split_min_mb) << 20;
+        for (size_t i = 0; i < copies.size();) {
+          size_t j = i;
+          while (j < copies.size() && copy_dst[j] == copy_dst[i]) ++j;
+          std::vector<CopyDesc> run(copies.begin() + i, copies.begin() + j);
+          uint32_t mask = copy_dst[i] >= 0 ? be_->copy_engine_mask(copy_dst[i], dev_) : 0;
+          std::vector<CopyDesc> part = split_over_engines(run, mask, min_piece, &engine_rot_);
+          split.insert(split.end(), part.begin(), part.end());
+          i = j;
+        }
+        copies.swap(split);
+      }
       if (st == Status::OK) st = be_->dma_copy(dev_, copies.data(), copies.size(), (int)kind_);
     }
     copies.clear();
+    copy_dst.clear();
   };
   for (auto& s : b.ops) {
     if (st != Status::OK) break;
@@ -198,10 +249,12 @@ Status Ring::run_batch(Batch& b) {
       case SqeOp::COPY:
         flush_decodes();
         if (!copies.empty() && copies.back().dst + copies.back().bytes == s.dst &&
-            copies.back().src + copies.back().bytes == s.src)
+            copies.back().src + copies.back().bytes == s.src && copy_dst.back() == s.dst_dev) {
           copies.back().bytes += s.bytes;
-        else
+        } else {
           copies.push_back(CopyDesc{s.dst, s.src, s.bytes});
+          copy_dst.push_back(s.dst_dev);
+        }
         break;
       case SqeOp::DECODE_BF12:
         flush_copies();
@@ -272,7 +325,9 @@ FenceRef Ring::submit_locked() {
   uint64_t last = 0;
   std::vector<CopyDesc> batch;
   std::vector<DecodeDesc> dbatch;
-  int engine = kind_ == RingKind::GPU_INTERNAL ? 2 : (int)config().copy_engine;
+  int engine = kind_ == RingKind::GPU_INTERNAL ? 2
+               : (kind_ == RingKind::GPU_TO_GPU && config().peer_copy_engine == 0) ? 4
+                                                                                  : (int)config().copy_engine;
   auto flush = [&]() {
     if (st == Status::OK && !batch.empty()) {
       st = be_->copy_batch(dev_, batch.data(), batch.size(), stream_, engine);

@@ -41,7 +41,7 @@ Runtime* Runtime::init(const std::string& backend, int fake_devices, uint64_t fa
     if (local(d)) first_local = d;
   rt->host_node_ = cfg.host_node >= 0 ? (int)cfg.host_node
                                        : (first_local >= 0 ? rt->be_->device_numa_node(first_local) : 0);
-  rt->cxl_topo_.discover((int)cfg.cxl_emulate_node);
+  rt->cxl_topo_.discover((int)cfg.cxl_emulate_node, "/sys", (uint64_t)cfg.cxl_emulate_mask);
   rt->cxl_ = std::make_unique<CxlRegistry>(rt->be_.get());
   rt->cxl_->init(system_ram_bytes() / 100 * (uint64_t)cfg.cxl_pin_budget_pct, (uint32_t)cfg.cxl_max_buffers,
                  (uint64_t)cfg.cxl_max_buffer_gb << 30);

@@ -27,6 +27,7 @@ struct CopyDesc {
   uint64_t dst;
   uint64_t src;
   uint64_t bytes;
+  uint32_t engine = 0;  // dma_copy: SDMA engine bit to use (0 = the backend picks by direction / channel)
 };
 
 // Page-list pack/unpack (k_gather_pages / k_scatter_pages): copies `npages`
@@ -112,7 +113,8 @@ class Backend {
 
   // ---- work submission (ordered on `stream`)
   // engine: 0 = copy kernel with the PCIe CU budget, 1 = hipMemcpyAsync, 2 = copy
-  // kernel with the whole chip (HBM<->HBM).
+  // kernel with the whole chip (HBM<->HBM), 4 = k_peer_push (source GPU writes
+  // the peer's HBM over xGMI with config().peer_push_wgs workgroups).
   virtual Status copy_batch(int dev, const CopyDesc* d, size_t n, void* stream, int engine) = 0;
   // ---- DMA copy engines (SDMA), driven from a ring's worker thread: no CU, no
   // stream. `channel` picks the engine (one per ring kind and direction).
@@ -121,6 +123,15 @@ class Backend {
   virtual Status dma_copy(int dev, const CopyDesc* d, size_t n, int channel) {
     (void)dev; (void)d; (void)n; (void)channel;
     return Status::NOT_SUPPORTED;
+  }
+  // SDMA engines of `src_dev` able to copy src_dev -> dst_dev (-1 = host
+  // memory): the bitmask of hsa_amd_memory_copy_engine_status(dst, src) - per
+  // GPU pair for xGMI peers (uvm_gpu.c:2332-2388 reads peer caps per pair).
+  virtual uint32_t copy_engine_mask(int dst_dev, int src_dev) { (void)dst_dev; (void)src_dev; return 0; }
+  // Bytes each SDMA engine of `dev` has copied (index = engine bit), for tests / stats.
+  virtual void engine_bytes(int dev, uint64_t out[32]) {
+    (void)dev;
+    for (int i = 0; i < 32; ++i) out[i] = 0;
   }
   // workgroups = 0: config().decode_workgroups (sized for H2D streaming); HBM->HBM
   // unpacking passes a full-chip grid.
@@ -149,6 +160,8 @@ class Backend {
   // Decode GEMM (ogkm/dgemm.hpp): split-K partials, then the fused epilogue.
   virtual Status dgemm(int dev, const DGemmArgs& a, int mode, void* stream) = 0;
   virtual Status dgemm_reduce(int dev, const DGemmReduceArgs& a, void* stream) = 0;
+  // Fused raw-weight decode GEMM (split-K reduce + epilogue in the same launch).
+  virtual Status dgemm_fused(int dev, const DGemmFusedArgs& a, void* stream) = 0;
   // Fused decode-step ops (ogkm/dgemm.hpp).
   virtual Status rmsnorm(int dev, const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim,
                          uint32_t ldx, uint32_t ldy, float eps, void* stream) = 0;

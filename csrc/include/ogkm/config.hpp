@@ -64,6 +64,9 @@ namespace ogkm {
   /* channels / ring */                                                                              \
   X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \
   X(copy_engine, 3, "PCIe/xGMI ring copies: 3=SDMA engines driven by the ring's worker (default) 1=hipMemcpyAsync 0=our CU copy kernels") \
+  X(peer_copy_engine, 3, "GPU->GPU ring copies: 3=SDMA split over the pair's xGMI engines 0=k_peer_push CU kernel") \
+  X(peer_split_min_mb, 8, "GPU->GPU copies >= 2x this are split into pieces over the pair's SDMA engines") \
+  X(peer_push_wgs, 64, "workgroups (CU budget) of one k_peer_push launch")                             \
   X(copy_workgroups, 16, "workgroups per copy-kernel launch (CU budget; 16 saturate PCIe, more starve HBM-bound compute)") \
   X(copy_piece_kb, 64, "bytes per copy work item (KB)")                                              \
   X(copy_nt_loads, 1, "copy kernels: non-temporal source loads (0 = plain loads)")                      \
@@ -81,6 +84,7 @@ namespace ogkm {
   X(cxl_pin_budget_pct, 90, "max pinned bytes as percent of system RAM")                             \
   X(cxl_max_dma_mb, 4095, "single CXL DMA request clamp (MB)")                                       \
   X(cxl_emulate_node, -1, "treat this NUMA node as CXL when no CXL hardware (-1 = off)")             \
+  X(cxl_emulate_mask, 0, "bitmask of NUMA nodes treated as CXL pools when no CXL hardware")          \
   /* debug */                                                                                        \
   X(lock_check, 0, "enable the lock-order checker")                                                  \
   X(fake_race_check, 0, "fake backend: report kernels (debug_touch) that touch a chunk an engine copy is using") \

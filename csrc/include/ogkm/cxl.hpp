@@ -56,14 +56,24 @@ class CxlTopology {
  public:
   // Scans /sys/bus/cxl/devices and /sys/devices/system/node; `emulate_node`
   // (config cxl_emulate_node) turns an ordinary NUMA node into a CXL pool.
-  void discover(int emulate_node, const std::string& sysfs_root = "/sys");
+  // `emulate_mask`: every NUMA node whose bit is set stands in for a CXL pool
+  // (ORed with `emulate_node`); only used when no real CXL memory is found.
+  void discover(int emulate_node, const std::string& sysfs_root = "/sys", uint64_t emulate_mask = 0);
   const CxlInfo& info() const { return info_; }
   CxlInfo& mutable_info() { return info_; }
   bool is_cxl_node(int nid) const;
   int first_node() const { return info_.numa_nodes.empty() ? -1 : info_.numa_nodes[0]; }
+  // SLIT distance between two NUMA nodes (node<from>/distance), -1 when unknown.
+  int distance(int from, int to) const;
+  // The CXL node closest to NUMA node `from` (smallest SLIT distance, ties to the
+  // lower node id; first_node() when distances are unknown): the placement rule
+  // of block_select_node_residency, uvm_va_block.c:11714-11760.
+  int nearest_node(int from) const;
 
  private:
   CxlInfo info_;
+  std::vector<int> node_ids_;                // online NUMA nodes, ascending (the SLIT column order)
+  std::vector<std::vector<int>> distances_;  // distances_[i][j]: node_ids_[i] -> node_ids_[j]
 };
 
 // Pin budget accounting (nv-p2p.c:1034-1111): max pinned bytes and max buffers.

@@ -182,6 +182,7 @@ enum class Counter : int {
   VmmRemaps,        // stable-VA block remaps (unmap / map of a 2 MB VMM handle)
   VmmErrors,        // failed stable-VA unmaps / maps / translation flushes
   TlbFlushes,       // GPU translation flushes after stable-VA remaps
+  FaultsCancelled,  // channels whose device faults were cancelled (precise cancel)
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -21,6 +21,12 @@
 // residency tables refreshed) the host bumps `replay`; a kernel stalled on a
 // fault (k_fault_gate) waits for the token to move, then re-checks residency -
 // the replay policy BATCH_FLUSH of uvm_gpu_replayable_faults.c:2986-3022.
+//
+// Precise cancel (cancel_faults_precise, uvm_gpu_replayable_faults.c:2863):
+// when servicing a channel's fault fails (or the fault is fatal: freed range,
+// out of bounds), the host bumps `cancel[channel % kFaultCancelSlots]` BEFORE
+// the replay token. A gate snapshots its channel's word at entry and, once the
+// replay wakes it, exits with status kGateCancelled instead of re-recording.
 #pragma once
 
 #include <cstdint>
@@ -28,6 +34,9 @@
 namespace ogkm {
 
 constexpr uint16_t kFaultWholeBlock = 0xffff;  // record.page: the access needs the whole 2 MB block
+constexpr uint32_t kFaultCancelSlots = 64;      // per-channel cancel words (channel id mod 64; 0 = no channel)
+// k_fault_gate status[0]
+constexpr uint32_t kGateResolved = 0, kGateTimeout = 2, kGateCancelled = 3;
 
 struct DeviceFaultRecord {
   uint64_t range_id;
@@ -51,8 +60,9 @@ struct FaultBufHeader {
   uint32_t pad2[15];
   uint64_t replay;     // bumped by the host after each serviced batch landed
   uint64_t pad3[7];
+  uint32_t cancel[kFaultCancelSlots];  // bumped (before `replay`) when a channel's faults are cancelled
 };
-static_assert(sizeof(FaultBufHeader) == 256, "fault buffer header layout");
+static_assert(sizeof(FaultBufHeader) == 256 + 4 * kFaultCancelSlots, "fault buffer header layout");
 
 // Host-side producer with the device protocol (fake backend, tests, CPU
 // emulation of a faulting processor). `entries` is a power of two. `may_drop`:

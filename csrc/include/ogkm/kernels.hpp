@@ -35,6 +35,10 @@ struct KInlineDescs {   // passed by value as a kernel argument for small batche
 hipError_t launch_batch_copy(const KCopyDesc* d_descs, const uint64_t* d_piece_start, const KInlineDescs* inl,
                              uint32_t n, uint64_t total_pieces, uint32_t piece_bytes, uint32_t workgroups,
                              hipStream_t s, bool nt_loads = true);
+// k_peer_push: source-GPU push of up to kInlineDescs copies (typically into a
+// peer's HBM over xGMI) with a bounded grid of `workgroups`.
+hipError_t launch_peer_push(const KInlineDescs& inl, uint32_t n, uint64_t total_pieces, uint32_t piece_bytes,
+                            uint32_t workgroups, hipStream_t s);
 hipError_t launch_gather_pages(uint64_t base, uint64_t contig, const uint32_t* d_idx, uint32_t npages,
                                uint32_t page_bytes, bool scatter, uint32_t workgroups, hipStream_t s);
 hipError_t launch_memset32(uint64_t dst, uint32_t pattern, uint64_t bytes, hipStream_t s);
@@ -77,6 +81,7 @@ hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, ui
 // Decode GEMM (csrc/kernels/decode_gemm.hip); argument structs in ogkm/dgemm.hpp.
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);
 hipError_t launch_dgemm_reduce(const DGemmReduceArgs& a, hipStream_t s);
+hipError_t launch_dgemm_fused(const DGemmFusedArgs& a, hipStream_t s);
 // Fused decode-step ops (csrc/kernels/decode_ops.hip).
 hipError_t launch_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim,
                           uint32_t ldx, uint32_t ldy, float eps, hipStream_t s);
@@ -100,9 +105,10 @@ hipError_t launch_managed_gather(const uint64_t* table, uint64_t range_id, const
 // [b0, b0 + nblocks) of a range in its device residency table; every block not
 // resident in HBM is recorded as a fault and the wave waits for the host's
 // replay token (re-recording every ~1 ms), then re-checks. Work queued behind
-// the gate on the stream runs once every block is resident. status[0]: 0 =
-// resolved, 2 = cancelled after `timeout_us` (the kernel always exits);
-// status[1] = number of replays the gate waited for.
+// the gate on the stream runs once every block is resident. status[0]:
+// kGateResolved, kGateTimeout (gave up after `timeout_us`; the kernel always
+// exits) or kGateCancelled (the host cancelled this channel's faults: precise
+// cancel, fault_abi.hpp); status[1] = number of replays the gate waited for.
 hipError_t launch_fault_gate(const uint64_t* table, uint64_t range_id, uint32_t b0, uint32_t nblocks, KFaultBuf fb,
                              uint32_t proc, uint32_t access, uint32_t timeout_us, uint32_t* status, hipStream_t s);
 

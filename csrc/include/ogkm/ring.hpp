@@ -59,6 +59,7 @@ struct Sqe {
   SqeOp op = SqeOp::NOP;
   uint64_t user_data = 0;
   uint64_t dst = 0, src = 0, bytes = 0;
+  int32_t dst_dev = -1;            // COPY on a GPU_TO_GPU ring: the peer GPU written (engine-mask lookup)
   uint32_t pattern = 0;            // MEMSET
   uint32_t page_bytes = 0;         // GATHER / SCATTER
   std::vector<uint32_t> idx;       // GATHER / SCATTER page indices
@@ -73,6 +74,13 @@ struct Cqe {
   uint64_t seq;
   int32_t status;
 };
+
+// Split copies over the SDMA engines in `mask` (bit per engine): a copy of at
+// least 2 * min_piece bytes becomes min(#engines, bytes / min_piece) pieces
+// (64 KB aligned), each on the next engine in rotation (`rot`, carried across
+// calls, so small copies spread over the engines too). mask 0: unchanged.
+std::vector<CopyDesc> split_over_engines(const std::vector<CopyDesc>& in, uint32_t mask, uint64_t min_piece,
+                                         uint32_t* rot);
 
 class Ring {
  public:
@@ -128,6 +136,7 @@ class Ring {
   std::atomic<uint64_t> next_seq_{1};  // read lock-free by pushed_seq()
   std::atomic<uint64_t> submitted_{0};  // read lock-free by wait_seq
   uint64_t batches_ = 0;
+  uint32_t engine_rot_ = 0;  // GPU_TO_GPU: engine rotation across split pieces (worker thread only)
   FenceRef last_fence_;
   std::atomic<Status> err_{Status::OK};
   std::string err_desc_;

@@ -52,6 +52,7 @@ struct FaultEntry {
   uint64_t block = 0;
   uint32_t first_page = 0, npages = 0;
   bool duplicate = false;
+  Status status = Status::OK;  // set by service_faults: this entry's group outcome (precise cancel)
 };
 
 // Device fault buffer: GET/PUT ring of DeviceFaultRecord (ogkm/fault_abi.hpp)
@@ -231,7 +232,7 @@ class Runtime {
     int dev = 0;
     void* stream = nullptr;
     std::string name;
-    uint64_t faults = 0, remote_accesses = 0, fatal_faults = 0;
+    uint64_t faults = 0, remote_accesses = 0, fatal_faults = 0, cancelled_faults = 0;
     Status error = Status::OK;
   };
   uint16_t register_channel(int dev, void* stream, const std::string& name);

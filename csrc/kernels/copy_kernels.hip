@@ -124,6 +124,52 @@ hipError_t launch_batch_copy(const KCopyDesc* d_descs, const uint64_t* d_piece_s
   return hipGetLastError();
 }
 
+// k_peer_push: the SOURCE GPU pushes its HBM into a peer's HBM over xGMI (the
+// reference pushes peer copies from the source GPU's channel,
+// uvm_va_block.c:3390-3460). A bounded grid (config peer_push_wgs = the CU
+// budget taken from compute); each workgroup streams whole 64 KB pieces with 8
+// 16-B loads in flight per lane (non-temporal: read once locally, written once
+// remotely), so the remote-write latency of the link is covered.
+__global__ void __launch_bounds__(kThreads)
+    k_peer_push(KInlineDescs inl, uint32_t n, uint64_t total_pieces, uint32_t piece_bytes) {
+  constexpr int kU = 8;
+  uint32_t i = 0;
+  for (uint64_t p = blockIdx.x; p < total_pieces; p += gridDim.x) {
+    while (i + 1 < n && inl.piece_start[i + 1] <= p) ++i;  // pieces visited in increasing order
+    const KCopyDesc d = inl.d[i];
+    const uint64_t off = (p - inl.piece_start[i]) * (uint64_t)piece_bytes;
+    uint64_t len = d.bytes - off;
+    if (len > piece_bytes) len = piece_bytes;
+    const uint64_t dst = d.dst + off, src = d.src + off;
+    if (((dst | src | len) & 15) == 0) {
+      const u32x4* s16 = reinterpret_cast<const u32x4*>(src);
+      u32x4* d16 = reinterpret_cast<u32x4*>(dst);
+      const uint64_t n16 = len >> 4;
+      uint64_t j = threadIdx.x;
+      for (; j + (kU - 1) * kThreads < n16; j += kU * kThreads) {
+        u32x4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[u] = __builtin_nontemporal_load(s16 + j + u * kThreads);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) __builtin_nontemporal_store(v[u], d16 + j + u * kThreads);
+      }
+      for (; j < n16; j += kThreads) __builtin_nontemporal_store(__builtin_nontemporal_load(s16 + j), d16 + j);
+    } else {
+      copy_span(dst, src, len);
+    }
+  }
+}
+
+hipError_t launch_peer_push(const KInlineDescs& inl, uint32_t n, uint64_t total_pieces, uint32_t piece_bytes,
+                            uint32_t workgroups, hipStream_t s) {
+  if (n == 0 || total_pieces == 0) return hipSuccess;
+  if (n > (uint32_t)kInlineDescs || piece_bytes % 4096 || inl.piece_start[n] != total_pieces) return hipErrorInvalidValue;
+  uint32_t grid = (uint32_t)(total_pieces < workgroups ? total_pieces : workgroups);
+  if (grid == 0) grid = 1;
+  hipLaunchKernelGGL(k_peer_push, dim3(grid), dim3(kThreads), 0, s, inl, n, total_pieces, piece_bytes);
+  return hipGetLastError();
+}
+
 // Pack (gather) / unpack (scatter) of a page list: page i <-> base + idx[i]*page_bytes.
 __global__ void __launch_bounds__(kThreads)
     k_gather_pages(uint64_t base, uint64_t contig, const uint32_t* __restrict__ idx, uint32_t npages,
@@ -302,8 +348,19 @@ __global__ void __launch_bounds__(64)
   const uint32_t lane = threadIdx.x;
   const uint64_t t0 = wall_clock64();
   uint32_t replays = 0;
+  // Precise cancel: the host bumps this channel's word before the replay token
+  // when it gives up on the channel's faults (fault_abi.hpp).
+  uint32_t* cancel_word = fb.hdr->cancel + ((proc >> 16) % kFaultCancelSlots);
+  const uint32_t cancel0 = __hip_atomic_load(cancel_word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
     const uint64_t token = __hip_atomic_load(&fb.hdr->replay, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (__hip_atomic_load(cancel_word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != cancel0) {
+      if (lane == 0) {
+        status[0] = kGateCancelled;
+        status[1] = replays;
+      }
+      return;
+    }
     int miss = 0;
     for (uint32_t b = b0 + lane; b < b0 + nblocks; b += 64) {
       uint64_t hbm = __hip_atomic_load(table + 2 * (uint64_t)b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -314,7 +371,7 @@ __global__ void __launch_bounds__(64)
     }
     if (!__any(miss)) {
       if (lane == 0) {
-        status[0] = 0;
+        status[0] = kGateResolved;
         status[1] = replays;
       }
       return;
@@ -327,7 +384,7 @@ __global__ void __launch_bounds__(64)
       uint64_t now = wall_clock64();
       if (now - t0 > timeout_ticks) {
         if (lane == 0) {
-          status[0] = 2;
+          status[0] = kGateTimeout;
           status[1] = replays;
         }
         return;

@@ -431,6 +431,7 @@ PYBIND11_MODULE(_ogkm, m) {
       d["faults"] = c.faults;
       d["remote_accesses"] = c.remote_accesses;
       d["fatal_faults"] = c.fatal_faults;
+      d["cancelled_faults"] = c.cancelled_faults;
       d["error"] = status_str(c.error);
       out.append(d);
     }
@@ -674,6 +675,27 @@ PYBIND11_MODULE(_ogkm, m) {
     check(r->submit()->wait(), "ring_gather");
   });
   m.def("ring_stream", [](int dev, int kind) { return (uint64_t)ring_of(dev, kind)->stream(); });
+  // Peer plane: SDMA engine masks per (dst, src) pair (-1 = host) and per-engine bytes.
+  m.def("copy_engine_mask", [](int dst, int src) { return rt()->be()->copy_engine_mask(dst, src); });
+  m.def("engine_bytes", [](int dev) {
+    uint64_t v[32];
+    rt()->be()->engine_bytes(dev, v);
+    return std::vector<uint64_t>(v, v + 32);
+  });
+  m.def("split_over_engines", [](std::vector<std::tuple<uint64_t, uint64_t, uint64_t>> copies, uint32_t mask,
+                                 uint64_t min_piece) {
+    std::vector<CopyDesc> in;
+    for (auto& c : copies) in.push_back(CopyDesc{std::get<0>(c), std::get<1>(c), std::get<2>(c)});
+    uint32_t rot = 0;
+    std::vector<std::tuple<uint64_t, uint64_t, uint64_t, uint32_t>> out;
+    for (auto& d : split_over_engines(in, mask, min_piece, &rot)) out.emplace_back(d.dst, d.src, d.bytes, d.engine);
+    return out;
+  });
+  // k_peer_push on `dev`'s stream (dst may be a peer's HBM or local), bounded grid.
+  m.def("peer_push", [](int dev, uint64_t stream, uint64_t dst, uint64_t src, uint64_t bytes) {
+    CopyDesc d{dst, src, bytes};
+    check(rt()->be()->copy_batch(dev, &d, 1, (void*)stream, 4), "peer_push");
+  });
   m.def("ring_wait_seq", [](int dev, int kind, uint64_t seq) {
     Ring* r = ring_of(dev, kind);
     py::gil_scoped_release nogil;
@@ -840,6 +862,44 @@ PYBIND11_MODULE(_ogkm, m) {
      py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("part"), py::arg("part_bytes"),
      py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("target_units") = 2048, py::arg("unroll") = 0,
      py::arg("lds_x") = 0);
+  // Fused raw-weight decode GEMM: (klw, kgroups, row_blocks, slab_bytes, cnt_words) for a shape.
+  m.def("dgemm_fused_plan", [](uint32_t N, uint32_t K, uint32_t M, uint32_t target_wgs, uint32_t unroll, bool silu) {
+    uint32_t klw, kg, rb;
+    dgemm_fused_plan(N, K, M, target_wgs, unroll, silu, &klw, &kg, &rb);
+    const uint64_t mb = (M + 63) / 64;
+    return py::make_tuple(klw, kg, rb, kg > 1 ? mb * rb * kg * kDgemmSlabFloats * 4 : 0, kg > 1 ? mb * rb : 0);
+  });
+  m.def("dgemm_fused", [](int dev, uint64_t stream, uint64_t w, uint64_t x, uint32_t ldx, uint32_t M, uint32_t N,
+                          uint32_t K, uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo,
+                          uint64_t slab, uint64_t slab_bytes, uint64_t cnt, uint64_t cnt_words, uint32_t target_wgs,
+                          uint32_t unroll) {
+    if (N % 16 || K % 32 || ldx % 8 || !M) throw StatusError("dgemm_fused: N % 16, K % 32, ldx % 8 and M > 0 required");
+    const bool silu = epi == DGEMM_EPI_SILU_MUL;
+    if (silu && N % 64) throw StatusError("dgemm_fused: SILU_MUL needs N % 64 == 0");
+    if (epi > DGEMM_EPI_SILU_MUL) throw StatusError("dgemm_fused: bad epilogue");
+    DGemmFusedArgs a{};
+    a.w = (const uint16_t*)w;
+    a.x = (const uint16_t*)x;
+    a.ldx = ldx; a.M = M; a.N = N; a.K = K;
+    a.unroll = unroll == 4 ? 4 : 2;
+    dgemm_fused_plan(N, K, M, target_wgs, a.unroll, silu, &a.klw, &a.kgroups, &a.row_blocks);
+    a.epi = epi;
+    a.resid = (const uint16_t*)resid; a.ldr = ldr;
+    a.out = (uint16_t*)out; a.ldo = ldo;
+    const uint64_t mb = (M + 63) / 64;
+    if (a.kgroups > 1) {
+      if (mb * a.row_blocks * a.kgroups * kDgemmSlabFloats * 4 > slab_bytes || mb * a.row_blocks > cnt_words || !slab ||
+          !cnt)
+        throw StatusError("dgemm_fused: slab / ticket workspace too small");
+      a.slab = (float*)slab;
+      a.cnt = (uint32_t*)cnt;
+    }
+    if (epi == DGEMM_EPI_RESID && !resid) throw StatusError("dgemm_fused: RESID needs resid");
+    check(rt()->be()->dgemm_fused(dev, a, (void*)stream), "dgemm_fused");
+    return a.kgroups;
+  }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("N"),
+     py::arg("K"), py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("slab"),
+     py::arg("slab_bytes"), py::arg("cnt"), py::arg("cnt_words"), py::arg("target_wgs") = 512, py::arg("unroll") = 2);
   // Fused decode-step ops (ops/fused.py).
   m.def("rmsnorm", [](int dev, uint64_t stream, uint64_t x, uint64_t w, uint64_t y, uint32_t rows, uint32_t dim,
                       uint32_t ldx, uint32_t ldy, float eps) {
@@ -879,6 +939,10 @@ PYBIND11_MODULE(_ogkm, m) {
     d["put"] = fb.hdr ? __atomic_load_n(&fb.hdr->put, __ATOMIC_ACQUIRE) : 0;
     d["get"] = fb.hdr ? __atomic_load_n(&fb.hdr->get, __ATOMIC_ACQUIRE) : 0;
     d["replay"] = fb.hdr ? __atomic_load_n(&fb.hdr->replay, __ATOMIC_ACQUIRE) : 0;
+    py::list cancel;
+    for (uint32_t i = 0; i < kFaultCancelSlots; ++i)
+      cancel.append(fb.hdr ? __atomic_load_n(&fb.hdr->cancel[i], __ATOMIC_ACQUIRE) : 0u);
+    d["cancel"] = cancel;
     return d;
   });
 
@@ -973,9 +1037,14 @@ PYBIND11_MODULE(_ogkm, m) {
     d["pin_budget_bytes"] = rt()->cxl().pins().max_bytes();
     return d;
   });
-  m.def("cxl_rediscover", [](int emulate_node, const std::string& root) {
-    rt()->cxl_topology().discover(emulate_node, root);
-  }, py::arg("emulate_node") = -1, py::arg("root") = "/sys");
+  m.def("cxl_rediscover", [](int emulate_node, const std::string& root, uint64_t emulate_mask) {
+    rt()->cxl_topology().discover(emulate_node, root, emulate_mask);
+  }, py::arg("emulate_node") = -1, py::arg("root") = "/sys", py::arg("emulate_mask") = 0);
+  m.def("cxl_nearest_node", [](int from) { return rt()->cxl_topology().nearest_node(from); });
+  m.def("demotion_target", [](int tier, int id) {
+    Loc l = rt()->demotion_target(make_loc(tier, id));
+    return py::make_tuple((int)l.tier, l.id);
+  });
   m.def("cxl_set_measured_bw", [](double mbps) { rt()->cxl_topology().mutable_info().per_link_bw_mbps = mbps; });
   m.def("cxl_register", [](uint64_t base, uint64_t size, int version) {
     uint64_t h;

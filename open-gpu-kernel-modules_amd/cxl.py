@@ -21,7 +21,7 @@ import os
 import ctypes.util
 import mmap
 import time
-from typing import Optional
+from typing import Iterable, Optional
 
 from ._native import lib
 
@@ -33,8 +33,14 @@ def get_info() -> dict:
     return lib.cxl_info()
 
 
-def rediscover(emulate_node: int = -1, sysfs_root: str = "/sys") -> dict:
-    lib.cxl_rediscover(emulate_node, sysfs_root)
+def rediscover(emulate_node: int = -1, sysfs_root: str = "/sys", emulate_nodes: Iterable[int] = ()) -> dict:
+    """Re-scan CXL memory. Without CXL hardware, ``emulate_node`` / every node in
+    ``emulate_nodes`` stands in for a CXL pool (one per socket lets every rank
+    demote to the pool on its own socket: ``lib.cxl_nearest_node``)."""
+    mask = 0
+    for n in emulate_nodes:
+        mask |= 1 << int(n)
+    lib.cxl_rediscover(emulate_node, sysfs_root, mask)
     return lib.cxl_info()
 
 

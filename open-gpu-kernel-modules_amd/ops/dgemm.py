@@ -36,6 +36,10 @@ TARGET_UNITS_PACKED = int(os.environ.get("OGKM_DGEMM_UNITS_PACKED", "2048"))
 LDS_X = int(os.environ.get("OGKM_DGEMM_LDS", "-1"))
 LDS_MAX_N = 8192
 UNROLL = int(os.environ.get("OGKM_DGEMM_UNROLL", "0"))  # K steps per pipelined block (0 = kernel default)
+# Raw weights: the fused kernel (k_dgemm_fused: split-K reduce + epilogue inside
+# the launch, two-deep register pipeline) replaces k_dgemm[_lds] + k_dgemm_reduce.
+FUSED = int(os.environ.get("OGKM_DGEMM_FUSED", "1"))
+FUSED_WGS = int(os.environ.get("OGKM_DGEMM_WGS", "512"))  # workgroups per GEMM (2 per CU)
 
 
 def frag_permute(w: torch.Tensor) -> torch.Tensor:
@@ -96,11 +100,33 @@ class _Workspace:
 
 _WS = _Workspace()
 _PLANS: dict = {}
+_FPLANS: dict = {}
+_TICKETS: dict = {}   # (device, stream) -> zeroed int32 ticket words (self-resetting)
+_SLABS: dict = {}     # (device, stream) -> f32 slab workspace
+
+
+def _fused_ws(device: torch.device, stream: int, slab_bytes: int, cnt_words: int):
+    key = (str(device), stream)
+    cnt = _TICKETS.get(key)
+    if cnt is None or cnt.numel() < cnt_words:
+        cnt = _TICKETS[key] = torch.zeros(max(cnt_words, 4096), dtype=torch.int32, device=device)
+    slab = _SLABS.get(key)
+    if slab is None or slab.numel() * 4 < slab_bytes:
+        slab = _SLABS[key] = torch.empty(max(slab_bytes // 4, 1 << 18), dtype=torch.float32, device=device)
+    return slab, cnt
+
+
+def fused_ok(w: "WeightRef", epi: str) -> bool:
+    """The fused kernel covers raw weights (any epilogue; SiLU needs N % 64)."""
+    return bool(FUSED) and w.mode == MODE_RAW and (epi != "silu_mul" or w.n % 64 == 0)
 
 
 def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tensor | None = None,
-           out: torch.Tensor | None = None, device_index: int = 0, lds: int | None = None) -> torch.Tensor:
-    """x: [M, K] bf16 (row stride % 8 == 0). Returns out [M, N] (silu_mul: [M, N/2])."""
+           out: torch.Tensor | None = None, device_index: int = 0, lds: int | None = None,
+           fused: bool | None = None) -> torch.Tensor:
+    """x: [M, K] bf16 (row stride % 8 == 0). Returns out [M, N] (silu_mul: [M, N/2]).
+    ``fused``: None = the fused kernel whenever it covers the call (raw weights),
+    False = the split-K kernels + reduce launch (``lds`` picks the raw variant)."""
     if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1 or x.shape[1] != w.k:
         raise ValueError("dgemm.linear: x must be a row-major bf16 [M, K] view")
     m = x.shape[0]
@@ -112,6 +138,22 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     if epi == "resid":
         if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
             raise ValueError("dgemm.linear: resid must match out")
+    stream = int(torch.cuda.current_stream(device_index).cuda_stream) if x.is_cuda else 0
+    if fused is None:
+        fused = fused_ok(w, epi) and lds is None
+    elif fused and not (w.mode == MODE_RAW and (epi != "silu_mul" or w.n % 64 == 0)):
+        raise ValueError("dgemm.linear: the fused kernel needs raw weights (SiLU: N % 64 == 0)")
+    if fused:
+        pk = (w.n, w.k, m, epi == "silu_mul")
+        plan = _FPLANS.get(pk)
+        if plan is None:
+            plan = _FPLANS[pk] = lib.dgemm_fused_plan(w.n, w.k, m, FUSED_WGS, 2, epi == "silu_mul")
+        slab, cnt = _fused_ws(x.device, stream, plan[3], plan[4])
+        lib.dgemm_fused(device_index, stream, w.ptr + 2 * w.off, x.data_ptr(), x.stride(0), m, w.n, w.k, EPI[epi],
+                        resid.data_ptr() if resid is not None else 0, resid.stride(0) if resid is not None else 0,
+                        out.data_ptr(), out.stride(0), slab.data_ptr(), slab.numel() * 4, cnt.data_ptr(), cnt.numel(),
+                        FUSED_WGS, 2)
+        return out
     lds = LDS_X if lds is None else int(lds)
     if lds < 0:
         lds = int(w.mode == MODE_RAW and w.n <= LDS_MAX_N)
@@ -123,7 +165,6 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
         ks = _PLANS[(w.n, w.k, units)] = lib.dgemm_plan(w.n, w.k, units)[0]
     ksplit = ks
     part = _WS.get(x.device, ksplit * m * w.n * 4)
-    stream = int(torch.cuda.current_stream(device_index).cuda_stream) if x.is_cuda else 0
     lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), x.stride(0), m, w.n, w.k,
               part.data_ptr(), part.numel() * 4, EPI[epi], resid.data_ptr() if resid is not None else 0,
               resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, UNROLL, lds)

@@ -133,3 +133,62 @@ def test_dma_roundtrip_verifies_data(fake_rt):
     lg.release(0)
     g.free()
     buf.unregister()
+
+
+def _two_socket_sysfs(tmp_path):
+    """Two CPU sockets (nodes 0, 1), each with a CPU-less CXL node attached:
+    node 2 behind socket 1, node 3 behind socket 0 (ids deliberately crossed,
+    so 'first node' and 'nearest node' differ for socket 0)."""
+    nodes = tmp_path / "devices" / "system" / "node"
+    slit = {0: "10 32 40 20", 1: "32 10 20 40", 2: "40 20 10 50", 3: "20 40 50 10"}
+    for nid, cpus in ((0, "0-7"), (1, "8-15"), (2, ""), (3, "")):
+        d = nodes / f"node{nid}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(cpus + "\n")
+        (d / "meminfo").write_text(f"Node {nid} MemTotal:       {1 << 20} kB\n")
+        (d / "distance").write_text(slit[nid] + "\n")
+    return tmp_path
+
+
+def test_demotion_goes_to_nearest_cxl_node(fake_rt, tmp_path):
+    """Host-tier data demotes to the CXL pool nearest the host node it leaves
+    (block_select_node_residency, uvm_va_block.c:11714-11760), not to the first
+    CXL node: socket 0 -> node 3, socket 1 -> node 2."""
+    root = _two_socket_sysfs(tmp_path)
+    info = cxl.rediscover(-1, str(root))
+    assert info["numa_nodes"] == [2, 3]
+    assert lib.cxl_nearest_node(0) == 3 and lib.cxl_nearest_node(1) == 2
+    TIER_HOST, TIER_CXL = 1, 2
+    assert lib.demotion_target(TIER_HOST, 0) == (TIER_CXL, 3)
+    assert lib.demotion_target(TIER_HOST, 1) == (TIER_CXL, 2)
+    # the demotions of a full host tier land on node 3 (nearest to host node 0)
+    lib.configure("host_budget_mb", 8)
+    lib.init_device(0, 8 * MB)
+    bufs = []
+    for i in range(6):
+        b = rt.malloc_managed(4 * MB, f"d{i}")
+        l = b.acquire(0, rt.WRITE)
+        l.wait(0)
+        l.tensor((4 * MB,), torch.uint8).fill_(i + 1)
+        l.release(0)
+        bufs.append(b)
+    placed = [(r["tier"], r["id"]) for b in bufs for o in (0, 2 * MB) for r in b.residency(o)["resident_on"]]
+    assert ("cxl", 3) in placed and ("cxl", 2) not in placed, placed
+    for i, b in enumerate(bufs):
+        assert int(b.read().min()) == i + 1
+        b.free()
+
+
+def test_emulated_cxl_pool_per_socket(fake_rt, tmp_path):
+    """Without CXL hardware, one emulated pool per socket: each host node's
+    nearest pool is its own socket's node."""
+    root = _two_socket_sysfs(tmp_path)
+    for nid in (2, 3):  # drop the CPU-less nodes: a plain 2-socket box
+        for f in (root / "devices" / "system" / "node" / f"node{nid}").iterdir():
+            f.unlink()
+        (root / "devices" / "system" / "node" / f"node{nid}").rmdir()
+    for nid, row in ((0, "10 32"), (1, "32 10")):
+        (root / "devices" / "system" / "node" / f"node{nid}" / "distance").write_text(row + "\n")
+    info = cxl.rediscover(-1, str(root), emulate_nodes=(0, 1))
+    assert info["emulated"] and info["numa_nodes"] == [0, 1]
+    assert lib.cxl_nearest_node(0) == 0 and lib.cxl_nearest_node(1) == 1

@@ -177,3 +177,40 @@ def test_user_channel_attribution_and_fatal_cancel(fake_rt):
     lib.unregister_channel(b_id)
     assert [c["name"] for c in lib.channels()] == ["decode"]
     b.free()
+
+
+def test_failed_service_cancels_channel_precisely(fake_rt):
+    """A fault whose service fails (injected populate error) is cancelled for
+    its channel only: the channel is marked errored, its cancel word is bumped
+    before the replay token (a gate waiting on it exits with kGateCancelled),
+    and a healthy channel's fault in the same batch is serviced
+    (cancel_faults_precise, uvm_gpu_replayable_faults.c:2863)."""
+    lib.init_device(0, 64 * MB)
+    ok_buf = rt.malloc_managed(2 * MB, "ok")
+    ok_buf.write(torch.ones(2 * MB, dtype=torch.uint8))
+    bad = rt.malloc_managed(2 * MB, "bad")            # never written: its first fault must populate
+    good_ch = lib.register_channel(0, 0x5000, "good")
+    bad_ch = lib.register_channel(0, 0x6000, "bad")
+    info0 = lib.fault_buffer_info(0)
+    lib.inject("populate_error", 1)
+    _inject([(bad.id, 0, 0xFFFF, 1, 0, bad_ch << 16)])
+    lib.poll_device_faults(0)
+    info1 = lib.fault_buffer_info(0)
+    assert info1["cancel"][bad_ch % 64] == info0["cancel"][bad_ch % 64] + 1
+    assert info1["cancel"][good_ch % 64] == info0["cancel"][good_ch % 64]
+    assert info1["replay"] == info0["replay"] + 1     # the gate is woken, and sees the cancel
+    ch = {c["name"]: c for c in lib.channels()}
+    assert ch["bad"]["error"] != "OK" and ch["bad"]["cancelled_faults"] == 1
+    assert ch["good"]["error"] == "OK"
+    assert lib.stats()["faults_cancelled"] >= 1
+    # the healthy channel's fault is serviced as usual, nothing cancelled
+    _inject([(ok_buf.id, 0, 0xFFFF, 1, 0, good_ch << 16)])
+    lib.poll_device_faults(0)
+    info2 = lib.fault_buffer_info(0)
+    assert info2["cancel"] == info1["cancel"] and info2["replay"] == info1["replay"] + 1
+    assert any(r["tier"] == "gpu" for r in ok_buf.residency(0)["resident_on"])
+    assert lib.global_status() == "OK"
+    lib.unregister_channel(good_ch)
+    lib.unregister_channel(bad_ch)
+    bad.free()
+    ok_buf.free()

@@ -96,6 +96,34 @@ def test_fault_gate_times_out_without_service(gpu_rt):
     b.free()
 
 
+def test_fault_gate_cancelled_when_service_fails(gpu_rt):
+    """Precise cancel on hardware: the gate's fault cannot be serviced (one
+    injected populate error), so the host cancels the gate's channel within one
+    poll - the gate exits with kGateCancelled (3) instead of re-recording until
+    its timeout, and the channel reports an error."""
+    b = rt.malloc_managed(2 * MB, "cancel")           # never written: the fault must populate
+    lib.device_table(b.id)
+    s = torch.cuda.Stream()
+    ch = lib.register_channel(0, s.cuda_stream, "gated")
+    status = torch.full((2,), 7, dtype=torch.int32, device="cuda")
+    lib.inject("populate_error", 1)
+    t0 = time.perf_counter()
+    lib.fault_gate(b.id, 0, 2 * MB, 0, s.cuda_stream, status.data_ptr(), timeout_ms=20000)
+    polls = 0
+    while not s.query() and time.perf_counter() - t0 < 15:
+        polls += lib.poll_device_faults(0) > 0
+        time.sleep(0.001)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    st = status.cpu().tolist()
+    chans = {c["id"]: c for c in lib.channels()}
+    lib.unregister_channel(ch)
+    assert st[0] == 3, st                             # cancelled, not resolved / timed out
+    assert 1 <= polls <= 2 and dt < 5, (polls, dt)  # a 1 ms re-record may race the first service
+    assert chans[ch]["error"] != "OK" and chans[ch]["cancelled_faults"] == 1, chans[ch]
+    b.free()
+
+
 def test_table_shootdown_fences_queued_readers(gpu_rt):
     """Evicting a block listed in a device table clears its entry and fences
     the chunk on the registered table streams (no stale-chunk reads)."""

@@ -317,3 +317,46 @@ def test_fragmented_block_copy_is_one_page_list_kernel(fake_rt):
     assert torch.equal(l.tensor((2 * MB,), torch.uint8).clone(), ref)
     l.release()
     b.free()
+
+
+def test_busy_cpu_fault_retried_later_without_blocking_others(fake_rt):
+    """A CPU fault on a block whose only copy a GPU lease pins is BUSY: the
+    service thread retries it in a LATER batch (uvm_va_space.c:2540-2590
+    retries) while other posted faults complete right away; it completes once
+    the lease is released."""
+    import ctypes
+    import threading
+    import time
+
+    a = rt.malloc_managed(2 * MB, "busy")
+    la = a.acquire(0, rt.WRITE)
+    la.wait(0)
+    la.tensor((2 * MB // 4,), torch.int32).fill_(11)
+    b = rt.malloc_managed(2 * MB, "free")
+    b.write(torch.full((2 * MB // 4,), 22, dtype=torch.int32))
+    lb = b.acquire(0, rt.READ)                     # GPU copy only while leased ...
+    lb.wait(0)
+    lb.release(0)
+    va, vb = a.cpu_view(torch.int32), b.cpu_view(torch.int32)
+    got = {}
+
+    def touch(name, view):
+        buf = ctypes.c_int32()
+        ctypes.memmove(ctypes.addressof(buf), view.data_ptr() + 4096, 4)   # faults with the GIL released
+        got[name] = (buf.value, time.perf_counter())
+
+    t0 = time.perf_counter()
+    ta = threading.Thread(target=touch, args=("a", va))
+    ta.start()
+    time.sleep(0.05)                                # a's fault is posted and BUSY
+    tb = threading.Thread(target=touch, args=("b", vb))
+    tb.start()
+    tb.join(5)
+    assert "b" in got and got["b"][0] == 22 and "a" not in got
+    time.sleep(0.05)
+    la.release(0)                                   # now a's retry succeeds
+    ta.join(10)
+    assert got["a"][0] == 11 and got["a"][1] > got["b"][1]
+    assert time.perf_counter() - t0 < 10
+    a.free()
+    b.free()

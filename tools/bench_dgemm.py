@@ -22,15 +22,32 @@ if os.environ.get("SHAPES"):  # e.g. "6144x4096,4096x4096,28672x4096,4096x14336"
     SHAPES = tuple(tuple(int(v) for v in s.split("x")) for s in os.environ["SHAPES"].split(","))
 
 
-def timeit(fn, it=10):
+def timeit(fn, it=20):
+    """GPU time per call from events around a captured HIP graph of `it` calls
+    (no host launch overhead in the number; falls back to eager launches)."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(it):
-        fn()
+    try:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(it):
+                    fn()
+        run = g.replay
+    except Exception:  # noqa: BLE001 - eager fallback
+        def run():
+            for _ in range(it):
+                fn()
+    run()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / it
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    run()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / it
 
 
 def main():
@@ -45,7 +62,7 @@ def main():
         ws[(n, k)] = (flat, stream.cuda(), info, dgemm.packed_mode(stream))
     xs = {k: (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16) for _, k in SHAPES}
     stage = torch.empty(max(n * k for n, k in SHAPES), dtype=torch.bfloat16, device="cuda")
-    variants = [("raw", u) for u in (2, 4)] + [("bf11", u) for u in (1, 2, 4)] + [("staged", 2)]
+    variants = [("fused", 2)] + [("raw", u) for u in (2, 4)] + [("bf11", u) for u in (1, 2, 4)] + [("staged", 2)]
     if os.environ.get("VARIANTS"):  # e.g. "bf11:2,raw:2"
         variants = [(v.split(":")[0], int(v.split(":")[1])) for v in os.environ["VARIANTS"].split(",")]
     for kind, u in variants:
@@ -54,9 +71,10 @@ def main():
         for (n, k), (flat, pk, info, mode) in ws.items():
             out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
             x = xs[k]
-            if kind == "raw":
+            if kind in ("raw", "fused"):
                 ref = dgemm.WeightRef(flat.data_ptr(), 0, n, k, dgemm.MODE_RAW)
-                fn = lambda: dgemm.linear(x, ref, out=out)  # noqa: E731
+                fz = kind == "fused"
+                fn = lambda: dgemm.linear(x, ref, out=out, fused=fz)  # noqa: E731
                 nb = n * k * 2
             elif kind == "bf11":
                 ref = dgemm.WeightRef(pk.data_ptr(), 0, n, k, mode, 20)
