@@ -96,8 +96,68 @@ def parse():
     ap.add_argument("--torch-managed", action="store_true",
                     help="run a stock torch.nn Llama (models/torch_llama.py) under ogkm.managed(): every tensor "
                          "oversubscribes HBM through the transparent mode, no hand-planned residency (1 GPU)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print the per-rank residency / traffic plan (JSON lines) of 70B and 405B, tp and shards, "
+                         "at N = 1, 2, 4, 8 GPUs - host and CXL NUMA nodes, PCIe and xGMI GB/step, predicted "
+                         "ms/step - without allocating anything (no GPU needed)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
+
+
+HBM_USABLE_GB = 270.0  # of the 288 GB per MI355X (runtime / RCCL / activation reserve)
+
+
+def plan_only(a) -> None:
+    """Dry-run residency plans (models/llama.py TieredLlama(dry_run=True) +
+    traffic()): what every rank of an N-GPU job would hold, stream and
+    exchange per decode step, before any multi-GPU run is launched."""
+    from ogkm.models import llama
+    try:
+        from ogkm._native import lib
+        n_dev = lib.device_count() if lib.is_initialized() else 0
+    except Exception:  # noqa: BLE001
+        n_dev = 0
+    models = [a.model] if a.model not in ("llama3-70b",) else ["llama3-70b", "llama3-405b"]
+    for model in models:
+        cfg = llama.CONFIGS[model]
+        tiers = "host+cxl" if model == "llama3-405b" else a.tiers
+        for parallel in ("tp", "shards"):
+            for n in (1, 2, 4, 8):
+                if parallel == "shards" and n == 1:
+                    continue
+                wf = "ans" if a.weights == "auto" else a.weights
+                kf = "ans" if a.kv_format == "auto" else a.kv_format
+                kw = dict(batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 3, tp_rank=0,
+                          tp_world=n, weight_format=wf, kv_format=kf, parallel=parallel, tiers=tiers,
+                          cxl_frac=a.cxl_frac, dry_run=True)
+                m = llama.TieredLlama(cfg, oversub=a.oversub, **kw)
+                oversub = a.oversub
+                if m.budget / 1e9 > HBM_USABLE_GB:  # the logical ratio does not fit one MI355X: cap at its HBM
+                    oversub = m.footprint / (HBM_USABLE_GB * 1e9)
+                    m = llama.TieredLlama(cfg, oversub=oversub, **kw)
+                d, t = m.describe(), m.traffic()
+                # one process per GPU: GPUs 0-3 sit on socket 0, 4-7 on socket 1 (MI355X 8-GPU node);
+                # each rank's host tier and its nearest (emulated) CXL pool are on its GPU's socket
+                nodes = [(lib.device_numa_node(r) if r < n_dev else r // 4) for r in range(n)]
+                out = {"plan": model, "parallel": f"{parallel}{n}", "n_gpus": n, "oversubscription": round(oversub, 3),
+                       "global_batch": a.batch, "seq_len": a.context, "weight_format": wf, "kv_format": kf,
+                       "tiers": tiers,
+                       "per_rank": {"host_numa_node": nodes, "cxl_numa_node": nodes,
+                                    "footprint_gb": round(d["footprint_gb"], 2), "hbm_budget_gb": round(d["hbm_budget_gb"], 2),
+                                    "resident_layers": d["resident_layers"], "streamed_layers": d["streamed_layers"],
+                                    "pcie_gb_per_step": round(t["pcie_gb"], 3),
+                                    "cxl_gb_per_step": round(d["cxl_streamed_gb_per_step"], 3),
+                                    "xgmi_gb_per_step": round(t["xgmi_gb"], 3), "hbm_gb_per_step": round(t["hbm_gb"], 2),
+                                    "collectives_per_step": t["collectives"],
+                                    "pcie_ms": round(t["pcie_ms"], 2), "xgmi_ms": round(t["xgmi_ms"], 2),
+                                    "hbm_ms": round(t["hbm_ms"], 2)},
+                       "predicted_ms_per_step": round(t["predicted_ms"], 2),
+                       "predicted_tokens_per_s": round(a.batch / (t["predicted_ms"] / 1e3), 1),
+                       "model": "PCIe %.1f GB/s, HBM %.0f GB/s, xGMI %.0f GB/s per link, %.0f us per collective"
+                                % (llama.PLAN_PCIE_GBPS, llama.PLAN_HBM_GBPS, __import__("ogkm.parallel.topology",
+                                   fromlist=["x"]).XGMI_LINK_GBPS, __import__("ogkm.parallel.topology",
+                                   fromlist=["x"]).COLLECTIVE_LATENCY_US)}
+                print(json.dumps(out), flush=True)
 
 
 def run_torch_managed(a) -> None:
@@ -115,11 +175,14 @@ def run_torch_managed(a) -> None:
     cfg = llama.CONFIGS[a.model]
     foot = torch_llama.footprint_bytes(cfg, a.batch, a.context)
     budget = int(foot / a.oversub)
-    allocator.enable(managed_min_mb=1)
+    # allocations >= OGKM_MANAGED_MIN_MB are managed (evictable) ranges; the
+    # op-trace prefetcher looks OGKM_MANAGED_LOOKAHEAD_MB ahead (-1: a quarter of the arena)
+    allocator.enable(managed_min_mb=int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")))
     rt.init("hip", hbm_budget={0: budget}, host_budget_mb=0)
     torch.cuda.set_device(0)
     prefill = a.context - (a.warmup + a.steps) - 1
-    mode = ogkm.managed()
+    la = int(os.environ.get("OGKM_MANAGED_LOOKAHEAD_MB", "-1"))
+    mode = ogkm.managed(lookahead_bytes=None if la < 0 else la << 20)
     t_init = time.perf_counter()
     with mode:
         model = torch_llama.build_on_device(cfg, a.batch, a.context, "cuda", seed=1234, prefill=prefill)
@@ -139,12 +202,14 @@ def run_torch_managed(a) -> None:
             pos += 1
         torch.cuda.synchronize()
         lib.reset_counters()
+        al0 = allocator.stats()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             tok = model.step(tok, pos)
             pos += 1
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        al1 = allocator.stats()
     s = lib.stats()
     name = {"llama3-70b": "Llama-3-70B", "llama3-405b": "Llama-3-405B", "llama3-8b": "Llama-3-8B"}.get(a.model, a.model)
     out = {
@@ -167,7 +232,10 @@ def run_torch_managed(a) -> None:
                 "dth_gb_per_step": round(s["bytes_xfer_dth"] / a.steps / 1e9, 2),
                 "link_gbps": round(s["bytes_xfer_htd"] / dt / 1e9, 2), "evictions": s["evictions"],
                 "vmm_remaps": s["vmm_remaps"], "tlb_flushes": s["tlb_flushes"], "ops": mode.ops,
-                "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches, "init_s": round(init_s, 1)},
+                "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches, "init_s": round(init_s, 1),
+                "allocs_per_step": (al1["allocs"] - al0["allocs"]) // max(1, a.steps), "alloc_peak_gb":
+                round(al1["peak"] / 1e9, 2), "managed_min_mb": int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")),
+                "lookahead_mb": la},
     }
     print(json.dumps(out), flush=True)
 
@@ -199,11 +267,18 @@ def bandwidth_probe(dev: int, barrier, nbytes: int = 1 << 30) -> tuple[dict, dic
         out[name] = 3 * nbytes / (time.perf_counter() - t0) / 1e9
     del g, h
     info = cxl.get_info()
-    node = info["numa_nodes"][0] if info["numa_nodes"] else lib.host_node()
-    meta = {"cxl_numa_node": node, "emulated": bool(info["emulated"] or not info["numa_nodes"])}
+    near = lib.cxl_nearest_node(lib.host_node()) if info["numa_nodes"] else lib.host_node()
+    far = [n for n in info["numa_nodes"] if n != near]
+    meta = {"cxl_numa_node": near, "emulated": bool(info["emulated"] or not info["numa_nodes"])}
     try:
-        r = cxl.measure_bandwidth(dev, nbytes, iters=3, node=node, barrier=barrier)
+        # the rank's own pool (nearest) is what tiering uses; the other socket's
+        # pool is measured too (remote CXL: the same full-rate SDMA engines)
+        r = cxl.measure_bandwidth(dev, nbytes, iters=3, node=near, barrier=barrier)
         out["cxl_to_hbm"], out["hbm_to_cxl"] = r["cxl_to_gpu_gbps"], r["gpu_to_cxl_gbps"]
+        if far:
+            r2 = cxl.measure_bandwidth(dev, nbytes, iters=3, node=far[0], barrier=barrier)
+            meta["remote"] = {"cxl_numa_node": far[0], "cxl_to_hbm": round(r2["cxl_to_gpu_gbps"], 2),
+                              "hbm_to_cxl": round(r2["gpu_to_cxl_gbps"], 2)}
     except Exception as e:  # no CXL / registration refused: report, do not fail the bench
         out["cxl_to_hbm"] = out["hbm_to_cxl"] = 0.0
         meta["error"] = str(e)
@@ -235,6 +310,9 @@ def probe_all_ranks(dev: int, rank: int) -> dict:
 
 def main() -> None:
     a = parse()
+    if a.plan_only:
+        plan_only(a)
+        return
     if a.torch_managed:
         run_torch_managed(a)
         return
@@ -276,12 +354,12 @@ def main() -> None:
         a.no_aux = True
     else:
         rt.init("hip", host_budget_mb=0, local_devices=1 << dev)
-    # The emulated CXL pool: a NUMA node that is not this GPU's (a remote memory node).
-    gpu_node = lib.device_numa_node(dev)
+    # No CXL hardware on the box: every NUMA node emulates a CXL pool, and each
+    # rank demotes to the pool nearest its GPU's node (SLIT distance,
+    # CxlTopology::nearest_node) - one pool per socket, as on a CXL-populated node.
     nodes = sorted({int(p.name[4:]) for p in Path("/sys/devices/system/node").glob("node[0-9]*")})
-    other = [n for n in nodes if n != gpu_node]
-    if not lib.cxl_info()["numa_nodes"] and other:
-        lib.cxl_rediscover(other[0], "/sys")
+    if not lib.cxl_info()["numa_nodes"] and nodes:
+        lib.cxl_rediscover(-1, "/sys", sum(1 << n for n in nodes))
     aux = {}
     if not a.no_aux:
         aux = probe_all_ranks(dev, e.rank)
@@ -309,6 +387,7 @@ def main() -> None:
     for _ in range(a.warmup):
         tok = model.step(tok)
     lib.reset_counters()
+    comm.reset_stats()
     if a.verbose:
         model.byte_trace = {}
     comm.barrier()
@@ -320,6 +399,8 @@ def main() -> None:
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
     s = lib.stats()
+    xgmi_in = comm.STATS["allreduce_bytes_in"] + comm.STATS["allgather_bytes_in"]
+    traffic = model.traffic()
     host_nodes = comm.all_gather_objects(lib.host_node())
     if a.dump_logits and e.rank == 0:
         torch.save(model.last_logits.float().cpu(), a.dump_logits)
@@ -399,6 +480,13 @@ def main() -> None:
             "aux": {
                 **aux,
                 "link_gbps_per_gpu": round((s["bytes_xfer_htd"] + s["bytes_xfer_ctd"]) / max(dt, 1e-9) / 1e9, 2),
+                # rank 0's per-step traffic: measured vs the plan (bench.py --plan-only prints the plan alone)
+                "traffic_per_step_gb": {
+                    "pcie_measured": round((s["bytes_xfer_htd"] + s["bytes_xfer_ctd"]) / a.steps / 1e9, 4),
+                    "pcie_planned": round(traffic["pcie_gb"], 4),
+                    "xgmi_measured": round(xgmi_in / a.steps / 1e9, 6),
+                    "xgmi_planned": round(traffic["xgmi_gb"], 6),
+                    "predicted_ms": round(traffic["predicted_ms"], 2)},
                 "cxl_to_hbm_gbps_per_gpu": round(s["bytes_xfer_ctd"] / max(dt, 1e-9) / 1e9, 2),
                 "evictions": s["evictions"],
                 "init_s": round(init_s, 1),

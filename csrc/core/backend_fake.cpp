@@ -181,9 +181,14 @@ class FakeBackend : public Backend {
     close((int)h);
     handles_.erase(it);
   }
-  Status va_reserve(size_t bytes, void** va) override {
-    void* m = mmap(nullptr, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    if (m == MAP_FAILED) return Status::NO_MEMORY;
+  Status va_reserve(size_t bytes, void** va, void* want) override {
+    void* m = mmap(want, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | (want ? MAP_FIXED_NOREPLACE : 0),
+                   -1, 0);
+    if (m == MAP_FAILED) return want ? Status::BUSY : Status::NO_MEMORY;
+    if (want && m != want) {
+      munmap(m, bytes);
+      return Status::BUSY;
+    }
     *va = m;
     return Status::OK;
   }

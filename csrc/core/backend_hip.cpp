@@ -5,10 +5,11 @@
 // * Host / CXL tiers: memfd pages registered with hipHostRegister (IOMMU-correct
 //   device mapping, identity address) - never raw physical addresses (fixes the
 //   reference's SKIP_IOMMU_MAPPING memdesc, p2p_cxl.c:167-217).
-// * Copies: hipMemcpyAsync on the ring's side stream (engine 1, the default for
-//   PCIe / xGMI copies; the kernel trace shows it as the runtime's
-//   __amd_rocclr_copyBuffer) or our hand-written copy kernels (engine 0;
-//   engine 2 = HBM<->HBM, always ours). Measured under the 70B decode
+// * Copies (config copy_engine): SDMA engines driven by the ring's worker thread
+//   (3, the default for PCIe / xGMI rings, below), hipMemcpyAsync on the ring's
+//   side stream (1; the kernel trace shows it as the runtime's
+//   __amd_rocclr_copyBuffer) or our hand-written copy kernels (0; engine 2 =
+//   HBM<->HBM, always ours; engine 4 = k_peer_push). Measured under the 70B decode
 //   (profiles/r1_copy_engine_interference.md): while our 16-WG copy kernel pulls
 //   host memory over PCIe, the HBM-bound compute kernels on the other stream
 //   run 3-7x slower (k_dgemm 42 -> 155 us, k_ans_unpack 114 -> 306 us); with
@@ -43,6 +44,7 @@
 #include "ogkm/config.hpp"
 #include "ogkm/kernels.hpp"
 #include "ogkm/events.hpp"
+#include "ogkm/ring.hpp"
 #include "ogkm/runtime.hpp"
 
 namespace ogkm {
@@ -231,8 +233,12 @@ class HipBackend : public Backend {
     return Status::OK;
   }
   void vmm_release(uint64_t h) override { (void)hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)h); }
-  Status va_reserve(size_t bytes, void** va) override {
-    HIPCHK(hipMemAddressReserve(va, bytes, kBlockSize, nullptr, 0));
+  Status va_reserve(size_t bytes, void** va, void* want) override {
+    HIPCHK(hipMemAddressReserve(va, bytes, kBlockSize, want, 0));
+    if (want && *va != want) {  // the address is only a hint to the driver
+      (void)hipMemAddressFree(*va, bytes);
+      return Status::BUSY;
+    }
     return Status::OK;
   }
   void va_free(void* va, size_t bytes) override { (void)hipMemAddressFree(va, bytes); }
@@ -470,8 +476,9 @@ class HipBackend : public Backend {
                (unsigned long long)dd.cpu.handle);
     for (auto& pc : pieces) {
       const bool h2d = pc.sa.handle == dd.cpu.handle, d2h = pc.da.handle == dd.cpu.handle;
-      uint32_t mask = h2d ? dd.h2d : (d2h ? dd.d2h : peer_mask(dd, pc.da));
-      uint32_t e = (pc.engine && (pc.engine & mask)) ? pc.engine : pick_engine(mask, channel);
+      const uint32_t mask = h2d ? dd.h2d : (d2h ? dd.d2h : peer_mask(dd, pc.da));
+      const uint32_t fast = h2d ? dd.h2d_fast : (d2h ? dd.d2h_fast : mask);
+      uint32_t e = (pc.engine && (pc.engine & mask)) ? pc.engine : pick_engine(fast ? fast : mask, dma_channel(channel));
       hsa_amd_sdma_engine_id_t eng = (hsa_amd_sdma_engine_id_t)e;
       __atomic_fetch_add(&dd.eng_bytes[__builtin_ctz(e)], (uint64_t)pc.len, __ATOMIC_RELAXED);
       hsa_status_t st = hsa_amd_memory_async_copy_on_engine(pc.dst, pc.da, pc.src, pc.sa, pc.len, 0, nullptr, sig,
@@ -479,12 +486,12 @@ class HipBackend : public Backend {
       if (st != HSA_STATUS_SUCCESS) {
         // Copies already issued still decrement the signal: drain them first.
         hsa_signal_subtract_relaxed(sig, (hsa_signal_value_t)(&pieces.back() - &pc + 1));
-        hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+        dma_wait(sig);
         last_err_ = "hsa_amd_memory_async_copy_on_engine failed";
         return Status::IO_ERROR;
       }
     }
-    hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+    dma_wait(sig);
     dma_launches_ += pieces.size();
     return Status::OK;
   }
@@ -720,7 +727,8 @@ class HipBackend : public Backend {
   struct DmaDev {
     bool ok = false;
     hsa_agent_t gpu{0}, cpu{0};
-    uint32_t h2d = 0, d2h = 0;
+    uint32_t h2d = 0, d2h = 0;        // engines able to copy host <-> this GPU
+    uint32_t h2d_fast = 0, d2h_fast = 0;  // of those, the full-rate PCIe ones (preferred mask / config)
     uint32_t peer[kMaxGpus] = {};     // engines copying this GPU -> GPU e (hsa_amd_memory_copy_engine_status(e, this))
     uint64_t eng_bytes[32] = {};      // bytes per SDMA engine (atomic adds)
   };
@@ -787,6 +795,21 @@ class HipBackend : public Backend {
             if (hsa_amd_memory_copy_engine_status(dd.gpu, cpu, &m) == HSA_STATUS_SUCCESS) dd.h2d = m;
             if (hsa_amd_memory_copy_engine_status(cpu, dd.gpu, &m) == HSA_STATUS_SUCCESS) dd.d2h = m;
             dd.ok = config().copy_engine == 3 && cpu.handle && dd.h2d && dd.d2h;
+            // Not every engine runs PCIe copies at link rate: on MI355X engines
+            // 0-3 move 56-57 GB/s each way to either socket's memory, engines
+            // 4-15 (the xGMI ones) only 12.8 / 10 / 7 GB/s GPU->host
+            // (profiles/r3_cxl_paths.md; ROCr's preferred masks, h2d 0x1 and d2h
+            // 0x6 on the box, are subsets). Host / CXL rings use ROCr's preferred
+            // engines plus 0-3, so H2D, D2H and CXL each get their own
+            // full-rate engine; config sdma_pcie_mask overrides.
+            uint32_t ph = 0, pd = 0;
+            (void)hsa_amd_memory_get_preferred_copy_engine(dd.gpu, cpu, &ph);
+            (void)hsa_amd_memory_get_preferred_copy_engine(cpu, dd.gpu, &pd);
+            const uint32_t o = (uint32_t)config().sdma_pcie_mask;
+            dd.h2d_fast = (o ? o : (ph | 0xFu)) & dd.h2d;
+            dd.d2h_fast = (o ? o : (pd | 0xFu)) & dd.d2h;
+            RT_INFO("GPU %d SDMA engines: h2d %#x (fast %#x) d2h %#x (fast %#x)", d, dd.h2d, dd.h2d_fast, dd.d2h,
+                    dd.d2h_fast);
           }
       }
       // Per GPU pair (xGMI peers): the engines of the source that reach the
@@ -810,6 +833,32 @@ class HipBackend : public Backend {
     dma_init();
     for (int i = 0; i < 32; ++i)
       out[i] = dev >= 0 && dev < (int)dma_.size() ? __atomic_load_n(&dma_[dev].eng_bytes[i], __ATOMIC_RELAXED) : 0;
+  }
+  // Completion wait of a worker's SDMA batch: spin (HSA_WAIT_STATE_ACTIVE) for
+  // at most config dma_spin_us - a small batch lands within it - then sleep in
+  // the kernel (BLOCKED, interrupt signal) so a long batch does not burn a host
+  // core per active ring (8 ranks x 4 DMA rings would compete with the codec
+  // and fault-service threads).
+  static void dma_wait(hsa_signal_t sig) {
+    static const uint64_t freq = [] {
+      uint64_t f = 0;
+      if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) != HSA_STATUS_SUCCESS || !f) f = 100000000ull;
+      return f;
+    }();
+    const uint64_t spin = (uint64_t)std::max<int64_t>(0, config().dma_spin_us) * freq / 1000000ull;
+    if (spin && hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, spin, HSA_WAIT_STATE_ACTIVE) == 0) return;
+    while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) != 0) {
+    }
+  }
+  // Ring kind -> engine slot: H2D, D2H and CXL rings get distinct engines of the
+  // fast set (peer copies pick from the pair's own mask).
+  static int dma_channel(int kind) {
+    switch ((RingKind)kind) {
+      case RingKind::CPU_TO_GPU: return 0;
+      case RingKind::GPU_TO_CPU: return 1;
+      case RingKind::CXL: return 2;
+      default: return 3;
+    }
   }
   // The ring kinds get distinct engines so H2D, D2H, CXL and peer traffic never
   // queue behind each other: channel k -> the k-th available engine of the mask.

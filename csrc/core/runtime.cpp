@@ -218,6 +218,40 @@ Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string&
   return Status::OK;
 }
 
+Status Runtime::malloc_managed_at(uint64_t size, uint32_t flags, const std::string& name, uint64_t id,
+                                  uint64_t cpu_addr, uint64_t dev_va, int stable_dev, Range** out) {
+  if (global_status() != Status::OK) return global_status();
+  if (size == 0 || id == 0) return Status::INVALID_ARGUMENT;
+  if (!cpu_addr) flags |= RANGE_NO_CPU_VIEW;
+  if (!dev_va) flags &= ~RANGE_STABLE_VA;
+  std::unique_lock<OrderedRWLock> vg(vs_.lock);
+  if (vs_.ranges.count(id)) return Status::BUSY;
+  auto r = std::make_unique<Range>(&vs_, id, RangeType::MANAGED, size, flags, name, cpu_addr);
+  if (cpu_addr && (uint64_t)r->cpu_view != cpu_addr) return Status::BUSY;  // the window is taken
+  if (flags & RANGE_STABLE_VA) {
+    if (!is_local(stable_dev)) return Status::INVALID_ARGUMENT;
+    vg.unlock();
+    ChunkArena* a = arena_for(Loc::gpu(stable_dev));
+    vg.lock();
+    if (!a || !static_cast<HbmArena*>(a)->vmm()) return Status::NOT_SUPPORTED;
+    void* va = nullptr;
+    Status st = be_->va_reserve(r->cpu_view_bytes, &va, (void*)dev_va);
+    if (st != Status::OK) return st;
+    r->dev_va = va;
+    r->stable_dev = stable_dev;
+    vs_.dev_tree[(uint64_t)va] = r.get();
+  }
+  if (vs_.ranges.count(id)) return Status::BUSY;  // raced with another restore while unlocked
+  if (r->cpu_view) {
+    vs_.tree[r->addr()] = r.get();
+    cpu_views_add(r->addr(), r->cpu_view_bytes);
+  }
+  vs_.next_range_id = std::max<uint64_t>(vs_.next_range_id, id + 1);
+  *out = r.get();
+  vs_.ranges[id] = std::move(r);
+  return Status::OK;
+}
+
 Status Runtime::map_external(uint64_t ptr, uint64_t size, int dev, const std::string& name, Range** out) {
   if (!ptr || !size || !is_local(dev)) return Status::INVALID_ARGUMENT;
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
@@ -1261,7 +1295,8 @@ Status Runtime::resume() {
 
 namespace {
 constexpr char kMagic[8] = {'O', 'G', 'K', 'M', 'R', 'M', 'A', 'P'};
-constexpr uint32_t kCkptVersion = 1;
+// v2 adds each range's CPU window address, stable device VA and its GPU (in-place restore).
+constexpr uint32_t kCkptVersion = 2;
 template <class T> void wr(std::ostream& o, const T& v) { o.write((const char*)&v, sizeof v); }
 template <class T> bool rd(std::istream& i, T* v) { return (bool)i.read((char*)v, sizeof *v); }
 }  // namespace
@@ -1309,6 +1344,9 @@ Status Runtime::checkpoint_save(const std::string& path, bool with_data) {
     uint8_t gm = r->group ? (uint8_t)r->group->migratable : 1;
     wr(o, gid);
     wr(o, gm);
+    wr(o, (uint64_t)(r->cpu_view ? r->addr() : 0));
+    wr(o, (uint64_t)r->dev_va);
+    wr(o, (int32_t)r->stable_dev);
     {
     std::shared_lock<OrderedRWLock> vg(vs_.lock);
     for (auto& bp : r->blocks) {
@@ -1352,7 +1390,8 @@ Status Runtime::checkpoint_save(const std::string& path, bool with_data) {
   return o ? Status::OK : Status::IO_ERROR;
 }
 
-Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::vector<uint64_t>* new_ids) {
+Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::vector<uint64_t>* new_ids,
+                                bool in_place) {
   std::ifstream in(path, std::ios::binary);
   if (!in) return Status::NOT_FOUND;
   char magic[8];
@@ -1361,7 +1400,8 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
   uint32_t ver = 0, flags = 0;
   rd(in, &ver);
   rd(in, &flags);
-  if (ver != kCkptVersion) return Status::NOT_SUPPORTED;
+  if (ver != 1 && ver != kCkptVersion) return Status::NOT_SUPPORTED;
+  if (in_place && ver < 2) return Status::NOT_SUPPORTED;  // v1 files carry no addresses
   bool has_data = flags & 1;
   uint64_t n = 0;
   rd(in, &n);
@@ -1377,8 +1417,16 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
     in.read(&name[0], nl);
     rd(in, &gid);
     rd(in, &gm);
+    uint64_t cpu_addr = 0, dev_va = 0;
+    int32_t sdev = -1;
+    if (ver >= 2) {
+      rd(in, &cpu_addr);
+      rd(in, &dev_va);
+      rd(in, &sdev);
+    }
     Range* r = nullptr;
-    Status st = malloc_managed(size, rflags & ~RANGE_STABLE_VA, name, &r, 0);
+    Status st = in_place ? malloc_managed_at(size, rflags, name, id, cpu_addr, dev_va, sdev, &r)
+                         : malloc_managed(size, rflags & ~RANGE_STABLE_VA, name, &r, 0);
     if (st != Status::OK) return st;
     if (new_ids) new_ids->push_back(r->id);
     struct BlockRec {

@@ -68,11 +68,16 @@ LocMask Block::resident_locs(const PageMask& pages) const {
   return m;
 }
 
-Range::Range(VaSpace* v, uint64_t i, RangeType t, uint64_t sz, uint32_t fl, std::string nm)
+Range::Range(VaSpace* v, uint64_t i, RangeType t, uint64_t sz, uint32_t fl, std::string nm, uint64_t want_view)
     : vs(v), id(i), type(t), size(sz), flags(fl), name(std::move(nm)) {
   nblocks = (sz + kBlockSize - 1) >> kBlockShift;
   cpu_view_bytes = nblocks << kBlockShift;
-  if (t == RangeType::MANAGED && !(fl & RANGE_NO_CPU_VIEW)) {
+  if (t == RangeType::MANAGED && !(fl & RANGE_NO_CPU_VIEW) && want_view) {
+    void* m = mmap((void*)want_view, cpu_view_bytes, PROT_NONE,
+                   MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | MAP_FIXED_NOREPLACE, -1, 0);
+    if (m == (void*)want_view) cpu_view = (uint8_t*)m;
+    else if (m != MAP_FAILED) munmap(m, cpu_view_bytes);
+  } else if (t == RangeType::MANAGED && !(fl & RANGE_NO_CPU_VIEW)) {
     // Reserve a 2 MB-aligned CPU window (PROT_NONE until blocks become
     // CPU-resident): over-reserve and trim.
     uint64_t want = cpu_view_bytes + kBlockSize;

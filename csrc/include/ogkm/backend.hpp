@@ -67,7 +67,8 @@ class Backend {
   virtual bool vmm_supported(int dev) = 0;
   virtual Status vmm_create(int dev, size_t bytes, uint64_t* handle) = 0;
   virtual void vmm_release(uint64_t handle) = 0;
-  virtual Status va_reserve(size_t bytes, void** va) = 0;
+  // `want` != null: reserve exactly there (in-place checkpoint restore) or fail with BUSY.
+  virtual Status va_reserve(size_t bytes, void** va, void* want = nullptr) = 0;
   virtual void va_free(void* va, size_t bytes) = 0;
   virtual Status vmm_map(void* va, size_t bytes, uint64_t handle, int dev) = 0;
   virtual Status vmm_unmap(void* va, size_t bytes) = 0;

@@ -64,6 +64,8 @@ namespace ogkm {
   /* channels / ring */                                                                              \
   X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \
   X(copy_engine, 3, "PCIe/xGMI ring copies: 3=SDMA engines driven by the ring's worker (default) 1=hipMemcpyAsync 0=our CU copy kernels") \
+  X(sdma_pcie_mask, 0, "SDMA engines used for host/CXL <-> HBM copies (bitmask; 0 = ROCr's preferred set, else engines 0-3)") \
+  X(dma_spin_us, 20, "SDMA worker: spin this long on a batch's completion signal, then block")             \
   X(peer_copy_engine, 3, "GPU->GPU ring copies: 3=SDMA split over the pair's xGMI engines 0=k_peer_push CU kernel") \
   X(peer_split_min_mb, 8, "GPU->GPU copies >= 2x this are split into pieces over the pair's SDMA engines") \
   X(peer_push_wgs, 64, "workgroups (CU budget) of one k_peer_push launch")                             \

@@ -160,6 +160,11 @@ class Runtime {
 
   // ---- allocation / ranges (UvmMemMap + mmap analog)
   Status malloc_managed(uint64_t size, uint32_t flags, const std::string& name, Range** out, int stable_dev = 0);
+  // In-place re-creation (checkpoint restore): range id `id`, CPU window at
+  // `cpu_addr`, stable device VA at `dev_va` (each 0 = none). BUSY when the id
+  // or an address is taken - the caller may fall back to a relocating restore.
+  Status malloc_managed_at(uint64_t size, uint32_t flags, const std::string& name, uint64_t id, uint64_t cpu_addr,
+                           uint64_t dev_va, int stable_dev, Range** out);
   Status map_external(uint64_t ptr, uint64_t size, int dev, const std::string& name, Range** out);
   Status alloc_device_p2p(uint64_t size, int dev, const std::string& name, Range** out);
   Status free_range(Range* r);
@@ -218,7 +223,11 @@ class Runtime {
   Status quiesce();
   Status resume();
   Status checkpoint_save(const std::string& path, bool with_data);
-  Status checkpoint_load(const std::string& path, bool with_data, std::vector<uint64_t>* new_range_ids);
+  // in_place: ranges come back under their recorded ids and VAs (CPU window and
+  // stable device VA) - pointers taken before the save stay valid (FBSR restores
+  // VRAM in place, fbsr.c:37-104; suspend/resume keeps VA spaces, uvm_global.c:272-415).
+  Status checkpoint_load(const std::string& path, bool with_data, std::vector<uint64_t>* new_range_ids,
+                         bool in_place = false);
 
   // ---- user channels (uvm_user_channel.c / the channel+TSG attribution of
   // uvm_gpu_replayable_faults.c): a stream registered as a channel gets the

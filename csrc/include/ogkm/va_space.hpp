@@ -141,7 +141,9 @@ enum RangeFlags : uint32_t {
 
 class Range {
  public:
-  Range(VaSpace* vs, uint64_t id, RangeType t, uint64_t size, uint32_t flags, std::string name);
+  // want_view != 0: the CPU window must sit exactly there (in-place restore); cpu_view stays null otherwise.
+  Range(VaSpace* vs, uint64_t id, RangeType t, uint64_t size, uint32_t flags, std::string name,
+        uint64_t want_view = 0);
   ~Range();
   VaSpace* vs;
   uint64_t id;

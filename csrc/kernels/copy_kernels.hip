@@ -12,11 +12,13 @@
 //    (vs one CE LAUNCH_DMA per contiguous run in the reference,
 //    uvm_va_block.c:4278-4326). Each wave keeps 4 dwordx4 loads in flight
 //    before storing (HBM/PCIe latency hiding without LDS).
-//  * PCIe-bound ring copies default to hipMemcpyAsync (config copy_engine=1):
-//    this kernel reading host memory slows concurrent HBM-bound kernels 3-7x
-//    (2.5x less with plain instead of non-temporal loads, copy_nt_loads=0;
-//    measured, profiles/r1_copy_engine_interference.md). These kernels serve HBM<->HBM
-//    copies, page gather/scatter, the fused copy+decode path and copy_engine=0.
+//  * PCIe-bound ring copies default to the SDMA engines (config copy_engine=3,
+//    driven from the ring's worker thread, backend_hip.cpp): this kernel reading
+//    host memory slows concurrent HBM-bound kernels 3-7x (2.5x less with plain
+//    instead of non-temporal loads, copy_nt_loads=0; measured,
+//    profiles/r1_copy_engine_interference.md), SDMA 1.06x. These kernels serve
+//    HBM<->HBM copies, page gather/scatter, the fused copy+decode path,
+//    k_peer_push (GPU->GPU, peer_copy_engine=0) and copy_engine=0.
 //  * Small batches pass their descriptors by value in the kernarg segment
 //    (scalar loads, no extra upload); big batches read them from device memory.
 #include <hip/hip_runtime.h>

@@ -713,6 +713,83 @@ __global__ void __launch_bounds__(256, 2) k_dgemm_fused(DGemmFusedArgs a, uint32
   }
 }
 
+// k_dgemm_pipe: raw-weight split-K unit per wave (one row block = 4 row tiles x
+// one K split, f32 partials for k_dgemm_reduce - the k_dgemm<RAW> contract) with
+// the fused kernel's main loop: two register sets of U K steps, batch b+1's
+// loads issued before batch b's MFMAs (sched_barrier-pinned), and every load
+// unconditional (row-tile / M-row indices clamped to valid memory; clamped
+// lanes' outputs are never stored).
+template <int U>
+__global__ void __launch_bounds__(256, 2) k_dgemm_pipe(DGemmArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t unit = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= a.row_blocks * a.ksplit) return;  // wave-uniform exit (no barriers in this kernel)
+  const uint32_t rb = unit / a.ksplit, ks = unit - rb * a.ksplit;
+  const uint32_t k_lo = ks * a.klen;
+  const uint32_t k_hi = k_lo + a.klen < a.K ? k_lo + a.klen : a.K;
+  const uint32_t ntiles = a.N >> 4, kfr = a.K >> 5;
+  const uint16_t* w = reinterpret_cast<const uint16_t*>(a.w) + a.w_off;
+  const uint16_t* wb[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t t = rb * 4 + r;
+    wb[r] = w + (uint64_t)(t < ntiles ? t : ntiles - 1) * kfr * 512u + lane * 8u;
+  }
+  const uint32_t m_base = blockIdx.y * 64u;
+  const uint16_t* xr[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const uint32_t m = m_base + mt * 16 + (lane & 15u);
+    xr[mt] = a.x + (uint64_t)(m < a.M ? m : a.M - 1) * a.ldx + 8u * (lane >> 4);
+  }
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[r][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const uint32_t s0 = k_lo >> 5, nsteps = k_hi > k_lo ? (k_hi - k_lo) >> 5 : 0;
+  const uint32_t nbat = nsteps / U;
+  if (nbat) {
+    u32x4_t wA[U][4], xA[U][4], wB[U][4], xB[U][4];
+    dgf_load<U>(wA, xA, wb, xr, s0);
+    uint32_t b = 0;
+    for (; b + 2 < nbat; b += 2) {
+      dgf_load<U>(wB, xB, wb, xr, s0 + (b + 1) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      dgf_mfma<U>(acc, wA, xA);
+      __builtin_amdgcn_sched_barrier(0);
+      dgf_load<U>(wA, xA, wb, xr, s0 + (b + 2) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      dgf_mfma<U>(acc, wB, xB);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (b + 1 < nbat) {
+      dgf_load<U>(wB, xB, wb, xr, s0 + (b + 1) * U);
+      __builtin_amdgcn_sched_barrier(0);
+      dgf_mfma<U>(acc, wA, xA);
+      dgf_mfma<U>(acc, wB, xB);
+    } else {
+      dgf_mfma<U>(acc, wA, xA);
+    }
+  }
+  for (uint32_t st = nbat * U; st < nsteps; ++st) {
+    u32x4_t w1[1][4], x1[1][4];
+    dgf_load<1>(w1, x1, wb, xr, s0 + st);
+    dgf_mfma<1>(acc, w1, x1);
+  }
+  // D layout (16x16x32): col = lane & 15 -> m, row = 4 (lane >> 4) + reg -> n.
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (rb * 4 + r >= ntiles) continue;
+    const uint32_t n = (rb * 4 + r) * 16u + 4u * (lane >> 4);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const uint32_t m = m_base + mt * 16 + (lane & 15u);
+      if (m < a.M) *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[r][mt];
+    }
+  }
+}
+
 hipError_t launch_dgemm_fused(const DGemmFusedArgs& a, hipStream_t s) {
   const bool silu = a.epi == DGEMM_EPI_SILU_MUL;
   if (a.N % 16 || a.K % 32 || a.klw % 32 || !a.klw || !a.kgroups || !a.M || (silu && a.N % 64) ||
@@ -747,6 +824,8 @@ hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s) {
     case DGEMM_W_RAW:
       if (a.unroll == 4)
         hipLaunchKernelGGL((k_dgemm<MODE_RAW, 4>), grid, dim3(256), 0, s, a);
+      else if (a.unroll == 1)  // unroll 1 = the pipelined raw kernel (k_dgemm_pipe, U = 2)
+        hipLaunchKernelGGL((k_dgemm_pipe<2>), grid, dim3(256), 0, s, a);
       else
         hipLaunchKernelGGL((k_dgemm<MODE_RAW, 2>), grid, dim3(256), 0, s, a);
       break;

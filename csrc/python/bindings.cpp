@@ -824,11 +824,12 @@ PYBIND11_MODULE(_ogkm, m) {
     return d;
   }, py::arg("reset") = false);
   // Decode GEMM + fused epilogue in one call: out = epi(X . W^T) (ops/dgemm.py).
-  m.def("dgemm_plan", [](uint32_t N, uint32_t K, uint32_t target_units) {
+  // (ksplit, klen) exactly as lib.dgemm plans it (lds: the LDS kernel's 4 waves per K split).
+  m.def("dgemm_plan", [](uint32_t N, uint32_t K, uint32_t target_units, bool lds) {
     uint32_t ks, kl;
-    dgemm_plan(N, K, target_units, &ks, &kl);
+    dgemm_plan(N, K, lds ? std::max<uint32_t>(1, target_units / 4) : target_units, &ks, &kl);
     return py::make_tuple(ks, kl);
-  });
+  }, py::arg("N"), py::arg("K"), py::arg("target_units"), py::arg("lds") = false);
   m.def("dgemm", [](int dev, uint64_t stream, uint64_t w, uint64_t w_off, int mode, uint32_t chunk_shift,
                     uint64_t x, uint32_t ldx, uint32_t M, uint32_t N, uint32_t K, uint64_t part, uint64_t part_bytes,
                     uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo, uint32_t target_units, uint32_t unroll,
@@ -1099,16 +1100,16 @@ PYBIND11_MODULE(_ogkm, m) {
     py::gil_scoped_release nogil;
     check(rt()->checkpoint_save(path, with_data), "checkpoint_save");
   });
-  m.def("checkpoint_load", [](const std::string& path, bool with_data) {
+  m.def("checkpoint_load", [](const std::string& path, bool with_data, bool in_place) {
     std::vector<uint64_t> ids;
     Status s;
     {
       py::gil_scoped_release nogil;
-      s = rt()->checkpoint_load(path, with_data, &ids);
+      s = rt()->checkpoint_load(path, with_data, &ids, in_place);
     }
     check(s, "checkpoint_load");
     return ids;
-  });
+  }, py::arg("path"), py::arg("with_data") = true, py::arg("in_place") = false);
 
   // ---- peers / export
   m.def("enable_peer", [](int a, int b) { check(rt()->enable_peer(a, b), "enable_peer"); });

@@ -4,9 +4,10 @@ The reference has no user-visible residency checkpoint; its closest artifacts
 are UVM_TEST_VA_RESIDENCY_INFO (uvm_test_ioctl.h:626-674) and FB save/restore
 (FBSR, fbsr.c:37-104, ``FBSR_TYPE_FILE``). This format combines both:
 
-  header   "OGKMRMAP" | u32 version=1 | u32 flags (bit0 = data present) | u64 nranges
+  header   "OGKMRMAP" | u32 version=2 | u32 flags (bit0 = data present) | u64 nranges
   range    u64 id | u32 type | u32 flags | u64 size | u64 nblocks | u32 name_len | name
            | u64 group_id | u8 group_migratable
+           | (v2) u64 cpu_view_addr | u64 stable_dev_va | i32 stable_dev
   block*   u64 index | u32 npages | u8 read_dup | u8 has_preferred | u8 pref_tier | i16 pref_id
            | u64 accessed_by | u8 thrash_pinned | u32 nres
            | nres x (u8 tier | i16 id | 64 B resident page mask over the 512 4 KB pages)
@@ -29,10 +30,13 @@ def save(path: str | Path, with_data: bool = False) -> None:
     lib.checkpoint_save(str(path), with_data)
 
 
-def load(path: str | Path, with_data: bool = True) -> list[int]:
-    """Recreate the recorded ranges (new ids, returned in file order), their
-    policies, and - with data - their contents at the recorded locations."""
-    return list(lib.checkpoint_load(str(path), with_data))
+def load(path: str | Path, with_data: bool = True, in_place: bool = False) -> list[int]:
+    """Recreate the recorded ranges (ids returned in file order), their
+    policies, and - with data - their contents at the recorded locations.
+    ``in_place``: the ranges keep their recorded ids, CPU windows and stable
+    device VAs (a resumed process finds its pointers valid); fails with BUSY
+    if one is taken. Otherwise ranges get new ids and VAs."""
+    return list(lib.checkpoint_load(str(path), with_data, in_place))
 
 
 def describe(path: str | Path) -> dict:
@@ -57,6 +61,9 @@ def describe(path: str | Path) -> dict:
         name = b[pos:pos + nl].decode()
         pos += nl
         gid, gm = take("Q"), take("B")
+        addrs = {}
+        if version >= 2:
+            addrs = {"cpu_view": take("Q"), "dev_va": take("Q"), "stable_dev": take("i")}
         blocks = []
         for _ in range(nblocks):
             idx, npages, rd, hp, pt, pid, ab, pinned, nres = (take("Q"), take("I"), take("B"), take("B"), take("B"),
@@ -73,7 +80,7 @@ def describe(path: str | Path) -> dict:
         if flags & 1:
             pos += size
         out["ranges"].append({"id": rid, "type": rtype, "flags": rflags, "size": size, "name": name,
-                              "group": gid, "group_migratable": bool(gm), "blocks": blocks})
+                              "group": gid, "group_migratable": bool(gm), "blocks": blocks, **addrs})
     return out
 
 

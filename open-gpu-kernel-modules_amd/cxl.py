@@ -142,7 +142,8 @@ def p2p_caps(device: int = 0, sysfs: str = "/sys") -> dict:
 
 def measure_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 5, node: Optional[int] = None,
                       barrier=None) -> dict:
-    """HBM<->CXL GB/s through the CXL ring (HIP copy kernels). Records the measured
+    """HBM<->CXL GB/s through the CXL ring (its configured engine: SDMA by default,
+    one of the full-rate PCIe engines - tools/probe_cxl_paths.hip). Records the measured
     per-link bandwidth in the runtime's CXL info (replacing the fork's constant).
     ``barrier``: called before each timed direction, so that N processes (one per
     GPU) measure concurrently and the sum of their rates is the node aggregate."""

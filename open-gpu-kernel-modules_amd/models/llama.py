@@ -52,6 +52,14 @@ from ..ops.memory import managed_embedding
 from ..parallel import comm, tp as tpmod
 
 ALIGN = 4096
+# Resting / raw bytes of the lossless formats on random-init N(0, 0.02) weights,
+# measured (BENCH_r02 resting_bytes_ratio for rANS; codec tests for BF11 / BF12):
+# what a dry-run plan uses instead of packing a layer.
+DRY_PACK_RATIO = {"ans": 0.6642, "bf11": 0.70, "bf12": 0.75, "bf16": 1.0}
+# Planning rates (per GPU): PCIe host->HBM measured on the box (profiles/), HBM
+# read rate of the decode kernels (profiles/r2_dgemm_sweep.txt, 70B shapes).
+PLAN_PCIE_GBPS = 56.7
+PLAN_HBM_GBPS = 4000.0
 # Diagnostics: the host waits for every streamed unit's copies (instead of a
 # GPU-side stream dependency).
 _HOST_LEASE_WAIT = os.environ.get("OGKM_HOST_LEASE_WAIT", "0") != "0"
@@ -164,7 +172,21 @@ class TieredLlama:
                  hbm_budget: Optional[int] = None, init_std: float = 0.02, verbose: bool = False,
                  packed: bool = True, weight_format: str = "bf11", tiers: str = "host", cxl_frac: float = 0.5,
                  kv_format: str = "bf16", parallel: str = "tp", planner: str = "static",
-                 kv_tiering: bool = False):
+                 kv_tiering: bool = False, dry_run: bool = False, pack_ratio: Optional[float] = None,
+                 attach: Optional[dict] = None):
+        """``dry_run``: compute the residency plan only (budget, resident / streamed
+        units, per-step traffic: ``traffic()``) - no runtime, no allocation, no
+        weights generated; packed formats use ``pack_ratio`` (resting / raw bytes,
+        default the measured rANS / BF11 ratios) instead of packing layer 0. Used
+        by ``bench.py --plan-only`` for configurations larger than the box.
+        ``attach``: resume a saved model (``TieredLlama.restore``) - the managed
+        ranges already exist (restored in place from a residency checkpoint with
+        data); nothing is generated or written, the position is the saved one."""
+        self._ctor = dict(cfg=cfg.name, batch=batch, context=context, max_new_tokens=max_new_tokens, oversub=oversub,
+                          device=device, tp_rank=tp_rank, tp_world=tp_world, seed=seed, lookahead=lookahead,
+                          hbm_budget=hbm_budget, init_std=init_std, packed=packed, weight_format=weight_format,
+                          tiers=tiers, cxl_frac=cxl_frac, kv_format=kv_format, parallel=parallel, planner=planner,
+                          kv_tiering=kv_tiering)
         if parallel not in ("tp", "shards"):
             raise ValueError("parallel must be 'tp' or 'shards'")
         # planner "static": the plan below picks resident layers and pins them
@@ -193,7 +215,8 @@ class TieredLlama:
         self.T = context + max_new_tokens
         self.dev = device
         self.rank, self.world = tp_rank, tp_world
-        self.fake = lib.backend_name() == "fake"
+        self.dry_run = dry_run
+        self.fake = dry_run or lib.backend_name() == "fake"
         self.tdev = torch.device("cpu") if self.fake else torch.device("cuda", device)
         self.verbose = verbose
         self.layout = LayerLayout.build(cfg, tp_world)
@@ -262,15 +285,17 @@ class TieredLlama:
         if not self.fake:
             from .. import allocator as _alloc
             self.torch_in_arena = _alloc.enabled()
+        self.arena_init_bytes = self.budget if self.torch_in_arena else self.arena_bytes
         if self.torch_in_arena:
-            lib.init_device(device, self.budget)
             self.arena_bytes -= 256 << 20
-        else:
-            lib.init_device(device, self.arena_bytes)
+        if not dry_run and attach is None:  # (restore sizes the arena before loading the checkpoint)
+            lib.init_device(device, self.arena_init_bytes)
+        if pack_ratio is None:
+            pack_ratio = DRY_PACK_RATIO.get(weight_format, 1.0)
         self.pinfo: dict = {}
         self.pmode: dict = {}
         gpu = rt.Loc.gpu(device)
-        host = rt.Loc.host()
+        host = rt.Loc.host(0 if dry_run else None)
         t0 = time.perf_counter()
         self._seed, self._std = seed, init_std
         # ---- KV cache format. "bf16": raw [L, 2, B, hkv, T, hd]. "bf11": the
@@ -294,7 +319,14 @@ class TieredLlama:
         self.kv_scratch_bytes = self.kv_layer_bytes if self.kv_split else 0
         self.kv_streams, self.kv_infos, self.kv_slot = [], [], 0
         self.kv_prefix_bytes = 2 * batch * self.hkv * context * hd * 2  # raw bf16 prefix of one layer
-        if kv_format != "bf16":
+        if kv_format != "bf16" and attach is not None:
+            self.kv_infos = [bf12.PackedInfo(**d) for d in attach["kv_infos"]]
+            self.kv_slot = attach["kv_slot"]
+            self.kv_resident_bytes = cfg.n_layers * self.kv_slot + _al(self.kv_tail_bytes)
+        elif kv_format != "bf16" and dry_run:
+            self.kv_slot = _al(int(self.kv_prefix_bytes * DRY_PACK_RATIO.get(kv_format, 1.0)) + 65536)
+            self.kv_resident_bytes = cfg.n_layers * self.kv_slot + _al(self.kv_tail_bytes)
+        elif kv_format != "bf16":
             for i, full in enumerate(self._gen_prefill()):
                 st, inf = bf12.pack(full, chunk_values=cv, fmt=kv_format)
                 self.kv_streams.append(st)
@@ -319,7 +351,15 @@ class TieredLlama:
         part_raw = {n: math.prod(sh) * 2 for n, sh in self.layout.shapes.items()}
         self.head_rows = self._head_split(max(part_raw.values()))
         first_parts = None
-        if self.wpacked:
+        if self.wpacked and attach is not None:  # the saved plan's unit sizes
+            self.res_part = dict(attach["res_part"])
+            self.res_head_part = list(attach["res_head_part"])
+        elif self.wpacked and dry_run:
+            ratio = pack_ratio
+            self.res_part = {n: _al(int(part_raw[n] * ratio * 1.002) + 4096) for n in self.parts}
+            self.res_head_part = [_al(int((r1 - r0) * cfg.dim * 2 * ratio * 1.002) + 8192)
+                                  for r0, r1 in self.head_rows]
+        elif self.wpacked:
             # Layer 0's packed sizes size the plan (all layers share one distribution).
             first_parts = self._pack_parts(self._gen_layer(0))
             ratio = sum(inf.nbytes for _, inf in first_parts.values()) / sum(part_raw.values())
@@ -353,7 +393,7 @@ class TieredLlama:
         window_min = int(float(os.environ.get("OGKM_WINDOW_MB", "384")) * 2**20)
         lookahead_arg = lookahead
         lookahead = max(lookahead, min(-(-window_min // slot), max(0, self.arena_bytes - fixed) // (4 * slot)))
-        runahead = int(os.environ.get("OGKM_RUNAHEAD", "1"))
+        runahead = self.runahead = int(os.environ.get("OGKM_RUNAHEAD", "1"))
         staging = (lookahead + 1 + runahead) * slot
         if self.arena_bytes - fixed - staging < slot:  # tiny budgets: no room for the run-ahead slot
             staging = (lookahead + 1) * slot
@@ -404,12 +444,18 @@ class TieredLlama:
                       + [("head", j) for j in range(len(self.head_rows))])
         streamed_keys = [k for k in self.order if not self._is_resident(k)]
         self.rest_loc = {}
-        cxl_loc = rt.Loc.cxl() if tiers == "host+cxl" else None
+        cxl_loc = (rt.Loc("cxl", 0) if dry_run else rt.Loc.cxl()) if tiers == "host+cxl" else None
         for j, key in enumerate(streamed_keys):
             to_cxl = cxl_loc is not None and int((j + 1) * cxl_frac) > int(j * cxl_frac)
             self.rest_loc[key] = cxl_loc if to_cxl else host
         self.cxl_streamed_bytes = sum(self._unit_bytes(k) for k, l in self.rest_loc.items()
                                       if l is cxl_loc and cxl_loc is not None)
+        if dry_run:
+            self.init_seconds = 0.0
+            return
+        if attach is not None:
+            self._attach(attach)
+            return
         # ---- allocate + init
         self.embed = rt.malloc_managed(self.embed_bytes, "embed")
         self.embed.set_preferred_location(host)
@@ -453,14 +499,24 @@ class TieredLlama:
         self.embed.write(self._gen_embed())
         if not self.fake:
             torch.cuda.synchronize(self.dev)
-        self.stage = (torch.empty(self.stage_bytes // 2, dtype=torch.bfloat16, device=self.tdev)
-                      if self.staged else None)
         # RMSNorm weights of every layer + the final norm (after the KV cache)
         self.kv.write(torch.ones((2 * cfg.n_layers + 1) * cfg.dim, dtype=torch.bfloat16),
                       offset=self.kv_resident_bytes)
         for i, st in enumerate(self.kv_streams):  # (tiering: written to the KV units above)
             self.kv.write(st, offset=i * self.kv_slot)
         self.kv_streams = []
+        self._finish_init(fill_prefill=True)
+        self.init_seconds = time.perf_counter() - t0
+        if verbose:
+            self.describe()
+
+    def _finish_init(self, fill_prefill: bool, pos: Optional[int] = None) -> None:
+        """Views, leases and the streaming state over the managed ranges (shared
+        by a fresh model and one attached to restored ranges)."""
+        cfg, batch, context, device = self.cfg, self.B, self.ctx, self.dev
+        hd = cfg.head_dim
+        self.stage = (torch.empty(self.stage_bytes // 2, dtype=torch.bfloat16, device=self.tdev)
+                      if self.staged else None)
         self.cos, self.sin = D.rope_tables(hd, self.T, cfg.rope_theta, self.tdev)
         # KV cache: leased for the model's lifetime (hot, written every step)
         self.kv_lease = self.kv.acquire(device, rt.WRITE)
@@ -471,9 +527,10 @@ class TieredLlama:
         self.final_norm = self.norm_w[2 * cfg.n_layers]
         if not self.kv_split:
             kv = self.kv_lease.tensor((cfg.n_layers, 2, batch, self.hkv, self.T, hd), torch.bfloat16)
-            for i, full in enumerate(self._gen_prefill()):
-                kv[i, :, :, :, :context].copy_(full)
-                del full
+            if fill_prefill:
+                for i, full in enumerate(self._gen_prefill()):
+                    kv[i, :, :, :, :context].copy_(full)
+                    del full
             self.kv_t = kv
         else:
             self.kv_t = None
@@ -482,7 +539,7 @@ class TieredLlama:
                                                  (cfg.n_layers, 2, batch, self.hkv, max(self.tail, 1), hd),
                                                  torch.bfloat16, tdev, device)
             self.kv_scratch = torch.empty(2, batch, self.hkv, self.T, hd, dtype=torch.bfloat16, device=self.tdev)
-        self.pos = context
+        self.pos = context if pos is None else pos
         # ---- streaming schedule: use order within a step
         self.stream_seq = [k for k in self.order if not self._is_resident(k)]
         self._pf_next = 0           # next index in stream_seq to prefetch (cyclic)
@@ -494,7 +551,7 @@ class TieredLlama:
         # behind compute and the link idles. The host waits for the unit
         # ``max_ahead`` streamed units back instead (OGKM_MAX_AHEAD).
         self._ahead = collections.deque()
-        self.max_ahead = int(os.environ.get("OGKM_MAX_AHEAD", "0")) or (self.lookahead + runahead)
+        self.max_ahead = int(os.environ.get("OGKM_MAX_AHEAD", "0")) or (self.lookahead + self.runahead)
         self._views: dict = {}
         self.byte_trace = None     # diagnostics: {key: H2D bytes submitted around its use}
         self.use_trace = None      # diagnostics: [(key, acquire s, wait s)] per streamed use
@@ -509,9 +566,60 @@ class TieredLlama:
             self.gather = UnitGather([k for k in self.order if k[0] != "kv"], self._buf, self._unit_bytes, self.sworld, self.gather_depth,
                                      device=self.tdev, dev_index=device)
         self._settle()
-        self.init_seconds = time.perf_counter() - t0
-        if verbose:
-            self.describe()
+
+    # ------------------------------------------------------------------ save / resume
+    def save(self, path: str) -> dict:
+        """Checkpoint the model mid-decode: the runtime's residency map WITH data
+        (every managed range - weights in their resting format, KV cache, norms -
+        with its residency, policies, id and VAs; the rings are quiesced first,
+        the uvm_suspend analog) plus a JSON sidecar: construction arguments,
+        decode position and the unit -> range-id table. ``restore`` resumes it in
+        a fresh process in place (same ids and VAs)."""
+        import dataclasses
+        import json
+        from .. import checkpoint
+        if not self.fake:
+            torch.cuda.synchronize(self.dev)
+        checkpoint.save(path + ".rmap", with_data=True)
+        side = {"ctor": self._ctor, "pos": self.pos, "embed": self.embed.id, "kv": self.kv.id,
+                "units": [[list(k), b.id] for k, b in self.ubuf.items()],
+                "pinfo": [[list(k), dataclasses.asdict(v)] for k, v in self.pinfo.items()],
+                "pmode": [[list(k), v] for k, v in self.pmode.items()],
+                "res_part": self.res_part, "res_head_part": self.res_head_part,
+                "kv_infos": [dataclasses.asdict(i) for i in getattr(self, "kv_infos", [])],
+                "kv_slot": getattr(self, "kv_slot", 0)}
+        with open(path, "w") as f:
+            json.dump(side, f)
+        return side
+
+    @staticmethod
+    def restore(path: str, verbose: bool = False) -> "TieredLlama":
+        """Resume a model saved by ``save`` in this (fresh) process: the ranges
+        come back under their recorded ids and VAs with their data
+        (checkpoint.load in place), then the model attaches to them - nothing is
+        regenerated; the next step continues at the saved position."""
+        import json
+        from .. import checkpoint
+        with open(path) as f:
+            side = json.load(f)
+        kw = dict(side["ctor"])
+        cfg = CONFIGS[kw.pop("cfg")]
+        # the saved plan's HBM arena first, so the data lands where it was
+        plan = TieredLlama(cfg, dry_run=True, pack_ratio=1.0, attach=None, **kw)
+        lib.init_device(kw["device"], plan.arena_init_bytes)
+        checkpoint.load(path + ".rmap", with_data=True, in_place=True)
+        return TieredLlama(cfg, verbose=verbose, attach=side, **kw)
+
+    def _attach(self, side: dict) -> None:
+        tup = lambda k: tuple(k)  # noqa: E731 - JSON lists back to unit keys
+        self.embed = rt.ManagedBuffer(side["embed"])
+        self.kv = rt.ManagedBuffer(side["kv"])
+        self.ubuf = {tup(k): rt.ManagedBuffer(i) for k, i in side["units"]}
+        self.pinfo = {tup(k): bf12.PackedInfo(**v) for k, v in side["pinfo"]}
+        self.pmode = {tup(k): v for k, v in side["pmode"]}
+        self.kv_streams = []
+        self._finish_init(fill_prefill=False, pos=side["pos"])
+        self.init_seconds = 0.0
 
     def _settle(self) -> None:
         """Bring the residency to its steady state before the first step: the
@@ -533,8 +641,9 @@ class TieredLlama:
             # where every later step finds it - what a serving engine's start-up
             # warm-up does. Step 0 of a run then costs what step 1 does.
             tok = torch.zeros(self.B, dtype=torch.int64, device=self.tdev)
+            pos = self.pos
             self.step(tok)
-            self.reset(self.ctx)
+            self.reset(pos)
         if not self.fake:
             torch.cuda.synchronize(self.dev)
 
@@ -581,6 +690,50 @@ class TieredLlama:
         if self.verbose and self.rank == 0:
             print("[ogkm] plan:", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items()}, flush=True)
         return d
+
+    def traffic(self) -> dict:
+        """Per-rank, per-step traffic this plan implies, and the time it predicts.
+          pcie_gb:  streamed units (host / CXL -> HBM over this GPU's PCIe link)
+          xgmi_gb:  bytes this rank receives over the links - tp: 2 ring
+                    all-reduces of the [B, dim] bf16 activations per layer
+                    (2 (W-1)/W each) + the vocab-argmax gather; shards: every
+                    unit all-gathered each step, (W-1) shards of it
+          hbm_gb:   weight + KV bytes the kernels read from HBM (staged formats:
+                    packed read + bf16 write + bf16 read)
+        predicted_ms = max(PCIe, HBM) time + the tp collectives' latency-bound
+        time (on the critical path), or max(PCIe, HBM, all-gather) for shards
+        (gathers run ahead on a side stream)."""
+        from ..parallel import topology
+        cfg, W = self.cfg, max(self.world, self.sworld)
+        n_units = len(self.order)
+        pcie = self.streamed_bytes
+        if self.sworld > 1:
+            shard = sum(self._unit_bytes(k) for k in self.order if k[0] != "kv")
+            xgmi = (self.sworld - 1) * shard
+            full = {k: self._unit_bytes(k) * self.sworld for k in self.order if k[0] != "kv"}
+            topo = topology.PeerTopology(self.sworld)
+            xgmi_s = sum(topo.allgather_seconds(b, self.sworld, "direct") for b in full.values())
+            n_coll = len(full)
+        elif self.world > 1:
+            act = self.B * cfg.dim * 2
+            n_coll = 2 * cfg.n_layers + 1
+            xgmi = 2 * cfg.n_layers * 2 * (self.world - 1) / self.world * act + (self.world - 1) * self.B * 2 * 4
+            lat = topology.COLLECTIVE_LATENCY_US * 1e-6
+            xgmi_s = n_coll * lat + xgmi / (topology.XGMI_LINK_GBPS * 1e9)
+        else:
+            xgmi, xgmi_s, n_coll = 0, 0.0, 0
+        resting = self.res_layer_bytes * cfg.n_layers + self.res_head_bytes
+        raw = self.layer_bytes * cfg.n_layers + self.head_bytes
+        if self.sworld > 1:  # every rank runs the whole model on gathered units
+            resting, raw = resting * self.sworld, raw
+        weights_hbm = resting + 2 * raw if self.staged else (resting if self.wpacked else raw)
+        kv_read = self.kv_bytes * (self.ctx + 1) / self.T
+        hbm = weights_hbm + kv_read
+        pcie_s, hbm_s = pcie / (PLAN_PCIE_GBPS * 1e9), hbm / (PLAN_HBM_GBPS * 1e9)
+        pred = max(pcie_s, hbm_s, xgmi_s) if self.sworld > 1 else max(pcie_s, hbm_s) + xgmi_s
+        return {"pcie_gb": pcie / 1e9, "xgmi_gb": xgmi / 1e9, "hbm_gb": hbm / 1e9, "collectives": n_coll,
+                "pcie_ms": pcie_s * 1e3, "xgmi_ms": xgmi_s * 1e3, "hbm_ms": hbm_s * 1e3,
+                "predicted_ms": pred * 1e3, "units": n_units, "world": W}
 
     def _is_resident(self, key) -> bool:
         if key[0] == "layer":

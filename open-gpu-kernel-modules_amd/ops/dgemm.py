@@ -38,8 +38,12 @@ LDS_MAX_N = 8192
 UNROLL = int(os.environ.get("OGKM_DGEMM_UNROLL", "0"))  # K steps per pipelined block (0 = kernel default)
 # Raw weights: the fused kernel (k_dgemm_fused: split-K reduce + epilogue inside
 # the launch, two-deep register pipeline) replaces k_dgemm[_lds] + k_dgemm_reduce.
-FUSED = int(os.environ.get("OGKM_DGEMM_FUSED", "1"))
+FUSED = int(os.environ.get("OGKM_DGEMM_FUSED", "0"))
 FUSED_WGS = int(os.environ.get("OGKM_DGEMM_WGS", "512"))  # workgroups per GEMM (2 per CU)
+# Raw weights on the split-K path: k_dgemm_pipe (two-deep register pipeline,
+# unconditional loads) instead of k_dgemm<RAW>; its own split target (waves per GEMM).
+PIPE = int(os.environ.get("OGKM_DGEMM_PIPE", "1"))
+TARGET_UNITS_PIPE = int(os.environ.get("OGKM_DGEMM_UNITS_PIPE", "1024"))
 
 
 def frag_permute(w: torch.Tensor) -> torch.Tensor:
@@ -158,14 +162,18 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     if lds < 0:
         lds = int(w.mode == MODE_RAW and w.n <= LDS_MAX_N)
     units = TARGET_UNITS if w.mode == MODE_RAW else TARGET_UNITS_PACKED
+    unroll = UNROLL
     if lds and w.mode == MODE_RAW:
         units *= 2  # waves; the kernel runs 4 per K split
-    ks = _PLANS.get((w.n, w.k, units))
-    if ks is None:
-        ks = _PLANS[(w.n, w.k, units)] = lib.dgemm_plan(w.n, w.k, units)[0]
+    elif w.mode == MODE_RAW and PIPE and not UNROLL:
+        units, unroll = TARGET_UNITS_PIPE, 1  # unroll 1 selects k_dgemm_pipe
+    raw_lds = bool(lds) and w.mode == MODE_RAW
+    ks = _PLANS.get((w.n, w.k, units, raw_lds))
+    if ks is None:  # the binding plans the launch with the same function: one source of truth
+        ks = _PLANS[(w.n, w.k, units, raw_lds)] = lib.dgemm_plan(w.n, w.k, units, raw_lds)[0]
     ksplit = ks
     part = _WS.get(x.device, ksplit * m * w.n * 4)
     lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), x.stride(0), m, w.n, w.k,
               part.data_ptr(), part.numel() * 4, EPI[epi], resid.data_ptr() if resid is not None else 0,
-              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, UNROLL, lds)
+              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, unroll, lds)
     return out

@@ -65,6 +65,21 @@ class DistEnv:
 
 _ENV: Optional[DistEnv] = None
 
+# Bytes this rank receives over the links per collective kind (the xGMI traffic
+# a plan predicts): a ring all-reduce of n bytes moves 2 (W-1)/W n in and out
+# of every rank; an all-gather receives the other W-1 shards.
+STATS = {"allreduce_bytes_in": 0, "allgather_bytes_in": 0, "collectives": 0}
+
+
+def reset_stats() -> None:
+    for k in STATS:
+        STATS[k] = 0
+
+
+def _count(kind: str, nbytes: float) -> None:
+    STATS[kind] += int(nbytes)
+    STATS["collectives"] += 1
+
 
 def init(backend: Optional[str] = None, timeout_s: int = 600) -> DistEnv:
     """Initialise from torchrun-style env vars (RANK / WORLD_SIZE / LOCAL_RANK /
@@ -122,8 +137,10 @@ def barrier() -> None:
 
 @_fatal_on_error
 def all_reduce_(t: torch.Tensor) -> torch.Tensor:
-    if env().is_dist:
+    e = env()
+    if e.is_dist:
         dist.all_reduce(t)
+        _count("allreduce_bytes_in", 2 * (e.world - 1) / e.world * t.numel() * t.element_size())
     return t
 
 
@@ -134,6 +151,7 @@ def all_gather_cat(t: torch.Tensor, dim: int = 0) -> torch.Tensor:
         return t
     out = [torch.empty_like(t) for _ in range(e.world)]
     dist.all_gather(out, t.contiguous())
+    _count("allgather_bytes_in", (e.world - 1) * t.numel() * t.element_size())
     return torch.cat(out, dim=dim)
 
 
@@ -144,20 +162,12 @@ def all_gather_into(out: torch.Tensor, shard: torch.Tensor) -> torch.Tensor:
     e = env()
     if not e.is_dist:
         out[:shard.numel()].copy_(shard.reshape(-1))
-    elif e.backend == "nccl":
-        dist.all_gather_into_tensor(out, shard)
-    else:
-        dist.all_gather(list(out.chunk(e.world)), shard.clone())
-    return out
-
-
-@_fatal_on_error
-def reduce_scatter_(out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
-    e = env()
-    if not e.is_dist:
-        out.copy_(inp)
         return out
-    dist.reduce_scatter_tensor(out, inp.contiguous())
+    if e.backend == "nccl":
+        dist.all_gather_into_tensor(out, shard)
+    else:  # gloo: list form; chunks of the flat output are 1-D, so is the shard
+        dist.all_gather(list(out.reshape(-1).chunk(e.world)), shard.reshape(-1).clone())
+    _count("allgather_bytes_in", (e.world - 1) * shard.numel() * shard.element_size())
     return out
 
 
@@ -182,34 +192,3 @@ def max_over_ranks(x: float) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
-
-
-class Bucketer:
-    """Coalesce many small tensors into ~bucket_bytes flat buffers for one
-    collective each (DP gradient / shard all-gather style traffic over xGMI)."""
-
-    def __init__(self, bucket_bytes: int = 64 << 20):
-        self.bucket_bytes = bucket_bytes
-
-    @_fatal_on_error
-    def all_reduce(self, tensors: list[torch.Tensor]) -> None:
-        if not env().is_dist or not tensors:
-            return
-        bucket: list[torch.Tensor] = []
-        size = 0
-        for t in tensors + [None]:
-            if t is not None and (not bucket or (size + t.numel() * t.element_size() <= self.bucket_bytes
-                                                 and t.dtype == bucket[0].dtype)):
-                bucket.append(t)
-                size += t.numel() * t.element_size()
-                continue
-            if bucket:
-                flat = torch.cat([b.reshape(-1) for b in bucket])
-                dist.all_reduce(flat)
-                off = 0
-                for b in bucket:
-                    n = b.numel()
-                    b.copy_(flat[off:off + n].view_as(b))
-                    off += n
-            bucket = [t] if t is not None else []
-            size = t.numel() * t.element_size() if t is not None else 0

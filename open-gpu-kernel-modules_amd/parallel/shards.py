@@ -32,168 +32,6 @@ from .. import rt
 from . import comm
 
 
-@dataclass
-class LayerSpec:
-    """Names and shapes of one layer's tensors (flattened in this order)."""
-
-    names: list
-    shapes: list
-
-    @property
-    def numel(self) -> int:
-        return sum(math.prod(s) for s in self.shapes)
-
-
-class ShardedWeights:
-    """Owns this rank's shard of every layer, in one managed buffer per layer."""
-
-    def __init__(self, specs: Sequence[LayerSpec], dtype: torch.dtype = torch.bfloat16, device: int = 0,
-                 rank: Optional[int] = None, world: Optional[int] = None, name: str = "shards"):
-        e = comm.env()
-        self.rank = e.rank if rank is None else rank
-        self.world = e.world if world is None else world
-        self.specs = list(specs)
-        self.dtype = dtype
-        self.device = device
-        self.esz = torch.empty((), dtype=dtype).element_size()
-        # Pad every layer to a multiple of world so all shards have one size.
-        self.shard_numel = [-(-s.numel // self.world) for s in self.specs]
-        self.bufs: list[rt.ManagedBuffer] = []
-        for i, n in enumerate(self.shard_numel):
-            b = rt.malloc_managed(max(n * self.esz, 4096), f"{name}.l{i}.r{self.rank}", cpu_view=False)
-            b.set_preferred_location(rt.Loc.gpu(device))
-            self.bufs.append(b)
-
-    def load_layer(self, i: int, full: torch.Tensor) -> None:
-        """Write this rank's slice of the flattened full layer ``full``."""
-        flat = full.reshape(-1).to(self.dtype)
-        n = self.shard_numel[i]
-        lo = self.rank * n
-        part = flat[lo:lo + n]
-        if part.numel() < n:
-            part = torch.cat([part, torch.zeros(n - part.numel(), dtype=self.dtype, device=part.device)])
-        self.bufs[i].write(part.contiguous())
-
-    def load_named(self, i: int, tensors: dict) -> None:
-        spec = self.specs[i]
-        self.load_layer(i, torch.cat([tensors[nm].reshape(-1).to(self.dtype).cpu() for nm in spec.names]))
-
-    @property
-    def max_full_numel(self) -> int:
-        return max(n * self.world for n in self.shard_numel)
-
-    def shard_bytes(self) -> int:
-        return sum(self.shard_numel) * self.esz
-
-    def free(self) -> None:
-        for b in self.bufs:
-            b.free()
-        self.bufs = []
-
-
-class GatheredLayer:
-    """A layer's full weights, valid until the pipeline reuses its buffer."""
-
-    def __init__(self, spec: LayerSpec, flat: torch.Tensor):
-        self.flat = flat
-        self.tensors = {}
-        off = 0
-        for nm, shp in zip(spec.names, spec.shapes):
-            n = math.prod(shp)
-            self.tensors[nm] = flat[off:off + n].view(shp)
-            off += n
-
-    def __getitem__(self, name: str) -> torch.Tensor:
-        return self.tensors[name]
-
-
-class ShardGatherPipeline:
-    """Double (``depth``-) buffered layer all-gather with look-ahead.
-
-    ``get(k)`` returns layer k gathered; it waits for k's gather (issued earlier
-    by look-ahead when possible) and issues the gathers of k+1 .. k+depth-1."""
-
-    def __init__(self, shards: ShardedWeights, depth: int = 2, device: Optional[torch.device] = None):
-        self.s = shards
-        self.depth = max(1, depth)
-        e = comm.env()
-        self.dist = e.is_dist and (shards.world > 1 or e.forced)
-        self.cuda = device is not None and device.type == "cuda"
-        self.device = device or torch.device("cpu")
-        self.full = [torch.empty(shards.max_full_numel, dtype=shards.dtype, device=self.device)
-                     for _ in range(self.depth)]
-        self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
-        self.pending: dict[int, tuple] = {}  # layer -> (slot, work, lease, event)
-        self.slot_of: dict[int, int] = {}
-        self.next_slot = 0
-        self.stats = {"gathers": 0, "bytes": 0}
-
-    def _issue(self, k: int) -> None:
-        if k in self.pending or k >= len(self.s.specs):
-            return
-        slot = self.next_slot
-        self.next_slot = (self.next_slot + 1) % self.depth
-        # A slot is reused only after its previous layer was consumed.
-        for lk, (sl, *_rest) in list(self.pending.items()):
-            if sl == slot:
-                self._finish(lk)
-        n = self.s.shard_numel[k]
-        lease = self.s.bufs[k].acquire(self.s.device, rt.READ, 0, n * self.s.esz)
-        out = self.full[slot][:n * self.s.world]
-        if self.cuda:
-            ev = torch.cuda.Event()
-            ev.record()
-            with torch.cuda.stream(self.stream):
-                self.stream.wait_event(ev)
-                lease.wait(self.stream.cuda_stream)
-                shard = lease.tensor((n,), self.s.dtype)
-                work = self._gather(out, shard)
-                done = torch.cuda.Event()
-                done.record(self.stream)
-        else:
-            lease.wait(0)
-            shard = lease.tensor((n,), self.s.dtype)
-            work = self._gather(out, shard)
-            done = None
-        self.pending[k] = (slot, work, lease, done)
-        self.stats["gathers"] += 1
-        self.stats["bytes"] += n * self.s.esz * (self.s.world - 1)
-
-    def _gather(self, out: torch.Tensor, shard: torch.Tensor):
-        if not self.dist:
-            out.copy_(shard)
-            return None
-        if shard.device != out.device:
-            shard = shard.to(out.device)
-        if comm.env().backend == "nccl":
-            return dist.all_gather_into_tensor(out, shard, async_op=True)
-        return dist.all_gather(list(out.chunk(self.s.world)), shard, async_op=True)
-
-    def _finish(self, k: int) -> int:
-        slot, work, lease, done = self.pending.pop(k)
-        if work is not None:
-            work.wait()
-        if done is not None:
-            torch.cuda.current_stream(self.device).wait_event(done)
-            lease.release(self.stream.cuda_stream)
-        else:
-            lease.release(0)
-        self.slot_of[k] = slot
-        return slot
-
-    def get(self, k: int) -> GatheredLayer:
-        self._issue(k)
-        slot = self._finish(k)
-        for j in range(1, self.depth):
-            self._issue(k + j)
-        spec = self.s.specs[k]
-        return GatheredLayer(spec, self.full[slot][:spec.numel])
-
-    def drain(self) -> None:
-        for k in list(self.pending):
-            self._finish(k)
-
-
 class UnitGather:
     """Per-unit all-gather pipeline of the sharded model (TieredLlama
     ``parallel="shards"``, config 4).

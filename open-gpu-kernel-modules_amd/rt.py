@@ -71,7 +71,7 @@ class Loc:
             nodes = lib.cxl_info()["numa_nodes"]
             if not nodes:
                 raise RuntimeStatusError("no CXL memory node (set cxl_emulate_node to emulate one)")
-            n = nodes[0]
+            n = lib.cxl_nearest_node(lib.host_node())  # the pool nearest this runtime's host node
         return Loc("cxl", n)
 
     @staticmethod

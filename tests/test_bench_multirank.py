@@ -74,3 +74,42 @@ def test_bench_forced_one_rank_group(single, tmp_path, parallel):
     out, logits = _bench(tmp_path, 1, ["--parallel", parallel], force_dist=True)
     assert out["n_gpus"] == 1
     assert torch.equal(logits, ref)
+
+
+@pytest.mark.parametrize("parallel", ["tp", "shards"])
+def test_plan_traffic_matches_measured_four_ranks(tmp_path, parallel):
+    """The plan's per-step traffic (TieredLlama.traffic(), what bench.py
+    --plan-only prints) against what a 4-rank run moved: xGMI bytes received by
+    the collectives exactly, PCIe (streamed units) within 10%."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", OGKM_UNIT_MIN_MB="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"), "--gpus", "4"]
+    args = list(ARGS)
+    args[args.index("--steps") + 1] = "2"
+    args += ["--parallel", parallel]
+    r = subprocess.run(cmd + args, env=env, capture_output=True, text=True, timeout=900)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-4000:]
+    t = json.loads(lines[-1])["aux"]["traffic_per_step_gb"]
+    assert t["xgmi_planned"] > 0
+    assert abs(t["xgmi_measured"] - t["xgmi_planned"]) <= 1e-6 + 1e-3 * t["xgmi_planned"], t
+    assert t["pcie_planned"] > 0 and abs(t["pcie_measured"] - t["pcie_planned"]) <= 0.1 * t["pcie_planned"], t
+
+
+def test_plan_only_prints_every_configuration():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--plan-only"], capture_output=True,
+                       text=True, timeout=300, env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    plans = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    got = {(p["plan"], p["parallel"]) for p in plans}
+    for m in ("llama3-70b", "llama3-405b"):
+        for n in (1, 2, 4, 8):
+            assert (m, f"tp{n}") in got
+            if n > 1:
+                assert (m, f"shards{n}") in got
+    for p in plans:
+        r0 = p["per_rank"]
+        assert len(r0["host_numa_node"]) == p["n_gpus"] and r0["cxl_numa_node"] == r0["host_numa_node"]
+        assert p["predicted_ms_per_step"] > 0 and r0["pcie_gb_per_step"] >= 0
+        if p["n_gpus"] > 1:
+            assert r0["xgmi_gb_per_step"] > 0

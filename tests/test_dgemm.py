@@ -83,7 +83,7 @@ def test_dgemm_cpu_strided_x_and_inplace_resid(fake_rt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("packed", [False, True, "generic", "lds", "fused"])
+@pytest.mark.parametrize("packed", [False, True, "generic", "lds", "fused", "split"])
 @pytest.mark.parametrize("epi", ["store", "resid", "silu_mul"])
 @pytest.mark.parametrize("m", [1, 7, 64, 80])
 @pytest.mark.parametrize("n", [320, 336])
@@ -96,7 +96,8 @@ def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m, n):
         pytest.skip("SiLU pairs need N % 64 == 0 on the fused path; covered at N = 320")
     lds = packed == "lds"
     fused = packed == "fused"
-    packed = False if (lds or fused) else packed
+    split = packed == "split"   # raw: k_dgemm<RAW> (False: k_dgemm_pipe, the default raw split-K kernel)
+    packed = False if (lds or fused or split) else packed
     k = 1024
     w = _weights(n, k, 5)
     x = (torch.randn(m, k) * 0.5).to(torch.bfloat16)
@@ -108,8 +109,13 @@ def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m, n):
         out = dgemm.linear(xd, ref_w, epi, resid=rd, fused=True)
         plan = lib.dgemm_fused_plan(n, k, m, dgemm.FUSED_WGS, 2, epi == "silu_mul")
         assert plan[1] > 1  # several K groups: the ticket / slab reduction runs
-    else:  # raw: the 4-row-tile kernel unless "lds"
-        out = dgemm.linear(xd, ref_w, epi, resid=rd, lds=int(lds), fused=False)
+    else:  # raw: the pipelined 4-row-tile kernel unless "lds" / "split"
+        pipe0 = dgemm.PIPE
+        dgemm.PIPE = 0 if split else pipe0
+        try:
+            out = dgemm.linear(xd, ref_w, epi, resid=rd, lds=int(lds), fused=False)
+        finally:
+            dgemm.PIPE = pipe0
     torch.cuda.synchronize()
     want = _ref(x, w, epi, resid)
     torch.testing.assert_close(out.float().cpu(), want, atol=2e-2, rtol=2e-2)

@@ -191,7 +191,11 @@ int main(int argc, char** argv) {
     hsa_amd_memory_copy_engine_status(s.gpu, s.cpu, &s.h2d);
     hsa_amd_memory_copy_engine_status(s.cpu, s.gpu, &s.d2h);
     hsa_signal_create(1, 0, nullptr, &s.sig);
-    printf("{\"cpu_agents\": %zu, \"sdma_h2d_mask\": %u, \"sdma_d2h_mask\": %u}\n", ag.cpus.size(), s.h2d, s.d2h);
+    uint32_t ph = 0, pd = 0;
+    hsa_amd_memory_get_preferred_copy_engine(s.gpu, s.cpu, &ph);
+    hsa_amd_memory_get_preferred_copy_engine(s.cpu, s.gpu, &pd);
+    printf("{\"cpu_agents\": %zu, \"sdma_h2d_mask\": %u, \"sdma_d2h_mask\": %u, \"preferred_h2d\": %u, "
+           "\"preferred_d2h\": %u}\n", ag.cpus.size(), s.h2d, s.d2h, ph, pd);
   }
 
   void* dev = nullptr;
