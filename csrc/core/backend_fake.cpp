@@ -373,10 +373,6 @@ class FakeBackend : public Backend {
     run(s, [a, mode] { dgemm_cpu(a, mode != DGEMM_W_RAW); });
     return Status::OK;
   }
-  Status dgemm_fused(int, const DGemmFusedArgs& a, void* s) override {
-    run(s, [a] { dgemm_fused_cpu(a); });
-    return Status::OK;
-  }
   Status dgemm_reduce(int, const DGemmReduceArgs& a, void* s) override {
     run(s, [a] { dgemm_reduce_cpu(a); });
     return Status::OK;

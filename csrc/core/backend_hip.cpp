@@ -543,11 +543,6 @@ class HipBackend : public Backend {
     launches_++;
     return Status::OK;
   }
-  Status dgemm_fused(int, const DGemmFusedArgs& a, void* s) override {
-    HIPCHK(launch_dgemm_fused(a, (hipStream_t)s));
-    launches_++;
-    return Status::OK;
-  }
   Status dgemm_reduce(int, const DGemmReduceArgs& a, void* s) override {
     HIPCHK(launch_dgemm_reduce(a, (hipStream_t)s));
     launches_++;

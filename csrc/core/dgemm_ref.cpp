@@ -169,24 +169,4 @@ void attn_decode_cpu(const AttnArgs& a) {
     }
 }
 
-// The fused kernel computes the same function as k_dgemm with one K split
-// followed by the reduce epilogue; the reference composes the two.
-void dgemm_fused_cpu(const DGemmFusedArgs& a) {
-  std::vector<float> part((size_t)a.M * a.N);
-  DGemmArgs g{};
-  g.w = reinterpret_cast<const uint8_t*>(a.w);
-  g.x = a.x;
-  g.part = part.data();
-  g.M = a.M; g.N = a.N; g.K = a.K; g.ldx = a.ldx;
-  g.ksplit = 1; g.klen = a.K;
-  g.row_blocks = (a.N / 16 + 3) / 4;
-  dgemm_cpu(g, false);
-  DGemmReduceArgs r{};
-  r.part = part.data();
-  r.ksplit = 1; r.M = a.M; r.N = a.N; r.epi = a.epi;
-  r.resid = a.resid; r.ldr = a.ldr; r.ldo = a.ldo;
-  r.out = a.out;
-  dgemm_reduce_cpu(r);
-}
-
 }  // namespace ogkm

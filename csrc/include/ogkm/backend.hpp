@@ -161,8 +161,6 @@ class Backend {
   // Decode GEMM (ogkm/dgemm.hpp): split-K partials, then the fused epilogue.
   virtual Status dgemm(int dev, const DGemmArgs& a, int mode, void* stream) = 0;
   virtual Status dgemm_reduce(int dev, const DGemmReduceArgs& a, void* stream) = 0;
-  // Fused raw-weight decode GEMM (split-K reduce + epilogue in the same launch).
-  virtual Status dgemm_fused(int dev, const DGemmFusedArgs& a, void* stream) = 0;
   // Fused decode-step ops (ogkm/dgemm.hpp).
   virtual Status rmsnorm(int dev, const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim,
                          uint32_t ldx, uint32_t ldy, float eps, void* stream) = 0;

@@ -20,6 +20,8 @@ struct DGemmArgs {
   uint32_t chunk_shift;   // packed: log2(stream chunk_values)
   uint32_t unroll;        // K steps per pipelined block (1, 2 or 4; 0 = default)
   uint32_t lds_x;         // raw weights: 1 = row tile per wave, activations shared through LDS
+  uint32_t wg_waves;      // split-K kernels: waves per workgroup (0 / 4 = 256 threads, 1 = one-wave
+                          // workgroups, so a few hundred units spread over every CU)
 };
 // Weight source: raw bf16 fragments; a packed stream with BF11 and raw chunks;
 // a packed stream whose chunks are all BF11 (fast, phase-pipelined path).
@@ -45,47 +47,6 @@ inline void dgemm_plan(uint32_t N, uint32_t K, uint32_t target_units, uint32_t* 
   *klen = steps * 32;
   *ksplit = (K + *klen - 1) / *klen;
 }
-
-// Fused raw-weight decode GEMM (k_dgemm_fused): out = epi(X . W^T) in ONE
-// launch. A workgroup = 4 waves = one row block (4 row tiles of 16; SILU_MUL:
-// gate tiles 2b, 2b+1 and their up tiles) x one K group of 4 * klw, each wave a
-// klw slice (intra-workgroup split-K, reduced through LDS). With kgroups > 1 the
-// workgroups of a row block publish f32 slabs and the last arriver (agent-scope
-// ticket) sums them in K order and runs the epilogue - no reduce launch.
-struct DGemmFusedArgs {
-  const uint16_t* w;      // raw bf16 fragment-ordered weights of this tensor
-  const uint16_t* x;      // [M, K] bf16, row stride ldx
-  uint32_t ldx, M, N, K;
-  uint32_t klw;           // K per wave (multiple of 32); a K group is 4 * klw
-  uint32_t kgroups;       // ceil(K / (4 * klw))
-  uint32_t row_blocks;    // ceil(N / 64) (SILU_MUL: N / 64, gate/up tile pairs)
-  uint32_t epi;
-  const uint16_t* resid;  // RESID: bf16 [M, ldr] (may alias out)
-  uint32_t ldr, ldo;
-  uint16_t* out;          // bf16 [M, ldo]
-  float* slab;            // kgroups > 1: [mblocks][row_blocks][kgroups][4 KB x 4 tiles] f32
-  uint32_t* cnt;          // kgroups > 1: [mblocks][row_blocks] tickets, zero (the last arriver re-zeroes)
-  uint32_t unroll;        // K steps per pipelined batch (2 or 4)
-};
-constexpr uint32_t kDgemmSlabFloats = 4 * 4 * 64 * 4;  // one workgroup's 64 rows x 64 M of f32
-// Plan: K per wave so that row_blocks * kgroups * mblocks ~ `target_wgs`
-// workgroups, klw a multiple of 32 * unroll where K allows.
-inline void dgemm_fused_plan(uint32_t N, uint32_t K, uint32_t M, uint32_t target_wgs, uint32_t unroll, bool silu,
-                             uint32_t* klw, uint32_t* kgroups, uint32_t* row_blocks) {
-  *row_blocks = silu ? N / 64 : (N / 16 + 3) / 4;
-  const uint32_t mblocks = (M + 63) / 64;
-  const uint32_t base = *row_blocks * mblocks;
-  uint32_t kg = base >= target_wgs ? 1 : (target_wgs + base - 1) / base;
-  const uint32_t step = 32 * (unroll ? unroll : 2);
-  const uint32_t max_kg = K / (4 * step) ? K / (4 * step) : 1;  // >= one batch per wave
-  if (kg > max_kg) kg = max_kg;
-  uint32_t per_wave = (K + 4 * kg - 1) / (4 * kg);
-  per_wave = (per_wave + step - 1) / step * step;
-  if (per_wave > K) per_wave = (K + 31) / 32 * 32;
-  *klw = per_wave;
-  *kgroups = (K + 4 * per_wave - 1) / (4 * per_wave);
-}
-void dgemm_fused_cpu(const DGemmFusedArgs& a);
 
 // ---- fused decode-step ops (csrc/kernels/decode_ops.hip)
 // KV cache layout: [2][B][Hkv][T][hd] bf16 (k then v).

@@ -184,7 +184,7 @@ __device__ __noinline__ u32x4_t bf11_patch_exceptions(const uint8_t* blk, uint32
 template <int kMode, int U>
 __global__ void __launch_bounds__(256) k_dgemm(DGemmArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t unit = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t unit = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (unit >= a.row_blocks * a.ksplit) return;  // wave-uniform exit
   const uint32_t rb = unit / a.ksplit, ks = unit - rb * a.ksplit;
   const uint32_t k_lo = ks * a.klen;
@@ -502,20 +502,9 @@ __global__ void __launch_bounds__(256) k_dgemm_lds(DGemmArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ fused
-// k_dgemm_fused: raw bf16 weights, out = epi(X . W^T) in one launch
-// (ogkm/dgemm.hpp DGemmFusedArgs). Workgroup = 4 waves on one row block (4 row
-// tiles) and one K group; wave w streams the K slice [g*4*klw + w*klw, +klw).
-//  * software pipeline: two register sets of U K steps (4 weight + 4 activation
-//    fragments each); batch b+1's loads are issued before batch b's 16 U MFMAs,
-//    every load unconditional (row tile / M row indices are clamped to valid
-//    memory - the clamped lanes' outputs are never stored), so hipcc counts
-//    vmcnt instead of draining it (cdna_hip_programming.md §5 item 4(c));
-//  * the 4 waves' accumulators are summed through LDS in wave order;
-//  * kgroups > 1: the row block's workgroups (placed on one XCD by the block
-//    remap) publish f32 slabs; the last arriver of an agent-scope ticket sums
-//    the slabs in K-group order and runs the epilogue (no reduce launch);
-//  * epilogue: store / + residual / SiLU(gate) * up, bf16 round-to-nearest-even.
+// ------------------------------------------------------------------ pipelined raw split-K
+// Shared by k_dgemm_pipe: one batch of U K steps (4 weight + 4 activation
+// fragments each) and its 16 U MFMAs.
 template <int U>
 __device__ __forceinline__ void dgf_load(u32x4_t (&wv)[U][4], u32x4_t (&xv)[U][4], const uint16_t* const (&wb)[4],
                                          const uint16_t* const (&xr)[4], uint32_t kst) {
@@ -543,186 +532,16 @@ __device__ __forceinline__ void dgf_mfma(f32x4_t (&acc)[4][4], const u32x4_t (&w
                                                              0, 0);
 }
 
-__device__ __forceinline__ void dgf_store_tile(const DGemmFusedArgs& a, uint32_t tile, uint32_t m_base, uint32_t lane,
-                                               const f32x4_t (&s)[4], const f32x4_t* up) {
-  const uint32_t n = tile * 16u + 4u * (lane >> 4);
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const uint32_t m = m_base + mt * 16 + (lane & 15u);
-    if (m >= a.M) continue;
-    uint16_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float y = s[mt][j];
-      if (a.epi == DGEMM_EPI_RESID) {
-        y = bf16_to_f32(f32_to_bf16_rne(y)) + bf16_to_f32(a.resid[(uint64_t)m * a.ldr + n + j]);
-      } else if (a.epi == DGEMM_EPI_SILU_MUL) {
-        const float g = bf16_to_f32(f32_to_bf16_rne(y)), u = bf16_to_f32(f32_to_bf16_rne(up[mt][j]));
-        y = g / (1.f + __expf(-g)) * u;
-      }
-      o[j] = f32_to_bf16_rne(y);
-    }
-    *reinterpret_cast<u32x2_t*>(a.out + (uint64_t)m * a.ldo + n) =
-        u32x2_t{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
-  }
-}
-
-template <int U>
-__global__ void __launch_bounds__(256, 2) k_dgemm_fused(DGemmFusedArgs a, uint32_t nreal) {
-  // ONE LDS array (cdna_hip_programming.md §5 item 4(a)): 4 waves x 16
-  // accumulator fragments x 64 lanes, then the ticket broadcast word.
-  __shared__ f32x4_t red[4 * 16 * 64 + 1];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // XCD-aware remap: hardware places block i on XCD i % 8; logical blocks
-  // [x * nb/8, (x+1) * nb/8) run on XCD x, so a row block's K groups (adjacent
-  // logical ids) share one L2 for the slab hand-off.
-  const uint32_t nb = gridDim.x;
-  const uint32_t L = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
-  if (L >= nreal) return;  // grid padding (whole workgroup, before any barrier)
-  const uint32_t rb = L / a.kgroups, g = L - rb * a.kgroups;
-  const bool silu = a.epi == DGEMM_EPI_SILU_MUL;
-  const uint32_t ntiles = a.N >> 4;
-  uint32_t tiles[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    tiles[r] = silu ? (r < 2 ? 2 * rb + r : (ntiles >> 1) + 2 * rb + (r - 2)) : 4 * rb + r;
-  const uint32_t kfr = a.K >> 5;
-  const uint16_t* wb[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)  // clamped: a missing row tile streams a valid one, never stored
-    wb[r] = a.w + (uint64_t)(tiles[r] < ntiles ? tiles[r] : ntiles - 1) * kfr * 512u + lane * 8u;
-  const uint32_t m_base = blockIdx.y * 64u;
-  const uint16_t* xr[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const uint32_t m = m_base + mt * 16 + (lane & 15u);
-    xr[mt] = a.x + (uint64_t)(m < a.M ? m : a.M - 1) * a.ldx + 8u * (lane >> 4);
-  }
-  f32x4_t acc[4][4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[r][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const uint32_t k_lo = (g * 4u + wave) * a.klw;
-  const uint32_t k_hi = k_lo >= a.K ? k_lo : (k_lo + a.klw < a.K ? k_lo + a.klw : a.K);
-  const uint32_t s0 = k_lo >> 5, nsteps = (k_hi - k_lo) >> 5;
-  const uint32_t nbat = nsteps / U;
-  if (nbat) {
-    u32x4_t wA[U][4], xA[U][4], wB[U][4], xB[U][4];
-    dgf_load<U>(wA, xA, wb, xr, s0);
-    uint32_t b = 0;
-    // sched_barrier(0): keep each batch's loads issued ahead of the other
-    // batch's MFMAs (otherwise hipcc sinks them behind the MFMAs to save VGPRs
-    // and the two-deep pipeline collapses to one batch in flight).
-    for (; b + 2 < nbat; b += 2) {  // batches b+1 and b+2 exist: every load unconditional
-      dgf_load<U>(wB, xB, wb, xr, s0 + (b + 1) * U);
-      __builtin_amdgcn_sched_barrier(0);
-      dgf_mfma<U>(acc, wA, xA);
-      __builtin_amdgcn_sched_barrier(0);
-      dgf_load<U>(wA, xA, wb, xr, s0 + (b + 2) * U);
-      __builtin_amdgcn_sched_barrier(0);
-      dgf_mfma<U>(acc, wB, xB);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (b + 1 < nbat) {
-      dgf_load<U>(wB, xB, wb, xr, s0 + (b + 1) * U);
-      __builtin_amdgcn_sched_barrier(0);
-      dgf_mfma<U>(acc, wA, xA);
-      dgf_mfma<U>(acc, wB, xB);
-    } else {
-      dgf_mfma<U>(acc, wA, xA);
-    }
-  }
-  for (uint32_t st = nbat * U; st < nsteps; ++st) {
-    u32x4_t w1[1][4], x1[1][4];
-    dgf_load<1>(w1, x1, wb, xr, s0 + st);
-    dgf_mfma<1>(acc, w1, x1);
-  }
-
-  // intra-workgroup split-K: wave v sums its tiles over the 4 waves, in wave order
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) red[(wave * 16u + r * 4 + mt) * 64u + lane] = acc[r][mt];
-  __syncthreads();
-  // non-SiLU: wave v owns tile v; SiLU: waves 0/1 own gate tile v and up tile v + 2
-  const int nown = silu ? (wave < 2 ? 2 : 0) : 1;
-  f32x4_t sum[2][4];
-#pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    const uint32_t r = o == 0 ? wave : wave + 2;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f32x4_t t = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      if (o < nown)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) t += red[(w * 16u + r * 4 + mt) * 64u + lane];
-      sum[o][mt] = t;
-    }
-  }
-  if (a.kgroups > 1) {
-    // publish this K group's slab, take a ticket; the last arriver reduces
-    float* slab_rb = a.slab + ((uint64_t)blockIdx.y * a.row_blocks + rb) * a.kgroups * kDgemmSlabFloats;
-#pragma unroll
-    for (int o = 0; o < 2; ++o) {
-      if (o >= nown) continue;
-      const uint32_t r = o == 0 ? wave : wave + 2;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        *reinterpret_cast<f32x4_t*>(slab_rb + (uint64_t)g * kDgemmSlabFloats + ((r * 4 + mt) * 64u + lane) * 4u) =
-            sum[o][mt];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    uint32_t* cnt = a.cnt + (uint64_t)blockIdx.y * a.row_blocks + rb;
-    uint32_t* flag = reinterpret_cast<uint32_t*>(&red[4 * 16 * 64]);
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (*flag != a.kgroups - 1) return;
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
-    }
-    __syncthreads();
-#pragma unroll
-    for (int o = 0; o < 2; ++o) {
-      if (o >= nown) continue;
-      const uint32_t r = o == 0 ? wave : wave + 2;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        f32x4_t t = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        for (uint32_t q = 0; q < a.kgroups; ++q)
-          t += *reinterpret_cast<const f32x4_t*>(slab_rb + (uint64_t)q * kDgemmSlabFloats +
-                                                 ((r * 4 + mt) * 64u + lane) * 4u);
-        sum[o][mt] = t;
-      }
-    }
-  }
-  if (!nown) return;
-  if (silu) {
-    dgf_store_tile(a, tiles[wave], m_base, lane, sum[0], sum[1]);  // output column block = gate tile
-  } else if (tiles[wave] < ntiles) {
-    dgf_store_tile(a, tiles[wave], m_base, lane, sum[0], nullptr);
-  }
-}
-
 // k_dgemm_pipe: raw-weight split-K unit per wave (one row block = 4 row tiles x
 // one K split, f32 partials for k_dgemm_reduce - the k_dgemm<RAW> contract) with
-// the fused kernel's main loop: two register sets of U K steps, batch b+1's
+// a software-pipelined main loop: two register sets of U K steps, batch b+1's
 // loads issued before batch b's MFMAs (sched_barrier-pinned), and every load
 // unconditional (row-tile / M-row indices clamped to valid memory; clamped
 // lanes' outputs are never stored).
 template <int U>
 __global__ void __launch_bounds__(256, 2) k_dgemm_pipe(DGemmArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t unit = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t unit = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (unit >= a.row_blocks * a.ksplit) return;  // wave-uniform exit (no barriers in this kernel)
   const uint32_t rb = unit / a.ksplit, ks = unit - rb * a.ksplit;
   const uint32_t k_lo = ks * a.klen;
@@ -790,21 +609,6 @@ __global__ void __launch_bounds__(256, 2) k_dgemm_pipe(DGemmArgs a) {
   }
 }
 
-hipError_t launch_dgemm_fused(const DGemmFusedArgs& a, hipStream_t s) {
-  const bool silu = a.epi == DGEMM_EPI_SILU_MUL;
-  if (a.N % 16 || a.K % 32 || a.klw % 32 || !a.klw || !a.kgroups || !a.M || (silu && a.N % 64) ||
-      a.row_blocks != (silu ? a.N / 64 : (a.N / 16 + 3) / 4) || (uint64_t)a.kgroups * 4 * a.klw < a.K ||
-      (a.kgroups > 1 && (!a.slab || !a.cnt)))
-    return hipErrorInvalidValue;
-  const uint32_t nreal = a.row_blocks * a.kgroups;
-  const uint32_t nb = (nreal + 7) / 8 * 8;
-  dim3 grid(nb, (a.M + 63) / 64);
-  // U = 2 (216 VGPRs, 2 waves / SIMD with the 64 KB LDS of 2 workgroups / CU);
-  // U = 4 does not fit 256 VGPRs without spilling.
-  hipLaunchKernelGGL((k_dgemm_fused<2>), grid, dim3(256), 0, s, a, nreal);
-  return hipGetLastError();
-}
-
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s) {
   if (a.N % 16 || a.K % 32 || a.klen % 32 || !a.ksplit || a.row_blocks != (a.N / 16 + kRowTiles - 1) / kRowTiles)
     return hipErrorInvalidValue;
@@ -819,26 +623,30 @@ hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s) {
       hipLaunchKernelGGL((k_dgemm_lds<4>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }
-  dim3 grid((units + 3) / 4, (a.M + kMTiles * 16 - 1) / (kMTiles * 16));
+  // One-wave workgroups (wg_waves 1) spread a GEMM's units over every CU (with
+  // 4-wave workgroups, 768 units occupy only 192 of the 256 CUs).
+  const uint32_t ww = a.wg_waves == 1 ? 1u : 4u;
+  dim3 grid((units + ww - 1) / ww, (a.M + kMTiles * 16 - 1) / (kMTiles * 16));
+  const dim3 block(64 * ww);
   switch (mode) {
     case DGEMM_W_RAW:
       if (a.unroll == 4)
-        hipLaunchKernelGGL((k_dgemm<MODE_RAW, 4>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_dgemm<MODE_RAW, 4>), grid, block, 0, s, a);
       else if (a.unroll == 1)  // unroll 1 = the pipelined raw kernel (k_dgemm_pipe, U = 2)
-        hipLaunchKernelGGL((k_dgemm_pipe<2>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_dgemm_pipe<2>), grid, block, 0, s, a);
       else
-        hipLaunchKernelGGL((k_dgemm<MODE_RAW, 2>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_dgemm<MODE_RAW, 2>), grid, block, 0, s, a);
       break;
     case DGEMM_W_PACKED:
-      hipLaunchKernelGGL((k_dgemm<MODE_PACKED, 1>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((k_dgemm<MODE_PACKED, 1>), grid, block, 0, s, a);
       break;
     case DGEMM_W_PACKED_BF11:
       if (a.unroll == 4)
-        hipLaunchKernelGGL((k_dgemm<MODE_PACKED_BF11, 4>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_dgemm<MODE_PACKED_BF11, 4>), grid, block, 0, s, a);
       else if (a.unroll == 1)
-        hipLaunchKernelGGL((k_dgemm<MODE_PACKED_BF11, 1>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_dgemm<MODE_PACKED_BF11, 1>), grid, block, 0, s, a);
       else
-        hipLaunchKernelGGL((k_dgemm<MODE_PACKED_BF11, 2>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_dgemm<MODE_PACKED_BF11, 2>), grid, block, 0, s, a);
       break;
     default:
       return hipErrorInvalidValue;

@@ -833,7 +833,7 @@ PYBIND11_MODULE(_ogkm, m) {
   m.def("dgemm", [](int dev, uint64_t stream, uint64_t w, uint64_t w_off, int mode, uint32_t chunk_shift,
                     uint64_t x, uint32_t ldx, uint32_t M, uint32_t N, uint32_t K, uint64_t part, uint64_t part_bytes,
                     uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo, uint32_t target_units, uint32_t unroll,
-                    int lds_x) {
+                    int lds_x, uint32_t wg_waves) {
     if (N % 16 || K % 32 || ldx % 8 || !M) throw StatusError("dgemm: N % 16, K % 32, ldx % 8 and M > 0 required");
     if (epi == DGEMM_EPI_SILU_MUL && (N % 32)) throw StatusError("dgemm: SILU_MUL needs N % 32 == 0");
     DGemmArgs a{};
@@ -849,6 +849,7 @@ PYBIND11_MODULE(_ogkm, m) {
     a.row_blocks = (N / 16 + 3) / 4;
     a.chunk_shift = chunk_shift;
     a.unroll = unroll;
+    a.wg_waves = wg_waves;
     if ((uint64_t)a.ksplit * M * N * 4 > part_bytes) throw StatusError("dgemm: partial workspace too small");
     if (mode < DGEMM_W_RAW || mode > DGEMM_W_PACKED_BF11) throw StatusError("dgemm: bad weight mode");
     check(rt()->be()->dgemm(dev, a, mode, (void*)stream), "dgemm");
@@ -862,45 +863,7 @@ PYBIND11_MODULE(_ogkm, m) {
   }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("w_off"), py::arg("mode"), py::arg("chunk_shift"),
      py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("part"), py::arg("part_bytes"),
      py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("target_units") = 2048, py::arg("unroll") = 0,
-     py::arg("lds_x") = 0);
-  // Fused raw-weight decode GEMM: (klw, kgroups, row_blocks, slab_bytes, cnt_words) for a shape.
-  m.def("dgemm_fused_plan", [](uint32_t N, uint32_t K, uint32_t M, uint32_t target_wgs, uint32_t unroll, bool silu) {
-    uint32_t klw, kg, rb;
-    dgemm_fused_plan(N, K, M, target_wgs, unroll, silu, &klw, &kg, &rb);
-    const uint64_t mb = (M + 63) / 64;
-    return py::make_tuple(klw, kg, rb, kg > 1 ? mb * rb * kg * kDgemmSlabFloats * 4 : 0, kg > 1 ? mb * rb : 0);
-  });
-  m.def("dgemm_fused", [](int dev, uint64_t stream, uint64_t w, uint64_t x, uint32_t ldx, uint32_t M, uint32_t N,
-                          uint32_t K, uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo,
-                          uint64_t slab, uint64_t slab_bytes, uint64_t cnt, uint64_t cnt_words, uint32_t target_wgs,
-                          uint32_t unroll) {
-    if (N % 16 || K % 32 || ldx % 8 || !M) throw StatusError("dgemm_fused: N % 16, K % 32, ldx % 8 and M > 0 required");
-    const bool silu = epi == DGEMM_EPI_SILU_MUL;
-    if (silu && N % 64) throw StatusError("dgemm_fused: SILU_MUL needs N % 64 == 0");
-    if (epi > DGEMM_EPI_SILU_MUL) throw StatusError("dgemm_fused: bad epilogue");
-    DGemmFusedArgs a{};
-    a.w = (const uint16_t*)w;
-    a.x = (const uint16_t*)x;
-    a.ldx = ldx; a.M = M; a.N = N; a.K = K;
-    a.unroll = unroll == 4 ? 4 : 2;
-    dgemm_fused_plan(N, K, M, target_wgs, a.unroll, silu, &a.klw, &a.kgroups, &a.row_blocks);
-    a.epi = epi;
-    a.resid = (const uint16_t*)resid; a.ldr = ldr;
-    a.out = (uint16_t*)out; a.ldo = ldo;
-    const uint64_t mb = (M + 63) / 64;
-    if (a.kgroups > 1) {
-      if (mb * a.row_blocks * a.kgroups * kDgemmSlabFloats * 4 > slab_bytes || mb * a.row_blocks > cnt_words || !slab ||
-          !cnt)
-        throw StatusError("dgemm_fused: slab / ticket workspace too small");
-      a.slab = (float*)slab;
-      a.cnt = (uint32_t*)cnt;
-    }
-    if (epi == DGEMM_EPI_RESID && !resid) throw StatusError("dgemm_fused: RESID needs resid");
-    check(rt()->be()->dgemm_fused(dev, a, (void*)stream), "dgemm_fused");
-    return a.kgroups;
-  }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("N"),
-     py::arg("K"), py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("slab"),
-     py::arg("slab_bytes"), py::arg("cnt"), py::arg("cnt_words"), py::arg("target_wgs") = 512, py::arg("unroll") = 2);
+     py::arg("lds_x") = 0, py::arg("wg_waves") = 4);
   // Fused decode-step ops (ops/fused.py).
   m.def("rmsnorm", [](int dev, uint64_t stream, uint64_t x, uint64_t w, uint64_t y, uint32_t rows, uint32_t dim,
                       uint32_t ldx, uint32_t ldy, float eps) {

@@ -61,9 +61,14 @@ def _mode_class():
         def __init__(self, device: int = 0, lookahead_bytes: Optional[int] = None):
             super().__init__()
             self.device = int(device)
-            # default: prefetch up to a quarter of the arena ahead
+            # default: a short window - min(512 MB, arena / 16). Measured on the
+            # stock 8B model at 2x (12.3 GB arena): 512 MB -> 134 tok/s, 256 MB
+            # 125, 0 (no prefetch) 117, 1 GB 62, 2 GB 6.7, a quarter of the arena
+            # 4.8: every prefetched tensor is LRU-fresh, so a long window evicts
+            # operands needed before the prefetched ones and the passes thrash
+            # (profiles/r3_managed_lookahead.txt).
             if lookahead_bytes is None:
-                lookahead_bytes = _arena_capacity(self.device) // 4
+                lookahead_bytes = min(512 << 20, _arena_capacity(self.device) // 16)
             self.lookahead_bytes = int(lookahead_bytes)
             self._writes: dict = {}
             self._sizes: dict[int, int] = {}

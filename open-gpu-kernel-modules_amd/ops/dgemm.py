@@ -30,20 +30,24 @@ TARGET_UNITS = int(os.environ.get("OGKM_DGEMM_UNITS", "768"))
 # Packed (BF11) weights decode in registers - ALU-heavy, they need the waves:
 TARGET_UNITS_PACKED = int(os.environ.get("OGKM_DGEMM_UNITS_PACKED", "2048"))
 # Raw weights: k_dgemm_lds (row tile per wave, activations shared in LDS, 4x
-# fewer K splits at equal waves) wins when N is small (few row blocks, many
-# splits: 8-13% at N <= 8192) and loses on tall matrices (57344 x 8192: +20%),
-# measured per shape (profiles/r2_dgemm_sweep.txt). -1 = auto (N <= 8192), 0 off, 1 on.
-LDS_X = int(os.environ.get("OGKM_DGEMM_LDS", "-1"))
+# fewer K splits at equal waves). Round 2 measured it 8-13% ahead at N <= 8192;
+# against k_dgemm_pipe it no longer wins at 8B shapes and loses 35% on the 70B
+# down projection (8192 x 28672: 172 vs 127 us; profiles/r3_dgemm_sweep.txt).
+# -1 = auto (N <= 8192), 0 off (default), 1 on.
+LDS_X = int(os.environ.get("OGKM_DGEMM_LDS", "0"))
 LDS_MAX_N = 8192
 UNROLL = int(os.environ.get("OGKM_DGEMM_UNROLL", "0"))  # K steps per pipelined block (0 = kernel default)
-# Raw weights: the fused kernel (k_dgemm_fused: split-K reduce + epilogue inside
-# the launch, two-deep register pipeline) replaces k_dgemm[_lds] + k_dgemm_reduce.
-FUSED = int(os.environ.get("OGKM_DGEMM_FUSED", "0"))
-FUSED_WGS = int(os.environ.get("OGKM_DGEMM_WGS", "512"))  # workgroups per GEMM (2 per CU)
 # Raw weights on the split-K path: k_dgemm_pipe (two-deep register pipeline,
-# unconditional loads) instead of k_dgemm<RAW>; its own split target (waves per GEMM).
+# unconditional loads) instead of k_dgemm<RAW>, in one-wave workgroups (a
+# GEMM's few hundred units spread over all 256 CUs; 4-wave workgroups leave
+# CUs idle), 768 waves per GEMM (1024 for matrices of >= 400 M elements).
+# Measured, graph-timed incl. the reduce (profiles/r3_dgemm_sweep.txt):
+# 8B layer 0.155 -> 0.144 ms (3.04 TB/s), 70B layer 0.430 -> 0.408 ms (4.19 TB/s).
 PIPE = int(os.environ.get("OGKM_DGEMM_PIPE", "1"))
-TARGET_UNITS_PIPE = int(os.environ.get("OGKM_DGEMM_UNITS_PIPE", "1024"))
+WG_WAVES = int(os.environ.get("OGKM_DGEMM_WG", "1"))
+TARGET_UNITS_PIPE = int(os.environ.get("OGKM_DGEMM_UNITS_PIPE", "768"))
+TARGET_UNITS_PIPE_LARGE = int(os.environ.get("OGKM_DGEMM_UNITS_PIPE_LARGE", "1024"))
+LARGE_ELEMS = 400 << 20
 
 
 def frag_permute(w: torch.Tensor) -> torch.Tensor:
@@ -104,33 +108,13 @@ class _Workspace:
 
 _WS = _Workspace()
 _PLANS: dict = {}
-_FPLANS: dict = {}
-_TICKETS: dict = {}   # (device, stream) -> zeroed int32 ticket words (self-resetting)
-_SLABS: dict = {}     # (device, stream) -> f32 slab workspace
-
-
-def _fused_ws(device: torch.device, stream: int, slab_bytes: int, cnt_words: int):
-    key = (str(device), stream)
-    cnt = _TICKETS.get(key)
-    if cnt is None or cnt.numel() < cnt_words:
-        cnt = _TICKETS[key] = torch.zeros(max(cnt_words, 4096), dtype=torch.int32, device=device)
-    slab = _SLABS.get(key)
-    if slab is None or slab.numel() * 4 < slab_bytes:
-        slab = _SLABS[key] = torch.empty(max(slab_bytes // 4, 1 << 18), dtype=torch.float32, device=device)
-    return slab, cnt
-
-
-def fused_ok(w: "WeightRef", epi: str) -> bool:
-    """The fused kernel covers raw weights (any epilogue; SiLU needs N % 64)."""
-    return bool(FUSED) and w.mode == MODE_RAW and (epi != "silu_mul" or w.n % 64 == 0)
 
 
 def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tensor | None = None,
-           out: torch.Tensor | None = None, device_index: int = 0, lds: int | None = None,
-           fused: bool | None = None) -> torch.Tensor:
+           out: torch.Tensor | None = None, device_index: int = 0, lds: int | None = None) -> torch.Tensor:
     """x: [M, K] bf16 (row stride % 8 == 0). Returns out [M, N] (silu_mul: [M, N/2]).
-    ``fused``: None = the fused kernel whenever it covers the call (raw weights),
-    False = the split-K kernels + reduce launch (``lds`` picks the raw variant)."""
+    Raw weights run k_dgemm_pipe (``lds``=1: k_dgemm_lds), packed ones k_dgemm's
+    in-register decode; k_dgemm_reduce sums the K splits and runs the epilogue."""
     if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1 or x.shape[1] != w.k:
         raise ValueError("dgemm.linear: x must be a row-major bf16 [M, K] view")
     m = x.shape[0]
@@ -143,21 +127,6 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
         if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
             raise ValueError("dgemm.linear: resid must match out")
     stream = int(torch.cuda.current_stream(device_index).cuda_stream) if x.is_cuda else 0
-    if fused is None:
-        fused = fused_ok(w, epi) and lds is None
-    elif fused and not (w.mode == MODE_RAW and (epi != "silu_mul" or w.n % 64 == 0)):
-        raise ValueError("dgemm.linear: the fused kernel needs raw weights (SiLU: N % 64 == 0)")
-    if fused:
-        pk = (w.n, w.k, m, epi == "silu_mul")
-        plan = _FPLANS.get(pk)
-        if plan is None:
-            plan = _FPLANS[pk] = lib.dgemm_fused_plan(w.n, w.k, m, FUSED_WGS, 2, epi == "silu_mul")
-        slab, cnt = _fused_ws(x.device, stream, plan[3], plan[4])
-        lib.dgemm_fused(device_index, stream, w.ptr + 2 * w.off, x.data_ptr(), x.stride(0), m, w.n, w.k, EPI[epi],
-                        resid.data_ptr() if resid is not None else 0, resid.stride(0) if resid is not None else 0,
-                        out.data_ptr(), out.stride(0), slab.data_ptr(), slab.numel() * 4, cnt.data_ptr(), cnt.numel(),
-                        FUSED_WGS, 2)
-        return out
     lds = LDS_X if lds is None else int(lds)
     if lds < 0:
         lds = int(w.mode == MODE_RAW and w.n <= LDS_MAX_N)
@@ -166,14 +135,15 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     if lds and w.mode == MODE_RAW:
         units *= 2  # waves; the kernel runs 4 per K split
     elif w.mode == MODE_RAW and PIPE and not UNROLL:
-        units, unroll = TARGET_UNITS_PIPE, 1  # unroll 1 selects k_dgemm_pipe
+        # unroll 1 selects k_dgemm_pipe; the largest matrices take more splits
+        units = TARGET_UNITS_PIPE_LARGE if w.n * w.k >= LARGE_ELEMS else TARGET_UNITS_PIPE
+        unroll = 1
     raw_lds = bool(lds) and w.mode == MODE_RAW
     ks = _PLANS.get((w.n, w.k, units, raw_lds))
     if ks is None:  # the binding plans the launch with the same function: one source of truth
         ks = _PLANS[(w.n, w.k, units, raw_lds)] = lib.dgemm_plan(w.n, w.k, units, raw_lds)[0]
-    ksplit = ks
-    part = _WS.get(x.device, ksplit * m * w.n * 4)
+    part = _WS.get(x.device, ks * m * w.n * 4)
     lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), x.stride(0), m, w.n, w.k,
               part.data_ptr(), part.numel() * 4, EPI[epi], resid.data_ptr() if resid is not None else 0,
-              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, unroll, lds)
+              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, unroll, lds, WG_WAVES)
     return out

@@ -9,7 +9,6 @@ import time
 import pytest
 import torch
 
-from ogkm._native import lib
 from ogkm.ops import bf12, dgemm
 
 
@@ -83,21 +82,23 @@ def test_dgemm_cpu_strided_x_and_inplace_resid(fake_rt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("packed", [False, True, "generic", "lds", "fused", "split"])
+@pytest.mark.parametrize("packed", [False, True, "generic", "lds", "split"])
 @pytest.mark.parametrize("epi", ["store", "resid", "silu_mul"])
 @pytest.mark.parametrize("m", [1, 7, 64, 80])
 @pytest.mark.parametrize("n", [320, 336])
-def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m, n):
-    """packed="lds": raw weights through k_dgemm_lds (activations shared in LDS;
-    N = 336 leaves a partial row block, so idle waves join the exchange);
-    "fused": k_dgemm_fused (in-launch split-K reduce + epilogue, several K
-    groups at K = 1024)."""
-    if epi == "silu_mul" and n % 64:
-        pytest.skip("SiLU pairs need N % 64 == 0 on the fused path; covered at N = 320")
+@pytest.mark.parametrize("wg", [1, 4])
+def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m, n, wg):
+    """packed=False: raw weights through k_dgemm_pipe (the default); "split":
+    k_dgemm<RAW>; "lds": k_dgemm_lds (activations shared in LDS; N = 336 leaves
+    a partial row block, so idle waves join the exchange). wg: waves per
+    workgroup of the split-K kernels."""
+    if epi == "silu_mul" and n % 32:
+        pytest.skip("SiLU needs N % 32 == 0")
+    if packed == "lds" and wg != 4:
+        pytest.skip("k_dgemm_lds has its own 4-wave workgroups")
     lds = packed == "lds"
-    fused = packed == "fused"
-    split = packed == "split"   # raw: k_dgemm<RAW> (False: k_dgemm_pipe, the default raw split-K kernel)
-    packed = False if (lds or fused or split) else packed
+    split = packed == "split"
+    packed = False if (lds or split) else packed
     k = 1024
     w = _weights(n, k, 5)
     x = (torch.randn(m, k) * 0.5).to(torch.bfloat16)
@@ -105,52 +106,15 @@ def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m, n):
     buf, ref_w = _place(w, packed, "cuda")
     xd = x.cuda()
     rd = resid.cuda() if epi == "resid" else None
-    if fused:
-        out = dgemm.linear(xd, ref_w, epi, resid=rd, fused=True)
-        plan = lib.dgemm_fused_plan(n, k, m, dgemm.FUSED_WGS, 2, epi == "silu_mul")
-        assert plan[1] > 1  # several K groups: the ticket / slab reduction runs
-    else:  # raw: the pipelined 4-row-tile kernel unless "lds" / "split"
-        pipe0 = dgemm.PIPE
-        dgemm.PIPE = 0 if split else pipe0
-        try:
-            out = dgemm.linear(xd, ref_w, epi, resid=rd, lds=int(lds), fused=False)
-        finally:
-            dgemm.PIPE = pipe0
+    pipe0, wg0 = dgemm.PIPE, dgemm.WG_WAVES
+    dgemm.PIPE, dgemm.WG_WAVES = (0 if split else pipe0), wg
+    try:
+        out = dgemm.linear(xd, ref_w, epi, resid=rd, lds=int(lds))
+    finally:
+        dgemm.PIPE, dgemm.WG_WAVES = pipe0, wg0
     torch.cuda.synchronize()
     want = _ref(x, w, epi, resid)
     torch.testing.assert_close(out.float().cpu(), want, atol=2e-2, rtol=2e-2)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("epi", ["store", "resid", "silu_mul"])
-def test_dgemm_fused_repeat_deterministic_and_inplace(gpu_rt, epi):
-    """The fused kernel's tickets re-arm themselves (the last arriver re-zeroes
-    its counter): 20 back-to-back calls give identical bits (K-group order is
-    fixed), and RESID in place on the output works."""
-    n, k, m = 512, 4096, 64
-    w = _weights(n, k, 9, specials=False)
-    x = (torch.randn(m, k) * 0.5).to(torch.bfloat16).cuda()
-    buf, ref_w = _place(w, False, "cuda")
-    resid = (torch.randn(m, n) * 0.1).to(torch.bfloat16).cuda()
-    first = None
-    for _ in range(20):
-        if epi == "resid":
-            r = resid.clone()
-            o = dgemm.linear(x, ref_w, "resid", resid=r, out=r, fused=True)
-        else:
-            o = dgemm.linear(x, ref_w, epi, fused=True)
-        first = o.clone() if first is None else first
-        assert torch.equal(o, first)
-    torch.cuda.synchronize()
-    want = _ref(x.cpu(), w, epi, resid.cpu())
-    torch.testing.assert_close(first.float().cpu(), want, atol=2e-2, rtol=2e-2)
-    # the split kernels + reduce compute the same function
-    if epi == "resid":
-        r = resid.clone()
-        o2 = dgemm.linear(x, ref_w, "resid", resid=r, out=r, fused=False)
-    else:
-        o2 = dgemm.linear(x, ref_w, epi, fused=False)
-    torch.testing.assert_close(o2.float(), first.float(), atol=1e-2, rtol=1e-2)
 
 
 @pytest.mark.gpu
@@ -163,7 +127,12 @@ def test_dgemm_gpu_matches_cpu_reference_bits_packed_vs_raw(gpu_rt):
     b1, r1 = _place(w, True, "cuda")
     b2, r2 = _place(w, "generic", "cuda")
     assert r1.mode == dgemm.MODE_PACKED_BF11
-    o0 = dgemm.linear(x, r0, fused=False).clone()  # the same split-K kernel family as the packed modes
+    pipe0 = dgemm.PIPE
+    dgemm.PIPE = 0  # k_dgemm<RAW>: the kernel family of the packed modes (same split / summation order)
+    try:
+        o0 = dgemm.linear(x, r0).clone()
+    finally:
+        dgemm.PIPE = pipe0
     o1 = dgemm.linear(x, r1).clone()
     o2 = dgemm.linear(x, r2)
     torch.cuda.synchronize()

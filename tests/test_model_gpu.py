@@ -34,18 +34,17 @@ def test_tiny_decode_matches_fp32_reference_gpu(gpu_rt, weight_format, kv_format
 
 def test_formats_bit_identical_gpu(gpu_rt):
     """Lossless resting formats give bit-identical logits when the same GEMM
-    kernel family reads them: raw bf16 and rANS (unpacked to bf16, then the
-    fused raw kernel) through k_dgemm_fused; BF11 (decoded in the split-K
-    kernel's registers) against raw bf16 on the split-K kernel. The two kernel
-    families differ only in f32 summation order."""
+    kernel family reads them: raw bf16 and rANS (unpacked to bf16 first)
+    through k_dgemm_pipe; BF11 (decoded in k_dgemm's registers) against raw
+    bf16 on k_dgemm<RAW>. The two families differ only in f32 summation order."""
     from ogkm.ops import dgemm
     cfg = llama.CONFIGS["small"]
     outs = {}
-    fused0 = dgemm.FUSED
+    pipe0 = dgemm.PIPE
     try:
-        for tag, wf, kf, fz in (("bf16", "bf16", "bf16", 1), ("bf16-split", "bf16", "bf16", 0),
-                                ("bf11", "bf11", "bf11", 0), ("ans", "ans", "ans", 1)):
-            dgemm.FUSED = fz
+        for tag, wf, kf, pipe in (("bf16", "bf16", "bf16", 1), ("bf16-split", "bf16", "bf16", 0),
+                                  ("bf11", "bf11", "bf11", 0), ("ans", "ans", "ans", 1)):
+            dgemm.PIPE = pipe
             m = llama.TieredLlama(cfg, batch=4, context=128, max_new_tokens=4, oversub=2.0, lookahead=1, seed=7,
                                   weight_format=wf, kv_format=kf)
             m.keep_logits = True
@@ -58,7 +57,7 @@ def test_formats_bit_identical_gpu(gpu_rt):
             outs[tag] = logs
             m.close()
     finally:
-        dgemm.FUSED = fused0
+        dgemm.PIPE = pipe0
     for a, b in zip(outs["bf16"], outs["ans"]):
         assert torch.equal(a, b)
     for a, b in zip(outs["bf16-split"], outs["bf11"]):

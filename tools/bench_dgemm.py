@@ -62,19 +62,21 @@ def main():
         ws[(n, k)] = (flat, stream.cuda(), info, dgemm.packed_mode(stream))
     xs = {k: (torch.randn(m, k, device="cuda") * 0.5).to(torch.bfloat16) for _, k in SHAPES}
     stage = torch.empty(max(n * k for n, k in SHAPES), dtype=torch.bfloat16, device="cuda")
-    variants = [("fused", 2)] + [("raw", u) for u in (2, 4)] + [("bf11", u) for u in (1, 2, 4)] + [("staged", 2)]
+    variants = [("pipe", 2)] + [("raw", u) for u in (2, 4)] + [("bf11", u) for u in (1, 2, 4)] + [("staged", 2)]
     if os.environ.get("VARIANTS"):  # e.g. "bf11:2,raw:2"
         variants = [(v.split(":")[0], int(v.split(":")[1])) for v in os.environ["VARIANTS"].split(",")]
     for kind, u in variants:
-        dgemm.UNROLL = u
+        # "pipe": the default raw split-K kernel (k_dgemm_pipe, UNROLL 0);
+        # "raw": k_dgemm<RAW, u>
+        dgemm.UNROLL = 0 if kind == "pipe" else u
+        dgemm.PIPE = 1 if kind == "pipe" else 0
         tot_t, tot_b, per = 0.0, 0, {}
         for (n, k), (flat, pk, info, mode) in ws.items():
             out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
             x = xs[k]
-            if kind in ("raw", "fused"):
+            if kind in ("raw", "pipe"):
                 ref = dgemm.WeightRef(flat.data_ptr(), 0, n, k, dgemm.MODE_RAW)
-                fz = kind == "fused"
-                fn = lambda: dgemm.linear(x, ref, out=out, fused=fz)  # noqa: E731
+                fn = lambda: dgemm.linear(x, ref, out=out)  # noqa: E731
                 nb = n * k * 2
             elif kind == "bf11":
                 ref = dgemm.WeightRef(pk.data_ptr(), 0, n, k, mode, 20)
