@@ -192,6 +192,56 @@ def test_cxl_dma_roundtrip(gpu_rt):
     buf.unregister()
 
 
+def test_cxl_dma_full_rate_every_node(gpu_rt):
+    """HBM <-> CXL pool on every NUMA node (local and the other socket) runs at
+    the PCIe rate through a full-rate SDMA engine: the CXL ring used to pick an
+    xGMI engine that moves GPU->host at 12.8 GB/s (profiles/r3_cxl_paths.md)."""
+    import glob
+    from ogkm import cxl
+
+    nodes = sorted(int(p.rsplit("node", 1)[1]) for p in glob.glob("/sys/devices/system/node/node[0-9]*"))
+    lib.cxl_rediscover(-1, "/sys", sum(1 << n for n in nodes))
+    res = {}
+    for n in nodes:
+        r = cxl.measure_bandwidth(0, 512 * MB, iters=3, node=n)
+        res[n] = (round(r["gpu_to_cxl_gbps"], 1), round(r["cxl_to_gpu_gbps"], 1))
+    print("hbm<->cxl per node (d2c, c2d) GB/s:", res, "gpu node", lib.device_numa_node(0))
+    for n, (d2c, c2d) in res.items():
+        assert d2c > 40 and c2d > 40, res
+
+
+def test_ring_copy_bandwidth_d2h(gpu_rt):
+    """GPU -> host through the D2H ring's SDMA engine at the PCIe rate."""
+    n = 1 << 30
+    g = torch.empty(n, dtype=torch.uint8, device="cuda")
+    h = torch.empty(n, dtype=torch.uint8).pin_memory()
+    lib.ring_copy(0, 1, h.data_ptr(), g.data_ptr(), n, True)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        lib.ring_copy(0, 1, h.data_ptr(), g.data_ptr(), n, True)
+    gbps = 3 * n / (time.perf_counter() - t0) / 1e9
+    print(f"D2H ring 1 GiB: {gbps:.1f} GB/s")
+    assert gbps > 50
+
+
+def test_peer_topology_on_hardware(gpu_rt):
+    """parallel/topology.py on the real box (round 2 only ran it on fake
+    devices): link types, NUMA node from sysfs, per-pair caps, CXL caps."""
+    from ogkm.parallel import topology
+
+    t = topology.discover()
+    assert t.n >= 1 and t.link_name(0, 0) == "self"
+    assert t.numa[0] == lib.device_numa_node(0) and t.numa[0] >= 0
+    caps = t.p2p_caps(0, 0)
+    assert caps["link"] == "self" and "cxl_reachable" in caps
+    d = t.to_dict()
+    print("topology", d)
+    for a in range(t.n):
+        for b in range(t.n):
+            if a != b:
+                assert t.link_name(a, b) in ("xgmi", "pcie")
+
+
 def test_dmabuf_export(gpu_rt):
     b = rt.alloc_device_p2p(4 * MB, 0, "p2p")
     info = lib.range_info(b.id)

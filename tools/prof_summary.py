@@ -11,15 +11,17 @@ import sqlite3
 
 def summarize(db: str, top: int = 25, title: str = "") -> str:
     c = sqlite3.connect(db)
-    rows = c.execute("select name, count(*), sum(duration), avg(duration), min(start), max(end) from kernels "
+    rows = c.execute("select name, count(*), sum(duration), avg(duration), min(start), max(end), max(grid_x * grid_y * "
+                     "grid_z), max(workgroup_x * workgroup_y * workgroup_z) from kernels "
                      "group by name order by sum(duration) desc").fetchall()
     total = sum(r[2] for r in rows) or 1
     span = (max(r[5] for r in rows) - min(r[4] for r in rows)) if rows else 0
     out = [f"## {title or db}", "", f"kernel time total {total/1e6:.1f} ms over a {span/1e6:.1f} ms trace window", "",
-           "| kernel | calls | total ms | % | avg us |", "|---|---:|---:|---:|---:|"]
-    for name, n, tot, avg, _, _ in rows[:top]:
+           "| kernel | calls | total ms | % | avg us | max threads (grid) | workgroup |",
+           "|---|---:|---:|---:|---:|---:|---:|"]
+    for name, n, tot, avg, _, _, grid, wg in rows[:top]:
         short = name.split("(")[0][:90]
-        out.append(f"| `{short}` | {n} | {tot/1e6:.2f} | {100*tot/total:.1f} | {avg/1e3:.1f} |")
+        out.append(f"| `{short}` | {n} | {tot/1e6:.2f} | {100*tot/total:.1f} | {avg/1e3:.1f} | {grid} | {wg} |")
     return "\n".join(out) + "\n"
 
 
