@@ -68,7 +68,6 @@ struct AttnArgs {
   float* part_ml;          // [B * hq * nsplit, 2]  (max, sum) per split
   uint32_t B, hq, hkv, hd, T, len, nsplit;
   float scale;
-  int32_t vpre;            // k_attn_decode_ws V preload: -1 auto (grids < 1024 workgroups), 0 off, 1 on
 };
 constexpr uint32_t kAttnSplitTokens = 256;
 

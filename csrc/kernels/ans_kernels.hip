@@ -132,17 +132,11 @@ __global__ void __launch_bounds__(kAnsThreads)
     const uint32_t nv = ch.n_values - base < kAnsSegValues ? ch.n_values - base : kAnsSegValues;
     const uint32_t groups = nv / 512u;
     const uint8_t* smp = blk + kAnsHeaderBytes;
-    // sign|mantissa bytes of the next kSmDepth groups in flight (8 B per lane
-    // per group): one group decodes in ~8 dependent table steps, far shorter
-    // than an HBM round trip, so a one-group prefetch left every group waiting.
-    constexpr uint32_t kSmDepth = 4;
-    au32x2 smq[kSmDepth];
-#pragma unroll
-    for (uint32_t q = 0; q < kSmDepth; ++q)
-      smq[q] = q < groups ? __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + base + (q * 64u + lane) * 8u))
-                          : au32x2{0u, 0u};
-    auto decode_group = [&](uint32_t g, au32x2 sm) {
+    au32x2 smn = __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + base + lane * 8u));
+    for (uint32_t g = 0; g < groups; ++g) {
       const uint32_t v0 = base + (g * 64u + lane) * 8u;
+      const au32x2 sm = smn;
+      if (g + 1 < groups) smn = __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + v0 + 512u));
       au32x4 o = {0u, 0u, 0u, 0u};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -170,22 +164,7 @@ __global__ void __launch_bounds__(kAnsThreads)
         o[j >> 1] |= val << (16 * (j & 1));
       }
       __builtin_nontemporal_store(o, reinterpret_cast<au32x4*>(dst + v0));
-    };
-    uint32_t g = 0;
-    for (; g + kSmDepth <= groups; g += kSmDepth) {
-#pragma unroll
-      for (uint32_t q = 0; q < kSmDepth; ++q) {
-        const au32x2 sm = smq[q];
-        const uint32_t nx = g + q + kSmDepth;  // refill the slot with the group kSmDepth ahead
-        smq[q] = nx < groups
-                     ? __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + base + (nx * 64u + lane) * 8u))
-                     : au32x2{0u, 0u};
-        decode_group(g + q, sm);
-      }
     }
-#pragma unroll
-    for (uint32_t q = 0; q < kSmDepth; ++q)
-      if (g + q < groups) decode_group(g + q, smq[q]);
   }
 }
 

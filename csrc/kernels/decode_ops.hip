@@ -11,8 +11,6 @@
 // The KV cache layout is [2][B][Hkv][T][hd] (k then v), bf16.
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
-
 #include "ogkm/kernels.hpp"
 
 namespace ogkm {
@@ -230,7 +228,7 @@ __global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a) {
 typedef __bf16 attn_bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float attn_f32x4_t __attribute__((ext_vector_type(4)));
 
-template <int HD, int G, bool VPRE_ON>
+template <int HD, int G>
 __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
   constexpr int KS = HD / 32;         // 32-dim MFMA steps
   constexpr int DPV = HD / 32;        // p.v dims per lane
@@ -257,23 +255,6 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
     const uint16_t* kbase = a.cache + ((uint64_t)b * a.hkv + kvh) * (uint64_t)a.T * HD;
     const uint16_t* vbase = a.cache + (((uint64_t)a.B + b) * a.hkv + kvh) * (uint64_t)a.T * HD;
     const uint32_t col = lane & 15, quad = lane >> 4;
-    // V for the whole wave (G <= 8): issued before the K work, so the 16 KB of
-    // V rows are in flight during QK^T and the softmax instead of trickling in
-    // 2 tokens per round trip inside the P.V loop (hkv = 1 tp8 shapes were
-    // latency-bound there). Lane (half, d0) holds tokens half, half + 2, ...;
-    // rows past the context are clamped (loaded, never used).
-    constexpr bool VPRE = VPRE_ON && G <= 8;
-    const uint32_t half = lane >> 5, d0 = (lane & 31) * DPV;
-    typedef typename std::conditional<DPV == 4, uint2, uint32_t>::type vword_t;
-    vword_t vpre[VPRE ? 32 : 1];
-    if constexpr (VPRE) {
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        const int32_t t = (int32_t)half + 2 * i;
-        const uint32_t row = wt0 + (uint32_t)(t < wn ? t : wn - 1);
-        vpre[i] = *reinterpret_cast<const vword_t*>(vbase + (uint64_t)row * HD + d0);
-      }
-    }
     // B fragments: the query group, head `col` (zero past the group)
     uint4 qb[KS];
     const uint16_t* qr = a.q + ((uint64_t)b * a.hq + kvh * g + (col < g ? col : 0)) * HD + 8 * quad;
@@ -339,38 +320,14 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // P.V: half a wave per token, DPV dims per lane
+    const uint32_t half = lane >> 5, d0 = (lane & 31) * DPV;
     float o[G][DPV];
 #pragma unroll
     for (int h = 0; h < G; ++h)
 #pragma unroll
       for (int j = 0; j < DPV; ++j) o[h][j] = 0.f;
-    if constexpr (VPRE) {
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        const int32_t t = (int32_t)half + 2 * i;
-        if (t >= wn) break;
-        float vf[DPV];
-        if constexpr (DPV == 4) {
-          const uint2 w = *reinterpret_cast<const uint2*>(&vpre[i]);
-          vf[0] = dbf((uint16_t)w.x);
-          vf[1] = dbf((uint16_t)(w.x >> 16));
-          vf[2] = dbf((uint16_t)w.y);
-          vf[3] = dbf((uint16_t)(w.y >> 16));
-        } else {
-          const uint32_t w = *reinterpret_cast<const uint32_t*>(&vpre[i]);
-          vf[0] = dbf((uint16_t)w);
-          vf[1] = dbf((uint16_t)(w >> 16));
-        }
-#pragma unroll
-        for (int h = 0; h < G; ++h) {
-          const float p = (uint32_t)h < g ? wps[h * 64 + t] : 0.f;
-#pragma unroll
-          for (int j = 0; j < DPV; ++j) o[h][j] += p * vf[j];
-        }
-      }
-    }
 #pragma unroll PU
-    for (int32_t t = (int32_t)half; !VPRE && t < wn; t += 2) {
+    for (int32_t t = (int32_t)half; t < wn; t += 2) {
       const uint16_t* vr = vbase + (uint64_t)(wt0 + t) * HD + d0;
       float vf[DPV];
       if constexpr (DPV == 4) {
@@ -464,15 +421,7 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
   const dim3 grid(a.nsplit, a.hkv, a.B);
   const size_t lds = (size_t)4 * g * (64 + a.hd) * sizeof(float);
   if (a.hd == 128 || a.hd == 64) {
-  // Few workgroups (hkv = 1 tensor-parallel shards): preload each wave's V rows
-  // up front (latency-bound otherwise, at the cost of occupancy); many: the
-  // leaner variant keeps 4 waves / SIMD.
-  const bool vpre = a.vpre < 0 ? (uint64_t)a.nsplit * a.hkv * a.B < 1024 : a.vpre > 0;
-#define OGKM_ATTN_WS(HD, L)                                                                 \
-  do {                                                                                      \
-    if (vpre) hipLaunchKernelGGL((k_attn_decode_ws<HD, L, true>), grid, dim3(256), lds, s, a); \
-    else hipLaunchKernelGGL((k_attn_decode_ws<HD, L, false>), grid, dim3(256), lds, s, a);     \
-  } while (0)
+#define OGKM_ATTN_WS(HD, L) hipLaunchKernelGGL((k_attn_decode_ws<HD, L>), grid, dim3(256), lds, s, a)
     if (a.hd == 128) {
       if (gg == 4) OGKM_ATTN_WS(128, 4);
       else if (gg == 8) OGKM_ATTN_WS(128, 8);

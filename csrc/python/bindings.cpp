@@ -880,9 +880,8 @@ PYBIND11_MODULE(_ogkm, m) {
   });
   m.def("attn_decode", [](int dev, uint64_t stream, uint64_t q, uint64_t cache, uint64_t out, uint64_t part,
                           uint64_t part_bytes, uint32_t B, uint32_t hq, uint32_t hkv, uint32_t hd, uint32_t T,
-                          uint32_t len, float scale, int vpre) {
+                          uint32_t len, float scale) {
     AttnArgs a{};
-    a.vpre = vpre;
     a.q = (const uint16_t*)q;
     a.cache = (const uint16_t*)cache;
     a.out = (uint16_t*)out;
@@ -895,7 +894,7 @@ PYBIND11_MODULE(_ogkm, m) {
     check(rt()->be()->attn_decode(dev, a, (void*)stream), "attn_decode");
   }, py::arg("dev"), py::arg("stream"), py::arg("q"), py::arg("cache"), py::arg("out"), py::arg("part"),
      py::arg("part_bytes"), py::arg("B"), py::arg("hq"), py::arg("hkv"), py::arg("hd"), py::arg("T"), py::arg("len"),
-     py::arg("scale"), py::arg("vpre") = -1);
+     py::arg("scale"));
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
     py::dict d;

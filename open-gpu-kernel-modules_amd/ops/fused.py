@@ -10,7 +10,6 @@ the same plumbing (layouts, strides, positions).
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
@@ -50,11 +49,6 @@ def rope_kv(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, cache: torc
     return q
 
 
-# k_attn_decode_ws V preload: -1 auto (grids under 1024 workgroups: hkv = 1
-# tensor-parallel shards), 0 off, 1 on (profiles/r3_attn_vpre.txt).
-ATTN_VPRE = int(os.environ.get("OGKM_ATTN_VPRE", "-1"))
-
-
 class _Work:
     buf: dict = {}
 
@@ -72,5 +66,5 @@ def attention(q: torch.Tensor, cache: torch.Tensor, length: int, device_index: i
         _Work.buf[key] = ws
     out = torch.empty(B, hq * hd, dtype=torch.bfloat16, device=q.device)
     lib.attn_decode(device_index, _stream(q, device_index), q.data_ptr(), cache.data_ptr(), out.data_ptr(),
-                    ws.data_ptr(), ws.numel() * 4, B, hq, hkv, hd, T, length, 1.0 / math.sqrt(hd), ATTN_VPRE)
+                    ws.data_ptr(), ws.numel() * 4, B, hq, hkv, hd, T, length, 1.0 / math.sqrt(hd))
     return out

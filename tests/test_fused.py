@@ -100,15 +100,7 @@ def test_attention_one_kv_head_gpu(gpu_rt, hq, hkv, length):
 @pytest.mark.gpu
 @pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (16, 4, 64), (8, 1, 64), (4, 4, 128), (12, 2, 128)])
 @pytest.mark.parametrize("length", [1, 63, 65, 700])
-@pytest.mark.parametrize("vpre", [0, 1])
-def test_attention_group_shapes_gpu(gpu_rt, hq, hkv, hd, length, vpre):
+def test_attention_group_shapes_gpu(gpu_rt, hq, hkv, hd, length):
     """Every group-size / head-dim instantiation of the wave-split kernel
-    (group 1..16 rounded up to 4 / 8 / 16, hd 64 / 128), partial waves
-    included, with and without the V preload."""
-    from ogkm.ops import fused
-    v0 = fused.ATTN_VPRE
-    fused.ATTN_VPRE = vpre
-    try:
-        _check_attention(True, length, hq, hkv, hd)
-    finally:
-        fused.ATTN_VPRE = v0
+    (group 1..16 rounded up to 4 / 8 / 16, hd 64 / 128), partial waves included."""
+    _check_attention(True, length, hq, hkv, hd)

@@ -38,7 +38,7 @@ def main() -> None:
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / iters
         gb = 2 * B * hkv * L * hd * 2 / 1e9
-        print(f"{name:9s} B={B} hq={hq} hkv={hkv} hd={hd} len={L} vpre={fused.ATTN_VPRE}: {us:8.1f} us  "
+        print(f"{name:9s} B={B} hq={hq} hkv={hkv} hd={hd} len={L} {us:8.1f} us  "
               f"KV {gb * 1e3:7.1f} MB  {gb / (us * 1e-6):7.0f} GB/s", flush=True)
 
 
