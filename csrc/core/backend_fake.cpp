@@ -377,9 +377,8 @@ class FakeBackend : public Backend {
     run(s, [a] { dgemm_reduce_cpu(a); });
     return Status::OK;
   }
-  Status rmsnorm(int, const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim, uint32_t ldx,
-                 uint32_t ldy, float eps, void* s) override {
-    run(s, [=] { rmsnorm_cpu(x, w, y, rows, dim, ldx, ldy, eps); });
+  Status rmsnorm(int, const ResidNormArgs& a, void* s) override {
+    run(s, [a] { rmsnorm_cpu(a); });
     return Status::OK;
   }
   Status rope_kv(int, const RopeKvArgs& a, void* s) override {

@@ -548,9 +548,8 @@ class HipBackend : public Backend {
     launches_++;
     return Status::OK;
   }
-  Status rmsnorm(int, const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim, uint32_t ldx,
-                 uint32_t ldy, float eps, void* s) override {
-    HIPCHK(launch_rmsnorm(x, w, y, rows, dim, ldx, ldy, eps, (hipStream_t)s));
+  Status rmsnorm(int, const ResidNormArgs& a, void* s) override {
+    HIPCHK(launch_rmsnorm(a, (hipStream_t)s));
     return Status::OK;
   }
   Status rope_kv(int, const RopeKvArgs& a, void* s) override {

@@ -62,11 +62,13 @@ void dgemm_cpu(const DGemmArgs& a, bool packed) {
         for (uint32_t l = 0; l < 64; ++l)
           for (uint32_t j = 0; j < 8; ++j) w[(l & 15) * 32 + 8 * (l >> 4) + j] = bf2f(frag[l * 8 + j]);
         for (uint32_t m = 0; m < a.M; ++m) {
-          const uint16_t* xr = a.x + (uint64_t)m * a.ldx + k;
+          float xv[32];
+          for (uint32_t kk = 0; kk < 32; ++kk)
+            xv[kk] = bf2f(a.x_frag ? a.x[frag_index(m, k + kk, a.K)] : a.x[(uint64_t)m * a.ldx + k + kk]);
           float* pr = a.part + ((uint64_t)ks * a.M + m) * a.N + rt * 16;
           for (uint32_t r = 0; r < 16; ++r) {
             float s = 0.f;
-            for (uint32_t kk = 0; kk < 32; ++kk) s += w[r * 32 + kk] * bf2f(xr[kk]);
+            for (uint32_t kk = 0; kk < 32; ++kk) s += w[r * 32 + kk] * xv[kk];
             pr[r] += s;
           }
         }
@@ -92,19 +94,27 @@ void dgemm_reduce_cpu(const DGemmReduceArgs& a) {
         const float g = bf2f(f2bf(y)), up = bf2f(f2bf(u));
         y = g / (1.f + std::exp(-g)) * up;
       }
-      a.out[(uint64_t)m * a.ldo + n] = f2bf(y);
+      a.out[a.out_frag ? frag_index(m, a.out_col0 + n, a.out_cols) : (uint64_t)m * a.ldo + n] = f2bf(y);
     }
   }
 }
 
-void rmsnorm_cpu(const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim, uint32_t ldx,
-                 uint32_t ldy, float eps) {
-  for (uint32_t r = 0; r < rows; ++r) {
-    const uint16_t* xr = x + (uint64_t)r * ldx;
+void rmsnorm_cpu(const ResidNormArgs& a) {
+  for (uint32_t r = 0; r < a.rows; ++r) {
+    uint16_t* xr = a.x + (uint64_t)r * a.ldx;
+    if (a.part) {  // the RESID epilogue of the deferred GEMM (k_dgemm_reduce order: k ascending)
+      for (uint32_t i = 0; i < a.dim; ++i) {
+        float s = 0.f;
+        for (uint32_t k = 0; k < a.ksplit; ++k) s += a.part[((uint64_t)k * a.rows + r) * a.dim + i];
+        xr[i] = f2bf(bf2f(f2bf(s)) + bf2f(xr[i]));
+      }
+    }
     float ss = 0.f;
-    for (uint32_t i = 0; i < dim; ++i) ss += bf2f(xr[i]) * bf2f(xr[i]);
-    const float inv = 1.f / std::sqrt(ss / (float)dim + eps);
-    for (uint32_t i = 0; i < dim; ++i) y[(uint64_t)r * ldy + i] = f2bf(bf2f(f2bf(bf2f(xr[i]) * inv)) * bf2f(w[i]));
+    for (uint32_t i = 0; i < a.dim; ++i) ss += bf2f(xr[i]) * bf2f(xr[i]);
+    const float inv = 1.f / std::sqrt(ss / (float)a.dim + a.eps);
+    for (uint32_t i = 0; i < a.dim; ++i)
+      a.y[a.y_frag ? frag_index(r, i, a.dim) : (uint64_t)r * a.ldy + i] =
+          f2bf(bf2f(f2bf(bf2f(xr[i]) * inv)) * bf2f(a.w[i]));
   }
 }
 
@@ -113,8 +123,21 @@ void rope_kv_cpu(const RopeKvArgs& a) {
   for (uint32_t b = 0; b < a.B; ++b)
     for (uint32_t hh = 0; hh < heads; ++hh)
       for (uint32_t i = 0; i < half; ++i) {
-        const uint16_t* src = a.qkv + (uint64_t)b * a.ldqkv + (uint64_t)hh * a.hd;
-        float x1 = bf2f(src[i]), x2 = bf2f(src[i + half]);
+        float x1, x2;
+        if (a.part) {  // deferred qkv GEMM: its store epilogue, here
+          const uint32_t n = heads * a.hd, c1 = hh * a.hd + i;
+          float s1 = 0.f, s2 = 0.f;
+          for (uint32_t k = 0; k < a.ksplit; ++k) {
+            s1 += a.part[((uint64_t)k * a.B + b) * n + c1];
+            s2 += a.part[((uint64_t)k * a.B + b) * n + c1 + half];
+          }
+          x1 = bf2f(f2bf(s1));
+          x2 = bf2f(f2bf(s2));
+        } else {
+          const uint16_t* src = a.qkv + (uint64_t)b * a.ldqkv + (uint64_t)hh * a.hd;
+          x1 = bf2f(src[i]);
+          x2 = bf2f(src[i + half]);
+        }
         if (hh < a.hq + a.hkv) {
           const float c = a.cos[i], s = a.sin[i];
           const float r1 = x1 * c - x2 * s, r2 = x2 * c + x1 * s;
@@ -165,7 +188,9 @@ void attn_decode_cpu(const AttnArgs& a) {
       std::fill(o.begin(), o.end(), 0.f);
       for (uint32_t t = 0; t < a.len; ++t)
         for (uint32_t d = 0; d < a.hd; ++d) o[d] += sc[t] * bf2f(vb[(uint64_t)t * a.hd + d]);
-      for (uint32_t d = 0; d < a.hd; ++d) a.out[((uint64_t)b * a.hq + qh) * a.hd + d] = f2bf(o[d] / l);
+      for (uint32_t d = 0; d < a.hd; ++d)
+        a.out[a.out_frag ? frag_index(b, qh * a.hd + d, a.hq * a.hd) : ((uint64_t)b * a.hq + qh) * a.hd + d] =
+            f2bf(o[d] / l);
     }
 }
 

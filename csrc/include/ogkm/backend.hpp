@@ -162,8 +162,7 @@ class Backend {
   virtual Status dgemm(int dev, const DGemmArgs& a, int mode, void* stream) = 0;
   virtual Status dgemm_reduce(int dev, const DGemmReduceArgs& a, void* stream) = 0;
   // Fused decode-step ops (ogkm/dgemm.hpp).
-  virtual Status rmsnorm(int dev, const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim,
-                         uint32_t ldx, uint32_t ldy, float eps, void* stream) = 0;
+  virtual Status rmsnorm(int dev, const ResidNormArgs& a, void* stream) = 0;
   virtual Status rope_kv(int dev, const RopeKvArgs& a, void* stream) = 0;
   virtual Status attn_decode(int dev, const AttnArgs& a, void* stream) = 0;
   virtual Status gather_pages(int dev, const PageListDesc& d, void* stream) = 0;

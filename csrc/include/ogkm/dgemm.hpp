@@ -22,7 +22,22 @@ struct DGemmArgs {
   uint32_t lds_x;         // raw weights: 1 = row tile per wave, activations shared through LDS
   uint32_t wg_waves;      // split-K kernels: waves per workgroup (0 / 4 = 256 threads, 1 = one-wave
                           // workgroups, so a few hundred units spread over every CU)
+  uint32_t depth;         // pipelined raw kernel: K steps of loads kept in flight per wave
+                          // (0 / 4 = k_dgemm_pipe's two register sets of 2; 6, 7, 8 = k_dgemm_deep)
+  uint32_t x_frag;        // 1: x is fragment-ordered (frag_index below; rows padded to 16, ldx unused)
 };
+
+// Fragment order of an [M, K] bf16 activation (K % 32 == 0, M padded to a
+// multiple of 16): 16 x 32 tiles, tile (m / 16, k / 32) at index
+// (m / 16) * (K / 32) + k / 32, 1 KB each, lane-major - the B-operand fragment
+// of v_mfma_f32_16x16x32_bf16, exactly as the weights are stored. A GEMM wave
+// then fetches each activation fragment with one contiguous 1 KB access (8
+// full cache lines) instead of 16 half-lines; the producers (RMSNorm, the
+// attention combine, the SiLU-mul epilogue) write this order directly.
+// Elements k .. k + 3 (k % 4 == 0) of one row are contiguous.
+constexpr uint64_t frag_index(uint32_t m, uint32_t k, uint32_t K) {
+  return ((((uint64_t)(m >> 4) * (K >> 5) + (k >> 5)) * 64u + (m & 15u) + 16u * ((k >> 3) & 3u)) << 3) + (k & 7u);
+}
 // Weight source: raw bf16 fragments; a packed stream with BF11 and raw chunks;
 // a packed stream whose chunks are all BF11 (fast, phase-pipelined path).
 enum DGemmWeights : int { DGEMM_W_RAW = 0, DGEMM_W_PACKED = 1, DGEMM_W_PACKED_BF11 = 2 };
@@ -34,6 +49,8 @@ struct DGemmReduceArgs {
   const uint16_t* resid;   // RESID: bf16 [M, ldr]
   uint32_t ldr, ldo;
   uint16_t* out;           // bf16 [M, ldo] (may alias resid)
+  uint32_t out_frag;       // 1: out is fragment-ordered [M16][out_cols]; this launch writes columns
+  uint32_t out_cols, out_col0;  // out_col0 .. out_col0 + nout of it (ldo unused)
 };
 // Split-K plan: enough waves to fill the chip (>= ~4 per CU over 256 CUs) while
 // keeping each split's K range a multiple of 32.
@@ -59,6 +76,24 @@ struct RopeKvArgs {
   uint16_t* cache;         // [2][B][hkv][T][hd]: rotated k and v written at `pos`
   uint16_t* tail;          // optional second copy [2][B][hkv][tail_T][hd] at `tail_pos`
   uint32_t B, hq, hkv, hd, T, pos, tail_T, tail_pos;
+  // Deferred qkv GEMM: when set, qkv is bf16(sum over ksplit of part[k][B][N])
+  // (N = (hq + 2 hkv) hd, the decode GEMM's store epilogue) and `qkv` is unused.
+  const float* part;
+  uint32_t ksplit;
+};
+// RMSNorm over `rows` rows of x, optionally after the deferred residual GEMM
+// epilogue: with part set, x += bf16(sum over ksplit of part[k][rows][dim])
+// (x updated in place, = k_dgemm_reduce's RESID epilogue), then
+// y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w).
+struct ResidNormArgs {
+  const float* part;       // nullptr: plain RMSNorm
+  uint32_t ksplit;
+  uint16_t* x;             // [rows, ldx] bf16
+  const uint16_t* w;       // [dim]
+  uint16_t* y;             // [rows, ldy] (y_frag: fragment-ordered [rows16][dim], ldy unused)
+  uint32_t rows, dim, ldx, ldy;
+  float eps;
+  uint32_t y_frag;
 };
 struct AttnArgs {
   const uint16_t* q;       // [B, hq, hd] (rotated)
@@ -68,12 +103,12 @@ struct AttnArgs {
   float* part_ml;          // [B * hq * nsplit, 2]  (max, sum) per split
   uint32_t B, hq, hkv, hd, T, len, nsplit;
   float scale;
+  uint32_t out_frag;       // 1: out is fragment-ordered [B16][hq * hd]
 };
 constexpr uint32_t kAttnSplitTokens = 256;
 
 // CPU references of the decode-step ops (fake backend, tests).
-void rmsnorm_cpu(const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim, uint32_t ldx,
-                 uint32_t ldy, float eps);
+void rmsnorm_cpu(const ResidNormArgs& a);
 void rope_kv_cpu(const RopeKvArgs& a);
 void attn_decode_cpu(const AttnArgs& a);
 

@@ -82,8 +82,7 @@ hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, ui
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);
 hipError_t launch_dgemm_reduce(const DGemmReduceArgs& a, hipStream_t s);
 // Fused decode-step ops (csrc/kernels/decode_ops.hip).
-hipError_t launch_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim,
-                          uint32_t ldx, uint32_t ldy, float eps, hipStream_t s);
+hipError_t launch_rmsnorm(const ResidNormArgs& a, hipStream_t s);
 hipError_t launch_rope_kv(const RopeKvArgs& a, hipStream_t s);
 hipError_t launch_attn_decode(AttnArgs a, hipStream_t s);
 

@@ -1,6 +1,7 @@
 // Fused decode-step kernels around the decode GEMM (one launch each, replacing
 // 5-20 framework kernels per op):
-//   k_rmsnorm       y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w)   one workgroup per row
+//   k_rmsnorm       y = bf16(bf16(x * rsqrt(mean(x^2) + eps)) * w)   one workgroup per row,
+//                   optionally after a deferred GEMM's residual epilogue
 //   k_rope_kv       q/k rotate-half RoPE at one position, k/v appended into the
 //                   KV cache (and a second copy, the packed cache's raw tail)
 //   k_attn_decode   GQA decode attention, flash-decoding split over the
@@ -34,30 +35,110 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// ---------------------------------------------------------------- RMSNorm
-__global__ void __launch_bounds__(256) k_rmsnorm(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-                                                 uint16_t* __restrict__ y, uint32_t dim, uint32_t ldx, uint32_t ldy,
-                                                 float eps) {
+// ---------------------------------------------------------------- RMSNorm (+ deferred residual GEMM epilogue)
+// One 256-thread workgroup per row; thread t owns columns 4t + 1024 j (16-byte
+// f32x4 partial loads, 8-byte bf16 loads/stores), its <= 16 groups held in
+// registers between the residual update, the sum of squares and the scaling.
+// With a.part set, the row first takes the deferred decode GEMM's RESID
+// epilogue: x = bf16(bf16(sum_k part[k]) + x), summed k ascending like
+// k_dgemm_reduce, so the fused and the separate path give identical bits -
+// and one launch (this one) replaces the reduce + the norm.
+constexpr uint32_t kNormMaxGroups = 16;  // dim <= 16384
+
+// Residual update of G column groups (4 columns each) of one row from the
+// deferred split-K partials: loads issued KB splits x G groups at a time (the
+// k loop is latency-bound otherwise: one dependent L2/MALL round trip per
+// split), summed k ascending per column like k_dgemm_reduce.
+template <int G, int KB>
+__device__ __forceinline__ void norm_resid_groups(const ResidNormArgs& a, uint32_t row, uint32_t t, uint16_t* xr,
+                                                  float (&v)[kNormMaxGroups][4]) {
+  float4 sum[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) sum[j] = float4{0.f, 0.f, 0.f, 0.f};
+  for (uint32_t k0 = 0; k0 < a.ksplit; k0 += KB) {
+    float4 q[KB][G];
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        const uint32_t c = 4 * t + 1024 * j;
+        q[kk][j] = (k0 + kk < a.ksplit && c < a.dim)
+                       ? *reinterpret_cast<const float4*>(a.part + ((uint64_t)(k0 + kk) * a.rows + row) * a.dim + c)
+                       : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+      for (int j = 0; j < G; ++j)
+        if (k0 + kk < a.ksplit) {
+          sum[j].x += q[kk][j].x; sum[j].y += q[kk][j].y; sum[j].z += q[kk][j].z; sum[j].w += q[kk][j].w;
+        }
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const uint32_t c = 4 * t + 1024 * j;
+    if (c >= a.dim) break;
+    const float s4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
+    uint16_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = df2bf(dbf(df2bf(s4[e])) + v[j][e]);
+      v[j][e] = dbf(o[e]);
+    }
+    *reinterpret_cast<uint2*>(xr + c) =
+        uint2{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rmsnorm(ResidNormArgs a) {
   __shared__ float red[4];
-  const uint16_t* xr = x + (uint64_t)blockIdx.x * ldx;
-  uint16_t* yr = y + (uint64_t)blockIdx.x * ldy;
+  const uint32_t row = blockIdx.x, t = threadIdx.x;
+  uint16_t* xr = a.x + (uint64_t)row * a.ldx;
+  uint16_t* yr = a.y + (uint64_t)row * a.ldy;
+  float v[kNormMaxGroups][4];
+#pragma unroll
+  for (uint32_t j = 0; j < kNormMaxGroups; ++j) {
+    const uint32_t c = 4 * t + 1024 * j;
+    if (c >= a.dim) break;
+    const uint2 p = *reinterpret_cast<const uint2*>(xr + c);
+    v[j][0] = dbf((uint16_t)p.x);
+    v[j][1] = dbf((uint16_t)(p.x >> 16));
+    v[j][2] = dbf((uint16_t)p.y);
+    v[j][3] = dbf((uint16_t)(p.y >> 16));
+  }
+  if (a.part) {
+    if (a.dim <= 4096)
+      norm_resid_groups<4, 8>(a, row, t, xr, v);
+    else if (a.dim <= 8192)
+      norm_resid_groups<8, 4>(a, row, t, xr, v);
+    else
+      norm_resid_groups<16, 2>(a, row, t, xr, v);
+  }
   float ss = 0.f;
-  for (uint32_t i = threadIdx.x * 2; i < dim; i += 512) {
-    const uint32_t p = *reinterpret_cast<const uint32_t*>(xr + i);
-    const float a = dbf((uint16_t)p), b = dbf((uint16_t)(p >> 16));
-    ss += a * a + b * b;
+#pragma unroll
+  for (uint32_t j = 0; j < kNormMaxGroups; ++j) {
+    const uint32_t c = 4 * t + 1024 * j;
+    if (c >= a.dim) break;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ss += v[j][e] * v[j][e];
   }
   ss = wave_sum(ss);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  if ((t & 63) == 0) red[t >> 6] = ss;
   __syncthreads();
   const float tot = red[0] + red[1] + red[2] + red[3];
-  const float r = rsqrtf(tot / (float)dim + eps);
-  for (uint32_t i = threadIdx.x * 2; i < dim; i += 512) {
-    const uint32_t p = *reinterpret_cast<const uint32_t*>(xr + i);
-    const uint32_t q = *reinterpret_cast<const uint32_t*>(w + i);
-    const float a = dbf(df2bf(dbf((uint16_t)p) * r)) * dbf((uint16_t)q);
-    const float b = dbf(df2bf(dbf((uint16_t)(p >> 16)) * r)) * dbf((uint16_t)(q >> 16));
-    *reinterpret_cast<uint32_t*>(yr + i) = (uint32_t)df2bf(a) | ((uint32_t)df2bf(b) << 16);
+  const float r = rsqrtf(tot / (float)a.dim + a.eps);
+#pragma unroll
+  for (uint32_t j = 0; j < kNormMaxGroups; ++j) {
+    const uint32_t c = 4 * t + 1024 * j;
+    if (c >= a.dim) break;
+    const uint2 q = *reinterpret_cast<const uint2*>(a.w + c);
+    const float wv[4] = {dbf((uint16_t)q.x), dbf((uint16_t)(q.x >> 16)), dbf((uint16_t)q.y), dbf((uint16_t)(q.y >> 16))};
+    uint16_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = df2bf(dbf(df2bf(v[j][e] * r)) * wv[e]);
+    uint16_t* dst = a.y_frag ? a.y + frag_index(row, c, a.dim) : yr + c;
+    *reinterpret_cast<uint2*>(dst) =
+        uint2{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
   }
 }
 
@@ -72,8 +153,34 @@ __global__ void __launch_bounds__(256) k_rope_kv(RopeKvArgs a) {
   const uint32_t i = (uint32_t)(idx % half);
   const uint32_t hh = (uint32_t)((idx / half) % heads);
   const uint32_t b = (uint32_t)(idx / ((uint64_t)half * heads));
-  const uint16_t* src = a.qkv + (uint64_t)b * a.ldqkv + (uint64_t)hh * a.hd;
-  float x1 = dbf(src[i]), x2 = dbf(src[i + half]);
+  float x1, x2;
+  if (a.part) {  // deferred qkv GEMM: its split-K sum + store epilogue, here
+    const uint32_t n = heads * a.hd, c1 = hh * a.hd + i;
+    float s1 = 0.f, s2 = 0.f;
+    constexpr uint32_t kB = 8;  // splits in flight per batch (summed k ascending)
+    for (uint32_t k0 = 0; k0 < a.ksplit; k0 += kB) {
+      float p1[kB], p2[kB];
+#pragma unroll
+      for (uint32_t kk = 0; kk < kB; ++kk) {
+        const bool ok = k0 + kk < a.ksplit;
+        const float* row = a.part + ((uint64_t)(ok ? k0 + kk : 0) * a.B + b) * n;
+        p1[kk] = ok ? row[c1] : 0.f;
+        p2[kk] = ok ? row[c1 + half] : 0.f;
+      }
+#pragma unroll
+      for (uint32_t kk = 0; kk < kB; ++kk)
+        if (k0 + kk < a.ksplit) {
+          s1 += p1[kk];
+          s2 += p2[kk];
+        }
+    }
+    x1 = dbf(df2bf(s1));
+    x2 = dbf(df2bf(s2));
+  } else {
+    const uint16_t* src = a.qkv + (uint64_t)b * a.ldqkv + (uint64_t)hh * a.hd;
+    x1 = dbf(src[i]);
+    x2 = dbf(src[i + half]);
+  }
   if (hh < a.hq + a.hkv) {
     const float c = a.cos[i], s = a.sin[i];
     const float r1 = x1 * c - x2 * s, r2 = x2 * c + x1 * s;
@@ -393,13 +500,17 @@ __global__ void k_attn_combine(AttnArgs a) {
     den += w * a.part_ml[row * 2 + 1];
     if (d < a.hd) num += w * a.part_o[row * a.hd + d];
   }
-  if (d < a.hd) a.out[(uint64_t)bh * a.hd + d] = df2bf(num / den);
+  if (d < a.hd) {
+    const uint32_t b = bh / a.hq, col = (bh - b * a.hq) * a.hd + d;
+    a.out[a.out_frag ? frag_index(b, col, a.hq * a.hd) : (uint64_t)bh * a.hd + d] = df2bf(num / den);
+  }
 }
 
-hipError_t launch_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, uint32_t rows, uint32_t dim,
-                          uint32_t ldx, uint32_t ldy, float eps, hipStream_t s) {
-  if (dim % 2 || ldx % 2 || ldy % 2 || !rows) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_rmsnorm, dim3(rows), dim3(256), 0, s, x, w, y, dim, ldx, ldy, eps);
+hipError_t launch_rmsnorm(const ResidNormArgs& a, hipStream_t s) {
+  if (a.dim % 4 || a.dim > 1024 * kNormMaxGroups || a.ldx % 4 || a.ldy % 4 || (a.y_frag && a.dim % 32))
+    return hipErrorInvalidValue;
+  if (!a.rows) return hipSuccess;
+  hipLaunchKernelGGL(k_rmsnorm, dim3(a.rows), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -416,6 +527,7 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
       !a.len || a.len > a.T)
     return hipErrorInvalidValue;
   if (a.nsplit != (a.len + kAttnSplit - 1) / kAttnSplit) return hipErrorInvalidValue;
+  if (a.out_frag && (a.hq * a.hd) % 32) return hipErrorInvalidValue;
   const uint32_t g = a.hq / a.hkv;
   const uint32_t gg = g <= 4 ? 4 : g <= 8 ? 8 : 16;
   const dim3 grid(a.nsplit, a.hkv, a.B);

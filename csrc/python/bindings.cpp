@@ -833,7 +833,8 @@ PYBIND11_MODULE(_ogkm, m) {
   m.def("dgemm", [](int dev, uint64_t stream, uint64_t w, uint64_t w_off, int mode, uint32_t chunk_shift,
                     uint64_t x, uint32_t ldx, uint32_t M, uint32_t N, uint32_t K, uint64_t part, uint64_t part_bytes,
                     uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo, uint32_t target_units, uint32_t unroll,
-                    int lds_x, uint32_t wg_waves) {
+                    int lds_x, uint32_t wg_waves, uint32_t depth, bool reduce, bool x_frag, bool out_frag,
+                    uint32_t out_cols, uint32_t out_col0) {
     if (N % 16 || K % 32 || ldx % 8 || !M) throw StatusError("dgemm: N % 16, K % 32, ldx % 8 and M > 0 required");
     if (epi == DGEMM_EPI_SILU_MUL && (N % 32)) throw StatusError("dgemm: SILU_MUL needs N % 32 == 0");
     DGemmArgs a{};
@@ -850,38 +851,59 @@ PYBIND11_MODULE(_ogkm, m) {
     a.chunk_shift = chunk_shift;
     a.unroll = unroll;
     a.wg_waves = wg_waves;
+    a.depth = depth;
+    a.x_frag = x_frag ? 1 : 0;
+    if (x_frag && K % 32) throw StatusError("dgemm: fragment-ordered x needs K % 32 == 0");
     if ((uint64_t)a.ksplit * M * N * 4 > part_bytes) throw StatusError("dgemm: partial workspace too small");
     if (mode < DGEMM_W_RAW || mode > DGEMM_W_PACKED_BF11) throw StatusError("dgemm: bad weight mode");
     check(rt()->be()->dgemm(dev, a, mode, (void*)stream), "dgemm");
+    if (!reduce) return a.ksplit;  // deferred: the consumer (rmsnorm / rope_kv) sums the splits
     DGemmReduceArgs r{};
     r.part = a.part;
     r.ksplit = a.ksplit; r.M = M; r.N = N; r.epi = epi;
     r.resid = (const uint16_t*)resid; r.ldr = ldr; r.ldo = ldo;
     r.out = (uint16_t*)out;
+    r.out_frag = out_frag ? 1 : 0;
+    r.out_cols = out_cols;
+    r.out_col0 = out_col0;
+    if (out_frag && (out_cols % 32 || out_col0 % 4 ||
+                     out_col0 + (epi == DGEMM_EPI_SILU_MUL ? N / 2 : N) > out_cols))
+      throw StatusError("dgemm: fragment-ordered out needs out_cols % 32 == 0 and the columns inside it");
     check(rt()->be()->dgemm_reduce(dev, r, (void*)stream), "dgemm_reduce");
     return a.ksplit;
   }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("w_off"), py::arg("mode"), py::arg("chunk_shift"),
      py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("part"), py::arg("part_bytes"),
      py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("target_units") = 2048, py::arg("unroll") = 0,
-     py::arg("lds_x") = 0, py::arg("wg_waves") = 4);
+     py::arg("lds_x") = 0, py::arg("wg_waves") = 4, py::arg("depth") = 0, py::arg("reduce") = true,
+     py::arg("x_frag") = false, py::arg("out_frag") = false, py::arg("out_cols") = 0, py::arg("out_col0") = 0);
   // Fused decode-step ops (ops/fused.py).
   m.def("rmsnorm", [](int dev, uint64_t stream, uint64_t x, uint64_t w, uint64_t y, uint32_t rows, uint32_t dim,
-                      uint32_t ldx, uint32_t ldy, float eps) {
-    check(rt()->be()->rmsnorm(dev, (const uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, rows, dim, ldx, ldy, eps,
-                              (void*)stream),
-          "rmsnorm");
-  });
+                      uint32_t ldx, uint32_t ldy, float eps, uint64_t part, uint32_t ksplit, bool y_frag) {
+    if (dim % 4 || dim > 16384 || ldx % 4 || ldy % 4) throw StatusError("rmsnorm: dim % 4, dim <= 16384, ld % 4");
+    if (y_frag && dim % 32) throw StatusError("rmsnorm: fragment-ordered output needs dim % 32 == 0");
+    ResidNormArgs a{(const float*)part, ksplit, (uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, rows, dim, ldx, ldy,
+                    eps, y_frag ? 1u : 0u};
+    check(rt()->be()->rmsnorm(dev, a, (void*)stream), "rmsnorm");
+  }, py::arg("dev"), py::arg("stream"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("rows"), py::arg("dim"),
+     py::arg("ldx"), py::arg("ldy"), py::arg("eps"), py::arg("part") = 0, py::arg("ksplit") = 0,
+     py::arg("y_frag") = false);
   m.def("rope_kv", [](int dev, uint64_t stream, uint64_t qkv, uint32_t ldqkv, uint64_t cos, uint64_t sin,
                       uint64_t q_out, uint64_t cache, uint64_t tail, uint32_t B, uint32_t hq, uint32_t hkv,
-                      uint32_t hd, uint32_t T, uint32_t pos, uint32_t tail_T, uint32_t tail_pos) {
+                      uint32_t hd, uint32_t T, uint32_t pos, uint32_t tail_T, uint32_t tail_pos, uint64_t part,
+                      uint32_t ksplit) {
     RopeKvArgs a{(const uint16_t*)qkv, ldqkv, (const float*)cos, (const float*)sin, (uint16_t*)q_out,
-                 (uint16_t*)cache, (uint16_t*)tail, B, hq, hkv, hd, T, pos, tail_T, tail_pos};
+                 (uint16_t*)cache, (uint16_t*)tail, B, hq, hkv, hd, T, pos, tail_T, tail_pos,
+                 (const float*)part, ksplit};
     check(rt()->be()->rope_kv(dev, a, (void*)stream), "rope_kv");
-  });
+  }, py::arg("dev"), py::arg("stream"), py::arg("qkv"), py::arg("ldqkv"), py::arg("cos"), py::arg("sin"),
+     py::arg("q_out"), py::arg("cache"), py::arg("tail"), py::arg("B"), py::arg("hq"), py::arg("hkv"), py::arg("hd"),
+     py::arg("T"), py::arg("pos"), py::arg("tail_T"), py::arg("tail_pos"), py::arg("part") = 0,
+     py::arg("ksplit") = 0);
   m.def("attn_decode", [](int dev, uint64_t stream, uint64_t q, uint64_t cache, uint64_t out, uint64_t part,
                           uint64_t part_bytes, uint32_t B, uint32_t hq, uint32_t hkv, uint32_t hd, uint32_t T,
-                          uint32_t len, float scale) {
+                          uint32_t len, float scale, bool out_frag) {
     AttnArgs a{};
+    a.out_frag = out_frag ? 1 : 0;
     a.q = (const uint16_t*)q;
     a.cache = (const uint16_t*)cache;
     a.out = (uint16_t*)out;
@@ -894,7 +916,7 @@ PYBIND11_MODULE(_ogkm, m) {
     check(rt()->be()->attn_decode(dev, a, (void*)stream), "attn_decode");
   }, py::arg("dev"), py::arg("stream"), py::arg("q"), py::arg("cache"), py::arg("out"), py::arg("part"),
      py::arg("part_bytes"), py::arg("B"), py::arg("hq"), py::arg("hkv"), py::arg("hd"), py::arg("T"), py::arg("len"),
-     py::arg("scale"));
+     py::arg("scale"), py::arg("out_frag") = false);
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
     py::dict d;

@@ -559,6 +559,11 @@ class TieredLlama:
         self._pin_leases: list = []
         self._kv_pinned: dict = {}  # kv tiering: resident layers' prefix pointers
         self.keep_logits = False   # tests: keep the full-vocab logits of the last step
+        # deferred GEMM epilogues in the next launch (step(); OGKM_FUSE_EPI=0: separate reduces)
+        self.fuse_epilogues = os.environ.get("OGKM_FUSE_EPI", "1") != "0"
+        # fragment-ordered GEMM activations (OGKM_XFRAG=0: row-major)
+        self.x_frag = os.environ.get("OGKM_XFRAG", "1") != "0"
+        self._xrows = None
         self.last_logits = None
         self.gather = None
         if self.sworld > 1:
@@ -1086,30 +1091,55 @@ class TieredLlama:
         if self.fake:
             x = x.to(self.tdev)
         dv = self.dev
+        # Deferred epilogues (one rank): the qkv GEMM's split-K sum runs in
+        # k_rope_kv, the o / down GEMMs' residual adds in the next k_rmsnorm -
+        # 3 fewer launches per layer, bit-identical to the separate reduce.
+        fuse = self.fuse_epilogues and self.world == 1
+        fuse_down = fuse and len(self.layout.roles["wd"]) == 1
+        # GEMM inputs (h, a, g) in the MFMA fragment order (dgemm.to_frag): every
+        # activation fragment is one contiguous 1 KB load in the GEMM
+        xf = self.x_frag
+        xr = self._xrows = B if xf else None
+        pend = None  # the previous layer's deferred down projection
         for i in range(cfg.n_layers):
-            h = fused.rms_norm(x, self.norm_w[2 * i], cfg.norm_eps, device_index=dv)
+            h = fused.rms_norm(x, self.norm_w[2 * i], cfg.norm_eps, device_index=dv, pending=pend, out_frag=xf)
+            pend = None
             lease, w = self._use(("layer", i, "wqkv"))
-            qkv = dgemm.linear(h, w, device_index=dv)
+            qkv = dgemm.linear(h, w, device_index=dv, defer=fuse, x_rows=xr)
             self._done(lease)
             kvl = self._kv_layer(i, pos)
             q = self._rope_append(i, pos, kvl, qkv)
-            a = fused.attention(q, kvl, pos + 1, device_index=dv)
+            a = fused.attention(q, kvl, pos + 1, device_index=dv, out_frag=xf)
             lease, w = self._use(("layer", i, "wo"))
-            x = self._row_parallel(a, w, x)
-            self._done(lease)
-            h = fused.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps, device_index=dv)
-            g = torch.empty(B, self.f_local, dtype=torch.bfloat16, device=x.device)
+            if fuse:
+                o = dgemm.linear(a, w, device_index=dv, defer=True, x_rows=xr)
+                self._done(lease)
+                h = fused.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps, device_index=dv, pending=o,
+                                   out_frag=xf)
+            else:
+                x = self._row_parallel(a, w, x)
+                self._done(lease)
+                h = fused.rms_norm(x, self.norm_w[2 * i + 1], cfg.norm_eps, device_index=dv, out_frag=xf)
+            g = torch.empty(dgemm.frag_rows(B) if xf else B, self.f_local, dtype=torch.bfloat16, device=x.device)
             for name in self.layout.roles["wgu"]:
                 r0, r1 = self.layout.rows[name]
                 lease, w = self._use(("layer", i, name))
-                dgemm.linear(h, w, "silu_mul", out=g[:, r0:r1], device_index=dv)
+                if xf:
+                    dgemm.linear(h, w, "silu_mul", out=g, out_frag=True, out_col0=r0, device_index=dv, x_rows=xr)
+                else:
+                    dgemm.linear(h, w, "silu_mul", out=g[:, r0:r1], device_index=dv)
                 self._done(lease)
-            x = self._down(i, g, x)
-        x = fused.rms_norm(x, self.final_norm, cfg.norm_eps, device_index=dv)
+            if fuse_down:
+                lease, w = self._use(("layer", i, self.layout.roles["wd"][0]))
+                pend = dgemm.linear(g, w, device_index=dv, defer=True, x_rows=xr)
+                self._done(lease)
+            else:
+                x = self._down(i, g, x)
+        x = fused.rms_norm(x, self.final_norm, cfg.norm_eps, device_index=dv, pending=pend, out_frag=xf)
         logits = torch.empty(B, self.vocab_local, dtype=torch.bfloat16, device=x.device)
         for j, (r0, r1) in enumerate(self.head_rows):
             lease, w = self._use(("head", j))
-            dgemm.linear(x, w, out=logits[:, r0:r1], device_index=dv)
+            dgemm.linear(x, w, out=logits[:, r0:r1], device_index=dv, x_rows=xr)
             self._done(lease)
         if self.keep_logits:
             # tp: vocab shards of every sequence; shards: every rank's own sequences
@@ -1122,8 +1152,8 @@ class TieredLlama:
         """x + (a @ W^T) summed over TP ranks. One rank: the residual add is fused
         into the GEMM epilogue (in place on x); else partial GEMM + RCCL all-reduce."""
         if self.world == 1:
-            return dgemm.linear(a, w, "resid", resid=x, out=x, device_index=self.dev)
-        o = dgemm.linear(a, w, device_index=self.dev)
+            return dgemm.linear(a, w, "resid", resid=x, out=x, device_index=self.dev, x_rows=self._xrows)
+        o = dgemm.linear(a, w, device_index=self.dev, x_rows=self._xrows)
         return x + tpmod.row_parallel_reduce(o)
 
     def _down(self, i: int, g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
@@ -1135,9 +1165,10 @@ class TieredLlama:
             n0, n1 = self.layout.rows[name]
             lease, w = self._use(("layer", i, name))
             if self.world == 1:
-                dgemm.linear(g, w, "resid", resid=x[:, n0:n1], out=x[:, n0:n1], device_index=self.dev)
+                dgemm.linear(g, w, "resid", resid=x[:, n0:n1], out=x[:, n0:n1], device_index=self.dev,
+                             x_rows=self._xrows)
             else:
-                dgemm.linear(g, w, out=o[:, n0:n1], device_index=self.dev)
+                dgemm.linear(g, w, out=o[:, n0:n1], device_index=self.dev, x_rows=self._xrows)
             self._done(lease)
         return x if self.world == 1 else x + tpmod.row_parallel_reduce(o)
 

@@ -48,6 +48,21 @@ WG_WAVES = int(os.environ.get("OGKM_DGEMM_WG", "1"))
 TARGET_UNITS_PIPE = int(os.environ.get("OGKM_DGEMM_UNITS_PIPE", "768"))
 TARGET_UNITS_PIPE_LARGE = int(os.environ.get("OGKM_DGEMM_UNITS_PIPE_LARGE", "1024"))
 LARGE_ELEMS = 400 << 20
+# Pipelined raw path kernel: 0 = auto (below), 4 = k_dgemm_pipe (two register
+# sets of 2 K steps), 3 / 6 / 7 = k_dgemm_deep (register ring of that many K
+# steps), 10 D + aux = k_dgemm_lring (LDS ring of D K steps; aux 2 = non-
+# temporal weight loads).
+DEPTH = int(os.environ.get("OGKM_DGEMM_DEPTH", "0"))
+# Auto: the LDS ring (5 slots = 20 KB of weights in flight per wave) at 512
+# waves when each wave's K range is short (<= LRING_MAX_STEPS 32-wide steps:
+# ramp-dominated units - every decode shape of Llama-3 8B and the 70B
+# attention projections), else k_dgemm_pipe at TARGET_UNITS_PIPE(_LARGE).
+# Measured per shape, graph-timed incl. the reduce (profiles/r3_dgemm_depth.txt):
+# 8B layer 0.143 -> 0.110 ms; 70B q/k/v+o 0.087 -> 0.066 ms; the long-K units
+# (70B gate/up with one K split, down with 224 steps) stay on k_dgemm_pipe.
+LRING_DEPTH = int(os.environ.get("OGKM_DGEMM_LRING_DEPTH", "50"))
+LRING_UNITS = int(os.environ.get("OGKM_DGEMM_LRING_UNITS", "512"))
+LRING_MAX_STEPS = int(os.environ.get("OGKM_DGEMM_LRING_MAX_STEPS", "96"))
 
 
 def frag_permute(w: torch.Tensor) -> torch.Tensor:
@@ -62,6 +77,25 @@ def frag_permute(w: torch.Tensor) -> torch.Tensor:
 def frag_unpermute(flat: torch.Tensor, n: int, k: int) -> torch.Tensor:
     """Inverse of frag_permute: flat fragment order -> [N, K]."""
     return flat.reshape(n // 16, k // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(n, k)
+
+
+def frag_rows(m: int) -> int:
+    """Rows of a fragment-ordered activation buffer holding m rows (16-row tiles)."""
+    return (m + 15) // 16 * 16
+
+
+def to_frag(x: torch.Tensor) -> torch.Tensor:
+    """[M, K] activation -> fragment-ordered [frag_rows(M), K] buffer (csrc
+    frag_index: the MFMA B-operand tiles, as the producers write them)."""
+    m, k = x.shape
+    pad = torch.zeros(frag_rows(m), k, dtype=x.dtype, device=x.device)
+    pad[:m] = x
+    return frag_permute(pad).view(frag_rows(m), k)
+
+
+def from_frag(xf: torch.Tensor, m: int) -> torch.Tensor:
+    """Inverse of to_frag: the first m rows, row-major."""
+    return frag_unpermute(xf.reshape(-1), xf.shape[0], xf.shape[1])[:m]
 
 
 MODE_RAW, MODE_PACKED, MODE_PACKED_BF11 = 0, 1, 2
@@ -110,23 +144,11 @@ _WS = _Workspace()
 _PLANS: dict = {}
 
 
-def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tensor | None = None,
-           out: torch.Tensor | None = None, device_index: int = 0, lds: int | None = None) -> torch.Tensor:
-    """x: [M, K] bf16 (row stride % 8 == 0). Returns out [M, N] (silu_mul: [M, N/2]).
-    Raw weights run k_dgemm_pipe (``lds``=1: k_dgemm_lds), packed ones k_dgemm's
-    in-register decode; k_dgemm_reduce sums the K splits and runs the epilogue."""
-    if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1 or x.shape[1] != w.k:
-        raise ValueError("dgemm.linear: x must be a row-major bf16 [M, K] view")
-    m = x.shape[0]
-    nout = w.n // 2 if epi == "silu_mul" else w.n
-    if out is None:
-        out = torch.empty(m, nout, dtype=torch.bfloat16, device=x.device)
-    if out.dtype != torch.bfloat16 or out.stride(1) != 1 or tuple(out.shape) != (m, nout):
-        raise ValueError("dgemm.linear: bad out")
-    if epi == "resid":
-        if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
-            raise ValueError("dgemm.linear: resid must match out")
-    stream = int(torch.cuda.current_stream(device_index).cuda_stream) if x.is_cuda else 0
+_PIPE_PLANS: dict = {}
+
+
+def _launch_cfg(w: "WeightRef", lds: int | None) -> tuple:
+    """(waves, unroll, lds_x, depth) of one decode GEMM launch."""
     lds = LDS_X if lds is None else int(lds)
     if lds < 0:
         lds = int(w.mode == MODE_RAW and w.n <= LDS_MAX_N)
@@ -134,16 +156,101 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     unroll = UNROLL
     if lds and w.mode == MODE_RAW:
         units *= 2  # waves; the kernel runs 4 per K split
-    elif w.mode == MODE_RAW and PIPE and not UNROLL:
-        # unroll 1 selects k_dgemm_pipe; the largest matrices take more splits
-        units = TARGET_UNITS_PIPE_LARGE if w.n * w.k >= LARGE_ELEMS else TARGET_UNITS_PIPE
+    depth = 0
+    if w.mode == MODE_RAW and PIPE and not UNROLL and not lds:
+        units, depth = _pipe_plan(w.n, w.k)  # unroll 1 selects the pipelined raw kernels
         unroll = 1
+    return units, unroll, lds, depth
+
+
+def _ksplit(w: "WeightRef", units: int, lds: int) -> int:
     raw_lds = bool(lds) and w.mode == MODE_RAW
     ks = _PLANS.get((w.n, w.k, units, raw_lds))
     if ks is None:  # the binding plans the launch with the same function: one source of truth
         ks = _PLANS[(w.n, w.k, units, raw_lds)] = lib.dgemm_plan(w.n, w.k, units, raw_lds)[0]
+    return ks
+
+
+def _pipe_plan(n: int, k: int) -> tuple:
+    """(waves, depth code) of the pipelined raw path for an [n, k] weight."""
+    key = (n, k, DEPTH, LRING_DEPTH, LRING_UNITS, LRING_MAX_STEPS, TARGET_UNITS_PIPE, TARGET_UNITS_PIPE_LARGE)
+    p = _PIPE_PLANS.get(key)
+    if p is None:
+        pipe_units = TARGET_UNITS_PIPE_LARGE if n * k >= LARGE_ELEMS else TARGET_UNITS_PIPE
+        if DEPTH >= 30:
+            p = (LRING_UNITS, DEPTH)
+        elif DEPTH:
+            p = (pipe_units, DEPTH)
+        else:
+            ks, klen = lib.dgemm_plan(n, k, LRING_UNITS, False)
+            p = (LRING_UNITS, LRING_DEPTH) if klen // 32 <= LRING_MAX_STEPS else (pipe_units, 4)
+        _PIPE_PLANS[key] = p
+    return p
+
+
+@dataclass(frozen=True)
+class Deferred:
+    """A decode GEMM whose split-K sum and epilogue run in its consumer's launch
+    (``linear(..., defer=True)``): ``part`` = f32 [ksplit][M][N] in the shared
+    per-device workspace, valid until the next ``linear`` call (``gen``)."""
+    part: int
+    ksplit: int
+    m: int
+    n: int
+    gen: int
+
+    def check(self, m: int, n: int) -> None:
+        if (m, n) != (self.m, self.n):
+            raise ValueError(f"deferred GEMM is [{self.m}, {self.n}], consumer wants [{m}, {n}]")
+        if _GEN[0] != self.gen:
+            raise RuntimeError("deferred GEMM partials were overwritten by a later dgemm.linear call")
+
+
+_GEN = [0]
+
+
+def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tensor | None = None,
+           out: torch.Tensor | None = None, device_index: int = 0, lds: int | None = None,
+           defer: bool = False, x_rows: int | None = None, out_frag: bool = False, out_col0: int = 0):
+    """x: [M, K] bf16 (row stride % 8 == 0). Returns out [M, N] (silu_mul: [M, N/2]).
+    Raw weights run the pipelined kernels (k_dgemm_lring / k_dgemm_pipe, see
+    _pipe_plan; ``lds``=1: k_dgemm_lds), packed ones k_dgemm's in-register decode;
+    k_dgemm_reduce sums the K splits and runs the epilogue. ``defer``: no
+    reduce launch - returns a Deferred whose consumer (fused.rms_norm's
+    residual form, fused.rope_kv) sums the splits and applies the epilogue.
+    ``x_rows``: x is a fragment-ordered [frag_rows(x_rows), K] buffer (to_frag)
+    with x_rows valid rows. ``out_frag``: out is a fragment-ordered
+    [frag_rows(M), C] buffer and this GEMM writes its columns out_col0 ..
+    out_col0 + N (silu_mul: N/2)."""
+    _GEN[0] += 1
+    xf = x_rows is not None
+    if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1 or x.shape[1] != w.k:
+        raise ValueError("dgemm.linear: x must be a row-major bf16 [M, K] view")
+    if xf and (not x.is_contiguous() or x.shape[0] != frag_rows(x_rows)):
+        raise ValueError("dgemm.linear: fragment-ordered x must be a contiguous [frag_rows(M), K] buffer")
+    m = x_rows if xf else x.shape[0]
+    ldx = w.k if xf else x.stride(0)
+    units, unroll, lds_, depth = _launch_cfg(w, lds)
+    ks = _ksplit(w, units, lds_)
     part = _WS.get(x.device, ks * m * w.n * 4)
-    lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), x.stride(0), m, w.n, w.k,
+    stream = int(torch.cuda.current_stream(device_index).cuda_stream) if x.is_cuda else 0
+    if defer:
+        lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), ldx, m, w.n, w.k,
+                  part.data_ptr(), part.numel() * 4, 0, 0, 0, 0, 0, units, unroll, lds_, WG_WAVES, depth, False, xf)
+        return Deferred(part.data_ptr(), ks, m, w.n, _GEN[0])
+    nout = w.n // 2 if epi == "silu_mul" else w.n
+    if out is None:
+        out = torch.empty(frag_rows(m) if out_frag else m, nout, dtype=torch.bfloat16, device=x.device)
+    if out_frag:
+        if out.dtype != torch.bfloat16 or not out.is_contiguous() or out.shape[0] != frag_rows(m) or epi == "resid":
+            raise ValueError("dgemm.linear: bad fragment-ordered out")
+    elif out.dtype != torch.bfloat16 or out.stride(1) != 1 or tuple(out.shape) != (m, nout):
+        raise ValueError("dgemm.linear: bad out")
+    if epi == "resid":
+        if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
+            raise ValueError("dgemm.linear: resid must match out")
+    lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), ldx, m, w.n, w.k,
               part.data_ptr(), part.numel() * 4, EPI[epi], resid.data_ptr() if resid is not None else 0,
-              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, unroll, lds, WG_WAVES)
+              resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, unroll, lds_,
+              WG_WAVES, depth, True, xf, out_frag, out.shape[1] if out_frag else 0, out_col0)
     return out

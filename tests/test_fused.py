@@ -53,6 +53,109 @@ def _check_attention(gpu, length, hq=16, hkv=2, hd=128):
     torch.testing.assert_close(got.float().cpu(), want, atol=2e-2, rtol=2e-2)
 
 
+def _check_deferred_epilogues(gpu):
+    """dgemm.linear(defer=True) + the consumer's fused epilogue == the separate
+    reduce launch, bit for bit: residual add + RMSNorm (o / down projections)
+    and the qkv store epilogue inside RoPE + KV append; a later linear() call
+    invalidates the deferred partials (loud error, not stale data)."""
+    from ogkm.ops import dgemm
+    dv = _dev(gpu)
+    m, d, k = 7, 1024, 2048
+    g = torch.Generator().manual_seed(11)
+    wt = (torch.randn(d, k, generator=g) * 0.02).to(torch.bfloat16)
+    wbuf = dgemm.frag_permute(wt).contiguous().to(dv)
+    wref = dgemm.WeightRef(wbuf.data_ptr(), 0, d, k, dgemm.MODE_RAW)
+    a = (torch.randn(m, k, generator=g) * 0.5).to(torch.bfloat16).to(dv)
+    x0 = (torch.randn(m, d, generator=g) * 0.3).to(torch.bfloat16).to(dv)
+    nw = (torch.rand(d, generator=g) + 0.5).to(torch.bfloat16).to(dv)
+    xa = x0.clone()
+    dgemm.linear(a, wref, "resid", resid=xa, out=xa)
+    ya = fused.rms_norm(xa, nw, 1e-5)
+    xb = x0.clone()
+    pend = dgemm.linear(a, wref, defer=True)
+    yb = fused.rms_norm(xb, nw, 1e-5, pending=pend)
+    assert torch.equal(xa.cpu(), xb.cpu()) and torch.equal(ya.cpu(), yb.cpu())
+    pend = dgemm.linear(a, wref, defer=True)
+    dgemm.linear(a, wref)
+    with pytest.raises(RuntimeError):
+        fused.rms_norm(x0.clone(), nw, 1e-5, pending=pend)
+    # qkv: store epilogue in rope_kv
+    B, hq, hkv, hd, T, pos = m, 12, 2, 64, 24, 5
+    n = (hq + 2 * hkv) * hd
+    wq = (torch.randn(n, k, generator=g) * 0.02).to(torch.bfloat16)
+    qbuf = dgemm.frag_permute(wq).contiguous().to(dv)
+    qref = dgemm.WeightRef(qbuf.data_ptr(), 0, n, k, dgemm.MODE_RAW)
+    cos, sin = D.rope_tables(hd, T, 500000.0, "cpu")
+    ca = torch.zeros(2, B, hkv, T, hd, dtype=torch.bfloat16, device=dv)
+    cb = ca.clone()
+    qa = fused.rope_kv(dgemm.linear(a, qref), cos[pos].to(dv), sin[pos].to(dv), ca, pos, hq, hkv)
+    qb = fused.rope_kv(dgemm.linear(a, qref, defer=True), cos[pos].to(dv), sin[pos].to(dv), cb, pos, hq, hkv)
+    assert torch.equal(qa.cpu(), qb.cpu()) and torch.equal(ca.cpu(), cb.cpu())
+
+
+def _check_fragment_ordered_activations(gpu):
+    """Producers writing the decode GEMM's fragment-ordered activations
+    (RMSNorm, attention, the SiLU-mul epilogue) match the row-major results
+    permuted by dgemm.to_frag, and the GEMM reading them gives the row-major
+    GEMM's bits - raw (the pipelined kernels), BF11-packed (k_dgemm) - for row
+    counts that are not a multiple of 16."""
+    from ogkm.ops import bf12, dgemm
+    dv = _dev(gpu)
+    g = torch.Generator().manual_seed(21)
+    m, d = 7, 1024
+    x = (torch.randn(m, d, generator=g) * 2).to(torch.bfloat16).to(dv)
+    nw = (torch.rand(d, generator=g) + 0.5).to(torch.bfloat16).to(dv)
+    y = fused.rms_norm(x, nw, 1e-5)
+    yf = fused.rms_norm(x, nw, 1e-5, out_frag=True)
+    assert yf.shape == (16, d)
+    assert torch.equal(dgemm.from_frag(yf, m).cpu(), y.cpu())
+    B, hq, hkv, hd, T = m, 8, 2, 64, 300
+    q = torch.randn(B, hq, hd, generator=g).to(torch.bfloat16).to(dv)
+    cache = torch.randn(2, B, hkv, T, hd, generator=g).to(torch.bfloat16).to(dv)
+    att = fused.attention(q, cache, 290)
+    attf = fused.attention(q, cache, 290, out_frag=True)
+    assert torch.equal(dgemm.from_frag(attf, B).cpu(), att.cpu())
+    for packed in (False, True):
+        n, k = 320, d
+        wt = (torch.randn(n, k, generator=g) * 0.02).to(torch.bfloat16)
+        flat = dgemm.frag_permute(wt).contiguous()
+        if packed:
+            stream, _ = bf12.pack(flat, chunk_values=1 << 16, fmt="bf11s")
+            buf = stream.to(dv)
+            ref = dgemm.WeightRef(buf.data_ptr(), 0, n, k, dgemm.packed_mode(stream), 16)
+        else:
+            buf = flat.to(dv)
+            ref = dgemm.WeightRef(buf.data_ptr(), 0, n, k, dgemm.MODE_RAW)
+        o_row = dgemm.linear(y, ref)
+        o_frag = dgemm.linear(yf, ref, x_rows=m)
+        assert torch.equal(o_row.cpu(), o_frag.cpu())
+        # SiLU-mul epilogue into two column ranges of a fragment-ordered buffer
+        gf = torch.zeros(16, 2 * (n // 2), dtype=torch.bfloat16, device=dv)
+        s_row = dgemm.linear(y, ref, "silu_mul")
+        dgemm.linear(yf, ref, "silu_mul", out=gf, out_frag=True, out_col0=0, x_rows=m)
+        dgemm.linear(yf, ref, "silu_mul", out=gf, out_frag=True, out_col0=n // 2, x_rows=m)
+        both = dgemm.from_frag(gf, m)
+        assert torch.equal(both[:, :n // 2].cpu(), s_row.cpu()) and torch.equal(both[:, n // 2:].cpu(), s_row.cpu())
+
+
+def test_fragment_ordered_activations_cpu(fake_rt):
+    _check_fragment_ordered_activations(False)
+
+
+@pytest.mark.gpu
+def test_fragment_ordered_activations_gpu(gpu_rt):
+    _check_fragment_ordered_activations(True)
+
+
+def test_deferred_epilogues_cpu(fake_rt):
+    _check_deferred_epilogues(False)
+
+
+@pytest.mark.gpu
+def test_deferred_epilogues_gpu(gpu_rt):
+    _check_deferred_epilogues(True)
+
+
 def test_rmsnorm_cpu(fake_rt):
     _check_rmsnorm(False)
 

@@ -104,6 +104,30 @@ def test_bf12_weights_bit_identical_to_bf16(fake_rt):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("fmt", ["bf16", "ans"])
+def test_fused_epilogues_bit_identical_to_separate_reduces(fake_rt, fmt):
+    """Deferred GEMM epilogues (qkv sum in rope_kv, o / down residual adds in
+    the next RMSNorm) give the same logits bit for bit as the separate
+    k_dgemm_reduce launches, streamed (oversubscribed) and resident."""
+    cfg = llama.CONFIGS["tiny"]
+    out = {}
+    for fuse in ((False, False), (True, False), (False, True), (True, True)):  # (deferred epilogues, frag x)
+        m = llama.TieredLlama(cfg, batch=3, context=8, max_new_tokens=4, oversub=1.5, lookahead=1, seed=4,
+                              weight_format=fmt)
+        m.fuse_epilogues, m.x_frag = fuse
+        m.keep_logits = True
+        logs = []
+        tok = torch.tensor([5, 7, 9])
+        for _ in range(3):
+            tok = m.step(tok)
+            logs.append(m.last_logits.clone())
+        out[fuse] = logs
+        m.close()
+    for key in list(out)[1:]:
+        for a, b in zip(out[(False, False)], out[key]):
+            assert torch.equal(a, b)
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -92,3 +92,26 @@ def test_kv_tiering_matches_fp32_reference_and_resident_kv_gpu(gpu_rt, kv_format
         m.close()
     for a, b in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
+
+
+def test_fused_epilogues_bit_identical_gpu(gpu_rt):
+    """Deferred GEMM epilogues (k_rope_kv / k_rmsnorm sum the split-K partials)
+    vs the separate k_dgemm_reduce launches: identical logits."""
+    cfg = llama.CONFIGS["small"]
+    outs = {}
+    for fuse in ((False, False), (True, False), (False, True), (True, True)):  # (deferred epilogues, frag x)
+        m = llama.TieredLlama(cfg, batch=4, context=128, max_new_tokens=4, oversub=2.0, lookahead=1, seed=7,
+                              weight_format="bf16", kv_format="bf16")
+        m.fuse_epilogues, m.x_frag = fuse
+        m.keep_logits = True
+        tok = torch.tensor([1, 2, 3, 4], device="cuda")
+        logs = []
+        for _ in range(3):
+            tok = m.step(tok)
+            logs.append(m.last_logits.clone())
+        torch.cuda.synchronize()
+        outs[fuse] = logs
+        m.close()
+    for key in list(outs)[1:]:
+        for a, b in zip(outs[(False, False)], outs[key]):
+            assert torch.equal(a, b)

@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--simulate-tp", type=int, default=8)
     ap.add_argument("--oversub", type=float, default=2.0)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--weight-format", default="ans")
+    ap.add_argument("--kv-format", default="ans")
+    ap.add_argument("--batch", type=int, default=64)
     a = ap.parse_args()
     import torch
 
@@ -28,11 +31,20 @@ def main():
     from ogkm.models import llama
     rt.init("hip", host_budget_mb=0)
     cfg = llama.CONFIGS[a.model]
-    m = llama.TieredLlama(cfg, batch=64, context=1024, max_new_tokens=a.steps + 8, oversub=a.oversub,
-                          tp_rank=0, tp_world=a.simulate_tp, weight_format="ans", kv_format="ans", lookahead=1)
-    tok = torch.zeros(64, dtype=torch.int64, device="cuda")
+    m = llama.TieredLlama(cfg, batch=a.batch, context=1024, max_new_tokens=2 * a.steps + 8, oversub=a.oversub,
+                          tp_rank=0, tp_world=a.simulate_tp, weight_format=a.weight_format, kv_format=a.kv_format,
+                          lookahead=1)
+    tok = torch.zeros(a.batch, dtype=torch.int64, device="cuda")
     tok = m.step(tok)
     torch.cuda.synchronize()
+    # unprofiled: host enqueue time vs synchronized step time (GPU-starved when close)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tok = m.step(tok)
+    h = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    print(f"host enqueue {1e3 * h / a.steps:.2f} ms/step (unprofiled), synchronized {1e3 * t / a.steps:.2f} ms/step")
     pr = cProfile.Profile()
     t0 = time.perf_counter()
     pr.enable()
