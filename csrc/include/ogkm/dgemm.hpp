@@ -22,8 +22,8 @@ struct DGemmArgs {
   uint32_t lds_x;         // raw weights: 1 = row tile per wave, activations shared through LDS
   uint32_t wg_waves;      // split-K kernels: waves per workgroup (0 / 4 = 256 threads, 1 = one-wave
                           // workgroups, so a few hundred units spread over every CU)
-  uint32_t depth;         // pipelined raw kernel: K steps of loads kept in flight per wave
-                          // (0 / 4 = k_dgemm_pipe's two register sets of 2; 6, 7, 8 = k_dgemm_deep)
+  uint32_t depth;         // pipelined raw kernel: 0 / 4 = k_dgemm_pipe (two register sets of 2 K
+                          // steps), 10 D = k_dgemm_lring (LDS ring of D K steps, D = 3..7)
   uint32_t x_frag;        // 1: x is fragment-ordered (frag_index below; rows padded to 16, ldx unused)
 };
 
@@ -104,9 +104,10 @@ struct AttnArgs {
   uint32_t B, hq, hkv, hd, T, len, nsplit;
   float scale;
   uint32_t out_frag;       // 1: out is fragment-ordered [B16][hq * hd]
+  uint32_t split_tokens;   // context tokens per workgroup: 256 (4 waves, default) or 64 (1 wave; hd 64 / 128 -
+                           // measured slower at every bench shape, kept as an explicit option)
 };
 constexpr uint32_t kAttnSplitTokens = 256;
-
 // CPU references of the decode-step ops (fake backend, tests).
 void rmsnorm_cpu(const ResidNormArgs& a);
 void rope_kv_cpu(const RopeKvArgs& a);

@@ -617,94 +617,13 @@ __global__ void __launch_bounds__(256, 2) k_dgemm_pipe(DGemmArgs a) {
   }
 }
 
-// k_dgemm_deep: k_dgemm_pipe with a ring of D register sets (U K steps each)
-// instead of two, so D x U x 4 KB of weight loads stay in flight per wave. A
-// decode GEMM runs ~3-4 waves per CU, and the per-wave in-flight bytes set the
-// streaming rate (Little's law: bytes in flight / HBM latency); the two-set
-// pipeline keeps only 8 KB per wave in flight. Same unit contract, same K-step
-// summation order as k_dgemm_pipe (bit-identical partials). The steady-state
-// loop is branch-free (every refill in range); the last 2D batches take the
-// guarded epilogue. D x U x 8 vector loads <= 63 (the vmcnt range).
-template <int U, int D>
-__global__ void __launch_bounds__(256) k_dgemm_deep(DGemmArgs a) {
-  static_assert(D * U * 8 <= 63, "loads in flight exceed the vmcnt range");
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t unit = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (unit >= a.row_blocks * a.ksplit) return;  // wave-uniform exit (no barriers in this kernel)
-  const uint32_t rb = unit / a.ksplit, ks = unit - rb * a.ksplit;
-  const uint32_t k_lo = ks * a.klen;
-  const uint32_t k_hi = k_lo + a.klen < a.K ? k_lo + a.klen : a.K;
-  const uint32_t ntiles = a.N >> 4, kfr = a.K >> 5;
-  const uint16_t* w = reinterpret_cast<const uint16_t*>(a.w) + a.w_off;
-  const uint16_t* wb[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const uint32_t t = rb * 4 + r;
-    wb[r] = w + (uint64_t)(t < ntiles ? t : ntiles - 1) * kfr * 512u + lane * 8u;
-  }
-  const uint32_t m_base = blockIdx.y * 64u;
-  const uint16_t* xr[4];
-  const uint32_t xstep = a.x_frag ? 512u : 32u;  // elements per K step of this lane's activation fragment
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const uint32_t m = m_base + mt * 16 + (lane & 15u), mc = m < a.M ? m : a.M - 1;
-    xr[mt] = a.x_frag ? a.x + (uint64_t)(mc >> 4) * kfr * 512u + (mc & 15u) * 8u + (lane >> 4) * 128u
-                      : a.x + (uint64_t)mc * a.ldx + 8u * (lane >> 4);
-  }
-  f32x4_t acc[4][4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[r][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const uint32_t s0 = k_lo >> 5, nsteps = k_hi > k_lo ? (k_hi - k_lo) >> 5 : 0;
-  const uint32_t nbat = nsteps / U;
-  u32x4_t wv[D][U][4], xv[D][U][4];
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-    if ((uint32_t)d < nbat) dgf_load<U>(wv[d], xv[d], wb, xr, s0 + d * U, xstep);
-  uint32_t b = 0;
-  for (; b + 2 * D <= nbat; b += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      dgf_mfma<U>(acc, wv[d], xv[d]);
-      __builtin_amdgcn_sched_barrier(0);
-      dgf_load<U>(wv[d], xv[d], wb, xr, s0 + (b + d + D) * U, xstep);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    if (b + d < nbat) {
-      dgf_mfma<U>(acc, wv[d], xv[d]);
-      if (b + d + D < nbat) dgf_load<U>(wv[d], xv[d], wb, xr, s0 + (b + d + D) * U, xstep);
-    }
-  }
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (b + D + d < nbat) dgf_mfma<U>(acc, wv[d], xv[d]);
-  for (uint32_t st = nbat * U; st < nsteps; ++st) {
-    u32x4_t w1[1][4], x1[1][4];
-    dgf_load<1>(w1, x1, wb, xr, s0 + st, xstep);
-    dgf_mfma<1>(acc, w1, x1);
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (rb * 4 + r >= ntiles) continue;
-    const uint32_t n = (rb * 4 + r) * 16u + 4u * (lane >> 4);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const uint32_t m = m_base + mt * 16 + (lane & 15u);
-      if (m < a.M) *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[r][mt];
-    }
-  }
-}
-
 // k_dgemm_lring: the same split-K unit (4 row tiles x one K range, one wave per
 // workgroup) with its operands staged through an LDS ring instead of VGPRs.
 // Every K step's 4 weight + 4 activation fragments (8 x 1 KB, lane-linear -
 // exactly the layout global_load_lds writes) go global -> LDS with no VGPR
 // round trip, so D steps (D x 4 KB of weights) stay in flight per wave at ~60
-// VGPRs: the VGPR ring (k_dgemm_deep) runs out of registers at 2-3 steps.
+// VGPRs (a register ring of 3+ K steps runs out of registers: the compiler
+// shuffles it through AGPRs).
 // Consumption waits on vmcnt by hand (loads retire in order: (D-1) x 8 newer
 // ones may stay outstanding) and reads the slot with ds_read_b128 in inline
 // asm, so the compiler's conservative LDS-DMA wait (vmcnt(0) before any LDS
@@ -714,21 +633,21 @@ __device__ __forceinline__ void dg_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int D, int WAUX>
+template <int D>
 __device__ __forceinline__ void lring_issue(u32x4_t (&ring)[D][8][64], uint32_t slot, uint32_t st,
                                             const uint16_t* const (&wb)[4], const uint16_t* const (&xr)[4],
                                             uint32_t xstep) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r)  // WAUX 2: non-temporal weight stream (leaves L2 to the activations)
+  for (int r = 0; r < 4; ++r)
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(wb[r] + (uint64_t)st * 512u), &ring[slot][r][0],
-                                     16, 0, WAUX);
+                                     16, 0, 0);
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(xr[mt] + st * xstep), &ring[slot][4 + mt][0], 16,
                                      0, 0);
 }
 
-template <int D, int WAUX>
+template <int D>
 __global__ void __launch_bounds__(64) k_dgemm_lring(DGemmArgs a) {
   static_assert((D - 1) * 8 <= 63, "vmcnt range");
   __shared__ u32x4_t ring[D][8][64];  // slot, fragment (w rt 0-3, x mt 0-3), lane
@@ -764,7 +683,7 @@ __global__ void __launch_bounds__(64) k_dgemm_lring(DGemmArgs a) {
 
 #pragma unroll
   for (int d = 0; d < D; ++d)
-    if ((uint32_t)d < nsteps) lring_issue<D, WAUX>(ring, d, s0 + d, wb, xr, xstep);
+    if ((uint32_t)d < nsteps) lring_issue<D>(ring, d, s0 + d, wb, xr, xstep);
   // LDS byte address of this lane's 16 B in slot 0, fragment 0
   const uint32_t lbase = (uint32_t)(uintptr_t)&ring[0][0][lane];
   uint32_t slot = 0;
@@ -788,7 +707,7 @@ __global__ void __launch_bounds__(64) k_dgemm_lring(DGemmArgs a) {
         : "=&v"(f0), "=&v"(f1), "=&v"(f2), "=&v"(f3), "=&v"(f4), "=&v"(f5), "=&v"(f6), "=&v"(f7)
         : "v"(la)
         : "memory");
-    if (st + D < nsteps) lring_issue<D, WAUX>(ring, slot, s0 + st + D, wb, xr, xstep);
+    if (st + D < nsteps) lring_issue<D>(ring, slot, s0 + st + D, wb, xr, xstep);
     const u32x4_t wf[4] = {f0, f1, f2, f3}, xf[4] = {f4, f5, f6, f7};
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -827,15 +746,14 @@ hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s) {
   }
   // One-wave workgroups (wg_waves 1) spread a GEMM's units over every CU (with
   // 4-wave workgroups, 768 units occupy only 192 of the 256 CUs).
-  if (mode == DGEMM_W_RAW && a.unroll == 1 && a.depth >= 30) {  // LDS ring: depth = 10 x slots + weight aux
+  if (mode == DGEMM_W_RAW && a.unroll == 1 && a.depth >= 30) {  // LDS ring: depth = 10 x slots
     dim3 grid(units, (a.M + kMTiles * 16 - 1) / (kMTiles * 16));
     switch (a.depth) {
-      case 30: hipLaunchKernelGGL((k_dgemm_lring<3, 0>), grid, dim3(64), 0, s, a); break;
-      case 40: hipLaunchKernelGGL((k_dgemm_lring<4, 0>), grid, dim3(64), 0, s, a); break;
-      case 42: hipLaunchKernelGGL((k_dgemm_lring<4, 2>), grid, dim3(64), 0, s, a); break;
-      case 50: hipLaunchKernelGGL((k_dgemm_lring<5, 0>), grid, dim3(64), 0, s, a); break;
-      case 60: hipLaunchKernelGGL((k_dgemm_lring<6, 0>), grid, dim3(64), 0, s, a); break;
-      case 70: hipLaunchKernelGGL((k_dgemm_lring<7, 0>), grid, dim3(64), 0, s, a); break;
+      case 30: hipLaunchKernelGGL((k_dgemm_lring<3>), grid, dim3(64), 0, s, a); break;
+      case 40: hipLaunchKernelGGL((k_dgemm_lring<4>), grid, dim3(64), 0, s, a); break;
+      case 50: hipLaunchKernelGGL((k_dgemm_lring<5>), grid, dim3(64), 0, s, a); break;
+      case 60: hipLaunchKernelGGL((k_dgemm_lring<6>), grid, dim3(64), 0, s, a); break;
+      case 70: hipLaunchKernelGGL((k_dgemm_lring<7>), grid, dim3(64), 0, s, a); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -847,13 +765,7 @@ hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s) {
     case DGEMM_W_RAW:
       if (a.unroll == 4)
         hipLaunchKernelGGL((k_dgemm<MODE_RAW, 4>), grid, block, 0, s, a);
-      else if (a.unroll == 1 && a.depth == 6)  // unroll 1 = the pipelined raw kernels; depth = K steps in flight
-        hipLaunchKernelGGL((k_dgemm_deep<2, 3>), grid, block, 0, s, a);
-      else if (a.unroll == 1 && a.depth == 7)
-        hipLaunchKernelGGL((k_dgemm_deep<1, 7>), grid, block, 0, s, a);
-      else if (a.unroll == 1 && a.depth == 3)
-        hipLaunchKernelGGL((k_dgemm_deep<1, 3>), grid, block, 0, s, a);
-      else if (a.unroll == 1)  // k_dgemm_pipe: two sets of U = 2
+      else if (a.unroll == 1)  // unroll 1 = the pipelined raw kernel (k_dgemm_pipe, two sets of U = 2)
         hipLaunchKernelGGL((k_dgemm_pipe<2>), grid, block, 0, s, a);
       else
         hipLaunchKernelGGL((k_dgemm<MODE_RAW, 2>), grid, block, 0, s, a);

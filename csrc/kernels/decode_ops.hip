@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a) {
 typedef __bf16 attn_bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float attn_f32x4_t __attribute__((ext_vector_type(4)));
 
-template <int HD, int G>
+template <int HD, int G, int NW>
 __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
   constexpr int KS = HD / 32;         // 32-dim MFMA steps
   constexpr int DPV = HD / 32;        // p.v dims per lane
@@ -343,12 +343,12 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
   static_assert((HD == 64 || HD == 128) && G <= 16, "shape");
   extern __shared__ float smem[];
   const uint32_t g = a.hq / a.hkv;    // <= G
-  float* ps = smem;                   // [4 waves][g][64] scores -> probabilities
-  float* po = smem + 4 * g * 64;      // [4 waves][g][HD] unnormalised outputs
-  __shared__ float wm[4][G], wl[4][G];
+  float* ps = smem;                   // [NW waves][g][64] scores -> probabilities
+  float* po = smem + NW * g * 64;     // [NW waves][g][HD] unnormalised outputs
+  __shared__ float wm[NW][G], wl[NW][G];
   const uint32_t split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t wt0 = split * kAttnSplit + wave * 64;
+  const uint32_t wt0 = split * (64u * NW) + wave * 64;
   const int32_t wn = (int32_t)a.len - (int32_t)wt0 < 64 ? (int32_t)a.len - (int32_t)wt0 : 64;
   float* wps = ps + wave * g * 64;
   float* wpo = po + wave * g * HD;
@@ -465,15 +465,15 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
     }
   }
   __syncthreads();
-  // merge the four wave partials into this split's partial
-  for (uint32_t e = threadIdx.x; e < g * HD; e += 256) {
+  // merge the NW wave partials into this split's partial
+  for (uint32_t e = threadIdx.x; e < g * HD; e += 64 * NW) {
     const uint32_t h = e / HD, d = e - h * HD;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, wm[w][h]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w][h]);
     float acc = 0.f, l = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float f = wm[w][h] == -INFINITY ? 0.f : __expf(wm[w][h] - M);
       acc += f * po[(w * g + h) * HD + d];
       l += f * wl[w][h];
@@ -526,23 +526,25 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
   if (!a.hkv || a.hq % a.hkv || a.hq / a.hkv > (uint32_t)kMaxGroup || a.hd > (uint32_t)kMaxHd || a.hd % 8 ||
       !a.len || a.len > a.T)
     return hipErrorInvalidValue;
-  if (a.nsplit != (a.len + kAttnSplit - 1) / kAttnSplit) return hipErrorInvalidValue;
+  const bool ws = a.hd == 128 || a.hd == 64;
+  const uint32_t st = ws ? a.split_tokens : (uint32_t)kAttnSplit;
+  if ((st != 64 && st != 256) || a.nsplit != (a.len + st - 1) / st) return hipErrorInvalidValue;
   if (a.out_frag && (a.hq * a.hd) % 32) return hipErrorInvalidValue;
   const uint32_t g = a.hq / a.hkv;
   const uint32_t gg = g <= 4 ? 4 : g <= 8 ? 8 : 16;
   const dim3 grid(a.nsplit, a.hkv, a.B);
-  const size_t lds = (size_t)4 * g * (64 + a.hd) * sizeof(float);
-  if (a.hd == 128 || a.hd == 64) {
-#define OGKM_ATTN_WS(HD, L) hipLaunchKernelGGL((k_attn_decode_ws<HD, L>), grid, dim3(256), lds, s, a)
+  const uint32_t nw = st / 64;
+  const size_t lds = (size_t)nw * g * (64 + a.hd) * sizeof(float);
+  if (ws) {
+#define OGKM_ATTN_WS(HD, L, NW) hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW>), grid, dim3(64 * NW), lds, s, a)
+#define OGKM_ATTN_WS_G(HD, NW) \
+  if (gg == 4) OGKM_ATTN_WS(HD, 4, NW); else if (gg == 8) OGKM_ATTN_WS(HD, 8, NW); else OGKM_ATTN_WS(HD, 16, NW)
     if (a.hd == 128) {
-      if (gg == 4) OGKM_ATTN_WS(128, 4);
-      else if (gg == 8) OGKM_ATTN_WS(128, 8);
-      else OGKM_ATTN_WS(128, 16);
+      if (nw == 1) { OGKM_ATTN_WS_G(128, 1); } else { OGKM_ATTN_WS_G(128, 4); }
     } else {
-      if (gg == 4) OGKM_ATTN_WS(64, 4);
-      else if (gg == 8) OGKM_ATTN_WS(64, 8);
-      else OGKM_ATTN_WS(64, 16);
+      if (nw == 1) { OGKM_ATTN_WS_G(64, 1); } else { OGKM_ATTN_WS_G(64, 4); }
     }
+#undef OGKM_ATTN_WS_G
 #undef OGKM_ATTN_WS
   } else {
     hipLaunchKernelGGL(k_attn_decode, grid, dim3(256), 0, s, a);

@@ -901,14 +901,16 @@ PYBIND11_MODULE(_ogkm, m) {
      py::arg("ksplit") = 0);
   m.def("attn_decode", [](int dev, uint64_t stream, uint64_t q, uint64_t cache, uint64_t out, uint64_t part,
                           uint64_t part_bytes, uint32_t B, uint32_t hq, uint32_t hkv, uint32_t hd, uint32_t T,
-                          uint32_t len, float scale, bool out_frag) {
+                          uint32_t len, float scale, bool out_frag, uint32_t split_tokens) {
     AttnArgs a{};
     a.out_frag = out_frag ? 1 : 0;
+    const bool ws = hd == 64 || hd == 128;
+    a.split_tokens = ws && split_tokens ? split_tokens : kAttnSplitTokens;
     a.q = (const uint16_t*)q;
     a.cache = (const uint16_t*)cache;
     a.out = (uint16_t*)out;
     a.B = B; a.hq = hq; a.hkv = hkv; a.hd = hd; a.T = T; a.len = len; a.scale = scale;
-    a.nsplit = (len + kAttnSplitTokens - 1) / kAttnSplitTokens;
+    a.nsplit = (len + a.split_tokens - 1) / a.split_tokens;
     const uint64_t rows = (uint64_t)B * hq * a.nsplit;
     if (rows * (hd + 2) * 4 > part_bytes) throw StatusError("attn_decode: partial workspace too small");
     a.part_o = (float*)part;
@@ -916,7 +918,7 @@ PYBIND11_MODULE(_ogkm, m) {
     check(rt()->be()->attn_decode(dev, a, (void*)stream), "attn_decode");
   }, py::arg("dev"), py::arg("stream"), py::arg("q"), py::arg("cache"), py::arg("out"), py::arg("part"),
      py::arg("part_bytes"), py::arg("B"), py::arg("hq"), py::arg("hkv"), py::arg("hd"), py::arg("T"), py::arg("len"),
-     py::arg("scale"), py::arg("out_frag") = false);
+     py::arg("scale"), py::arg("out_frag") = false, py::arg("split_tokens") = 0);
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
     py::dict d;

@@ -219,7 +219,10 @@ class TieredLlama:
         self.fake = dry_run or lib.backend_name() == "fake"
         self.tdev = torch.device("cpu") if self.fake else torch.device("cuda", device)
         self.verbose = verbose
-        self.layout = LayerLayout.build(cfg, tp_world)
+        # Fully resident (oversub <= 1): nothing streams, so each role is one
+        # unit - one GEMM per role (a gate/up split only pays when streaming).
+        whole = oversub <= 1.0 and not os.environ.get("OGKM_UNIT_MB")
+        self.layout = LayerLayout.build(cfg, tp_world, unit_bytes=(1 << 62) if whole else None)
         hd = cfg.head_dim
         self.hq, self.hkv = cfg.n_heads // tp_world, cfg.n_kv_heads // tp_world
         self.f_local = cfg.ffn_dim // tp_world

@@ -49,9 +49,8 @@ TARGET_UNITS_PIPE = int(os.environ.get("OGKM_DGEMM_UNITS_PIPE", "768"))
 TARGET_UNITS_PIPE_LARGE = int(os.environ.get("OGKM_DGEMM_UNITS_PIPE_LARGE", "1024"))
 LARGE_ELEMS = 400 << 20
 # Pipelined raw path kernel: 0 = auto (below), 4 = k_dgemm_pipe (two register
-# sets of 2 K steps), 3 / 6 / 7 = k_dgemm_deep (register ring of that many K
-# steps), 10 D + aux = k_dgemm_lring (LDS ring of D K steps; aux 2 = non-
-# temporal weight loads).
+# sets of 2 K steps), 10 D = k_dgemm_lring (LDS ring of D K steps, D = 3..7).
+# (A register ring of 3+ sets was tried and dropped: profiles/r3_dgemm_xfrag.md.)
 DEPTH = int(os.environ.get("OGKM_DGEMM_DEPTH", "0"))
 # Auto: the LDS ring (5 slots = 20 KB of weights in flight per wave) at 512
 # waves when each wave's K range is short (<= LRING_MAX_STEPS 32-wide steps:

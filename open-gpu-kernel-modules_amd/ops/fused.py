@@ -74,12 +74,12 @@ class _Work:
 
 
 def attention(q: torch.Tensor, cache: torch.Tensor, length: int, device_index: int = 0,
-              out_frag: bool = False) -> torch.Tensor:
+              out_frag: bool = False, split_tokens: int = 0) -> torch.Tensor:
     """q [B, hq, hd] (rotated), cache [2, B, hkv, T, hd] -> [B, hq * hd] bf16 over positions [0, length)
     (``out_frag``: the decode GEMM's fragment-ordered [frag_rows(B), hq * hd] buffer)."""
     B, hq, hd = q.shape
     hkv, T = cache.shape[2], cache.shape[3]
-    nsplit = (length + 255) // 256
+    nsplit = (length + 63) // 64  # upper bound (split_tokens 64)
     need = B * hq * nsplit * (hd + 2) * 4
     key = str(q.device)
     ws = _Work.buf.get(key)
@@ -88,5 +88,6 @@ def attention(q: torch.Tensor, cache: torch.Tensor, length: int, device_index: i
         _Work.buf[key] = ws
     out = torch.empty((B + 15) // 16 * 16 if out_frag else B, hq * hd, dtype=torch.bfloat16, device=q.device)
     lib.attn_decode(device_index, _stream(q, device_index), q.data_ptr(), cache.data_ptr(), out.data_ptr(),
-                    ws.data_ptr(), ws.numel() * 4, B, hq, hkv, hd, T, length, 1.0 / math.sqrt(hd), out_frag)
+                    ws.data_ptr(), ws.numel() * 4, B, hq, hkv, hd, T, length, 1.0 / math.sqrt(hd), out_frag,
+                    split_tokens)
     return out

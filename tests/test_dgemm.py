@@ -118,11 +118,11 @@ def test_dgemm_gpu_numerics(gpu_rt, packed, epi, m, n, wg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("depth", [3, 6, 7, 30, 40, 42, 50, 70])
+@pytest.mark.parametrize("depth", [30, 40, 50, 70])
 @pytest.mark.parametrize("n,k,m", [(320, 1024, 64), (336, 2048, 7), (4096, 4096, 64), (64, 96, 80)])
 def test_dgemm_gpu_pipeline_depths_bit_identical(gpu_rt, depth, n, k, m):
-    """The deeper pipelines (k_dgemm_deep register rings, k_dgemm_lring LDS
-    rings with hand-counted vmcnt) sum the K steps in k_dgemm_pipe's order:
+    """The LDS-ring pipelines (k_dgemm_lring, hand-counted vmcnt) sum the K
+    steps in k_dgemm_pipe's order:
     partials and outputs must be bit-identical to it, for K ranges shorter and
     longer than the ring, and they must match the fp32 reference."""
     w = _weights(n, k, 9, specials=False)
@@ -206,5 +206,5 @@ def test_dgemm_gpu_bandwidth_70b_shapes(gpu_rt, packed):
         del buf
     print(f"dgemm {'bf11' if packed else 'bf16'} layer total: {total_t*1e3:.3f} ms ({total_bytes/total_t/1e9:.0f} GB/s)")
     # ~90 % of the measured rates (profiles/r3_dgemm_xfrag.md: raw 4.9 TB/s on
-    # MALL-cold weights; the in-register BF11 decode ~0.8 TB/s of packed bytes)
-    assert total_bytes / total_t > (0.7e12 if packed else 4.3e12)
+    # MALL-cold weights, 4.94 in this test; the in-register BF11 decode 0.88 TB/s)
+    assert total_bytes / total_t > (0.78e12 if packed else 4.3e12)

@@ -43,13 +43,13 @@ def _check_rope_kv(gpu):
     assert cd[:, :, :, pos + 1:].abs().sum() == 0 and cd[:, :, :, :pos].abs().sum() == 0
 
 
-def _check_attention(gpu, length, hq=16, hkv=2, hd=128):
+def _check_attention(gpu, length, hq=16, hkv=2, hd=128, split_tokens=0):
     B, T = 2, 700
     q = torch.randn(B, hq, hd).to(torch.bfloat16)
     cache = torch.randn(2, B, hkv, T, hd).to(torch.bfloat16)
     want = D.gqa_decode_attention(q.float(), cache[0].float(), cache[1].float(), length)
     dv = _dev(gpu)
-    got = fused.attention(q.to(dv), cache.to(dv), length)
+    got = fused.attention(q.to(dv), cache.to(dv), length, split_tokens=split_tokens)
     torch.testing.assert_close(got.float().cpu(), want, atol=2e-2, rtol=2e-2)
 
 
@@ -201,9 +201,12 @@ def test_attention_one_kv_head_gpu(gpu_rt, hq, hkv, length):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (16, 4, 64), (8, 1, 64), (4, 4, 128), (12, 2, 128)])
-@pytest.mark.parametrize("length", [1, 63, 65, 700])
-def test_attention_group_shapes_gpu(gpu_rt, hq, hkv, hd, length):
+@pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (16, 4, 64), (8, 1, 64), (4, 4, 128), (12, 2, 128), (16, 1, 128)])
+@pytest.mark.parametrize("length", [1, 63, 64, 65, 700])
+@pytest.mark.parametrize("split_tokens", [64, 256])
+def test_attention_group_shapes_gpu(gpu_rt, hq, hkv, hd, length, split_tokens):
     """Every group-size / head-dim instantiation of the wave-split kernel
-    (group 1..16 rounded up to 4 / 8 / 16, hd 64 / 128), partial waves included."""
-    _check_attention(True, length, hq, hkv, hd)
+    (group 1..16 rounded up to 4 / 8 / 16, hd 64 / 128), partial waves included,
+    in both workgroup shapes: 256-token four-wave splits and 64-token one-wave
+    splits (an explicit option; measured slower at the bench shapes, profiles/r3_attn_split.txt)."""
+    _check_attention(True, length, hq, hkv, hd, split_tokens)

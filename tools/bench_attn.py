@@ -26,20 +26,26 @@ def main() -> None:
     for name, (B, hq, hkv, hd, L) in SHAPES.items():
         T = L
         q = torch.randn(B, hq, hd, device="cuda").to(torch.bfloat16)
-        cache = torch.randn(2, B, hkv, T, hd, device="cuda").to(torch.bfloat16)
-        for _ in range(3):
-            fused.attention(q, cache, L)
+        # MALL-cold: rotate over >= 1 GB of caches (a decode step reads every
+        # layer's KV once; one layer's KV re-read would sit in the 256 MB MALL)
+        kvb = 2 * B * hkv * T * hd * 2
+        ncopy = max(1, -(-(1 << 30) // kvb)) if int(os.environ.get("COLD", "1")) else 1
+        caches = [torch.randn(2, B, hkv, T, hd, device="cuda").to(torch.bfloat16) for _ in range(ncopy)]
+        st = int(os.environ.get("SPLIT", "0"))
+        for i in range(3):
+            fused.attention(q, caches[i % ncopy], L, split_tokens=st)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(iters):
-            fused.attention(q, cache, L)
+        for i in range(iters):
+            fused.attention(q, caches[i % ncopy], L, split_tokens=st)
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / iters
         gb = 2 * B * hkv * L * hd * 2 / 1e9
         print(f"{name:9s} B={B} hq={hq} hkv={hkv} hd={hd} len={L} {us:8.1f} us  "
-              f"KV {gb * 1e3:7.1f} MB  {gb / (us * 1e-6):7.0f} GB/s", flush=True)
+              f"KV {gb * 1e3:7.1f} MB  {gb / (us * 1e-6):7.0f} GB/s  split {st or 'auto'}", flush=True)
+        del caches
 
 
 if __name__ == "__main__":

@@ -74,7 +74,7 @@ def main():
         dgemm.UNROLL = 0 if kind == "pipe" else u
         dgemm.PIPE = 1 if kind == "pipe" else 0
         # "pipe:D": the pipelined raw path at DEPTH D (0 = auto, 4 = k_dgemm_pipe,
-        # 3/6/7 = k_dgemm_deep, 10 x slots (+2 nt) = the LDS-ring k_dgemm_lring)
+        # 10 x slots = the LDS-ring k_dgemm_lring)
         dgemm.DEPTH = u if kind == "pipe" else 4
         tot_t, tot_b, per = 0.0, 0, {}
         for (n, k), (flat, pk, info, mode) in ws.items():
