@@ -95,6 +95,7 @@ struct ResidNormArgs {
   float eps;
   uint32_t y_frag;
 };
+constexpr uint32_t kNormCols = 1024;  // RMSNorm columns per pass of a 256-thread workgroup (4 per thread)
 struct AttnArgs {
   const uint16_t* q;       // [B, hq, hd] (rotated)
   const uint16_t* cache;   // [2][B][hkv][T][hd]

@@ -36,110 +36,106 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // ---------------------------------------------------------------- RMSNorm (+ deferred residual GEMM epilogue)
-// One 256-thread workgroup per row; thread t owns columns 4t + 1024 j (16-byte
-// f32x4 partial loads, 8-byte bf16 loads/stores), its <= 16 groups held in
-// registers between the residual update, the sum of squares and the scaling.
-// With a.part set, the row first takes the deferred decode GEMM's RESID
-// epilogue: x = bf16(bf16(sum_k part[k]) + x), summed k ascending like
-// k_dgemm_reduce, so the fused and the separate path give identical bits -
-// and one launch (this one) replaces the reduce + the norm.
-constexpr uint32_t kNormMaxGroups = 16;  // dim <= 16384
-
-// Residual update of G column groups (4 columns each) of one row from the
-// deferred split-K partials: loads issued KB splits x G groups at a time (the
-// k loop is latency-bound otherwise: one dependent L2/MALL round trip per
-// split), summed k ascending per column like k_dgemm_reduce.
-template <int G, int KB>
-__device__ __forceinline__ void norm_resid_groups(const ResidNormArgs& a, uint32_t row, uint32_t t, uint16_t* xr,
-                                                  float (&v)[kNormMaxGroups][4]) {
-  float4 sum[G];
+// One 256-thread workgroup per row; thread t owns columns 4t + 1024 j of its G
+// column groups (16-byte f32x4 partial loads, 8-byte bf16 loads/stores). With
+// a.part set, the row first takes the deferred decode GEMM's RESID epilogue:
+// x = bf16(bf16(sum_k part[k]) + x), summed k ascending like k_dgemm_reduce, so
+// the fused and the separate path give identical bits - and one launch (this
+// one) replaces the reduce + the norm. Every load is unconditional (clamped
+// index, predicated use) and a batch of them is issued before the first use:
+// a per-element load-or-zero select makes the compiler wait vmcnt(0) per
+// element (one dependent round trip each). (A multi-workgroup form - one
+// workgroup per 1024 columns, the row's last arriver normalising - measured
+// slower: 11.2 vs 9.5 us, the release/acquire hand-off costs more than it
+// spreads.)
+__device__ __forceinline__ void norm_store4(const ResidNormArgs& a, uint32_t row, uint32_t c, const float (&x4)[4],
+                                            uint2 wp, float r) {
+  const float w4[4] = {dbf((uint16_t)wp.x), dbf((uint16_t)(wp.x >> 16)), dbf((uint16_t)wp.y),
+                       dbf((uint16_t)(wp.y >> 16))};
+  uint16_t o[4];
 #pragma unroll
-  for (int j = 0; j < G; ++j) sum[j] = float4{0.f, 0.f, 0.f, 0.f};
-  for (uint32_t k0 = 0; k0 < a.ksplit; k0 += KB) {
-    float4 q[KB][G];
-#pragma unroll
-    for (int kk = 0; kk < KB; ++kk)
-#pragma unroll
-      for (int j = 0; j < G; ++j) {
-        const uint32_t c = 4 * t + 1024 * j;
-        q[kk][j] = (k0 + kk < a.ksplit && c < a.dim)
-                       ? *reinterpret_cast<const float4*>(a.part + ((uint64_t)(k0 + kk) * a.rows + row) * a.dim + c)
-                       : float4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-    for (int kk = 0; kk < KB; ++kk)
-#pragma unroll
-      for (int j = 0; j < G; ++j)
-        if (k0 + kk < a.ksplit) {
-          sum[j].x += q[kk][j].x; sum[j].y += q[kk][j].y; sum[j].z += q[kk][j].z; sum[j].w += q[kk][j].w;
-        }
-  }
-#pragma unroll
-  for (int j = 0; j < G; ++j) {
-    const uint32_t c = 4 * t + 1024 * j;
-    if (c >= a.dim) break;
-    const float s4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
-    uint16_t o[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      o[e] = df2bf(dbf(df2bf(s4[e])) + v[j][e]);
-      v[j][e] = dbf(o[e]);
-    }
-    *reinterpret_cast<uint2*>(xr + c) =
-        uint2{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
-  }
+  for (int e = 0; e < 4; ++e) o[e] = df2bf(dbf(df2bf(x4[e] * r)) * w4[e]);
+  uint16_t* dst = a.y_frag ? a.y + frag_index(row, c, a.dim) : a.y + (uint64_t)row * a.ldy + c;
+  *reinterpret_cast<uint2*>(dst) =
+      uint2{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
 }
 
+template <int G>
 __global__ void __launch_bounds__(256) k_rmsnorm(ResidNormArgs a) {
   __shared__ float red[4];
   const uint32_t row = blockIdx.x, t = threadIdx.x;
   uint16_t* xr = a.x + (uint64_t)row * a.ldx;
-  uint16_t* yr = a.y + (uint64_t)row * a.ldy;
-  float v[kNormMaxGroups][4];
+  uint32_t cl[G];  // clamped column of each group (loads); c < dim gates the use
+  bool on[G];
+  uint2 xp[G], wp[G];
 #pragma unroll
-  for (uint32_t j = 0; j < kNormMaxGroups; ++j) {
-    const uint32_t c = 4 * t + 1024 * j;
-    if (c >= a.dim) break;
-    const uint2 p = *reinterpret_cast<const uint2*>(xr + c);
-    v[j][0] = dbf((uint16_t)p.x);
-    v[j][1] = dbf((uint16_t)(p.x >> 16));
-    v[j][2] = dbf((uint16_t)p.y);
-    v[j][3] = dbf((uint16_t)(p.y >> 16));
+  for (int j = 0; j < G; ++j) {
+    const uint32_t c = 4 * t + kNormCols * j;
+    on[j] = c < a.dim;
+    cl[j] = on[j] ? c : a.dim - 4;
+    xp[j] = *reinterpret_cast<const uint2*>(xr + cl[j]);
+    wp[j] = *reinterpret_cast<const uint2*>(a.w + cl[j]);
+  }
+  float v[G][4];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    v[j][0] = dbf((uint16_t)xp[j].x);
+    v[j][1] = dbf((uint16_t)(xp[j].x >> 16));
+    v[j][2] = dbf((uint16_t)xp[j].y);
+    v[j][3] = dbf((uint16_t)(xp[j].y >> 16));
   }
   if (a.part) {
-    if (a.dim <= 4096)
-      norm_resid_groups<4, 8>(a, row, t, xr, v);
-    else if (a.dim <= 8192)
-      norm_resid_groups<8, 4>(a, row, t, xr, v);
-    else
-      norm_resid_groups<16, 2>(a, row, t, xr, v);
+    constexpr uint32_t KB = G <= 4 ? 8 : G <= 8 ? 4 : 2;  // splits per batch: KB x G loads in flight
+    float4 sum[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) sum[j] = float4{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t k0 = 0; k0 < a.ksplit; k0 += KB) {
+      float4 pv[KB][G];
+#pragma unroll
+      for (uint32_t kk = 0; kk < KB; ++kk) {
+        const uint32_t k = k0 + kk < a.ksplit ? k0 + kk : a.ksplit - 1;
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+          pv[kk][j] = *reinterpret_cast<const float4*>(a.part + ((uint64_t)k * a.rows + row) * a.dim + cl[j]);
+      }
+#pragma unroll
+      for (uint32_t kk = 0; kk < KB; ++kk) {
+        const bool in = k0 + kk < a.ksplit;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          sum[j].x = in ? sum[j].x + pv[kk][j].x : sum[j].x;
+          sum[j].y = in ? sum[j].y + pv[kk][j].y : sum[j].y;
+          sum[j].z = in ? sum[j].z + pv[kk][j].z : sum[j].z;
+          sum[j].w = in ? sum[j].w + pv[kk][j].w : sum[j].w;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const float s4[4] = {sum[j].x, sum[j].y, sum[j].z, sum[j].w};
+      uint16_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = df2bf(dbf(df2bf(s4[e])) + v[j][e]);
+        v[j][e] = dbf(o[e]);
+      }
+      if (on[j])
+        *reinterpret_cast<uint2*>(xr + cl[j]) =
+            uint2{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
+    }
   }
   float ss = 0.f;
 #pragma unroll
-  for (uint32_t j = 0; j < kNormMaxGroups; ++j) {
-    const uint32_t c = 4 * t + 1024 * j;
-    if (c >= a.dim) break;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) ss += v[j][e] * v[j][e];
-  }
+  for (int j = 0; j < G; ++j)
+    ss = on[j] ? ss + v[j][0] * v[j][0] + v[j][1] * v[j][1] + v[j][2] * v[j][2] + v[j][3] * v[j][3] : ss;
   ss = wave_sum(ss);
   if ((t & 63) == 0) red[t >> 6] = ss;
   __syncthreads();
   const float tot = red[0] + red[1] + red[2] + red[3];
   const float r = rsqrtf(tot / (float)a.dim + a.eps);
 #pragma unroll
-  for (uint32_t j = 0; j < kNormMaxGroups; ++j) {
-    const uint32_t c = 4 * t + 1024 * j;
-    if (c >= a.dim) break;
-    const uint2 q = *reinterpret_cast<const uint2*>(a.w + c);
-    const float wv[4] = {dbf((uint16_t)q.x), dbf((uint16_t)(q.x >> 16)), dbf((uint16_t)q.y), dbf((uint16_t)(q.y >> 16))};
-    uint16_t o[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = df2bf(dbf(df2bf(v[j][e] * r)) * wv[e]);
-    uint16_t* dst = a.y_frag ? a.y + frag_index(row, c, a.dim) : yr + c;
-    *reinterpret_cast<uint2*>(dst) =
-        uint2{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
-  }
+  for (int j = 0; j < G; ++j)
+    if (on[j]) norm_store4(a, row, cl[j], v[j], wp[j], r);
 }
 
 // ---------------------------------------------------------------- RoPE + KV append
@@ -161,18 +157,18 @@ __global__ void __launch_bounds__(256) k_rope_kv(RopeKvArgs a) {
     for (uint32_t k0 = 0; k0 < a.ksplit; k0 += kB) {
       float p1[kB], p2[kB];
 #pragma unroll
-      for (uint32_t kk = 0; kk < kB; ++kk) {
-        const bool ok = k0 + kk < a.ksplit;
-        const float* row = a.part + ((uint64_t)(ok ? k0 + kk : 0) * a.B + b) * n;
-        p1[kk] = ok ? row[c1] : 0.f;
-        p2[kk] = ok ? row[c1 + half] : 0.f;
+      for (uint32_t kk = 0; kk < kB; ++kk) {  // unconditional (clamped) loads, predicated adds
+        const uint32_t k = k0 + kk < a.ksplit ? k0 + kk : a.ksplit - 1;
+        const float* row = a.part + ((uint64_t)k * a.B + b) * n;
+        p1[kk] = row[c1];
+        p2[kk] = row[c1 + half];
       }
 #pragma unroll
-      for (uint32_t kk = 0; kk < kB; ++kk)
-        if (k0 + kk < a.ksplit) {
-          s1 += p1[kk];
-          s2 += p2[kk];
-        }
+      for (uint32_t kk = 0; kk < kB; ++kk) {
+        const bool in = k0 + kk < a.ksplit;
+        s1 = in ? s1 + p1[kk] : s1;
+        s2 = in ? s2 + p2[kk] : s2;
+      }
     }
     x1 = dbf(df2bf(s1));
     x2 = dbf(df2bf(s2));
@@ -507,10 +503,17 @@ __global__ void k_attn_combine(AttnArgs a) {
 }
 
 hipError_t launch_rmsnorm(const ResidNormArgs& a, hipStream_t s) {
-  if (a.dim % 4 || a.dim > 1024 * kNormMaxGroups || a.ldx % 4 || a.ldy % 4 || (a.y_frag && a.dim % 32))
+  if (a.dim % 4 || a.dim < 4 || a.dim > 16 * kNormCols || a.ldx % 4 || a.ldy % 4 || (a.y_frag && a.dim % 32))
     return hipErrorInvalidValue;
   if (!a.rows) return hipSuccess;
-  hipLaunchKernelGGL(k_rmsnorm, dim3(a.rows), dim3(256), 0, s, a);
+  if (a.dim <= kNormCols)
+    hipLaunchKernelGGL((k_rmsnorm<1>), dim3(a.rows), dim3(256), 0, s, a);
+  else if (a.dim <= 4 * kNormCols)
+    hipLaunchKernelGGL((k_rmsnorm<4>), dim3(a.rows), dim3(256), 0, s, a);
+  else if (a.dim <= 8 * kNormCols)
+    hipLaunchKernelGGL((k_rmsnorm<8>), dim3(a.rows), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_rmsnorm<16>), dim3(a.rows), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -879,7 +879,8 @@ PYBIND11_MODULE(_ogkm, m) {
   // Fused decode-step ops (ops/fused.py).
   m.def("rmsnorm", [](int dev, uint64_t stream, uint64_t x, uint64_t w, uint64_t y, uint32_t rows, uint32_t dim,
                       uint32_t ldx, uint32_t ldy, float eps, uint64_t part, uint32_t ksplit, bool y_frag) {
-    if (dim % 4 || dim > 16384 || ldx % 4 || ldy % 4) throw StatusError("rmsnorm: dim % 4, dim <= 16384, ld % 4");
+    if (dim % 4 || dim < 4 || dim > 16384 || ldx % 4 || ldy % 4)
+      throw StatusError("rmsnorm: dim % 4, 4 <= dim <= 16384, ld % 4");
     if (y_frag && dim % 32) throw StatusError("rmsnorm: fragment-ordered output needs dim % 32 == 0");
     ResidNormArgs a{(const float*)part, ksplit, (uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, rows, dim, ldx, ldy,
                     eps, y_frag ? 1u : 0u};

@@ -16,9 +16,9 @@ def _dev(gpu):
     return "cuda" if gpu else "cpu"
 
 
-def _check_rmsnorm(gpu):
-    x = (torch.randn(5, 1024) * 3).to(torch.bfloat16)
-    w = (torch.rand(1024) + 0.5).to(torch.bfloat16)
+def _check_rmsnorm(gpu, dim=1024):
+    x = (torch.randn(5, dim) * 3).to(torch.bfloat16)
+    w = (torch.rand(dim) + 0.5).to(torch.bfloat16)
     want = D.rms_norm(x.float(), w.float(), 1e-5)
     got = fused.rms_norm(x.to(_dev(gpu)), w.to(_dev(gpu)), 1e-5)
     torch.testing.assert_close(got.float().cpu(), want, atol=2e-2, rtol=2e-2)
@@ -53,14 +53,14 @@ def _check_attention(gpu, length, hq=16, hkv=2, hd=128, split_tokens=0):
     torch.testing.assert_close(got.float().cpu(), want, atol=2e-2, rtol=2e-2)
 
 
-def _check_deferred_epilogues(gpu):
+def _check_deferred_epilogues(gpu, d=1024):
     """dgemm.linear(defer=True) + the consumer's fused epilogue == the separate
     reduce launch, bit for bit: residual add + RMSNorm (o / down projections)
     and the qkv store epilogue inside RoPE + KV append; a later linear() call
     invalidates the deferred partials (loud error, not stale data)."""
     from ogkm.ops import dgemm
     dv = _dev(gpu)
-    m, d, k = 7, 1024, 2048
+    m, k = 7, 2048
     g = torch.Generator().manual_seed(11)
     wt = (torch.randn(d, k, generator=g) * 0.02).to(torch.bfloat16)
     wbuf = dgemm.frag_permute(wt).contiguous().to(dv)
@@ -152,8 +152,9 @@ def test_deferred_epilogues_cpu(fake_rt):
 
 
 @pytest.mark.gpu
-def test_deferred_epilogues_gpu(gpu_rt):
-    _check_deferred_epilogues(True)
+@pytest.mark.parametrize("d", [1024, 4096, 8192])
+def test_deferred_epilogues_gpu(gpu_rt, d):
+    _check_deferred_epilogues(True, d)
 
 
 def test_rmsnorm_cpu(fake_rt):
@@ -170,8 +171,11 @@ def test_attention_cpu(fake_rt, length):
 
 
 @pytest.mark.gpu
-def test_rmsnorm_gpu(gpu_rt):
-    _check_rmsnorm(True)
+@pytest.mark.parametrize("dim", [512, 1024, 2048, 4096, 5120, 8192, 16384])
+def test_rmsnorm_gpu(gpu_rt, dim):
+    """One workgroup per row (dim <= 1024) and the multi-workgroup form (one per
+    1024 columns, the row's last arriver normalises), ragged last quarter (5120)."""
+    _check_rmsnorm(True, dim)
 
 
 @pytest.mark.gpu
