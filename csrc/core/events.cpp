@@ -139,7 +139,8 @@ const char* counter_name(Counter c) {
                             "vmm_remaps",
                             "vmm_errors",
                             "tlb_flushes",
-                            "faults_cancelled"};
+                            "faults_cancelled",
+                            "tlb_flushes_elided"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

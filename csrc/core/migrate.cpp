@@ -575,7 +575,7 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
     if (b->range->dev_va) stable_map_block(b);
   }
   // A caller that remaps several groups flushes once at its end (place_stable).
-  if (!c.defer_flush && tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
+  if (!c.defer_flush && (thread_tlb_need() || tlb_dirty_.load(std::memory_order_relaxed))) flush_translations();
   // The context is spent; what the caller still needs for its retry (the
   // arena to evict from on MORE_PROCESSING_REQUIRED) survives the reset.
   ChunkArena* need_arena = c.need_arena;
@@ -1048,7 +1048,7 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
       std::lock_guard<OrderedMutex> g(b->lock);
       stable_map_block(b);
     }
-    if (tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
+    if (thread_tlb_need() || tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
   }
   if (st != Status::OK) {
     if (L) {
@@ -1228,7 +1228,7 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
   for (uint32_t ch : kept) ga->unpin(ch);
   // Blocks whose chunk did not change since they were last mapped are already
   // right; every other one was remapped above: one flush before any use.
-  if (tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
+  if (thread_tlb_need() || tlb_dirty_.load(std::memory_order_relaxed)) flush_translations();
   if (st != Status::OK) {
     if (L) {
       for (auto& pc : L->pinned_chunks) pc.first->unpin(pc.second);

@@ -290,9 +290,11 @@ Status Runtime::free_range(Range* r) {
     Block* b = bp.get();
     std::lock_guard<OrderedMutex> g(b->lock);
     b->tracker.wait();
-    if (r->dev_va && b->stable_chunk.load() >= 0) {
+    if (r->dev_va && (b->stable_chunk.load() >= 0 || b->stale_mapping)) {
       std::lock_guard<std::mutex> sg(stable_m_);
       stable_unmap_locked(b);  // after the kernels still reading through the mapping
+      if (!stale_maps_.empty())
+        stale_maps_.erase(std::remove(stale_maps_.begin(), stale_maps_.end(), b), stale_maps_.end());
     }
     for (auto& x : b->res)
       if (x.chunk >= 0) x.arena->free((uint32_t)x.chunk, 1);
@@ -505,6 +507,26 @@ void Runtime::stable_unmap_locked(Block* b) {
            (unsigned long long)b->index, be_->last_error().c_str());
   }
   b->stable_chunk.store(-1);
+  b->va_unmap_seq = tlb_started_[r->stable_dev].load();
+  b->stale_mapping = false;  // its stale_maps_ entry is dropped by the next reap
+}
+
+void Runtime::reap_stale_maps_locked() {
+  size_t w = 0;
+  for (Block* b : stale_maps_) {
+    if (!b->stale_mapping) continue;  // remapped / unmapped meanwhile: drop the entry
+    if (config().stable_lazy_unmap || !b->stable_users.query()) {
+      stale_maps_[w++] = b;  // users still running (or lazy mode): keep
+      continue;
+    }
+    stable_unmap_locked(b);
+  }
+  stale_maps_.resize(w);
+}
+
+uint32_t& Runtime::thread_tlb_need() {
+  static thread_local uint32_t need = 0;
+  return need;
 }
 
 // Point block b's stable VA at its HBM chunk (block lock held). A mapping is
@@ -520,16 +542,26 @@ void Runtime::stable_map_block(Block* b) {
   TraceRange tr(be_.get(), "ogkm:stable_map", 2);
   Residency* g = b->find(Loc::gpu(r->stable_dev));
   const int64_t want = (g && g->chunk >= 0) ? g->chunk : -1;
-  if (want == b->stable_chunk.load()) return;
+  if (want == b->stable_chunk.load() && !b->stale_mapping) return;
   std::lock_guard<std::mutex> sg(stable_m_);
-  if (want == b->stable_chunk.load()) return;
+  if (want == b->stable_chunk.load()) {  // back on the chunk it still maps: valid again
+    b->stale_mapping = false;
+    return;
+  }
   if (want < 0) {
     // Evicted: kernels enqueued before the last lease release may still read
     // the VA. Unmap at once only when they are done (and not in lazy mode);
     // otherwise the stale mapping stays - a stray access then reads whatever
-    // the chunk holds instead of faulting.
+    // the chunk holds instead of faulting - and the reaper tears it down
+    // before a later flush once they are.
     b->stable_users.merge(b->tracker);
-    if (config().stable_lazy_unmap || !b->stable_users.query()) return;
+    if (config().stable_lazy_unmap || !b->stable_users.query()) {
+      if (b->stable_chunk.load() >= 0 && !b->stale_mapping) {
+        b->stale_mapping = true;
+        stale_maps_.push_back(b);
+      }
+      return;
+    }
     stable_unmap_locked(b);
     return;
   }
@@ -539,7 +571,15 @@ void Runtime::stable_map_block(Block* b) {
   Tools::get().inc(Counter::VmmRemaps);
   if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) {
     b->stable_chunk.store(want);
-    tlb_dirty_.fetch_or(1u << r->stable_dev);
+    // A translation of this VA can still sit in the GPU's TLB only if no
+    // flush begun after its last unmap has completed; otherwise (the common
+    // case of a block evicted a while ago) the new mapping needs no flush.
+    if (b->va_unmap_seq == ~0ull || tlb_done_[r->stable_dev].load() <= b->va_unmap_seq) {
+      thread_tlb_need() |= 1u << r->stable_dev;
+      tlb_dirty_.fetch_or(1u << r->stable_dev);
+    } else {
+      Tools::get().inc(Counter::TlbFlushesElided);
+    }
   } else {
     Tools::get().inc(Counter::VmmErrors);
     RT_ERR("stable VA map of range %llu block %llu to chunk %lld failed: %s", (unsigned long long)r->id,
@@ -590,14 +630,24 @@ std::string Runtime::describe_device_address(uint64_t va) {
 }
 
 void Runtime::flush_translations() {
-  uint32_t m = tlb_dirty_.exchange(0);
+  {
+    // stale mappings whose users finished go now, so this flush covers them
+    std::lock_guard<std::mutex> sg(stable_m_);
+    if (!stale_maps_.empty()) reap_stale_maps_locked();
+  }
+  uint32_t m = tlb_dirty_.exchange(0) | thread_tlb_need();
+  thread_tlb_need() = 0;
   for (int d = 0; m; ++d, m >>= 1) {
     if (!(m & 1)) continue;
+    const uint64_t k = tlb_started_[d].fetch_add(1) + 1;  // covers every unmap before this point
     if (be_->tlb_flush(d) != Status::OK) {
       Tools::get().inc(Counter::VmmErrors);
       RT_ERR("GPU %d translation flush after stable-VA remaps failed: %s", d, be_->last_error().c_str());
     } else {
       Tools::get().inc(Counter::TlbFlushes);
+      uint64_t cur = tlb_done_[d].load();
+      while (cur < k && !tlb_done_[d].compare_exchange_weak(cur, k)) {
+      }
     }
   }
 }

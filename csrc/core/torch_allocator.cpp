@@ -34,6 +34,7 @@
 // The C entry points ogkm_torch_alloc / ogkm_torch_free are what
 // CUDAPluggableAllocator dlsym()s.
 #include <cstdlib>
+#include <deque>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -85,6 +86,13 @@ struct DevAlloc {
   };
   std::unordered_map<uint64_t, Managed> managed;   // stable VA -> range
   std::vector<std::pair<Range*, Tracker>> deferred;  // freed, waiting for their stream fence
+  // Freed managed ranges kept for reuse by an allocation of the same size
+  // (oldest first): the range keeps its stable VA, its blocks their chunks
+  // and mappings, so a reuse costs no VA reservation, no remap and no
+  // translation flush. Bounded by torch_alloc_cache_mb; the oldest go to
+  // `deferred` beyond it. The fence orders the next owner after the last uses.
+  std::deque<std::pair<Range*, Tracker>> cache;
+  uint64_t cache_bytes = 0, cache_hits = 0;
   uint64_t allocated = 0, peak = 0, nallocs = 0, stream_waits = 0;
   uint64_t managed_bytes = 0, parks = 0, unparks = 0, op_holds = 0;
   uint64_t op_seq = 0;  // dispatched ops that held managed operands (the persistence clock)
@@ -166,10 +174,22 @@ Status lease_on(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, voi
 void* managed_alloc(Runtime* rt, DevAlloc* da, size_t size, int device, void* stream) {
   Range* r = nullptr;
   uint64_t bytes = align_up((uint64_t)size, kBlockSize);
-  if (rt->malloc_managed(bytes, RANGE_STABLE_VA | RANGE_NO_CPU_VIEW | RANGE_NO_ZERO_FILL, "torch", &r, device) !=
-      Status::OK)
-    return nullptr;
-  rt->mem_advise(r, 0, bytes, Advice::SET_PREFERRED_LOCATION, Loc::gpu(device), device);
+  // newest cached range of this size first (likeliest still resident)
+  for (size_t i = da->cache.size(); i-- > 0;) {
+    if (da->cache[i].first->size != bytes) continue;
+    r = da->cache[i].first;
+    order_after(rt, da, da->cache[i].second, stream);
+    da->cache_bytes -= bytes;
+    da->cache.erase(da->cache.begin() + (ptrdiff_t)i);
+    da->cache_hits++;
+    break;
+  }
+  if (!r) {
+    if (rt->malloc_managed(bytes, RANGE_STABLE_VA | RANGE_NO_CPU_VIEW | RANGE_NO_ZERO_FILL, "torch", &r, device) !=
+        Status::OK)
+      return nullptr;
+    rt->mem_advise(r, 0, bytes, Advice::SET_PREFERRED_LOCATION, Loc::gpu(device), device);
+  }
   DevAlloc::Managed m{r, nullptr, bytes};
   m.holds = 1;
   m.alloc_hold = true;
@@ -190,6 +210,9 @@ void* managed_alloc(Runtime* rt, DevAlloc* da, size_t size, int device, void* st
 // for the streams that last used them) - the caching-allocator move of freeing
 // its cache and synchronizing before reporting OOM. da->m held.
 static bool drain_deferred(Runtime* rt, DevAlloc* da) {
+  for (auto& c : da->cache) da->deferred.push_back(std::move(c));
+  da->cache.clear();
+  da->cache_bytes = 0;
   if (da->deferred.empty()) return false;
   for (auto& d : da->deferred) {
     (void)d.second.wait();
@@ -292,7 +315,18 @@ void torch_free(void* p, int device, void* stream) {
     if (m.lease) rt->release(m.lease, stream);
     Tracker t;
     if (f) t.add(f);
-    da->deferred.emplace_back(m.r, std::move(t));
+    const uint64_t cap = (uint64_t)std::max<int64_t>(0, config().torch_alloc_cache_mb) << 20;
+    if (m.size <= cap) {
+      da->cache.emplace_back(m.r, std::move(t));
+      da->cache_bytes += m.size;
+      while (da->cache_bytes > cap) {  // the oldest leave the cache: freed once their uses completed
+        da->cache_bytes -= da->cache.front().first->size;
+        da->deferred.push_back(std::move(da->cache.front()));
+        da->cache.pop_front();
+      }
+    } else {
+      da->deferred.emplace_back(m.r, std::move(t));
+    }
     reap_deferred(rt, da);
     return;
   }

@@ -183,6 +183,7 @@ enum class Counter : int {
   VmmErrors,        // failed stable-VA unmaps / maps / translation flushes
   TlbFlushes,       // GPU translation flushes after stable-VA remaps
   FaultsCancelled,  // channels whose device faults were cancelled (precise cancel)
+  TlbFlushesElided, // stable-VA maps that needed no flush (a flush since the VA's last unmap covered it)
   NumCounters
 };
 const char* counter_name(Counter c);

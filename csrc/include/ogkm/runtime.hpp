@@ -301,6 +301,20 @@ class Runtime {
   void flush_translations();
   std::string describe_device_address(uint64_t va);  // for GPU memory-fault reports
   std::atomic<uint32_t> tlb_dirty_{0};  // bit d: device d has remapped stable VAs
+  // Translation-flush sequence per device: started (numbered at their start)
+  // and the highest completed. A VA unmapped when tlb_started_ was S is
+  // covered once tlb_done_ > S (a flush begun after the unmap finished).
+  std::atomic<uint64_t> tlb_started_[kMaxGpus] = {};
+  std::atomic<uint64_t> tlb_done_[kMaxGpus] = {};
+  // The calling thread's remaps that still need a covering flush (per device
+  // bit): another thread clearing tlb_dirty_ does not release them (its flush
+  // may still be running).
+  static uint32_t& thread_tlb_need();
+  // Blocks with a stale stable-VA mapping (Block::stale_mapping), guarded by
+  // stable_m_: torn down before each translation flush once their users are
+  // done, so that flush covers the unmap and the block's next remap needs none.
+  std::vector<Block*> stale_maps_;
+  void reap_stale_maps_locked();
   Status finish_ctx(Ctx& c, Tracker* out);
   void drop_copy(Ctx& c, Block* b, const Loc& l);  // release a residency (block lock held)
   void touch_residency(Block* b, Residency* r, bool prefetched = false);  // LRU bump (preferred / prefetch aware)

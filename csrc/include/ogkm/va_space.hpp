@@ -100,6 +100,14 @@ class Block {
   // the mapping is torn down only once it completed (a kernel queued before the
   // release would otherwise fault on an unmapped VA). Guarded by Runtime::stable_m_.
   Tracker stable_users;
+  // Value of Runtime::tlb_started_ when the stable VA was last unmapped (~0:
+  // unknown - a fresh block): a translation of the VA can linger in a GPU TLB
+  // until a flush that started after that unmap has completed, so a remap
+  // needs a flush only then (Runtime::stable_map_block). Guarded by stable_m_.
+  uint64_t va_unmap_seq = ~0ull;
+  // The stable VA still maps a chunk the block left (its users were running at
+  // the eviction): listed in Runtime::stale_maps_ until the mapping goes.
+  std::atomic<bool> stale_mapping{false};
   uint32_t lease_pins = 0;
   uint32_t gpu_evictions = 0;  // times an HBM copy of this block was evicted (refault detection)
   uint64_t gpu_evicted_at = 0; // the HBM arena's eviction count when it last was (refault distance)

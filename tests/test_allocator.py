@@ -209,3 +209,31 @@ def test_stable_placement_batches_evictions(managed_rt, lazy):
     finally:
         lib.configure("stable_lazy_unmap", 0)
         lib.configure("stable_batch_blocks", 32)
+
+
+def test_cyclic_remaps_elide_covered_flushes(managed_rt):
+    """Cycling 6 x 8 MB tensors through a 32 MB arena: a block that comes back
+    long after its eviction (a flush begun after its unmap has completed) is
+    mapped without another translation flush; one that returns right away is
+    flushed. Data stays right on every pass."""
+    n = 8 * MB
+    ptrs = []
+    for i in range(6):
+        p = lib.torch_alloc(n, 0)
+        _write(p, np.full(n // 4, i, dtype=np.int32))
+        lib.torch_park(p, 0)
+        ptrs.append(p)
+    s0 = lib.stats()
+    for _ in range(4):
+        for i, p in enumerate(ptrs):
+            lib.torch_unpark(p, 0)
+            assert int(_read(p, n // 4)[-1]) == i
+            lib.torch_park(p, 0)
+    s1 = lib.stats()
+    remaps = s1["vmm_remaps"] - s0["vmm_remaps"]
+    flushes = s1["tlb_flushes"] - s0["tlb_flushes"]
+    elided = s1["tlb_flushes_elided"] - s0["tlb_flushes_elided"]
+    assert remaps > 0 and elided > 0 and s1["vmm_errors"] == 0
+    assert flushes < 24  # at most one per unpark; covered maps flush nothing
+    for p in ptrs:
+        lib.torch_free(p, 0)
