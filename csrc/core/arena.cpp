@@ -368,7 +368,7 @@ Block* ChunkArena::owner(uint32_t i) {
 }
 
 void ChunkArena::touch(uint32_t i, bool has_data, bool preferred, bool prefetched, uint64_t refault_key,
-                       uint64_t evicted_at) {
+                       uint64_t evicted_at, bool clean) {
   std::lock_guard<OrderedMutex> g(m_);
   ChunkInfo& c = chunks_[i];
   if (c.state != ChunkState::ALLOCATED) return;
@@ -388,7 +388,7 @@ void ChunkArena::touch(uint32_t i, bool has_data, bool preferred, bool prefetche
     }
   }
   lru_remove(i);
-  lru_push_tail(i, !has_data ? 1 : (pref ? 3 : 2));
+  lru_push_tail(i, !has_data ? 1 : (pref && !clean ? 3 : 2));
 }
 
 void ChunkArena::pin(uint32_t i) {

@@ -115,8 +115,15 @@ void Runtime::touch_residency(Block* b, Residency* r, bool prefetched) {
   if (!r || r->chunk < 0) return;
   bool pref = b->policy.has_preferred && b->policy.preferred == r->loc;
   const bool refault = r->loc.is_gpu() && b->gpu_evictions > 0;
+  bool clean = false;
+  if (r->loc.is_gpu() && config().evict_clean_first) {
+    PageMask others;
+    for (auto& x : b->res)
+      if (&x != r) others |= x.resident;
+    clean = r->resident.andnot(others).empty();
+  }
   r->arena->touch((uint32_t)r->chunk, !r->resident.empty(), pref, prefetched, refault ? b->range->id + 1 : 0,
-                  b->gpu_evicted_at);
+                  b->gpu_evicted_at, clean);
 }
 
 // Populate: give block b a chunk at location dst (block lock held).

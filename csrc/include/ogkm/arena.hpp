@@ -112,8 +112,11 @@ class ChunkArena {
   // admitted when its hash falls in the first active_limit / W of the hash
   // space, so resident units interleave with streamed ones over the cycle (the
   // link keeps streaming behind them) instead of forming one long stretch.
+  // clean: every page also has a valid copy elsewhere - evicting it costs no
+  // copy-out, so it goes to the normal list even when preferred (dirty data,
+  // which costs a copy-out and a refill, stays in the protected list).
   void touch(uint32_t i, bool has_data, bool preferred = false, bool prefetched = false, uint64_t refault_key = 0,
-             uint64_t evicted_at = 0);
+             uint64_t evicted_at = 0, bool clean = false);
   uint64_t evictions() {
     std::lock_guard<OrderedMutex> g(m_);
     return st_.evictions;

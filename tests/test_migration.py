@@ -360,3 +360,39 @@ def test_busy_cpu_fault_retried_later_without_blocking_others(fake_rt):
     assert time.perf_counter() - t0 < 10
     a.free()
     b.free()
+
+
+@pytest.mark.parametrize("clean_first", [1, 0])
+def test_eviction_prefers_clean_copies(fake_rt, clean_first):
+    """HBM LRU with evict_clean_first: among GPU-preferred data (the managed
+    torch tensors' advice), a block that still has a valid host copy
+    (read-mostly data) is evicted before an older block whose only copy is in
+    HBM (written there) - the clean victim costs no copy-out."""
+    lib.configure("evict_clean_first", clean_first)
+    lib.init_device(0, 16 * MB)  # 8 chunks
+    dirty = rt.malloc_managed(8 * MB, "dirty")
+    dirty.set_preferred_location("gpu:0")
+    dirty.write(torch.full((2 * MB,), 3, dtype=torch.int32))
+    l = dirty.acquire(0, rt.WRITE)  # written on the GPU: the host copy is gone
+    l.release(0)
+    clean = rt.malloc_managed(8 * MB, "clean")
+    clean.write(torch.full((2 * MB,), 5, dtype=torch.int32))  # on the host
+    clean.set_preferred_location("gpu:0")
+    clean.set_read_mostly(True)
+    l = clean.acquire(0, rt.READ)  # read-duplicated: host copy stays valid
+    l.release(0)
+    rt.sync()
+    d0 = lib.stats()["bytes_xfer_dth"]
+    third = rt.malloc_managed(8 * MB, "third")
+    third.write(torch.full((2 * MB,), 7, dtype=torch.int32))
+    l = third.acquire(0, rt.READ)  # needs 4 chunks: evicts 4 of the 8
+    l.release(0)
+    rt.sync()
+    dth = lib.stats()["bytes_xfer_dth"] - d0
+    if clean_first:
+        assert dth == 0  # the newer but clean blocks went first
+    else:
+        assert dth >= 8 * MB  # plain LRU: the older dirty blocks were copied out
+    assert int(dirty.read().view(torch.int32).min()) == 3 and int(clean.read().view(torch.int32).min()) == 5
+    for b in (dirty, clean, third):
+        b.free()
