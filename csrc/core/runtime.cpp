@@ -290,11 +290,13 @@ Status Runtime::free_range(Range* r) {
     Block* b = bp.get();
     std::lock_guard<OrderedMutex> g(b->lock);
     b->tracker.wait();
-    if (r->dev_va && (b->stable_chunk.load() >= 0 || b->stale_mapping)) {
+    if (r->dev_va) {
       std::lock_guard<std::mutex> sg(stable_m_);
-      stable_unmap_locked(b);  // after the kernels still reading through the mapping
-      if (!stale_maps_.empty())
+      if (b->stable_chunk.load() >= 0) stable_unmap_locked(b);  // after the kernels still reading through the mapping
+      if (b->in_stale_list) {  // the block is about to go: no dangling stale_maps_ entry
         stale_maps_.erase(std::remove(stale_maps_.begin(), stale_maps_.end(), b), stale_maps_.end());
+        b->in_stale_list = false;
+      }
     }
     for (auto& x : b->res)
       if (x.chunk >= 0) x.arena->free((uint32_t)x.chunk, 1);
@@ -514,12 +516,12 @@ void Runtime::stable_unmap_locked(Block* b) {
 void Runtime::reap_stale_maps_locked() {
   size_t w = 0;
   for (Block* b : stale_maps_) {
-    if (!b->stale_mapping) continue;  // remapped / unmapped meanwhile: drop the entry
-    if (config().stable_lazy_unmap || !b->stable_users.query()) {
+    if (b->stale_mapping && (config().stable_lazy_unmap || !b->stable_users.query())) {
       stale_maps_[w++] = b;  // users still running (or lazy mode): keep
       continue;
     }
-    stable_unmap_locked(b);
+    if (b->stale_mapping) stable_unmap_locked(b);  // else remapped / unmapped meanwhile: drop the entry
+    b->in_stale_list = false;
   }
   stale_maps_.resize(w);
 }
@@ -558,7 +560,10 @@ void Runtime::stable_map_block(Block* b) {
     if (config().stable_lazy_unmap || !b->stable_users.query()) {
       if (b->stable_chunk.load() >= 0 && !b->stale_mapping) {
         b->stale_mapping = true;
-        stale_maps_.push_back(b);
+        if (!b->in_stale_list) {
+          b->in_stale_list = true;
+          stale_maps_.push_back(b);
+        }
       }
       return;
     }

@@ -108,6 +108,7 @@ class Block {
   // The stable VA still maps a chunk the block left (its users were running at
   // the eviction): listed in Runtime::stale_maps_ until the mapping goes.
   std::atomic<bool> stale_mapping{false};
+  bool in_stale_list = false;  // listed in Runtime::stale_maps_ (guarded by stable_m_)
   uint32_t lease_pins = 0;
   uint32_t gpu_evictions = 0;  // times an HBM copy of this block was evicted (refault detection)
   uint64_t gpu_evicted_at = 0; // the HBM arena's eviction count when it last was (refault distance)
