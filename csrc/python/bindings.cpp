@@ -854,6 +854,9 @@ PYBIND11_MODULE(_ogkm, m) {
     a.depth = depth;
     a.x_frag = x_frag ? 1 : 0;
     if (x_frag && K % 32) throw StatusError("dgemm: fragment-ordered x needs K % 32 == 0");
+    if (reduce && out_frag && (out_cols % 32 || out_col0 % 4 ||
+                               out_col0 + (epi == DGEMM_EPI_SILU_MUL ? N / 2 : N) > out_cols))
+      throw StatusError("dgemm: fragment-ordered out needs out_cols % 32 == 0 and the columns inside it");
     if ((uint64_t)a.ksplit * M * N * 4 > part_bytes) throw StatusError("dgemm: partial workspace too small");
     if (mode < DGEMM_W_RAW || mode > DGEMM_W_PACKED_BF11) throw StatusError("dgemm: bad weight mode");
     check(rt()->be()->dgemm(dev, a, mode, (void*)stream), "dgemm");
@@ -866,9 +869,6 @@ PYBIND11_MODULE(_ogkm, m) {
     r.out_frag = out_frag ? 1 : 0;
     r.out_cols = out_cols;
     r.out_col0 = out_col0;
-    if (out_frag && (out_cols % 32 || out_col0 % 4 ||
-                     out_col0 + (epi == DGEMM_EPI_SILU_MUL ? N / 2 : N) > out_cols))
-      throw StatusError("dgemm: fragment-ordered out needs out_cols % 32 == 0 and the columns inside it");
     check(rt()->be()->dgemm_reduce(dev, r, (void*)stream), "dgemm_reduce");
     return a.ksplit;
   }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("w_off"), py::arg("mode"), py::arg("chunk_shift"),
