@@ -100,8 +100,92 @@ def parse():
                     help="print the per-rank residency / traffic plan (JSON lines) of 70B and 405B, tp and shards, "
                          "at N = 1, 2, 4, 8 GPUs - host and CXL NUMA nodes, PCIe and xGMI GB/step, predicted "
                          "ms/step - without allocating anything (no GPU needed)")
+    ap.add_argument("--launch-timeout", type=float, default=float(os.environ.get("OGKM_LAUNCH_TIMEOUT_S", "3000")),
+                    help="--gpus N without torchrun: seconds the rank processes may run before all are killed")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _kill_groups(procs, grace_s: float = 10.0) -> None:
+    """SIGTERM every still-running rank's process group, SIGKILL what is left after ``grace_s``."""
+    import signal
+
+    live = [p for p in procs if p.poll() is None]
+    for p in live:
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+    t_end = time.monotonic() + grace_s
+    for p in live:
+        try:
+            p.wait(timeout=max(0.1, t_end - time.monotonic()))
+        except Exception:  # noqa: BLE001 - still alive: the hard kill below
+            pass
+    for p in live:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait()
+
+
+def launch_ranks(a) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start N rank processes of this
+    script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, RCCL
+    over xGMI - or gloo with ``--backend fake``) and wait for them.
+
+    This process never touches the GPU (torch is not even imported), so no
+    GPU-initialised process is ever replaced or forked. Every rank runs in its
+    own process group; if one exits non-zero, or the job outlives
+    ``--launch-timeout``, every other rank is killed (SIGTERM, then SIGKILL)
+    and the launcher exits non-zero. Rank 0's stdout (the JSON line) is
+    inherited, so it reaches our stdout unchanged. Returns the exit code."""
+    import subprocess
+
+    n = a.gpus
+    port = _free_port()
+    base = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(port), OGKM_BENCH_LAUNCHED="1")
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    try:
+        for r in range(n):
+            env = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0", ROLE_RANK=str(r))
+            procs.append(subprocess.Popen(cmd, env=env, start_new_session=True,
+                                          stdout=None if r == 0 else subprocess.DEVNULL))
+        deadline = time.monotonic() + a.launch_timeout
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print(f"[bench] rank {r} exited with status {c}: stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                _kill_groups(procs)
+                return c if c > 0 else 1
+            if all(c == 0 for c in codes):
+                return 0
+            if time.monotonic() > deadline:
+                print(f"[bench] ranks still running after {a.launch_timeout:.0f} s: killing all {n}",
+                      file=sys.stderr, flush=True)
+                _kill_groups(procs)
+                return 124
+            time.sleep(0.2)
+    except BaseException:
+        _kill_groups(procs)
+        raise
 
 
 HBM_USABLE_GB = 270.0  # of the 288 GB per MI355X (runtime / RCCL / activation reserve)
@@ -313,6 +397,14 @@ def main() -> None:
     if a.plan_only:
         plan_only(a)
         return
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and a.gpus > 1:
+        # no launcher: become one (before anything touches the GPU)
+        if a.torch_managed or a.simulate_tp:
+            raise SystemExit("--torch-managed / --simulate-tp are one-process runs: use --gpus 1")
+        sys.exit(launch_ranks(a))
+    if ws is not None and int(ws) != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ws}: one rank process per GPU is required")
     if a.torch_managed:
         run_torch_managed(a)
         return
@@ -338,8 +430,15 @@ def main() -> None:
         from ogkm import allocator
         allocator.enable()
     e = comm.init("gloo" if fake else None)
-    if e.world != a.gpus and e.world > 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={e.world}")
+    if e.world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but the process group has {e.world} ranks")
+    # failure drills for the launcher tests: one rank dies / hangs after joining the group
+    if os.environ.get("OGKM_BENCH_FAIL_RANK", "") == str(e.rank):
+        print(f"[bench] rank {e.rank}: injected failure", file=sys.stderr, flush=True)
+        os._exit(3)
+    if os.environ.get("OGKM_BENCH_HANG_RANK", "") == str(e.rank):
+        time.sleep(1e6)
+    pg_world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
     dev = e.local_rank
     if not fake:
         torch.cuda.set_device(dev)
@@ -451,6 +550,11 @@ def main() -> None:
                 "parallelism": (f"tp{a.simulate_tp}-rank0-simulated" if sim
                                 else f"{'shards' if a.parallel == 'shards' else 'tp'}{world}"),
                 "backend": a.backend,
+                # ranks in the process group that ran the step (RCCL on GPUs, gloo with --backend fake)
+                "rccl_world": pg_world,
+                "process_group": e.backend,
+                "launcher": ("bench.py" if os.environ.get("OGKM_BENCH_LAUNCHED") == "1"
+                             else "external" if world > 1 else "none"),
                 "planner": a.planner,
                 "kv_tiering": a.kv_tiering,
                 "torch_allocator": "ogkm-arena" if a.allocator else "torch-caching",

@@ -9,6 +9,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 import torch
@@ -26,12 +27,17 @@ def _port() -> int:
     return p
 
 
-def _bench(tmp_path, nproc: int, extra: list, force_dist: bool = False) -> tuple[dict, torch.Tensor]:
-    dump = str(tmp_path / f"logits_{nproc}_{int(force_dist)}_{'_'.join(extra)}.pt")
+def _bench(tmp_path, nproc: int, extra: list, force_dist: bool = False,
+           self_launch: bool = False) -> tuple[dict, torch.Tensor]:
+    dump = str(tmp_path / f"logits_{nproc}_{int(force_dist)}_{int(self_launch)}_{'_'.join(extra)}.pt")
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", OGKM_UNIT_MIN_MB="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
     if force_dist:
         env["OGKM_DIST_FORCE"] = "1"
-    if nproc == 1 and not force_dist:
+    if self_launch:  # bench.py spawns its own rank processes (no torchrun)
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nproc)]
+    elif nproc == 1 and not force_dist:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py")]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -49,12 +55,18 @@ def single(tmp_path_factory):
     return _bench(tmp_path_factory.mktemp("b1"), 1, [])
 
 
+@pytest.fixture(scope="module")
+def torchrun_tp4(tmp_path_factory):
+    return _bench(tmp_path_factory.mktemp("tr4"), 4, ["--parallel", "tp"])
+
+
 @pytest.mark.parametrize("parallel", ["tp", "shards"])
-def test_bench_four_ranks(single, tmp_path, parallel):
+def test_bench_four_ranks(single, torchrun_tp4, tmp_path, parallel):
     one, ref = single
-    out, logits = _bench(tmp_path, 4, ["--parallel", parallel])
+    out, logits = torchrun_tp4 if parallel == "tp" else _bench(tmp_path, 4, ["--parallel", parallel])
     cfg = out["config"]
     assert out["n_gpus"] == 4 and cfg["parallelism"] == f"{parallel}4" and cfg["global_batch"] == 8
+    assert cfg["rccl_world"] == 4 and cfg["launcher"] == "external"
     # fake_numa_nodes=2: GPUs 0-1 on node 0, 2-3 on node 1 - each rank's host tier follows its GPU
     assert cfg["rank_host_numa_nodes"] == [0, 0, 1, 1]
     assert logits.shape == ref.shape
@@ -113,3 +125,48 @@ def test_plan_only_prints_every_configuration():
         assert p["predicted_ms_per_step"] > 0 and r0["pcie_gb_per_step"] >= 0
         if p["n_gpus"] > 1:
             assert r0["xgmi_gb_per_step"] > 0
+
+
+def test_bench_self_launch_four_ranks(single, torchrun_tp4, tmp_path):
+    """``bench.py --gpus 4`` without torchrun spawns 4 rank processes itself:
+    a real 4-rank job whose logits equal the torchrun run's bit for bit."""
+    out, logits = _bench(tmp_path, 4, ["--parallel", "tp"], self_launch=True)
+    cfg = out["config"]
+    assert out["n_gpus"] == 4 and cfg["rccl_world"] == 4 and cfg["launcher"] == "bench.py"
+    assert cfg["parallelism"] == "tp4" and cfg["rank_host_numa_nodes"] == [0, 0, 1, 1]
+    assert torch.equal(logits, torchrun_tp4[1])
+    one, _ = single
+    assert one["n_gpus"] == 1 and one["config"]["rccl_world"] == 1 and one["config"]["launcher"] == "none"
+
+
+def _launch(extra_env: dict, extra_args: list, timeout: float):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", OGKM_UNIT_MIN_MB="0", **extra_env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"] + ARGS + extra_args
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    return r, time.monotonic() - t0
+
+
+def test_bench_launcher_child_failure_stops_job():
+    """One rank dies after joining the group: the launcher kills the other
+    three (blocked in a collective) and exits non-zero, without a JSON line."""
+    r, dt = _launch({"OGKM_BENCH_FAIL_RANK": "1"}, ["--launch-timeout", "600"], timeout=300)
+    assert r.returncode != 0 and "rank 1 exited with status 3" in r.stderr, r.stderr[-3000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert dt < 200
+
+
+def test_bench_launcher_timeout_kills_hung_rank():
+    r, dt = _launch({"OGKM_BENCH_HANG_RANK": "2"}, ["--launch-timeout", "20"], timeout=300)
+    assert r.returncode == 124 and "killing all 4" in r.stderr, r.stderr[-3000:]
+    assert dt < 120
+
+
+@pytest.mark.parametrize("ws,gpus", [("2", "4"), ("4", "1"), ("1", "2")])
+def test_bench_refuses_world_size_mismatch(ws, gpus):
+    env = dict(os.environ, PYTHONPATH=ROOT, WORLD_SIZE=ws, RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", gpus] + ARGS, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr, r.stderr[-2000:]
