@@ -100,6 +100,9 @@ def parse():
                     help="print the per-rank residency / traffic plan (JSON lines) of 70B and 405B, tp and shards, "
                          "at N = 1, 2, 4, 8 GPUs - host and CXL NUMA nodes, PCIe and xGMI GB/step, predicted "
                          "ms/step - without allocating anything (no GPU needed)")
+    ap.add_argument("--same-gpu", action="store_true",
+                    help="test drill: every rank runs on GPU 0 (own runtime and arena each) over a gloo process group "
+                         "- RCCL refuses two ranks on one device; exercises the multi-rank kernels on a 1-GPU box")
     ap.add_argument("--launch-timeout", type=float, default=float(os.environ.get("OGKM_LAUNCH_TIMEOUT_S", "3000")),
                     help="--gpus N without torchrun: seconds the rank processes may run before all are killed")
     ap.add_argument("--verbose", action="store_true")
@@ -353,7 +356,8 @@ def bandwidth_probe(dev: int, barrier, nbytes: int = 1 << 30) -> tuple[dict, dic
     info = cxl.get_info()
     near = lib.cxl_nearest_node(lib.host_node()) if info["numa_nodes"] else lib.host_node()
     far = [n for n in info["numa_nodes"] if n != near]
-    meta = {"cxl_numa_node": near, "emulated": bool(info["emulated"] or not info["numa_nodes"])}
+    meta = {"cxl_numa_node": near, "host_numa_node": lib.host_node(),
+            "emulated": bool(info["emulated"] or not info["numa_nodes"])}
     try:
         # the rank's own pool (nearest) is what tiering uses; the other socket's
         # pool is measured too (remote CXL: the same full-rate SDMA engines)
@@ -429,7 +433,7 @@ def main() -> None:
         # tensor exists); allocations resolve once the runtime is up.
         from ogkm import allocator
         allocator.enable()
-    e = comm.init("gloo" if fake else None)
+    e = comm.init("gloo" if fake or a.same_gpu else None)
     if e.world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but the process group has {e.world} ranks")
     # failure drills for the launcher tests: one rank dies / hangs after joining the group
@@ -439,7 +443,7 @@ def main() -> None:
     if os.environ.get("OGKM_BENCH_HANG_RANK", "") == str(e.rank):
         time.sleep(1e6)
     pg_world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
-    dev = e.local_rank
+    dev = 0 if a.same_gpu else e.local_rank
     if not fake:
         torch.cuda.set_device(dev)
     world = e.world
@@ -456,9 +460,17 @@ def main() -> None:
     # No CXL hardware on the box: every NUMA node emulates a CXL pool, and each
     # rank demotes to the pool nearest its GPU's node (SLIT distance,
     # CxlTopology::nearest_node) - one pool per socket, as on a CXL-populated node.
+    # The rank's own host node is left out of the emulated pool whenever another
+    # node exists: a "CXL" tier on the host tier's node would be the same DRAM
+    # counted twice, so the emulated pool is the other socket's memory (a farther
+    # tier, reached over the socket link as a CXL expander on that socket would be).
     nodes = sorted({int(p.name[4:]) for p in Path("/sys/devices/system/node").glob("node[0-9]*")})
+    cxl_kind = "cxl-device"
     if not lib.cxl_info()["numa_nodes"] and nodes:
-        lib.cxl_rediscover(-1, "/sys", sum(1 << n for n in nodes))
+        pool = [n for n in nodes if n != lib.host_node()] or nodes
+        cxl_kind = ("emulated: other-socket DRAM" if pool != nodes
+                    else "emulated: host-node DRAM (single NUMA node)")
+        lib.cxl_rediscover(-1, "/sys", sum(1 << n for n in pool))
     aux = {}
     if not a.no_aux:
         aux = probe_all_ranks(dev, e.rank)
@@ -560,6 +572,7 @@ def main() -> None:
                 "torch_allocator": "ogkm-arena" if a.allocator else "torch-caching",
                 "rank_host_numa_nodes": host_nodes,
                 "tiers": plan["tiers"],
+                "cxl_tier": cxl_kind,
                 "kv_format": plan["kv_format"],
                 "kv_resident_gb_per_gpu": round(plan["kv_resident_gb"], 2),
                 "cxl_streamed_gb_per_step_per_gpu": round(plan["cxl_streamed_gb_per_step"], 2),

@@ -158,6 +158,9 @@ int CxlTopology::distance(int from, int to) const {
 int CxlTopology::nearest_node(int from) const {
   int best = first_node(), best_d = -1;
   for (int n : info_.numa_nodes) {
+    // A pool on the asking node itself is that node's DRAM (an emulated pool
+    // over a CPU node): never a farther tier while another pool exists.
+    if (n == from && info_.numa_nodes.size() > 1) continue;
     int d = distance(from, n);
     if (d < 0) continue;
     if (best_d < 0 || d < best_d || (d == best_d && n < best)) {

@@ -124,6 +124,7 @@ def _mode_class():
             self.ops += 1
             if self._last is not None:
                 self._last.append((self.ops, func.__name__, len(held)))
+            out = None  # an op that raises allocated nothing: its holds are still dropped below
             try:
                 out = func(*args, **kwargs)
             except BaseException:

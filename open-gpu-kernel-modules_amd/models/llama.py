@@ -1094,9 +1094,14 @@ class TieredLlama:
         if self.fake:
             x = x.to(self.tdev)
         dv = self.dev
-        # Deferred epilogues (one rank): the qkv GEMM's split-K sum runs in
-        # k_rope_kv, the o / down GEMMs' residual adds in the next k_rmsnorm -
-        # 3 fewer launches per layer, bit-identical to the separate reduce.
+        # Deferred epilogues: the qkv GEMM's split-K sum runs in k_rope_kv (any
+        # TP degree: QKV is column-parallel, nothing to reduce across ranks);
+        # with one TP rank the o / down GEMMs' residual adds also run in the
+        # next k_rmsnorm - 3 fewer launches per layer, bit-identical to the
+        # separate reduce. Under TP the o / down outputs are partial sums that
+        # must be all-reduced over the ranks before the residual add, so their
+        # epilogue cannot run on the local split-K partials.
+        fuse_qkv = self.fuse_epilogues
         fuse = self.fuse_epilogues and self.world == 1
         fuse_down = fuse and len(self.layout.roles["wd"]) == 1
         # GEMM inputs (h, a, g) in the MFMA fragment order (dgemm.to_frag): every
@@ -1108,7 +1113,7 @@ class TieredLlama:
             h = fused.rms_norm(x, self.norm_w[2 * i], cfg.norm_eps, device_index=dv, pending=pend, out_frag=xf)
             pend = None
             lease, w = self._use(("layer", i, "wqkv"))
-            qkv = dgemm.linear(h, w, device_index=dv, defer=fuse, x_rows=xr)
+            qkv = dgemm.linear(h, w, device_index=dv, defer=fuse_qkv, x_rows=xr)
             self._done(lease)
             kvl = self._kv_layer(i, pos)
             q = self._rope_append(i, pos, kvl, qkv)

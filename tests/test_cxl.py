@@ -180,8 +180,9 @@ def test_demotion_goes_to_nearest_cxl_node(fake_rt, tmp_path):
 
 
 def test_emulated_cxl_pool_per_socket(fake_rt, tmp_path):
-    """Without CXL hardware, one emulated pool per socket: each host node's
-    nearest pool is its own socket's node."""
+    """Without CXL hardware, one emulated pool per socket: a host node's own
+    DRAM is never its CXL tier while another pool exists (the same memory
+    would back both tiers), so each host node demotes to the other socket."""
     root = _two_socket_sysfs(tmp_path)
     for nid in (2, 3):  # drop the CPU-less nodes: a plain 2-socket box
         for f in (root / "devices" / "system" / "node" / f"node{nid}").iterdir():
@@ -191,4 +192,8 @@ def test_emulated_cxl_pool_per_socket(fake_rt, tmp_path):
         (root / "devices" / "system" / "node" / f"node{nid}" / "distance").write_text(row + "\n")
     info = cxl.rediscover(-1, str(root), emulate_nodes=(0, 1))
     assert info["emulated"] and info["numa_nodes"] == [0, 1]
-    assert lib.cxl_nearest_node(0) == 0 and lib.cxl_nearest_node(1) == 1
+    assert lib.cxl_nearest_node(0) == 1 and lib.cxl_nearest_node(1) == 0
+    info = cxl.rediscover(-1, str(root), emulate_nodes=(1,))  # bench.py: the host node left out of the pool
+    assert info["numa_nodes"] == [1] and lib.cxl_nearest_node(0) == 1
+    info = cxl.rediscover(-1, str(root), emulate_nodes=(0,))  # single-node box: the only pool is the host's
+    assert lib.cxl_nearest_node(0) == 0
