@@ -137,6 +137,8 @@ Status ChunkArena::alloc(uint32_t n, Block* owner, int64_t hint, uint32_t* first
     c.owner = owner;
     c.pin_count = pin ? 1 : 0;
     c.last_use = ++clock_;
+    c.last_op = op_clock_;
+    c.next_use = 0;
     lru_push_tail((uint32_t)pick + i, 1);
   }
   if (pin) st_.pinned += (uint64_t)n << kBlockShift;
@@ -182,14 +184,17 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
   uint32_t start = 0;
   // Cost of evicting a chunk: 0 if free, its recency otherwise; chunks on the
   // preferred list cost more than any ordinary chunk.
+  const uint64_t floor = hinted_ ? VictimFloor::value() : 0;
   auto cost_of = [&](uint32_t i) -> uint64_t {
     const ChunkInfo& c = chunks_[i];
     if (c.state == ChunkState::FREE) return 0;
+    if (hinted_) return ~victim_key_locked(c);  // a window of the furthest-needed data
     return c.last_use + (c.list == 3 ? (1ull << 62) : 0) + (c.active ? (1ull << 61) : 0);
   };
   for (uint32_t i = 0; i < nchunks_; ++i) {
     ChunkInfo& c = chunks_[i];
-    bool ok = c.state == ChunkState::FREE || (c.state == ChunkState::ALLOCATED && c.pin_count == 0);
+    bool ok = c.state == ChunkState::FREE ||
+              (c.state == ChunkState::ALLOCATED && c.pin_count == 0 && !floor_protects_locked(c, floor));
     if (!ok) {
       start = i + 1;
       dq.clear();
@@ -236,6 +241,11 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
 // chunks carry a recency bonus and lose to genuinely cold data).
 // Workingset-protected (active) chunks go only when nothing inactive is left.
 int32_t ChunkArena::pick_victim_locked() {
+  if (hinted_) {
+    std::vector<uint32_t> v;
+    pick_victims_by_next_use_locked(1, &v);
+    return v.empty() ? -1 : (int32_t)v[0];
+  }
   for (int pass = 0; pass < 6; ++pass) {
     const int list = 1 + pass % 3;
     const bool allow_active = pass >= 3;
@@ -252,6 +262,60 @@ int32_t ChunkArena::pick_victim_locked() {
   return -1;
 }
 
+uint64_t& VictimFloor::value() {
+  static thread_local uint64_t floor = 0;
+  return floor;
+}
+
+void ChunkArena::set_next_use(uint32_t i, uint64_t when) {
+  std::lock_guard<OrderedMutex> g(m_);
+  if (i >= nchunks_ || chunks_[i].state != ChunkState::ALLOCATED) return;
+  chunks_[i].next_use = when;
+  if (when && when != kDeadUse) hinted_ = true;
+}
+
+void ChunkArena::set_op_clock(uint64_t now) {
+  std::lock_guard<OrderedMutex> g(m_);
+  op_clock_ = std::max(op_clock_, now);
+}
+
+// Larger = evicted sooner: dead data, then unhinted data by age, then hinted
+// data by the distance to its next use. Unhinted data touched within the last
+// two ops (an activation between its producer and consumer) ranks as needed
+// next. Hints in the past (the trace moved on without a use) count as unknown.
+uint64_t ChunkArena::victim_key_locked(const ChunkInfo& c) const {
+  if (c.next_use == kDeadUse) return kDeadUse;
+  if (c.next_use > op_clock_) return c.next_use - op_clock_;
+  if (op_clock_ - c.last_op <= 2) return 1;
+  return (1ull << 62) + (clock_ - std::min(clock_, c.last_use));
+}
+
+// The floor is an op-clock time: data whose next use comes no later is kept.
+bool ChunkArena::floor_protects_locked(const ChunkInfo& c, uint64_t floor) const {
+  if (!floor || !hinted_) return false;
+  const uint64_t k = victim_key_locked(c);
+  return k < (1ull << 62) && k + op_clock_ <= floor;
+}
+
+void ChunkArena::pick_victims_by_next_use_locked(uint32_t n, std::vector<uint32_t>* out) {
+  const uint64_t floor = VictimFloor::value();
+  std::vector<std::pair<uint64_t, uint32_t>> cand;
+  for (uint32_t i = 0; i < nchunks_; ++i) {
+    const ChunkInfo& c = chunks_[i];
+    if (c.state != ChunkState::ALLOCATED || c.pin_count != 0) continue;
+    if (floor_protects_locked(c, floor)) continue;
+    cand.emplace_back(victim_key_locked(c), i);
+  }
+  if (cand.size() > n) {
+    std::nth_element(cand.begin(), cand.begin() + n, cand.end(),
+                     [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
+                       return a.first > b.first;
+                     });
+    cand.resize(n);
+  }
+  for (auto& c : cand) out->push_back(c.second);
+}
+
 Status ChunkArena::reserve_scattered(uint32_t n, Reservation* r) {
   std::lock_guard<OrderedMutex> g(m_);
   if (n == 0 || n > nchunks_) return Status::NO_MEMORY;
@@ -265,6 +329,16 @@ Status ChunkArena::reserve_scattered(uint32_t n, Reservation* r) {
     take_run(k, 1);
     chunks_[k].state = ChunkState::RESERVED;
     r->list.push_back(k);
+  }
+  if (hinted_ && r->list.size() < n) {
+    std::vector<uint32_t> v;
+    pick_victims_by_next_use_locked(n - (uint32_t)r->list.size(), &v);
+    for (uint32_t k : v) {
+      lru_remove(k);
+      chunks_[k].state = ChunkState::EVICTING;
+      r->list.push_back(k);
+      r->victims.push_back(k);
+    }
   }
   while (r->list.size() < n) {
     int32_t v = pick_victim_locked();
@@ -300,6 +374,7 @@ void ChunkArena::evicted(uint32_t i) {
   RT_ASSERT_RELEASE(c.state == ChunkState::EVICTING);
   c.state = ChunkState::RESERVED;
   c.owner = nullptr;
+  c.next_use = 0;
   deactivate(c);
   st_.allocated -= kBlockSize;
   st_.evictions++;
@@ -314,6 +389,8 @@ void ChunkArena::commit(const Reservation& r, bool pin) {
     c.owner = nullptr;
     c.pin_count = pin ? 1 : 0;
     c.last_use = ++clock_;
+    c.last_op = op_clock_;
+    c.next_use = 0;
     lru_push_tail(k, 1);
   });
   if (pin) st_.pinned += (uint64_t)r.n << kBlockShift;
@@ -349,6 +426,7 @@ void ChunkArena::free(uint32_t first, uint32_t n) {
     c.state = ChunkState::FREE;
     c.owner = nullptr;
     c.pin_count = 0;
+    c.next_use = 0;
     c.zeroed = false;
     deactivate(c);
   }
@@ -373,6 +451,7 @@ void ChunkArena::touch(uint32_t i, bool has_data, bool preferred, bool prefetche
   ChunkInfo& c = chunks_[i];
   if (c.state != ChunkState::ALLOCATED) return;
   c.last_use = ++clock_ + (prefetched ? kPrefetchBoost : 0);
+  if (!prefetched) c.last_op = op_clock_;
   // A chunk keeps its preferred status until it loses its data.
   bool pref = has_data && (preferred || c.list == 3);
   if (!has_data) {

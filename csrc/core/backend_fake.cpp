@@ -192,19 +192,60 @@ class FakeBackend : public Backend {
     *va = m;
     return Status::OK;
   }
-  void va_free(void* va, size_t bytes) override { munmap(va, bytes); }
-  Status vmm_map(void* va, size_t bytes, uint64_t h, int) override {
-    void* m = mmap(va, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, (int)h, 0);
-    if (m == MAP_FAILED) return Status::IO_ERROR;
-    std::lock_guard<std::mutex> g(race_m_);
-    vmaps_[(uint64_t)va] = {bytes, h};
-    return Status::OK;
+  void va_free(void* va, size_t bytes) override {
+    {
+      std::lock_guard<std::mutex> g(tlb_m_);
+      for (auto it = live_.lower_bound((uint64_t)va); it != live_.end() && it->first < (uint64_t)va + bytes;)
+        it = live_.erase(it);
+      for (auto it = pending_.lower_bound((uint64_t)va); it != pending_.end() && it->first < (uint64_t)va + bytes;)
+        it = pending_.erase(it);
+    }
+    munmap(va, bytes);
   }
-  Status vmm_unmap(void* va, size_t bytes) override {
-    void* m = mmap(va, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
-    std::lock_guard<std::mutex> g(race_m_);
-    vmaps_.erase((uint64_t)va);
+  // Translation model (Injection::tlb_mode): with mode >= 1 a VA whose old
+  // mapping may be cached keeps serving it after an unmap / remap until
+  // tlb_flush applies the new state (mode 2: the flush does nothing) - the
+  // behaviour of gfx950 VMM remaps (tools/probe_vmm_tlb.hip), on the CPU.
+  int tlb_mode() {
+    Runtime* rt = Runtime::get();
+    return rt ? rt->inject().tlb_mode.load() : 0;
+  }
+  static Status apply_map(void* va, size_t bytes, uint64_t h) {
+    void* m = h ? mmap(va, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, (int)h, 0)
+                : mmap(va, bytes, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_FIXED | MAP_NORESERVE, -1, 0);
     return m == MAP_FAILED ? Status::IO_ERROR : Status::OK;
+  }
+  Status set_translation(void* va, size_t bytes, uint64_t h) {
+    {
+      std::lock_guard<std::mutex> g(race_m_);
+      if (h)
+        vmaps_[(uint64_t)va] = {bytes, h};
+      else
+        vmaps_.erase((uint64_t)va);
+    }
+    std::lock_guard<std::mutex> g(tlb_m_);
+    auto lv = live_.find((uint64_t)va);
+    const bool cached = lv != live_.end() && lv->second.second != 0;  // a translation may be cached
+    if (tlb_mode() >= 1 && cached) {
+      pending_[(uint64_t)va] = {bytes, h};
+      return Status::OK;
+    }
+    pending_.erase((uint64_t)va);
+    live_[(uint64_t)va] = {bytes, h};
+    return apply_map(va, bytes, h);
+  }
+  Status vmm_map(void* va, size_t bytes, uint64_t h, int) override { return set_translation(va, bytes, h); }
+  Status vmm_unmap(void* va, size_t bytes) override { return set_translation(va, bytes, 0); }
+  Status tlb_flush(int) override {
+    if (tlb_mode() >= 2) return Status::OK;  // a flush that does not work
+    std::lock_guard<std::mutex> g(tlb_m_);
+    Status st = Status::OK;
+    for (auto& kv : pending_) {
+      live_[kv.first] = kv.second;
+      if (apply_map((void*)kv.first, kv.second.first, kv.second.second) != Status::OK) st = Status::IO_ERROR;
+    }
+    pending_.clear();
+    return st;
   }
   // Race detector for tests (fake_race_check): the VMM handle behind an
   // address, and the handles an in-flight engine copy reads / writes.
@@ -253,6 +294,9 @@ class FakeBackend : public Backend {
     }
   }
   std::mutex race_m_;
+  std::mutex tlb_m_;
+  std::map<uint64_t, std::pair<size_t, uint64_t>> live_;     // va -> (bytes, handle) the "GPU" sees (0 = none)
+  std::map<uint64_t, std::pair<size_t, uint64_t>> pending_;  // va -> mapping applied at the next tlb_flush
   std::map<uint64_t, std::pair<uint64_t, uint64_t>> vmaps_;  // va -> (bytes, handle)
   std::map<uint64_t, int64_t> busy_w_, busy_r_, busy_k_, busy_kw_;
   std::atomic<uint64_t> races_{0};

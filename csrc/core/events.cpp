@@ -140,7 +140,9 @@ const char* counter_name(Counter c) {
                             "vmm_errors",
                             "tlb_flushes",
                             "faults_cancelled",
-                            "tlb_flushes_elided"};
+                            "tlb_flushes_elided",
+                            "write_invalidations",
+                            "remote_fallbacks"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -124,6 +124,93 @@ void Runtime::touch_residency(Block* b, Residency* r, bool prefetched) {
   }
   r->arena->touch((uint32_t)r->chunk, !r->resident.empty(), pref, prefetched, refault ? b->range->id + 1 : 0,
                   b->gpu_evicted_at, clean);
+  if (r->loc.is_gpu()) {
+    const uint64_t nu = b->range->dead.load(std::memory_order_relaxed) ? kDeadUse : b->range->next_use.load();
+    if (nu) r->arena->set_next_use((uint32_t)r->chunk, nu);
+  }
+}
+
+// Next-use hint of a whole range (the transparent mode's op trace): stored on
+// the range for chunks it gets later, and set on the HBM chunks it holds now.
+void Runtime::hint_next_use(Range* r, uint64_t when) {
+  r->next_use.store(when);
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  for (auto& bp : r->blocks) {
+    Block* b = bp.get();
+    std::lock_guard<OrderedMutex> g(b->lock);
+    for (auto& x : b->res)
+      if (x.loc.is_gpu() && x.chunk >= 0) x.arena->set_next_use((uint32_t)x.chunk, when);
+  }
+}
+
+void Runtime::set_op_clock(int dev, uint64_t now) {
+  if (ChunkArena* a = arena_for(Loc::gpu(dev))) a->set_op_clock(now);
+}
+
+// The range's contents are dead (`dead`: a freed torch allocation) or live
+// again. Dead: every copy off the GPU is dropped now (a later reuse must not
+// copy garbage back) and evicting its HBM chunks copies nothing out; the
+// chunks rank first among victims. Live again: the next writes repopulate it.
+void Runtime::set_dead(Range* r, bool dead) {
+  r->dead.store(dead);
+  r->next_use.store(0);
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  Ctx c;
+  for (auto& bp : r->blocks) {
+    Block* b = bp.get();
+    std::lock_guard<OrderedMutex> g(b->lock);
+    if (dead) {
+      std::vector<Loc> off_gpu;
+      for (auto& x : b->res)
+        if (!x.loc.is_gpu()) off_gpu.push_back(x.loc);
+      for (auto& l : off_gpu) drop_copy(c, b, l);
+    }
+    for (auto& x : b->res)
+      if (x.loc.is_gpu() && x.chunk >= 0) x.arena->set_next_use((uint32_t)x.chunk, dead ? kDeadUse : 0);
+  }
+  finish_ctx(c, nullptr);
+}
+
+// The GPU copy of `pages` (byte intervals of r) is about to be written by
+// `gpu`: every other copy of those pages is revoked, the rest of each block
+// keeps its duplicates - so an eviction copies out only what was written
+// since the data was last duplicated (per-page dirty tracking,
+// uvm_va_block.h:101-230 resident masks; block_copy_resident_pages copies
+// only the pages it needs, uvm_va_block.c:4143-4326). The pages must be
+// resident on `gpu` (a lease holds them); others are made resident first.
+Status Runtime::invalidate_others(Range* r, const std::vector<std::pair<uint64_t, uint64_t>>& bytes, int gpu) {
+  if (!r || !is_local(gpu)) return Status::INVALID_ARGUMENT;
+  std::map<uint64_t, PageMask> per_block;
+  for (auto& iv : bytes) {
+    uint64_t lo = std::min(iv.first, r->size), hi = std::min(iv.second, r->size);
+    if (hi <= lo) continue;
+    for (uint64_t p = lo >> kPageShift, pe = (hi - 1) >> kPageShift; p <= pe;) {
+      const uint64_t bi = p >> (kBlockShift - kPageShift);
+      const uint32_t p0 = (uint32_t)(p & ((kBlockSize >> kPageShift) - 1));
+      const uint64_t last_in_block = ((bi + 1) << (kBlockShift - kPageShift)) - 1;
+      const uint64_t q = std::min(pe, last_in_block);
+      per_block[bi] |= PageMask::range(p0, (uint32_t)(q - p + 1));
+      p = q + 1;
+    }
+  }
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  Ctx c;
+  Status st = Status::OK;
+  const Loc dst = Loc::gpu(gpu);
+  for (auto& kv : per_block) {
+    Block* b = r->block(kv.first);
+    if (!b) continue;
+    std::lock_guard<OrderedMutex> g(b->lock);
+    bool others = false;
+    for (auto& x : b->res)
+      if (!(x.loc == dst) && x.resident.intersects(kv.second)) others = true;
+    if (!others) continue;
+    st = make_resident(c, b, kv.second, dst, false, Cause::User);
+    if (st != Status::OK) break;
+    Tools::get().inc(Counter::WriteInvalidations);
+  }
+  Status fs = finish_ctx(c, nullptr);
+  return st != Status::OK ? st : fs;
 }
 
 // Populate: give block b a chunk at location dst (block lock held).
@@ -628,6 +715,7 @@ Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
   for (auto& x : b->res)
     if (&x != r) others |= x.resident;
   PageMask only_here = r->resident.andnot(others);
+  if (b->range->dead.load(std::memory_order_relaxed)) only_here.zero();  // nothing worth keeping
   Loc from = r->loc;
   uint64_t bytes = (uint64_t)r->resident.count() << kPageShift;
   if (!only_here.empty()) {
@@ -1256,7 +1344,8 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
 }
 
 // ------------------------------------------------------------------ leases
-Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out) {
+Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out,
+                        bool allow_remote) {
   TraceRange tr(be_.get(), "ogkm:acquire");
   if (global_status() != Status::OK) return global_status();
   if (quiesced_.load()) return Status::BUSY;
@@ -1299,6 +1388,15 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
       }
       // Readers never revoke another processor's leased copy: duplicate instead.
       if (access == Access::READ && b->lease_pins) dec[k].read_dup = true;
+      if (!allow_remote && dec[k].map_remote && proc != kCpuProc) {
+        // The caller needs the data at its own device address: a local copy
+        // instead of the zero-copy mapping. A reader keeps the remote copy
+        // (duplicate), so a thrash-pinned block is not pulled back and forth.
+        dec[k].map_remote = false;
+        dec[k].dst = dst;
+        dec[k].read_dup = access == Access::READ || access == Access::PREFETCH;
+        Tools::get().inc(Counter::RemoteFallbacks);
+      }
       if (!dec[k].map_remote) all_remote = false;
     }
     Ctx c;

@@ -145,7 +145,93 @@ Status Runtime::init_device(int d, uint64_t budget) {
   }
   devs_[d]->hbm = std::make_unique<HbmArena>(be_.get(), d, budget, (int)config().hbm_provider);
   devs_[d]->hbm_live.store(devs_[d]->hbm.get(), std::memory_order_release);
+  if (devs_[d]->hbm->init_status() == Status::OK && devs_[d]->hbm->vmm()) (void)vmm_self_test(d);
   return devs_[d]->hbm->init_status();
+}
+
+Status Runtime::vmm_self_test(int d) {
+  if (!is_local(d)) return Status::INVALID_ARGUMENT;
+  HbmArena* ha = devs_[d]->hbm_live.load();
+  VmmSelfTest& T = devs_[d]->vmm_test;
+  T = VmmSelfTest{};
+  if (!ha || !ha->vmm() || ha->nchunks() < 2) return Status::NOT_SUPPORTED;
+  T.ran = true;
+  uint32_t ch[2] = {0, 0};
+  void* va = nullptr;
+  uint32_t* out = nullptr;
+  void* stream = nullptr;
+  bool mapped = false;
+  Status st = Status::OK;
+  const uint32_t pat[2] = {0xA5C30F01u, 0x5A3CF102u};
+  auto fail = [&](const char* what) {
+    T.ok = false;
+    T.detail = std::string(what) + ": " + be_->last_error();
+  };
+  int nch = 0;
+  for (; nch < 2 && st == Status::OK; ++nch)
+    if ((st = ha->alloc(1, nullptr, -1, &ch[nch], true)) != Status::OK) break;
+  if (st != Status::OK) {
+    fail("no free chunks");
+  } else if ((st = be_->va_reserve(kBlockSize, &va)) != Status::OK) {
+    fail("va_reserve");
+  } else if ((st = be_->host_alloc_coherent(4096, (void**)&out)) != Status::OK) {
+    fail("host_alloc_coherent");
+  } else if (!(stream = be_->stream_create(d, 0))) {
+    fail("stream_create");
+  } else {
+    for (int i = 0; i < 2 && st == Status::OK; ++i)
+      st = be_->memset32(d, ha->chunk_addr(ch[i]), pat[i], kBlockSize, stream);
+    if (st == Status::OK) st = be_->stream_sync(stream);
+    if (st != Status::OK) fail("fill");
+    // Read one page of the canary VA through a CU copy (the shader path that
+    // kernels use) and return the number of words holding `want`.
+    auto probe = [&](uint32_t want) -> int {
+      memset(out, 0, 4096);
+      CopyDesc cd{(uint64_t)out, (uint64_t)va + kBlockSize / 2, 4096, 0};
+      if (be_->copy_batch(d, &cd, 1, stream, 0) != Status::OK || be_->stream_sync(stream) != Status::OK) return -1;
+      int n = 0;
+      for (int k = 0; k < 1024; ++k) n += out[k] == want;
+      return n;
+    };
+    const uint32_t rounds = 6;
+    for (uint32_t r = 0; r < rounds && T.ok; ++r) {
+      const int h = r & 1;
+      if (mapped && be_->vmm_unmap(va, kBlockSize) != Status::OK) {
+        fail("vmm_unmap");
+        break;
+      }
+      if (be_->vmm_map(va, kBlockSize, ha->handle(ch[h]), d) != Status::OK) {
+        fail("vmm_map");
+        break;
+      }
+      mapped = true;
+      if (r > 0 && probe(pat[h]) != 1024) T.unflushed_stale++;  // before the flush: informational
+      if (be_->tlb_flush(d) != Status::OK) {
+        fail("tlb_flush");
+        break;
+      }
+      T.rounds++;
+      int n = probe(pat[h]);
+      if (n == 1024) {
+        T.flushed_ok++;
+      } else {
+        T.ok = false;
+        T.detail = "after a remap and a translation flush a kernel read " + std::to_string(n < 0 ? 0 : n) +
+                   "/1024 words of the new chunk (stale translation)";
+      }
+    }
+  }
+  if (mapped) be_->vmm_unmap(va, kBlockSize);
+  (void)be_->tlb_flush(d);
+  if (stream) be_->stream_destroy(stream);
+  if (out) be_->host_free_coherent(out);
+  if (va) be_->va_free(va, kBlockSize);
+  for (int i = 0; i < nch; ++i) ha->free(ch[i], 1);
+  if (!T.ok)
+    RT_ERR("gpu %d: stable-VA translation self-test FAILED (%s): stable-VA managed ranges (the transparent "
+           "managed mode) are refused on this GPU",
+           d, T.detail.c_str());
+  return T.ok ? Status::OK : Status::NOT_SUPPORTED;
 }
 
 HostArena* Runtime::host_arena(Tier t, int node) {
@@ -177,6 +263,7 @@ ChunkArena* Runtime::arena_for(const Loc& l) {
     if (!d.hbm) {
       d.hbm = std::make_unique<HbmArena>(be_.get(), l.id, budget, (int)config().hbm_provider);
       d.hbm_live.store(d.hbm.get(), std::memory_order_release);
+      if (d.hbm->init_status() == Status::OK && d.hbm->vmm()) (void)vmm_self_test(l.id);
     }
     return d.hbm.get();
   }
@@ -202,6 +289,7 @@ Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string&
     ChunkArena* a = arena_for(Loc::gpu(stable_dev));
     vg.lock();
     if (!a || !static_cast<HbmArena*>(a)->vmm()) return Status::NOT_SUPPORTED;  // needs hbm_provider=1
+    if (!devs_[stable_dev]->vmm_test.ok) return Status::NOT_SUPPORTED;  // remaps are not seen reliably here
     void* va = nullptr;
     Status st = be_->va_reserve(r->cpu_view_bytes, &va);
     if (st != Status::OK) return st;
@@ -233,7 +321,7 @@ Status Runtime::malloc_managed_at(uint64_t size, uint32_t flags, const std::stri
     vg.unlock();
     ChunkArena* a = arena_for(Loc::gpu(stable_dev));
     vg.lock();
-    if (!a || !static_cast<HbmArena*>(a)->vmm()) return Status::NOT_SUPPORTED;
+    if (!a || !static_cast<HbmArena*>(a)->vmm() || !devs_[stable_dev]->vmm_test.ok) return Status::NOT_SUPPORTED;
     void* va = nullptr;
     Status st = be_->va_reserve(r->cpu_view_bytes, &va, (void*)dev_va);
     if (st != Status::OK) return st;

@@ -33,13 +33,17 @@
 // completes (no host stall in free).
 // The C entry points ogkm_torch_alloc / ogkm_torch_free are what
 // CUDAPluggableAllocator dlsym()s.
+#include <cstdio>
 #include <cstdlib>
 #include <deque>
 #include <mutex>
+#include <stdexcept>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "ogkm/runtime.hpp"
+#include "ogkm/torch_alloc.hpp"
 
 namespace ogkm {
 
@@ -75,7 +79,10 @@ struct DevAlloc {
     uint64_t size;
     uint32_t holds = 0;       // allocation hold + op holds (the lease lives while > 0)
     bool alloc_hold = false;  // the allocation's own hold (dropped by park / the end of the allocating op)
-    bool read_mostly = false;
+    // The lease's extent: the whole allocation for the allocation hold, the
+    // pages of the op's views for an op hold.
+    uint64_t lease_off = 0, lease_len = 0;
+    uint64_t next_use = 0;    // last next-use hint applied (op clock)
     // Long-lived (parameters, buffers, caches): held by two ops at least
     // torch_persistent_ops ops apart. Activations are consumed within a few ops
     // and get a new address every pass; the transparent mode's prefetcher keys
@@ -96,6 +103,7 @@ struct DevAlloc {
   uint64_t allocated = 0, peak = 0, nallocs = 0, stream_waits = 0;
   uint64_t managed_bytes = 0, parks = 0, unparks = 0, op_holds = 0;
   uint64_t op_seq = 0;  // dispatched ops that held managed operands (the persistence clock)
+  std::string last_error;  // last allocation failure (surfaced by ogkm_torch_alloc)
 };
 
 std::mutex g_m;
@@ -156,18 +164,23 @@ void reap_deferred(Runtime* rt, DevAlloc* da) {
   }
 }
 
-// Lease the whole range on `device` (resident in HBM at its stable VA, pinned)
-// and make `stream` wait for the copies that bring it there.
-Status lease_on(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, void* stream, Access access) {
+// Lease [off, off + len) of the range on `device` (resident in HBM at its
+// stable VA, pinned) and make `stream` wait for the copies that bring it there.
+// A zero-copy decision (thrashing pin, accessed_by) is served by a local copy:
+// the stable VA maps HBM only (acquire(allow_remote = false)).
+Status lease_on(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, void* stream, Access access,
+                uint64_t off, uint64_t len) {
   Lease* L = nullptr;
-  Status st = rt->acquire(m.r, 0, m.size, device, access, &L);
+  Status st = rt->acquire(m.r, off, len, device, access, &L, false);
   if (st != Status::OK) return st;
-  if (L->remote) {  // thrashing / accessed-by chose a zero-copy mapping: the stable VA would not map it
+  if (L->remote) {  // cannot happen with allow_remote = false; never hand out a VA that maps nothing
     rt->release(L, stream);
-    return Status::BUSY;
+    return Status::NOT_SUPPORTED;
   }
   order_after(rt, da, L->ready, stream);
   m.lease = L;
+  m.lease_off = off;
+  m.lease_len = len;
   return Status::OK;
 }
 
@@ -182,18 +195,27 @@ void* managed_alloc(Runtime* rt, DevAlloc* da, size_t size, int device, void* st
     da->cache_bytes -= bytes;
     da->cache.erase(da->cache.begin() + (ptrdiff_t)i);
     da->cache_hits++;
+    rt->set_dead(r, false);
     break;
   }
   if (!r) {
-    if (rt->malloc_managed(bytes, RANGE_STABLE_VA | RANGE_NO_CPU_VIEW | RANGE_NO_ZERO_FILL, "torch", &r, device) !=
-        Status::OK)
+    Status st = rt->malloc_managed(bytes, RANGE_STABLE_VA | RANGE_NO_CPU_VIEW | RANGE_NO_ZERO_FILL, "torch", &r,
+                                   device);
+    if (st != Status::OK) {
+      da->last_error = std::string("managed range of ") + std::to_string(bytes) + " bytes: " + status_str(st);
       return nullptr;
+    }
     rt->mem_advise(r, 0, bytes, Advice::SET_PREFERRED_LOCATION, Loc::gpu(device), device);
+    // Reads duplicate (the host copy of evicted data stays valid), writes
+    // revoke only the pages they write: an eviction copies out only pages
+    // written since the tensor last came back (TorchOperand::written).
+    rt->mem_advise(r, 0, bytes, Advice::SET_READ_MOSTLY, Loc::gpu(device), device);
   }
   DevAlloc::Managed m{r, nullptr, bytes};
   m.holds = 1;
   m.alloc_hold = true;
-  if (lease_on(rt, da, m, device, stream, Access::WRITE) != Status::OK) {
+  if (Status st = lease_on(rt, da, m, device, stream, Access::WRITE, 0, bytes); st != Status::OK) {
+    da->last_error = std::string("lease of a ") + std::to_string(bytes >> 20) + " MB managed tensor: " + status_str(st);
     rt->free_range(r);
     return nullptr;
   }
@@ -233,9 +255,11 @@ void* torch_alloc(size_t size, int device, void* stream) {
   if (size == 0) size = 1;
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);
+  da->last_error.clear();
   if (!da->deferred.empty()) reap_deferred(rt, da);
   void* p = torch_alloc_locked(rt, a, da, size, device, stream);
   if (!p && drain_deferred(rt, da)) p = torch_alloc_locked(rt, a, da, size, device, stream);
+  if (!p && da->last_error.empty()) da->last_error = "no free or evictable HBM chunks";
   return p;
 }
 
@@ -243,7 +267,11 @@ void* torch_alloc(size_t size, int device, void* stream) {
 static void* torch_alloc_locked(Runtime* rt, ChunkArena* a, DevAlloc* da, size_t size, int device, void* stream) {
   int cls = class_of(size);
   const int64_t mmin = config().torch_alloc_managed_min_mb;
-  if (mmin > 0 && size >= ((uint64_t)mmin << 20) && static_cast<HbmArena*>(a)->vmm()) {
+  // Managed (stable-VA) tensors need a VMM arena whose remaps passed the
+  // translation self-test; otherwise the tensor is an ordinary arena extent
+  // (it cannot oversubscribe, but it is never read through a stale mapping).
+  if (mmin > 0 && size >= ((uint64_t)mmin << 20) && static_cast<HbmArena*>(a)->vmm() &&
+      rt->dev(device).vmm_test.ok) {
     void* p = managed_alloc(rt, da, size, device, stream);
     if (p) {
       da->nallocs++;
@@ -313,6 +341,7 @@ void torch_free(void* p, int device, void* stream) {
     da->allocated -= m.size;
     da->managed_bytes -= m.size;
     if (m.lease) rt->release(m.lease, stream);
+    rt->set_dead(m.r, true);  // evicting it now copies nothing out; off-GPU copies are dropped
     Tracker t;
     if (f) t.add(f);
     const uint64_t cap = (uint64_t)std::max<int64_t>(0, config().torch_alloc_cache_mb) << 20;
@@ -377,11 +406,28 @@ Status drop_hold(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, void* stream) 
   return st;
 }
 
-// Add one hold; the first one leases the tensor (resident at its VA, pinned;
-// the stream waits GPU-side for the copies). da->m held.
-Status add_hold(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, void* stream, Access access) {
-  if (m.holds++ > 0 && m.lease) return Status::OK;
-  Status st = lease_on(rt, da, m, device, stream, m.read_mostly && access == Access::READ ? Access::READ : access);
+// Add one hold of [off, off + len); the first one leases it (resident at its
+// VA, pinned; the stream waits GPU-side for the copies). A hold beyond the
+// current lease's extent re-leases the whole allocation. da->m held.
+Status add_hold(Runtime* rt, DevAlloc* da, DevAlloc::Managed& m, int device, void* stream, Access access,
+                uint64_t off, uint64_t len) {
+  if (m.holds > 0 && m.lease) {
+    if (off >= m.lease_off && off + len <= m.lease_off + m.lease_len) {
+      m.holds++;
+      return Status::OK;
+    }
+    Lease* old = m.lease;
+    Status st = lease_on(rt, da, m, device, stream, access, 0, m.size);
+    if (st != Status::OK) {
+      m.lease = old;
+      return st;
+    }
+    rt->release(old, stream);
+    m.holds++;
+    return Status::OK;
+  }
+  m.holds++;
+  Status st = lease_on(rt, da, m, device, stream, access, off, len);
   if (st != Status::OK) {
     m.holds--;
     return st;
@@ -413,7 +459,7 @@ Status torch_unpark(void* p, int device, void* stream) {
   auto it = da->managed.find((uint64_t)p);
   if (it == da->managed.end()) return Status::NOT_FOUND;
   if (it->second.alloc_hold) return Status::OK;
-  Status st = add_hold(rt, da, it->second, device, stream, Access::WRITE);
+  Status st = add_hold(rt, da, it->second, device, stream, Access::WRITE, 0, it->second.size);
   if (st == Status::OK) it->second.alloc_hold = true;
   return st;
 }
@@ -433,64 +479,99 @@ void torch_park_all(int device, void* stream) {
   }
 }
 
-// Tensor-granular software faults for one dispatched op (the transparent mode,
+// Software faults for one dispatched op (the transparent mode,
 // open-gpu-kernel-modules_amd/managed.py): every managed storage the op reads
-// or writes gets an op hold - made resident at its stable VA, pinned, the
-// stream ordered after the copies - before the op is enqueued. Non-managed
-// pointers are ignored. Returns the pointers that were held (for op_end).
+// or writes gets an op hold over the pages its views span - made resident at
+// its stable VA (reads duplicate: host copies stay valid), pinned, the stream
+// ordered after the copies - before the op is enqueued. For a written operand
+// the other copies of exactly the written pages are revoked, so the tensor's
+// dirty set is what the op wrote, not the whole allocation (a KV-cache row
+// append dirties 4 KB pages, not the cache). Non-managed pointers are ignored.
+// Returns the pointers that were held (for op_end).
 // Reference: the fault -> service -> replay path of
-// uvm_gpu_replayable_faults.c:2906 at tensor granularity, with the operands
-// declared by the dispatcher instead of reported by the MMU.
-Status torch_op_begin(const std::vector<std::pair<uint64_t, bool>>& ptrs, int device, void* stream,
-                      std::vector<uint64_t>* held, std::vector<uint64_t>* persistent) {
+// uvm_gpu_replayable_faults.c:2906 with the faulted pages declared by the
+// dispatcher instead of reported by the MMU; per-page residency / dirty state
+// as uvm_va_block.h:101-230.
+Status torch_op_begin(const std::vector<TorchOperand>& ops, int device, void* stream, std::vector<uint64_t>* held,
+                      std::vector<uint64_t>* persistent) {
   Runtime* rt = Runtime::get();
   if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);
   if (da->managed.empty()) return Status::OK;
-  // Writers first: a tensor both read and written is leased for writing.
-  std::vector<std::pair<uint64_t, bool>> v;
-  for (auto& pw : ptrs) {
-    if (!da->managed.count(pw.first)) continue;
-    bool dup = false;
-    for (auto& x : v)
-      if (x.first == pw.first) {
-        x.second |= pw.second;
-        dup = true;
-      }
-    if (!dup) v.push_back(pw);
+  // One entry per storage: extents unioned, written intervals collected.
+  std::vector<TorchOperand> v;
+  for (auto& o : ops) {
+    auto mt = da->managed.find(o.ptr);
+    if (mt == da->managed.end()) continue;
+    const uint64_t size = mt->second.size;
+    uint64_t lo = o.hi ? std::min(o.lo, size) : 0, hi = o.hi ? std::min(o.hi, size) : size;
+    if (hi <= lo) continue;  // an empty view touches nothing
+    TorchOperand* x = nullptr;
+    for (auto& y : v)
+      if (y.ptr == o.ptr) x = &y;
+    if (!x) {
+      v.push_back(TorchOperand{o.ptr, false, lo, hi, {}});
+      x = &v.back();
+    } else {
+      x->lo = std::min(x->lo, lo);
+      x->hi = std::max(x->hi, hi);
+    }
+    if (o.write) {
+      x->write = true;
+      if (o.written.empty())
+        x->written.emplace_back(lo, hi);
+      else
+        x->written.insert(x->written.end(), o.written.begin(), o.written.end());
+    }
   }
   if (!v.empty()) da->op_seq++;
-  for (auto& pw : v) {
-    auto& m = da->managed[pw.first];
-    Status st = add_hold(rt, da, m, device, stream, pw.second ? Access::WRITE : Access::READ);
-    if (st != Status::OK) {
-      for (uint64_t p : *held) (void)drop_hold(rt, da, da->managed[p], stream);
-      held->clear();
-      return st;
+  auto undo = [&](Status st) {
+    for (uint64_t p : *held) (void)drop_hold(rt, da, da->managed[p], stream);
+    held->clear();
+    persistent->clear();
+    return st;
+  };
+  for (auto& o : v) {
+    auto& m = da->managed[o.ptr];
+    const uint64_t lo = align_down(o.lo, kPageSize), hi = std::min(align_up(o.hi, kPageSize), m.size);
+    Status st = add_hold(rt, da, m, device, stream, Access::READ, lo, hi - lo);
+    if (st != Status::OK) return undo(st);
+    held->push_back(o.ptr);
+    if (o.write) {
+      st = rt->invalidate_others(m.r, o.written, device);
+      if (st != Status::OK) return undo(st);
     }
-    held->push_back(pw.first);
     if (m.held_once && da->op_seq - m.last_hold_op >= (uint64_t)std::max<int64_t>(1, config().torch_persistent_ops))
       m.persistent = true;
     m.held_once = true;
     m.last_hold_op = da->op_seq;
-    if (m.persistent) persistent->push_back(pw.first);
+    if (m.persistent) persistent->push_back(o.ptr);
     da->op_holds++;
   }
   return Status::OK;
 }
 
-// End of a dispatched op: drop the op holds of `held`, and the allocation hold
-// of every managed operand and output (from its first use as an operand on,
-// a tensor is resident only while an op holds it; a tensor never passed to an
-// op - a library workspace used behind the dispatcher's back - keeps its
-// allocation hold and is never evicted).
-Status torch_op_end(const std::vector<uint64_t>& held, const std::vector<uint64_t>& outs, int device, void* stream) {
+// End of a dispatched op: apply the trace's next-use hints of its operands,
+// then drop the op holds of `held`, and the allocation hold of every managed
+// operand and output (from its first use as an operand on, a tensor is
+// resident only while an op holds it; a tensor never passed to an op - a
+// library workspace used behind the dispatcher's back - keeps its allocation
+// hold and is never evicted).
+Status torch_op_end(const std::vector<uint64_t>& held, const std::vector<uint64_t>& outs, int device, void* stream,
+                    const std::vector<std::pair<uint64_t, uint64_t>>& hints, uint64_t now) {
   Runtime* rt = Runtime::get();
   if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);
   Status res = Status::OK;
+  if (now) rt->set_op_clock(device, now);
+  for (auto& h : hints) {
+    auto it = da->managed.find(h.first);
+    if (it == da->managed.end() || it->second.next_use == h.second) continue;
+    it->second.next_use = h.second;
+    rt->hint_next_use(it->second.r, h.second);
+  }
   auto drop_alloc = [&](uint64_t p) {
     auto it = da->managed.find(p);
     if (it == da->managed.end() || !it->second.alloc_hold) return;
@@ -518,27 +599,55 @@ Status torch_set_read_mostly(void* p, int device, bool on) {
   std::lock_guard<std::mutex> g(da->m);
   auto it = da->managed.find((uint64_t)p);
   if (it == da->managed.end()) return Status::NOT_FOUND;
-  it->second.read_mostly = on;
   return rt->mem_advise(it->second.r, 0, it->second.size, on ? Advice::SET_READ_MOSTLY : Advice::UNSET_READ_MOSTLY,
                         Loc::gpu(device), device);
 }
 
+// cudaMemAdvise on a managed tensor (advice / location / processor as
+// rt.mem_advise: loc_kind 0 gpu, 1 host node, 2 cxl node).
+Status torch_advise(void* p, int device, int advice, int loc_kind, int loc_id, int proc) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return Status::INVALID_ARGUMENT;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  auto it = da->managed.find((uint64_t)p);
+  if (it == da->managed.end()) return Status::NOT_FOUND;
+  Loc loc = loc_kind == 0 ? Loc::gpu(loc_id) : loc_kind == 1 ? Loc::host(loc_id) : Loc::cxl(loc_id);
+  return rt->mem_advise(it->second.r, 0, it->second.size, (Advice)advice, loc, proc);
+}
+
 // Layer-ahead prefetch of managed tensors not currently held: queue their
 // H2D copies (no lease, no stream wait; a later op hold finds them resident or
-// waits for the copies). Returns how many prefetches were queued.
-size_t torch_prefetch(const std::vector<uint64_t>& ptrs, int device) {
+// waits for the copies). Each comes with the op-clock time it is needed at:
+// with next-use hints the prefetch evicts only data needed later than that,
+// or is dropped (VictimFloor) - a window never pushes out what it will need
+// first. Returns how many prefetches were queued.
+size_t torch_prefetch(const std::vector<std::pair<uint64_t, uint64_t>>& ptrs, int device) {
   Runtime* rt = Runtime::get();
   if (!rt || !rt->is_local(device)) return 0;
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);
   size_t n = 0;
-  for (uint64_t p : ptrs) {
-    auto it = da->managed.find(p);
+  for (auto& pw : ptrs) {
+    auto it = da->managed.find(pw.first);
     if (it == da->managed.end() || it->second.holds) continue;
+    if (pw.second && it->second.next_use != pw.second) {
+      it->second.next_use = pw.second;
+      rt->hint_next_use(it->second.r, pw.second);
+    }
+    VictimFloor floor(pw.second);
     Tracker t;
     if (rt->prefetch(it->second.r, 0, it->second.size, Loc::gpu(device), &t, Cause::Prefetch) == Status::OK) ++n;
   }
   return n;
+}
+
+const char* torch_last_error(int device) {
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  static thread_local std::string copy;
+  copy = da->last_error;
+  return copy.c_str();
 }
 
 uint64_t torch_managed_size(void* p, int device) {
@@ -546,6 +655,26 @@ uint64_t torch_managed_size(void* p, int device) {
   std::lock_guard<std::mutex> g(da->m);
   auto it = da->managed.find((uint64_t)p);
   return it == da->managed.end() ? 0 : it->second.size;
+}
+
+uint64_t torch_resident_bytes(void* p, int device) {
+  Runtime* rt = Runtime::get();
+  Range* r = nullptr;
+  {
+    DevAlloc* da = dev_alloc(device);
+    std::lock_guard<std::mutex> g(da->m);
+    auto it = da->managed.find((uint64_t)p);
+    if (!rt || it == da->managed.end()) return 0;
+    r = it->second.r;
+  }
+  uint64_t n = 0;
+  for (uint64_t bi = 0; bi < r->nblocks; ++bi) {
+    ResidencyInfo ri;
+    if (rt->residency_info(r, bi << kBlockShift, &ri) != Status::OK) continue;
+    for (size_t k = 0; k < ri.resident_on.size(); ++k)
+      if (ri.resident_on[k] == Loc::gpu(device)) n += (uint64_t)ri.pages[k] << kPageShift;
+  }
+  return n;
 }
 
 bool torch_is_managed(void* p, int device) {
@@ -576,21 +705,26 @@ void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t
 }  // namespace ogkm
 
 extern "C" {
+// torch's pluggable-allocator path does not check for null (a null tensor
+// would reach a kernel and fault the GPU), so a failed allocation throws: the
+// exception unwinds through torch's allocator call into the aten op, and the
+// Python caller gets a RuntimeError naming the HBM arena's state (catchable -
+// e.g. free tensors and retry - instead of the process aborting).
 __attribute__((visibility("default"))) void* ogkm_torch_alloc(size_t size, int device, void* stream) {
   void* p = ogkm::torch_alloc(size, device, stream);
   if (!p && size) {
-    // torch's pluggable-allocator path does not check for null: a null
-    // tensor would reach a kernel and fault the GPU. Fail loudly on the CPU.
     ogkm::Runtime* rt = ogkm::Runtime::get();
     ogkm::ChunkArena* a = rt ? rt->arena_for(ogkm::Loc::gpu(device)) : nullptr;
     ogkm::ChunkArena::Stats st = a ? a->stats() : ogkm::ChunkArena::Stats{};
-    RT_ERR("torch allocation of %zu bytes on gpu %d failed: HBM arena %llu MB, allocated %llu MB, pinned %llu MB "
-           "(pinned = leased / held tensors + allocator slabs + tensors never used as an operand, e.g. library "
-           "workspaces). Raise the HBM budget or lower the working set of one op; aborting instead of returning "
-           "a null device pointer.",
-           size, device, (unsigned long long)(st.capacity >> 20), (unsigned long long)(st.allocated >> 20),
-           (unsigned long long)(st.pinned >> 20));
-    std::abort();
+    char msg[768];
+    snprintf(msg, sizeof(msg),
+             "ogkm: out of memory: torch allocation of %zu bytes on gpu %d failed (%s). HBM arena %llu MB, "
+             "allocated %llu MB, pinned %llu MB (pinned = leased / held tensors + allocator slabs + tensors never "
+             "used as an operand, e.g. library workspaces). Raise the HBM budget or lower the working set of one op.",
+             size, device, ogkm::torch_last_error(device), (unsigned long long)(st.capacity >> 20),
+             (unsigned long long)(st.allocated >> 20), (unsigned long long)(st.pinned >> 20));
+    RT_ERR("%s", msg);
+    throw std::runtime_error(msg);
   }
   return p;
 }

@@ -45,6 +45,8 @@ struct ChunkInfo {
   Block* owner = nullptr;
   int32_t prev = -1, next = -1;  // LRU links
   uint64_t last_use = 0;         // logical clock
+  uint64_t next_use = 0;         // op clock of the owner's next use (0 = unknown, kDeadUse = never)
+  uint64_t last_op = 0;          // op clock at the last touch
   Tracker reuse_fence;           // work that must finish before the chunk is overwritten
 };
 
@@ -117,6 +119,20 @@ class ChunkArena {
   // which costs a copy-out and a refill, stays in the protected list).
   void touch(uint32_t i, bool has_data, bool preferred = false, bool prefetched = false, uint64_t refault_key = 0,
              uint64_t evicted_at = 0, bool clean = false);
+  // Next-use (Belady) victim order. Once any chunk carries a hint the
+  // evictable chunks are ranked by the op clock of their next use instead of
+  // recency: dead data first, then unhinted data by age (data not seen for a few
+  // ops; just-touched unhinted data counts as needed next), then hinted data
+  // furthest in the future first - the optimal replacement order for a known
+  // access sequence (a cyclic decode step under LRU evicts every block just
+  // before its next use). Victims never have a next use before the thread's
+  // VictimFloor (a prefetch must not evict data needed before its own).
+  void set_next_use(uint32_t i, uint64_t when);
+  void set_op_clock(uint64_t now);
+  bool next_use_mode() {
+    std::lock_guard<OrderedMutex> g(m_);
+    return hinted_;
+  }
   uint64_t evictions() {
     std::lock_guard<OrderedMutex> g(m_);
     return st_.evictions;
@@ -148,6 +164,12 @@ class ChunkArena {
 
  private:
   int32_t pick_victim_locked();  // coldest evictable chunk (reserve(1) order), -1 = none
+  uint64_t victim_key_locked(const ChunkInfo& c) const;  // next-use mode: larger = evict sooner
+  bool floor_protects_locked(const ChunkInfo& c, uint64_t floor) const;
+  // next-use mode: up to n evictable chunks with the largest keys above the floor
+  void pick_victims_by_next_use_locked(uint32_t n, std::vector<uint32_t>* out);
+  bool hinted_ = false;
+  uint64_t op_clock_ = 0;
   void lru_remove(uint32_t i);
   void lru_push_tail(uint32_t i, uint8_t list);
   void take_run(uint32_t first, uint32_t n);  // remove [first,first+n) from free runs
@@ -216,6 +238,20 @@ class HostArena : public ChunkArena {
   bool numa_bound_ = false;
   bool thp_advised_ = false;
   Status init_ = Status::OK;
+};
+
+constexpr uint64_t kDeadUse = ~0ull;  // ChunkInfo::next_use of dead data
+
+// Scoped lower bound on the next-use key of eviction victims for the calling
+// thread (next-use mode only): a prefetch of data needed at op T evicts only
+// data needed after T, or nothing.
+struct VictimFloor {
+  static uint64_t& value();
+  uint64_t saved;
+  explicit VictimFloor(uint64_t floor) : saved(value()) { value() = floor; }
+  ~VictimFloor() { value() = saved; }
+  VictimFloor(const VictimFloor&) = delete;
+  VictimFloor& operator=(const VictimFloor&) = delete;
 };
 
 constexpr uint64_t kHostSegment = 1ull << 30;

@@ -184,6 +184,8 @@ enum class Counter : int {
   TlbFlushes,       // GPU translation flushes after stable-VA remaps
   FaultsCancelled,  // channels whose device faults were cancelled (precise cancel)
   TlbFlushesElided, // stable-VA maps that needed no flush (a flush since the VA's last unmap covered it)
+  WriteInvalidations,  // blocks whose other copies were revoked for a page-granular write (invalidate_others)
+  RemoteFallbacks,     // remote (zero-copy) decisions served by a local copy (acquire allow_remote=false)
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -87,8 +87,23 @@ struct Lease {
   Tracker ready;         // consumer must wait on this before use
 };
 
+// Init-time check that a stable-VA remap followed by a translation flush is
+// seen by kernels on this GPU (Runtime::vmm_self_test): a canary VA is
+// remapped between two chunks of known contents and read through the shader
+// path after every flush (and once before it, to record whether the stack
+// leaves stale translations at all). A failed check refuses stable-VA ranges
+// - the transparent managed mode - instead of risking silent stale reads
+// (the reference invalidates explicitly, uvm_hal.h:797-799, in batches,
+// uvm_tlb_batch.c:27-116).
+struct VmmSelfTest {
+  bool ran = false, ok = true;
+  uint32_t rounds = 0, flushed_ok = 0, unflushed_stale = 0;
+  std::string detail;
+};
+
 struct Device {
   int id = 0;
+  VmmSelfTest vmm_test;
   int numa = 0;
   // Managed by this process (config local_devices). One process per GPU keeps
   // every other GPU non-local: no rings, fault buffer or arena are created on
@@ -116,6 +131,10 @@ struct Injection {
   std::atomic<int64_t> host_alloc_error{0};    // next N host chunk allocs fail
   std::atomic<int64_t> async_copy_error{0};     // next N ring completions report a post-submission failure
   std::atomic<int64_t> ecc_ue{0}, ecc_ce{0}, link_ue{0};  // fake backend RAS counters
+  // Fake backend translation model: 0 coherent (a remap is visible at once),
+  // 1 stale until tlb_flush (what gfx950 VMM does), 2 stale and tlb_flush
+  // ineffective (a box where the flush does not work).
+  std::atomic<int> tlb_mode{0};
 };
 
 struct ResidencyInfo {   // UVM_TEST_VA_RESIDENCY_INFO analog (uvm_test_ioctl.h:626-674)
@@ -153,6 +172,8 @@ class Runtime {
 
   // ---- tiers
   Status init_device(int d, uint64_t budget_bytes);   // (re)create the HBM arena of d
+  // Run the stable-VA translation self-test on d's (VMM) arena; see VmmSelfTest.
+  Status vmm_self_test(int d);
   HostArena* host_arena(Tier t, int node);            // created on first use
   ChunkArena* arena_for(const Loc& l);
   // nullptr for a non-local device
@@ -184,8 +205,21 @@ class Runtime {
 
   // ---- software faults / leases
   Status service_faults(std::vector<FaultEntry>& faults, Tracker* out);
-  Status acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out);
+  // allow_remote = false: a zero-copy (remote) decision - thrashing pin,
+  // accessed_by - is overridden by a local copy (callers that need the data at a
+  // fixed device address, e.g. the stable VA of a managed torch tensor).
+  Status acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out,
+                 bool allow_remote = true);
   Status release(Lease* l, void* stream);  // consumer's last use recorded on `stream`
+  // Page-granular write fault: revoke the other copies of these byte intervals
+  // of r (resident on gpu) so only written pages are dirty.
+  Status invalidate_others(Range* r, const std::vector<std::pair<uint64_t, uint64_t>>& bytes, int gpu);
+  // Next-use (Belady) eviction hints: the op-clock time of r's next use, and the
+  // current op clock of a device's HBM arena (see ChunkArena::set_next_use).
+  void hint_next_use(Range* r, uint64_t when);
+  void set_op_clock(int dev, uint64_t now);
+  // Mark r's contents dead (free: no copy-out, off-GPU copies dropped) or live.
+  void set_dead(Range* r, bool dead);
   Lease* lease_by_id(uint64_t id);
   Status cpu_fault(uint64_t addr, bool write);        // SIGSEGV path
   // Several CPU faults (addr, write) serviced as one batch; out[i] per fault.

@@ -172,6 +172,13 @@ class Range {
   RangeGroup* group = nullptr;
   std::vector<std::unique_ptr<Block>> blocks;
   std::atomic<int64_t> views{0};  // live tensor views / leases
+  // Op-clock time of the range's next use (0 = unknown), from a recorded
+  // access trace (the transparent mode, torch_allocator.cpp): its HBM chunks
+  // then carry it and eviction picks the data used furthest in the future.
+  std::atomic<uint64_t> next_use{0};
+  // Contents are dead (a freed torch allocation waiting for reuse or for its
+  // stream fence): evicting its blocks copies nothing out.
+  std::atomic<bool> dead{false};
   bool destroyed = false;
   OrderedMutex place_lock{LockOrder::RANGE_PLACE};  // GPU extent placement
 

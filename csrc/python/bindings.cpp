@@ -2,6 +2,7 @@
 // open-gpu-kernel-modules_amd/_native.py). Thin: every call maps to one Runtime
 // operation; Status codes become Python exceptions with the status name.
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include <hip/hip_runtime.h>
@@ -12,26 +13,11 @@
 #include "ogkm/kernels.hpp"
 #include "ogkm/lock_order.hpp"
 #include "ogkm/runtime.hpp"
+#include "ogkm/torch_alloc.hpp"
 
 namespace py = pybind11;
 using namespace ogkm;
 
-namespace ogkm {
-void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits);
-void* torch_alloc(size_t size, int device, void* stream);
-void torch_free(void* p, int device, void* stream);
-Status torch_park(void* p, int device, void* stream);
-Status torch_unpark(void* p, int device, void* stream);
-void torch_managed_stats(int device, uint64_t* active, uint64_t* parked, uint64_t* parks, uint64_t* unparks);
-void torch_park_all(int device, void* stream);
-Status torch_op_begin(const std::vector<std::pair<uint64_t, bool>>& ptrs, int device, void* stream,
-                      std::vector<uint64_t>* held, std::vector<uint64_t>* persistent);
-Status torch_op_end(const std::vector<uint64_t>& held, const std::vector<uint64_t>& outs, int device, void* stream);
-Status torch_set_read_mostly(void* p, int device, bool on);
-bool torch_is_managed(void* p, int device);
-size_t torch_prefetch(const std::vector<uint64_t>& ptrs, int device);
-uint64_t torch_managed_size(void* p, int device);
-}  // namespace ogkm
 
 namespace {
 
@@ -535,6 +521,15 @@ PYBIND11_MODULE(_ogkm, m) {
       torch_alloc_stats(g, &al, &pk, &na, &sw);
       a["torch_allocated"] = al;
       a["torch_peak"] = pk;
+      const VmmSelfTest& T = r->dev(g).vmm_test;
+      py::dict vt;
+      vt["ran"] = T.ran;
+      vt["ok"] = T.ok;
+      vt["rounds"] = T.rounds;
+      vt["flushed_ok"] = T.flushed_ok;
+      vt["unflushed_stale"] = T.unflushed_stale;
+      vt["detail"] = T.detail;
+      a["vmm_selftest"] = vt;
       arenas.append(a);
     }
     for (int t = 1; t <= 2; ++t)
@@ -585,6 +580,10 @@ PYBIND11_MODULE(_ogkm, m) {
     out["now"] = h2d(d.health);
     out["status"] = status_str(st);
     return out;
+  });
+  m.def("vmm_self_test", [](int dev) {
+    Status st = rt()->vmm_self_test(dev);
+    return st == Status::OK;
   });
   m.def("inject_ras", [](int64_t ue, int64_t ce, int64_t link_ue) {
     rt()->inject().ecc_ue.store(ue);
@@ -995,6 +994,7 @@ PYBIND11_MODULE(_ogkm, m) {
     else if (kind == "populate_error") in.populate_error.store(v);
     else if (kind == "host_alloc_error") in.host_alloc_error.store(v);
     else if (kind == "async_copy_error") in.async_copy_error.store(v);
+    else if (kind == "tlb_mode") in.tlb_mode.store((int)v);
     else throw StatusError("unknown injection " + kind);
   });
 
@@ -1152,34 +1152,62 @@ PYBIND11_MODULE(_ogkm, m) {
   }, py::arg("ptr"), py::arg("dev"), py::arg("stream") = 0);
   m.def("torch_park_all", [](int dev, uint64_t stream) { torch_park_all(dev, (void*)stream); },
         py::arg("dev"), py::arg("stream") = 0);
-  m.def("torch_op_begin", [](const std::vector<std::pair<uint64_t, bool>>& ptrs, int dev, uint64_t stream) {
+  // operands: [(storage_ptr, write, lo, hi, written)] - lo/hi the byte extent
+  // of the op's views (hi == 0: whole allocation), written None (the whole
+  // extent) or a flat int64 array of [start, end) byte pairs.
+  m.def("torch_op_begin", [](py::list operands, int dev, uint64_t stream) {
+    std::vector<TorchOperand> ops;
+    ops.reserve(operands.size());
+    for (auto item : operands) {
+      auto t = item.cast<py::tuple>();
+      TorchOperand o;
+      o.ptr = t[0].cast<uint64_t>();
+      o.write = t[1].cast<bool>();
+      if (t.size() >= 4) {  // (ptr, write) alone: the whole allocation
+        o.lo = t[2].cast<uint64_t>();
+        o.hi = t[3].cast<uint64_t>();
+      }
+      if (t.size() > 4 && !t[4].is_none()) {
+        auto a = t[4].cast<py::array_t<int64_t, py::array::c_style | py::array::forcecast>>();
+        auto r = a.unchecked<1>();
+        if (r.shape(0) % 2) throw StatusError("torch_op_begin: written intervals must come in pairs");
+        for (py::ssize_t i = 0; i + 1 < r.shape(0); i += 2) o.written.emplace_back((uint64_t)r(i), (uint64_t)r(i + 1));
+      }
+      ops.push_back(std::move(o));
+    }
     std::vector<uint64_t> held, persistent;
     Status st;
     {
       py::gil_scoped_release nogil;
-      st = torch_op_begin(ptrs, dev, (void*)stream, &held, &persistent);
+      st = torch_op_begin(ops, dev, (void*)stream, &held, &persistent);
     }
     check(st, "torch_op_begin");
     return py::make_tuple(held, persistent);
   });
   m.def("torch_op_end", [](const std::vector<uint64_t>& held, const std::vector<uint64_t>& outs, int dev,
-                           uint64_t stream) {
+                           uint64_t stream, const std::vector<std::pair<uint64_t, uint64_t>>& hints, uint64_t now) {
     Status st;
     {
       py::gil_scoped_release nogil;
-      st = torch_op_end(held, outs, dev, (void*)stream);
+      st = torch_op_end(held, outs, dev, (void*)stream, hints, now);
     }
     check(st, "torch_op_end");
+  }, py::arg("held"), py::arg("outs"), py::arg("dev"), py::arg("stream"),
+     py::arg("hints") = std::vector<std::pair<uint64_t, uint64_t>>{}, py::arg("now") = 0);
+  m.def("torch_advise", [](uint64_t p, int dev, int advice, int loc_kind, int loc_id, int proc) {
+    check(torch_advise((void*)p, dev, advice, loc_kind, loc_id, proc), "torch_advise");
   });
+  m.def("torch_last_error", [](int dev) { return std::string(torch_last_error(dev)); });
   m.def("torch_set_read_mostly", [](uint64_t p, int dev, bool on) {
     check(torch_set_read_mostly((void*)p, dev, on), "torch_set_read_mostly");
   });
   m.def("torch_is_managed", [](uint64_t p, int dev) { return torch_is_managed((void*)p, dev); });
-  m.def("torch_prefetch", [](const std::vector<uint64_t>& ptrs, int dev) {
+  m.def("torch_prefetch", [](const std::vector<std::pair<uint64_t, uint64_t>>& ptrs, int dev) {
     py::gil_scoped_release nogil;
     return torch_prefetch(ptrs, dev);
   });
   m.def("torch_managed_size", [](uint64_t p, int dev) { return torch_managed_size((void*)p, dev); });
+  m.def("torch_resident_bytes", [](uint64_t p, int dev) { return torch_resident_bytes((void*)p, dev); });
   m.def("torch_managed_stats", [](int dev) {
     uint64_t a, p, np, nu;
     torch_managed_stats(dev, &a, &p, &np, &nu);

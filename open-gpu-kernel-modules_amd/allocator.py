@@ -99,6 +99,24 @@ def set_read_mostly(*tensors, on: bool = True) -> None:
         lib.torch_set_read_mostly(p, d, on)
 
 
+def advise(t, advice: int, loc=None, proc: int | None = None) -> None:
+    """cudaMemAdvise on a managed tensor (``advice`` = rt.ADVISE_*; ``loc`` as
+    in rt.mem_advise, e.g. "gpu:0" / "host:1" / "cxl:2"; ``proc`` the accessing
+    processor for SET_ACCESSED_BY). Under ``ogkm.managed()`` a decision to
+    access the tensor remotely (accessed_by, a thrashing pin) is served by a
+    local copy: the tensor's device address maps HBM only."""
+    from .rt import CPU, Loc
+
+    p, d = _base(t)
+    kind, i = Loc.parse(loc).code if loc is not None else (0, d)
+    lib.torch_advise(p, d, int(advice), int(kind), int(i), d if proc is None else (CPU if proc == "cpu" else int(proc)))
+
+
+def last_error(device: int = 0) -> str:
+    """Why the last allocation on ``device`` failed (empty: it did not)."""
+    return lib.torch_last_error(device)
+
+
 def is_managed(t) -> bool:
     p, d = _base(t)
     return lib.torch_is_managed(p, d)

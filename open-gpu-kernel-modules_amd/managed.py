@@ -21,11 +21,20 @@ replay, ``uvm_gpu_replayable_faults.c:2906``), the CPU fault entry
 declared by the dispatcher instead of reported by the MMU (no XNACK on this
 stack: SURVEY.md §7.1 design (1)).
 
-Layer-ahead prefetch (the D26 prefetcher at op granularity): the mode records
-the sequence of managed operand sets of the first pass; on later passes it
-recognises its position and prefetches the operands of the next ops (up to
-``lookahead_bytes``) right after enqueueing the current one, so the H2D copies
-overlap compute.
+Operand geometry: an op hold covers only the pages its views of a storage
+span (storage offset, sizes, strides), and a written view revokes the other
+copies of exactly the 4 KB pages it writes - reads duplicate, so an evicted
+tensor's host copy stays valid and only what was written since goes back
+(a KV-cache row append dirties B x H pages, not the cache).
+
+Layer-ahead prefetch and next-use eviction (the D26 prefetcher at op
+granularity, with Belady replacement): the mode records the sequence of
+persistent operand sets of the first pass; on later passes it recognises its
+position, tells the runtime when each operand is needed next (the arena then
+evicts the data needed furthest in the future instead of the least recently
+used - which, on a cyclic decode step larger than HBM, is exactly the data
+needed next), and prefetches the operands of the next ops (up to
+``lookahead_bytes``), each allowed to evict only data needed after it.
 
 Tensors become managed when the pluggable allocator is enabled in managed
 mode (``allocator.enable(managed_min_mb=N)``, before the first CUDA
@@ -58,24 +67,28 @@ def _mode_class():
         return frozenset(pos), frozenset(names)
 
     class ManagedMode(TorchDispatchMode):
+        device_type = "cuda"
+
         def __init__(self, device: int = 0, lookahead_bytes: Optional[int] = None):
             super().__init__()
             self.device = int(device)
-            # default: a short window - min(512 MB, arena / 16). Measured on the
-            # stock 8B model at 2x (12.3 GB arena): 512 MB -> 134 tok/s, 256 MB
-            # 125, 0 (no prefetch) 117, 1 GB 62, 2 GB 6.7, a quarter of the arena
-            # 4.8: every prefetched tensor is LRU-fresh, so a long window evicts
-            # operands needed before the prefetched ones and the passes thrash
+            # default: an eighth of the arena. With next-use eviction a longer
+            # window cannot push out operands needed before the prefetched ones
+            # (each prefetch evicts only data needed after it, or is dropped);
+            # under plain LRU anything above ~512 MB thrashed
             # (profiles/r3_managed_lookahead.txt).
             if lookahead_bytes is None:
-                lookahead_bytes = min(512 << 20, _arena_capacity(self.device) // 16)
+                lookahead_bytes = _arena_capacity(self.device) // 8
             self.lookahead_bytes = int(lookahead_bytes)
             self._writes: dict = {}
             self._sizes: dict[int, int] = {}
             self._trace: list[tuple[int, ...]] = []   # operand sets of the recorded pass
             self._first: dict[tuple[int, ...], int] = {}
+            self._nextd: list[dict[int, int]] = []    # per position: operand -> positions to its next use
             self._pos = -1
+            self._abs = 0          # op clock: trace positions passed since recording ended
             self._recording = True
+            self._requested: dict[int, int] = {}  # operand -> op-clock time a prefetch was queued for
             self.ops = 0
             self.faulted_ops = 0
             # OGKM_MODE_TRACE=N: remember the last N ops, printed when one fails.
@@ -103,14 +116,18 @@ def _mode_class():
             if w is None:
                 w = self._writes[func] = _writes_of(func)
             wpos, wnames = w
-            ptrs: list[tuple[int, bool]] = []
+            operands: list = []
+            dev_type = self.device_type
 
             def add(x, write: bool):
                 if isinstance(x, torch.Tensor):
-                    if x.device.type == "cuda" and (x.device.index or 0) == self.device:
-                        p = x.untyped_storage().data_ptr()
+                    if x.device.type == dev_type and (x.device.index or 0) == self.device:
+                        st = x.untyped_storage()
+                        p = st.data_ptr()
                         if p:
-                            ptrs.append((p, write))
+                            op = _operand(x, p, st.nbytes(), write)
+                            if op is not None:
+                                operands.append(op)
                 elif isinstance(x, (list, tuple)):
                     for y in x:
                         add(y, write)
@@ -119,14 +136,17 @@ def _mode_class():
                 add(a, i in wpos)
             for k, a in kwargs.items():
                 add(a, k in wnames)
-            stream = self._stream() if ptrs else 0
-            held, persistent = lib.torch_op_begin(ptrs, self.device, stream) if ptrs else ((), ())
+            stream = self._stream() if operands else 0
+            held, persistent = lib.torch_op_begin(operands, self.device, stream) if operands else ((), ())
             self.ops += 1
             if self._last is not None:
                 self._last.append((self.ops, func.__name__, len(held)))
             out = None  # an op that raises allocated nothing: its holds are still dropped below
+            done = False
+            hints, want = (), ()
             try:
                 out = func(*args, **kwargs)
+                done = True
             except BaseException:
                 if self._last is not None:
                     import sys
@@ -135,22 +155,26 @@ def _mode_class():
                           file=sys.stderr, flush=True)
                 raise
             finally:
+                # Position in the trace (long-lived operands key it: activations
+                # get new addresses every pass) -> next-use hints and prefetches.
+                if persistent and done:
+                    hints, want = self._advance(tuple(persistent))
                 # Outputs the op allocated hold their allocation lease: drop it.
                 outs = []
-                flat, _ = tree_flatten(out)
-                for t in flat:
-                    if isinstance(t, torch.Tensor) and t.device.type == "cuda":
-                        p = t.untyped_storage().data_ptr()
-                        if p:
-                            outs.append(p)
+                if out is not None:
+                    flat, _ = tree_flatten(out)
+                    for t in flat:
+                        if isinstance(t, torch.Tensor) and t.device.type == dev_type:
+                            p = t.untyped_storage().data_ptr()
+                            if p:
+                                outs.append(p)
                 if held or outs:
-                    lib.torch_op_end(held, outs, self.device, stream or self._stream())
+                    lib.torch_op_end(list(held), outs, self.device, stream or self._stream(), list(hints),
+                                     self._abs if not self._recording else 0)
             if held:
                 self.faulted_ops += 1
-            if persistent:
-                # Position key: the long-lived operands (parameters / buffers);
-                # activations get new addresses every pass.
-                self._advance(tuple(persistent))
+            if want:
+                self.prefetches += lib.torch_prefetch(want, self.device)
             return out
 
         # ---------------------------------------------------------- multi-tensor ops
@@ -193,45 +217,69 @@ def _mode_class():
         def _arena_bytes(self) -> int:
             return _arena_capacity(self.device) or (1 << 62)
 
-        # ---------------------------------------------------------- prefetch
-        def _advance(self, key: tuple[int, ...]) -> None:
-            """Track the position in the recorded operand sequence and prefetch
-            the operands of the ops that follow."""
-            if self.lookahead_bytes <= 0:
-                return
+        # ---------------------------------------------------------- trace / prefetch
+        def _advance(self, key: tuple[int, ...]):
+            """Track the position in the recorded operand sequence. Returns the
+            next-use hints of this op's operands [(ptr, op clock)] and the
+            prefetches to queue [(ptr, op clock it is needed at)]."""
             n = len(self._trace)
             nxt = self._pos + 1
             if n and nxt < n and self._trace[nxt] == key:
-                self._pos = nxt
+                new = nxt
             elif key in self._first:
-                self._pos = self._first[key]
-                self._recording = False
+                new = self._first[key]
+                if self._recording:
+                    self._recording = False
+                    self._build_next_use()
             elif self._recording:
                 self._first[key] = n
                 self._trace.append(key)
                 self._pos = n
-                return
+                return (), ()
             else:
-                return
+                return (), ()  # an op outside the recorded pass
             if self._recording:
-                return
-            want, seen, budget = [], set(key), self.lookahead_bytes
-            i = self._pos + 1
-            while budget > 0 and i < self._pos + 1 + len(self._trace):
-                for p in self._trace[i % len(self._trace)]:
-                    if p in seen:
-                        continue
-                    seen.add(p)
-                    sz = self._sizes.get(p)
-                    if sz is None:
-                        sz = self._sizes[p] = lib.torch_managed_size(p, self.device)
-                    budget -= sz
-                    if budget < 0:
+                self._pos = new
+                return (), ()
+            step = (new - self._pos) % n if self._pos >= 0 else 0
+            self._abs += step if step else n
+            self._pos = new
+            now = self._abs
+            nd = self._nextd[new]
+            hints = [(p, now + nd[p]) for p in key]
+            want = []
+            if self.lookahead_bytes > 0:
+                seen, budget = set(key), self.lookahead_bytes
+                for j in range(1, n + 1):
+                    if budget <= 0:
                         break
-                    want.append(p)
-                i += 1
-            if want:
-                self.prefetches += lib.torch_prefetch(want, self.device)
+                    for p in self._trace[(new + j) % n]:
+                        if p in seen:
+                            continue
+                        seen.add(p)
+                        sz = self._sizes.get(p)
+                        if sz is None:
+                            sz = self._sizes[p] = lib.torch_managed_size(p, self.device)
+                        budget -= sz
+                        if budget < 0:
+                            break
+                        at = now + j
+                        if self._requested.get(p) != at:
+                            self._requested[p] = at
+                            want.append((p, at))
+            return hints, want
+
+        def _build_next_use(self) -> None:
+            """For every position: positions until each operand's next use (cyclic)."""
+            n = len(self._trace)
+            last: dict[int, int] = {}
+            nextd: list[dict[int, int]] = [dict() for _ in range(n)]
+            for i in range(2 * n - 1, -1, -1):
+                for p in self._trace[i % n]:
+                    if i < n:
+                        nextd[i][p] = last[p] - i if p in last else n
+                    last[p] = i
+            self._nextd = nextd
 
     _MODE_CLS = ManagedMode
     return ManagedMode
@@ -239,6 +287,63 @@ def _mode_class():
 
 _METADATA_OPS: frozenset = frozenset()
 _NOT_SPLIT = object()
+_MAX_RUNS = 16384  # contiguous runs enumerated per written view (beyond: its bounding extent)
+
+
+def _operand(x, ptr: int, nbytes: int, write: bool) -> tuple:
+    """(storage ptr, write, lo, hi, written) of one tensor argument: the byte
+    extent its view spans in the storage (hi == 0: all of it) and, for a
+    written non-contiguous view, the 4 KB-page intervals it writes (a flat
+    int64 array of [start, end) pairs; None: the whole extent). Conservative by
+    construction - every byte the view can address is inside."""
+    es = x.element_size()
+    off = x.storage_offset() * es
+    n = x.numel()
+    if n == 0:
+        return None  # touches nothing
+    if x.is_contiguous():
+        lo, hi = off, off + n * es
+        if lo == 0 and hi >= nbytes:
+            return (ptr, write, 0, 0, None)
+        return (ptr, write, lo, hi, None)
+    dims = [(s, st * es) for s, st in zip(x.shape, x.stride()) if s > 1 and st != 0]
+    hi = off + sum((s - 1) * st for s, st in dims) + es
+    if not write:
+        return (ptr, False, off, hi, None)
+    return (ptr, True, off, hi, _written_pages(off, es, dims))
+
+
+def _written_pages(off: int, es: int, dims: list):
+    """Page intervals (bytes, flat [start, end) pairs) addressed by a strided
+    view: the innermost dims that are contiguous form runs; the runs' start
+    offsets are enumerated and merged page by page. None when there are more
+    than _MAX_RUNS runs (the caller then uses the bounding extent)."""
+    import numpy as np
+
+    dims = sorted(dims, key=lambda d: d[1])
+    run, k = es, 0
+    while k < len(dims) and dims[k][1] == run:
+        run *= dims[k][0]
+        k += 1
+    outer = dims[k:]
+    cnt = 1
+    for s, _ in outer:
+        cnt *= s
+    if cnt > _MAX_RUNS:
+        return None
+    starts = np.array([off], dtype=np.int64)
+    for s, st in outer:
+        starts = (starts[:, None] + np.arange(s, dtype=np.int64) * st).ravel()
+    p0 = np.sort(starts) >> 12
+    p1 = (np.sort(starts) + (run - 1)) >> 12
+    end = np.maximum.accumulate(p1)
+    new = np.empty(len(p0), dtype=bool)
+    new[0] = True
+    new[1:] = p0[1:] > end[:-1] + 1
+    idx = np.flatnonzero(new)
+    lo_p = p0[idx]
+    hi_p = np.append(end[idx[1:] - 1], end[-1])
+    return np.stack([lo_p << 12, (hi_p + 1) << 12], axis=1).ravel()
 
 
 def _arena_capacity(device: int) -> int:
@@ -257,6 +362,12 @@ def managed(device: int = 0, lookahead_bytes: Optional[int] = None):
     global _METADATA_OPS
     import torch
 
+    if lib.is_initialized():
+        for a in lib.stats().get("arenas", []):
+            t = a.get("vmm_selftest", {})
+            if a["name"] == f"hbm{device}" and t.get("ran") and not t.get("ok"):
+                raise RuntimeError(f"ogkm.managed(): GPU {device} failed the stable-VA translation self-test "
+                                   f"({t.get('detail')}); the transparent mode would risk stale reads and is off")
     if not _METADATA_OPS:
         aten = torch.ops.aten
         _METADATA_OPS = frozenset({aten.detach.default, aten.sym_size.int, aten.sym_stride.int,

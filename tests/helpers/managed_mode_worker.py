@@ -98,9 +98,22 @@ def main() -> None:
     param_bytes = sum(p.numel() * p.element_size() for p in model.parameters())
     mode = ogkm.managed()
     t0 = time.perf_counter()
+    advised = 0
     with mode:
         model = model.cuda()
         print("model on gpu", flush=True)
+        if "--advise" in sys.argv:
+            # Every 4th weight prefers host DRAM and is accessed_by the GPU: the
+            # runtime decides to access it remotely once it rests in host DRAM,
+            # which the stable VA cannot map - served by a local copy instead.
+            from ogkm._native import lib
+
+            for i, p in enumerate(model.parameters()):
+                if i % 4 == 0 and allocator.is_managed(p):
+                    allocator.set_read_mostly(p, on=False)
+                    allocator.advise(p, rt.ADVISE_SET_PREFERRED_LOCATION, f"host:{lib.host_node()}")
+                    allocator.advise(p, rt.ADVISE_SET_ACCESSED_BY, proc=0)
+                    advised += 1
         res = run(model, x.cuda(), log=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -110,7 +123,9 @@ def main() -> None:
                          "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches,
                          "evictions": st["evictions"], "htd_mb": st["bytes_xfer_htd"] >> 20,
                          "dth_mb": st["bytes_xfer_dth"] >> 20, "vmm_remaps": st["vmm_remaps"],
-                         "tlb_flushes": st["tlb_flushes"], "vmm_errors": st["vmm_errors"], "seconds": round(dt, 3)})
+                         "tlb_flushes": st["tlb_flushes"], "vmm_errors": st["vmm_errors"], "seconds": round(dt, 3),
+                         "advised": advised, "remote_fallbacks": st["remote_fallbacks"],
+                         "write_invalidations": st["write_invalidations"]})
 
 
 if __name__ == "__main__":

@@ -237,3 +237,207 @@ def test_cyclic_remaps_elide_covered_flushes(managed_rt):
     assert flushes < 24  # at most one per unpark; covered maps flush nothing
     for p in ptrs:
         lib.torch_free(p, 0)
+
+
+def _cycle(ptrs, skip=()):
+    """Hold each tensor for one read op (pushes the others out of a small arena)."""
+    for p in ptrs:
+        if p in skip:
+            continue
+        held, _ = lib.torch_op_begin([(p, False)], 0, 0)
+        lib.torch_op_end(held, [], 0, 0)
+
+
+def test_partial_write_dirties_only_written_pages(managed_rt):
+    """A written view revokes the host copy of only the pages it writes: after
+    a read brought the tensor back (duplicated), a one-row write followed by an
+    eviction copies out those pages, not the tensor (per-page dirty state,
+    uvm_va_block.h:101-230)."""
+    lib.configure("perf_workingset_active_pct", 0)  # plain LRU: every tensor of the cycle is evicted each pass
+    lib.init_device(0, 32 * MB)  # (the arena reads it at creation)
+    n = 8 * MB
+    p = lib.torch_alloc(n, 0)
+    ref = np.arange(n // 4, dtype=np.int32)
+    _write(p, ref)
+    held, _ = lib.torch_op_begin([(p, True)], 0, 0)
+    lib.torch_op_end(held, [p], 0, 0)
+    others = [lib.torch_alloc(8 * MB, 0) for _ in range(4)]
+    for q in others:
+        held, _ = lib.torch_op_begin([(q, True)], 0, 0)
+        lib.torch_op_end(held, [q], 0, 0)
+    _cycle([p] + others)
+    _cycle([p] + others)  # 5 x 8 MB cycled through 32 MB: every tensor was evicted, each has a host copy
+    # read: resident in HBM as a duplicate of its host copy
+    held, _ = lib.torch_op_begin([(p, False)], 0, 0)
+    lib.torch_op_end(held, [], 0, 0)
+    # write 3 scattered 1 KB rows (pages 1, 700, 1500) through a strided view
+    rows = [1 * 4096 + 64, 700 * 4096 + 8, 1500 * 4096 + 1000]
+    written = np.array([x for r in rows for x in (r & ~4095, (r & ~4095) + 4096)], dtype=np.int64)
+    held, _ = lib.torch_op_begin([(p, True, rows[0], rows[-1] + 1024, written)], 0, 0)
+    for r in rows:
+        ref[r // 4:(r + 1024) // 4] = -7
+        _write(p + r, np.full(256, -7, dtype=np.int32))
+    lib.torch_op_end(held, [], 0, 0)
+    assert lib.stats()["write_invalidations"] >= 2  # blocks 0 and 1 (page 1500 is in block 2... of 4)
+    lib.sync_all()
+    d0 = lib.stats()["bytes_xfer_dth"]
+    _cycle(others)  # evicts p again
+    lib.sync_all()
+    dth = lib.stats()["bytes_xfer_dth"] - d0
+    # the 3 written pages: the other tensors were only read since their last eviction (clean)
+    assert dth == 3 * 4096, dth
+    held, _ = lib.torch_op_begin([(p, False)], 0, 0)
+    assert np.array_equal(_read(p, n // 4), ref)
+    lib.torch_op_end(held, [], 0, 0)
+    for q in others + [p]:
+        lib.torch_free(q, 0)
+
+
+def test_next_use_hints_evict_the_furthest_needed(managed_rt):
+    """With next-use hints the arena evicts the tensor needed furthest in the
+    future, whatever its recency (Belady order; LRU would pick `a`)."""
+    ts = [lib.torch_alloc(8 * MB, 0) for _ in range(3)]
+    a, b, c = ts
+    for t in ts:  # written once, then each op ends; a is least recently used
+        held, _ = lib.torch_op_begin([(t, True)], 0, 0)
+        lib.torch_op_end(held, [t], 0, 0, [], 0)
+    lib.torch_op_end([], [], 0, 0, [(a, 12), (b, 1000), (c, 11)], 10)
+    d = lib.torch_alloc(16 * MB, 0)  # needs 2 of the 3: b (furthest) goes first, then ... not a/c both
+    held, _ = lib.torch_op_begin([(d, True)], 0, 0)
+    lib.torch_op_end(held, [d], 0, 0)
+    info = {t: lib.torch_resident_bytes(t, 0) for t in ts}
+    assert info[b] == 0, info
+    assert info[a] + info[c] >= 8 * MB, info
+    for t in ts + [d]:
+        lib.torch_free(t, 0)
+
+
+def test_prefetch_never_evicts_data_needed_sooner(managed_rt):
+    ts = [lib.torch_alloc(8 * MB, 0) for _ in range(4)]  # 32 MB: the whole arena
+    for t in ts:
+        held, _ = lib.torch_op_begin([(t, True)], 0, 0)
+        lib.torch_op_end(held, [t], 0, 0)
+    lib.torch_op_end([], [], 0, 0, [(t, 20 + i) for i, t in enumerate(ts)], 10)
+    e = lib.torch_alloc(8 * MB, 0)
+    held, _ = lib.torch_op_begin([(e, True)], 0, 0)
+    lib.torch_op_end(held, [e], 0, 0, [(e, 100)], 10)  # e needed last: it was written, one of ts went
+    gone = [t for t in ts if lib.torch_resident_bytes(t, 0) < 8 * MB]
+    assert gone == [ts[3]]  # the furthest-needed of ts (23) made room
+    # prefetching ts[3] for time 23 may evict e (needed at 100) ...
+    assert lib.torch_prefetch([(ts[3], 23)], 0) == 1
+    lib.sync_all()
+    assert lib.torch_resident_bytes(ts[3], 0) == 8 * MB and lib.torch_resident_bytes(e, 0) < 8 * MB
+    # ... but prefetching e for time 100 must not evict anything needed before 100
+    n0 = lib.stats()["evictions"]
+    lib.torch_prefetch([(e, 100)], 0)
+    lib.sync_all()
+    assert all(lib.torch_resident_bytes(t, 0) == 8 * MB for t in ts)
+    assert lib.stats()["evictions"] == n0
+    for t in ts + [e]:
+        lib.torch_free(t, 0)
+
+
+def test_freed_tensor_eviction_copies_nothing(managed_rt):
+    """A freed tensor's data is dead: evicting its chunks (in the reuse cache or
+    awaiting its fence) copies nothing out, and a reuse does not copy it back."""
+    lib.configure("torch_alloc_cache_mb", 64)
+    p = lib.torch_alloc(8 * MB, 0)
+    _write(p, np.ones(2 * MB, dtype=np.int32))
+    held, _ = lib.torch_op_begin([(p, True)], 0, 0)
+    lib.torch_op_end(held, [p], 0, 0)
+    lib.torch_free(p, 0)
+    lib.sync_all()
+    s0 = lib.stats()
+    big = [lib.torch_alloc(10 * MB, 0) for _ in range(3)]  # 30 MB: pushes the cached range out
+    lib.sync_all()
+    s1 = lib.stats()
+    assert s1["evictions"] > s0["evictions"]
+    assert s1["bytes_xfer_dth"] == s0["bytes_xfer_dth"]
+    for q in big:
+        lib.torch_free(q, 0)
+    q = lib.torch_alloc(8 * MB, 0)  # a reuse of a cached range: nothing comes back over the link
+    lib.sync_all()
+    assert lib.stats()["bytes_xfer_htd"] == s1["bytes_xfer_htd"]
+    lib.torch_free(q, 0)
+
+
+def test_accessed_by_is_served_by_a_local_copy(managed_rt):
+    """A remote (zero-copy) decision - accessed_by the GPU with the data resting
+    in host DRAM - would not be mapped by the tensor's stable VA: the op hold
+    falls back to a local copy instead of failing the op (uvm_va_block.c:11625-11664
+    keeps such data remote; the stable VA maps HBM only)."""
+    n = 8 * MB
+    p = lib.torch_alloc(n, 0)
+    ref = np.arange(n // 4, dtype=np.int32) * 3
+    _write(p, ref)
+    held, _ = lib.torch_op_begin([(p, True)], 0, 0)
+    lib.torch_op_end(held, [p], 0, 0)
+    lib.torch_set_read_mostly(p, 0, False)
+    lib.torch_advise(p, 0, rt.ADVISE_SET_PREFERRED_LOCATION, 1, 0, 0)
+    lib.torch_advise(p, 0, rt.ADVISE_SET_ACCESSED_BY, 0, 0, 0)
+    others = [lib.torch_alloc(8 * MB, 0) for _ in range(4)]
+    for q in others:
+        held, _ = lib.torch_op_begin([(q, True)], 0, 0)
+        lib.torch_op_end(held, [q], 0, 0)
+    lib.sync_all()
+    assert lib.torch_resident_bytes(p, 0) < n  # out in host DRAM
+    f0 = lib.stats()["remote_fallbacks"]
+    held, _ = lib.torch_op_begin([(p, False)], 0, 0)
+    assert held == [p]
+    assert np.array_equal(_read(p, n // 4), ref)
+    lib.torch_op_end(held, [], 0, 0)
+    assert lib.stats()["remote_fallbacks"] > f0
+    for q in others + [p]:
+        lib.torch_free(q, 0)
+
+
+def test_stale_translations_are_flushed(managed_rt):
+    """Fake translation model of gfx950 VMM (a remapped VA serves the old chunk
+    until a flush): the init-time self-test sees the stale reads and that the
+    flush cures them, and managed tensors cycled through the arena - every
+    remap followed by the runtime's (elided where safe) flushes - keep their
+    contents."""
+    lib.inject("tlb_mode", 1)
+    lib.init_device(0, 32 * MB)
+    t = [a for a in lib.stats()["arenas"] if a["name"] == "hbm0"][0]["vmm_selftest"]
+    assert t["ran"] and t["ok"] and t["flushed_ok"] == t["rounds"] > 0 and t["unflushed_stale"] > 0, t
+    n = 8 * MB
+    ptrs, refs = [], []
+    for i in range(6):
+        p = lib.torch_alloc(n, 0)
+        assert lib.torch_is_managed(p, 0)
+        ref = np.arange(n // 4, dtype=np.int32) * (i + 1)
+        _write(p, ref)
+        held, _ = lib.torch_op_begin([(p, True)], 0, 0)
+        lib.torch_op_end(held, [p], 0, 0)
+        ptrs.append(p)
+        refs.append(ref)
+    for rnd in range(3):
+        for p, ref in zip(ptrs, refs):
+            held, _ = lib.torch_op_begin([(p, False)], 0, 0)
+            assert np.array_equal(_read(p, n // 4), ref)
+            lib.torch_op_end(held, [], 0, 0)
+    assert lib.stats()["vmm_remaps"] > 12 and lib.stats()["tlb_flushes"] > 0
+    for p in ptrs:
+        lib.torch_free(p, 0)
+    lib.inject("tlb_mode", 0)
+
+
+def test_failed_translation_self_test_refuses_managed_mode(managed_rt):
+    """A GPU whose translation flush does not work fails the self-test: torch
+    allocations stay plain arena extents (never read through a stale mapping)
+    and ogkm.managed() refuses to start."""
+    import ogkm
+
+    lib.inject("tlb_mode", 2)
+    try:
+        lib.init_device(0, 32 * MB)
+        t = [a for a in lib.stats()["arenas"] if a["name"] == "hbm0"][0]["vmm_selftest"]
+        assert t["ran"] and not t["ok"] and "stale" in t["detail"], t
+        p = lib.torch_alloc(8 * MB, 0)
+        assert p and not lib.torch_is_managed(p, 0)
+        lib.torch_free(p, 0)
+        with pytest.raises(RuntimeError, match="self-test"):
+            ogkm.managed(0)
+    finally:
+        lib.inject("tlb_mode", 0)

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: GPU suite on the new transparent mode (page-granular holds, next-use
+# eviction, remote fallback, OOM error), then the stock-torch managed 8B and a
+# lookahead sweep.
+set -o pipefail
+ulimit -c 0
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r4
+timeout -k 10 500 python -u -m pytest tests/test_managed_mode_gpu.py tests/test_gpu_tp2.py -x -v --timeout 240 --timeout-method thread -m gpu > gpurun_out/r4/b_new.log 2>&1 || { echo NEW_FAIL; tail -80 gpurun_out/r4/b_new.log; exit 1; }
+tail -3 gpurun_out/r4/b_new.log
+timeout -k 10 600 python -u -m pytest tests -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/r4/b_gpu.log 2>&1 || { echo GPU_FAIL; tail -60 gpurun_out/r4/b_gpu.log; exit 1; }
+tail -3 gpurun_out/r4/b_gpu.log
+for la in -1 256 2048; do
+  OGKM_MANAGED_LOOKAHEAD_MB=$la timeout -k 10 400 python -u bench.py --torch-managed --model llama3-8b --oversub 2 --steps 4 --warmup 2 > gpurun_out/r4/b_tm_$la.log 2>&1 || { echo TM_FAIL $la; tail -30 gpurun_out/r4/b_tm_$la.log; exit 1; }
+  grep '^{' gpurun_out/r4/b_tm_$la.log | cut -c1-120
+  grep '^{' gpurun_out/r4/b_tm_$la.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('la', $la, d['value'], d['aux'])"
+done
+echo ALL_OK
