@@ -2038,7 +2038,11 @@ size_t Runtime::poll_device_faults(int dev) {
           ch.cancelled_faults++;
         }
       }
-      __atomic_fetch_add(&fb.hdr->cancel[cc.first % kFaultCancelSlots], 1u, __ATOMIC_RELEASE);
+      // Unattributed faults (channel 0) are never cancelled: their gates fall
+      // back to the replay / timeout path (a cancel word shared by every
+      // unregistered stream would cancel gates whose faults were serviced).
+      if (!cc.first || cc.first >= kFaultCancelSlots) continue;
+      __atomic_fetch_add(&fb.hdr->cancel[cc.first], 1u, __ATOMIC_RELEASE);
       Tools::get().inc(Counter::FaultsCancelled);
     }
   }

@@ -633,6 +633,20 @@ void Runtime::stable_map_block(Block* b) {
   Residency* g = b->find(Loc::gpu(r->stable_dev));
   const int64_t want = (g && g->chunk >= 0) ? g->chunk : -1;
   if (want == b->stable_chunk.load() && !b->stale_mapping) return;
+  if (want >= 0 && b->stable_chunk.load() >= 0 && want != b->stable_chunk.load()) {
+    // Remap from a stale mapping: its users (kernels queued before the
+    // eviction) must finish before the VA moves. Wait for them without
+    // stable_m_ - other blocks' remaps, the reaper and translation flushes go
+    // on meanwhile; b itself is held by its block lock (the reaper may still
+    // unmap it, which only makes the unmap below a no-op).
+    Tracker users;
+    {
+      std::lock_guard<std::mutex> sg(stable_m_);
+      users = b->stable_users;
+    }
+    if (users.wait() != Status::OK)
+      RT_ERR("stable VA users of range %llu block %llu failed", (unsigned long long)r->id, (unsigned long long)b->index);
+  }
   std::lock_guard<std::mutex> sg(stable_m_);
   if (want == b->stable_chunk.load()) {  // back on the chunk it still maps: valid again
     b->stale_mapping = false;
@@ -1231,7 +1245,13 @@ uint16_t Runtime::register_channel(int dev, void* stream, const std::string& nam
     if (c.id && c.dev == dev && c.stream == stream) return c.id;
   size_t slot = 0;
   while (slot < channels_.size() && channels_[slot].id) ++slot;
-  if (slot >= 0xffff) return 0;
+  // One cancel word per channel id (fault_abi.hpp): ids stay below
+  // kFaultCancelSlots so no two channels share one. Past that a stream runs
+  // unattributed (channel 0: its faults are serviced, never precisely cancelled).
+  if (slot + 1 >= kFaultCancelSlots) {
+    RT_WARN("register_channel: all %u channel ids in use; stream %p runs unattributed", kFaultCancelSlots - 1, stream);
+    return 0;
+  }
   if (slot == channels_.size()) channels_.emplace_back();
   Channel c;
   c.id = (uint16_t)(slot + 1);
@@ -1549,13 +1569,23 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
   uint64_t n = 0;
   rd(in, &n);
   std::vector<char> page(kBlockSize);
+  // All or nothing: a failure part-way (an id or address taken, a short
+  // file) frees every range this call created, so a caller falling back to a
+  // relocating restore does not end up with duplicates of the first ones.
+  std::vector<Range*> created;
+  const size_t ids0 = new_ids ? new_ids->size() : 0;
+  auto fail = [&](Status st) {
+    for (Range* x : created) free_range(x);
+    if (new_ids) new_ids->resize(ids0);
+    return st;
+  };
   for (uint64_t i = 0; i < n; ++i) {
     uint64_t id, size, nblocks, gid;
     uint32_t type, rflags, nl;
     uint8_t gm;
     if (!rd(in, &id) || !rd(in, &type) || !rd(in, &rflags) || !rd(in, &size) || !rd(in, &nblocks) ||
         !rd(in, &nl))
-      return Status::IO_ERROR;
+      return fail(Status::IO_ERROR);
     std::string name(nl, '\0');
     in.read(&name[0], nl);
     rd(in, &gid);
@@ -1570,7 +1600,8 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
     Range* r = nullptr;
     Status st = in_place ? malloc_managed_at(size, rflags, name, id, cpu_addr, dev_va, sdev, &r)
                          : malloc_managed(size, rflags & ~RANGE_STABLE_VA, name, &r, 0);
-    if (st != Status::OK) return st;
+    if (st != Status::OK) return fail(st);
+    created.push_back(r);
     if (new_ids) new_ids->push_back(r->id);
     struct BlockRec {
       Policy pol;
@@ -1592,7 +1623,7 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
       rd(in, &ab);
       rd(in, &pinned);
       rd(in, &nres);
-      if (!in || idx >= nblocks) return Status::IO_ERROR;
+      if (!in || idx >= nblocks) return fail(Status::IO_ERROR);
       recs[idx].pol.read_dup = rdup;
       recs[idx].pol.has_preferred = hp;
       recs[idx].pol.preferred = Loc{(Tier)pt, pid};
@@ -1617,7 +1648,7 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
         uint64_t boff = k << kBlockShift;
         uint64_t bytes = std::min<uint64_t>(kBlockSize, size - boff);
         in.read(page.data(), bytes);
-        if (!in) return Status::IO_ERROR;
+        if (!in) return fail(Status::IO_ERROR);
         if (!with_data) continue;
         // Restore data at the first recorded location, then re-create copies.
         const auto& rs = recs[k].res;
@@ -1637,7 +1668,7 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
           std::lock_guard<OrderedMutex> g(r->block(k)->lock);
           r->block(k)->policy = recs[k].pol;
         }
-        if (st != Status::OK) return st;
+        if (st != Status::OK) return fail(st);
         for (size_t q = 1; q < rs.size(); ++q) {
           if (!arena_for(rs[q].first)) continue;
           Tracker t;
@@ -1653,7 +1684,7 @@ Status Runtime::checkpoint_load(const std::string& path, bool with_data, std::ve
           }
           finish_ctx(c, &t);
           t.wait();
-          if (st != Status::OK && st != Status::MORE_PROCESSING_REQUIRED) return st;
+          if (st != Status::OK && st != Status::MORE_PROCESSING_REQUIRED) return fail(st);
         }
       }
     }

@@ -24,7 +24,8 @@
 //
 // Precise cancel (cancel_faults_precise, uvm_gpu_replayable_faults.c:2863):
 // when servicing a channel's fault fails (or the fault is fatal: freed range,
-// out of bounds), the host bumps `cancel[channel % kFaultCancelSlots]` BEFORE
+// out of bounds), the host bumps `cancel[channel]` (ids 1..kFaultCancelSlots-1;
+// unattributed faults, channel 0, are never cancelled) BEFORE
 // the replay token. A gate snapshots its channel's word at entry and, once the
 // replay wakes it, exits with status kGateCancelled instead of re-recording.
 #pragma once
@@ -34,7 +35,7 @@
 namespace ogkm {
 
 constexpr uint16_t kFaultWholeBlock = 0xffff;  // record.page: the access needs the whole 2 MB block
-constexpr uint32_t kFaultCancelSlots = 64;      // per-channel cancel words (channel id mod 64; 0 = no channel)
+constexpr uint32_t kFaultCancelSlots = 64;      // per-channel cancel words (channel ids 1..63; 0 = no channel)
 // k_fault_gate status[0]
 constexpr uint32_t kGateResolved = 0, kGateTimeout = 2, kGateCancelled = 3;
 

@@ -30,7 +30,7 @@ __version__ = "0.1.0"
 from . import _native  # noqa: E402,F401  (fails loudly if the native core is missing)
 from . import rt, tools, checkpoint, cxl, allocator, p2p  # noqa: E402,F401
 from .managed import managed  # noqa: E402,F401
-from . import utils, ops, parallel, models  # noqa: E402,F401
+from . import ops, parallel, models  # noqa: E402,F401
 
 # Register the importable alias "ogkm" for the package and every loaded submodule.
 _sys.modules.setdefault("ogkm", _sys.modules[__name__])

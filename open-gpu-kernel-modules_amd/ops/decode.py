@@ -1,10 +1,13 @@
-"""Decode-step math for the Llama-3 family (bf16 compute, fp32 reductions).
+"""Plain-PyTorch reference math of one Llama-3 decode step (bf16 / fp32).
 
-The GEMMs are plain library GEMMs (hipBLASLt through torch.matmul, M = batch);
-at 2x oversubscription a decode step is bound by PCIe weight streaming, not by
-these ops (profiles/ show them at a few % of the step), so they stay library
-calls. The attention uses the grouped-query layout directly (no KV repeat):
-q is viewed as [B, Hkv, group, hd] so each KV head is read once.
+These are the fp32 references the numerics tests compare the HIP kernels
+against (llama.reference_step, tests/test_fused.py, tests/test_dgemm.py) and
+the CPU path of the fake backend. The GPU decode itself runs the hand-written
+gfx950 kernels: the MFMA decode GEMM (ops/dgemm.py, csrc/kernels/decode_gemm.hip)
+and the fused RMSNorm / RoPE + KV append / GQA attention (ops/fused.py,
+csrc/kernels/decode_ops.hip). The attention reference uses the grouped-query
+layout directly (no KV repeat): q is viewed as [B, Hkv, group, hd] so each KV
+head is read once.
 """
 from __future__ import annotations
 

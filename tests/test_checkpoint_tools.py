@@ -49,6 +49,30 @@ def test_checkpoint_map_only(fake_rt, tmp_path):
     assert len(ids) == 1 and lib.range_info(ids[0])["size"] == 2 * MB
 
 
+def test_in_place_restore_is_all_or_nothing(fake_rt, tmp_path):
+    """An in-place restore whose second range's id / address is taken fails
+    without leaving the first range behind; the relocating restore the caller
+    falls back to then creates exactly one copy of each range."""
+    import pytest
+
+    a = rt.malloc_managed(2 * MB, "first")
+    a.fill(1)
+    b = rt.malloc_managed(2 * MB, "second")
+    b.fill(2)
+    p = tmp_path / "ip.bin"
+    checkpoint.save(p, with_data=True)
+    a_id = a.id
+    a.free()  # the first range's id and addresses are free again, the second's are not
+    with pytest.raises(Exception, match="BUSY"):
+        checkpoint.load(p, with_data=True, in_place=True)
+    with pytest.raises(Exception):
+        lib.range_info(a_id)  # rolled back, not leaked
+    ids = checkpoint.load(p, with_data=True)
+    assert len(ids) == 2
+    assert int(rt.ManagedBuffer(ids[0]).read()[0]) == 1 and int(rt.ManagedBuffer(ids[1]).read()[0]) == 2
+    b.free()
+
+
 def test_tools_event_queue(fake_rt):
     q = tools.EventQueue(entries=1024, events=["Migration", "Eviction", "ReadDuplicate"])
     b = rt.malloc_managed(4 * MB, "ev")

@@ -7,6 +7,7 @@ from __future__ import annotations
 import ctypes
 import time
 
+import pytest
 import torch
 
 from ogkm import rt
@@ -214,3 +215,26 @@ def test_failed_service_cancels_channel_precisely(fake_rt):
     lib.unregister_channel(bad_ch)
     bad.free()
     ok_buf.free()
+
+
+def test_channel_ids_never_share_a_cancel_word(fake_rt):
+    """Channel ids stay below the 64 cancel words (no aliasing: channel 64 would
+    otherwise cancel the gates of unattributed kernels), and a failed fault of
+    an unattributed stream (channel 0) bumps no cancel word at all - its gate
+    falls back to the replay / timeout path."""
+    live = [lib.register_channel(0, 0x10000 + i, f"c{i}") for i in range(63)]
+    assert len(set(live)) == 63 and max(live) == 63
+    with pytest.raises(Exception, match="no channel slot left"):
+        lib.register_channel(0, 0x20000, "one too many")
+    for i in live:
+        lib.unregister_channel(i)
+    lib.init_device(0, 64 * MB)
+    bad = rt.malloc_managed(2 * MB, "bad0")
+    info0 = lib.fault_buffer_info(0)
+    lib.inject("populate_error", 1)
+    _inject([(bad.id, 0, 0xFFFF, 1, 0, 0)])  # no channel
+    lib.poll_device_faults(0)
+    info1 = lib.fault_buffer_info(0)
+    assert info1["cancel"] == info0["cancel"]
+    assert info1["replay"] == info0["replay"] + 1
+    bad.free()

@@ -342,7 +342,7 @@ def test_managed_park_unpark_round_trip_throughput_subprocess():
     """Managed-tensor round-trip rate with the working set at 2x the arena
     (tools/bench_managed.py: 8 x 256 MB tensors, 1 GB arena, every touch brings
     256 MB in over PCIe and pushes another 256 MB out). Round 3 measured
-    41-47 GB/s of touched bytes; the guard sits below that at 25 GB/s."""
+    41-47 GB/s of touched bytes; the guard sits ~10% under the low end at 38 GB/s."""
     tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bench_managed.py")
     r = subprocess.run([sys.executable, tool, "--tensors", "8", "--mb", "256", "--arena-mb", "1024", "--iters", "2"],
                        capture_output=True, text=True, timeout=300)
@@ -352,7 +352,7 @@ def test_managed_park_unpark_round_trip_throughput_subprocess():
     print(res)
     assert res["correct"], res
     assert res["counters"].get("evictions", 0) > 0, res
-    assert res["round_trip_gbps"] > 25.0, res
+    assert res["round_trip_gbps"] > 38.0, res
 
 
 def test_allocator_free_on_busy_stream_is_stream_ordered(gpu_rt):
@@ -445,7 +445,7 @@ def test_bf12_decode_bandwidth(gpu_rt):
     b.free()
 
 
-@pytest.mark.parametrize("fmt,max_ratio,min_gbps", [("bf12", 0.78, 1000), ("bf11", 0.71, 1000), ("ans", 0.69, 400)])
+@pytest.mark.parametrize("fmt,max_ratio,min_gbps", [("bf12", 0.78, 1000), ("bf11", 0.71, 1000), ("ans", 0.69, 800)])
 def test_bf12_stream_unpack_hbm_bit_exact_and_fast(gpu_rt, fmt, max_ratio, min_gbps):
     """k_bf12_unpack (HBM-resident packed weights -> bf16 staging) reproduces every
     bit and runs at HBM speed (a 70B layer is ~1.7 GB of bf16), for BF12 and
