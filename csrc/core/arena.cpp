@@ -12,6 +12,7 @@
 
 #include "ogkm/config.hpp"
 #include "ogkm/events.hpp"
+#include "ogkm/va_space.hpp"
 
 namespace ogkm {
 
@@ -285,7 +286,7 @@ void ChunkArena::set_op_clock(uint64_t now) {
 // next. Hints in the past (the trace moved on without a use) count as unknown.
 uint64_t ChunkArena::victim_key_locked(const ChunkInfo& c) const {
   if (c.next_use == kDeadUse) return kDeadUse;
-  if (c.next_use > op_clock_) return c.next_use - op_clock_;
+  if (c.next_use >= op_clock_) return c.next_use - op_clock_;  // due now: 0, the last to go
   if (op_clock_ - c.last_op <= 2) return 1;
   return (1ull << 62) + (clock_ - std::min(clock_, c.last_use));
 }
@@ -313,7 +314,17 @@ void ChunkArena::pick_victims_by_next_use_locked(uint32_t n, std::vector<uint32_
                      });
     cand.resize(n);
   }
-  for (auto& c : cand) out->push_back(c.second);
+  static const bool dbg = getenv("OGKM_DEBUG_VICTIMS") != nullptr;
+  for (auto& c : cand) {
+    if (dbg) {
+      Block* ob = chunks_[c.second].owner;
+      fprintf(stderr, "[victim] %s chunk %u key %llu next_use %llu clock %llu floor %llu owner %s/%llu\n",
+              name_.c_str(), c.second, (unsigned long long)c.first, (unsigned long long)chunks_[c.second].next_use,
+              (unsigned long long)op_clock_, (unsigned long long)floor, ob ? ob->range->name.c_str() : "-",
+              ob ? (unsigned long long)ob->index : 0ull);
+    }
+    out->push_back(c.second);
+  }
 }
 
 Status ChunkArena::reserve_scattered(uint32_t n, Reservation* r) {

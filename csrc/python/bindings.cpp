@@ -244,16 +244,22 @@ PYBIND11_MODULE(_ogkm, m) {
   m.def("mem_advise", [](uint64_t id, uint64_t off, uint64_t len, int advice, int tier, int loc, int proc) {
     check(rt()->mem_advise(range(id), off, len, (Advice)advice, make_loc(tier, loc), proc), "mem_advise");
   });
-  m.def("prefetch", [](uint64_t id, uint64_t off, uint64_t len, int tier, int loc) {
+  // floor > 0 (next-use mode): the op-clock time the data is needed at; the
+  // prefetch evicts only data needed later (VictimFloor), else it is refused
+  // (NO_MEMORY) and the caller faults the data in at its use instead.
+  m.def("prefetch", [](uint64_t id, uint64_t off, uint64_t len, int tier, int loc, uint64_t floor) {
     auto t = std::make_unique<PyTracker>();
     Status s;
     {
       py::gil_scoped_release nogil;
+      VictimFloor vf(floor);
       s = rt()->prefetch(range(id), off, len, make_loc(tier, loc), &t->t, Cause::Prefetch);
     }
     check(s, "prefetch");
     return t;
-  });
+  }, py::arg("id"), py::arg("off"), py::arg("len"), py::arg("tier"), py::arg("loc"), py::arg("floor") = 0);
+  m.def("hint_next_use", [](uint64_t id, uint64_t when) { rt()->hint_next_use(range(id), when); });
+  m.def("set_op_clock", [](int dev, uint64_t now) { rt()->set_op_clock(dev, now); });
   m.def("migrate", [](uint64_t id, uint64_t off, uint64_t len, int tier, int loc) {
     Range* r = range(id);
     py::gil_scoped_release nogil;

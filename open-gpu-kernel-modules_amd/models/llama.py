@@ -547,6 +547,16 @@ class TieredLlama:
         self.stream_seq = [k for k in self.order if not self._is_resident(k)]
         self._pf_next = 0           # next index in stream_seq to prefetch (cyclic)
         self._inflight: list = []   # prefetched, not yet consumed
+        # Next-use hints (planner off): a streamed unit is next used one step
+        # later at the same place in the use order, so the runtime can evict
+        # in next-use order (Belady, ChunkArena::set_next_use) instead of
+        # recency - on a cyclic step larger than HBM, LRU evicts every unit just
+        # before its reuse; Belady keeps a fixed subset resident, as the static
+        # plan does by hand. Op clock = passes * len(stream_seq) + position.
+        self.next_use = (self.planner == "off" and os.environ.get("OGKM_NEXT_USE", "1") != "0"
+                         and bool(self.stream_seq))
+        self._seq_pos = {k: j for j, k in enumerate(self.stream_seq)}
+        self._pass, self._last_pos = 0, -1
         # Bounded run-ahead: compute events of streamed units enqueued but maybe
         # not yet run. Leases wait GPU-side, so without a bound the host would
         # prefetch a whole step ahead and the ring would evict (and wait on)
@@ -966,6 +976,29 @@ class TieredLlama:
         return dgemm.frag_unpermute(self.host_weights(key)[:n * k], n, k)
 
     # ------------------------------------------------------------------ streaming
+    def _due(self, key) -> int:
+        """Op-clock time of the next use of streamed unit ``key``."""
+        p = self._seq_pos[key]
+        return (self._pass + (p <= self._last_pos)) * len(self.stream_seq) + p
+
+    def _clock_use(self, key) -> None:
+        """Next-use mode: advance the op clock to ``key``'s use."""
+        p = self._seq_pos.get(key)
+        if p is None:
+            return
+        if p <= self._last_pos:
+            self._pass += 1
+        self._last_pos = p
+        lib.set_op_clock(self.dev, self._pass * len(self.stream_seq) + p)
+
+    def _hint_used(self, key) -> None:
+        """Next-use mode, once ``key`` is leased: its next use is one pass later
+        (hinted after the lease pinned it - before, the prefetches queued for
+        this use would see it as the furthest-needed unit and evict it)."""
+        if key in self._seq_pos:
+            n = len(self.stream_seq)
+            self._buf(key).hint_next_use(self._pass * n + self._seq_pos[key] + n)
+
     def _prefetch_ahead(self) -> None:
         """Keep up to ``window_bytes`` of upcoming streamed tensors in flight on the ring."""
         if not self.stream_seq:
@@ -977,7 +1010,14 @@ class TieredLlama:
             nb = self._buf(key).size
             if self._inflight and inflight + nb > self.window_bytes:
                 break
-            self._buf(key).prefetch(rt.Loc.gpu(self.dev))
+            if self.next_use:
+                # evict only units needed after this one, or leave it to its use
+                try:
+                    self._buf(key).prefetch(rt.Loc.gpu(self.dev), needed_at=self._due(key))
+                except lib.RuntimeStatusError:
+                    break
+            else:
+                self._buf(key).prefetch(rt.Loc.gpu(self.dev))
             self._inflight.append(key)
             inflight += nb
             self._pf_next = (self._pf_next + 1) % n
@@ -1001,9 +1041,13 @@ class TieredLlama:
         if not self._is_resident(key):
             if self._inflight and self._inflight[0] == key:
                 self._inflight.pop(0)
+            if self.next_use:
+                self._clock_use(key)
             self._prefetch_ahead()
         t_a = time.perf_counter()
         lease = self._buf(key).acquire(self.dev, rt.READ)
+        if self.next_use:
+            self._hint_used(key)
         if acct:  # H2D bytes submitted while servicing this tensor (prefetch window + its own faults)
             self.byte_trace[key] = self.byte_trace.get(key, 0) + lib.stats()["bytes_xfer_htd"] - b0
         t_w = time.perf_counter()
@@ -1031,8 +1075,12 @@ class TieredLlama:
         if not self._is_resident(key):
             if self._inflight and self._inflight[0] == key:
                 self._inflight.pop(0)
+            if self.next_use:
+                self._clock_use(key)
             self._prefetch_ahead()
         lease = self._buf(key).acquire(self.dev, rt.READ)
+        if self.next_use:
+            self._hint_used(key)
         lease.wait(0 if (self.fake or _HOST_LEASE_WAIT) else None)
         return lease, lease.dptr
 

@@ -269,10 +269,17 @@ class ManagedBuffer:
         self.advise(ADVISE_SET_ACCESSED_BY if on else ADVISE_UNSET_ACCESSED_BY, None, offset, length, proc)
 
     # -- migration
-    def prefetch(self, loc, offset: int = 0, length: Optional[int] = None):
+    def prefetch(self, loc, offset: int = 0, length: Optional[int] = None, needed_at: int = 0):
+        """``needed_at`` (op clock, next-use mode): evict only data needed later,
+        or raise (NO_MEMORY) and leave the data where it is."""
         length = self.size - offset if length is None else length
         t, i = Loc.parse(loc).code
-        return lib.prefetch(self.id, offset, length, t, i)
+        return lib.prefetch(self.id, offset, length, t, i, int(needed_at))
+
+    def hint_next_use(self, when: int) -> None:
+        """Op-clock time of this range's next use: its HBM chunks are then evicted
+        in next-use (Belady) order - see lib.set_op_clock."""
+        lib.hint_next_use(self.id, int(when))
 
     def migrate(self, loc, offset: int = 0, length: Optional[int] = None) -> None:
         length = self.size - offset if length is None else length

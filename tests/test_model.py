@@ -314,3 +314,31 @@ def test_long_context_packed_kv_rows_of_chunks(fake_rt):
         out[fmt] = m.last_logits.clone()
         m.close()
     assert torch.equal(out["bf16"], out["ans"])
+
+
+def test_planner_off_next_use_streams_like_the_plan(fake_rt, monkeypatch):
+    """planner='off' with next-use hints (each streamed unit is next used one
+    pass later): the arena evicts in Belady order, keeping a fixed subset
+    resident as the static plan does by hand - the bytes streamed per step come
+    within 10% of the plan's, and below the hint-less (recency) run's."""
+    lib.shutdown()
+    rt.init("fake", fake_devices=1, fake_hbm_mb=1024, host_budget_mb=4096)
+    cfg = llama.CONFIGS["small"]
+    htd = {}
+    for name, planner, nu in (("static", "static", "1"), ("lru", "off", "0"), ("next_use", "off", "1")):
+        monkeypatch.setenv("OGKM_NEXT_USE", nu)
+        m = llama.TieredLlama(cfg, batch=8, context=32, max_new_tokens=12, oversub=2.0, device=0, seed=1,
+                              weight_format="ans", kv_format="bf16", planner=planner)
+        assert m.next_use == (name == "next_use")
+        tok = torch.arange(8) * 7
+        for _ in range(3):
+            tok = m.step(tok)
+        lib.sync_all()
+        lib.reset_counters()
+        for _ in range(4):
+            tok = m.step(tok)
+        lib.sync_all()
+        htd[name] = lib.stats()["bytes_xfer_htd"] / 4
+        m.close()
+    assert htd["next_use"] < htd["lru"], htd
+    assert htd["next_use"] <= 1.10 * htd["static"], htd

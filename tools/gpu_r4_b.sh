@@ -15,4 +15,6 @@ for la in -1 256 2048; do
   grep '^{' gpurun_out/r4/b_tm_$la.log | cut -c1-120
   grep '^{' gpurun_out/r4/b_tm_$la.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('la', $la, d['value'], d['aux'])"
 done
+timeout -k 10 600 python -u bench.py --planner off --steps 10 --warmup 3 > gpurun_out/r4/b_off.log 2>&1 || { echo OFF_FAIL; tail -30 gpurun_out/r4/b_off.log; exit 1; }
+grep '^{' gpurun_out/r4/b_off.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('planner_off', d['value'], d['ms_per_step'], d['aux']['traffic_per_step_gb'], d['aux']['evictions'])"
 echo ALL_OK
