@@ -94,8 +94,13 @@ struct ResidNormArgs {
   uint32_t rows, dim, ldx, ldy;
   float eps;
   uint32_t y_frag;
+  // Optional [rows][ceil(dim / kNormCols)] f32 scratch: with it, few-row norms
+  // run as two wide launches (residual + partial sums of squares over every
+  // 1024-column block, then the scaling) instead of one workgroup per row.
+  float* ssq = nullptr;
 };
 constexpr uint32_t kNormCols = 1024;  // RMSNorm columns per pass of a 256-thread workgroup (4 per thread)
+constexpr uint32_t kNormWideRows = 256;  // with an ssq scratch, norms of fewer rows take the two-launch path
 struct AttnArgs {
   const uint16_t* q;       // [B, hq, hd] (rotated)
   const uint16_t* cache;   // [2][B][hkv][T][hd]

@@ -138,6 +138,75 @@ __global__ void __launch_bounds__(256) k_rmsnorm(ResidNormArgs a) {
     if (on[j]) norm_store4(a, row, cl[j], v[j], wp[j], r);
 }
 
+// Two-launch RMSNorm for few rows (decode batches): a row's 1024-column blocks
+// are spread over workgroups, so a 64-row norm runs on dim / 4 x 64 / 256
+// workgroups instead of 64 (one per CU - latency-bound at ~8 us for the
+// residual's split-K partials). k_norm_ssq: residual epilogue (as k_rmsnorm:
+// x = bf16(bf16(sum_k part[k]) + x), k ascending) and the block's sum of
+// squares into ssq[row][block]; k_norm_scale: r = rsqrt(sum of the row's block
+// sums / dim + eps), y = bf16(bf16(x r) w). Deterministic (fixed summation
+// order, no atomics).
+__global__ void __launch_bounds__(256) k_norm_ssq(ResidNormArgs a) {
+  __shared__ float red[4];
+  const uint32_t row = blockIdx.y, t = threadIdx.x;
+  const uint32_t c = blockIdx.x * kNormCols + 4 * t;
+  const bool on = c < a.dim;
+  const uint32_t cl = on ? c : a.dim - 4;
+  uint16_t* xr = a.x + (uint64_t)row * a.ldx;
+  const uint2 xp = *reinterpret_cast<const uint2*>(xr + cl);
+  float v[4] = {dbf((uint16_t)xp.x), dbf((uint16_t)(xp.x >> 16)), dbf((uint16_t)xp.y), dbf((uint16_t)(xp.y >> 16))};
+  if (a.part) {
+    constexpr uint32_t KB = 16;  // splits in flight per batch
+    float4 sum = float4{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t k0 = 0; k0 < a.ksplit; k0 += KB) {
+      float4 pv[KB];
+#pragma unroll
+      for (uint32_t kk = 0; kk < KB; ++kk) {
+        const uint32_t k = k0 + kk < a.ksplit ? k0 + kk : a.ksplit - 1;
+        pv[kk] = *reinterpret_cast<const float4*>(a.part + ((uint64_t)k * a.rows + row) * a.dim + cl);
+      }
+#pragma unroll
+      for (uint32_t kk = 0; kk < KB; ++kk) {
+        const bool in = k0 + kk < a.ksplit;
+        sum.x = in ? sum.x + pv[kk].x : sum.x;
+        sum.y = in ? sum.y + pv[kk].y : sum.y;
+        sum.z = in ? sum.z + pv[kk].z : sum.z;
+        sum.w = in ? sum.w + pv[kk].w : sum.w;
+      }
+    }
+    const float s4[4] = {sum.x, sum.y, sum.z, sum.w};
+    uint16_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = df2bf(dbf(df2bf(s4[e])) + v[e]);
+      v[e] = dbf(o[e]);
+    }
+    if (on)
+      *reinterpret_cast<uint2*>(xr + cl) =
+          uint2{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
+  }
+  float ss = on ? v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3] : 0.f;
+  ss = wave_sum(ss);
+  if ((t & 63) == 0) red[t >> 6] = ss;
+  __syncthreads();
+  if (t == 0) a.ssq[(uint64_t)row * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(256) k_norm_scale(ResidNormArgs a) {
+  const uint32_t row = blockIdx.y, t = threadIdx.x;
+  const uint32_t c = blockIdx.x * kNormCols + 4 * t;
+  if (c >= a.dim) return;
+  const uint32_t nb = gridDim.x;
+  float tot = 0.f;
+  for (uint32_t j = 0; j < nb; ++j) tot += a.ssq[(uint64_t)row * nb + j];
+  const float r = rsqrtf(tot / (float)a.dim + a.eps);
+  const uint2 xp = *reinterpret_cast<const uint2*>(a.x + (uint64_t)row * a.ldx + c);
+  const uint2 wp = *reinterpret_cast<const uint2*>(a.w + c);
+  const float v[4] = {dbf((uint16_t)xp.x), dbf((uint16_t)(xp.x >> 16)), dbf((uint16_t)xp.y),
+                      dbf((uint16_t)(xp.y >> 16))};
+  norm_store4(a, row, c, v, wp, r);
+}
+
 // ---------------------------------------------------------------- RoPE + KV append
 // One thread per (b, head, i < hd/2) over the q heads, then the k heads (rotated,
 // appended) and the v heads (appended).
@@ -649,6 +718,13 @@ hipError_t launch_rmsnorm(const ResidNormArgs& a, hipStream_t s) {
   if (a.dim % 4 || a.dim < 4 || a.dim > 16 * kNormCols || a.ldx % 4 || a.ldy % 4 || (a.y_frag && a.dim % 32))
     return hipErrorInvalidValue;
   if (!a.rows) return hipSuccess;
+  // Few rows: two wide launches (every 1024-column block its own workgroup).
+  if (a.ssq && a.rows < kNormWideRows) {
+    const dim3 grid((a.dim + kNormCols - 1) / kNormCols, a.rows);
+    hipLaunchKernelGGL(k_norm_ssq, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_norm_scale, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   if (a.dim <= kNormCols)
     hipLaunchKernelGGL((k_rmsnorm<1>), dim3(a.rows), dim3(256), 0, s, a);
   else if (a.dim <= 4 * kNormCols)

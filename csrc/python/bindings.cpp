@@ -883,16 +883,19 @@ PYBIND11_MODULE(_ogkm, m) {
      py::arg("x_frag") = false, py::arg("out_frag") = false, py::arg("out_cols") = 0, py::arg("out_col0") = 0);
   // Fused decode-step ops (ops/fused.py).
   m.def("rmsnorm", [](int dev, uint64_t stream, uint64_t x, uint64_t w, uint64_t y, uint32_t rows, uint32_t dim,
-                      uint32_t ldx, uint32_t ldy, float eps, uint64_t part, uint32_t ksplit, bool y_frag) {
+                      uint32_t ldx, uint32_t ldy, float eps, uint64_t part, uint32_t ksplit, bool y_frag,
+                      uint64_t ssq, uint64_t ssq_bytes) {
     if (dim % 4 || dim < 4 || dim > 16384 || ldx % 4 || ldy % 4)
       throw StatusError("rmsnorm: dim % 4, 4 <= dim <= 16384, ld % 4");
     if (y_frag && dim % 32) throw StatusError("rmsnorm: fragment-ordered output needs dim % 32 == 0");
+    if (ssq && (uint64_t)rows * ((dim + kNormCols - 1) / kNormCols) * 4 > ssq_bytes)
+      throw StatusError("rmsnorm: ssq scratch too small");
     ResidNormArgs a{(const float*)part, ksplit, (uint16_t*)x, (const uint16_t*)w, (uint16_t*)y, rows, dim, ldx, ldy,
-                    eps, y_frag ? 1u : 0u};
+                    eps, y_frag ? 1u : 0u, (float*)ssq};
     check(rt()->be()->rmsnorm(dev, a, (void*)stream), "rmsnorm");
   }, py::arg("dev"), py::arg("stream"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("rows"), py::arg("dim"),
      py::arg("ldx"), py::arg("ldy"), py::arg("eps"), py::arg("part") = 0, py::arg("ksplit") = 0,
-     py::arg("y_frag") = false);
+     py::arg("y_frag") = false, py::arg("ssq") = 0, py::arg("ssq_bytes") = 0);
   m.def("rope_kv", [](int dev, uint64_t stream, uint64_t qkv, uint32_t ldqkv, uint64_t cos, uint64_t sin,
                       uint64_t q_out, uint64_t cache, uint64_t tail, uint32_t B, uint32_t hq, uint32_t hkv,
                       uint32_t hd, uint32_t T, uint32_t pos, uint32_t tail_T, uint32_t tail_pos, uint64_t part,

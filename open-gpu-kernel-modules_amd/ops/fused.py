@@ -10,6 +10,7 @@ the same plumbing (layouts, strides, positions).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -36,9 +37,26 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | N
     if pending is not None:
         pending.check(x.shape[0], x.shape[1])
         part, ks = pending.part, pending.ksplit
+    ssq, ssq_bytes = 0, 0
+    if WIDE_NORM and x.device.type == "cuda":
+        need = x.shape[0] * ((x.shape[1] + 1023) // 1024) * 4
+        key = str(x.device)
+        t = _NormScratch.buf.get(key)
+        if t is None or t.numel() * 4 < need:
+            t = _NormScratch.buf[key] = torch.empty(max(need, 1 << 16) // 4, dtype=torch.float32, device=x.device)
+        ssq, ssq_bytes = t.data_ptr(), t.numel() * 4
     lib.rmsnorm(device_index, _stream(x, device_index), x.data_ptr(), w.data_ptr(), out.data_ptr(), x.shape[0],
-                x.shape[1], x.stride(0), out.stride(0), float(eps), part, ks, out_frag)
+                x.shape[1], x.stride(0), out.stride(0), float(eps), part, ks, out_frag, ssq, ssq_bytes)
     return out
+
+
+# Few-row norms as two wide launches (k_norm_ssq + k_norm_scale) instead of one
+# workgroup per row (OGKM_WIDE_NORM=0: the one-launch kernel).
+WIDE_NORM = os.environ.get("OGKM_WIDE_NORM", "1") != "0"
+
+
+class _NormScratch:
+    buf: dict = {}
 
 
 def rope_kv(qkv, cos: torch.Tensor, sin: torch.Tensor, cache: torch.Tensor, pos: int, hq: int,
