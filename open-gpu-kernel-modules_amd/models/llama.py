@@ -63,6 +63,7 @@ PLAN_HBM_GBPS = 4000.0
 # Diagnostics: the host waits for every streamed unit's copies (instead of a
 # GPU-side stream dependency).
 _HOST_LEASE_WAIT = os.environ.get("OGKM_HOST_LEASE_WAIT", "0") != "0"
+_FLOOR_FALLBACK = os.environ.get("OGKM_FLOOR_FALLBACK", "stop")
 
 
 @dataclass(frozen=True)
@@ -1011,11 +1012,16 @@ class TieredLlama:
             if self._inflight and inflight + nb > self.window_bytes:
                 break
             if self.next_use:
-                # evict only units needed after this one, or leave it to its use
+                # evict only units needed after this one; refused (no such
+                # window): OGKM_FLOOR_FALLBACK=stop leaves it to its use,
+                # =plain prefetches it anyway (recency / next-use order without
+                # the floor, as the fault at its use would)
                 try:
                     self._buf(key).prefetch(rt.Loc.gpu(self.dev), needed_at=self._due(key))
                 except lib.RuntimeStatusError:
-                    break
+                    if _FLOOR_FALLBACK != "plain":
+                        break
+                    self._buf(key).prefetch(rt.Loc.gpu(self.dev))
             else:
                 self._buf(key).prefetch(rt.Loc.gpu(self.dev))
             self._inflight.append(key)
