@@ -1292,6 +1292,9 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
           if (st == Status::OK) {
             y = b->find(dst);
             touch_residency(b, y, cause == Cause::Prefetch && !L);
+            // Mapped by another thread whose translation flush has not
+            // completed yet: this lease flushes too before any use.
+            if (b->map_seq != ~0ull && tlb_done_[gpu].load() <= b->map_seq) thread_tlb_need() |= 1u << gpu;
             if (L) {
               b->lease_pins++;
               y->arena->pin((uint32_t)y->chunk);

@@ -684,8 +684,10 @@ void Runtime::stable_map_block(Block* b) {
     if (b->va_unmap_seq == ~0ull || tlb_done_[r->stable_dev].load() <= b->va_unmap_seq) {
       thread_tlb_need() |= 1u << r->stable_dev;
       tlb_dirty_.fetch_or(1u << r->stable_dev);
+      b->map_seq = tlb_started_[r->stable_dev].load();
     } else {
       Tools::get().inc(Counter::TlbFlushesElided);
+      b->map_seq = ~0ull;
     }
   } else {
     Tools::get().inc(Counter::VmmErrors);

@@ -33,10 +33,12 @@
 // completes (no host stall in free).
 // The C entry points ogkm_torch_alloc / ogkm_torch_free are what
 // CUDAPluggableAllocator dlsym()s.
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -90,6 +92,7 @@ struct DevAlloc {
     bool persistent = false;
     bool held_once = false;
     uint64_t last_hold_op = 0;
+    uint32_t prefetching = 0;  // the prefetch worker is placing it (a free waits for it)
   };
   std::unordered_map<uint64_t, Managed> managed;   // stable VA -> range
   std::vector<std::pair<Range*, Tracker>> deferred;  // freed, waiting for their stream fence
@@ -104,6 +107,26 @@ struct DevAlloc {
   uint64_t managed_bytes = 0, parks = 0, unparks = 0, op_holds = 0;
   uint64_t op_seq = 0;  // dispatched ops that held managed operands (the persistence clock)
   std::string last_error;  // last allocation failure (surfaced by ogkm_torch_alloc)
+  // Asynchronous op-trace prefetch (torch_async_prefetch): the dispatching
+  // thread queues (tensor, op-clock time needed); a worker places them.
+  struct PrefetchReq {
+    uint64_t ptr, when;
+  };
+  std::deque<PrefetchReq> pq;
+  std::condition_variable pq_cv, pf_done_cv;
+  std::thread worker;
+  bool stop = false;
+  uint64_t pf_queued = 0, pf_done = 0, pf_skipped = 0;
+  void stop_worker() {
+    if (!worker.joinable()) return;
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    pq_cv.notify_all();
+    worker.join();
+  }
+  ~DevAlloc() { stop_worker(); }  // process exit without a runtime shutdown
 };
 
 std::mutex g_m;
@@ -333,8 +356,16 @@ void torch_free(void* p, int device, void* stream) {
   DevAlloc* da = dev_alloc(device);
   // The freeing stream's queued work may still use the memory.
   FenceRef f = fence_record(rt->be(), device, stream);
-  std::lock_guard<std::mutex> g(da->m);
+  std::unique_lock<std::mutex> g(da->m);
   auto mt = da->managed.find((uint64_t)p);
+  if (mt != da->managed.end() && mt->second.prefetching) {
+    // the worker is placing it right now: let that finish before the range goes
+    da->pf_done_cv.wait(g, [&] {
+      auto it = da->managed.find((uint64_t)p);
+      return it == da->managed.end() || !it->second.prefetching;
+    });
+    mt = da->managed.find((uint64_t)p);
+  }
   if (mt != da->managed.end()) {
     DevAlloc::Managed m = mt->second;
     da->managed.erase(mt);
@@ -392,6 +423,8 @@ void torch_free(void* p, int device, void* stream) {
 // any device memory does once its context is gone.
 void torch_alloc_reset() {
   std::lock_guard<std::mutex> g(g_m);
+  for (auto& d : g_devs)
+    if (d) d->stop_worker();
   g_devs.clear();
 }
 
@@ -616,18 +649,60 @@ Status torch_advise(void* p, int device, int advice, int loc_kind, int loc_id, i
   return rt->mem_advise(it->second.r, 0, it->second.size, (Advice)advice, loc, proc);
 }
 
+// One prefetch: hint the tensor's next use and place it on the GPU, evicting
+// only data needed after `when` (VictimFloor). da->m NOT held.
+static bool prefetch_one(Runtime* rt, Range* r, uint64_t size, int device, uint64_t when) {
+  VictimFloor floor(when);
+  Tracker t;
+  return rt->prefetch(r, 0, size, Loc::gpu(device), &t, Cause::Prefetch) == Status::OK;
+}
+
+// Prefetch worker of one GPU: places queued tensors in FIFO order. A tensor
+// that an op holds by now is skipped (its op faulted it in); a tensor being
+// placed is marked so that a concurrent free waits for it.
+static void prefetch_worker(DevAlloc* da, int device) {
+  std::unique_lock<std::mutex> g(da->m);
+  for (;;) {
+    da->pq_cv.wait(g, [&] { return da->stop || !da->pq.empty(); });
+    if (da->stop) return;
+    DevAlloc::PrefetchReq q = da->pq.front();
+    da->pq.pop_front();
+    auto it = da->managed.find(q.ptr);
+    Runtime* rt = Runtime::get();
+    if (!rt || it == da->managed.end() || it->second.holds) {
+      da->pf_skipped++;
+      da->pf_done_cv.notify_all();
+      continue;
+    }
+    it->second.prefetching++;
+    Range* r = it->second.r;
+    const uint64_t size = it->second.size;
+    g.unlock();
+    prefetch_one(rt, r, size, device, q.when);
+    g.lock();
+    auto jt = da->managed.find(q.ptr);
+    if (jt != da->managed.end() && jt->second.prefetching) jt->second.prefetching--;
+    da->pf_done++;
+    da->pf_done_cv.notify_all();
+  }
+}
+
 // Layer-ahead prefetch of managed tensors not currently held: queue their
 // H2D copies (no lease, no stream wait; a later op hold finds them resident or
 // waits for the copies). Each comes with the op-clock time it is needed at:
 // with next-use hints the prefetch evicts only data needed later than that,
 // or is dropped (VictimFloor) - a window never pushes out what it will need
-// first. Returns how many prefetches were queued.
+// first. With torch_async_prefetch the placement itself (evictions, stable-VA
+// remaps, translation flushes: most of the host time of a streaming step)
+// runs on the GPU's prefetch worker, beside the dispatching thread. Returns
+// how many prefetches were queued / done.
 size_t torch_prefetch(const std::vector<std::pair<uint64_t, uint64_t>>& ptrs, int device) {
   Runtime* rt = Runtime::get();
   if (!rt || !rt->is_local(device)) return 0;
   DevAlloc* da = dev_alloc(device);
-  std::lock_guard<std::mutex> g(da->m);
+  std::unique_lock<std::mutex> g(da->m);
   size_t n = 0;
+  const bool async = config().torch_async_prefetch != 0;
   for (auto& pw : ptrs) {
     auto it = da->managed.find(pw.first);
     if (it == da->managed.end() || it->second.holds) continue;
@@ -635,11 +710,26 @@ size_t torch_prefetch(const std::vector<std::pair<uint64_t, uint64_t>>& ptrs, in
       it->second.next_use = pw.second;
       rt->hint_next_use(it->second.r, pw.second);
     }
-    VictimFloor floor(pw.second);
-    Tracker t;
-    if (rt->prefetch(it->second.r, 0, it->second.size, Loc::gpu(device), &t, Cause::Prefetch) == Status::OK) ++n;
+    if (async) {
+      da->pq.push_back(DevAlloc::PrefetchReq{pw.first, pw.second});
+      da->pf_queued++;
+      ++n;
+      continue;
+    }
+    if (prefetch_one(rt, it->second.r, it->second.size, device, pw.second)) ++n;
+  }
+  if (async && n) {
+    if (!da->worker.joinable()) da->worker = std::thread(prefetch_worker, da, device);
+    da->pq_cv.notify_one();
   }
   return n;
+}
+
+// Wait until every queued prefetch of `device` has been placed (or skipped).
+void torch_prefetch_wait(int device) {
+  DevAlloc* da = dev_alloc(device);
+  std::unique_lock<std::mutex> g(da->m);
+  da->pf_done_cv.wait(g, [&] { return da->pq.empty() && da->pf_done + da->pf_skipped >= da->pf_queued; });
 }
 
 const char* torch_last_error(int device) {

@@ -41,6 +41,7 @@ bool torch_is_managed(void* p, int device);
 // (storage, op-clock time it is needed at; 0 = unknown): prefetches evict only
 // data needed later than that.
 size_t torch_prefetch(const std::vector<std::pair<uint64_t, uint64_t>>& ptrs, int device);
+void torch_prefetch_wait(int device);  // every queued (asynchronous) prefetch placed
 uint64_t torch_managed_size(void* p, int device);
 uint64_t torch_resident_bytes(void* p, int device);  // bytes of the tensor resident in HBM
 // Last allocation failure on `device` (empty: none): the message a caller

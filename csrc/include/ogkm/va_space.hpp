@@ -105,6 +105,12 @@ class Block {
   // until a flush that started after that unmap has completed, so a remap
   // needs a flush only then (Runtime::stable_map_block). Guarded by stable_m_.
   uint64_t va_unmap_seq = ~0ull;
+  // Value of Runtime::tlb_started_ when the stable VA was last remapped in a
+  // way that needs a translation flush (~0: none needed): a lease of the block
+  // from ANY thread must see a flush started after that complete before its
+  // kernels use the VA (another thread's remap may still await its flush).
+  // Guarded by the block lock.
+  uint64_t map_seq = ~0ull;
   // The stable VA still maps a chunk the block left (its users were running at
   // the eviction): listed in Runtime::stale_maps_ until the mapping goes.
   std::atomic<bool> stale_mapping{false};

@@ -1219,6 +1219,10 @@ PYBIND11_MODULE(_ogkm, m) {
     return torch_prefetch(ptrs, dev);
   });
   m.def("torch_managed_size", [](uint64_t p, int dev) { return torch_managed_size((void*)p, dev); });
+  m.def("torch_prefetch_wait", [](int dev) {
+    py::gil_scoped_release nogil;
+    torch_prefetch_wait(dev);
+  });
   m.def("torch_resident_bytes", [](uint64_t p, int dev) { return torch_resident_bytes((void*)p, dev); });
   m.def("torch_managed_stats", [](int dev) {
     uint64_t a, p, np, nu;

@@ -325,11 +325,13 @@ def test_prefetch_never_evicts_data_needed_sooner(managed_rt):
     assert gone == [ts[3]]  # the furthest-needed of ts (23) made room
     # prefetching ts[3] for time 23 may evict e (needed at 100) ...
     assert lib.torch_prefetch([(ts[3], 23)], 0) == 1
+    lib.torch_prefetch_wait(0)
     lib.sync_all()
     assert lib.torch_resident_bytes(ts[3], 0) == 8 * MB and lib.torch_resident_bytes(e, 0) < 8 * MB
     # ... but prefetching e for time 100 must not evict anything needed before 100
     n0 = lib.stats()["evictions"]
     lib.torch_prefetch([(e, 100)], 0)
+    lib.torch_prefetch_wait(0)
     lib.sync_all()
     assert all(lib.torch_resident_bytes(t, 0) == 8 * MB for t in ts)
     assert lib.stats()["evictions"] == n0
