@@ -486,6 +486,13 @@ void ChunkArena::pin(uint32_t i) {
   if (chunks_[i].pin_count++ == 0) st_.pinned += kBlockSize;
 }
 
+bool ChunkArena::try_pin(uint32_t i) {
+  std::lock_guard<OrderedMutex> g(m_);
+  if (chunks_[i].state != ChunkState::ALLOCATED) return false;
+  if (chunks_[i].pin_count++ == 0) st_.pinned += kBlockSize;
+  return true;
+}
+
 void ChunkArena::unpin(uint32_t i) {
   std::lock_guard<OrderedMutex> g(m_);
   RT_ASSERT_RELEASE(chunks_[i].pin_count > 0);

@@ -1,4 +1,5 @@
 // Common utilities: status strings, page-mask helpers, leveled logging, sticky fatal status.
+#include <execinfo.h>
 #include "ogkm/common.hpp"
 
 #include <cstdarg>
@@ -162,6 +163,12 @@ extern "C" void __sanitizer_print_stack_trace();
 
 void assert_fail(const char* cond, const char* file, int line, bool release) {
   log_msg(LogLevel::ERROR, file, line, "assertion failed: %s", cond);
+  {
+    // where the invariant broke (symbolize the offsets with llvm-symbolizer --obj=<.so>)
+    void* frames[32];
+    const int n = backtrace(frames, 32);
+    backtrace_symbols_fd(frames, n, 2);
+  }
 #if defined(__SANITIZE_ADDRESS__) || defined(__SANITIZE_THREAD__)
   __sanitizer_print_stack_trace();  // sanitizer test builds: where the broken invariant was hit
 #endif

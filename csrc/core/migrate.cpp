@@ -90,12 +90,17 @@ Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool 
     Tools::get().inc(Counter::InjectedErrors);
     return Status::NO_MEMORY;  // injected allocation failure: eviction cannot help either
   }
-  Status st = a->reserve(n, r);
-  if (st != Status::OK) return st;
-  Status es = evict_batch(a, r->victims);
-  if (es != Status::OK) {
-    a->cancel(*r);
-    return es;
+  Status st = Status::OK, es = Status::OK;
+  for (int attempt = 0;; ++attempt) {
+    st = a->reserve(n, r);
+    if (st != Status::OK) return st;
+    es = evict_batch(a, r->victims);
+    if (es == Status::OK) break;
+    a->cancel(*r);  // evicted victims come back free, the busy one stays with its user
+    // BUSY: a victim was leased / pinned after the reservation chose it
+    // (another thread's lease): choose again.
+    if (es != Status::BUSY || attempt >= 8) return es;
+    std::this_thread::yield();
   }
   if (!a->loc().is_gpu()) {
     st = static_cast<HostArena*>(a)->ensure_registered((uint32_t)r->first, r->n);
@@ -710,7 +715,9 @@ Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
     *detached = true;
     return Status::OK;
   }
-  if (b->lease_pins || b->user_pins) return Status::BUSY;
+  // Leased / pinned since the reservation chose it (a concurrent lease or
+  // placement): not a victim after all.
+  if (b->lease_pins || b->user_pins || a->pinned(i)) return Status::BUSY;
   PageMask others;
   for (auto& x : b->res)
     if (&x != r) others |= x.resident;
@@ -1209,14 +1216,23 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
     std::vector<int64_t> hints;
     for (uint64_t bi = G.g0; bi <= G.g1; ++bi) {
       Block* b = r->block(bi);
-      std::lock_guard<OrderedMutex> g(b->lock);
-      Residency* x = b->find(dst);
-      if (!x) {
-        G.need.push_back(bi);
-        hints.push_back(b->stable_chunk.load());
-      } else if (x->chunk >= 0) {
-        ga->pin((uint32_t)x->chunk);
-        kept.push_back((uint32_t)x->chunk);
+      for (int spin = 0;; ++spin) {
+        std::unique_lock<OrderedMutex> g(b->lock);
+        Residency* x = b->find(dst);
+        if (!x) {
+          G.need.push_back(bi);
+          hints.push_back(b->stable_chunk.load());
+        } else if (x->chunk >= 0) {
+          if (!ga->try_pin((uint32_t)x->chunk)) {
+            // Another thread chose this chunk as an eviction victim: it needs
+            // the block lock to detach it - let it, then place the block anew.
+            g.unlock();
+            std::this_thread::yield();
+            continue;
+          }
+          kept.push_back((uint32_t)x->chunk);
+        }
+        break;
       }
     }
     for (size_t k = 0; k < G.need.size(); ++k) {
@@ -1235,9 +1251,15 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
       } else {
         st = ga->reserve_scattered(m, &rv);
       }
-      if (st == Status::OK) {
+      for (int attempt = 0; st == Status::OK; ++attempt) {
         st = evict_batch(ga, rv.victims);
-        if (st != Status::OK) ga->cancel(rv);
+        if (st == Status::OK) break;
+        ga->cancel(rv);
+        // BUSY: a victim was leased meanwhile (another thread): choose again
+        if (st != Status::BUSY || attempt >= 8) break;
+        std::this_thread::yield();
+        rv = Reservation{};
+        st = ga->reserve_scattered(m, &rv);
       }
       if (st == Status::OK) {
         ga->commit(rv, true);

@@ -138,6 +138,10 @@ class ChunkArena {
     return st_.evictions;
   }
   void pin(uint32_t i);
+  // Pin only an ALLOCATED chunk: false when it is reserved for eviction (or
+  // free) - a pin taken after another thread chose the chunk as a victim would
+  // be overwritten by that reservation's commit.
+  bool try_pin(uint32_t i);
   void unpin(uint32_t i);
   bool pinned(uint32_t i);
   void add_reuse_fence(uint32_t i, const FenceRef& f);
