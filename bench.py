@@ -319,6 +319,8 @@ def run_torch_managed(a) -> None:
                 "dth_gb_per_step": round(s["bytes_xfer_dth"] / a.steps / 1e9, 2),
                 "link_gbps": round(s["bytes_xfer_htd"] / dt / 1e9, 2), "evictions": s["evictions"],
                 "vmm_remaps": s["vmm_remaps"], "tlb_flushes": s["tlb_flushes"], "ops": mode.ops,
+                "host_ms_per_step": {k: round(s[k + "_ns"] / 1e6 / a.steps, 1)
+                                     for k in ("place_stable", "vmm_map", "vmm_unmap", "tlb_flush")},
                 "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches, "init_s": round(init_s, 1),
                 "allocs_per_step": (al1["allocs"] - al0["allocs"]) // max(1, a.steps), "alloc_peak_gb":
                 round(al1["peak"] / 1e9, 2), "managed_min_mb": int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")),

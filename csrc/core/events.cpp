@@ -142,7 +142,11 @@ const char* counter_name(Counter c) {
                             "faults_cancelled",
                             "tlb_flushes_elided",
                             "write_invalidations",
-                            "remote_fallbacks"};
+                            "remote_fallbacks",
+                            "vmm_map_ns",
+                            "vmm_unmap_ns",
+                            "tlb_flush_ns",
+                            "place_stable_ns"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -1186,6 +1186,10 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
 Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, const std::vector<bool>& read_dup,
                              Lease* L, Tracker* out, Cause cause) {
   TraceRange tr(be_.get(), "ogkm:place_stable");
+  struct Clock {
+    uint64_t t0 = now_ns();
+    ~Clock() { Tools::get().inc(Counter::PlaceStableNs, now_ns() - t0); }
+  } clock;
   Loc dst = Loc::gpu(gpu);
   ChunkArena* ga = arena_for(dst);
   if (!ga) return Status::INVALID_ARGUMENT;

@@ -591,7 +591,10 @@ void Runtime::stable_unmap_locked(Block* b) {
     RT_ERR("stable VA users of range %llu block %llu failed", (unsigned long long)r->id, (unsigned long long)b->index);
   b->stable_users.clear();
   Tools::get().inc(Counter::VmmRemaps);
-  if (be_->vmm_unmap((char*)r->dev_va + b->block_offset(), kBlockSize) != Status::OK) {
+  const uint64_t t_unmap = now_ns();
+  const Status ust = be_->vmm_unmap((char*)r->dev_va + b->block_offset(), kBlockSize);
+  Tools::get().inc(Counter::VmmUnmapNs, now_ns() - t_unmap);
+  if (ust != Status::OK) {
     Tools::get().inc(Counter::VmmErrors);
     RT_ERR("stable VA unmap of range %llu block %llu failed: %s", (unsigned long long)r->id,
            (unsigned long long)b->index, be_->last_error().c_str());
@@ -676,7 +679,10 @@ void Runtime::stable_map_block(Block* b) {
   stable_unmap_locked(b);  // b's own previous mapping (stale, another chunk)
   char* va = (char*)r->dev_va + b->block_offset();
   Tools::get().inc(Counter::VmmRemaps);
-  if (be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev) == Status::OK) {
+  const uint64_t t_map = now_ns();
+  const Status mst = be_->vmm_map(va, kBlockSize, ha->handle((uint32_t)want), r->stable_dev);
+  Tools::get().inc(Counter::VmmMapNs, now_ns() - t_map);
+  if (mst == Status::OK) {
     b->stable_chunk.store(want);
     // A translation of this VA can still sit in the GPU's TLB only if no
     // flush begun after its last unmap has completed; otherwise (the common
@@ -749,7 +755,10 @@ void Runtime::flush_translations() {
   for (int d = 0; m; ++d, m >>= 1) {
     if (!(m & 1)) continue;
     const uint64_t k = tlb_started_[d].fetch_add(1) + 1;  // covers every unmap before this point
-    if (be_->tlb_flush(d) != Status::OK) {
+    const uint64_t t_fl = now_ns();
+    const Status fst = be_->tlb_flush(d);
+    Tools::get().inc(Counter::TlbFlushNs, now_ns() - t_fl);
+    if (fst != Status::OK) {
       Tools::get().inc(Counter::VmmErrors);
       RT_ERR("GPU %d translation flush after stable-VA remaps failed: %s", d, be_->last_error().c_str());
     } else {

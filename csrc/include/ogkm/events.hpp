@@ -186,6 +186,10 @@ enum class Counter : int {
   TlbFlushesElided, // stable-VA maps that needed no flush (a flush since the VA's last unmap covered it)
   WriteInvalidations,  // blocks whose other copies were revoked for a page-granular write (invalidate_others)
   RemoteFallbacks,     // remote (zero-copy) decisions served by a local copy (acquire allow_remote=false)
+  VmmMapNs,            // host time in stable-VA maps (map + access)
+  VmmUnmapNs,          // host time in stable-VA unmaps
+  TlbFlushNs,          // host time in translation flushes
+  PlaceStableNs,       // host time in stable-VA placement (place_stable, incl. the above and evictions)
   NumCounters
 };
 const char* counter_name(Counter c);
