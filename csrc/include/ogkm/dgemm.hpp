@@ -114,9 +114,6 @@ struct AttnArgs {
                            // measured slower at every bench shape, kept as an explicit option)
 };
 constexpr uint32_t kAttnSplitTokens = 256;
-// split_tokens value selecting the LDS-staged one-wave kernel (64-token splits,
-// k_attn_decode_lds): every K / V row of a split in flight at once.
-constexpr uint32_t kAttnSplitLds = 1064;
 // CPU references of the decode-step ops (fake backend, tests).
 void rmsnorm_cpu(const ResidNormArgs& a);
 void rope_kv_cpu(const RopeKvArgs& a);

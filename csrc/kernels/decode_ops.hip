@@ -552,149 +552,6 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
   }
 }
 
-// LDS-staged one-wave decode attention (hd 64 / 128): one wave per 64-token
-// split. The wave issues ALL of its K and V rows (2 x 64 x hd bf16, 32 KB at
-// hd 128) global -> LDS with global_load_lds before touching any of them, so
-// the whole split's KV is in flight at once: one memory round trip per wave
-// instead of the chain of dependent K-tile / V-batch loads of the register
-// kernels (which leaves the HBM idle at the small grids of tensor-parallel
-// shards: one KV head per rank gives 17 x B waves). Q.K runs on the matrix
-// cores with A fragments read from LDS; K rows are stored chunk-swizzled
-// (row r's 16-byte chunk c at slot (c + r) mod CH of its row) so the 16 rows
-// of an A fragment sit in 16 different banks. P.V stays on the vector ALUs
-// (fp32, p broadcast from LDS). Same split partials as the other kernels.
-template <int HD, int G>
-__global__ void __launch_bounds__(64) k_attn_decode_lds(AttnArgs a) {
-  constexpr int CH = HD / 8;          // 16-byte chunks per row
-  constexpr int RPK = 64 / CH;        // rows per 1 KB global_load_lds block
-  constexpr int NB = 64 / RPK;        // blocks per 64-token tile
-  constexpr int KS = HD / 32;         // 32-dim MFMA steps
-  constexpr int DPV = HD / 32;        // p.v dims per lane
-  constexpr int PU = G <= 4 ? 8 : G <= 8 ? 4 : 2;
-  static_assert((HD == 64 || HD == 128) && G <= 16, "shape");
-  __shared__ __attribute__((aligned(16))) uint16_t ks[64 * HD];
-  __shared__ __attribute__((aligned(16))) uint16_t vs[64 * HD];
-  __shared__ float ps[G][64];
-  const uint32_t g = a.hq / a.hkv;    // <= G
-  const uint32_t split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t wt0 = split * 64u;
-  const int32_t wn = (int32_t)a.len - (int32_t)wt0 < 64 ? (int32_t)a.len - (int32_t)wt0 : 64;
-  if (wn <= 0) return;  // nsplit = ceil(len / 64): never
-  const uint16_t* kbase = a.cache + ((uint64_t)b * a.hkv + kvh) * (uint64_t)a.T * HD + (uint64_t)wt0 * HD;
-  const uint16_t* vbase = a.cache + (((uint64_t)a.B + b) * a.hkv + kvh) * (uint64_t)a.T * HD + (uint64_t)wt0 * HD;
-  {
-    const uint32_t j = lane / CH, sl = lane % CH;  // this lane's row in a block / slot in the row
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const uint32_t r = i * RPK + j, rc = (int32_t)r < wn ? r : (uint32_t)wn - 1;  // rows past the context: clamped
-      const uint32_t c = (sl + CH - (r % CH)) % CH;                                 // K: chunk swizzled by row
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(kbase + (uint64_t)rc * HD + 8 * c),
-                                       reinterpret_cast<char*>(ks) + 1024 * i, 16, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const uint32_t r = i * RPK + j, rc = (int32_t)r < wn ? r : (uint32_t)wn - 1;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(vbase + (uint64_t)rc * HD + 8 * sl),
-                                       reinterpret_cast<char*>(vs) + 1024 * i, 16, 0, 0);
-    }
-  }
-  const uint32_t col = lane & 15, quad = lane >> 4;
-  uint4 qb[KS];
-  const uint16_t* qr = a.q + ((uint64_t)b * a.hq + kvh * g + (col < g ? col : 0)) * HD + 8 * quad;
-#pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    qb[k] = *reinterpret_cast<const uint4*>(qr + 32 * k);
-    if (col >= g) qb[k] = uint4{0u, 0u, 0u, 0u};
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  attn_f32x4_t sc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const uint32_t r = t * 16 + col;
-    attn_f32x4_t acc = attn_f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      const uint32_t c = 4 * k + quad, slot = (r % RPK) * CH + (c + r) % CH;
-      const uint4 ka = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(ks) + 1024 * (r / RPK) + 16 * slot);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(attn_bf16x8_t, ka),
-                                                    __builtin_bit_cast(attn_bf16x8_t, qb[k]), acc, 0, 0, 0);
-    }
-    sc[t] = acc;
-  }
-  // softmax partials: lane = head col, tokens t*16 + 4*quad + r
-  float m = -INFINITY;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int32_t tok = t * 16 + 4 * (int32_t)quad + r;
-      const float v = tok < wn ? sc[t][r] * a.scale : -INFINITY;
-      sc[t][r] = v;
-      m = fmaxf(m, v);
-    }
-  m = fmaxf(m, __shfl_xor(m, 16, 64));
-  m = fmaxf(m, __shfl_xor(m, 32, 64));
-  float l = 0.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = __expf(sc[t][r] - m);
-      l += p;
-      if (col < g) ps[col][t * 16 + 4 * quad + r] = p;
-    }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  // P.V: half a wave per token, DPV dims per lane, V rows from LDS
-  const uint32_t half = lane >> 5, d0 = (lane & 31) * DPV;
-  float o[G][DPV];
-#pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int j = 0; j < DPV; ++j) o[h][j] = 0.f;
-#pragma unroll PU
-  for (int32_t t = (int32_t)half; t < wn; t += 2) {
-    float vf[DPV];
-    if constexpr (DPV == 4) {
-      const uint2 w = *reinterpret_cast<const uint2*>(vs + t * HD + d0);
-      vf[0] = dbf((uint16_t)w.x);
-      vf[1] = dbf((uint16_t)(w.x >> 16));
-      vf[2] = dbf((uint16_t)w.y);
-      vf[3] = dbf((uint16_t)(w.y >> 16));
-    } else {
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(vs + t * HD + d0);
-      vf[0] = dbf((uint16_t)w);
-      vf[1] = dbf((uint16_t)(w >> 16));
-    }
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      const float p = (uint32_t)h < g ? ps[h][t] : 0.f;
-#pragma unroll
-      for (int j = 0; j < DPV; ++j) o[h][j] += p * vf[j];
-    }
-  }
-  // this split's partial (unnormalised) + (max, sum) per head
-#pragma unroll
-  for (int h = 0; h < G; ++h) {
-    if ((uint32_t)h >= g) continue;
-    const float mh = __shfl(m, h, 64), lh = __shfl(l, h, 64);
-    const uint64_t row = ((uint64_t)b * a.hq + kvh * g + h) * a.nsplit + split;
-#pragma unroll
-    for (int j = 0; j < DPV; ++j) {
-      const float x = o[h][j] + __shfl_xor(o[h][j], 32, 64);
-      if (half == 0) a.part_o[row * HD + d0 + j] = x;
-    }
-    if (lane == 0) {
-      a.part_ml[row * 2] = mh;
-      a.part_ml[row * 2 + 1] = lh;
-    }
-  }
-}
-
 // One workgroup of hd threads per (b, q head): merge the splits.
 __global__ void k_attn_combine(AttnArgs a) {
   const uint32_t bh = blockIdx.x;  // b * hq + h
@@ -749,7 +606,7 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
       !a.len || a.len > a.T)
     return hipErrorInvalidValue;
   const bool ws = a.hd == 128 || a.hd == 64;
-  const uint32_t st = ws ? (a.split_tokens == kAttnSplitLds ? 64u : a.split_tokens) : (uint32_t)kAttnSplit;
+  const uint32_t st = ws ? a.split_tokens : (uint32_t)kAttnSplit;
   if ((st != 64 && st != 256) || a.nsplit != (a.len + st - 1) / st) return hipErrorInvalidValue;
   if (a.out_frag && (a.hq * a.hd) % 32) return hipErrorInvalidValue;
   const uint32_t g = a.hq / a.hkv;
@@ -757,15 +614,7 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
   const dim3 grid(a.nsplit, a.hkv, a.B);
   const uint32_t nw = st / 64;
   const size_t lds = (size_t)nw * g * (64 + a.hd) * sizeof(float);
-  if (ws && a.split_tokens == kAttnSplitLds) {
-#define OGKM_ATTN_LDS(HD, L) hipLaunchKernelGGL((k_attn_decode_lds<HD, L>), grid, dim3(64), 0, s, a)
-    if (a.hd == 128) {
-      if (gg == 4) OGKM_ATTN_LDS(128, 4); else if (gg == 8) OGKM_ATTN_LDS(128, 8); else OGKM_ATTN_LDS(128, 16);
-    } else {
-      if (gg == 4) OGKM_ATTN_LDS(64, 4); else if (gg == 8) OGKM_ATTN_LDS(64, 8); else OGKM_ATTN_LDS(64, 16);
-    }
-#undef OGKM_ATTN_LDS
-  } else if (ws) {
+  if (ws) {
 #define OGKM_ATTN_WS(HD, L, NW) hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW>), grid, dim3(64 * NW), lds, s, a)
 #define OGKM_ATTN_WS_G(HD, NW) \
   if (gg == 4) OGKM_ATTN_WS(HD, 4, NW); else if (gg == 8) OGKM_ATTN_WS(HD, 8, NW); else OGKM_ATTN_WS(HD, 16, NW)

@@ -915,14 +915,13 @@ PYBIND11_MODULE(_ogkm, m) {
     a.out_frag = out_frag ? 1 : 0;
     const bool ws = hd == 64 || hd == 128;
     a.split_tokens = ws && split_tokens ? split_tokens : kAttnSplitTokens;
-    if (a.split_tokens != 64 && a.split_tokens != 256 && a.split_tokens != kAttnSplitLds)
-      throw StatusError("attn_decode: split_tokens must be 64, 256 or 1064 (LDS-staged)");
+    if (a.split_tokens != 64 && a.split_tokens != 256)
+      throw StatusError("attn_decode: split_tokens must be 64 or 256");
     a.q = (const uint16_t*)q;
     a.cache = (const uint16_t*)cache;
     a.out = (uint16_t*)out;
     a.B = B; a.hq = hq; a.hkv = hkv; a.hd = hd; a.T = T; a.len = len; a.scale = scale;
-    const uint32_t st = a.split_tokens == kAttnSplitLds ? 64u : a.split_tokens;
-    a.nsplit = (len + st - 1) / st;
+    a.nsplit = (len + a.split_tokens - 1) / a.split_tokens;
     const uint64_t rows = (uint64_t)B * hq * a.nsplit;
     if (rows * (hd + 2) * 4 > part_bytes) throw StatusError("attn_decode: partial workspace too small");
     a.part_o = (float*)part;

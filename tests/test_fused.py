@@ -207,7 +207,7 @@ def test_attention_one_kv_head_gpu(gpu_rt, hq, hkv, length):
 @pytest.mark.gpu
 @pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (16, 4, 64), (8, 1, 64), (4, 4, 128), (12, 2, 128), (16, 1, 128)])
 @pytest.mark.parametrize("length", [1, 63, 64, 65, 700])
-@pytest.mark.parametrize("split_tokens", [64, 256, 1064])  # 1064: LDS-staged one-wave kernel
+@pytest.mark.parametrize("split_tokens", [64, 256])
 def test_attention_group_shapes_gpu(gpu_rt, hq, hkv, hd, length, split_tokens):
     """Every group-size / head-dim instantiation of the wave-split kernel
     (group 1..16 rounded up to 4 / 8 / 16, hd 64 / 128), partial waves included,

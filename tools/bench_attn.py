@@ -31,7 +31,7 @@ def main() -> None:
         kvb = 2 * B * hkv * T * hd * 2
         ncopy = max(1, -(-(1 << 30) // kvb)) if int(os.environ.get("COLD", "1")) else 1
         caches = [torch.randn(2, B, hkv, T, hd, device="cuda").to(torch.bfloat16) for _ in range(ncopy)]
-        st = int(os.environ.get("SPLIT", "0"))  # 0 auto, 64, 256, 1064 (LDS-staged one-wave kernel)
+        st = int(os.environ.get("SPLIT", "0"))  # 0 auto, 64, 256
         for i in range(3):
             fused.attention(q, caches[i % ncopy], L, split_tokens=st)
         torch.cuda.synchronize()
