@@ -57,6 +57,13 @@ def _mode_class():
     from torch.utils._python_dispatch import TorchDispatchMode
     from torch.utils._pytree import tree_flatten
 
+    # the current stream's handle without building a torch.cuda.Stream object
+    # (~2.5 us per op otherwise)
+    _raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+    def _raw_stream(device: int) -> int:
+        return _raw(device) if _raw is not None else torch.cuda.current_stream(device).cuda_stream
+
     def _writes_of(func) -> tuple[frozenset, frozenset]:
         """(positional indices, kwarg names) of the arguments the op writes."""
         pos, names = set(), set()
@@ -102,7 +109,7 @@ def _mode_class():
         # ---------------------------------------------------------- mode
 
         def _stream(self) -> int:
-            return torch.cuda.current_stream(self.device).cuda_stream
+            return _raw_stream(self.device)
 
         def __torch_dispatch__(self, func, types, args=(), kwargs=None):
             kwargs = kwargs or {}
