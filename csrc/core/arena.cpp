@@ -327,6 +327,107 @@ void ChunkArena::pick_victims_by_next_use_locked(uint32_t n, std::vector<uint32_
   }
 }
 
+Status ChunkArena::reserve_for(const std::vector<int64_t>& want, std::vector<uint32_t>* got, Reservation* r) {
+  std::lock_guard<OrderedMutex> g(m_);
+  const uint32_t n = (uint32_t)want.size();
+  constexpr uint32_t kNone = UINT32_MAX;
+  got->assign(n, kNone);
+  r->first = -1;
+  r->n = n;
+  r->victims.clear();
+  r->list.clear();
+  if (n == 0) return Status::OK;
+  auto undo = [&]() {
+    for (uint32_t k : r->list) {
+      ChunkInfo& c = chunks_[k];
+      if (c.state == ChunkState::RESERVED) {
+        c.state = ChunkState::FREE;
+        add_run(k, 1);
+      } else {
+        c.state = ChunkState::ALLOCATED;
+        lru_push_tail(k, 2);
+      }
+    }
+    r->list.clear();
+    r->victims.clear();
+    r->n = 0;
+    got->assign(n, kNone);
+    return Status::NO_MEMORY;
+  };
+  auto take_free = [&](uint32_t i, uint32_t k) {
+    take_run(k, 1);
+    chunks_[k].state = ChunkState::RESERVED;
+    r->list.push_back(k);
+    (*got)[i] = k;
+  };
+  auto take_victim = [&](uint32_t i, uint32_t k) {
+    lru_remove(k);
+    chunks_[k].state = ChunkState::EVICTING;
+    r->list.push_back(k);
+    r->victims.push_back(k);
+    (*got)[i] = k;
+  };
+  // 1. free home chunks
+  uint32_t left = n;
+  for (uint32_t i = 0; i < n; ++i) {
+    const int64_t h = want[i];
+    if (h >= 0 && h < (int64_t)nchunks_ && chunks_[h].state == ChunkState::FREE) {
+      take_free(i, (uint32_t)h);
+      --left;
+    }
+  }
+  uint64_t nfree = 0;
+  for (auto& fr : free_runs_) nfree += fr.second;
+  const uint32_t evict = left > nfree ? (uint32_t)(left - nfree) : 0;
+  std::vector<std::pair<uint64_t, uint32_t>> cand;
+  if (evict) {
+    const uint64_t floor = VictimFloor::value();
+    for (uint32_t i = 0; i < nchunks_; ++i) {
+      const ChunkInfo& c = chunks_[i];
+      if (c.state != ChunkState::ALLOCATED || c.pin_count != 0 || floor_protects_locked(c, floor)) continue;
+      cand.emplace_back(victim_key_locked(c), i);
+    }
+    if (cand.size() < evict) return undo();
+    auto by_key = [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
+      return a.first > b.first || (a.first == b.first && a.second < b.second);
+    };
+    std::partial_sort(cand.begin(), cand.begin() + std::min<size_t>(cand.size(), evict + n), cand.end(), by_key);
+    const uint64_t kthr = cand[evict - 1].first;  // Belady's worst pick for `evict` victims
+    // 2. home chunks that are as good a victim as Belady's own picks
+    uint32_t used = 0;
+    for (uint32_t i = 0; i < n && used < evict; ++i) {
+      const int64_t h = want[i];
+      if ((*got)[i] != kNone || h < 0 || h >= (int64_t)nchunks_) continue;
+      const ChunkInfo& c = chunks_[h];
+      if (c.state != ChunkState::ALLOCATED || c.pin_count != 0 || floor_protects_locked(c, floor)) continue;
+      if (victim_key_locked(c) < kthr) continue;
+      take_victim(i, (uint32_t)h);
+      ++used;
+      --left;
+    }
+    // 3. the rest of the evictions in next-use order
+    size_t ci = 0;
+    for (uint32_t i = 0; i < n && used < evict; ++i) {
+      if ((*got)[i] != kNone) continue;
+      while (ci < cand.size() && chunks_[cand[ci].second].state != ChunkState::ALLOCATED) ++ci;
+      if (ci >= cand.size()) return undo();
+      take_victim(i, cand[ci++].second);
+      ++used;
+      --left;
+    }
+  }
+  // 4. free chunks for the others
+  for (uint32_t i = 0; i < n && left; ++i) {
+    if ((*got)[i] != kNone) continue;
+    if (free_runs_.empty()) return undo();
+    take_free(i, free_runs_.begin()->first);
+    --left;
+  }
+  if (left) return undo();
+  st_.reservations++;
+  return Status::OK;
+}
+
 Status ChunkArena::reserve_scattered(uint32_t n, Reservation* r) {
   std::lock_guard<OrderedMutex> g(m_);
   if (n == 0 || n > nchunks_) return Status::NO_MEMORY;

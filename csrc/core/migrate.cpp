@@ -488,6 +488,24 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
   Status st = populate(c, b, dst, hint, &to);
   if (st != Status::OK) return st;
   PageMask missing = pages.andnot(to->resident);
+  if (missing.empty() && dst.is_gpu()) {
+    // Already resident here (the common case of a lease on a unit that stayed
+    // in HBM): nothing moves, so no copies, no events, no CPU-view / table
+    // refresh and no perf-module migration notice - only a write must still
+    // revoke the other copies of these pages, and a stale stable-VA mapping
+    // is still refreshed.
+    bool others = false;
+    if (!read_dup)
+      for (auto& r : b->res)
+        if (&r != to && r.resident.intersects(pages)) others = true;
+    if (!others) {
+      touch_residency(b, to, cause == Cause::Prefetch);
+      b->last_access_ns = now_ns();
+      if (b->range->dev_va && (b->stable_chunk.load() != to->chunk || b->stale_mapping.load()))
+        c.cpu_refresh.push_back(b);
+      return Status::OK;
+    }
+  }
   bool copied = false;
   if (!missing.empty() && to->fmt == 1) {
     // Raw pages are about to land in an encoded chunk: expand it in place first.
@@ -1238,6 +1256,31 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
         }
         break;
       }
+    }
+    if (!G.need.empty() && ga->next_use_mode() && config().global_oversubscription &&
+        inject_.alloc_fail_after.load() < 0) {
+      // Next-use mode: every block back on its home chunk when that is free or
+      // an eviction victim as good as any (ChunkArena::reserve_for) - a block
+      // whose stable VA still maps its chunk needs no remap and no flush.
+      std::vector<uint32_t> got;
+      Reservation rv;
+      st = ga->reserve_for(hints, &got, &rv);
+      for (int attempt = 0; st == Status::OK; ++attempt) {
+        st = evict_batch(ga, rv.victims);
+        if (st == Status::OK) break;
+        ga->cancel(rv);
+        if (st != Status::BUSY || attempt >= 8) break;
+        std::this_thread::yield();
+        rv = Reservation{};
+        st = ga->reserve_for(hints, &got, &rv);
+      }
+      if (st == Status::OK) {
+        ga->commit(rv, true);
+        if (!rv.victims.empty()) Tools::get().inc(Counter::AllocRetries);
+        G.chunks.assign(got.begin(), got.end());
+      }
+      groups.push_back(std::move(G));
+      continue;
     }
     for (size_t k = 0; k < G.need.size(); ++k) {
       uint32_t ch = 0;

@@ -88,6 +88,14 @@ class ChunkArena {
   // no contiguity): free chunks first, then victims in reserve(1)'s order.
   // All or nothing.
   Status reserve_scattered(uint32_t n, Reservation* r);
+  // Next-use mode: one chunk per requested block, honouring each block's home
+  // chunk `want[i]` (the chunk its stable VA still maps, -1 = none) - free, or
+  // an eviction victim as good as Belady's own choice (its next use no sooner
+  // than the furthest-needed chunks that would be evicted otherwise). A block
+  // back on its home chunk needs no VMM remap and no translation flush. The
+  // rest: free chunks, then next-use victims. got[i] = the block's chunk; all
+  // or nothing (NO_MEMORY).
+  Status reserve_for(const std::vector<int64_t>& want, std::vector<uint32_t>* got, Reservation* r);
   void commit(const Reservation& r, bool pin = false);  // window -> ALLOCATED (owners set later)
   void cancel(const Reservation& r);                // give the window back
   void free(uint32_t first, uint32_t n);

@@ -41,6 +41,9 @@ lib.configure("fake_race_check", 1)  # engine copy vs kernel on one chunk -> "[f
 lib.inject("tlb_mode", %d)  # 1: a remapped VA serves its old chunk until a translation flush
 lib.init_device(0, 24 * MB)  # 12 chunks
 PREFETCH = %d  # asynchronous op-trace prefetches between ops (the prefetch worker remaps concurrently)
+HINTS = %d  # next-use hints on every op: Belady victims and home-chunk placement (ChunkArena::reserve_for)
+if PREFETCH:
+    lib.configure("torch_async_prefetch", 1)
 s = lib.debug_stream_create(0)
 rng = random.Random(%d)
 live = []
@@ -68,9 +71,13 @@ for it in range(%d):
         # host duplicates valid): only writers count
         lib.debug_touch(s, p, n, rng.choice([0, 100, 400]), w)
         touches[p] += int(w)
-    lib.torch_op_end(held, [], 0, s)
+    if HINTS:
+        lib.torch_op_end(held, [], 0, s, [(p, it + 1 + rng.randint(0, 40)) for p, _ in ops], it + 1)
+    else:
+        lib.torch_op_end(held, [], 0, s)
     if PREFETCH and rng.random() < 0.6:
-        lib.torch_prefetch([(q, 0) for q, _ in rng.sample(live, min(2, len(live)))], 0)
+        lib.torch_prefetch([(q, it + 1 + rng.randint(0, 40) if HINTS else 0)
+                            for q, _ in rng.sample(live, min(2, len(live)))], 0)
     r = rng.random()
     if r < 0.1 and len(live) > 4:
         p, n = live.pop(rng.randrange(len(live)))
@@ -96,15 +103,16 @@ print("STRESS_OK", st["evictions"], st["vmm_remaps"], st["tlb_flushes"], st["vmm
 '''
 
 
-@pytest.mark.parametrize("lazy,batch,seed,tlb,prefetch", [(0, 32, 1, 0, 0), (1, 32, 2, 0, 0), (0, 1, 3, 0, 0),
-                                                         (1, 2, 4, 0, 0), (0, 32, 5, 1, 1), (1, 2, 6, 1, 1),
-                                                         (0, 4, 7, 0, 1)])
-def test_stable_va_stress_async_users(lazy, batch, seed, tlb, prefetch):
+@pytest.mark.parametrize("lazy,batch,seed,tlb,prefetch,hints", [(0, 32, 1, 0, 0, 0), (1, 32, 2, 0, 0, 0), (0, 1, 3, 0, 0, 0),
+                                                               (1, 2, 4, 0, 0, 0), (0, 32, 5, 1, 1, 0), (1, 2, 6, 1, 1, 0),
+                                                               (0, 4, 7, 0, 1, 0), (1, 32, 8, 1, 0, 1), (0, 4, 9, 1, 1, 1),
+                                                               (1, 2, 10, 0, 1, 1)])
+def test_stable_va_stress_async_users(lazy, batch, seed, tlb, prefetch, hints):
     """tlb=1: the fake translation model of gfx950 VMM - a lost update means a
     kernel ran on a stale mapping (a flush missing or not yet complete);
     prefetch=1: the asynchronous prefetch worker evicts / remaps / flushes
     concurrently with the dispatching thread's op holds."""
-    code = WORKER % (ROOT, lazy, batch, tlb, prefetch, seed, 300)
+    code = WORKER % (ROOT, lazy, batch, tlb, prefetch, hints, seed, 300)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
     assert "STRESS_OK" in r.stdout
