@@ -322,6 +322,7 @@ def run_torch_managed(a) -> None:
                 "host_ms_per_step": {k: round(s[k + "_ns"] / 1e6 / a.steps, 1)
                                      for k in ("place_stable", "vmm_map", "vmm_unmap", "tlb_flush")},
                 "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches, "init_s": round(init_s, 1),
+                "trace_len": len(mode._trace), "hinted_ops": mode.hinted_ops, "trace_misses": mode.trace_misses,
                 "allocs_per_step": (al1["allocs"] - al0["allocs"]) // max(1, a.steps), "alloc_peak_gb":
                 round(al1["peak"] / 1e9, 2), "managed_min_mb": int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")),
                 "lookahead_mb": la},

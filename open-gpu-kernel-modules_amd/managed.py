@@ -98,6 +98,8 @@ def _mode_class():
             self._requested: dict[int, int] = {}  # operand -> op-clock time a prefetch was queued for
             self.ops = 0
             self.faulted_ops = 0
+            self.hinted_ops = 0      # ops whose operands got next-use hints (position found in the trace)
+            self.trace_misses = 0    # ops with persistent operands not found in the recorded trace
             # OGKM_MODE_TRACE=N: remember the last N ops, printed when one fails.
             import collections
             import os
@@ -244,6 +246,7 @@ def _mode_class():
                 self._pos = n
                 return (), ()
             else:
+                self.trace_misses += 1
                 return (), ()  # an op outside the recorded pass
             if self._recording:
                 self._pos = new
@@ -254,6 +257,7 @@ def _mode_class():
             now = self._abs
             nd = self._nextd[new]
             hints = [(p, now + nd[p]) for p in key]
+            self.hinted_ops += 1
             want = []
             if self.lookahead_bytes > 0:
                 seen, budget = set(key), self.lookahead_bytes

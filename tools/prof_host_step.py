@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--weight-format", default="ans")
     ap.add_argument("--kv-format", default="ans")
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--planner", default="static")
+    ap.add_argument("--warmup", type=int, default=1)
     a = ap.parse_args()
     import torch
 
@@ -31,11 +33,12 @@ def main():
     from ogkm.models import llama
     rt.init("hip", host_budget_mb=0)
     cfg = llama.CONFIGS[a.model]
-    m = llama.TieredLlama(cfg, batch=a.batch, context=1024, max_new_tokens=2 * a.steps + 8, oversub=a.oversub,
+    m = llama.TieredLlama(cfg, batch=a.batch, context=1024, max_new_tokens=2 * a.steps + a.warmup + 8, oversub=a.oversub,
                           tp_rank=0, tp_world=a.simulate_tp, weight_format=a.weight_format, kv_format=a.kv_format,
-                          lookahead=1)
+                          lookahead=1, planner=a.planner)
     tok = torch.zeros(a.batch, dtype=torch.int64, device="cuda")
-    tok = m.step(tok)
+    for _ in range(a.warmup):
+        tok = m.step(tok)
     torch.cuda.synchronize()
     # unprofiled: host enqueue time vs synchronized step time (GPU-starved when close)
     t0 = time.perf_counter()
