@@ -414,7 +414,10 @@ class FakeBackend : public Backend {
     return Status::OK;
   }
   Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {
-    run(s, [a, mode] { dgemm_cpu(a, mode != DGEMM_W_RAW); });
+    run(s, [a, mode] {
+      dgemm_cpu(a, mode != DGEMM_W_RAW);
+      if (a.fix_cnt) dgemm_reduce_cpu(a.fix);  // the in-kernel fixup's result
+    });
     return Status::OK;
   }
   Status dgemm_reduce(int, const DGemmReduceArgs& a, void* s) override {

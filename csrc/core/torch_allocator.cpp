@@ -85,13 +85,15 @@ struct DevAlloc {
     // pages of the op's views for an op hold.
     uint64_t lease_off = 0, lease_len = 0;
     uint64_t next_use = 0;    // last next-use hint applied (op clock)
-    // Long-lived (parameters, buffers, caches): held by two ops at least
-    // torch_persistent_ops ops apart. Activations are consumed within a few ops
-    // and get a new address every pass; the transparent mode's prefetcher keys
-    // its trace on persistent operands only.
+    // Long-lived (parameters, buffers, caches): held again at least
+    // torch_persistent_ops ops after its first hold. Activations die within a
+    // layer (a residual stream lives ~35 ops) and their recycled addresses come
+    // back every layer - keyed on them, the transparent mode's op trace would
+    // see its first repeat inside the first layer; it keys on persistent
+    // operands only.
     bool persistent = false;
     bool held_once = false;
-    uint64_t last_hold_op = 0;
+    uint64_t first_hold_op = 0;
     uint32_t prefetching = 0;  // the prefetch worker is placing it (a free waits for it)
   };
   std::unordered_map<uint64_t, Managed> managed;   // stable VA -> range
@@ -575,10 +577,12 @@ Status torch_op_begin(const std::vector<TorchOperand>& ops, int device, void* st
       st = rt->invalidate_others(m.r, o.written, device);
       if (st != Status::OK) return undo(st);
     }
-    if (m.held_once && da->op_seq - m.last_hold_op >= (uint64_t)std::max<int64_t>(1, config().torch_persistent_ops))
+    if (!m.held_once) {
+      m.held_once = true;
+      m.first_hold_op = da->op_seq;
+    } else if (da->op_seq - m.first_hold_op >= (uint64_t)std::max<int64_t>(1, config().torch_persistent_ops)) {
       m.persistent = true;
-    m.held_once = true;
-    m.last_hold_op = da->op_seq;
+    }
     if (m.persistent) persistent->push_back(o.ptr);
     da->op_holds++;
   }

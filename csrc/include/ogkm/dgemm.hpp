@@ -6,6 +6,17 @@
 
 namespace ogkm {
 
+enum DGemmEpilogue : uint32_t { DGEMM_EPI_STORE = 0, DGEMM_EPI_RESID = 1, DGEMM_EPI_SILU_MUL = 2 };
+struct DGemmReduceArgs {
+  const float* part;
+  uint32_t ksplit, M, N;   // N = columns of part (SILU_MUL: 2 f, gate then up)
+  uint32_t epi;
+  const uint16_t* resid;   // RESID: bf16 [M, ldr]
+  uint32_t ldr, ldo;
+  uint16_t* out;           // bf16 [M, ldo] (may alias resid)
+  uint32_t out_frag;       // 1: out is fragment-ordered [M16][out_cols]; this launch writes columns
+  uint32_t out_cols, out_col0;  // out_col0 .. out_col0 + nout of it (ldo unused)
+};
 // Decode GEMM (csrc/kernels/decode_gemm.hip): part[ks][M][N] = X[M,K] . W[N,K]^T
 // over K split `ks`, with W in fragment order (16x32 MFMA A-tiles, 1 KB each)
 // either as raw bf16 or inside a BF11/raw packed stream (decoded in registers).
@@ -25,6 +36,16 @@ struct DGemmArgs {
   uint32_t depth;         // pipelined raw kernel: 0 / 4 = k_dgemm_pipe (two register sets of 2 K
                           // steps), 10 D = k_dgemm_lring (LDS ring of D K steps, D = 3..7)
   uint32_t x_frag;        // 1: x is fragment-ordered (frag_index below; rows padded to 16, ldx unused)
+  // In-kernel split-K fixup (k_dgemm_pipe / k_dgemm_lring): when set, every
+  // wave counts its arrival on its output group's counter (agent-scope
+  // atomic between release / acquire fences); the last of the group's
+  // ksplit (SILU_MUL: 2 ksplit - the gate and up row blocks) sums the splits
+  // and applies `fix`'s epilogue - no k_dgemm_reduce launch. Counters are
+  // zero between launches (the last arrival resets its own); one slab per
+  // stream. Group = row block (SILU_MUL: row block mod row_blocks / 2,
+  // needs (N / 2) % 64 == 0); index blockIdx.y * row_blocks + group.
+  uint32_t* fix_cnt;
+  DGemmReduceArgs fix;
 };
 
 // Fragment order of an [M, K] bf16 activation (K % 32 == 0, M padded to a
@@ -41,17 +62,15 @@ constexpr uint64_t frag_index(uint32_t m, uint32_t k, uint32_t K) {
 // Weight source: raw bf16 fragments; a packed stream with BF11 and raw chunks;
 // a packed stream whose chunks are all BF11 (fast, phase-pipelined path).
 enum DGemmWeights : int { DGEMM_W_RAW = 0, DGEMM_W_PACKED = 1, DGEMM_W_PACKED_BF11 = 2 };
-enum DGemmEpilogue : uint32_t { DGEMM_EPI_STORE = 0, DGEMM_EPI_RESID = 1, DGEMM_EPI_SILU_MUL = 2 };
-struct DGemmReduceArgs {
-  const float* part;
-  uint32_t ksplit, M, N;   // N = columns of part (SILU_MUL: 2 f, gate then up)
-  uint32_t epi;
-  const uint16_t* resid;   // RESID: bf16 [M, ldr]
-  uint32_t ldr, ldo;
-  uint16_t* out;           // bf16 [M, ldo] (may alias resid)
-  uint32_t out_frag;       // 1: out is fragment-ordered [M16][out_cols]; this launch writes columns
-  uint32_t out_cols, out_col0;  // out_col0 .. out_col0 + nout of it (ldo unused)
-};
+// The fixup runs in the pipelined raw kernels only (k_dgemm_pipe /
+// k_dgemm_lring: raw weights, unroll 1, no LDS-x), with `fix` describing the
+// same partial slab; SILU_MUL pairs gate row block g with up row block
+// g + row_blocks / 2, so the halves must be whole 64-row blocks.
+inline bool dgemm_fixup_ok(const DGemmArgs& a, int mode) {
+  if (mode != DGEMM_W_RAW || a.unroll != 1 || a.lds_x) return false;
+  if (a.fix.part != a.part || a.fix.ksplit != a.ksplit || a.fix.M != a.M || a.fix.N != a.N) return false;
+  return a.fix.epi != DGEMM_EPI_SILU_MUL || (a.N / 2) % 64 == 0;
+}
 // Split-K plan: enough waves to fill the chip (>= ~4 per CU over 256 CUs) while
 // keeping each split's K range a multiple of 32.
 inline void dgemm_plan(uint32_t N, uint32_t K, uint32_t target_units, uint32_t* ksplit, uint32_t* klen) {

@@ -377,13 +377,9 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
 }
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
 
-// One thread = 4 consecutive output columns of one row.
-__global__ void __launch_bounds__(256) k_dgemm_reduce(DGemmReduceArgs a) {
+// Split-K sum + epilogue of 4 consecutive output columns (n .. n + 3) of row m.
+__device__ __forceinline__ void dg_reduce_quad(const DGemmReduceArgs& a, uint32_t m, uint32_t n) {
   const uint32_t nout = a.epi == DGEMM_EPI_SILU_MUL ? a.N / 2 : a.N;
-  const uint32_t q = nout / 4;
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (uint64_t)a.M * q) return;
-  const uint32_t m = (uint32_t)(i / q), n = (uint32_t)(i - (uint64_t)m * q) * 4u;
   f32x4_t s = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
   // Batches of 8 split rows: all loads of a batch are issued before the first
   // add (8 requests in flight per lane instead of one dependent load per split;
@@ -423,6 +419,95 @@ __global__ void __launch_bounds__(256) k_dgemm_reduce(DGemmReduceArgs a) {
   }
   uint16_t* dst = a.out_frag ? a.out + frag_index(m, a.out_col0 + n, a.out_cols) : a.out + (uint64_t)m * a.ldo + n;
   *reinterpret_cast<u32x2_t*>(dst) = u32x2_t{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
+}
+
+// One thread = 4 consecutive output columns of one row.
+__global__ void __launch_bounds__(256) k_dgemm_reduce(DGemmReduceArgs a) {
+  const uint32_t nout = a.epi == DGEMM_EPI_SILU_MUL ? a.N / 2 : a.N;
+  const uint32_t q = nout / 4;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)a.M * q) return;
+  const uint32_t m = (uint32_t)(i / q), n = (uint32_t)(i - (uint64_t)m * q) * 4u;
+  dg_reduce_quad(a, m, n);
+}
+
+// In-kernel split-K fixup (DGemmArgs::fix_cnt), called by every wave of
+// k_dgemm_pipe / k_dgemm_lring after its partial stores (the counter form of
+// cdna_hip_programming.md's in-launch split-K reduction): the agent-scope
+// release fence writes this wave's partials back from its XCD's L2 before its
+// arrival is counted; the group's last arrival fences acquire (so it reads the
+// other XCDs' partials, not stale lines), resets the counter for the next
+// launch and writes the group's 64 output columns x (up to) 64 rows - 8 quads
+// per lane per batch with every split load issued before the first add (the
+// reducer is one wave: its loads in flight set its speed). Summation order
+// is k ascending, as in k_dgemm_reduce: the output is bit-identical.
+__device__ __forceinline__ void dg_fixup(const DGemmArgs& a, uint32_t rb, uint32_t lane) {
+  const bool silu = a.fix.epi == DGEMM_EPI_SILU_MUL;
+  const uint32_t groups = silu ? a.row_blocks / 2 : a.row_blocks;
+  const uint32_t g = rb < groups ? rb : rb - groups;
+  uint32_t* cnt = a.fix_cnt + (uint64_t)blockIdx.y * a.row_blocks + g;
+  const uint32_t arrivals = silu ? 2u * a.ksplit : a.ksplit;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fence's own wait can be dropped (guide, Pitfall 12)
+  uint32_t old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (old + 1u != arrivals) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const DGemmReduceArgs& r = a.fix;
+  const uint32_t nout = silu ? r.N / 2 : r.N;
+  const uint32_t n0 = g * 64u, m0 = blockIdx.y * 64u;
+  const uint32_t items = (r.M - m0 < 64u ? r.M - m0 : 64u) * 16u;
+  constexpr int kQ = 8;
+  for (uint32_t i0 = 0; i0 < items; i0 += 64u * kQ) {
+    uint32_t mm[kQ], nn[kQ];
+    bool ok[kQ];
+    f32x4_t s[kQ], u[kQ];
+#pragma unroll
+    for (int j = 0; j < kQ; ++j) {
+      const uint32_t i = i0 + j * 64u + lane;
+      mm[j] = m0 + (i >> 4);
+      nn[j] = n0 + (i & 15u) * 4u;
+      ok[j] = i < items && nn[j] < nout;
+      s[j] = u[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    for (uint32_t k = 0; k < r.ksplit; ++k) {
+      f32x4_t v[kQ], w[kQ];
+#pragma unroll
+      for (int j = 0; j < kQ; ++j) {
+        const float* row = r.part + ((uint64_t)k * r.M + (ok[j] ? mm[j] : m0)) * r.N;
+        v[j] = *reinterpret_cast<const f32x4_t*>(row + (ok[j] ? nn[j] : 0u));
+        if (silu) w[j] = *reinterpret_cast<const f32x4_t*>(row + nout + (ok[j] ? nn[j] : 0u));
+      }
+#pragma unroll
+      for (int j = 0; j < kQ; ++j) {
+        s[j] += v[j];
+        if (silu) u[j] += w[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kQ; ++j) {
+      if (!ok[j]) continue;
+      uint16_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float y = s[j][e];
+        if (r.epi == DGEMM_EPI_RESID) {
+          y = bf16_to_f32(f32_to_bf16_rne(y)) + bf16_to_f32(r.resid[(uint64_t)mm[j] * r.ldr + nn[j] + e]);
+        } else if (silu) {
+          const float gt = bf16_to_f32(f32_to_bf16_rne(y)), up = bf16_to_f32(f32_to_bf16_rne(u[j][e]));
+          y = gt / (1.f + __expf(-gt)) * up;
+        }
+        o[e] = f32_to_bf16_rne(y);
+      }
+      uint16_t* dst = r.out_frag ? r.out + frag_index(mm[j], r.out_col0 + nn[j], r.out_cols)
+                                 : r.out + (uint64_t)mm[j] * r.ldo + nn[j];
+      *reinterpret_cast<u32x2_t*>(dst) =
+          u32x2_t{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
+    }
+  }
 }
 
 // Raw-weight variant with the activations shared through LDS: a workgroup's 4
@@ -615,6 +700,7 @@ __global__ void __launch_bounds__(256, 2) k_dgemm_pipe(DGemmArgs a) {
       if (m < a.M) *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[r][mt];
     }
   }
+  if (a.fix_cnt) dg_fixup(a, rb, lane);
 }
 
 // k_dgemm_lring: the same split-K unit (4 row tiles x one K range, one wave per
@@ -728,11 +814,13 @@ __global__ void __launch_bounds__(64) k_dgemm_lring(DGemmArgs a) {
       if (m < a.M) *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[r][mt];
     }
   }
+  if (a.fix_cnt) dg_fixup(a, rb, lane);
 }
 
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s) {
   if (a.N % 16 || a.K % 32 || a.klen % 32 || !a.ksplit || a.row_blocks != (a.N / 16 + kRowTiles - 1) / kRowTiles)
     return hipErrorInvalidValue;
+  if (a.fix_cnt && !dgemm_fixup_ok(a, mode)) return hipErrorInvalidValue;
   const uint32_t units = a.row_blocks * a.ksplit;
   if (mode == DGEMM_W_RAW && a.lds_x) {
     dim3 grid(units, (a.M + kMTiles * 16 - 1) / (kMTiles * 16));

@@ -5,7 +5,9 @@ W is stored in *fragment order* (16 x 32 tiles, 1 KB each, lane-major = the
 A-operand fragment of v_mfma_f32_16x16x32_bf16), either as raw bf16 or inside a
 BF11 packed stream (ops/bf12.py, "bf11s": BF11-or-raw chunks) that the kernel
 decodes in registers - the packed bytes are the only weight bytes read from HBM
-and no bf16 staging copy exists. Epilogues are fused into the split-K reduce:
+and no bf16 staging copy exists. Epilogues are fused into the split-K sum
+(in-kernel for raw weights: the last-arriving wave of each output group runs
+it; a k_dgemm_reduce launch otherwise):
 ``store``, ``resid`` (out = resid + x @ W^T, in place allowed) and ``silu_mul``
 (W = [gate; up] rows, out = silu(gate) * up).
 
@@ -62,6 +64,11 @@ DEPTH = int(os.environ.get("OGKM_DGEMM_DEPTH", "0"))
 LRING_DEPTH = int(os.environ.get("OGKM_DGEMM_LRING_DEPTH", "50"))
 LRING_UNITS = int(os.environ.get("OGKM_DGEMM_LRING_UNITS", "512"))
 LRING_MAX_STEPS = int(os.environ.get("OGKM_DGEMM_LRING_MAX_STEPS", "96"))
+# Split-K fixup inside the pipelined raw kernels (the last-arriving wave of an
+# output group sums the splits and runs the epilogue) instead of a
+# k_dgemm_reduce launch; 0 = always launch the reduce.
+FIXUP = int(os.environ.get("OGKM_DGEMM_FIXUP", "1"))
+FIX_SLOTS = 1 << 16  # arrival counters per (device, stream): grid.y x row blocks
 
 
 def frag_permute(w: torch.Tensor) -> torch.Tensor:
@@ -141,6 +148,17 @@ class _Workspace:
 
 _WS = _Workspace()
 _PLANS: dict = {}
+_FIX: dict = {}
+
+
+def _fix_counters(device: torch.device, stream: int) -> torch.Tensor:
+    """The zeroed arrival-counter slab of the in-kernel fixup for one stream
+    (kernels on one stream never overlap; each last arrival re-zeroes its own)."""
+    key = (str(device), stream)
+    t = _FIX.get(key)
+    if t is None:
+        t = _FIX[key] = torch.zeros(FIX_SLOTS, dtype=torch.int32, device=device)
+    return t
 
 
 _PIPE_PLANS: dict = {}
@@ -214,7 +232,9 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     """x: [M, K] bf16 (row stride % 8 == 0). Returns out [M, N] (silu_mul: [M, N/2]).
     Raw weights run the pipelined kernels (k_dgemm_lring / k_dgemm_pipe, see
     _pipe_plan; ``lds``=1: k_dgemm_lds), packed ones k_dgemm's in-register decode;
-    k_dgemm_reduce sums the K splits and runs the epilogue. ``defer``: no
+    the pipelined raw kernels sum the K splits and run the epilogue themselves
+    (FIXUP: the last-arriving wave of each output group), the others leave it
+    to a k_dgemm_reduce launch. ``defer``: no
     reduce launch - returns a Deferred whose consumer (fused.rms_norm's
     residual form, fused.rope_kv) sums the splits and applies the epilogue.
     ``x_rows``: x is a fragment-ordered [frag_rows(x_rows), K] buffer (to_frag)
@@ -248,8 +268,10 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     if epi == "resid":
         if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
             raise ValueError("dgemm.linear: resid must match out")
+    fix = _fix_counters(x.device, stream) if FIXUP and unroll == 1 and not lds_ and w.mode == MODE_RAW else None
     lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), ldx, m, w.n, w.k,
               part.data_ptr(), part.numel() * 4, EPI[epi], resid.data_ptr() if resid is not None else 0,
               resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, unroll, lds_,
-              WG_WAVES, depth, True, xf, out_frag, out.shape[1] if out_frag else 0, out_col0)
+              WG_WAVES, depth, True, xf, out_frag, out.shape[1] if out_frag else 0, out_col0,
+              fix.data_ptr() if fix is not None else 0, FIX_SLOTS if fix is not None else 0)
     return out

@@ -183,6 +183,38 @@ def test_op_hold_nests_with_allocation_hold(managed_rt):
     lib.torch_free(p, 0)
 
 
+def test_recycled_activation_never_keys_the_trace(managed_rt):
+    """A residual-stream activation lives ~35 ops and its address comes back
+    every layer (the allocation cache): held at both ends of its life it must
+    not count as long-lived (the stock 70B's 1 MB residual did, and the op
+    trace saw its first repeat inside layer one); a parameter used once per
+    pass does."""
+    lib.configure("torch_persistent_ops", 64)
+    try:
+        w = lib.torch_alloc(8 * MB, 0)  # a parameter
+        h, pers = lib.torch_op_begin([(w, False)], 0, 0)
+        lib.torch_op_end(h, [], 0, 0)
+        other = lib.torch_alloc(4 * MB, 0)
+        addrs = set()
+        for layer in range(6):
+            x = lib.torch_alloc(4 * MB, 0)
+            addrs.add(x)
+            for j in range(40):
+                ops = [(x, False)] if j in (0, 39) else [(other, False)]
+                h, pers = lib.torch_op_begin(ops, 0, 0)
+                assert x not in pers
+                lib.torch_op_end(h, [], 0, 0)
+            lib.torch_free(x, 0)
+        assert len(addrs) < 6  # the address was recycled
+        h, pers = lib.torch_op_begin([(w, False)], 0, 0)
+        assert pers == [w]
+        lib.torch_op_end(h, [], 0, 0)
+        lib.torch_free(other, 0)
+        lib.torch_free(w, 0)
+    finally:
+        lib.configure("torch_persistent_ops", 128)
+
+
 @pytest.mark.parametrize("lazy", [0, 1])
 def test_stable_placement_batches_evictions(managed_rt, lazy):
     """A stable-VA lease needs no contiguous extent: blocks take any chunk,

@@ -9,6 +9,7 @@ import time
 import pytest
 import torch
 
+from ogkm._native import lib
 from ogkm.ops import bf12, dgemm
 
 
@@ -208,3 +209,53 @@ def test_dgemm_gpu_bandwidth_70b_shapes(gpu_rt, packed):
     # ~90 % of the measured rates (profiles/r3_dgemm_xfrag.md: raw 4.9 TB/s on
     # MALL-cold weights, 4.94 in this test; the in-register BF11 decode 0.88 TB/s)
     assert total_bytes / total_t > (0.78e12 if packed else 4.3e12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [4, 50])
+@pytest.mark.parametrize("epi", ["store", "resid", "silu_mul"])
+@pytest.mark.parametrize("n,k,m,frag", [(256, 1024, 64, False), (1024, 2048, 80, False), (336, 1024, 7, False),
+                                        (320, 1024, 7, False), (512, 4096, 64, True)])
+def test_dgemm_gpu_fixup_matches_reduce_launch(gpu_rt, depth, epi, n, k, m, frag):
+    """The in-kernel split-K fixup (the last-arriving wave of each output
+    group sums the splits and runs the epilogue) is bit-identical to the
+    k_dgemm_reduce launch it replaces, across repeated launches (the counters
+    reset themselves), two M blocks (m = 80), a partial row block (n = 336)
+    and fragment-ordered outputs; SiLU with (N / 2) % 64 != 0 falls back to
+    the reduce launch."""
+    if epi == "silu_mul" and n % 32:
+        pytest.skip("SiLU needs N % 32 == 0")
+    if frag and epi == "resid":
+        pytest.skip("fragment-ordered out takes no residual")
+    w = _weights(n, k, 11, specials=False)
+    x = (torch.randn(m, k) * 0.5).to(torch.bfloat16)
+    resid = (torch.randn(m, n) * 0.1).to(torch.bfloat16).cuda()
+    buf, ref_w = _place(w, False, "cuda")
+    xd = x.cuda()
+    nout = n // 2 if epi == "silu_mul" else n
+
+    def run(fix):
+        f0, d0 = dgemm.FIXUP, dgemm.DEPTH
+        dgemm.FIXUP, dgemm.DEPTH = fix, depth
+        try:
+            outs = []
+            for _ in range(3):
+                o = torch.zeros(dgemm.frag_rows(m) if frag else m, nout, dtype=torch.bfloat16, device="cuda")
+                if epi == "resid":
+                    o.copy_(resid)
+                dgemm.linear(xd, ref_w, epi, resid=o if epi == "resid" else None, out=o, out_frag=frag)
+                outs.append(o)
+            return outs
+        finally:
+            dgemm.FIXUP, dgemm.DEPTH = f0, d0
+
+    base = run(0)
+    n0 = lib.dgemm_fixups()
+    fused = run(1)
+    torch.cuda.synchronize()
+    engaged = lib.dgemm_fixups() - n0
+    assert engaged == (0 if epi == "silu_mul" and (n // 2) % 64 else 3)
+    for o in fused:
+        assert torch.equal(o, base[0])
+    got = dgemm.from_frag(base[0], m) if frag else base[0]
+    torch.testing.assert_close(got.float().cpu(), _ref(x, w, epi, resid.cpu()), atol=2e-2, rtol=2e-2)
