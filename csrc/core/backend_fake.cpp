@@ -416,7 +416,7 @@ class FakeBackend : public Backend {
   Status dgemm(int, const DGemmArgs& a, int mode, void* s) override {
     run(s, [a, mode] {
       dgemm_cpu(a, mode != DGEMM_W_RAW);
-      if (a.fix_cnt) dgemm_reduce_cpu(a.fix);  // the in-kernel fixup's result
+      if (a.fix_cnt || a.direct) dgemm_reduce_cpu(a.fix);  // the in-kernel epilogue's result
     });
     return Status::OK;
   }

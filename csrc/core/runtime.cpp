@@ -1214,6 +1214,29 @@ Status Runtime::fill(Range* r, uint64_t off, uint64_t bytes, uint32_t pattern) {
 }
 
 // ------------------------------------------------------------------ introspection
+uint64_t Runtime::resident_bytes(Range* r, Loc loc, uint64_t off, uint64_t len) {
+  if (!r || r->type != RangeType::MANAGED || off >= r->size) return 0;
+  const uint64_t end = len > r->size - off ? r->size : off + len;
+  std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  uint64_t n = 0;
+  for (uint64_t bi = off >> kBlockShift; bi <= (end - 1) >> kBlockShift; ++bi) {
+    Block* b = r->block(bi);
+    const uint64_t b0 = bi << kBlockShift;
+    const uint64_t p0 = off > b0 ? (off - b0) >> kPageShift : 0;
+    const uint64_t p1 = std::min<uint64_t>(kBlockSize, end - b0 + kPageSize - 1) >> kPageShift;
+    std::lock_guard<OrderedMutex> g(b->lock);
+    for (auto& x : b->res) {
+      if (!(x.loc == loc)) continue;
+      if (p0 == 0 && p1 == kPagesPerBlock) {
+        n += (uint64_t)x.resident.count() << kPageShift;
+      } else {
+        for (uint64_t p = p0; p < p1; ++p) n += x.resident.test(p) ? kPageSize : 0;
+      }
+    }
+  }
+  return n;
+}
+
 Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
   if (!r || off >= r->size) return Status::INVALID_ARGUMENT;
   *out = ResidencyInfo{};

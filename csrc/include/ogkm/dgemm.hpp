@@ -46,6 +46,9 @@ struct DGemmArgs {
   // needs (N / 2) % 64 == 0); index blockIdx.y * row_blocks + group.
   uint32_t* fix_cnt;
   DGemmReduceArgs fix;
+  // One K split, STORE / RESID epilogue (same kernels): every wave writes
+  // `fix`'s epilogue from its accumulators - no partials, no reduce launch.
+  uint32_t direct;
 };
 
 // Fragment order of an [M, K] bf16 activation (K % 32 == 0, M padded to a

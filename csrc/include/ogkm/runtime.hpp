@@ -246,6 +246,8 @@ class Runtime {
 
   // ---- introspection
   Status residency_info(Range* r, uint64_t off, ResidencyInfo* out);
+  // Bytes of [off, off + len) resident at `loc` (page granular; one block lock at a time).
+  uint64_t resident_bytes(Range* r, Loc loc, uint64_t off = 0, uint64_t len = ~0ull);
   Status sync_all();
 
   // ---- CXL (fork capability)

@@ -431,6 +431,21 @@ __global__ void __launch_bounds__(256) k_dgemm_reduce(DGemmReduceArgs a) {
   dg_reduce_quad(a, m, n);
 }
 
+// DGemmArgs::direct (one K split, STORE / RESID): the epilogue straight from
+// the accumulators - no partial slab, no reduce. Same arithmetic as
+// k_dgemm_reduce with one split (0 + x == x: the accumulator is never -0).
+__device__ __forceinline__ void dg_store_direct(const DGemmReduceArgs& r, uint32_t m, uint32_t n, f32x4_t v) {
+  uint16_t o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float y = v[e];
+    if (r.epi == DGEMM_EPI_RESID) y = bf16_to_f32(f32_to_bf16_rne(y)) + bf16_to_f32(r.resid[(uint64_t)m * r.ldr + n + e]);
+    o[e] = f32_to_bf16_rne(y);
+  }
+  uint16_t* dst = r.out_frag ? r.out + frag_index(m, r.out_col0 + n, r.out_cols) : r.out + (uint64_t)m * r.ldo + n;
+  *reinterpret_cast<u32x2_t*>(dst) = u32x2_t{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
+}
+
 // In-kernel split-K fixup (DGemmArgs::fix_cnt), called by every wave of
 // k_dgemm_pipe / k_dgemm_lring after its partial stores (the counter form of
 // cdna_hip_programming.md's in-launch split-K reduction): the agent-scope
@@ -697,7 +712,11 @@ __global__ void __launch_bounds__(256, 2) k_dgemm_pipe(DGemmArgs a) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const uint32_t m = m_base + mt * 16 + (lane & 15u);
-      if (m < a.M) *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[r][mt];
+      if (m >= a.M) continue;
+      if (a.direct)
+        dg_store_direct(a.fix, m, n, acc[r][mt]);
+      else
+        *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[r][mt];
     }
   }
   if (a.fix_cnt) dg_fixup(a, rb, lane);
@@ -811,7 +830,11 @@ __global__ void __launch_bounds__(64) k_dgemm_lring(DGemmArgs a) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const uint32_t m = m_base + mt * 16 + (lane & 15u);
-      if (m < a.M) *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[r][mt];
+      if (m >= a.M) continue;
+      if (a.direct)
+        dg_store_direct(a.fix, m, n, acc[r][mt]);
+      else
+        *reinterpret_cast<f32x4_t*>(a.part + ((uint64_t)ks * a.M + m) * a.N + n) = acc[r][mt];
     }
   }
   if (a.fix_cnt) dg_fixup(a, rb, lane);
@@ -820,7 +843,8 @@ __global__ void __launch_bounds__(64) k_dgemm_lring(DGemmArgs a) {
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s) {
   if (a.N % 16 || a.K % 32 || a.klen % 32 || !a.ksplit || a.row_blocks != (a.N / 16 + kRowTiles - 1) / kRowTiles)
     return hipErrorInvalidValue;
-  if (a.fix_cnt && !dgemm_fixup_ok(a, mode)) return hipErrorInvalidValue;
+  if ((a.fix_cnt || a.direct) && !dgemm_fixup_ok(a, mode)) return hipErrorInvalidValue;
+  if (a.direct && (a.fix_cnt || a.ksplit != 1 || a.fix.epi == DGEMM_EPI_SILU_MUL)) return hipErrorInvalidValue;
   const uint32_t units = a.row_blocks * a.ksplit;
   if (mode == DGEMM_W_RAW && a.lds_x) {
     dim3 grid(units, (a.M + kMTiles * 16 - 1) / (kMTiles * 16));

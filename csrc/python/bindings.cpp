@@ -261,6 +261,11 @@ PYBIND11_MODULE(_ogkm, m) {
     check(s, "prefetch");
     return t;
   }, py::arg("id"), py::arg("off"), py::arg("len"), py::arg("tier"), py::arg("loc"), py::arg("floor") = 0);
+  m.def("resident_bytes", [](uint64_t id, int tier, int loc, uint64_t off, uint64_t len) {
+    Range* r = range(id);
+    py::gil_scoped_release nogil;
+    return rt()->resident_bytes(r, make_loc(tier, loc), off, len);
+  }, py::arg("id"), py::arg("tier"), py::arg("loc"), py::arg("off") = 0, py::arg("len") = ~0ull);
   m.def("hint_next_use", [](uint64_t id, uint64_t when) { rt()->hint_next_use(range(id), when); });
   m.def("set_op_clock", [](int dev, uint64_t now) { rt()->set_op_clock(dev, now); });
   m.def("migrate", [](uint64_t id, uint64_t off, uint64_t len, int tier, int loc) {
@@ -833,7 +838,7 @@ PYBIND11_MODULE(_ogkm, m) {
   }, py::arg("reset") = false);
   // Decode GEMM + fused epilogue in one call: out = epi(X . W^T) (ops/dgemm.py).
   // (ksplit, klen) exactly as lib.dgemm plans it (lds: the LDS kernel's 4 waves per K split).
-  m.def("dgemm_fixups", [] { return g_dgemm_fixups.load(); });  // GEMMs whose split-K sum ran in-kernel
+  m.def("dgemm_fixups", [] { return g_dgemm_fixups.load(); });  // GEMMs whose epilogue ran in the GEMM kernel
   m.def("dgemm_plan", [](uint32_t N, uint32_t K, uint32_t target_units, bool lds) {
     uint32_t ks, kl;
     dgemm_plan(N, K, lds ? std::max<uint32_t>(1, target_units / 4) : target_units, &ks, &kl);
@@ -843,7 +848,7 @@ PYBIND11_MODULE(_ogkm, m) {
                     uint64_t x, uint32_t ldx, uint32_t M, uint32_t N, uint32_t K, uint64_t part, uint64_t part_bytes,
                     uint32_t epi, uint64_t resid, uint32_t ldr, uint64_t out, uint32_t ldo, uint32_t target_units, uint32_t unroll,
                     int lds_x, uint32_t wg_waves, uint32_t depth, bool reduce, bool x_frag, bool out_frag,
-                    uint32_t out_cols, uint32_t out_col0, uint64_t fix_cnt, uint64_t fix_cnt_len) {
+                    uint32_t out_cols, uint32_t out_col0, uint64_t fix_cnt, uint64_t fix_cnt_len, bool direct) {
     if (N % 16 || K % 32 || ldx % 8 || !M) throw StatusError("dgemm: N % 16, K % 32, ldx % 8 and M > 0 required");
     if (epi == DGEMM_EPI_SILU_MUL && (N % 32)) throw StatusError("dgemm: SILU_MUL needs N % 32 == 0");
     DGemmArgs a{};
@@ -876,14 +881,17 @@ PYBIND11_MODULE(_ogkm, m) {
     r.out_frag = out_frag ? 1 : 0;
     r.out_cols = out_cols;
     r.out_col0 = out_col0;
-    if (reduce && fix_cnt) {  // in-kernel fixup where the kernel supports it (else the reduce launch below)
+    if (reduce && (fix_cnt || direct)) {  // epilogue in the GEMM kernel where it can run there
       a.fix = r;
       const uint64_t need = (uint64_t)((M + 63) / 64) * a.row_blocks;
-      if (dgemm_fixup_ok(a, mode) && need <= fix_cnt_len) a.fix_cnt = (uint32_t*)fix_cnt;
+      if (direct && a.ksplit == 1 && epi != DGEMM_EPI_SILU_MUL && dgemm_fixup_ok(a, mode))
+        a.direct = 1;
+      else if (fix_cnt && dgemm_fixup_ok(a, mode) && need <= fix_cnt_len)
+        a.fix_cnt = (uint32_t*)fix_cnt;
     }
     check(rt()->be()->dgemm(dev, a, mode, (void*)stream), "dgemm");
-    g_dgemm_fixups += a.fix_cnt ? 1 : 0;
-    if (!reduce || a.fix_cnt) return a.ksplit;  // deferred: the consumer (rmsnorm / rope_kv) sums the splits
+    g_dgemm_fixups += (a.fix_cnt || a.direct) ? 1 : 0;
+    if (!reduce || a.fix_cnt || a.direct) return a.ksplit;  // deferred: the consumer (rmsnorm / rope_kv) sums the splits
     check(rt()->be()->dgemm_reduce(dev, r, (void*)stream), "dgemm_reduce");
     return a.ksplit;
   }, py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("w_off"), py::arg("mode"), py::arg("chunk_shift"),
@@ -891,7 +899,7 @@ PYBIND11_MODULE(_ogkm, m) {
      py::arg("epi"), py::arg("resid"), py::arg("ldr"), py::arg("out"), py::arg("ldo"), py::arg("target_units") = 2048, py::arg("unroll") = 0,
      py::arg("lds_x") = 0, py::arg("wg_waves") = 4, py::arg("depth") = 0, py::arg("reduce") = true,
      py::arg("x_frag") = false, py::arg("out_frag") = false, py::arg("out_cols") = 0, py::arg("out_col0") = 0,
-     py::arg("fix_cnt") = 0, py::arg("fix_cnt_len") = 0);
+     py::arg("fix_cnt") = 0, py::arg("fix_cnt_len") = 0, py::arg("direct") = false);
   // Fused decode-step ops (ops/fused.py).
   m.def("rmsnorm", [](int dev, uint64_t stream, uint64_t x, uint64_t w, uint64_t y, uint32_t rows, uint32_t dim,
                       uint32_t ldx, uint32_t ldy, float eps, uint64_t part, uint32_t ksplit, bool y_frag,

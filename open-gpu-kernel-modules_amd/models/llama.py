@@ -64,6 +64,8 @@ PLAN_HBM_GBPS = 4000.0
 # GPU-side stream dependency).
 _HOST_LEASE_WAIT = os.environ.get("OGKM_HOST_LEASE_WAIT", "0") != "0"
 _FLOOR_FALLBACK = os.environ.get("OGKM_FLOOR_FALLBACK", "stop")
+# planner off: count only the bytes a prefetch moves against the window (0: unit sizes)
+_WINDOW_MISSING = os.environ.get("OGKM_WINDOW_MISSING", "1") != "0"
 
 
 @dataclass(frozen=True)
@@ -548,6 +550,7 @@ class TieredLlama:
         self.stream_seq = [k for k in self.order if not self._is_resident(k)]
         self._pf_next = 0           # next index in stream_seq to prefetch (cyclic)
         self._inflight: list = []   # prefetched, not yet consumed
+        self._inflight_b: dict = {}  # key -> bytes its prefetch counted against the window
         # Next-use hints (planner off): a streamed unit is next used one step
         # later at the same place in the use order, so the runtime can evict
         # in next-use order (Belady, ChunkArena::set_next_use) instead of
@@ -1004,11 +1007,16 @@ class TieredLlama:
         """Keep up to ``window_bytes`` of upcoming streamed tensors in flight on the ring."""
         if not self.stream_seq:
             return
-        inflight = sum(self._buf(k).size for k in self._inflight)
+        inflight = sum(self._inflight_b.get(k, 0) for k in self._inflight)
         n = len(self.stream_seq)
         while len(self._inflight) < n:
             key = self.stream_seq[self._pf_next]
-            nb = self._buf(key).size
+            buf = self._buf(key)
+            nb = buf.size
+            if self.next_use and _WINDOW_MISSING:
+                # next-use mode keeps part of the units resident: the window
+                # is the bytes in flight on the link, not the units ahead
+                nb -= buf.resident_bytes(rt.Loc.gpu(self.dev))
             if self._inflight and inflight + nb > self.window_bytes:
                 break
             if self.next_use:
@@ -1025,6 +1033,7 @@ class TieredLlama:
             else:
                 self._buf(key).prefetch(rt.Loc.gpu(self.dev))
             self._inflight.append(key)
+            self._inflight_b[key] = nb
             inflight += nb
             self._pf_next = (self._pf_next + 1) % n
 

@@ -67,7 +67,12 @@ LRING_MAX_STEPS = int(os.environ.get("OGKM_DGEMM_LRING_MAX_STEPS", "96"))
 # Split-K fixup inside the pipelined raw kernels (the last-arriving wave of an
 # output group sums the splits and runs the epilogue) instead of a
 # k_dgemm_reduce launch; 0 = always launch the reduce.
-FIXUP = int(os.environ.get("OGKM_DGEMM_FIXUP", "1"))
+# Measured slower on config 2 (7.84 vs 6.43 ms/step, profiles/r4_config2.md):
+# every wave's agent-scope release writes its XCD's L2 back - off by default.
+FIXUP = int(os.environ.get("OGKM_DGEMM_FIXUP", "0"))
+# One K split (the LM head's row blocks outnumber the waves): the kernel
+# writes the store / resid epilogue from its accumulators - no partials.
+DIRECT = int(os.environ.get("OGKM_DGEMM_DIRECT", "1"))
 FIX_SLOTS = 1 << 16  # arrival counters per (device, stream): grid.y x row blocks
 
 
@@ -268,10 +273,12 @@ def linear(x: torch.Tensor, w: WeightRef, epi: str = "store", resid: torch.Tenso
     if epi == "resid":
         if resid is None or resid.shape != out.shape or resid.stride(1) != 1:
             raise ValueError("dgemm.linear: resid must match out")
-    fix = _fix_counters(x.device, stream) if FIXUP and unroll == 1 and not lds_ and w.mode == MODE_RAW else None
+    inkernel = unroll == 1 and not lds_ and w.mode == MODE_RAW
+    fix = _fix_counters(x.device, stream) if FIXUP and inkernel else None
     lib.dgemm(device_index, stream, w.ptr, w.off, w.mode, w.chunk_shift, x.data_ptr(), ldx, m, w.n, w.k,
               part.data_ptr(), part.numel() * 4, EPI[epi], resid.data_ptr() if resid is not None else 0,
               resid.stride(0) if resid is not None else 0, out.data_ptr(), out.stride(0), units, unroll, lds_,
               WG_WAVES, depth, True, xf, out_frag, out.shape[1] if out_frag else 0, out_col0,
-              fix.data_ptr() if fix is not None else 0, FIX_SLOTS if fix is not None else 0)
+              fix.data_ptr() if fix is not None else 0, FIX_SLOTS if fix is not None else 0,
+              bool(DIRECT and inkernel and epi != "silu_mul"))
     return out

@@ -276,6 +276,12 @@ class ManagedBuffer:
         t, i = Loc.parse(loc).code
         return lib.prefetch(self.id, offset, length, t, i, int(needed_at))
 
+    def resident_bytes(self, loc, offset: int = 0, length: Optional[int] = None) -> int:
+        """Bytes of [offset, offset + length) resident at ``loc`` (page granular)."""
+        length = self.size - offset if length is None else length
+        t, i = Loc.parse(loc).code
+        return lib.resident_bytes(self.id, t, i, offset, length)
+
     def hint_next_use(self, when: int) -> None:
         """Op-clock time of this range's next use: its HBM chunks are then evicted
         in next-use (Belady) order - see lib.set_op_clock."""

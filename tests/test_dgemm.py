@@ -215,14 +215,16 @@ def test_dgemm_gpu_bandwidth_70b_shapes(gpu_rt, packed):
 @pytest.mark.parametrize("depth", [4, 50])
 @pytest.mark.parametrize("epi", ["store", "resid", "silu_mul"])
 @pytest.mark.parametrize("n,k,m,frag", [(256, 1024, 64, False), (1024, 2048, 80, False), (336, 1024, 7, False),
-                                        (320, 1024, 7, False), (512, 4096, 64, True)])
+                                        (320, 1024, 7, False), (512, 4096, 64, True), (65536, 256, 64, False),
+                                        (65536, 256, 80, True)])
 def test_dgemm_gpu_fixup_matches_reduce_launch(gpu_rt, depth, epi, n, k, m, frag):
     """The in-kernel split-K fixup (the last-arriving wave of each output
     group sums the splits and runs the epilogue) is bit-identical to the
     k_dgemm_reduce launch it replaces, across repeated launches (the counters
     reset themselves), two M blocks (m = 80), a partial row block (n = 336)
     and fragment-ordered outputs; SiLU with (N / 2) % 64 != 0 falls back to
-    the reduce launch."""
+    the reduce launch. N = 65536 plans one K split: store / resid then take
+    the direct epilogue (from the accumulators, no partials)."""
     if epi == "silu_mul" and n % 32:
         pytest.skip("SiLU needs N % 32 == 0")
     if frag and epi == "resid":
@@ -235,8 +237,8 @@ def test_dgemm_gpu_fixup_matches_reduce_launch(gpu_rt, depth, epi, n, k, m, frag
     nout = n // 2 if epi == "silu_mul" else n
 
     def run(fix):
-        f0, d0 = dgemm.FIXUP, dgemm.DEPTH
-        dgemm.FIXUP, dgemm.DEPTH = fix, depth
+        f0, d0, x0 = dgemm.FIXUP, dgemm.DEPTH, dgemm.DIRECT
+        dgemm.FIXUP, dgemm.DEPTH, dgemm.DIRECT = fix, depth, fix
         try:
             outs = []
             for _ in range(3):
@@ -247,7 +249,7 @@ def test_dgemm_gpu_fixup_matches_reduce_launch(gpu_rt, depth, epi, n, k, m, frag
                 outs.append(o)
             return outs
         finally:
-            dgemm.FIXUP, dgemm.DEPTH = f0, d0
+            dgemm.FIXUP, dgemm.DEPTH, dgemm.DIRECT = f0, d0, x0
 
     base = run(0)
     n0 = lib.dgemm_fixups()
