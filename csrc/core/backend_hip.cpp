@@ -36,6 +36,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <unordered_map>
 #include <mutex>
 #include <string>
 
@@ -243,6 +244,23 @@ class HipBackend : public Backend {
   }
   void va_free(void* va, size_t bytes) override { (void)hipMemAddressFree(va, bytes); }
   Status vmm_map(void* va, size_t bytes, uint64_t h, int dev) override {
+    if (rocr_va(va)) {  // a prepared stable VA: ROCr maps it (HIP keeps its placeholder view)
+      hsa_amd_vmem_alloc_handle_t rh;
+      if (!rocr_handle(h, &rh)) return Status::IO_ERROR;
+      hsa_amd_memory_access_desc_t d{HSA_ACCESS_PERMISSION_RW, dma_[dev].gpu};
+      if (hsa_amd_vmem_map(va, bytes, 0, rh, 0) != HSA_STATUS_SUCCESS) {
+        last_err_ = "hsa_amd_vmem_map failed";
+        return Status::IO_ERROR;
+      }
+      if (hsa_amd_vmem_set_access(va, bytes, &d, 1) != HSA_STATUS_SUCCESS) {
+        (void)hsa_amd_vmem_unmap(va, bytes);
+        last_err_ = "hsa_amd_vmem_set_access failed";
+        return Status::IO_ERROR;
+      }
+      std::lock_guard<std::mutex> g(reg_m_);
+      vmm_maps_[(uint64_t)va] = {bytes, dev};
+      return Status::OK;
+    }
     HIPCHK(hipMemMap(va, bytes, 0, (hipMemGenericAllocationHandle_t)(uintptr_t)h, 0));
     hipMemAccessDesc ad = {};
     ad.location.type = hipMemLocationTypeDevice;
@@ -251,13 +269,141 @@ class HipBackend : public Backend {
     HIPCHK(hipMemSetAccess(va, bytes, &ad, 1));
     std::lock_guard<std::mutex> g(reg_m_);
     vmm_maps_[(uint64_t)va] = {bytes, dev};
+    handle_home_.emplace(h, (uint64_t)va);  // where ROCr can look the handle up (rocr_handle)
     return Status::OK;
   }
   Status vmm_unmap(void* va, size_t bytes) override {
-    HIPCHK(hipMemUnmap(va, bytes));
+    if (rocr_va(va)) {
+      if (hsa_amd_vmem_unmap(va, bytes) != HSA_STATUS_SUCCESS) {
+        last_err_ = "hsa_amd_vmem_unmap failed";
+        return Status::IO_ERROR;
+      }
+    } else {
+      HIPCHK(hipMemUnmap(va, bytes));
+    }
     std::lock_guard<std::mutex> g(reg_m_);
     vmm_maps_.erase((uint64_t)va);
     return Status::OK;
+  }
+  // Stable VAs remapped through ROCr. HIP's VMM layer costs 14 us per 2 MB
+  // unmap against ROCr's 2.3 (and 7.6 vs 5.3 per map + access;
+  // tools/probe_vmm_rocr_path.hip), but HIP copies (torch's hipMemcpy on a
+  // managed tensor) resolve only VAs HIP itself mapped - on a VA only ROCr
+  // maps they crash. So HIP maps every block of the reservation once, to a
+  // per-device placeholder handle, and ROCr unmaps them again: HIP's table
+  // then always holds a mapping for the VA while ROCr's holds the real chunk
+  // (or none), and copies through the VA reach whatever ROCr maps.
+  Status stable_va_prepare(void* va, size_t bytes, int dev) override {
+    if (!config().vmm_rocr_remap) return Status::OK;
+    dma_init();
+    if (dev < 0 || dev >= (int)dma_.size() || !dma_[dev].gpu.handle) return Status::OK;  // HIP path
+    uint64_t ph = 0;
+    {
+      std::lock_guard<std::mutex> g(reg_m_);
+      ph = placeholder_[dev];
+    }
+    if (!ph) {
+      hipMemAllocationProp prop = {};
+      prop.type = hipMemAllocationTypePinned;
+      prop.location.type = hipMemLocationTypeDevice;
+      prop.location.id = dev;
+      hipMemGenericAllocationHandle_t hh;
+      HIPCHK(hipMemCreate(&hh, kBlockSize, &prop, 0));
+      std::lock_guard<std::mutex> g(reg_m_);
+      if (!placeholder_[dev]) {
+        placeholder_[dev] = (uint64_t)(uintptr_t)hh;
+      } else {
+        (void)hipMemRelease(hh);
+      }
+      ph = placeholder_[dev];
+    }
+    const size_t n = bytes / kBlockSize;
+    size_t i = 0;
+    for (; i < n; ++i)
+      if (hipMemMap((char*)va + i * kBlockSize, kBlockSize, 0, (hipMemGenericAllocationHandle_t)(uintptr_t)ph, 0) !=
+          hipSuccess)
+        break;
+    hipMemAccessDesc ad = {};
+    ad.location.type = hipMemLocationTypeDevice;
+    ad.location.id = dev;
+    ad.flags = hipMemAccessFlagsProtReadWrite;
+    if (i < n || hipMemSetAccess(va, bytes, &ad, 1) != hipSuccess) {
+      (void)hipGetLastError();
+      for (size_t k = 0; k < i; ++k) (void)hipMemUnmap((char*)va + k * kBlockSize, kBlockSize);
+      last_err_ = "placeholder mapping of a stable VA failed";
+      return Status::IO_ERROR;
+    }
+    {
+      std::lock_guard<std::mutex> g(reg_m_);
+      if (!placeholder_rh_[dev].handle &&
+          hsa_amd_vmem_retain_alloc_handle(&placeholder_rh_[dev], va) != HSA_STATUS_SUCCESS)
+        placeholder_rh_[dev].handle = 0;
+    }
+    bool ok = placeholder_rh_[dev].handle != 0;
+    size_t u = 0;
+    for (; ok && u < n; ++u) ok = hsa_amd_vmem_unmap((char*)va + u * kBlockSize, kBlockSize) == HSA_STATUS_SUCCESS;
+    if (!ok) {  // back to HIP's own mappings, then undo them
+      hsa_amd_memory_access_desc_t d{HSA_ACCESS_PERMISSION_RW, dma_[dev].gpu};
+      for (size_t k = 0; k < u && placeholder_rh_[dev].handle; ++k) {
+        (void)hsa_amd_vmem_map((char*)va + k * kBlockSize, kBlockSize, 0, placeholder_rh_[dev], 0);
+        (void)hsa_amd_vmem_set_access((char*)va + k * kBlockSize, kBlockSize, &d, 1);
+      }
+      for (size_t k = 0; k < n; ++k) (void)hipMemUnmap((char*)va + k * kBlockSize, kBlockSize);
+      last_err_ = "ROCr unmap of a placeholder mapping failed";
+      return Status::IO_ERROR;
+    }
+    std::lock_guard<std::mutex> g(reg_m_);
+    rocr_vas_[(uint64_t)va] = {bytes, dev};
+    return Status::OK;
+  }
+  void stable_va_release(void* va, size_t bytes) override {
+    int dev = -1;
+    {
+      std::lock_guard<std::mutex> g(reg_m_);
+      auto it = rocr_vas_.find((uint64_t)va);
+      if (it == rocr_vas_.end()) return;
+      dev = it->second.second;
+      rocr_vas_.erase(it);
+    }
+    // Restore HIP's view block by block (the placeholder), then let HIP unmap it.
+    for (size_t k = 0; k < bytes / kBlockSize; ++k) {
+      char* b = (char*)va + k * kBlockSize;
+      bool mapped;
+      {
+        std::lock_guard<std::mutex> g(reg_m_);
+        mapped = vmm_maps_.erase((uint64_t)b) != 0;
+      }
+      if (mapped) (void)hsa_amd_vmem_unmap(b, kBlockSize);
+      (void)hsa_amd_vmem_map(b, kBlockSize, 0, placeholder_rh_[dev], 0);
+      (void)hipMemUnmap(b, kBlockSize);
+    }
+    (void)hipGetLastError();
+  }
+  bool rocr_va(void* p) {
+    const uint64_t a = (uint64_t)p;
+    std::lock_guard<std::mutex> g(reg_m_);
+    auto it = rocr_vas_.upper_bound(a);
+    if (it == rocr_vas_.begin()) return false;
+    --it;
+    return a < it->first + it->second.first;
+  }
+  // ROCr's handle for a HIP VMM handle (looked up at an address where HIP mapped it; cached).
+  bool rocr_handle(uint64_t h, hsa_amd_vmem_alloc_handle_t* out) {
+    std::lock_guard<std::mutex> g(reg_m_);
+    auto it = rocr_h_.find(h);
+    if (it != rocr_h_.end()) {
+      *out = it->second;
+      return true;
+    }
+    auto home = handle_home_.find(h);
+    hsa_amd_vmem_alloc_handle_t rh;
+    if (home == handle_home_.end() || hsa_amd_vmem_retain_alloc_handle(&rh, (void*)home->second) != HSA_STATUS_SUCCESS) {
+      last_err_ = "no ROCr handle for a VMM chunk (not mapped at its arena view)";
+      return false;
+    }
+    rocr_h_[h] = rh;
+    *out = rh;
+    return true;
   }
   // Heavyweight translation flush provoked from user space: mapping a 4 KB SVM
   // page on the GPU and revoking it again runs the KFD SVM unmap path, which
@@ -930,6 +1076,11 @@ class HipBackend : public Backend {
   std::mutex ev_m_, df_m_, reg_m_;
   std::map<uint64_t, uint64_t> regs_;  // host registrations: base -> bytes
   std::map<uint64_t, std::pair<uint64_t, int>> vmm_maps_;  // VMM mappings: va -> (bytes, device)
+  std::map<uint64_t, std::pair<uint64_t, int>> rocr_vas_;  // stable VAs remapped through ROCr: base -> (bytes, device)
+  std::unordered_map<uint64_t, uint64_t> handle_home_;     // HIP VMM handle -> a VA HIP mapped it at
+  std::unordered_map<uint64_t, hsa_amd_vmem_alloc_handle_t> rocr_h_;  // HIP VMM handle -> retained ROCr handle
+  uint64_t placeholder_[kMaxGpus] = {};                    // per device: HIP's placeholder handle for stable VAs
+  hsa_amd_vmem_alloc_handle_t placeholder_rh_[kMaxGpus] = {};
   std::mutex flush_m_;
   void* flush_page_ = nullptr;  // the SVM page toggled by tlb_flush (never freed: process lifetime)
   std::vector<void*> free_events_[64];

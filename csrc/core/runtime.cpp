@@ -174,6 +174,10 @@ Status Runtime::vmm_self_test(int d) {
     fail("no free chunks");
   } else if ((st = be_->va_reserve(kBlockSize, &va)) != Status::OK) {
     fail("va_reserve");
+  } else if ((st = be_->stable_va_prepare(va, kBlockSize, d)) != Status::OK) {  // the ranges' remap path
+    fail("stable_va_prepare");
+    be_->va_free(va, kBlockSize);
+    va = nullptr;
   } else if ((st = be_->host_alloc_coherent(4096, (void**)&out)) != Status::OK) {
     fail("host_alloc_coherent");
   } else if (!(stream = be_->stream_create(d, 0))) {
@@ -225,7 +229,10 @@ Status Runtime::vmm_self_test(int d) {
   (void)be_->tlb_flush(d);
   if (stream) be_->stream_destroy(stream);
   if (out) be_->host_free_coherent(out);
-  if (va) be_->va_free(va, kBlockSize);
+  if (va) {
+    be_->stable_va_release(va, kBlockSize);
+    be_->va_free(va, kBlockSize);
+  }
   for (int i = 0; i < nch; ++i) ha->free(ch[i], 1);
   if (!T.ok)
     RT_ERR("gpu %d: stable-VA translation self-test FAILED (%s): stable-VA managed ranges (the transparent "
@@ -293,6 +300,10 @@ Status Runtime::malloc_managed(uint64_t size, uint32_t flags, const std::string&
     void* va = nullptr;
     Status st = be_->va_reserve(r->cpu_view_bytes, &va);
     if (st != Status::OK) return st;
+    if ((st = be_->stable_va_prepare(va, r->cpu_view_bytes, stable_dev)) != Status::OK) {
+      be_->va_free(va, r->cpu_view_bytes);
+      return st;
+    }
     r->dev_va = va;
     r->stable_dev = stable_dev;
     vs_.dev_tree[(uint64_t)va] = r.get();
@@ -325,6 +336,10 @@ Status Runtime::malloc_managed_at(uint64_t size, uint32_t flags, const std::stri
     void* va = nullptr;
     Status st = be_->va_reserve(r->cpu_view_bytes, &va, (void*)dev_va);
     if (st != Status::OK) return st;
+    if ((st = be_->stable_va_prepare(va, r->cpu_view_bytes, stable_dev)) != Status::OK) {
+      be_->va_free(va, r->cpu_view_bytes);
+      return st;
+    }
     r->dev_va = va;
     r->stable_dev = stable_dev;
     vs_.dev_tree[(uint64_t)va] = r.get();
@@ -393,6 +408,7 @@ Status Runtime::free_range(Range* r) {
   }
   if (r->dev_va) {
     vs_.dev_tree.erase((uint64_t)r->dev_va);
+    be_->stable_va_release(r->dev_va, r->cpu_view_bytes);
     be_->va_free(r->dev_va, r->cpu_view_bytes);
   }
   if (r->ext_owned && r->ext_ptr) be_->hbm_free(r->ext_dev, (void*)r->ext_ptr, align_up(r->size, kBlockSize));
