@@ -321,6 +321,7 @@ def run_torch_managed(a) -> None:
                 "vmm_remaps": s["vmm_remaps"], "tlb_flushes": s["tlb_flushes"], "ops": mode.ops,
                 "host_ms_per_step": {k: round(s[k + "_ns"] / 1e6 / a.steps, 1)
                                      for k in ("place_stable", "vmm_map", "vmm_unmap", "tlb_flush")},
+                "ring_per_step": _ring_per_step(s, a.steps),
                 "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches, "init_s": round(init_s, 1),
                 "trace_len": len(mode._trace), "hinted_ops": mode.hinted_ops, "trace_misses": mode.trace_misses,
                 "allocs_per_step": (al1["allocs"] - al0["allocs"]) // max(1, a.steps), "alloc_peak_gb":
@@ -328,6 +329,14 @@ def run_torch_managed(a) -> None:
                 "lookahead_mb": la},
     }
     print(json.dumps(out), flush=True)
+
+
+def _ring_per_step(s: dict, steps: int) -> dict:
+    """DMA ring workers (all rings summed): ms per step waiting for copy
+    dependencies, in engine copies, idle; engine copy calls per step."""
+    out = {k: round(s.get(f"ring_{k}_ns", 0) / 1e6 / max(1, steps), 1) for k in ("fence_wait", "copy", "idle")}
+    out["copy_calls"] = s.get("ring_copy_calls", 0) // max(1, steps)
+    return out
 
 
 PROBE_KEYS = ("host_to_hbm", "hbm_to_host", "cxl_to_hbm", "hbm_to_cxl")
@@ -609,6 +618,7 @@ def main() -> None:
                     "predicted_ms": round(traffic["predicted_ms"], 2)},
                 "cxl_to_hbm_gbps_per_gpu": round(s["bytes_xfer_ctd"] / max(dt, 1e-9) / 1e9, 2),
                 "evictions": s["evictions"],
+                "ring_per_step": _ring_per_step(s, a.steps),
                 "init_s": round(init_s, 1),
             },
         }

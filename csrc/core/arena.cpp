@@ -286,6 +286,12 @@ void ChunkArena::set_op_clock(uint64_t now) {
 // next. Hints in the past (the trace moved on without a use) count as unknown.
 uint64_t ChunkArena::victim_key_locked(const ChunkInfo& c) const {
   if (c.next_use == kDeadUse) return kDeadUse;
+  // Just used: its readers may still be queued, so a copy into the chunk would
+  // wait for them (the reuse fence) and the link would idle behind compute -
+  // keep it for arena_reuse_cooldown op-clock steps (it is next needed a whole
+  // pass later: evicting the data used a few steps earlier costs the same).
+  const int64_t cool = config().arena_reuse_cooldown;
+  if (cool > 0 && c.last_op && op_clock_ >= c.last_op && op_clock_ - c.last_op < (uint64_t)cool) return 1;
   if (c.next_use >= op_clock_) return c.next_use - op_clock_;  // due now: 0, the last to go
   if (op_clock_ - c.last_op <= 2) return 1;
   return (1ull << 62) + (clock_ - std::min(clock_, c.last_use));
@@ -298,22 +304,51 @@ bool ChunkArena::floor_protects_locked(const ChunkInfo& c, uint64_t floor) const
   return k < (1ull << 62) && k + op_clock_ <= floor;
 }
 
+void ChunkArena::next_victims_locked(uint32_t want, uint64_t floor, std::vector<std::pair<uint64_t, uint32_t>>* out) {
+  out->clear();
+  if (!want) return;
+  const int64_t every = config().arena_victim_cache_ops;
+  for (int pass = 0; pass < 2 && out->size() < want; ++pass) {
+    const bool stale = !vcache_valid_ || vcache_pos_ >= vcache_.size() || every <= 0 ||
+                       op_clock_ < vcache_clock_ || op_clock_ - vcache_clock_ > (uint64_t)every;
+    if (pass == 1 || stale) {  // full scan: every evictable chunk, best first
+      vcache_.clear();
+      for (uint32_t i = 0; i < nchunks_; ++i) {
+        const ChunkInfo& c = chunks_[i];
+        if (c.state != ChunkState::ALLOCATED || c.pin_count != 0) continue;
+        vcache_.emplace_back(victim_key_locked(c), i);
+      }
+      std::sort(vcache_.begin(), vcache_.end(),
+                [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
+                  return a.first > b.first || (a.first == b.first && a.second < b.second);
+                });
+      vcache_pos_ = 0;
+      vcache_clock_ = op_clock_;
+      vcache_valid_ = true;
+      out->clear();
+    }
+    const uint64_t shift = op_clock_ - vcache_clock_;  // every hinted key fell by this much since the build
+    bool front = true;
+    for (size_t k = vcache_pos_; k < vcache_.size() && out->size() < want; ++k) {
+      const ChunkInfo& c = chunks_[vcache_[k].second];
+      const uint64_t key = victim_key_locked(c);
+      const bool gone = c.state != ChunkState::ALLOCATED || c.pin_count != 0 ||
+                        (key < (1ull << 62) && key + shift < vcache_[k].first && vcache_[k].first < (1ull << 62));
+      if (gone) {
+        if (front) vcache_pos_ = k + 1;  // never a candidate again before the next build
+        continue;
+      }
+      front = false;
+      if (floor_protects_locked(c, floor)) continue;
+      out->emplace_back(key, vcache_[k].second);
+    }
+  }
+}
+
 void ChunkArena::pick_victims_by_next_use_locked(uint32_t n, std::vector<uint32_t>* out) {
   const uint64_t floor = VictimFloor::value();
   std::vector<std::pair<uint64_t, uint32_t>> cand;
-  for (uint32_t i = 0; i < nchunks_; ++i) {
-    const ChunkInfo& c = chunks_[i];
-    if (c.state != ChunkState::ALLOCATED || c.pin_count != 0) continue;
-    if (floor_protects_locked(c, floor)) continue;
-    cand.emplace_back(victim_key_locked(c), i);
-  }
-  if (cand.size() > n) {
-    std::nth_element(cand.begin(), cand.begin() + n, cand.end(),
-                     [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
-                       return a.first > b.first;
-                     });
-    cand.resize(n);
-  }
+  next_victims_locked(n, floor, &cand);
   static const bool dbg = getenv("OGKM_DEBUG_VICTIMS") != nullptr;
   for (auto& c : cand) {
     if (dbg) {
@@ -382,17 +417,10 @@ Status ChunkArena::reserve_for(const std::vector<int64_t>& want, std::vector<uin
   std::vector<std::pair<uint64_t, uint32_t>> cand;
   if (evict) {
     const uint64_t floor = VictimFloor::value();
-    for (uint32_t i = 0; i < nchunks_; ++i) {
-      const ChunkInfo& c = chunks_[i];
-      if (c.state != ChunkState::ALLOCATED || c.pin_count != 0 || floor_protects_locked(c, floor)) continue;
-      cand.emplace_back(victim_key_locked(c), i);
-    }
+    next_victims_locked(evict + n, floor, &cand);
     if (cand.size() < evict) return undo();
-    auto by_key = [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
-      return a.first > b.first || (a.first == b.first && a.second < b.second);
-    };
-    std::partial_sort(cand.begin(), cand.begin() + std::min<size_t>(cand.size(), evict + n), cand.end(), by_key);
-    const uint64_t kthr = cand[evict - 1].first;  // Belady's worst pick for `evict` victims
+    uint64_t kthr = ~0ull;  // Belady's worst pick for `evict` victims
+    for (uint32_t k = 0; k < evict; ++k) kthr = std::min(kthr, cand[k].first);
     // 2. home chunks that are as good a victim as Belady's own picks
     uint32_t used = 0;
     for (uint32_t i = 0; i < n && used < evict; ++i) {

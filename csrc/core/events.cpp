@@ -146,7 +146,11 @@ const char* counter_name(Counter c) {
                             "vmm_map_ns",
                             "vmm_unmap_ns",
                             "tlb_flush_ns",
-                            "place_stable_ns"};
+                            "place_stable_ns",
+                            "ring_fence_wait_ns",
+                            "ring_copy_ns",
+                            "ring_idle_ns",
+                            "ring_copy_calls"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -148,7 +148,11 @@ void Ring::worker() {
     Batch b;
     {
       std::unique_lock<std::mutex> g(wm_);
-      wcv_.wait(g, [&] { return stop_ || !work_.empty(); });
+      if (work_.empty() && !stop_) {
+        const uint64_t t_idle = now_ns();
+        wcv_.wait(g, [&] { return stop_ || !work_.empty(); });
+        Tools::get().inc(Counter::RingIdleNs, now_ns() - t_idle);
+      }
       if (work_.empty()) return;  // stop_ with nothing left
       b = std::move(work_.front());
       work_.pop_front();
@@ -238,7 +242,12 @@ Status Ring::run_batch(Batch& b) {
         }
         copies.swap(split);
       }
-      if (st == Status::OK) st = be_->dma_copy(dev_, copies.data(), copies.size(), (int)kind_);
+      if (st == Status::OK) {
+        const uint64_t t_copy = now_ns();
+        st = be_->dma_copy(dev_, copies.data(), copies.size(), (int)kind_);
+        Tools::get().inc(Counter::RingCopyNs, now_ns() - t_copy);
+        Tools::get().inc(Counter::RingCopyCalls, copies.size());
+      }
     }
     copies.clear();
     copy_dst.clear();
@@ -265,7 +274,11 @@ Status Ring::run_batch(Batch& b) {
         // host, before the engine / stream is handed anything after the wait.
         flush_decodes();
         flush_copies();
-        if (st == Status::OK && s.wait && !s.wait->done.load(std::memory_order_acquire)) st = s.wait->wait();
+        if (st == Status::OK && s.wait && !s.wait->done.load(std::memory_order_acquire)) {
+          const uint64_t t_wait = now_ns();
+          st = s.wait->wait();
+          Tools::get().inc(Counter::RingFenceWaitNs, now_ns() - t_wait);
+        }
         break;
       case SqeOp::NOP:
         break;

@@ -180,8 +180,18 @@ class ChunkArena {
   bool floor_protects_locked(const ChunkInfo& c, uint64_t floor) const;
   // next-use mode: up to n evictable chunks with the largest keys above the floor
   void pick_victims_by_next_use_locked(uint32_t n, std::vector<uint32_t>* out);
+  // The next `want` victims in next-use order, (current key, chunk), from a
+  // ranked candidate list rebuilt by a full scan only when it runs dry or the
+  // op clock moved arena_victim_cache_ops past its build (a full scan per
+  // fault was ~1 s per 70B step over 40k chunks). Entries that left ALLOCATED,
+  // got pinned or fell in rank (re-used for data needed sooner) are skipped.
+  void next_victims_locked(uint32_t want, uint64_t floor, std::vector<std::pair<uint64_t, uint32_t>>* out);
   bool hinted_ = false;
   uint64_t op_clock_ = 0;
+  std::vector<std::pair<uint64_t, uint32_t>> vcache_;  // (key at build, chunk), best first
+  size_t vcache_pos_ = 0;
+  uint64_t vcache_clock_ = 0;
+  bool vcache_valid_ = false;
   void lru_remove(uint32_t i);
   void lru_push_tail(uint32_t i, uint8_t list);
   void take_run(uint32_t first, uint32_t n);  // remove [first,first+n) from free runs

@@ -64,8 +64,10 @@ PLAN_HBM_GBPS = 4000.0
 # GPU-side stream dependency).
 _HOST_LEASE_WAIT = os.environ.get("OGKM_HOST_LEASE_WAIT", "0") != "0"
 _FLOOR_FALLBACK = os.environ.get("OGKM_FLOOR_FALLBACK", "stop")
-# planner off: count only the bytes a prefetch moves against the window (0: unit sizes)
-_WINDOW_MISSING = os.environ.get("OGKM_WINDOW_MISSING", "1") != "0"
+# planner off: count only the bytes a prefetch moves against the window (1; default
+# 0: unit sizes - measured the same on the 70B, 103.4 vs 102.7 tok/s, and a
+# larger in-flight share of a small arena streams more)
+_WINDOW_MISSING = os.environ.get("OGKM_WINDOW_MISSING", "0") != "0"
 
 
 @dataclass(frozen=True)
