@@ -582,15 +582,32 @@ class HipBackend : public Backend {
   }
 
   Status dma_copy(int dev, const CopyDesc* d, size_t n, int channel) override {
+    Status st = dma_issue(dev, d, n, channel, 0);
+    if (st != Status::OK) return st;
+    return dma_complete(0);
+  }
+  // Per worker thread: two completion signals (a batch in flight while the
+  // next one is issued), each decremented by every copy of its batch.
+  static hsa_signal_t* dma_sigs() {
+    thread_local hsa_signal_t sig[2] = {{0}, {0}};
+    return sig;
+  }
+  Status dma_complete(int slot) override {
+    hsa_signal_t sig = dma_sigs()[slot & 1];
+    if (sig.handle) dma_wait(sig);
+    return Status::OK;
+  }
+  Status dma_issue(int dev, const CopyDesc* d, size_t n, int channel, int slot) override {
     if (!dma_supported(dev)) return Status::NOT_SUPPORTED;
     if (n == 0) return Status::OK;
     DmaDev& dd = dma_[dev];
-    // One completion signal per worker thread, decremented by every copy of the batch.
-    thread_local hsa_signal_t sig{0};
-    if (!sig.handle && hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) {
+    hsa_signal_t& sig = dma_sigs()[slot & 1];
+    if (!sig.handle && hsa_signal_create(0, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) {
+      sig.handle = 0;
       last_err_ = "hsa_signal_create failed";
       return Status::NO_MEMORY;
     }
+    dma_wait(sig);  // the slot's previous batch (normally completed already)
     struct Piece { void* dst; hsa_agent_t da; const void* src; hsa_agent_t sa; size_t len; uint32_t engine; };
     std::vector<Piece> pieces;
     pieces.reserve(n);
@@ -637,7 +654,6 @@ class HipBackend : public Backend {
         return Status::IO_ERROR;
       }
     }
-    dma_wait(sig);
     dma_launches_ += pieces.size();
     return Status::OK;
   }

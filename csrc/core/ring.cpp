@@ -142,12 +142,59 @@ FenceRef Ring::submit_dma_locked() {
   return f;
 }
 
-// DMA ring worker: batches complete in submission order.
+// A batch of copies only (the common streaming case): its engine copies,
+// adjacent ones merged as run_batch does. False when it holds anything else
+// (fence waits, kernels) or the ring splits peer copies over engines.
+bool Ring::pure_copies(const Batch& b, std::vector<CopyDesc>* out) const {
+  if (kind_ == RingKind::GPU_TO_GPU) return false;
+  out->clear();
+  for (const auto& s : b.ops) {
+    if (s.op == SqeOp::NOP) continue;
+    if (s.op != SqeOp::COPY) return false;
+    if (!out->empty() && out->back().dst + out->back().bytes == s.dst && out->back().src + out->back().bytes == s.src)
+      out->back().bytes += s.bytes;
+    else
+      out->push_back(CopyDesc{s.dst, s.src, s.bytes});
+  }
+  return true;
+}
+
+// DMA ring worker: batches complete in submission order. A batch of plain
+// copies is issued on one of two completion slots and the worker moves on:
+// the next batch goes to the engines while this one is still copying, so
+// small batches (a stable-VA fault's blocks, a planner-off unit) no longer
+// leave the link idle for the worker's complete -> publish -> issue turn
+// (ring_pipeline; the tracking value is still published in order, after the
+// batch's copies completed).
 void Ring::worker() {
+  int pend = -1;  // slot of the issued, not yet completed batch
+  uint64_t pend_last = 0;
+  auto fail = [&](Status st, uint64_t last) {
+    if (st != Status::OK && err_ == Status::OK) {
+      err_ = st;
+      RT_ERR("ring %s/%d batch up to seq %llu failed: %s (%s)", ring_kind_str(kind_), dev_,
+             (unsigned long long)last, status_str(st), be_->last_error().c_str());
+      if (st != Status::INJECTED_ERROR) set_fatal(st, "DMA ring batch failed");
+    }
+  };
+  auto complete_pending = [&] {
+    if (pend < 0) return;
+    const uint64_t t0 = now_ns();
+    fail(be_->dma_complete(pend), pend_last);
+    Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
+    publish(pend_last);
+    pend = -1;
+  };
+  std::vector<CopyDesc> copies;
   for (;;) {
     Batch b;
     {
       std::unique_lock<std::mutex> g(wm_);
+      if (work_.empty() && pend >= 0) {  // nothing to overlap with: finish the batch in flight
+        g.unlock();
+        complete_pending();
+        g.lock();
+      }
       if (work_.empty() && !stop_) {
         const uint64_t t_idle = now_ns();
         wcv_.wait(g, [&] { return stop_ || !work_.empty(); });
@@ -157,13 +204,26 @@ void Ring::worker() {
       b = std::move(work_.front());
       work_.pop_front();
     }
-    Status st = err_ == Status::OK ? run_batch(b) : err_.load();
-    if (st != Status::OK && err_ == Status::OK) {
-      err_ = st;
-      RT_ERR("ring %s/%d batch up to seq %llu failed: %s (%s)", ring_kind_str(kind_), dev_,
-             (unsigned long long)b.last, status_str(st), be_->last_error().c_str());
-      if (st != Status::INJECTED_ERROR) set_fatal(st, "DMA ring batch failed");
+    if (err_ == Status::OK && config().ring_pipeline && pure_copies(b, &copies)) {
+      const int slot = pend == 0 ? 1 : 0;
+      const uint64_t t0 = now_ns();
+      Status st = copies.empty() ? Status::OK : be_->dma_issue(dev_, copies.data(), copies.size(), (int)kind_, slot);
+      Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
+      Tools::get().inc(Counter::RingCopyCalls, copies.size());
+      complete_pending();  // the batch before (its copies are ahead of these on the engines)
+      if (st != Status::OK) {
+        fail(st, b.last);
+        (void)be_->dma_complete(slot);
+        publish(b.last);
+        continue;
+      }
+      pend = slot;
+      pend_last = b.last;
+      continue;
     }
+    complete_pending();
+    Status st = err_ == Status::OK ? run_batch(b) : err_.load();
+    fail(st, b.last);
     // Publish even on error (robust channel): waiters then see err_.
     publish(b.last);
   }

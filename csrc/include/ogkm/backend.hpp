@@ -132,6 +132,17 @@ class Backend {
     (void)dev; (void)d; (void)n; (void)channel;
     return Status::NOT_SUPPORTED;
   }
+  // Split form of dma_copy for a pipelined ring worker: issue a batch on the
+  // calling thread's completion slot (0 / 1) and return at once; dma_complete
+  // waits for that slot. Default: synchronous (dma_copy, nothing to wait for).
+  virtual Status dma_issue(int dev, const CopyDesc* d, size_t n, int channel, int slot) {
+    (void)slot;
+    return dma_copy(dev, d, n, channel);
+  }
+  virtual Status dma_complete(int slot) {
+    (void)slot;
+    return Status::OK;
+  }
   // SDMA engines of `src_dev` able to copy src_dev -> dst_dev (-1 = host
   // memory): the bitmask of hsa_amd_memory_copy_engine_status(dst, src) - per
   // GPU pair for xGMI peers (uvm_gpu.c:2332-2388 reads peer caps per pair).

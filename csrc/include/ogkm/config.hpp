@@ -57,6 +57,7 @@ namespace ogkm {
   X(stable_batch_blocks, 32, "stable-VA placement: 2 MB blocks per eviction / fill / remap group (pipelined)") \
   X(arena_reuse_cooldown, 0, "next-use eviction: data used within this many op-clock steps is kept (its readers may still be queued)") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
+  X(ring_pipeline, 1, "DMA ring workers issue the next batch of plain copies before the previous one completed (two completion slots)") \
   X(vmm_rocr_remap, 1, "stable-VA remaps through ROCr hsa_amd_vmem_* (HIP keeps a placeholder mapping of the VA); 0 = hipMemMap / hipMemUnmap") \
   X(torch_persistent_ops, 128, "transparent mode: a managed tensor held again this many ops after its first hold is long-lived (keys the op-trace prefetcher)") \
   X(evict_clean_first, 0, "HBM LRU: GPU-preferred data with a valid copy elsewhere (clean) is evicted before data only in HBM (dirty: a copy-out plus a refill). Off: on the stock-torch managed 8B it protected every activation and thrashed the weights (193 -> 47 tok/s)") \

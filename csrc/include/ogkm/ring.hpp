@@ -122,6 +122,7 @@ class Ring {
   FenceRef submit_locked();
   FenceRef submit_dma_locked();
   void worker();
+  bool pure_copies(const Batch& b, std::vector<CopyDesc>* out) const;
   Status run_batch(Batch& b);
   void publish(uint64_t seq);
   Backend* be_;
