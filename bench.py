@@ -511,6 +511,7 @@ def main() -> None:
         tok = model.step(tok)
     lib.reset_counters()
     comm.reset_stats()
+    model.sstats = dict.fromkeys(model.sstats, 0)
     if a.verbose:
         model.byte_trace = {}
     comm.barrier()
@@ -551,7 +552,7 @@ def main() -> None:
                                                                                                         a.model)
         metric = f"tokens/sec {name} {a.oversub:g}x oversubscribe"
         if a.planner == "off":
-            metric += " (planner off: runtime LRU residency)"
+            metric += " (planner off: runtime-decided residency, next-use eviction)"
         if sim:  # one shard of an N-GPU job on one GPU: an upper bound, not a measured N-GPU rate
             metric += f" (tp{a.simulate_tp} rank-0 shard simulated on 1 GPU, collectives skipped)"
         out = {
@@ -619,6 +620,7 @@ def main() -> None:
                 "cxl_to_hbm_gbps_per_gpu": round(s["bytes_xfer_ctd"] / max(dt, 1e-9) / 1e9, 2),
                 "evictions": s["evictions"],
                 "ring_per_step": _ring_per_step(s, a.steps),
+                "stream_stats_per_step": {k: round(v / a.steps, 1) for k, v in model.sstats.items()},
                 "init_s": round(init_s, 1),
             },
         }

@@ -553,6 +553,10 @@ class TieredLlama:
         self._pf_next = 0           # next index in stream_seq to prefetch (cyclic)
         self._inflight: list = []   # prefetched, not yet consumed
         self._inflight_b: dict = {}  # key -> bytes its prefetch counted against the window
+        # streaming diagnostics (bench.py aux "stream_stats"): prefetches issued /
+        # refused by the victim floor, uses that found their unit not prefetched,
+        # host ms in acquire and in the run-ahead bound's waits
+        self.sstats = dict.fromkeys(("prefetched", "refused", "demand", "acquire_ms", "ahead_wait_ms"), 0)
         # Next-use hints (planner off): a streamed unit is next used one step
         # later at the same place in the use order, so the runtime can evict
         # in next-use order (Belady, ChunkArena::set_next_use) instead of
@@ -1029,12 +1033,14 @@ class TieredLlama:
                 try:
                     self._buf(key).prefetch(rt.Loc.gpu(self.dev), needed_at=self._due(key))
                 except lib.RuntimeStatusError:
+                    self.sstats["refused"] += 1
                     if _FLOOR_FALLBACK != "plain":
                         break
                     self._buf(key).prefetch(rt.Loc.gpu(self.dev))
             else:
                 self._buf(key).prefetch(rt.Loc.gpu(self.dev))
             self._inflight.append(key)
+            self.sstats["prefetched"] += 1
             self._inflight_b[key] = nb
             inflight += nb
             self._pf_next = (self._pf_next + 1) % n
@@ -1058,11 +1064,14 @@ class TieredLlama:
         if not self._is_resident(key):
             if self._inflight and self._inflight[0] == key:
                 self._inflight.pop(0)
+            else:
+                self.sstats["demand"] += 1
             if self.next_use:
                 self._clock_use(key)
             self._prefetch_ahead()
         t_a = time.perf_counter()
         lease = self._buf(key).acquire(self.dev, rt.READ)
+        self.sstats["acquire_ms"] += (time.perf_counter() - t_a) * 1e3
         if self.next_use:
             self._hint_used(key)
         if acct:  # H2D bytes submitted while servicing this tensor (prefetch window + its own faults)
@@ -1110,7 +1119,9 @@ class TieredLlama:
         ev.record(torch.cuda.current_stream(self.dev))
         self._ahead.append(ev)
         while len(self._ahead) > self.max_ahead:
+            t0 = time.perf_counter()
             self._ahead.popleft().synchronize()
+            self.sstats["ahead_wait_ms"] += (time.perf_counter() - t0) * 1e3
 
     def _use_gathered(self, key):
         """shards: fault this rank's shard in (the runtime prefetches streamed
