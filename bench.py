@@ -512,6 +512,7 @@ def main() -> None:
     lib.reset_counters()
     comm.reset_stats()
     model.sstats = dict.fromkeys(model.sstats, 0)
+    model.diag = a.verbose
     if a.verbose:
         model.byte_trace = {}
     comm.barrier()

@@ -192,24 +192,31 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
     if (hinted_) return ~victim_key_locked(c);  // a window of the furthest-needed data
     return c.last_use + (c.list == 3 ? (1ull << 62) : 0) + (c.active ? (1ull << 61) : 0);
   };
+  // Costs first (one key per chunk; UINT64_MAX = not evictable), then the
+  // monotone-deque window pass over the array.
+  static thread_local std::vector<uint64_t> costs;
+  costs.resize(nchunks_);
   for (uint32_t i = 0; i < nchunks_; ++i) {
-    ChunkInfo& c = chunks_[i];
-    bool ok = c.state == ChunkState::FREE ||
-              (c.state == ChunkState::ALLOCATED && c.pin_count == 0 && !floor_protects_locked(c, floor));
-    if (!ok) {
+    const ChunkInfo& c = chunks_[i];
+    const bool ok = c.state == ChunkState::FREE ||
+                    (c.state == ChunkState::ALLOCATED && c.pin_count == 0 && !floor_protects_locked(c, floor));
+    costs[i] = ok ? cost_of(i) : UINT64_MAX;
+  }
+  for (uint32_t i = 0; i < nchunks_; ++i) {
+    const uint64_t cost = costs[i];
+    if (cost == UINT64_MAX) {
       start = i + 1;
       dq.clear();
       continue;
     }
-    uint64_t cost = cost_of(i);
-    while (!dq.empty() && cost_of(dq.back()) <= cost) dq.pop_back();
+    while (!dq.empty() && costs[dq.back()] <= cost) dq.pop_back();
     dq.push_back(i);
     if (i + 1 - start > n) {
       start = i + 1 - n;
       while (!dq.empty() && dq.front() < start) dq.pop_front();
     }
     if (i + 1 - start == n) {
-      uint64_t wcost = cost_of(dq.front());
+      const uint64_t wcost = costs[dq.front()];
       if (wcost < best_cost) {
         best_cost = wcost;
         best_first = start;

@@ -181,7 +181,7 @@ void Ring::worker() {
     if (pend < 0) return;
     const uint64_t t0 = now_ns();
     fail(be_->dma_complete(pend), pend_last);
-    Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
+    if (kind_ == RingKind::CPU_TO_GPU) Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
     publish(pend_last);
     pend = -1;
   };
@@ -198,7 +198,7 @@ void Ring::worker() {
       if (work_.empty() && !stop_) {
         const uint64_t t_idle = now_ns();
         wcv_.wait(g, [&] { return stop_ || !work_.empty(); });
-        Tools::get().inc(Counter::RingIdleNs, now_ns() - t_idle);
+        if (kind_ == RingKind::CPU_TO_GPU) Tools::get().inc(Counter::RingIdleNs, now_ns() - t_idle);
       }
       if (work_.empty()) return;  // stop_ with nothing left
       b = std::move(work_.front());
@@ -208,8 +208,10 @@ void Ring::worker() {
       const int slot = pend == 0 ? 1 : 0;
       const uint64_t t0 = now_ns();
       Status st = copies.empty() ? Status::OK : be_->dma_issue(dev_, copies.data(), copies.size(), (int)kind_, slot);
-      Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
-      Tools::get().inc(Counter::RingCopyCalls, copies.size());
+      if (kind_ == RingKind::CPU_TO_GPU) {
+        Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
+        Tools::get().inc(Counter::RingCopyCalls, copies.size());
+      }
       complete_pending();  // the batch before (its copies are ahead of these on the engines)
       if (st != Status::OK) {
         fail(st, b.last);
@@ -305,8 +307,10 @@ Status Ring::run_batch(Batch& b) {
       if (st == Status::OK) {
         const uint64_t t_copy = now_ns();
         st = be_->dma_copy(dev_, copies.data(), copies.size(), (int)kind_);
-        Tools::get().inc(Counter::RingCopyNs, now_ns() - t_copy);
-        Tools::get().inc(Counter::RingCopyCalls, copies.size());
+        if (kind_ == RingKind::CPU_TO_GPU) {
+          Tools::get().inc(Counter::RingCopyNs, now_ns() - t_copy);
+          Tools::get().inc(Counter::RingCopyCalls, copies.size());
+        }
       }
     }
     copies.clear();
@@ -337,7 +341,7 @@ Status Ring::run_batch(Batch& b) {
         if (st == Status::OK && s.wait && !s.wait->done.load(std::memory_order_acquire)) {
           const uint64_t t_wait = now_ns();
           st = s.wait->wait();
-          Tools::get().inc(Counter::RingFenceWaitNs, now_ns() - t_wait);
+          if (kind_ == RingKind::CPU_TO_GPU) Tools::get().inc(Counter::RingFenceWaitNs, now_ns() - t_wait);
         }
         break;
       case SqeOp::NOP:

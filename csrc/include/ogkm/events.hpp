@@ -190,10 +190,10 @@ enum class Counter : int {
   VmmUnmapNs,          // host time in stable-VA unmaps
   TlbFlushNs,          // host time in translation flushes
   PlaceStableNs,       // host time in stable-VA placement (place_stable, incl. the above and evictions)
-  RingFenceWaitNs,     // DMA ring workers: host time waiting for a copy's dependencies (reuse fences)
-  RingCopyNs,          // DMA ring workers: time in engine copies (issue + completion)
-  RingIdleNs,          // DMA ring workers: time with no batch to run
-  RingCopyCalls,       // DMA ring workers: engine copy calls (merged runs)
+  RingFenceWaitNs,     // H2D DMA ring workers: host time waiting for a copy's dependencies (reuse fences)
+  RingCopyNs,          // H2D DMA ring workers: time in engine copies (issue + completion)
+  RingIdleNs,          // H2D DMA ring workers: time with no batch to run
+  RingCopyCalls,       // H2D DMA ring workers: engine copy calls (merged runs)
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -556,7 +556,10 @@ class TieredLlama:
         # streaming diagnostics (bench.py aux "stream_stats"): prefetches issued /
         # refused by the victim floor, uses that found their unit not prefetched,
         # host ms in acquire and in the run-ahead bound's waits
-        self.sstats = dict.fromkeys(("prefetched", "refused", "demand", "acquire_ms", "ahead_wait_ms"), 0)
+        self.sstats = dict.fromkeys(("prefetched", "refused", "demand", "prefetch_ms", "acquire_ms", "ahead_wait_ms",
+                                     "late_uses", "late_mb"), 0)
+        self.diag = False  # bench --verbose: also count bytes not yet placed in HBM when a unit is used
+
         # Next-use hints (planner off): a streamed unit is next used one step
         # later at the same place in the use order, so the runtime can evict
         # in next-use order (Belady, ChunkArena::set_next_use) instead of
@@ -1025,6 +1028,7 @@ class TieredLlama:
                 nb -= buf.resident_bytes(rt.Loc.gpu(self.dev))
             if self._inflight and inflight + nb > self.window_bytes:
                 break
+            t_pf = time.perf_counter()
             if self.next_use:
                 # evict only units needed after this one; refused (no such
                 # window): OGKM_FLOOR_FALLBACK=stop leaves it to its use,
@@ -1039,6 +1043,7 @@ class TieredLlama:
                     self._buf(key).prefetch(rt.Loc.gpu(self.dev))
             else:
                 self._buf(key).prefetch(rt.Loc.gpu(self.dev))
+            self.sstats["prefetch_ms"] += (time.perf_counter() - t_pf) * 1e3
             self._inflight.append(key)
             self.sstats["prefetched"] += 1
             self._inflight_b[key] = nb
@@ -1069,6 +1074,11 @@ class TieredLlama:
             if self.next_use:
                 self._clock_use(key)
             self._prefetch_ahead()
+        if self.diag and not self.fake:
+            miss = self._buf(key).size - self._buf(key).resident_bytes(rt.Loc.gpu(self.dev))
+            if miss > 0:
+                self.sstats["late_uses"] += 1
+                self.sstats["late_mb"] += miss / 2**20
         t_a = time.perf_counter()
         lease = self._buf(key).acquire(self.dev, rt.READ)
         self.sstats["acquire_ms"] += (time.perf_counter() - t_a) * 1e3
