@@ -51,8 +51,9 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | N
 
 
 # Few-row norms as two wide launches (k_norm_ssq + k_norm_scale) instead of one
-# workgroup per row (OGKM_WIDE_NORM=0: the one-launch kernel).
-WIDE_NORM = os.environ.get("OGKM_WIDE_NORM", "1") != "0"
+# workgroup per row (OGKM_WIDE_NORM=1). Off by default: measured 5.1 + 5.1 us
+# per norm on config 2 against the one-launch kernel's 8.5 (profiles/r4_config2.md).
+WIDE_NORM = os.environ.get("OGKM_WIDE_NORM", "0") != "0"
 
 
 class _NormScratch:

@@ -171,10 +171,13 @@ def test_attention_cpu(fake_rt, length):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("dim", [512, 1024, 2048, 4096, 5120, 8192, 16384])
-def test_rmsnorm_gpu(gpu_rt, dim):
+def test_rmsnorm_gpu(gpu_rt, dim, wide, monkeypatch):
     """One workgroup per row (dim <= 1024) and the multi-workgroup form (one per
-    1024 columns, the row's last arriver normalises), ragged last quarter (5120)."""
+    1024 columns, the row's last arriver normalises), ragged last quarter (5120);
+    wide: the two-launch form (k_norm_ssq + k_norm_scale, OGKM_WIDE_NORM=1)."""
+    monkeypatch.setattr(fused, "WIDE_NORM", wide)
     _check_rmsnorm(True, dim)
 
 
