@@ -320,7 +320,7 @@ def run_torch_managed(a) -> None:
                 "link_gbps": round(s["bytes_xfer_htd"] / dt / 1e9, 2), "evictions": s["evictions"],
                 "vmm_remaps": s["vmm_remaps"], "tlb_flushes": s["tlb_flushes"], "ops": mode.ops,
                 "host_ms_per_step": {k: round(s[k + "_ns"] / 1e6 / a.steps, 1)
-                                     for k in ("place_stable", "vmm_map", "vmm_unmap", "tlb_flush")},
+                                     for k in ("place_stable", "vmm_map", "vmm_unmap", "tlb_flush", "stable_wait")},
                 "ring_per_step": _ring_per_step(s, a.steps),
                 "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches, "init_s": round(init_s, 1),
                 "trace_len": len(mode._trace), "hinted_ops": mode.hinted_ops, "trace_misses": mode.trace_misses,

@@ -291,23 +291,40 @@ void ChunkArena::set_op_clock(uint64_t now) {
 // data by the distance to its next use. Unhinted data touched within the last
 // two ops (an activation between its producer and consumer) ranks as needed
 // next. Hints in the past (the trace moved on without a use) count as unknown.
-uint64_t ChunkArena::victim_key_locked(const ChunkInfo& c) const {
-  if (c.next_use == kDeadUse) return kDeadUse;
+uint64_t ChunkArena::base_key_locked(const ChunkInfo& c) const {
+  if (c.next_use == kDeadUse) {
+    // Freed data: nothing to copy out - but kernels queued before the free may
+    // still read it, and a freed torch tensor is usually re-allocated (same
+    // size, same stable VA) within a few ops: evicting it then costs a remap
+    // that waits for those readers. Recently used dead data ranks as just used.
+    const int64_t dc = config().arena_dead_cooldown;
+    if (dc > 0 && c.last_op && op_clock_ >= c.last_op && op_clock_ - c.last_op < (uint64_t)dc) return 1;
+    return kDeadUse;
+  }
   // Just used: its readers may still be queued, so a copy into the chunk would
   // wait for them (the reuse fence) and the link would idle behind compute -
   // keep it for arena_reuse_cooldown op-clock steps (it is next needed a whole
   // pass later: evicting the data used a few steps earlier costs the same).
   const int64_t cool = config().arena_reuse_cooldown;
   if (cool > 0 && c.last_op && op_clock_ >= c.last_op && op_clock_ - c.last_op < (uint64_t)cool) return 1;
-  if (c.next_use >= op_clock_) return c.next_use - op_clock_;  // due now: 0, the last to go
+  const uint64_t nu = c.next_use & ~kEvictFirst;
+  if (nu >= op_clock_) return nu - op_clock_;  // due now: 0, the last to go
   if (op_clock_ - c.last_op <= 2) return 1;
   return (1ull << 62) + (clock_ - std::min(clock_, c.last_use));
+}
+
+// Ranking key: the base key, hinted data flagged kEvictFirst (the "stream"
+// class of a spread plan) ahead of every unflagged hinted chunk.
+uint64_t ChunkArena::victim_key_locked(const ChunkInfo& c) const {
+  const uint64_t k = base_key_locked(c);
+  const bool first = c.next_use != kDeadUse && (c.next_use & kEvictFirst);
+  return first && k < kEvictFirst ? k + kEvictFirst : k;
 }
 
 // The floor is an op-clock time: data whose next use comes no later is kept.
 bool ChunkArena::floor_protects_locked(const ChunkInfo& c, uint64_t floor) const {
   if (!floor || !hinted_) return false;
-  const uint64_t k = victim_key_locked(c);
+  const uint64_t k = base_key_locked(c);  // the true next use, not the class bonus
   return k < (1ull << 62) && k + op_clock_ <= floor;
 }
 

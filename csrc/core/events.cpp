@@ -147,6 +147,7 @@ const char* counter_name(Counter c) {
                             "vmm_unmap_ns",
                             "tlb_flush_ns",
                             "place_stable_ns",
+                            "stable_wait_ns",
                             "ring_fence_wait_ns",
                             "ring_copy_ns",
                             "ring_idle_ns",

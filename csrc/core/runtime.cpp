@@ -603,8 +603,10 @@ void Runtime::stable_unmap_locked(Block* b) {
   const int64_t c = b->stable_chunk.load();
   if (c < 0) return;
   Range* r = b->range;
+  const uint64_t t_w = now_ns();
   if (b->stable_users.wait() != Status::OK)
     RT_ERR("stable VA users of range %llu block %llu failed", (unsigned long long)r->id, (unsigned long long)b->index);
+  Tools::get().inc(Counter::StableWaitNs, now_ns() - t_w);
   b->stable_users.clear();
   Tools::get().inc(Counter::VmmRemaps);
   const uint64_t t_unmap = now_ns();
@@ -663,8 +665,10 @@ void Runtime::stable_map_block(Block* b) {
       std::lock_guard<std::mutex> sg(stable_m_);
       users = b->stable_users;
     }
+    const uint64_t t_w = now_ns();
     if (users.wait() != Status::OK)
       RT_ERR("stable VA users of range %llu block %llu failed", (unsigned long long)r->id, (unsigned long long)b->index);
+    Tools::get().inc(Counter::StableWaitNs, now_ns() - t_w);
   }
   std::lock_guard<std::mutex> sg(stable_m_);
   if (want == b->stable_chunk.load()) {  // back on the chunk it still maps: valid again

@@ -177,6 +177,7 @@ class ChunkArena {
  private:
   int32_t pick_victim_locked();  // coldest evictable chunk (reserve(1) order), -1 = none
   uint64_t victim_key_locked(const ChunkInfo& c) const;  // next-use mode: larger = evict sooner
+  uint64_t base_key_locked(const ChunkInfo& c) const;    // the same without the kEvictFirst class bonus
   bool floor_protects_locked(const ChunkInfo& c, uint64_t floor) const;
   // next-use mode: up to n evictable chunks with the largest keys above the floor
   void pick_victims_by_next_use_locked(uint32_t n, std::vector<uint32_t>* out);
@@ -263,6 +264,10 @@ class HostArena : public ChunkArena {
 };
 
 constexpr uint64_t kDeadUse = ~0ull;  // ChunkInfo::next_use of dead data
+// Flag bit of a next-use hint (hint_next_use(when | kEvictFirst)): among data
+// with a known next use, flagged data is evicted first (a spread residency:
+// the "stream" class); the floor still compares the true next use.
+constexpr uint64_t kEvictFirst = 1ull << 61;
 
 // Scoped lower bound on the next-use key of eviction victims for the calling
 // thread (next-use mode only): a prefetch of data needed at op T evicts only

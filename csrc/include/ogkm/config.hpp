@@ -56,6 +56,7 @@ namespace ogkm {
   X(stable_lazy_unmap, 0, "stable VAs of evicted blocks stay mapped to their old chunk until the block returns (saves the unmap; a stray access reads stale data instead of faulting)") \
   X(stable_batch_blocks, 32, "stable-VA placement: 2 MB blocks per eviction / fill / remap group (pipelined)") \
   X(arena_reuse_cooldown, 0, "next-use eviction: data used within this many op-clock steps is kept (its readers may still be queued)") \
+  X(arena_dead_cooldown, 0, "next-use eviction: freed data used within this many op-clock steps ranks as just used, not as the first victim") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
   X(ring_pipeline, 1, "DMA ring workers issue the next batch of plain copies before the previous one completed (two completion slots)") \
   X(vmm_rocr_remap, 1, "stable-VA remaps through ROCr hsa_amd_vmem_* (HIP keeps a placeholder mapping of the VA); 0 = hipMemMap / hipMemUnmap") \

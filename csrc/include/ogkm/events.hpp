@@ -190,6 +190,7 @@ enum class Counter : int {
   VmmUnmapNs,          // host time in stable-VA unmaps
   TlbFlushNs,          // host time in translation flushes
   PlaceStableNs,       // host time in stable-VA placement (place_stable, incl. the above and evictions)
+  StableWaitNs,        // host time waiting for kernels still using a stable VA before its remap / unmap
   RingFenceWaitNs,     // H2D DMA ring workers: host time waiting for a copy's dependencies (reuse fences)
   RingCopyNs,          // H2D DMA ring workers: time in engine copies (issue + completion)
   RingIdleNs,          // H2D DMA ring workers: time with no batch to run

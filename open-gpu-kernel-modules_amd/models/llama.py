@@ -68,6 +68,7 @@ _FLOOR_FALLBACK = os.environ.get("OGKM_FLOOR_FALLBACK", "stop")
 # 0: unit sizes - measured the same on the 70B, 103.4 vs 102.7 tok/s, and a
 # larger in-flight share of a small arena streams more)
 _WINDOW_MISSING = os.environ.get("OGKM_WINDOW_MISSING", "0") != "0"
+_EVICT_FIRST = 1 << 61  # kEvictFirst (csrc/include/ogkm/arena.hpp): evict before unflagged hinted data
 
 
 @dataclass(frozen=True)
@@ -570,6 +571,15 @@ class TieredLlama:
                          and bool(self.stream_seq))
         self._seq_pos = {k: j for j, k in enumerate(self.stream_seq)}
         self._pass, self._last_pos = 0, -1
+        # Spread classes (see _hint_used): alternate runs of ~spread bytes in use order.
+        self._spread_class = None
+        if self.next_use and os.environ.get("OGKM_SPREAD", "1") != "0":
+            q = int(float(os.environ.get("OGKM_SPREAD_MB", "0")) * 2**20) or max(self.window_bytes, 1)
+            cum, cls = 0, []
+            for k in self.stream_seq:
+                cls.append((cum // q) % 2 == 1)
+                cum += self._unit_bytes(k)
+            self._spread_class = cls
         # Bounded run-ahead: compute events of streamed units enqueued but maybe
         # not yet run. Leases wait GPU-side, so without a bound the host would
         # prefetch a whole step ahead and the ring would evict (and wait on)
@@ -1007,10 +1017,22 @@ class TieredLlama:
     def _hint_used(self, key) -> None:
         """Next-use mode, once ``key`` is leased: its next use is one pass later
         (hinted after the lease pinned it - before, the prefetches queued for
-        this use would see it as the furthest-needed unit and evict it)."""
+        this use would see it as the furthest-needed unit and evict it).
+        Spread (OGKM_SPREAD, default on): units of the "stream" class - every
+        other run of ~window bytes in use order - carry the kEvictFirst flag,
+        so the arena evicts them before any "keep"-class unit (the prefetch
+        floor still compares true next uses). Plain Belady keeps
+        one contiguous run of the cycle resident, and the link idles while the
+        compute crosses it (126 ms of a 614 ms 70B step, profiles/
+        r4_planner_off_diag.jsonl); interleaved runs keep the prefetch window
+        streaming throughout, as the static plan's evenly spread resident
+        layers do. Hints only order the victims: a stream-class unit is still
+        kept when there is room, a keep-class one still evicted when there is not."""
         if key in self._seq_pos:
             n = len(self.stream_seq)
-            self._buf(key).hint_next_use(self._pass * n + self._seq_pos[key] + n)
+            p = self._seq_pos[key]
+            flag = _EVICT_FIRST if (self._spread_class is not None and self._spread_class[p]) else 0
+            self._buf(key).hint_next_use((self._pass * n + p + n) | flag)
 
     def _prefetch_ahead(self) -> None:
         """Keep up to ``window_bytes`` of upcoming streamed tensors in flight on the ring."""
