@@ -411,6 +411,7 @@ class TieredLlama:
             raise ValueError(f"HBM budget {self.budget/2**30:.1f} GiB too small for KV + staging "
                              f"({(fixed + staging + self.stage_bytes)/2**30:.1f} GiB)")
         n_res = max(0, min(cfg.n_layers, avail // layer_cost - int(os.environ.get("OGKM_RESIDENT_MARGIN", "0"))))
+        self._spread_room = max(0, avail)  # planner off: HBM the runtime may keep units in (spread classes)
         if planner == "off":
             n_res, avail = 0, 0
         left = avail - n_res * layer_cost
@@ -571,14 +572,22 @@ class TieredLlama:
                          and bool(self.stream_seq))
         self._seq_pos = {k: j for j, k in enumerate(self.stream_seq)}
         self._pass, self._last_pos = 0, -1
-        # Spread classes (see _hint_used): alternate runs of ~spread bytes in use order.
+        # Spread classes (see _hint_used): the "keep" share of the units is the
+        # share of their bytes the arena can hold (less 3 %), spread over the
+        # use order unit by unit (error diffusion), like the static plan's
+        # evenly spread resident layers; the rest is the "stream" class.
         self._spread_class = None
         if self.next_use and os.environ.get("OGKM_SPREAD", "1") != "0":
-            q = int(float(os.environ.get("OGKM_SPREAD_MB", "0")) * 2**20) or max(self.window_bytes, 1)
-            cum, cls = 0, []
+            tot = sum(self._unit_bytes(k) for k in self.stream_seq) or 1
+            f = min(1.0, float(os.environ.get("OGKM_SPREAD_KEEP", "0.97")) * self._spread_room / tot)
+            acc, cls = 0.0, []
             for k in self.stream_seq:
-                cls.append((cum // q) % 2 == 1)
-                cum += self._unit_bytes(k)
+                nb = self._unit_bytes(k)
+                acc += nb * f
+                keep = acc >= nb
+                if keep:
+                    acc -= nb
+                cls.append(not keep)
             self._spread_class = cls
         # Bounded run-ahead: compute events of streamed units enqueued but maybe
         # not yet run. Leases wait GPU-side, so without a bound the host would
@@ -1018,8 +1027,8 @@ class TieredLlama:
         """Next-use mode, once ``key`` is leased: its next use is one pass later
         (hinted after the lease pinned it - before, the prefetches queued for
         this use would see it as the furthest-needed unit and evict it).
-        Spread (OGKM_SPREAD, default on): units of the "stream" class - every
-        other run of ~window bytes in use order - carry the kEvictFirst flag,
+        Spread (OGKM_SPREAD, default on): units of the "stream" class - spread
+        over the use order so the "keep" class fits the arena - carry the kEvictFirst flag,
         so the arena evicts them before any "keep"-class unit (the prefetch
         floor still compares true next uses). Plain Belady keeps
         one contiguous run of the cycle resident, and the link idles while the
