@@ -86,9 +86,10 @@ def parse():
     ap.add_argument("--fake-hbm-mb", type=int, default=1024)
     ap.add_argument("--dump-logits", default="",
                     help="write the last step's logits [global batch, vocab] (fp32) to this file (rank 0)")
-    ap.add_argument("--planner", choices=("static", "off"), default="static",
-                    help="off: no residency plan - every weight prefers HBM, nothing is pinned, the runtime's "
-                         "LRU / prefetch / eviction decide residency")
+    ap.add_argument("--planner", choices=("static", "off"), default="off",
+                    help="off (default): no residency plan - every weight prefers HBM, nothing is pinned; the "
+                         "runtime decides residency from the model's next-use hints (Belady order, spread "
+                         "classes) and its prefetch / eviction. static: a hand-made plan pins whole layers")
     ap.add_argument("--kv-tiering", action="store_true",
                     help="KV prefixes as evictable per-layer units (resident with their layer, else streamed)")
     ap.add_argument("--allocator", action="store_true",
@@ -551,9 +552,8 @@ def main() -> None:
     if e.rank == 0:
         name = {"llama3-70b": "Llama-3-70B", "llama3-405b": "Llama-3-405B", "llama3-8b": "Llama-3-8B"}.get(a.model,
                                                                                                         a.model)
+        # the residency policy is config.planner ("off" = runtime-decided, the default)
         metric = f"tokens/sec {name} {a.oversub:g}x oversubscribe"
-        if a.planner == "off":
-            metric += " (planner off: runtime-decided residency, next-use eviction)"
         if sim:  # one shard of an N-GPU job on one GPU: an upper bound, not a measured N-GPU rate
             metric += f" (tp{a.simulate_tp} rank-0 shard simulated on 1 GPU, collectives skipped)"
         out = {

@@ -412,6 +412,11 @@ class TieredLlama:
                              f"({(fixed + staging + self.stage_bytes)/2**30:.1f} GiB)")
         n_res = max(0, min(cfg.n_layers, avail // layer_cost - int(os.environ.get("OGKM_RESIDENT_MARGIN", "0"))))
         self._spread_room = max(0, avail)  # planner off: HBM the runtime may keep units in (spread classes)
+        # What the static plan would stream per step (planner off: the bytes the
+        # runtime's own residency is measured against; traffic() plans with it).
+        res_s = [((i + 1) * n_res) // cfg.n_layers > (i * n_res) // cfg.n_layers for i in range(cfg.n_layers)]
+        self.plan_streamed_bytes = (sum(self.res_layer_bytes + self.kv_unit_bytes for r in res_s if not r)
+                                    + (0 if avail - n_res * layer_cost >= head_cost else self.res_head_bytes))
         if planner == "off":
             n_res, avail = 0, 0
         left = avail - n_res * layer_cost
@@ -439,6 +444,8 @@ class TieredLlama:
         self.streamed_bytes = (sum(self.res_layer_bytes + self.kv_unit_bytes for r in self.resident if not r)
                                - sum(self.res_part[k[2]] for k in self.extra_resident)
                                + (0 if self.head_resident else self.res_head_bytes))
+        if planner != "off":
+            self.plan_streamed_bytes = self.streamed_bytes
         # a window that wraps around a small streamed set would evict units before their use
         self.lookahead = min(lookahead, max(lookahead_arg, self.streamed_bytes // (8 * slot)))
         self.window_bytes = self.lookahead * slot
@@ -722,7 +729,7 @@ class TieredLlama:
             "layer_gb": self.layer_bytes / 1e9, "resident_layers": sum(self.resident),
             "extra_resident_units": len(self.extra_resident),
             "streamed_layers": self.cfg.n_layers - sum(self.resident), "head_resident": self.head_resident,
-            "streamed_gb_per_step": self.streamed_bytes / 1e9, "init_s": getattr(self, "init_seconds", None),
+            "streamed_gb_per_step": self.plan_streamed_bytes / 1e9, "init_s": getattr(self, "init_seconds", None),
             "packed_host_copies": getattr(self, "packed", False),
             "weight_format": self.wfmt, "resting_layer_gb": self.res_layer_bytes / 1e9,
             "stage_gb": self.stage_bytes / 1e9, "tiers": self.tiers, "kv_format": self.kv_format,
@@ -756,7 +763,7 @@ class TieredLlama:
         from ..parallel import topology
         cfg, W = self.cfg, max(self.world, self.sworld)
         n_units = len(self.order)
-        pcie = self.streamed_bytes
+        pcie = self.plan_streamed_bytes
         if self.sworld > 1:
             shard = sum(self._unit_bytes(k) for k in self.order if k[0] != "kv")
             xgmi = (self.sworld - 1) * shard

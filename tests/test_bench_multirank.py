@@ -92,13 +92,15 @@ def test_bench_forced_one_rank_group(single, tmp_path, parallel):
 def test_plan_traffic_matches_measured_four_ranks(tmp_path, parallel):
     """The plan's per-step traffic (TieredLlama.traffic(), what bench.py
     --plan-only prints) against what a 4-rank run moved: xGMI bytes received by
-    the collectives exactly, PCIe (streamed units) within 10%."""
+    the collectives exactly, PCIe (streamed units) within 10% - under the static
+    plan, whose residency the traffic model describes (planner off, the
+    bench default, decides residency at run time: tests/test_model.py)."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", OGKM_UNIT_MIN_MB="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"), "--gpus", "4"]
     args = list(ARGS)
     args[args.index("--steps") + 1] = "2"
-    args += ["--parallel", parallel]
+    args += ["--parallel", parallel, "--planner", "static"]
     r = subprocess.run(cmd + args, env=env, capture_output=True, text=True, timeout=900)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-4000:]
