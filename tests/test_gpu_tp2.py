@@ -36,9 +36,9 @@ def _run2(tmp_path, parallel: str) -> tuple[dict, torch.Tensor]:
     env = dict(os.environ, PYTHONPATH=ROOT, OGKM_UNIT_MIN_MB="0", OMP_NUM_THREADS="4")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-gpu", "--launch-timeout", "200",
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-gpu", "--launch-timeout", "120",
            "--parallel", parallel] + ARGS + ["--dump-logits", dump]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=260)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-4000:]
     return json.loads(lines[-1]), torch.load(dump)
