@@ -575,8 +575,11 @@ class TieredLlama:
         # recency - on a cyclic step larger than HBM, LRU evicts every unit just
         # before its reuse; Belady keeps a fixed subset resident, as the static
         # plan does by hand. Op clock = passes * len(stream_seq) + position.
+        # (not for peer shards: their units stream through the all-gather
+        # pipeline, which does not keep the op clock - the workingset policy
+        # decides there)
         self.next_use = (self.planner == "off" and os.environ.get("OGKM_NEXT_USE", "1") != "0"
-                         and bool(self.stream_seq))
+                         and bool(self.stream_seq) and self.sworld <= 1)
         self._seq_pos = {k: j for j, k in enumerate(self.stream_seq)}
         self._pass, self._last_pos = 0, -1
         # Spread classes (see _hint_used): the "keep" share of the units is the
