@@ -490,11 +490,15 @@ def main() -> None:
     comm.barrier()
     t_init = time.perf_counter()
     sim = a.simulate_tp > 1 and world == 1
+    # Peer shards stream every unit through the all-gather pipeline, which the
+    # runtime-decided residency does not drive (it hung on the 2-rank GPU run):
+    # shards keep the static plan.
+    planner = "static" if a.parallel == "shards" and world > 1 else a.planner
     model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 3,
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
                               seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
                               weight_format=a.weights, tiers=a.tiers, cxl_frac=a.cxl_frac, kv_format=a.kv_format,
-                              parallel=a.parallel, planner=a.planner, kv_tiering=a.kv_tiering)
+                              parallel=a.parallel, planner=planner, kv_tiering=a.kv_tiering)
     plan = model.describe()
     init_s = time.perf_counter() - t_init
     g = torch.Generator(device="cpu").manual_seed(42)
@@ -581,7 +585,7 @@ def main() -> None:
                 "process_group": e.backend,
                 "launcher": ("bench.py" if os.environ.get("OGKM_BENCH_LAUNCHED") == "1"
                              else "external" if world > 1 else "none"),
-                "planner": a.planner,
+                "planner": planner,
                 "kv_tiering": a.kv_tiering,
                 "torch_allocator": "ogkm-arena" if a.allocator else "torch-caching",
                 "rank_host_numa_nodes": host_nodes,
