@@ -334,7 +334,9 @@ def _mode_class():
 _METADATA_OPS: frozenset = frozenset()
 _NOT_SPLIT = object()
 _EVICT_FIRST = 1 << 61  # kEvictFirst (csrc/include/ogkm/arena.hpp)
-_SPREAD = __import__("os").environ.get("OGKM_MANAGED_SPREAD", "1") != "0"
+# off by default: measured slower on the stock 70B (36.4 vs 38.9 tok/s, 89.7 vs 81.8 GB/step
+# H2D - the activations share the arena, so the stream class thrashes; tools/gpu_r4_sp.sh)
+_SPREAD = __import__("os").environ.get("OGKM_MANAGED_SPREAD", "0") != "0"
 _SPREAD_KEEP = float(__import__("os").environ.get("OGKM_MANAGED_SPREAD_KEEP", "0.85"))
 _MAX_RUNS = 16384  # contiguous runs enumerated per written view (beyond: its bounding extent)
 
