@@ -74,8 +74,15 @@ def test_bench_four_ranks(single, torchrun_tp4, tmp_path, parallel):
         # the same single-GPU math on each rank's own sequences: bit-identical
         assert torch.equal(logits, ref)
     else:
-        # row-parallel partial sums are reduced in a different order
-        torch.testing.assert_close(logits, ref, atol=0.05, rtol=0.05)
+        # row-parallel partial sums are reduced in a different order (bf16
+        # activations between the GEMMs): measured max |diff| 0.023, mean 0.0044
+        # on logits of magnitude ~3; the greedy tokens agree wherever the
+        # 1-rank top-2 margin exceeds twice the worst difference
+        torch.testing.assert_close(logits, ref, atol=0.03, rtol=0.01)
+        assert (logits.float() - ref.float()).abs().mean() < 0.01
+        top2 = ref.float().topk(2, dim=-1).values
+        clear = (top2[:, 0] - top2[:, 1]) > 0.05
+        assert torch.equal(logits.argmax(-1)[clear], ref.argmax(-1)[clear])
 
 
 @pytest.mark.parametrize("parallel", ["tp", "shards"])
