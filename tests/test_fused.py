@@ -217,3 +217,30 @@ def test_attention_group_shapes_gpu(gpu_rt, hq, hkv, hd, length, split_tokens):
     in both workgroup shapes: 256-token four-wave splits and 64-token one-wave
     splits (an explicit option; measured slower at the bench shapes, profiles/r3_attn_split.txt)."""
     _check_attention(True, length, hq, hkv, hd, split_tokens)
+
+
+# KV-read rate guards at ~85 % of the measured MALL-cold rates (tools/bench_attn.py,
+# profiles/r4_attn_variants.txt: 8B 4.28, 70B 3.69, 70B-tp8 1.42 TB/s).
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,B,hq,hkv,floor_tbps", [("8b", 64, 32, 8, 3.6), ("70b", 64, 64, 8, 3.1),
+                                                      ("70b-tp8", 64, 8, 1, 1.2)])
+def test_attention_gpu_kv_rate(gpu_rt, name, B, hq, hkv, floor_tbps):
+    hd, L = 128, 1025
+    q = torch.randn(B, hq, hd, device="cuda").to(torch.bfloat16)
+    kvb = 2 * B * hkv * L * hd * 2
+    ncopy = max(1, -(-(1 << 30) // kvb))  # rotate over >= 1 GB: past the 256 MB MALL
+    caches = [torch.randn(2, B, hkv, L, hd, device="cuda").to(torch.bfloat16) for _ in range(ncopy)]
+    for i in range(3):
+        fused.attention(q, caches[i % ncopy], L)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    iters = 30
+    e0.record()
+    for i in range(iters):
+        fused.attention(q, caches[i % ncopy], L)
+    e1.record()
+    torch.cuda.synchronize()
+    sec = e0.elapsed_time(e1) / 1e3 / iters
+    tbps = kvb / sec / 1e12
+    print(f"attention {name}: {sec * 1e6:.1f} us, {tbps:.2f} TB/s of KV")
+    assert tbps > floor_tbps
