@@ -585,7 +585,7 @@ def main() -> None:
                 "process_group": e.backend,
                 "launcher": ("bench.py" if os.environ.get("OGKM_BENCH_LAUNCHED") == "1"
                              else "external" if world > 1 else "none"),
-                "planner": planner,
+                "planner": model.planner,
                 "kv_tiering": a.kv_tiering,
                 "torch_allocator": "ogkm-arena" if a.allocator else "torch-caching",
                 "rank_host_numa_nodes": host_nodes,
