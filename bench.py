@@ -50,6 +50,11 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+if hasattr(__import__("signal"), "pthread_sigmask"):
+    # Hang dumps (ogkm.diag): SIGUSR1 is blocked before torch / HIP start any
+    # thread, so every thread inherits the mask and only the dump thread takes it.
+    import signal as _signal
+    _signal.pthread_sigmask(_signal.SIG_BLOCK, {_signal.SIGUSR1})
 
 
 def parse():
@@ -120,6 +125,23 @@ def _free_port() -> int:
     return p
 
 
+def _request_dumps(procs, wait_s: float = None) -> None:
+    """SIGUSR1 to every still-running rank (ogkm.diag dumps its threads' stacks and
+    the runtime's rings / leases to stderr), then give the dumps time to finish."""
+    import signal
+
+    if wait_s is None:
+        wait_s = float(os.environ.get("OGKM_HANG_DUMP_WAIT_S", "8"))
+    live = [p for p in procs if p.poll() is None]
+    for p in live:
+        try:
+            os.kill(p.pid, signal.SIGUSR1)
+        except ProcessLookupError:
+            pass
+    if live:
+        time.sleep(wait_s)
+
+
 def _kill_groups(procs, grace_s: float = 10.0) -> None:
     """SIGTERM every still-running rank's process group, SIGKILL what is left after ``grace_s``."""
     import signal
@@ -182,8 +204,9 @@ def launch_ranks(a) -> int:
             if all(c == 0 for c in codes):
                 return 0
             if time.monotonic() > deadline:
-                print(f"[bench] ranks still running after {a.launch_timeout:.0f} s: killing all {n}",
-                      file=sys.stderr, flush=True)
+                print(f"[bench] ranks still running after {a.launch_timeout:.0f} s: dumping their stacks, "
+                      f"then killing all {n}", file=sys.stderr, flush=True)
+                _request_dumps(procs)
                 _kill_groups(procs)
                 return 124
             time.sleep(0.2)
@@ -446,6 +469,11 @@ def main() -> None:
         # tensor exists); allocations resolve once the runtime is up.
         from ogkm import allocator
         allocator.enable()
+    from ogkm import diag
+    diag.install(tag=f"rank {os.environ.get('RANK', '0')} ")
+    # torchrun does not signal a hung rank: each rank dumps itself if init or the
+    # timed steps overrun (generous: a 405B init takes minutes)
+    diag.arm(float(os.environ.get("OGKM_INIT_WATCHDOG_S", "1500")), "init")
     e = comm.init("gloo" if fake or a.same_gpu else None)
     if e.world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but the process group has {e.world} ranks")
@@ -453,7 +481,8 @@ def main() -> None:
     if os.environ.get("OGKM_BENCH_FAIL_RANK", "") == str(e.rank):
         print(f"[bench] rank {e.rank}: injected failure", file=sys.stderr, flush=True)
         os._exit(3)
-    if os.environ.get("OGKM_BENCH_HANG_RANK", "") == str(e.rank):
+    hang_here = os.environ.get("OGKM_BENCH_HANG_RANK", "") == str(e.rank)
+    if hang_here and os.environ.get("OGKM_BENCH_HANG_AT", "init") == "init":
         time.sleep(1e6)
     pg_world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
     dev = 0 if a.same_gpu else e.local_rank
@@ -493,7 +522,7 @@ def main() -> None:
     # Peer shards stream every unit through the all-gather pipeline, which the
     # runtime-decided residency does not drive (it hung on the 2-rank GPU run):
     # shards keep the static plan.
-    planner = "static" if a.parallel == "shards" and world > 1 else a.planner
+    planner = os.environ.get("OGKM_SHARDS_PLANNER", "static") if a.parallel == "shards" and world > 1 else a.planner
     model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 3,
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
                               seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
@@ -512,7 +541,10 @@ def main() -> None:
     def sync():
         if not fake:
             torch.cuda.synchronize()
-    for _ in range(a.warmup):
+    diag.arm(float(os.environ.get("OGKM_STEP_WATCHDOG_S", str(120 + 30 * (a.warmup + a.steps)))), "decode steps")
+    for w in range(a.warmup):
+        if hang_here and w == 1:  # the drill's hang inside decode (runtime up, rings live)
+            time.sleep(1e6)
         tok = model.step(tok)
     lib.reset_counters()
     comm.reset_stats()
@@ -528,6 +560,7 @@ def main() -> None:
     sync()
     comm.barrier()
     dt = comm.max_over_ranks(time.perf_counter() - t0)
+    diag.disarm()
     s = lib.stats()
     xgmi_in = comm.STATS["allreduce_bytes_in"] + comm.STATS["allgather_bytes_in"]
     traffic = model.traffic()

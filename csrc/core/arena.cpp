@@ -280,11 +280,31 @@ void ChunkArena::set_next_use(uint32_t i, uint64_t when) {
   if (i >= nchunks_ || chunks_[i].state != ChunkState::ALLOCATED) return;
   chunks_[i].next_use = when;
   if (when && when != kDeadUse) hinted_ = true;
+  // A new hint can raise the chunk's rank past where the victim cache has it
+  // (data just used gets a far next use, or the evict-first class): remember
+  // it, next_victims_locked ranks these ahead of the cache's stale order.
+  if (vcache_valid_) vrisen_.push_back(i);
 }
 
 void ChunkArena::set_op_clock(uint64_t now) {
   std::lock_guard<OrderedMutex> g(m_);
   op_clock_ = std::max(op_clock_, now);
+}
+
+void ChunkArena::reset_op_clock() {
+  std::lock_guard<OrderedMutex> g(m_);
+  op_clock_ = 0;
+  hinted_ = false;
+  vcache_.clear();
+  vcache_pos_ = 0;
+  vcache_clock_ = 0;
+  vcache_valid_ = false;
+  vrisen_.clear();
+  for (uint32_t i = 0; i < nchunks_; ++i) {
+    ChunkInfo& c = chunks_[i];
+    if (c.next_use != kDeadUse) c.next_use = 0;
+    c.last_op = 0;
+  }
 }
 
 // Larger = evicted sooner: dead data, then unhinted data by age, then hinted
@@ -337,6 +357,7 @@ void ChunkArena::next_victims_locked(uint32_t want, uint64_t floor, std::vector<
                        op_clock_ < vcache_clock_ || op_clock_ - vcache_clock_ > (uint64_t)every;
     if (pass == 1 || stale) {  // full scan: every evictable chunk, best first
       vcache_.clear();
+      vrisen_.clear();
       for (uint32_t i = 0; i < nchunks_; ++i) {
         const ChunkInfo& c = chunks_[i];
         if (c.state != ChunkState::ALLOCATED || c.pin_count != 0) continue;
@@ -352,8 +373,46 @@ void ChunkArena::next_victims_locked(uint32_t want, uint64_t floor, std::vector<
       out->clear();
     }
     const uint64_t shift = op_clock_ - vcache_clock_;  // every hinted key fell by this much since the build
+    // Chunks re-hinted since the build, ranked now: those that outrank the
+    // cache's current front go first.
+    size_t nrisen = 0;
+    if (!vrisen_.empty()) {
+      std::vector<std::pair<uint64_t, uint32_t>> risen;
+      for (uint32_t i : vrisen_) {
+        const ChunkInfo& c = chunks_[i];
+        if (c.state != ChunkState::ALLOCATED || c.pin_count != 0) continue;
+        risen.emplace_back(victim_key_locked(c), i);
+      }
+      std::sort(risen.begin(), risen.end(), [](const auto& a, const auto& b) {
+        return a.first > b.first || (a.first == b.first && a.second < b.second);
+      });
+      risen.erase(std::unique(risen.begin(), risen.end()), risen.end());
+      uint64_t front_key = 0;  // the best cache entry still valid (the same test as the scan below)
+      for (size_t k = vcache_pos_; k < vcache_.size(); ++k) {
+        const ChunkInfo& c = chunks_[vcache_[k].second];
+        const uint64_t key = victim_key_locked(c);
+        const bool gone = c.state != ChunkState::ALLOCATED || c.pin_count != 0 ||
+                          (key < (1ull << 62) && key + shift < vcache_[k].first && vcache_[k].first < (1ull << 62));
+        if (!gone) {
+          front_key = key;
+          break;
+        }
+      }
+      for (auto& e : risen) {
+        if (out->size() >= want || e.first < front_key) break;
+        if (floor_protects_locked(chunks_[e.second], floor)) continue;
+        out->push_back(e);
+      }
+      nrisen = out->size();
+    }
+    auto taken = [&](uint32_t i) {
+      for (size_t k = 0; k < nrisen; ++k)
+        if ((*out)[k].second == i) return true;
+      return false;
+    };
     bool front = true;
     for (size_t k = vcache_pos_; k < vcache_.size() && out->size() < want; ++k) {
+      if (nrisen && taken(vcache_[k].second)) continue;
       const ChunkInfo& c = chunks_[vcache_[k].second];
       const uint64_t key = victim_key_locked(c);
       const bool gone = c.state != ChunkState::ALLOCATED || c.pin_count != 0 ||
@@ -374,6 +433,18 @@ void ChunkArena::pick_victims_by_next_use_locked(uint32_t n, std::vector<uint32_
   std::vector<std::pair<uint64_t, uint32_t>> cand;
   next_victims_locked(n, floor, &cand);
   static const bool dbg = getenv("OGKM_DEBUG_VICTIMS") != nullptr;
+  static const bool dbg2 = getenv("OGKM_DEBUG_VICTIMS_ALL") != nullptr;
+  if (dbg2) {
+    for (uint32_t i = 0; i < nchunks_; ++i) {
+      const ChunkInfo& c = chunks_[i];
+      Block* ob = c.owner;
+      fprintf(stderr, "  [chunk] %u state %d pin %u key %llu nu %llu owner %s\n", i, (int)c.state, c.pin_count,
+              (unsigned long long)victim_key_locked(c), (unsigned long long)c.next_use,
+              ob ? ob->range->name.c_str() : "-");
+    }
+    fprintf(stderr, "  [vcache] pos %zu size %zu valid %d clock %llu risen %zu\n", vcache_pos_, vcache_.size(),
+            (int)vcache_valid_, (unsigned long long)vcache_clock_, vrisen_.size());
+  }
   for (auto& c : cand) {
     if (dbg) {
       Block* ob = chunks_[c.second].owner;

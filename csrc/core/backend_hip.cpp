@@ -233,7 +233,24 @@ class HipBackend : public Backend {
     *h = (uint64_t)(uintptr_t)hh;
     return Status::OK;
   }
-  void vmm_release(uint64_t h) override { (void)hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)h); }
+  void vmm_release(uint64_t h) override {
+    // Drop the ROCr handle retained for this chunk (rocr_handle) and its lookup
+    // address before HIP frees it: a recreated arena may get the same numeric
+    // handle back, and a stale cache entry would map the stable VA to the old
+    // (leaked) physical chunk.
+    hsa_amd_vmem_alloc_handle_t rh{0};
+    {
+      std::lock_guard<std::mutex> g(reg_m_);
+      auto it = rocr_h_.find(h);
+      if (it != rocr_h_.end()) {
+        rh = it->second;
+        rocr_h_.erase(it);
+      }
+      handle_home_.erase(h);
+    }
+    if (rh.handle) (void)hsa_amd_vmem_handle_release(rh);
+    (void)hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)h);
+  }
   Status va_reserve(size_t bytes, void** va, void* want) override {
     HIPCHK(hipMemAddressReserve(va, bytes, kBlockSize, want, 0));
     if (want && *va != want) {  // the address is only a hint to the driver
@@ -269,7 +286,7 @@ class HipBackend : public Backend {
     HIPCHK(hipMemSetAccess(va, bytes, &ad, 1));
     std::lock_guard<std::mutex> g(reg_m_);
     vmm_maps_[(uint64_t)va] = {bytes, dev};
-    handle_home_.emplace(h, (uint64_t)va);  // where ROCr can look the handle up (rocr_handle)
+    handle_home_.insert_or_assign(h, (uint64_t)va);  // where ROCr can look the handle up (rocr_handle)
     return Status::OK;
   }
   Status vmm_unmap(void* va, size_t bytes) override {

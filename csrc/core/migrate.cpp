@@ -138,6 +138,7 @@ void Runtime::touch_residency(Block* b, Residency* r, bool prefetched) {
 // Next-use hint of a whole range (the transparent mode's op trace): stored on
 // the range for chunks it gets later, and set on the HBM chunks it holds now.
 void Runtime::hint_next_use(Range* r, uint64_t when) {
+  when = classify_hint(r, when);
   r->next_use.store(when);
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   for (auto& bp : r->blocks) {
@@ -146,6 +147,41 @@ void Runtime::hint_next_use(Range* r, uint64_t when) {
     for (auto& x : b->res)
       if (x.loc.is_gpu() && x.chunk >= 0) x.arena->set_next_use((uint32_t)x.chunk, when);
   }
+}
+
+void Runtime::reset_op_clock(int dev) {
+  if (ChunkArena* a = arena_for(Loc::gpu(dev))) a->reset_op_clock();
+  if (is_local(dev)) devs_[dev]->spread.reset();
+}
+
+// The GPU whose arena a range's hints order: its stable-VA device, else its
+// preferred GPU, else the first local GPU.
+uint64_t Runtime::classify_hint(Range* r, uint64_t when) {
+  if (!config().perf_spread_enable || !when || when == kDeadUse || (when & kEvictFirst)) return when;
+  int dev = r->stable_dev;
+  if (dev < 0 && !r->blocks.empty()) {
+    Block* b0 = r->blocks[0].get();
+    std::lock_guard<OrderedMutex> g(b0->lock);
+    if (b0->policy.has_preferred && b0->policy.preferred.is_gpu()) dev = b0->policy.preferred.id;
+  }
+  if (dev < 0) {
+    for (auto& d : devs_)
+      if (d->local) {
+        dev = d->id;
+        break;
+      }
+  }
+  if (!is_local(dev)) return when;
+  ChunkArena* a = arena_for(Loc::gpu(dev));
+  if (!a) return when;
+  return when | devs_[dev]->spread.on_hint(r->id, r->size, [a] {
+           auto st = a->stats();
+           return SpreadPolicy::ArenaView{st.capacity, st.pinned};
+         });
+}
+
+SpreadPolicy::Stats Runtime::spread_stats(int dev) {
+  return is_local(dev) ? devs_[dev]->spread.stats() : SpreadPolicy::Stats{};
 }
 
 void Runtime::set_op_clock(int dev, uint64_t now) {
@@ -766,6 +802,7 @@ Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
   if (from.is_gpu()) {
     b->gpu_evictions++;
     b->gpu_evicted_at = a->evictions();
+    if (is_local(from.id)) devs_[from.id]->spread.on_evict(b->range->id);
     // Users of the stable VA's mapping of this chunk (see Block::stable_users).
     if (b->range->dev_va && b->stable_chunk.load() == (int64_t)i) {
       std::lock_guard<std::mutex> sg(stable_m_);
@@ -876,6 +913,9 @@ Status Runtime::prefetch(Range* r, uint64_t off, uint64_t len, Loc dst, Tracker*
     // acquire() finds the span in place (no relocation).
     for (uint64_t bi = off >> kBlockShift; bi <= (off + len - 1) >> kBlockShift; ++bi)
       if (r->block(bi)->user_pins) return Status::BUSY;
+    // a prefetch ahead of a known use (next-use mode): it sits in the window
+    if (VictimFloor::value() && is_local(dst.id) && config().perf_spread_enable)
+      devs_[dst.id]->spread.on_prefetch(r->id, len);
     return gpu_extent_resident(r, off, len, dst.id, {}, nullptr, out, cause);
   }
   uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;

@@ -56,6 +56,9 @@ void Ring::push_wait(const FenceRef& f) {
   // A tracking-value fence of another ring must be submitted before anything
   // waits on it (never from inside a submission: two ring locks at once).
   if (f->ring && !f->event && f->seq > f->ring->submitted_seq()) f->ring->submit();
+  // A stream ring turns this into a GPU-side wait on the DMA ring's value:
+  // that value's work must be on the engines first (issued_seq).
+  if (!dma_ && f->ring && !f->event) (void)f->ring->wait_issued(f->seq);
   Sqe w;
   w.op = SqeOp::WAIT_FENCE;
   w.wait = f;
@@ -115,6 +118,7 @@ FenceRef Ring::submit_dma_locked() {
     {
       std::lock_guard<std::mutex> g(wm_);
       work_.push_back(std::move(b));
+      queued_.fetch_add(1, std::memory_order_relaxed);
     }
     wcv_.notify_one();
   } else {
@@ -125,6 +129,7 @@ FenceRef Ring::submit_dma_locked() {
     {
       std::lock_guard<std::mutex> g(wm_);
       work_.push_back(std::move(b));
+      queued_.fetch_add(1, std::memory_order_relaxed);
     }
     wcv_.notify_one();
     RT_ERR("ring %s/%d error %s at %s", ring_kind_str(kind_), dev_, status_str(err_), err_desc_.c_str());
@@ -179,6 +184,7 @@ void Ring::worker() {
   };
   auto complete_pending = [&] {
     if (pend < 0) return;
+    set_phase(Phase::COMPLETE, pend_last);
     const uint64_t t0 = now_ns();
     fail(be_->dma_complete(pend), pend_last);
     if (kind_ == RingKind::CPU_TO_GPU) Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
@@ -196,6 +202,7 @@ void Ring::worker() {
         g.lock();
       }
       if (work_.empty() && !stop_) {
+        set_phase(Phase::IDLE, 0);
         const uint64_t t_idle = now_ns();
         wcv_.wait(g, [&] { return stop_ || !work_.empty(); });
         if (kind_ == RingKind::CPU_TO_GPU) Tools::get().inc(Counter::RingIdleNs, now_ns() - t_idle);
@@ -203,11 +210,14 @@ void Ring::worker() {
       if (work_.empty()) return;  // stop_ with nothing left
       b = std::move(work_.front());
       work_.pop_front();
+      queued_.fetch_sub(1, std::memory_order_relaxed);
     }
     if (err_ == Status::OK && config().ring_pipeline && pure_copies(b, &copies)) {
       const int slot = pend == 0 ? 1 : 0;
+      set_phase(Phase::ISSUE, b.last);
       const uint64_t t0 = now_ns();
       Status st = copies.empty() ? Status::OK : be_->dma_issue(dev_, copies.data(), copies.size(), (int)kind_, slot);
+      mark_issued(b.last);  // on the engines (or failed: published below)
       if (kind_ == RingKind::CPU_TO_GPU) {
         Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
         Tools::get().inc(Counter::RingCopyCalls, copies.size());
@@ -224,6 +234,7 @@ void Ring::worker() {
       continue;
     }
     complete_pending();
+    set_phase(Phase::ISSUE, b.last);
     Status st = err_ == Status::OK ? run_batch(b) : err_.load();
     fail(st, b.last);
     // Publish even on error (robust channel): waiters then see err_.
@@ -272,8 +283,13 @@ Status Ring::run_batch(Batch& b) {
   std::vector<DecodeDesc> decodes;
   Status st = Status::OK;
   bool kernels_pending = false;
+  bool final_flush = false;
   auto drain = [&] {
-    if (st == Status::OK && kernels_pending) st = be_->stream_sync(stream_);
+    if (st == Status::OK && kernels_pending) {
+      set_phase(Phase::STREAM_DRAIN, b.last);
+      st = be_->stream_sync(stream_);
+      set_phase(Phase::ISSUE, b.last);
+    }
     kernels_pending = false;
   };
   auto flush_decodes = [&] {
@@ -306,7 +322,15 @@ Status Ring::run_batch(Batch& b) {
       }
       if (st == Status::OK) {
         const uint64_t t_copy = now_ns();
-        st = be_->dma_copy(dev_, copies.data(), copies.size(), (int)kind_);
+        snprintf(phase_what_, sizeof(phase_what_), "engine copy: %zu descriptors, first %llu B", copies.size(),
+                 (unsigned long long)copies[0].bytes);
+        set_phase(Phase::ENGINE_ISSUE, b.last);
+        st = be_->dma_issue(dev_, copies.data(), copies.size(), (int)kind_, 0);
+        // the batch's last copies are on the engines: GPU waits may be enqueued
+        if (final_flush && st == Status::OK) mark_issued(b.last);
+        set_phase(Phase::ENGINE_WAIT, b.last);
+        if (st == Status::OK) st = be_->dma_complete(0);
+        set_phase(Phase::ISSUE, b.last);
         if (kind_ == RingKind::CPU_TO_GPU) {
           Tools::get().inc(Counter::RingCopyNs, now_ns() - t_copy);
           Tools::get().inc(Counter::RingCopyCalls, copies.size());
@@ -340,7 +364,12 @@ Status Ring::run_batch(Batch& b) {
         flush_copies();
         if (st == Status::OK && s.wait && !s.wait->done.load(std::memory_order_acquire)) {
           const uint64_t t_wait = now_ns();
+          snprintf(phase_what_, sizeof(phase_what_), "%s %s/%d seq %llu (%s:%d %s)",
+                   s.wait->event ? "event" : "ring", s.wait->ring ? ring_kind_str(s.wait->ring->kind()) : "-",
+                   s.wait->dev, (unsigned long long)s.wait->seq, s.file, s.line, s.desc.c_str());
+          set_phase(Phase::FENCE_WAIT, b.last);
           st = s.wait->wait();
+          set_phase(Phase::ISSUE, b.last);
           if (kind_ == RingKind::CPU_TO_GPU) Tools::get().inc(Counter::RingFenceWaitNs, now_ns() - t_wait);
         }
         break;
@@ -350,6 +379,8 @@ Status Ring::run_batch(Batch& b) {
         flush_decodes();
         flush_copies();
         if (st != Status::OK) break;
+        snprintf(phase_what_, sizeof(phase_what_), "kernel op %d (%s:%d %s)", (int)s.op, s.file, s.line,
+                 s.desc.c_str());
         if (s.op == SqeOp::MEMSET) {
           st = be_->memset32(dev_, s.dst, s.pattern, s.bytes, stream_);
         } else if (s.op == SqeOp::PAGE_COPY) {
@@ -365,6 +396,7 @@ Status Ring::run_batch(Batch& b) {
     }
   }
   flush_decodes();
+  if (!kernels_pending) final_flush = true;  // (with kernels queued, the drain below comes first)
   flush_copies();
   drain();
   return st;
@@ -516,6 +548,7 @@ FenceRef Ring::submit_locked() {
 // Monotonic release store of the tracking value (a waiter on seq s must never
 // see the value drop below s once it was published).
 void Ring::publish(uint64_t seq) {
+  mark_issued(seq);
   if (!sem_) return;
   uint64_t cur = __atomic_load_n(sem_, __ATOMIC_RELAXED);
   while (cur < seq && !__atomic_compare_exchange_n(sem_, &cur, seq, true, __ATOMIC_RELEASE, __ATOMIC_RELAXED)) {
@@ -532,6 +565,18 @@ Status Ring::wait_seq(uint64_t seq) {
     if (spins > (1ull << 34)) return Status::TIMEOUT;
   }
   return check_errors();
+}
+
+Status Ring::wait_issued(uint64_t seq) {
+  if (!dma_) return Status::OK;
+  if (seq > submitted_) submit();
+  uint64_t spins = 0;
+  while (issued_.load(std::memory_order_acquire) < seq) {
+    if (err_ != Status::OK) return err_;
+    if (++spins > 64) std::this_thread::yield();
+    if (spins > (1ull << 34)) return Status::TIMEOUT;
+  }
+  return Status::OK;
 }
 
 Status Ring::check_errors() {
@@ -578,6 +623,30 @@ void Ring::clear_error_for_test() {
   std::lock_guard<OrderedMutex> g(m_);
   err_ = Status::OK;
   err_desc_.clear();
+}
+
+std::string Ring::debug_state() {
+  static const char* ph[] = {"idle", "issue", "complete", "fence_wait", "stream_drain", "engine_issue", "engine_wait"};
+  char buf[512];
+  const int p = phase_.load(std::memory_order_acquire);
+  const uint64_t since = phase_ns_.load(std::memory_order_relaxed);
+  const double age_ms = since ? (now_ns() - since) / 1e6 : 0.0;
+  size_t sq = 0, infl = 0;
+  bool locked = m_.try_lock();
+  if (locked) {
+    sq = sq_.size();
+    infl = inflight_.size();
+    m_.unlock();
+  }
+  snprintf(buf, sizeof(buf),
+           "ring %s/%d%s pushed=%llu submitted=%llu issued=%llu completed=%llu sq=%s inflight=%s worker_queue=%llu "
+           "phase=%s for %.1f ms (batch up to %llu)%s%s err=%s",
+           ring_kind_str(kind_), dev_, dma_ ? " dma" : " stream", (unsigned long long)pushed_seq(),
+           (unsigned long long)submitted_.load(), (unsigned long long)issued_seq(), (unsigned long long)completed_seq(),
+           locked ? std::to_string(sq).c_str() : "?(locked)", locked ? std::to_string(infl).c_str() : "?",
+           (unsigned long long)queued_.load(), dma_ ? ph[p < 7 ? p : 0] : "-", dma_ ? age_ms : 0.0,
+           (unsigned long long)phase_seq_.load(), p >= (int)Phase::FENCE_WAIT ? ": " : "", p >= (int)Phase::FENCE_WAIT ? phase_what_ : "", status_str(err_.load()));
+  return buf;
 }
 
 std::string Ring::last_error_desc() {

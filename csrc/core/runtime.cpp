@@ -1369,6 +1369,38 @@ Status Runtime::check_health(int dev, bool force) {
   return global_status();
 }
 
+std::string Runtime::debug_dump(size_t max_leases) {
+  std::string out;
+  char buf[320];
+  snprintf(buf, sizeof(buf), "[ogkm-dump] pid %d status %s%s%s\n", (int)getpid(), status_str(global_status()),
+           global_status() == Status::OK ? "" : ": ", fatal_reason());
+  out += buf;
+  for (auto& d : devs_) {
+    if (!d->local) continue;
+    for (int k = 0; k < (int)RingKind::COUNT; ++k)
+      if (d->rings[k]) out += "[ogkm-dump]   " + d->rings[k]->debug_state() + "\n";
+  }
+  if (leases_m_.try_lock()) {
+    std::vector<const Lease*> ls;
+    for (auto& kv : leases_) ls.push_back(kv.second.get());
+    std::sort(ls.begin(), ls.end(), [](const Lease* a, const Lease* b) { return a->id < b->id; });
+    snprintf(buf, sizeof(buf), "[ogkm-dump]   leases outstanding: %zu\n", ls.size());
+    out += buf;
+    for (size_t i = 0; i < ls.size() && i < max_leases; ++i) {
+      const Lease* l = ls[i];
+      snprintf(buf, sizeof(buf), "[ogkm-dump]     lease %llu range %llu '%s' [%llu, +%llu) proc %d %s chunks %zu ready_fences %zu\n",
+               (unsigned long long)l->id, (unsigned long long)(l->range ? l->range->id : 0),
+               l->range ? l->range->name.c_str() : "?", (unsigned long long)l->offset, (unsigned long long)l->bytes,
+               l->proc, l->remote ? "remote" : "local", l->pinned_chunks.size(), l->ready.size());
+      out += buf;
+    }
+    leases_m_.unlock();
+  } else {
+    out += "[ogkm-dump]   leases: (lease table locked by another thread)\n";
+  }
+  return out;
+}
+
 Status Runtime::sync_all() {
   Status st = Status::OK;
   for (auto& d : devs_)

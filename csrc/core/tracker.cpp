@@ -115,7 +115,10 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
       // Tracking-value fence: make sure the ring work is submitted, then let
       // the stream wait for the ring's semaphore GPU-side.
       if (f->seq > f->ring->submitted_seq()) f->ring->submit();
-      s = be->wait_value(stream, f->ring->semaphore(), f->seq);
+      // ... and issued to the engines, so no copy of it can queue behind work
+      // enqueued after this wait (Ring::issued_seq)
+      s = f->ring->wait_issued(f->seq);
+      if (s == Status::OK) s = be->wait_value(stream, f->ring->semaphore(), f->seq);
     }
     else s = f->wait();
     uint64_t dt = now_ns() - t0;

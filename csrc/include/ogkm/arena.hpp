@@ -137,6 +137,10 @@ class ChunkArena {
   // VictimFloor (a prefetch must not evict data needed before its own).
   void set_next_use(uint32_t i, uint64_t when);
   void set_op_clock(uint64_t now);
+  // A new hint producer (another ogkm.managed() context, a new model) restarts
+  // its op clock at 0: forget the old clock, every chunk's hint and the victim
+  // cache, so the new hints are not read as lying in the past.
+  void reset_op_clock();
   bool next_use_mode() {
     std::lock_guard<OrderedMutex> g(m_);
     return hinted_;
@@ -193,6 +197,7 @@ class ChunkArena {
   size_t vcache_pos_ = 0;
   uint64_t vcache_clock_ = 0;
   bool vcache_valid_ = false;
+  std::vector<uint32_t> vrisen_;  // chunks re-hinted since the cache was built (set_next_use)
   void lru_remove(uint32_t i);
   void lru_push_tail(uint32_t i, uint8_t list);
   void take_run(uint32_t first, uint32_t n);  // remove [first,first+n) from free runs

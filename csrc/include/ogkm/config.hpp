@@ -57,6 +57,10 @@ namespace ogkm {
   X(stable_batch_blocks, 32, "stable-VA placement: 2 MB blocks per eviction / fill / remap group (pipelined)") \
   X(arena_reuse_cooldown, 0, "next-use eviction: data used within this many op-clock steps is kept (its readers may still be queued)") \
   X(arena_dead_cooldown, 0, "next-use eviction: freed data used within this many op-clock steps ranks as just used, not as the first victim") \
+  X(perf_spread_enable, 1, "next-use eviction: the runtime splits cyclically hinted data into a keep class (error-diffused over the use order, sized to the arena) and a stream class evicted first (ogkm/spread.hpp); hints that carry their own class flag are left alone") \
+  X(perf_spread_keep_pct, 97, "spread classes: percent of the HBM arena's unpinned capacity the keep class may fill") \
+  X(perf_spread_adapt, 1, "spread classes: a pass that evicted keep-class data shrinks the keep class (online, from refaults)") \
+  X(perf_spread_step_pct, 2, "spread classes: keep-share reduction per adaptation (percent)") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
   X(ring_pipeline, 1, "DMA ring workers issue the next batch of plain copies before the previous one completed (two completion slots)") \
   X(vmm_rocr_remap, 1, "stable-VA remaps through ROCr hsa_amd_vmem_* (HIP keeps a placeholder mapping of the VA); 0 = hipMemMap / hipMemUnmap") \

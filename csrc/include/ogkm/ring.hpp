@@ -98,6 +98,15 @@ class Ring {
   uint64_t submitted_seq() const { return submitted_; }
   uint64_t pushed_seq() const { return next_seq_ - 1; }
   Status wait_seq(uint64_t seq);
+  // DMA rings: highest tracking value whose work has been handed to the copy
+  // engines / streams (every batch up to it issued; it may still be running).
+  // A GPU-side wait on a DMA ring's value is enqueued only once that value is
+  // issued (wait_issued): otherwise a queue waiting on it could sit ahead of
+  // HIP's own engine copies (torch / gloo D2H on a stream behind the wait) and
+  // the worker's later copies would queue behind those - a cycle through the
+  // shared SDMA engine (the round-4 2-rank peer-shard hang, gpurun_out/r5).
+  uint64_t issued_seq() const { return dma_ ? issued_.load(std::memory_order_acquire) : submitted_.load(); }
+  Status wait_issued(uint64_t seq);
   size_t reap(Cqe* out, size_t max);
   // Post-completion error check (uvm_channel.c:2047-2112 channel error
   // detection): a copy or kernel that failed AFTER submission - a faulting
@@ -113,6 +122,11 @@ class Ring {
   std::string last_error_desc();
   bool is_dma() const { return dma_; }
   uint64_t* semaphore() const { return sem_; }
+  // Hang diagnostics (Runtime::debug_dump): sequence numbers, queued worker
+  // batches and what the DMA worker is doing right now, and for how long.
+  // Lock-free or try-lock only: safe to call while another thread is stuck.
+  std::string debug_state();
+  enum class Phase : int { IDLE = 0, ISSUE, COMPLETE, FENCE_WAIT, STREAM_DRAIN, ENGINE_ISSUE, ENGINE_WAIT };
 
  private:
   struct Batch {
@@ -148,6 +162,22 @@ class Ring {
   std::condition_variable wcv_;
   std::deque<Batch> work_;
   bool stop_ = false;
+  std::atomic<int> phase_{0};             // Phase of the worker
+  std::atomic<uint64_t> phase_ns_{0};     // when it entered it
+  std::atomic<uint64_t> phase_seq_{0};    // the batch (last seq) it works on
+  std::atomic<uint64_t> queued_{0};       // batches handed to the worker, not yet taken
+  std::atomic<uint64_t> issued_{0};       // see issued_seq()
+  void mark_issued(uint64_t seq) {
+    uint64_t cur = issued_.load(std::memory_order_relaxed);
+    while (cur < seq && !issued_.compare_exchange_weak(cur, seq, std::memory_order_release)) {
+    }
+  }
+  char phase_what_[128] = {0};            // the fence / kernel it waits for (worker writes; the dump reads racily)
+  void set_phase(Phase p, uint64_t seq) {
+    phase_ns_.store(now_ns(), std::memory_order_relaxed);
+    phase_seq_.store(seq, std::memory_order_relaxed);
+    phase_.store((int)p, std::memory_order_release);
+  }
 };
 
 }  // namespace ogkm

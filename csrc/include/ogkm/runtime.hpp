@@ -23,6 +23,7 @@
 #include "ogkm/events.hpp"
 #include "ogkm/fault_abi.hpp"
 #include "ogkm/ring.hpp"
+#include "ogkm/spread.hpp"
 #include "ogkm/tracker.hpp"
 #include "ogkm/va_space.hpp"
 
@@ -115,6 +116,7 @@ struct Device {
   DeviceFaultBuffer fault_buf;
   // RAS counters at init (the baseline) and the last check: an uncorrectable
   // error past the baseline makes the runtime FATAL (uvm_gpu.c:1328-1354).
+  SpreadPolicy spread;  // keep / stream classes of cyclically hinted data (ogkm/spread.hpp)
   Backend::Health health0, health;
   bool health_ok = false;           // the platform reports RAS counters
   std::string health_reason;        // why they are unreadable (empty when readable)
@@ -218,6 +220,12 @@ class Runtime {
   // current op clock of a device's HBM arena (see ChunkArena::set_next_use).
   void hint_next_use(Range* r, uint64_t when);
   void set_op_clock(int dev, uint64_t now);
+  void reset_op_clock(int dev);
+  // The spread class flag (0 / kEvictFirst) the runtime gives a hint of r that
+  // carries none (config perf_spread_enable; SpreadPolicy).
+  uint64_t classify_hint(Range* r, uint64_t when);
+  SpreadPolicy::Stats spread_stats(int dev);
+  int spread_class(int dev, uint64_t range_id) { return is_local(dev) ? devs_[dev]->spread.range_class(range_id) : -1; }
   // Mark r's contents dead (free: no copy-out, off-GPU copies dropped) or live.
   void set_dead(Range* r, bool dead);
   Lease* lease_by_id(uint64_t id);
@@ -249,6 +257,11 @@ class Runtime {
   // Bytes of [off, off + len) resident at `loc` (page granular; one block lock at a time).
   uint64_t resident_bytes(Range* r, Loc loc, uint64_t off = 0, uint64_t len = ~0ull);
   Status sync_all();
+  // Hang diagnostics: every local ring's sequence numbers and worker phase,
+  // the outstanding leases (oldest first), the fatal status. Try-locks only, so
+  // it can run from a watchdog / signal thread while another thread is stuck
+  // inside the runtime (the push description dump of uvm_channel.c:2090-2100).
+  std::string debug_dump(size_t max_leases = 24);
 
   // ---- CXL (fork capability)
   Status cxl_dma(uint64_t handle, uint64_t gpu_ptr, int dev, uint64_t cxl_off, uint64_t size, int dir, bool async,

@@ -171,6 +171,10 @@ PYBIND11_MODULE(_ogkm, m) {
   m.def("set_fatal", [](const std::string& why) { set_fatal(Status::FATAL, why.c_str()); });
   m.def("fatal_reason", [] { return std::string(fatal_reason()); });
   m.def("init_device", [](int d, uint64_t budget) { check(rt()->init_device(d, budget), "init_device"); });
+  m.def("debug_dump", [](size_t max_leases) {
+    Runtime* rt = Runtime::get();
+    return rt ? rt->debug_dump(max_leases) : std::string("[ogkm-dump] runtime not initialised\n");
+  }, py::arg("max_leases") = 24, py::call_guard<py::gil_scoped_release>());
   m.def("sync_all", [] {
     py::gil_scoped_release nogil;
     check(rt()->sync_all(), "sync_all");
@@ -267,7 +271,24 @@ PYBIND11_MODULE(_ogkm, m) {
     return rt()->resident_bytes(r, make_loc(tier, loc), off, len);
   }, py::arg("id"), py::arg("tier"), py::arg("loc"), py::arg("off") = 0, py::arg("len") = ~0ull);
   m.def("hint_next_use", [](uint64_t id, uint64_t when) { rt()->hint_next_use(range(id), when); });
+  m.def("spread_class", [](int dev, uint64_t id) { return rt()->spread_class(dev, id); });
+  m.def("spread_stats", [](int dev) {
+    auto st = rt()->spread_stats(dev);
+    py::dict d;
+    d["ready"] = st.ready;
+    d["ranges"] = st.ranges;
+    d["cycle_bytes"] = st.cycle_bytes;
+    d["keep_ranges"] = st.keep_ranges;
+    d["keep_bytes"] = st.keep_bytes;
+    d["passes"] = st.passes;
+    d["keep_evictions"] = st.keep_evictions;
+    d["adaptations"] = st.adaptations;
+    d["keep_fraction"] = st.keep_fraction;
+    d["window_reserve"] = st.window_reserve;
+    return d;
+  });
   m.def("set_op_clock", [](int dev, uint64_t now) { rt()->set_op_clock(dev, now); });
+  m.def("reset_op_clock", [](int dev) { rt()->reset_op_clock(dev); });
   m.def("migrate", [](uint64_t id, uint64_t off, uint64_t len, int tier, int loc) {
     Range* r = range(id);
     py::gil_scoped_release nogil;

@@ -19,7 +19,7 @@ Layout
   ops/         HIP kernel entry points (copies, managed gather) + decode ops
   models/      Llama-3 decode engine with tiered (oversubscribed) weights
   parallel/    RCCL comm, tensor parallel, peer-shard weights, topology
-  utils/       logging, timing, env helpers
+  diag         hang diagnostics: SIGUSR1 / watchdog dumps of every thread's stack + the runtime's rings and leases
 """
 from __future__ import annotations
 
@@ -28,7 +28,7 @@ import sys as _sys
 __version__ = "0.1.0"
 
 from . import _native  # noqa: E402,F401  (fails loudly if the native core is missing)
-from . import rt, tools, checkpoint, cxl, allocator, p2p  # noqa: E402,F401
+from . import rt, tools, checkpoint, cxl, allocator, p2p, diag  # noqa: E402,F401
 from .managed import managed  # noqa: E402,F401
 from . import ops, parallel, models  # noqa: E402,F401
 

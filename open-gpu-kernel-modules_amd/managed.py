@@ -65,10 +65,17 @@ def _mode_class():
         return _raw(device) if _raw is not None else torch.cuda.current_stream(device).cuda_stream
 
     def _writes_of(func) -> tuple[frozenset, frozenset]:
-        """(positional indices, kwarg names) of the arguments the op writes."""
+        """(positional indices, kwarg names) of the arguments the op writes.
+        aten / prims schemas declare every mutation; an op from any other
+        namespace (a custom op registered without ``mutates_args``, an
+        extension kernel that writes an input) is not trusted: all its tensor
+        arguments count as written, so the pages it covers revoke their other
+        copies - otherwise a read-mostly host duplicate would stay valid and an
+        eviction would drop the GPU write."""
         pos, names = set(), set()
+        trusted = getattr(func, "namespace", "aten") in ("aten", "prims")
         for i, a in enumerate(func._schema.arguments):
-            if a.alias_info is not None and a.alias_info.is_write:
+            if (a.alias_info is not None and a.alias_info.is_write) or not trusted:
                 pos.add(i)
                 names.add(a.name)
         return frozenset(pos), frozenset(names)
@@ -87,6 +94,10 @@ def _mode_class():
             if lookahead_bytes is None:
                 lookahead_bytes = _arena_capacity(self.device) // 8
             self.lookahead_bytes = int(lookahead_bytes)
+            # this mode's op clock starts at 0: drop the arena's clock and the
+            # hints a previous producer (another managed() context) left behind
+            if lib.is_initialized():
+                lib.reset_op_clock(self.device)
             self._writes: dict = {}
             self._sizes: dict[int, int] = {}
             self._trace: list[tuple[int, ...]] = []   # operand sets of the recorded pass
@@ -335,7 +346,7 @@ _METADATA_OPS: frozenset = frozenset()
 _NOT_SPLIT = object()
 _EVICT_FIRST = 1 << 61  # kEvictFirst (csrc/include/ogkm/arena.hpp)
 # off by default: measured slower on the stock 70B (36.4 vs 38.9 tok/s, 89.7 vs 81.8 GB/step
-# H2D - the activations share the arena, so the stream class thrashes; tools/gpu_r4_sp.sh)
+# H2D - the activations share the arena, so the stream class thrashes; tools/sessions/gpu_r4_sp.sh)
 _SPREAD = __import__("os").environ.get("OGKM_MANAGED_SPREAD", "0") != "0"
 _SPREAD_KEEP = float(__import__("os").environ.get("OGKM_MANAGED_SPREAD_KEEP", "0.85"))
 _MAX_RUNS = 16384  # contiguous runs enumerated per written view (beyond: its bounding extent)

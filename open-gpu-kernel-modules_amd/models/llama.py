@@ -588,6 +588,8 @@ class TieredLlama:
                          and bool(self.stream_seq) and self.sworld <= 1)
         self._seq_pos = {k: j for j, k in enumerate(self.stream_seq)}
         self._pass, self._last_pos = 0, -1
+        if self.next_use and not self.dry_run:
+            lib.reset_op_clock(self.dev)  # our clock restarts at 0 (a previous model's hints are stale)
         # Spread classes (see _hint_used): the "keep" share of the units is the
         # share of their bytes the arena can hold (less 3 %), spread over the
         # use order unit by unit (error diffusion), like the static plan's

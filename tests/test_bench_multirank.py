@@ -167,10 +167,27 @@ def test_bench_launcher_child_failure_stops_job():
     assert dt < 200
 
 
-def test_bench_launcher_timeout_kills_hung_rank():
-    r, dt = _launch({"OGKM_BENCH_HANG_RANK": "2"}, ["--launch-timeout", "20"], timeout=300)
-    assert r.returncode == 124 and "killing all 4" in r.stderr, r.stderr[-3000:]
-    assert dt < 120
+@pytest.mark.parametrize("where", ["init", "step"])
+def test_bench_launcher_timeout_kills_hung_rank(where):
+    """A rank that stops making progress: on the launch timeout the launcher
+    SIGUSR1s every rank - each prints all its threads' Python stacks and the
+    runtime's rings / leases (ogkm.diag) - then kills the job (exit 124)."""
+    timeout = "20" if where == "init" else "60"
+    args = ["--launch-timeout", timeout] + (["--warmup", "2"] if where == "step" else [])
+    r, dt = _launch({"OGKM_BENCH_HANG_RANK": "2", "OGKM_BENCH_HANG_AT": where, "OGKM_HANG_DUMP_WAIT_S": "5"},
+                    args, timeout=300)
+    err = r.stderr
+    assert r.returncode == 124 and "killing all 4" in err, err[-3000:]
+    assert dt < 180
+    # every rank dumped; the hung one shows where it sleeps
+    for rank in range(4):
+        assert f"[ogkm-hang] rank {rank} pid" in err, err[-5000:]
+    assert err.count("[ogkm-hang]") >= 8  # a header and an end line per rank
+    assert "time.sleep" in err or "in main" in err, err[-5000:]
+    assert "[ogkm-dump]" in err
+    if where == "step":
+        # the runtime is up on the hung rank: its rings and leases are listed
+        assert "ring cpu_to_gpu/" in err and "leases outstanding" in err, err[-5000:]
 
 
 @pytest.mark.parametrize("ws,gpus", [("2", "4"), ("4", "1"), ("1", "2")])

@@ -93,3 +93,46 @@ def test_allocation_failure_is_a_python_error():
     assert "CAUGHT RuntimeError True True" in r.stdout or "CAUGHT MemoryError True True" in r.stdout, \
         r.stdout + r.stderr[-2000:]
     assert f"AFTER {4 << 20} True" in r.stdout, r.stdout
+
+
+UNDECLARED_WRITE_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, os.environ["OGKM_ROOT"])
+import torch
+import ogkm
+from ogkm import allocator, rt
+from ogkm._native import lib
+allocator.enable(managed_min_mb=1)
+rt.init("hip", hbm_budget={0: 256 << 20})
+# an extension op whose schema declares no mutation but writes its input
+L = torch.library.Library("ogkm_test", "DEF")
+L.define("scribble(Tensor x) -> Tensor")
+def _scribble(x):
+    x.fill_(3)
+    return x.sum(dtype=torch.int64).reshape(1)
+L.impl("scribble", _scribble, "CUDA")
+a = torch.ones(64 << 20, dtype=torch.uint8, device="cuda")
+allocator.set_read_mostly(a)
+with ogkm.managed():
+    s0 = int(a.sum(dtype=torch.int64).item())          # read: host duplicate kept (read-mostly)
+    s1 = int(torch.ops.ogkm_test.scribble(a).item())   # undeclared write
+    big = [torch.full((64 << 20,), i, dtype=torch.uint8, device="cuda") for i in range(8)]  # 512 MB: a is evicted
+    for b in big:
+        b.add_(1)
+    torch.cuda.synchronize()
+    ev = lib.stats()["evictions"]
+    s2 = int(a.sum(dtype=torch.int64).item())          # faulted back in: the write must have been kept
+print("RESULT", s0, s1, s2, ev > 0)
+"""
+
+
+def test_undeclared_write_by_extension_op_survives_eviction():
+    """A custom op registered without a mutation annotation writes a
+    read-mostly managed tensor: the transparent mode treats operands of ops
+    outside aten / prims as written, so the host duplicate is revoked and the
+    eviction copies the GPU data out instead of dropping it."""
+    r = subprocess.run([sys.executable, "-c", UNDECLARED_WRITE_SCRIPT], capture_output=True, text=True, timeout=150,
+                       env=dict(os.environ, OGKM_ROOT=os.path.dirname(HERE), HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    n = 64 << 20
+    assert f"RESULT {n} {3 * n} {3 * n} True" in r.stdout, r.stdout + r.stderr[-2000:]
