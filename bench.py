@@ -350,7 +350,8 @@ def run_torch_managed(a) -> None:
                 "trace_len": len(mode._trace), "hinted_ops": mode.hinted_ops, "trace_misses": mode.trace_misses,
                 "allocs_per_step": (al1["allocs"] - al0["allocs"]) // max(1, a.steps), "alloc_peak_gb":
                 round(al1["peak"] / 1e9, 2), "managed_min_mb": int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")),
-                "lookahead_mb": la},
+                "lookahead_mb": la,
+                "spread": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in lib.spread_stats(0).items()}},
     }
     print(json.dumps(out), flush=True)
 
@@ -519,10 +520,7 @@ def main() -> None:
     comm.barrier()
     t_init = time.perf_counter()
     sim = a.simulate_tp > 1 and world == 1
-    # Peer shards stream every unit through the all-gather pipeline, which the
-    # runtime-decided residency does not drive (it hung on the 2-rank GPU run):
-    # shards keep the static plan.
-    planner = os.environ.get("OGKM_SHARDS_PLANNER", "static") if a.parallel == "shards" and world > 1 else a.planner
+    planner = a.planner
     model = llama.TieredLlama(cfg, batch=a.batch, context=a.context, max_new_tokens=a.warmup + a.steps + 3,
                               oversub=a.oversub, device=dev, tp_rank=e.rank, tp_world=a.simulate_tp if sim else world,
                               seed=1234, lookahead=a.lookahead, verbose=a.verbose, packed=not a.no_packed,
@@ -659,6 +657,8 @@ def main() -> None:
                 "evictions": s["evictions"],
                 "ring_per_step": _ring_per_step(s, a.steps),
                 "stream_stats_per_step": {k: round(v / a.steps, 1) for k, v in model.sstats.items()},
+                # the runtime's keep / stream classes (planner off; csrc/core/spread.cpp)
+                "spread": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in lib.spread_stats(dev).items()},
                 "init_s": round(init_s, 1),
             },
         }

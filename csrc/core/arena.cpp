@@ -1,5 +1,6 @@
 // ChunkArena / HbmArena / HostArena implementation.
 #include "ogkm/arena.hpp"
+#include "ogkm/ledger.hpp"
 
 #include <fcntl.h>
 #include <numaif.h>
@@ -278,12 +279,23 @@ uint64_t& VictimFloor::value() {
 void ChunkArena::set_next_use(uint32_t i, uint64_t when) {
   std::lock_guard<OrderedMutex> g(m_);
   if (i >= nchunks_ || chunks_[i].state != ChunkState::ALLOCATED) return;
+  const bool track = vcache_valid_ && hinted_ && config().arena_victim_rerank;
+  const uint64_t before = track ? victim_key_locked(chunks_[i]) : 0;
   chunks_[i].next_use = when;
   if (when && when != kDeadUse) hinted_ = true;
-  // A new hint can raise the chunk's rank past where the victim cache has it
-  // (data just used gets a far next use, or the evict-first class): remember
-  // it, next_victims_locked ranks these ahead of the cache's stale order.
-  if (vcache_valid_) vrisen_.push_back(i);
+  // A new hint that raises the chunk's rank (data just used gets a far next
+  // use, or the evict-first class) puts it past where the victim cache has
+  // it: remember it, next_victims_locked ranks these ahead of the cache's
+  // stale order. (Many at once - a whole op trace re-hinting - rebuild the
+  // cache instead of sorting a long list on every victim query.)
+  if (track && victim_key_locked(chunks_[i]) > before) {
+    if (vrisen_.size() >= 256) {
+      vcache_valid_ = false;
+      vrisen_.clear();
+    } else {
+      vrisen_.push_back(i);
+    }
+  }
 }
 
 void ChunkArena::set_op_clock(uint64_t now) {
@@ -882,16 +894,19 @@ HostArena::HostArena(Backend* be, Tier tier, int node, uint64_t capacity)
     numa_bound_ = mbind(view_, bytes_, MPOL_BIND, &mask, 64, 0) == 0;
     if (!numa_bound_) RT_DBG("mbind to node %d failed (errno %d); pages use the default policy", node, errno);
   }
-  seg_registered_.assign((bytes_ + kHostSegment - 1) / kHostSegment, 0);
+  if (config().host_segment_mb > 0) seg_ = std::max<uint64_t>(kBlockSize, (uint64_t)config().host_segment_mb << 20) / kBlockSize * kBlockSize;
+  seg_registered_.assign((bytes_ + seg_ - 1) / seg_, 0);
   init_chunks((uint64_t)view_, n);
 }
 
 HostArena::~HostArena() {
   if (view_) {
     for (size_t s = 0; s < seg_registered_.size(); ++s)
-      if (seg_registered_[s]) be_->host_unregister((char*)view_ + s * kHostSegment);
+      if (seg_registered_[s]) be_->host_unregister((char*)view_ + s * seg_);
     munmap(view_, bytes_);
   }
+  NodeLedger& L = NodeLedger::get();
+  if (ledger_bytes_ && L.epoch() == ledger_epoch_) L.release(node_, ledger_bytes_);
   if (fd_ >= 0) close(fd_);
 }
 
@@ -899,16 +914,33 @@ Status HostArena::ensure_registered(uint32_t first, uint32_t n) {
   if (!view_) return Status::NO_MEMORY;
   uint64_t lo = (uint64_t)first << kBlockShift, hi = ((uint64_t)(first + n) << kBlockShift);
   std::lock_guard<std::mutex> g(seg_m_);
-  for (uint64_t s = lo / kHostSegment; s * kHostSegment < hi; ++s) {
+  NodeLedger& L = NodeLedger::get();
+  for (uint64_t s = lo / seg_; s * seg_ < hi; ++s) {
     if (seg_registered_[s]) continue;
-    char* p = (char*)view_ + s * kHostSegment;
-    uint64_t len = std::min<uint64_t>(kHostSegment, bytes_ - s * kHostSegment);
+    char* p = (char*)view_ + s * seg_;
+    uint64_t len = std::min<uint64_t>(seg_, bytes_ - s * seg_);
+    // Node-wide budget first (every rank process on this node shares it): a
+    // segment the node cannot back is refused here, before it is touched.
+    if (!L.reserve(node_, len)) {
+      ledger_refused() = true;
+      Tools::get().inc(Counter::LedgerRefusals);
+      RT_WARN("%s: node %d budget exhausted across processes (ledger %s: %llu of %llu MB reserved)", name_.c_str(),
+              node_, L.path().c_str(), (unsigned long long)(L.view(node_).reserved >> 20),
+              (unsigned long long)(L.view(node_).capacity >> 20));
+      return Status::NO_MEMORY;
+    }
+    if (ledger_bytes_ && ledger_epoch_ != L.epoch()) ledger_bytes_ = 0;  // (reserved under an old attachment)
+    ledger_epoch_ = L.epoch();
     // Populate first (fault in on the bound node), then pin for device DMA.
     if (madvise(p, len, MADV_POPULATE_WRITE) != 0) {
       for (uint64_t o = 0; o < len; o += kPageSize) ((volatile char*)p)[o] = 0;
     }
     Status st = be_->host_register(p, len);
-    if (st != Status::OK) return st;
+    if (st != Status::OK) {
+      L.release(node_, len);
+      return st;
+    }
+    ledger_bytes_ += len;
     seg_registered_[s] = 1;
   }
   return Status::OK;

@@ -151,7 +151,9 @@ const char* counter_name(Counter c) {
                             "ring_fence_wait_ns",
                             "ring_copy_ns",
                             "ring_idle_ns",
-                            "ring_copy_calls"};
+                            "ring_copy_calls",
+                            "demotion_fallbacks",
+                            "ledger_refusals"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -26,6 +26,7 @@
 
 #include "ogkm/codec.hpp"
 #include "ogkm/runtime.hpp"
+#include "ogkm/ledger.hpp"
 
 namespace ogkm {
 
@@ -46,6 +47,25 @@ Counter xfer_counter(const Loc& s, const Loc& d) {
 }  // namespace
 
 // ------------------------------------------------------------------ helpers
+// Where evicted data goes when `full` cannot take it: the tier below it, then
+// host memory of the other NUMA nodes this process knows (its GPUs' nodes and
+// its host node), nearest node first.
+std::vector<Loc> Runtime::fallback_targets(const Loc& full) {
+  std::vector<Loc> out;
+  if (full.tier == Tier::HOST) {
+    Loc d = demotion_target(full);
+    if (d.id >= 0) out.push_back(d);
+  }
+  std::vector<int> nodes{host_node_};
+  for (auto& d : devs_) nodes.push_back(d->numa);
+  std::sort(nodes.begin(), nodes.end());
+  nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+  std::sort(nodes.begin(), nodes.end(), [&](int a, int b) { return std::abs(a - full.id) < std::abs(b - full.id); });
+  for (int n : nodes)
+    if (!(full.tier == Tier::HOST && n == full.id) && n >= 0) out.push_back(Loc::host(n));
+  return out;
+}
+
 Loc Runtime::demotion_target(const Loc& from) {
   if (from.is_gpu()) {
     // Evicted HBM data goes to host DRAM; a CXL preferred location is honoured
@@ -267,7 +287,27 @@ Status Runtime::populate(Ctx& c, Block* b, Loc dst, int64_t hint, Residency** ou
   ChunkArena* a = arena_for(dst);
   if (!a) return Status::INVALID_ARGUMENT;
   uint32_t chunk = 0;
+  ledger_refused() = false;
   Status st = alloc_chunks(a, 1, hint, &chunk, b);
+  if (st == Status::NO_MEMORY && !dst.is_gpu() && ledger_refused()) {
+    // The node's budget is spent by the ranks that share it (NodeLedger), not
+    // by this arena: evicting our own data would not make room. The data rests
+    // on the next tier / node instead (nearest first).
+    for (const Loc& alt : fallback_targets(dst)) {
+      if (Residency* x = b->find(alt)) {
+        *out = x;
+        return Status::OK;
+      }
+      ChunkArena* a2 = arena_for(alt);
+      if (a2 && alloc_chunks(a2, 1, -1, &chunk, b) == Status::OK) {
+        Tools::get().inc(Counter::DemotionFallbacks);
+        dst = alt;
+        a = a2;
+        st = Status::OK;
+        break;
+      }
+    }
+  }
   if (st == Status::NO_MEMORY) {
     c.need_arena = a;
     c.need_n = 1;

@@ -568,7 +568,7 @@ Status Ring::wait_seq(uint64_t seq) {
 }
 
 Status Ring::wait_issued(uint64_t seq) {
-  if (!dma_) return Status::OK;
+  if (!dma_ || !config().ring_wait_issued) return Status::OK;
   if (seq > submitted_) submit();
   uint64_t spins = 0;
   while (issued_.load(std::memory_order_acquire) < seq) {

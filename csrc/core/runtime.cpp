@@ -2,6 +2,7 @@
 // CPU/stable-VA mapping maintenance, CXL DMA, quiesce/resume and the
 // residency-map checkpoint format.
 #include "ogkm/runtime.hpp"
+#include "ogkm/ledger.hpp"
 #include "ogkm/codec.hpp"
 
 #include <sys/mman.h>
@@ -128,7 +129,8 @@ Runtime::~Runtime() {
     d->hbm_live.store(nullptr);
     d->hbm.reset();
   }
-  host_arenas_.clear();
+  host_arenas_.clear();  // (each arena returns its ledger reservations)
+  NodeLedger::get().detach();
 }
 
 // ------------------------------------------------------------------ tiers
@@ -247,8 +249,10 @@ HostArena* Runtime::host_arena(Tier t, int node) {
   size_t idx = (size_t)(t == Tier::CXL ? 1 : 0) * kMaxNodes + node;
   if (host_arenas_.size() <= idx) host_arenas_.resize(2 * kMaxNodes);
   if (!host_arenas_[idx]) {
-    uint64_t cap = config().host_budget_mb ? (uint64_t)config().host_budget_mb << 20
-                                           : system_ram_bytes() / 100 * (uint64_t)config().cxl_pin_budget_pct;
+    // This process's view of the node: at most the node's budget (its memory,
+    // not the machine's); the node-wide ledger splits it between processes.
+    uint64_t cap = config().host_budget_mb ? (uint64_t)config().host_budget_mb << 20 : node_budget_bytes(node);
+    (void)NodeLedger::get().attach();
     auto a = std::make_unique<HostArena>(be_.get(), t, node, cap);
     if (a->init_status() != Status::OK) return nullptr;
     host_arenas_[idx] = std::move(a);
@@ -1041,6 +1045,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
         if (src_dev < 0 && dst.is_gpu()) stage = cpu_loc();  // pageable host source: stage on host
         Residency* to = nullptr;
         st = populate(c, b, stage, -1, &to);
+        if (st == Status::OK) stage = to->loc;  // (a full node's data rests on the next one: populate)
         if (st == Status::OK) {
           // Old data only for partially covered pages.
           PageMask partial = pages.andnot(full);

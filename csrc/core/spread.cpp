@@ -66,9 +66,10 @@ uint64_t SpreadPolicy::on_hint(uint64_t id, uint64_t bytes, const std::function<
     // The first range of the cycle again: one pass done. Keep-class data
     // evicted during it means the keep class does not fit: shrink it.
     ++passes_;
-    if (!ready_) {  // the first pass was the discovery: its evictions predate the classes
+    if (!ready_) {  // the first pass was the discovery: the whole cycle is known now
       ready_ = true;
       pass_keep_evictions_ = 0;
+      assign_locked(view);  // exact cycle bytes (the interim assignments saw part of it)
     }
     const uint64_t keep_n = std::count_if(ranges_.begin(), ranges_.end(),
                                           [](const auto& kv) { return kv.second.cls == 0; });
@@ -78,6 +79,7 @@ uint64_t SpreadPolicy::on_hint(uint64_t id, uint64_t bytes, const std::function<
       ++adaptations_;
       assign_locked(view);
     }
+    last_pass_keep_evictions_ = pass_keep_evictions_;
     pass_keep_evictions_ = 0;
     for (auto p = pending_.begin(); p != pending_.end();) {  // prefetched a pass ago, never used
       if (p->second.second + 1 < passes_) {
@@ -132,6 +134,7 @@ void SpreadPolicy::reset() {
   pending_.clear();
   pending_bytes_ = max_range_bytes_ = reserve_ = assigned_reserve_ = 0;
   grace_until_ = 0;
+  last_pass_keep_evictions_ = 0;
 }
 
 SpreadPolicy::Stats SpreadPolicy::stats() {
@@ -150,6 +153,7 @@ SpreadPolicy::Stats SpreadPolicy::stats() {
   s.adaptations = adaptations_;
   s.keep_fraction = f_;
   s.window_reserve = reserve_;
+  s.last_pass_keep_evictions = last_pass_keep_evictions_;
   return s;
 }
 

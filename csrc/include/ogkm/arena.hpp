@@ -238,6 +238,8 @@ class HbmArena : public ChunkArena {
   Status init_ = Status::OK;
 };
 
+constexpr uint64_t kHostSegment = 1ull << 30;  // default host_segment_mb
+
 // Host DRAM or CXL.mem of one NUMA node: a memfd mapped once (the arena view,
 // device-registered segment by segment) and bound to the node with mbind.
 // CPU views of managed ranges map the same memfd pages with MAP_FIXED, so the
@@ -254,6 +256,7 @@ class HostArena : public ChunkArena {
   Status init_status() const { return init_; }
   bool numa_bound() const { return numa_bound_; }
   bool thp_advised() const { return thp_advised_; }
+  uint64_t ledger_bytes() const { return ledger_bytes_; }
 
  private:
   Backend* be_;
@@ -261,8 +264,13 @@ class HostArena : public ChunkArena {
   int fd_ = -1;
   void* view_ = nullptr;
   uint64_t bytes_ = 0;
-  std::vector<uint8_t> seg_registered_;  // per 1 GB segment
+  std::vector<uint8_t> seg_registered_;  // per segment (host_segment_mb, default 1 GB)
+  uint64_t seg_ = kHostSegment;
   std::mutex seg_m_;
+  // Bytes reserved in the node-wide ledger (NodeLedger) for the populated
+  // segments, and the ledger attachment they were reserved under.
+  uint64_t ledger_bytes_ = 0;
+  uint64_t ledger_epoch_ = 0;
   bool numa_bound_ = false;
   bool thp_advised_ = false;
   Status init_ = Status::OK;
@@ -286,7 +294,6 @@ struct VictimFloor {
   VictimFloor& operator=(const VictimFloor&) = delete;
 };
 
-constexpr uint64_t kHostSegment = 1ull << 30;
 constexpr uint64_t kPrefetchBoost = 1ull << 40;  // recency bonus of not-yet-used prefetched chunks
 
 }  // namespace ogkm

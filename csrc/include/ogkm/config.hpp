@@ -62,6 +62,8 @@ namespace ogkm {
   X(perf_spread_adapt, 1, "spread classes: a pass that evicted keep-class data shrinks the keep class (online, from refaults)") \
   X(perf_spread_step_pct, 2, "spread classes: keep-share reduction per adaptation (percent)") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
+  X(ring_wait_issued, 1, "a GPU-side wait on a DMA ring value is enqueued only once that value's copies are on the engines (Ring::issued_seq; prevents an SDMA-engine cycle with HIP's own copies)") \
+  X(arena_victim_rerank, 1, "next-use eviction: chunks re-hinted since the victim cache was built are ranked ahead of its stale order") \
   X(ring_pipeline, 1, "DMA ring workers issue the next batch of plain copies before the previous one completed (two completion slots)") \
   X(vmm_rocr_remap, 1, "stable-VA remaps through ROCr hsa_amd_vmem_* (HIP keeps a placeholder mapping of the VA); 0 = hipMemMap / hipMemUnmap") \
   X(torch_persistent_ops, 128, "transparent mode: a managed tensor held again this many ops after its first hold is long-lived (keys the op-trace prefetcher)") \
@@ -72,7 +74,10 @@ namespace ogkm {
   X(host_node, -1, "NUMA node for the host tier (-1 = NUMA node of the first local GPU)")             \
   X(local_devices, 0, "bitmask of the GPUs this process manages (0 = all; one process per GPU: 1<<rank)") \
   X(fake_numa_nodes, 1, "fake backend: NUMA nodes the fake GPUs are spread over (GPU d on node d*n/ndev)") \
-  X(host_budget_mb, 0, "host-tier arena limit in MB (0 = pin budget)")                               \
+  X(host_budget_mb, 0, "host-tier arena limit in MB (0 = the node budget)")                          \
+  X(node_ledger, 1, "host / CXL arenas reserve their segments in a node-wide shared-memory ledger (every runtime process on the machine; OGKM_NODE_LEDGER = its path)") \
+  X(node_budget_mb, 0, "per-NUMA-node byte budget of the node ledger in MB (0 = the node's MemTotal x cxl_pin_budget_pct)") \
+  X(host_segment_mb, 1024, "host / CXL arenas populate, pin and reserve their memory in segments of this many MB") \
   /* channels / ring */                                                                              \
   X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \
   X(copy_engine, 3, "PCIe/xGMI ring copies: 3=SDMA engines driven by the ring's worker (default) 1=hipMemcpyAsync 0=our CU copy kernels") \

@@ -195,6 +195,8 @@ enum class Counter : int {
   RingCopyNs,          // H2D DMA ring workers: time in engine copies (issue + completion)
   RingIdleNs,          // H2D DMA ring workers: time with no batch to run
   RingCopyCalls,       // H2D DMA ring workers: engine copy calls (merged runs)
+  DemotionFallbacks,   // evictions demoted past a full node (node-wide budget spent) to the next tier / node
+  LedgerRefusals,      // host / CXL segments the node-wide ledger refused (budget shared by all ranks)
   NumCounters
 };
 const char* counter_name(Counter c);

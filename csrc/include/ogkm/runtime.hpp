@@ -340,6 +340,7 @@ class Runtime {
   Status alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* first, Block* owner = nullptr,
                       bool pin = false);
   Loc demotion_target(const Loc& from);
+  std::vector<Loc> fallback_targets(const Loc& full);  // when `full` refuses evicted data (node budget spent)
   void cpu_map_block(Block* b);  // refresh CPU view protections
   void stable_map_block(Block* b);
   // stable_m_ held: tear down b's stable-VA mapping after its users finished.

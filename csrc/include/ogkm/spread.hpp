@@ -56,7 +56,7 @@ class SpreadPolicy {
   struct Stats {
     bool ready = false;
     uint64_t ranges = 0, cycle_bytes = 0, keep_ranges = 0, keep_bytes = 0, passes = 0, keep_evictions = 0,
-             adaptations = 0, window_reserve = 0;
+             adaptations = 0, window_reserve = 0, last_pass_keep_evictions = 0;
     double keep_fraction = 0.0;
   };
   Stats stats();
@@ -81,7 +81,8 @@ class SpreadPolicy {
   std::unordered_map<uint64_t, std::pair<uint64_t, uint64_t>> pending_;  // prefetched, unused: id -> (bytes, pass)
   uint64_t pending_bytes_ = 0, max_range_bytes_ = 0;
   uint64_t reserve_ = 0, assigned_reserve_ = 0;
-  uint64_t grace_until_ = 0;  // no adaptation before this pass (transition after an assignment)  // peak window + largest range; at the last assignment
+  uint64_t grace_until_ = 0;
+  uint64_t last_pass_keep_evictions_ = 0;  // no adaptation before this pass (transition after an assignment)  // peak window + largest range; at the last assignment
 };
 
 }  // namespace ogkm

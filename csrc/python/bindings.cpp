@@ -14,6 +14,7 @@
 #include "ogkm/kernels.hpp"
 #include "ogkm/lock_order.hpp"
 #include "ogkm/runtime.hpp"
+#include "ogkm/ledger.hpp"
 #include "ogkm/torch_alloc.hpp"
 
 namespace py = pybind11;
@@ -271,6 +272,25 @@ PYBIND11_MODULE(_ogkm, m) {
     return rt()->resident_bytes(r, make_loc(tier, loc), off, len);
   }, py::arg("id"), py::arg("tier"), py::arg("loc"), py::arg("off") = 0, py::arg("len") = ~0ull);
   m.def("hint_next_use", [](uint64_t id, uint64_t when) { rt()->hint_next_use(range(id), when); });
+  m.def("node_ledger", [](int max_nodes) {
+    NodeLedger& L = NodeLedger::get();
+    py::dict d;
+    d["attached"] = L.attached();
+    d["path"] = L.path();
+    d["refusals"] = L.refusals();
+    py::list nodes;
+    for (int n = 0; n < max_nodes && n < kMaxNodes; ++n) {
+      auto v = L.view(n);
+      py::dict e;
+      e["node"] = n;
+      e["capacity"] = v.capacity;
+      e["reserved"] = v.reserved;
+      e["mine"] = v.mine;
+      nodes.append(e);
+    }
+    d["nodes"] = nodes;
+    return d;
+  }, py::arg("max_nodes") = 8);
   m.def("spread_class", [](int dev, uint64_t id) { return rt()->spread_class(dev, id); });
   m.def("spread_stats", [](int dev) {
     auto st = rt()->spread_stats(dev);
@@ -285,6 +305,7 @@ PYBIND11_MODULE(_ogkm, m) {
     d["adaptations"] = st.adaptations;
     d["keep_fraction"] = st.keep_fraction;
     d["window_reserve"] = st.window_reserve;
+    d["last_pass_keep_evictions"] = st.last_pass_keep_evictions;
     return d;
   });
   m.def("set_op_clock", [](int dev, uint64_t now) { rt()->set_op_clock(dev, now); });

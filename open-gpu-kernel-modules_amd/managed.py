@@ -107,7 +107,6 @@ def _mode_class():
             self._abs = 0          # op clock: trace positions passed since recording ended
             self._recording = True
             self._requested: dict[int, int] = {}  # operand -> op-clock time a prefetch was queued for
-            self._evict_first: set = set()  # spread "stream" class (see _build_spread)
             self.ops = 0
             self.faulted_ops = 0
             self.hinted_ops = 0      # ops whose operands got next-use hints (position found in the trace)
@@ -268,8 +267,8 @@ def _mode_class():
             self._pos = new
             now = self._abs
             nd = self._nextd[new]
-            ev = self._evict_first
-            hints = [(p, (now + nd[p]) | (_EVICT_FIRST if p in ev else 0)) for p in key]
+            # next uses only: the runtime decides keep / stream classes itself (SpreadPolicy)
+            hints = [(p, now + nd[p]) for p in key]
             self.hinted_ops += 1
             want = []
             if self.lookahead_bytes > 0:
@@ -293,41 +292,8 @@ def _mode_class():
                             want.append((p, at))
             return hints, want
 
-        def _build_spread(self) -> None:
-            """Spread classes (as TieredLlama's planner-off mode): the share of
-            the trace's long-lived bytes the arena can hold is error-diffused
-            over the operands in first-use order as a "keep" class; the rest
-            carry the evict-first hint flag. Plain Belady keeps one contiguous
-            run of the cycle resident and the link idles while the compute
-            crosses it."""
-            self._evict_first = set()
-            if not _SPREAD:
-                return
-            order, seen = [], set()
-            for key in self._trace:
-                for p in key:
-                    if p not in seen:
-                        seen.add(p)
-                        order.append(p)
-            sizes = {}
-            for p in order:
-                sz = self._sizes.get(p)
-                if sz is None:
-                    sz = self._sizes[p] = lib.torch_managed_size(p, self.device)
-                sizes[p] = sz
-            tot = sum(sizes.values()) or 1
-            f = min(1.0, _SPREAD_KEEP * self._arena_bytes() / tot)
-            acc = 0.0
-            for p in order:
-                acc += sizes[p] * f
-                if acc >= sizes[p]:
-                    acc -= sizes[p]
-                else:
-                    self._evict_first.add(p)
-
         def _build_next_use(self) -> None:
             """For every position: positions until each operand's next use (cyclic)."""
-            self._build_spread()
             n = len(self._trace)
             last: dict[int, int] = {}
             nextd: list[dict[int, int]] = [dict() for _ in range(n)]
@@ -344,11 +310,6 @@ def _mode_class():
 
 _METADATA_OPS: frozenset = frozenset()
 _NOT_SPLIT = object()
-_EVICT_FIRST = 1 << 61  # kEvictFirst (csrc/include/ogkm/arena.hpp)
-# off by default: measured slower on the stock 70B (36.4 vs 38.9 tok/s, 89.7 vs 81.8 GB/step
-# H2D - the activations share the arena, so the stream class thrashes; tools/sessions/gpu_r4_sp.sh)
-_SPREAD = __import__("os").environ.get("OGKM_MANAGED_SPREAD", "0") != "0"
-_SPREAD_KEEP = float(__import__("os").environ.get("OGKM_MANAGED_SPREAD_KEEP", "0.85"))
 _MAX_RUNS = 16384  # contiguous runs enumerated per written view (beyond: its bounding extent)
 
 

@@ -68,7 +68,6 @@ _FLOOR_FALLBACK = os.environ.get("OGKM_FLOOR_FALLBACK", "stop")
 # 0: unit sizes - measured the same on the 70B, 103.4 vs 102.7 tok/s, and a
 # larger in-flight share of a small arena streams more)
 _WINDOW_MISSING = os.environ.get("OGKM_WINDOW_MISSING", "0") != "0"
-_EVICT_FIRST = 1 << 61  # kEvictFirst (csrc/include/ogkm/arena.hpp): evict before unflagged hinted data
 
 
 @dataclass(frozen=True)
@@ -411,7 +410,6 @@ class TieredLlama:
             raise ValueError(f"HBM budget {self.budget/2**30:.1f} GiB too small for KV + staging "
                              f"({(fixed + staging + self.stage_bytes)/2**30:.1f} GiB)")
         n_res = max(0, min(cfg.n_layers, avail // layer_cost - int(os.environ.get("OGKM_RESIDENT_MARGIN", "0"))))
-        self._spread_room = max(0, avail)  # planner off: HBM the runtime may keep units in (spread classes)
         # What the static plan would stream per step (planner off: the bytes the
         # runtime's own residency is measured against; traffic() plans with it).
         res_s = [((i + 1) * n_res) // cfg.n_layers > (i * n_res) // cfg.n_layers for i in range(cfg.n_layers)]
@@ -579,34 +577,18 @@ class TieredLlama:
         # later at the same place in the use order, so the runtime can evict
         # in next-use order (Belady, ChunkArena::set_next_use) instead of
         # recency - on a cyclic step larger than HBM, LRU evicts every unit just
-        # before its reuse; Belady keeps a fixed subset resident, as the static
-        # plan does by hand. Op clock = passes * len(stream_seq) + position.
-        # (not for peer shards: their units stream through the all-gather
-        # pipeline, which does not keep the op clock - the workingset policy
-        # decides there)
+        # before its reuse. The runtime itself splits the hinted units into a
+        # keep class sized to its arena, spread over the use order, and a
+        # stream class evicted first (SpreadPolicy, csrc/core/spread.cpp) -
+        # the model passes nothing but the next uses. Op clock = passes *
+        # len(stream_seq) + position. Peer shards hint the same way: each rank's
+        # shards are used (gathered) in the same cyclic order.
         self.next_use = (self.planner == "off" and os.environ.get("OGKM_NEXT_USE", "1") != "0"
-                         and bool(self.stream_seq) and self.sworld <= 1)
+                         and bool(self.stream_seq))
         self._seq_pos = {k: j for j, k in enumerate(self.stream_seq)}
         self._pass, self._last_pos = 0, -1
         if self.next_use and not self.dry_run:
             lib.reset_op_clock(self.dev)  # our clock restarts at 0 (a previous model's hints are stale)
-        # Spread classes (see _hint_used): the "keep" share of the units is the
-        # share of their bytes the arena can hold (less 3 %), spread over the
-        # use order unit by unit (error diffusion), like the static plan's
-        # evenly spread resident layers; the rest is the "stream" class.
-        self._spread_class = None
-        if self.next_use and os.environ.get("OGKM_SPREAD", "1") != "0":
-            tot = sum(self._unit_bytes(k) for k in self.stream_seq) or 1
-            f = min(1.0, float(os.environ.get("OGKM_SPREAD_KEEP", "0.97")) * self._spread_room / tot)
-            acc, cls = 0.0, []
-            for k in self.stream_seq:
-                nb = self._unit_bytes(k)
-                acc += nb * f
-                keep = acc >= nb
-                if keep:
-                    acc -= nb
-                cls.append(not keep)
-            self._spread_class = cls
         # Bounded run-ahead: compute events of streamed units enqueued but maybe
         # not yet run. Leases wait GPU-side, so without a bound the host would
         # prefetch a whole step ahead and the ring would evict (and wait on)
@@ -1044,22 +1026,12 @@ class TieredLlama:
     def _hint_used(self, key) -> None:
         """Next-use mode, once ``key`` is leased: its next use is one pass later
         (hinted after the lease pinned it - before, the prefetches queued for
-        this use would see it as the furthest-needed unit and evict it).
-        Spread (OGKM_SPREAD, default on): units of the "stream" class - spread
-        over the use order so the "keep" class fits the arena - carry the kEvictFirst flag,
-        so the arena evicts them before any "keep"-class unit (the prefetch
-        floor still compares true next uses). Plain Belady keeps
-        one contiguous run of the cycle resident, and the link idles while the
-        compute crosses it (126 ms of a 614 ms 70B step, profiles/
-        r4_planner_off_diag.jsonl); interleaved runs keep the prefetch window
-        streaming throughout, as the static plan's evenly spread resident
-        layers do. Hints only order the victims: a stream-class unit is still
-        kept when there is room, a keep-class one still evicted when there is not."""
+        this use would see it as the furthest-needed unit and evict it). The
+        runtime decides the unit's keep / stream class from these hints."""
         if key in self._seq_pos:
             n = len(self.stream_seq)
             p = self._seq_pos[key]
-            flag = _EVICT_FIRST if (self._spread_class is not None and self._spread_class[p]) else 0
-            self._buf(key).hint_next_use((self._pass * n + p + n) | flag)
+            self._buf(key).hint_next_use(self._pass * n + p + n)
 
     def _prefetch_ahead(self) -> None:
         """Keep up to ``window_bytes`` of upcoming streamed tensors in flight on the ring."""
@@ -1189,8 +1161,12 @@ class TieredLlama:
         if not self._is_resident(key):
             if self._inflight and self._inflight[0] == key:
                 self._inflight.pop(0)
+            if self.next_use:
+                self._clock_use(key)
             self._prefetch_ahead()
         full = self.gather.get(key)
+        if self.next_use:
+            self._hint_used(key)  # this rank's shard: read by the gather just issued
         if self.staged:
             ref = self._unstage(key, full.data_ptr())
             self.gather.done(key)

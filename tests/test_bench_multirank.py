@@ -196,3 +196,17 @@ def test_bench_refuses_world_size_mismatch(ws, gpus):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", gpus] + ARGS, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr, r.stderr[-2000:]
+
+
+def test_shards_two_ranks_planner_off_small_arena(single, tmp_path):
+    """Peer shards under the default runtime-decided residency (planner off,
+    next-use hints) on a small fake HBM (forced evictions while gathers are in
+    flight): the 2-rank job completes - the configuration that hung on the GPU
+    in round 4 - and decodes the single-rank logits bit for bit."""
+    _, ref = single
+    out, logits = _bench(tmp_path, 2, ["--parallel", "shards", "--planner", "off", "--oversub", "2.0", "--fake-hbm-mb", "96",
+                                       "--launch-timeout", "300"], self_launch=True)
+    cfg = out["config"]
+    assert cfg["planner"] == "off" and cfg["parallelism"] == "shards2"
+    assert out["aux"]["evictions"] > 0
+    assert torch.equal(logits, ref)

@@ -318,25 +318,26 @@ def test_long_context_packed_kv_rows_of_chunks(fake_rt):
 
 def test_planner_off_next_use_streams_like_the_plan(fake_rt, monkeypatch):
     """planner='off' with next-use hints (each streamed unit is next used one
-    pass later): the arena evicts in Belady order, keeping a fixed subset
-    resident as the static plan does by hand - the bytes streamed per step come
-    within 10% of the plan's, and below the hint-less (recency) run's. With the
-    spread classes (the default: part of the units flagged evict-first, spread
-    over the use order so the link streams throughout) the order is no longer
-    pure Belady: it stays below the recency run and within 25% of the plan on
-    this small model, whose prefetch window is a large share of the arena."""
+    pass later) and nothing else from the model: the arena evicts in Belady
+    order, keeping a fixed subset resident as the static plan does by hand -
+    the bytes streamed per step come within 10% of the plan's, and below the
+    hint-less (recency) run's. With the runtime's spread classes (the default,
+    perf_spread_enable: it splits the hinted units into a keep class sized to
+    its arena, spread over the use order, and a stream class evicted first) the
+    order is no longer pure Belady: it stays below the recency run and within
+    25% of the plan on this small model, whose prefetch window is a large share
+    of the arena - and the runtime, not the model, found the classes."""
     lib.shutdown()
     rt.init("fake", fake_devices=1, fake_hbm_mb=1024, host_budget_mb=4096)
     cfg = llama.CONFIGS["small"]
-    htd = {}
-    for name, planner, nu, spread in (("static", "static", "1", "1"), ("lru", "off", "0", "1"),
-                                      ("next_use", "off", "1", "0"), ("spread", "off", "1", "1")):
+    htd, spread_st = {}, {}
+    for name, planner, nu, spread in (("static", "static", "1", 1), ("lru", "off", "0", 1),
+                                      ("next_use", "off", "1", 0), ("spread", "off", "1", 1)):
         monkeypatch.setenv("OGKM_NEXT_USE", nu)
-        monkeypatch.setenv("OGKM_SPREAD", spread)
+        lib.configure("perf_spread_enable", spread)
         m = llama.TieredLlama(cfg, batch=8, context=32, max_new_tokens=12, oversub=2.0, device=0, seed=1,
                               weight_format="ans", kv_format="bf16", planner=planner)
         assert m.next_use == (name in ("next_use", "spread"))
-        assert (m._spread_class is not None) == (name == "spread")
         tok = torch.arange(8) * 7
         for _ in range(3):
             tok = m.step(tok)
@@ -346,8 +347,13 @@ def test_planner_off_next_use_streams_like_the_plan(fake_rt, monkeypatch):
             tok = m.step(tok)
         lib.sync_all()
         htd[name] = lib.stats()["bytes_xfer_htd"] / 4
+        spread_st[name] = lib.spread_stats(0)
         m.close()
+    lib.configure("perf_spread_enable", 1)
     assert htd["next_use"] < htd["lru"], htd
     assert htd["next_use"] <= 1.10 * htd["static"], htd
     assert htd["spread"] < htd["lru"], htd
     assert htd["spread"] <= 1.25 * htd["static"], htd
+    s = spread_st["spread"]
+    assert s["ready"] and s["ranges"] > 0 and 0 < s["keep_ranges"] < s["ranges"], s
+    assert spread_st["next_use"]["ranges"] == 0
