@@ -121,6 +121,20 @@ Status ChunkArena::alloc(uint32_t n, Block* owner, int64_t hint, uint32_t* first
       }
     }
   }
+  const int side = PlacementSide::value();
+  if (pick < 0 && side == 1) {  // low end: first fit
+    for (auto& r : free_runs_)
+      if (r.second >= n) {
+        pick = r.first;
+        break;
+      }
+  } else if (pick < 0 && side == 2) {  // high end: the top n chunks of the highest run that fits
+    for (auto it = free_runs_.rbegin(); it != free_runs_.rend(); ++it)
+      if (it->second >= n) {
+        pick = it->first + it->second - n;
+        break;
+      }
+  }
   if (pick < 0) {
     // Best fit: smallest run that holds n chunks (limits fragmentation).
     uint32_t best = UINT32_MAX;
@@ -218,7 +232,7 @@ Status ChunkArena::reserve(uint32_t n, Reservation* r) {
     }
     if (i + 1 - start == n) {
       const uint64_t wcost = costs[dq.front()];
-      if (wcost < best_cost) {
+      if (wcost < best_cost || (wcost == best_cost && PlacementSide::value() == 2)) {  // (high end: the last tie)
         best_cost = wcost;
         best_first = start;
       }
@@ -269,6 +283,11 @@ int32_t ChunkArena::pick_victim_locked() {
     if (best >= 0) return best;
   }
   return -1;
+}
+
+int& PlacementSide::value() {
+  static thread_local int side = 0;
+  return side;
 }
 
 uint64_t& VictimFloor::value() {

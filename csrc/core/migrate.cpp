@@ -194,10 +194,12 @@ uint64_t Runtime::classify_hint(Range* r, uint64_t when) {
   if (!is_local(dev)) return when;
   ChunkArena* a = arena_for(Loc::gpu(dev));
   if (!a) return when;
-  return when | devs_[dev]->spread.on_hint(r->id, r->size, [a] {
-           auto st = a->stats();
-           return SpreadPolicy::ArenaView{st.capacity, st.pinned};
-         });
+  const uint64_t flag = devs_[dev]->spread.on_hint(r->id, r->size, [a] {
+    auto st = a->stats();
+    return SpreadPolicy::ArenaView{st.capacity, st.pinned};
+  });
+  r->spread_cls.store(flag ? 1 : 0, std::memory_order_relaxed);
+  return when | flag;
 }
 
 SpreadPolicy::Stats Runtime::spread_stats(int dev) {
@@ -1129,6 +1131,8 @@ Status Runtime::place_extent(Range* r, uint64_t off, uint64_t len, int gpu, cons
     if (in_place) first = c0;
   }
   if (!in_place) {
+    const int cls = config().arena_class_sides ? r->spread_cls.load(std::memory_order_relaxed) : -1;
+    PlacementSide side(cls < 0 ? 0 : cls == 0 ? 1 : 2);
     // The fresh extent stays pinned until the end of this call: its chunks have
     // no owner until each block takes its chunk, and an unpinned owner-less
     // chunk is a free eviction victim for a concurrent reserve() (two blocks

@@ -240,6 +240,20 @@ class HbmArena : public ChunkArena {
 
 constexpr uint64_t kHostSegment = 1ull << 30;  // default host_segment_mb
 
+// Scoped placement side for the calling thread's arena allocations: 0 any
+// (best fit), 1 low end (first fit), 2 high end (last fit). Data that stays
+// (the keep class) packs at one end, data that cycles through (the stream
+// class) at the other, so contiguous extents for the stream class are found
+// among stream-class chunks instead of cutting into kept ones.
+struct PlacementSide {
+  static int& value();
+  int saved;
+  explicit PlacementSide(int side) : saved(value()) { value() = side; }
+  ~PlacementSide() { value() = saved; }
+  PlacementSide(const PlacementSide&) = delete;
+  PlacementSide& operator=(const PlacementSide&) = delete;
+};
+
 // Host DRAM or CXL.mem of one NUMA node: a memfd mapped once (the arena view,
 // device-registered segment by segment) and bound to the node with mbind.
 // CPU views of managed ranges map the same memfd pages with MAP_FIXED, so the

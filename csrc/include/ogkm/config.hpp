@@ -59,11 +59,12 @@ namespace ogkm {
   X(arena_dead_cooldown, 0, "next-use eviction: freed data used within this many op-clock steps ranks as just used, not as the first victim") \
   X(perf_spread_enable, 1, "next-use eviction: the runtime splits cyclically hinted data into a keep class (error-diffused over the use order, sized to the arena) and a stream class evicted first (ogkm/spread.hpp); hints that carry their own class flag are left alone") \
   X(perf_spread_keep_pct, 97, "spread classes: percent of the HBM arena's unpinned capacity the keep class may fill") \
-  X(perf_spread_adapt, 1, "spread classes: a pass that evicted keep-class data shrinks the keep class (online, from refaults)") \
+  X(perf_spread_adapt, 0, "spread classes: a pass that evicted keep-class data shrinks the keep class (online, from refaults). Off by default: on the 70B headline the keep-class evictions are structural (contiguous extents), shrinking the class only streams more (123.1 vs 129.4 tok/s, profiles/r5_spread.md)") \
   X(perf_spread_step_pct, 2, "spread classes: keep-share reduction per adaptation (percent)") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
   X(ring_wait_issued, 1, "a GPU-side wait on a DMA ring value is enqueued only once that value's copies are on the engines (Ring::issued_seq; prevents an SDMA-engine cycle with HIP's own copies)") \
-  X(arena_victim_rerank, 1, "next-use eviction: chunks re-hinted since the victim cache was built are ranked ahead of its stale order") \
+  X(arena_class_sides, 0, "spread classes: HBM extents of keep-class ranges are placed from the arena's low end, stream-class ones from its high end (less fragmentation of kept data by the stream turnover)") \
+  X(arena_victim_rerank, 0, "next-use eviction: chunks whose key rose since the victim cache was built (re-hinted) are ranked ahead of its stale order. Off by default: the 70B headline is unchanged (129.5 vs 129.4) and the transparent 8B lost 12 % with it (profiles/r5_spread.md)") \
   X(ring_pipeline, 1, "DMA ring workers issue the next batch of plain copies before the previous one completed (two completion slots)") \
   X(vmm_rocr_remap, 1, "stable-VA remaps through ROCr hsa_amd_vmem_* (HIP keeps a placeholder mapping of the VA); 0 = hipMemMap / hipMemUnmap") \
   X(torch_persistent_ops, 128, "transparent mode: a managed tensor held again this many ops after its first hold is long-lived (keys the op-trace prefetcher)") \

@@ -185,6 +185,11 @@ class Range {
   // Contents are dead (a freed torch allocation waiting for reuse or for its
   // stream fence): evicting its blocks copies nothing out.
   std::atomic<bool> dead{false};
+  // Spread class the runtime gave the range's hints (SpreadPolicy): -1 none,
+  // 0 keep, 1 stream. HBM extents of the two classes are laid out from
+  // opposite ends of the arena (PlacementSide) so the stream class's turnover
+  // does not fragment the keep class's chunks.
+  std::atomic<int> spread_cls{-1};
   bool destroyed = false;
   OrderedMutex place_lock{LockOrder::RANGE_PLACE};  // GPU extent placement
 

@@ -21,6 +21,7 @@ ARENA_MB = 64         # 32 chunks: the cycle is 1.5x the arena
 
 def _run_cycle(passes: int, spread: bool, window: int = 2, after_pass=None):
     lib.configure("perf_spread_enable", 1 if spread else 0)
+    lib.configure("arena_victim_rerank", 1)  # exact next-use victim order (the fake arena is tiny)
     lib.init_device(0, ARENA_MB * MB)
     units = []
     for i in range(N_UNITS):
@@ -102,6 +103,7 @@ def test_spread_adapts_down_on_keep_evictions(fake_rt):
     and after that pass the runtime shrinks the keep class (online adaptation
     from refaults) until it fits again."""
     held = []
+    lib.configure("perf_spread_adapt", 1)
 
     def squeeze(p):
         if p == 3:
