@@ -295,8 +295,17 @@ uint64_t& VictimFloor::value() {
   return floor;
 }
 
+void ChunkArena::set_next_use_many(const uint32_t* idx, size_t n, uint64_t when) {
+  std::lock_guard<OrderedMutex> g(m_);
+  for (size_t k = 0; k < n; ++k) set_next_use_locked(idx[k], when);
+}
+
 void ChunkArena::set_next_use(uint32_t i, uint64_t when) {
   std::lock_guard<OrderedMutex> g(m_);
+  set_next_use_locked(i, when);
+}
+
+void ChunkArena::set_next_use_locked(uint32_t i, uint64_t when) {
   if (i >= nchunks_ || chunks_[i].state != ChunkState::ALLOCATED) return;
   const bool track = vcache_valid_ && hinted_ && config().arena_victim_rerank;
   const uint64_t before = track ? victim_key_locked(chunks_[i]) : 0;
@@ -714,6 +723,31 @@ Block* ChunkArena::owner(uint32_t i) {
 void ChunkArena::touch(uint32_t i, bool has_data, bool preferred, bool prefetched, uint64_t refault_key,
                        uint64_t evicted_at, bool clean) {
   std::lock_guard<OrderedMutex> g(m_);
+  touch_locked(i, has_data, preferred, prefetched, refault_key, evicted_at, clean);
+}
+
+bool ChunkArena::try_pin_many(const uint32_t* idx, size_t n) {
+  std::lock_guard<OrderedMutex> g(m_);
+  for (size_t k = 0; k < n; ++k)
+    if (chunks_[idx[k]].state != ChunkState::ALLOCATED) return false;
+  for (size_t k = 0; k < n; ++k)
+    if (chunks_[idx[k]].pin_count++ == 0) st_.pinned += kBlockSize;
+  return true;
+}
+
+void ChunkArena::release_many(const uint32_t* idx, size_t n, const FenceRef& f) {
+  std::lock_guard<OrderedMutex> g(m_);
+  for (size_t k = 0; k < n; ++k) {
+    ChunkInfo& c = chunks_[idx[k]];
+    if (f) c.reuse_fence.add(f);
+    RT_ASSERT_RELEASE(c.pin_count > 0);
+    if (--c.pin_count == 0) st_.pinned -= kBlockSize;
+    touch_locked(idx[k], true, false, false, 0, 0, false);
+  }
+}
+
+void ChunkArena::touch_locked(uint32_t i, bool has_data, bool preferred, bool prefetched, uint64_t refault_key,
+                              uint64_t evicted_at, bool clean) {
   ChunkInfo& c = chunks_[i];
   if (c.state != ChunkState::ALLOCATED) return;
   c.last_use = ++clock_ + (prefetched ? kPrefetchBoost : 0);

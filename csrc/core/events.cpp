@@ -153,7 +153,8 @@ const char* counter_name(Counter c) {
                             "ring_idle_ns",
                             "ring_copy_calls",
                             "demotion_fallbacks",
-                            "ledger_refusals"};
+                            "ledger_refusals",
+                            "lease_fast_paths"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

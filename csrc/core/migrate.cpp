@@ -161,12 +161,24 @@ void Runtime::hint_next_use(Range* r, uint64_t when) {
   when = classify_hint(r, when);
   r->next_use.store(when);
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
+  // The range's HBM chunks, collected under their block locks, hinted under one
+  // arena lock per arena (a 118-block unit: one arena lock instead of 118).
+  std::vector<uint32_t> idx;
+  ChunkArena* arena = nullptr;
   for (auto& bp : r->blocks) {
     Block* b = bp.get();
     std::lock_guard<OrderedMutex> g(b->lock);
-    for (auto& x : b->res)
-      if (x.loc.is_gpu() && x.chunk >= 0) x.arena->set_next_use((uint32_t)x.chunk, when);
+    for (auto& x : b->res) {
+      if (!x.loc.is_gpu() || x.chunk < 0) continue;
+      if (arena && x.arena != arena) {
+        arena->set_next_use_many(idx.data(), idx.size(), when);
+        idx.clear();
+      }
+      arena = x.arena;
+      idx.push_back((uint32_t)x.chunk);
+    }
   }
+  if (arena && !idx.empty()) arena->set_next_use_many(idx.data(), idx.size(), when);
 }
 
 void Runtime::reset_op_clock(int dev) {
@@ -958,6 +970,9 @@ Status Runtime::prefetch(Range* r, uint64_t off, uint64_t len, Loc dst, Tracker*
     // a prefetch ahead of a known use (next-use mode): it sits in the window
     if (VictimFloor::value() && is_local(dst.id) && config().perf_spread_enable)
       devs_[dst.id]->spread.on_prefetch(r->id, len);
+    // already resident in one contiguous extent (a kept unit): an LRU touch
+    if (config().lease_fast_path && !(r->dev_va && r->stable_dev == dst.id) && resident_extent(r, off, len, dst.id))
+      return Status::OK;
     return gpu_extent_resident(r, off, len, dst.id, {}, nullptr, out, cause);
   }
   uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
@@ -1530,6 +1545,21 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
       return PageMask::range((uint32_t)(lo >> kPageShift), (uint32_t)((hi - lo + kPageSize - 1 + (lo & (kPageSize - 1))) >> kPageShift));
     };
     Loc dst = proc_loc(proc);
+    // 0) fast path: a GPU read of data already resident in one contiguous
+    // extent of this GPU's arena (the common streamed-or-kept unit at its use).
+    // Every decision below would keep it where it is; only the pins, the LRU /
+    // next-use touch and the readiness fences are needed - one arena lock for
+    // all chunks instead of a placement pass (config lease_fast_path).
+    if (proc != kCpuProc && access == Access::READ && !packed && !(r->dev_va && r->stable_dev == proc) &&
+        config().lease_fast_path && fast_lease(r, off, len, proc, L.get())) {
+      Tools::get().inc(Counter::LeaseFastPaths);
+      r->views.fetch_add(1);
+      std::lock_guard<std::mutex> g(leases_m_);
+      L->id = next_lease_++;
+      *out = L.get();
+      leases_[L->id] = std::move(L);
+      return Status::OK;
+    }
     // 1) residency decisions
     bool all_remote = proc != kCpuProc;
     std::vector<ResidencyDecision> dec(n);
@@ -1552,6 +1582,19 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
         dec[k].dst = dst;
         dec[k].read_dup = access == Access::READ || access == Access::PREFETCH;
         Tools::get().inc(Counter::RemoteFallbacks);
+        // Software access counters on this path too (the transparent mode's op
+        // holds): each such access is one the reference would count as a
+        // remote access (uvm_gpu_access_counters.c:1617); at the threshold the
+        // block is promoted - its next decision migrates it to this GPU
+        // instead of serving another duplicate of the remote copy.
+        Tools::get().inc(Counter::AccessCounterNotifications);
+        uint32_t& cnt = b->counters.remote_hits[proc];
+        if (++cnt >= (uint64_t)std::max<int64_t>(1, config().perf_access_counter_threshold)) {
+          cnt = 0;
+          if (config().perf_access_counter_migration_enable) b->counters.promote[proc] = true;
+          tools_event(ToolsEventType::AccessCounter, Cause::AccessCounters, Loc{}, Loc::gpu(proc), proc,
+                      r->addr() + b->block_offset(), kBlockSize, r->id);
+        }
       }
       if (!dec[k].map_remote) all_remote = false;
     }
@@ -1704,6 +1747,77 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
   return Status::OK;
 }
 
+bool Runtime::resident_extent(Range* r, uint64_t off, uint64_t len, int gpu) {
+  const Loc me = Loc::gpu(gpu);
+  ChunkArena* ga = arena_for(me);
+  if (!ga) return false;
+  const uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
+  int64_t first = -1;
+  for (uint64_t bi = b0; bi <= b1; ++bi) {
+    Block* b = r->block(bi);
+    const uint64_t lo = std::max(off, bi << kBlockShift) - (bi << kBlockShift);
+    const uint64_t hi = std::min(off + len, (bi + 1) << kBlockShift) - (bi << kBlockShift);
+    const PageMask want = PageMask::range((uint32_t)(lo >> kPageShift),
+                                          (uint32_t)((hi + kPageSize - 1) >> kPageShift) - (uint32_t)(lo >> kPageShift));
+    std::lock_guard<OrderedMutex> g(b->lock);
+    Residency* x = b->find(me);
+    if (!x || x->chunk < 0 || x->arena != ga || (bi > b0 && x->chunk != first + (int64_t)(bi - b0)) ||
+        b->unpublished || !want.andnot(x->resident).empty())
+      return false;
+    if (bi == b0) first = x->chunk;
+    touch_residency(b, x, true);
+  }
+  return true;
+}
+
+bool Runtime::fast_lease(Range* r, uint64_t off, uint64_t len, int proc, Lease* L) {
+  const Loc me = Loc::gpu(proc);
+  ChunkArena* ga = arena_for(me);
+  if (!ga || (r->group && !r->group->migratable)) return false;
+  const uint64_t b0 = off >> kBlockShift, b1 = (off + len - 1) >> kBlockShift;
+  const uint32_t n = (uint32_t)(b1 - b0 + 1);
+  std::vector<Block*> bl;
+  std::vector<uint32_t> ch;
+  bl.reserve(n);
+  ch.reserve(n);
+  Tracker ready;
+  bool ok = true;
+  for (uint32_t k = 0; k < n && ok; ++k) {
+    Block* b = r->block(b0 + k);
+    const uint64_t bi = b0 + k;
+    const uint64_t lo = std::max(off, bi << kBlockShift) - (bi << kBlockShift);
+    const uint64_t hi = std::min(off + len, (bi + 1) << kBlockShift) - (bi << kBlockShift);
+    const PageMask want = PageMask::range((uint32_t)(lo >> kPageShift),
+                                          (uint32_t)((hi + kPageSize - 1) >> kPageShift) - (uint32_t)(lo >> kPageShift));
+    std::lock_guard<OrderedMutex> g(b->lock);
+    Residency* x = b->find(me);
+    if (!x || x->chunk < 0 || x->arena != ga || (k && x->chunk != (int64_t)ch[0] + k) || b->unpublished ||
+        b->user_pins || !want.andnot(x->resident).empty()) {
+      ok = false;
+      break;
+    }
+    b->lease_pins++;
+    bl.push_back(b);
+    ch.push_back((uint32_t)x->chunk);
+    touch_residency(b, x);
+    ready.merge(b->tracker);
+  }
+  if (ok) ok = ga->try_pin_many(ch.data(), ch.size());
+  if (!ok) {
+    for (Block* b : bl) {
+      std::lock_guard<OrderedMutex> g(b->lock);
+      b->lease_pins--;
+    }
+    return false;
+  }
+  L->blocks = std::move(bl);
+  L->pinned_chunks.reserve(ch.size());
+  for (uint32_t c : ch) L->pinned_chunks.emplace_back(ga, c);
+  L->ready = std::move(ready);
+  L->dptr = ga->chunk_addr(ch[0]) + (off - (b0 << kBlockShift));
+  return true;
+}
+
 Status Runtime::release(Lease* l, void* stream) {
   if (!l) return Status::INVALID_ARGUMENT;
   std::unique_ptr<Lease> own;
@@ -1716,11 +1830,21 @@ Status Runtime::release(Lease* l, void* stream) {
   }
   FenceRef f;
   if (l->proc != kCpuProc && !l->pinned_chunks.empty()) f = fence_record(be_.get(), l->proc, stream);
+  // Chunks of one arena: fence + unpin + LRU touch under one arena lock.
+  std::vector<uint32_t> idx;
+  ChunkArena* cur = nullptr;
+  auto flush = [&] {
+    if (cur && !idx.empty()) cur->release_many(idx.data(), idx.size(), f);
+    idx.clear();
+  };
   for (auto& pc : l->pinned_chunks) {
-    if (f) pc.first->add_reuse_fence(pc.second, f);
-    pc.first->unpin(pc.second);
-    pc.first->touch(pc.second, true);
+    if (pc.first != cur) {
+      flush();
+      cur = pc.first;
+    }
+    idx.push_back(pc.second);
   }
+  flush();
   {
     std::shared_lock<OrderedRWLock> vg(vs_.lock);
     for (Block* b : l->blocks) {

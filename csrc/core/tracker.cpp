@@ -106,6 +106,11 @@ Status Tracker::wait() {
 Status Tracker::gpu_wait(Backend* be, void* stream) const {
   for (auto& f : fences_) {
     if (f->done.load(std::memory_order_relaxed)) continue;
+    // An event recorded on this very stream is already ordered before
+    // anything enqueued on it now: no barrier packet (a lease of a unit whose
+    // previous readers ran on the consumer's own stream - every resident unit
+    // of a decode step).
+    if (f->event && f->stream == stream && stream) continue;
     Status s;
     uint64_t t0 = now_ns();
     bool had_event = f->event != nullptr;

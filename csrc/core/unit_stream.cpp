@@ -1,0 +1,109 @@
+// Native per-unit protocol of a cyclic consumer (see ogkm/unit_stream.hpp).
+#include "ogkm/unit_stream.hpp"
+
+#include "ogkm/arena.hpp"
+#include "ogkm/runtime.hpp"
+
+namespace ogkm {
+
+UnitStream::UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_t window_bytes, bool next_use,
+                       uint32_t max_ahead)
+    : rt_(rt), dev_(dev), ranges_(std::move(ranges)), window_(window_bytes), next_use_(next_use),
+      max_ahead_(max_ahead) {}
+
+UnitStream::~UnitStream() {
+  for (void* e : ahead_) {
+    (void)rt_->be()->event_sync(e);
+    rt_->be()->event_destroy(e);
+  }
+}
+
+uint64_t UnitStream::due(uint32_t pos) const {
+  const uint64_t n = ranges_.size();
+  return (pass_ + ((int64_t)pos <= last_pos_ ? 1 : 0)) * n + pos;
+}
+
+void UnitStream::prefetch_window() {
+  const uint32_t n = (uint32_t)ranges_.size();
+  const Loc gpu = Loc::gpu(dev_);
+  while (inflight_.size() < n) {
+    Range* r = ranges_[pf_next_];
+    const uint64_t nb = r->size;
+    if (!inflight_.empty() && inflight_bytes_ + nb > window_) break;
+    const uint64_t t0 = now_ns();
+    Tracker t;
+    Status st;
+    {
+      // next-use mode: evict only data needed after this unit's own use
+      VictimFloor vf(next_use_ ? due(pf_next_) : 0);
+      st = rt_->prefetch(r, 0, r->size, gpu, &t, Cause::Prefetch);
+    }
+    st_.prefetch_ns += now_ns() - t0;
+    if (st != Status::OK) {
+      // refused by the floor (no victim needed later than it): left to its use
+      ++st_.refused;
+      break;
+    }
+    inflight_.push_back(pf_next_);
+    inflight_bytes_ += nb;
+    ++st_.prefetched;
+    pf_next_ = (pf_next_ + 1) % n;
+  }
+}
+
+Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
+  if (pos >= ranges_.size()) return Status::INVALID_ARGUMENT;
+  const uint64_t n = ranges_.size();
+  Range* r = ranges_[pos];
+  if (!inflight_.empty() && inflight_.front() == pos) {
+    inflight_.pop_front();
+    inflight_bytes_ -= r->size;
+  } else {
+    ++st_.demand;
+  }
+  if (next_use_) {  // the op clock moves to this use
+    if ((int64_t)pos <= last_pos_) ++pass_;
+    last_pos_ = pos;
+    rt_->set_op_clock(dev_, pass_ * n + pos);
+  }
+  prefetch_window();
+  const uint64_t t0 = now_ns();
+  Status st = rt_->acquire(r, 0, r->size, dev_, Access::READ, out);
+  st_.acquire_ns += now_ns() - t0;
+  if (st != Status::OK) return st;
+  // hinted once leased (before, the prefetches queued for this use would see it
+  // as the furthest-needed unit and evict it): next used one pass later
+  if (next_use_) rt_->hint_next_use(r, pass_ * n + pos + n);
+  // the consumer's stream waits GPU-side (no stream: the host waits)
+  st = stream ? (*out)->ready.gpu_wait(rt_->be(), stream) : (*out)->ready.wait();
+  if (st != Status::OK) {
+    (void)rt_->release(*out, stream);
+    *out = nullptr;
+  }
+  return st;
+}
+
+Status UnitStream::release(Lease* l, void* stream) {
+  Status st = rt_->release(l, stream);
+  if (!max_ahead_ || !stream) return st;
+  // Bounded run-ahead: leases wait GPU-side, so without a bound the host would
+  // prefetch a whole step ahead and the ring would evict (and wait on) chunks
+  // whose readers are still queued - the copies then serialise behind compute.
+  void* e = rt_->be()->event_create(dev_);
+  if (!e) return st;
+  if (rt_->be()->event_record(e, stream) != Status::OK) {
+    rt_->be()->event_destroy(e);
+    return st;
+  }
+  ahead_.push_back(e);
+  while (ahead_.size() > max_ahead_) {
+    const uint64_t t0 = now_ns();
+    (void)rt_->be()->event_sync(ahead_.front());
+    st_.ahead_wait_ns += now_ns() - t0;
+    rt_->be()->event_destroy(ahead_.front());
+    ahead_.pop_front();
+  }
+  return st;
+}
+
+}  // namespace ogkm

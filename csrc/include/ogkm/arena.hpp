@@ -136,6 +136,7 @@ class ChunkArena {
   // before its next use). Victims never have a next use before the thread's
   // VictimFloor (a prefetch must not evict data needed before its own).
   void set_next_use(uint32_t i, uint64_t when);
+  void set_next_use_many(const uint32_t* idx, size_t n, uint64_t when);  // one lock for a range's chunks
   void set_op_clock(uint64_t now);
   // A new hint producer (another ogkm.managed() context, a new model) restarts
   // its op clock at 0: forget the old clock, every chunk's hint and the victim
@@ -149,6 +150,11 @@ class ChunkArena {
     std::lock_guard<OrderedMutex> g(m_);
     return st_.evictions;
   }
+  // Lease fast path (Runtime::acquire of a resident extent): pin every chunk
+  // under one lock, or none (false) when any is no longer ALLOCATED; release
+  // = reuse fence + unpin + LRU touch of each, under one lock.
+  bool try_pin_many(const uint32_t* idx, size_t n);
+  void release_many(const uint32_t* idx, size_t n, const FenceRef& f);
   void pin(uint32_t i);
   // Pin only an ALLOCATED chunk: false when it is reserved for eviction (or
   // free) - a pin taken after another thread chose the chunk as a victim would
@@ -179,6 +185,9 @@ class ChunkArena {
   uint32_t nchunks_ = 0;
 
  private:
+  void set_next_use_locked(uint32_t i, uint64_t when);
+  void touch_locked(uint32_t i, bool has_data, bool preferred, bool prefetched, uint64_t refault_key,
+                    uint64_t evicted_at, bool clean);
   int32_t pick_victim_locked();  // coldest evictable chunk (reserve(1) order), -1 = none
   uint64_t victim_key_locked(const ChunkInfo& c) const;  // next-use mode: larger = evict sooner
   uint64_t base_key_locked(const ChunkInfo& c) const;    // the same without the kEvictFirst class bonus

@@ -62,6 +62,7 @@ namespace ogkm {
   X(perf_spread_adapt, 0, "spread classes: a pass that evicted keep-class data shrinks the keep class (online, from refaults). Off by default: on the 70B headline the keep-class evictions are structural (contiguous extents), shrinking the class only streams more (123.1 vs 129.4 tok/s, profiles/r5_spread.md)") \
   X(perf_spread_step_pct, 2, "spread classes: keep-share reduction per adaptation (percent)") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
+  X(lease_fast_path, 1, "acquire: a GPU read of data resident in one contiguous extent only pins, touches and waits (no placement pass)") \
   X(ring_wait_issued, 1, "a GPU-side wait on a DMA ring value is enqueued only once that value's copies are on the engines (Ring::issued_seq; prevents an SDMA-engine cycle with HIP's own copies)") \
   X(arena_class_sides, 0, "spread classes: HBM extents of keep-class ranges are placed from the arena's low end, stream-class ones from its high end (less fragmentation of kept data by the stream turnover)") \
   X(arena_victim_rerank, 0, "next-use eviction: chunks whose key rose since the victim cache was built (re-hinted) are ranked ahead of its stale order. Off by default: the 70B headline is unchanged (129.5 vs 129.4) and the transparent 8B lost 12 % with it (profiles/r5_spread.md)") \

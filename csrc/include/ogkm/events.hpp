@@ -197,6 +197,7 @@ enum class Counter : int {
   RingCopyCalls,       // H2D DMA ring workers: engine copy calls (merged runs)
   DemotionFallbacks,   // evictions demoted past a full node (node-wide budget spent) to the next tier / node
   LedgerRefusals,      // host / CXL segments the node-wide ledger refused (budget shared by all ranks)
+  LeaseFastPaths,      // acquires served by the resident-extent fast path (Runtime::fast_lease)
   NumCounters
 };
 const char* counter_name(Counter c);

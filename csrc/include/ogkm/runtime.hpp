@@ -213,6 +213,13 @@ class Runtime {
   Status acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out,
                  bool allow_remote = true);
   Status release(Lease* l, void* stream);  // consumer's last use recorded on `stream`
+  // acquire() fast path: a GPU read of a range span resident in one contiguous
+  // extent of that GPU's arena - pin + touch + readiness only (false: take the
+  // full path).
+  bool fast_lease(Range* r, uint64_t off, uint64_t len, int proc, Lease* L);
+  // True (and the blocks' chunks LRU-touched as prefetched) when the span is
+  // resident on `gpu` in one contiguous extent with nothing pending.
+  bool resident_extent(Range* r, uint64_t off, uint64_t len, int gpu);
   // Page-granular write fault: revoke the other copies of these byte intervals
   // of r (resident on gpu) so only written pages are dirty.
   Status invalidate_others(Range* r, const std::vector<std::pair<uint64_t, uint64_t>>& bytes, int gpu);

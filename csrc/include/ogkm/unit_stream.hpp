@@ -1,0 +1,70 @@
+// Per-unit fault / prefetch protocol of a cyclic consumer, in one native call.
+//
+// A decode step uses its weight units (and KV prefixes) in the same order
+// every pass. Under runtime-decided residency (planner off) each use is: move
+// the op clock to the unit, keep a byte window of the following units in
+// flight on the migration ring (each prefetch evicting only data needed later
+// than it - the victim floor), fault the unit in (a lease), let the consumer's
+// stream wait for its copies GPU-side, hint its next use one pass later; and
+// after its kernels are enqueued, release it fenced on the stream and keep the
+// host at most `max_ahead` units ahead of the GPU. Done from Python that was
+// ~100 us of host time per unit in round 4 (five calls, list bookkeeping),
+// which made a fully resident 8B decode host-bound (10.8 vs 6.8 ms/step); here
+// it is two calls per unit. The reference services a whole batch of faults per
+// pass for the same reason (uvm_gpu_replayable_faults.c:2906 batch loop;
+// multi-block migration uvm_migrate.c:456-553).
+#pragma once
+
+#include <cstdint>
+#include <deque>
+#include <vector>
+
+#include "ogkm/common.hpp"
+
+namespace ogkm {
+
+class Runtime;
+class Range;
+struct Lease;
+
+class UnitStream {
+ public:
+  struct Stats {
+    uint64_t prefetched = 0, refused = 0, demand = 0, prefetch_ns = 0, acquire_ns = 0, ahead_wait_ns = 0;
+  };
+  // `ranges`: the units in use order; `window_bytes`: bytes of following units
+  // kept in flight; `next_use`: hint next uses / floor prefetches (planner off);
+  // `max_ahead`: released units whose kernels may still be queued before the
+  // host waits (0 = unbounded).
+  UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_t window_bytes, bool next_use,
+             uint32_t max_ahead);
+  ~UnitStream();
+  // Unit `pos` is used now on `stream`: returns its lease (device pointer =
+  // lease->dptr) with the stream already ordered after its copies.
+  Status use(uint32_t pos, void* stream, Lease** out);
+  // Its kernels are enqueued on `stream`.
+  Status release(Lease* l, void* stream);
+  // Keep the window full (the step's start: nothing used yet).
+  void prefetch_window();
+  const Stats& stats() const { return st_; }
+  void reset_stats() { st_ = Stats{}; }
+  uint32_t size() const { return (uint32_t)ranges_.size(); }
+
+ private:
+  uint64_t due(uint32_t pos) const;
+  Runtime* rt_;
+  int dev_;
+  std::vector<Range*> ranges_;
+  uint64_t window_;
+  bool next_use_;
+  uint32_t max_ahead_;
+  uint32_t pf_next_ = 0;
+  std::deque<uint32_t> inflight_;
+  uint64_t inflight_bytes_ = 0;
+  uint64_t pass_ = 0;
+  int64_t last_pos_ = -1;
+  std::deque<void*> ahead_;  // events of released units (host bound)
+  Stats st_;
+};
+
+}  // namespace ogkm

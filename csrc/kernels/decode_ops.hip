@@ -10,6 +10,7 @@
 //                   softmax partials and P.V (lane = head-dim pair) in f32;
 //   k_attn_combine  merges the splits (log-sum-exp) and writes bf16.
 // The KV cache layout is [2][B][Hkv][T][hd] (k then v), bf16.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include "ogkm/kernels.hpp"
@@ -400,22 +401,20 @@ __global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a) {
 typedef __bf16 attn_bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float attn_f32x4_t __attribute__((ext_vector_type(4)));
 
-template <int HD, int G, int NW>
+template <int HD, int G, int NW, int DPL>
 __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
   constexpr int KS = HD / 32;         // 32-dim MFMA steps
-  constexpr int DPV = HD / 32;        // p.v dims per lane
-  constexpr int PU = G <= 4 ? 8 : G <= 8 ? 4 : 2;
   static_assert((HD == 64 || HD == 128) && G <= 16, "shape");
   extern __shared__ float smem[];
   const uint32_t g = a.hq / a.hkv;    // <= G
-  float* ps = smem;                   // [NW waves][g][64] scores -> probabilities
-  float* po = smem + NW * g * 64;     // [NW waves][g][HD] unnormalised outputs
+  float* ps = smem;                   // [NW waves][64 tokens][G] probabilities (token-major, G padded)
+  float* po = smem + NW * G * 64;     // [NW waves][g][HD] unnormalised outputs
   __shared__ float wm[NW][G], wl[NW][G];
   const uint32_t split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t wt0 = split * (64u * NW) + wave * 64;
   const int32_t wn = (int32_t)a.len - (int32_t)wt0 < 64 ? (int32_t)a.len - (int32_t)wt0 : 64;
-  float* wps = ps + wave * g * 64;
+  float* wps = ps + wave * G * 64;
   float* wpo = po + wave * g * HD;
   if (wn <= 0) {  // this wave's tokens are past the context: an empty partial
     for (uint32_t e = lane; e < g * HD; e += 64) wpo[e] = 0.f;
@@ -481,7 +480,7 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         const float p = __expf(sc[t][r] - m);  // masked tokens: exp(-inf) = 0
         l += p;
-        if (col < g) wps[col * 64 + t * 16 + 4 * quad + r] = p;
+        if (col < G) wps[(t * 16 + 4 * quad + r) * G + col] = col < g ? p : 0.f;
       }
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
@@ -491,41 +490,79 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // P.V: half a wave per token, DPV dims per lane
-    const uint32_t half = lane >> 5, d0 = (lane & 31) * DPV;
-    float o[G][DPV];
+    // P.V on the vector ALUs, bound by how many V bytes are in flight: lane l
+    // owns 8 dims (dim group l % LPT) of every TPI-th token (token group
+    // l / LPT); one wave instruction loads TPI whole V rows (1 KB) and VB of
+    // them are issued before the first FMA (8 KB per wave for G <= 8 - the
+    // half-wave-per-token loop had 2 KB in flight and capped the tp8 shape,
+    // one KV head per batch row, at ~1.3 TB/s). The token groups' partial
+    // sums are reduced with xor shuffles at the end.
+    // P.V on the vector ALUs, bound by how many V bytes are in flight: lane l
+    // owns DPL dims (dim group l % LPT) of every TPI-th token (token group
+    // l / LPT); one wave instruction loads TPI whole V rows and VB of them are
+    // issued before the first FMA (8 KB per wave for G <= 8 - the
+    // half-wave-per-token loop had 2 KB in flight and capped the tp8 shape,
+    // one KV head per batch row, at ~1.3 TB/s). The token groups' partial
+    // sums are reduced with xor shuffles at the end.
+    // DPL dims per lane (template): 8 - one 16 B load per row piece, 8 KB in
+    // flight per wave, 164 VGPRs for 8 heads - when the grid has few waves per
+    // SIMD (one KV head per batch row: the tp8 shapes); 4 - 96 VGPRs, four
+    // waves per SIMD - when it has many, and always for 16 heads.
+    static_assert(DPL == 8 || DPL == 4, "dims per lane");
+    constexpr int LPT = HD / DPL, TPI = 64 / LPT, NI = 64 / TPI;
+    constexpr int VB = 8;
+    const uint32_t tg = lane / LPT, dg = lane % LPT;
+    float o[G][DPL];
 #pragma unroll
     for (int h = 0; h < G; ++h)
 #pragma unroll
-      for (int j = 0; j < DPV; ++j) o[h][j] = 0.f;
-#pragma unroll PU
-    for (int32_t t = (int32_t)half; t < wn; t += 2) {
-      const uint16_t* vr = vbase + (uint64_t)(wt0 + t) * HD + d0;
-      float vf[DPV];
-      if constexpr (DPV == 4) {
-        const uint2 w = *reinterpret_cast<const uint2*>(vr);
-        vf[0] = dbf((uint16_t)w.x);
-        vf[1] = dbf((uint16_t)(w.x >> 16));
-        vf[2] = dbf((uint16_t)w.y);
-        vf[3] = dbf((uint16_t)(w.y >> 16));
-      } else {
-        const uint32_t w = *reinterpret_cast<const uint32_t*>(vr);
-        vf[0] = dbf((uint16_t)w);
-        vf[1] = dbf((uint16_t)(w >> 16));
+      for (int j = 0; j < DPL; ++j) o[h][j] = 0.f;
+    const uint16_t* vcol = vbase + (uint64_t)wt0 * HD + dg * DPL;
+#pragma unroll 1
+    for (int i0 = 0; i0 < NI; i0 += VB) {
+      uint32_t vv[VB][DPL / 2];
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const int32_t t = (i0 + i) * TPI + (int32_t)tg;
+        const int32_t tt = t < wn ? t : wn - 1;  // past the context: clamped, its p is 0
+        if constexpr (DPL == 8) {
+          const uint4 w = *reinterpret_cast<const uint4*>(vcol + (uint64_t)tt * HD);
+          vv[i][0] = w.x;
+          vv[i][1] = w.y;
+          vv[i][2] = w.z;
+          vv[i][3] = w.w;
+        } else {
+          const uint2 w = *reinterpret_cast<const uint2*>(vcol + (uint64_t)tt * HD);
+          vv[i][0] = w.x;
+          vv[i][1] = w.y;
+        }
       }
 #pragma unroll
-      for (int h = 0; h < G; ++h) {
-        const float p = (uint32_t)h < g ? wps[h * 64 + t] : 0.f;
+      for (int i = 0; i < VB; ++i) {
+        const int32_t t = (i0 + i) * TPI + (int32_t)tg;
+        float vf[DPL];
 #pragma unroll
-        for (int j = 0; j < DPV; ++j) o[h][j] += p * vf[j];
+        for (int j = 0; j < DPL / 2; ++j) {
+          vf[2 * j] = dbf((uint16_t)vv[i][j]);
+          vf[2 * j + 1] = dbf((uint16_t)(vv[i][j] >> 16));
+        }
+        const float* pt = wps + t * G;  // token-major probabilities, G (padded) heads
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+          const float p = pt[h];
+#pragma unroll
+          for (int j = 0; j < DPL; ++j) o[h][j] += p * vf[j];
+        }
       }
     }
 #pragma unroll
     for (int h = 0; h < G; ++h) {
 #pragma unroll
-      for (int j = 0; j < DPV; ++j) {
-        const float x = o[h][j] + __shfl_xor(o[h][j], 32, 64);
-        if (half == 0 && (uint32_t)h < g) wpo[h * HD + d0 + j] = x;
+      for (int j = 0; j < DPL; ++j) {
+        float x = o[h][j];
+#pragma unroll
+        for (int sh = LPT; sh < 64; sh <<= 1) x += __shfl_xor(x, sh, 64);
+        if (tg == 0 && (uint32_t)h < g) wpo[h * HD + dg * DPL + j] = x;
       }
     }
   }
@@ -613,11 +650,18 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
   const uint32_t gg = g <= 4 ? 4 : g <= 8 ? 8 : 16;
   const dim3 grid(a.nsplit, a.hkv, a.B);
   const uint32_t nw = st / 64;
-  const size_t lds = (size_t)nw * g * (64 + a.hd) * sizeof(float);
+  const size_t lds = (size_t)nw * (gg * 64 + g * a.hd) * sizeof(float);  // token-major p (G padded) + outputs
   if (ws) {
-#define OGKM_ATTN_WS(HD, L, NW) hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW>), grid, dim3(64 * NW), lds, s, a)
-#define OGKM_ATTN_WS_G(HD, NW) \
-  if (gg == 4) OGKM_ATTN_WS(HD, 4, NW); else if (gg == 8) OGKM_ATTN_WS(HD, 8, NW); else OGKM_ATTN_WS(HD, 16, NW)
+#define OGKM_ATTN_WS(HD, L, NW, D) \
+  hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW, D>), grid, dim3(64 * NW), lds, s, a)
+    // few waves per SIMD (<= 2 of the chip's 1024 SIMDs' worth): the wide rows
+    static const int force_dpl = getenv("OGKM_ATTN_DPL") ? atoi(getenv("OGKM_ATTN_DPL")) : 0;  // A/B drills
+    const bool wide = force_dpl ? force_dpl == 8 : (uint64_t)grid.x * grid.y * grid.z * nw <= 2048;
+#define OGKM_ATTN_WS_G(HD, NW)                      \
+  if (gg == 4) OGKM_ATTN_WS(HD, 4, NW, 8);          \
+  else if (gg == 8 && wide) OGKM_ATTN_WS(HD, 8, NW, 8); \
+  else if (gg == 8) OGKM_ATTN_WS(HD, 8, NW, 4);     \
+  else OGKM_ATTN_WS(HD, 16, NW, 4)
     if (a.hd == 128) {
       if (nw == 1) { OGKM_ATTN_WS_G(128, 1); } else { OGKM_ATTN_WS_G(128, 4); }
     } else {

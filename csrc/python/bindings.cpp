@@ -14,6 +14,7 @@
 #include "ogkm/kernels.hpp"
 #include "ogkm/lock_order.hpp"
 #include "ogkm/runtime.hpp"
+#include "ogkm/unit_stream.hpp"
 #include "ogkm/ledger.hpp"
 #include "ogkm/torch_alloc.hpp"
 
@@ -291,6 +292,46 @@ PYBIND11_MODULE(_ogkm, m) {
     d["nodes"] = nodes;
     return d;
   }, py::arg("max_nodes") = 8);
+  // Native per-unit fault / prefetch protocol of a cyclic consumer (TieredLlama, planner off).
+  py::class_<UnitStream>(m, "UnitStream")
+      .def(py::init([](int dev, const std::vector<uint64_t>& ids, uint64_t window, bool next_use, uint32_t max_ahead) {
+             std::vector<Range*> rs;
+             for (uint64_t id : ids) rs.push_back(range(id));
+             return new UnitStream(rt(), dev, std::move(rs), window, next_use, max_ahead);
+           }),
+           py::arg("dev"), py::arg("ranges"), py::arg("window_bytes"), py::arg("next_use"), py::arg("max_ahead"))
+      .def("use", [](UnitStream& u, uint32_t pos, uint64_t stream) {
+             Lease* l = nullptr;
+             Status s;
+             {
+               py::gil_scoped_release nogil;
+               s = u.use(pos, (void*)stream, &l);
+             }
+             check(s, "unit use");
+             return py::make_tuple(l->id, l->dptr);
+           })
+      .def("release", [](UnitStream& u, uint64_t lid, uint64_t stream) {
+             Lease* l = rt()->lease_by_id(lid);
+             if (!l) throw StatusError("unknown lease");
+             py::gil_scoped_release nogil;
+             check(u.release(l, (void*)stream), "unit release");
+           })
+      .def("prefetch_window", [](UnitStream& u) {
+             py::gil_scoped_release nogil;
+             u.prefetch_window();
+           })
+      .def("stats", [](UnitStream& u) {
+             const auto& st = u.stats();
+             py::dict d;
+             d["prefetched"] = st.prefetched;
+             d["refused"] = st.refused;
+             d["demand"] = st.demand;
+             d["prefetch_ms"] = st.prefetch_ns / 1e6;
+             d["acquire_ms"] = st.acquire_ns / 1e6;
+             d["ahead_wait_ms"] = st.ahead_wait_ns / 1e6;
+             return d;
+           })
+      .def("reset_stats", &UnitStream::reset_stats);
   m.def("spread_class", [](int dev, uint64_t id) { return rt()->spread_class(dev, id); });
   m.def("spread_stats", [](int dev) {
     auto st = rt()->spread_stats(dev);
@@ -331,13 +372,13 @@ PYBIND11_MODULE(_ogkm, m) {
   });
 
   // ---- leases
-  m.def("acquire", [](uint64_t id, uint64_t off, uint64_t len, int proc, int access) {
+  m.def("acquire", [](uint64_t id, uint64_t off, uint64_t len, int proc, int access, bool allow_remote) {
     Range* r = range(id);
     Lease* l = nullptr;
     Status s;
     {
       py::gil_scoped_release nogil;
-      s = rt()->acquire(r, off, len, proc, (Access)access, &l);
+      s = rt()->acquire(r, off, len, proc, (Access)access, &l, allow_remote);
     }
     check(s, "acquire");
     py::dict d;
@@ -346,7 +387,8 @@ PYBIND11_MODULE(_ogkm, m) {
     d["remote"] = l->remote;
     d["pending"] = l->ready.size();
     return d;
-  });
+  }, py::arg("id"), py::arg("off"), py::arg("len"), py::arg("proc"), py::arg("access"),
+     py::arg("allow_remote") = true);
   // on_stream: GPU-side dependency of `stream` (0 = the null stream) on the
   // lease's copies - the host never blocks. Otherwise the host waits.
   m.def("lease_wait", [](uint64_t lid, uint64_t stream, bool on_stream) {

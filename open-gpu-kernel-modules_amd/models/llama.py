@@ -415,11 +415,11 @@ class TieredLlama:
         res_s = [((i + 1) * n_res) // cfg.n_layers > (i * n_res) // cfg.n_layers for i in range(cfg.n_layers)]
         self.plan_streamed_bytes = (sum(self.res_layer_bytes + self.kv_unit_bytes for r in res_s if not r)
                                     + (0 if avail - n_res * layer_cost >= head_cost else self.res_head_bytes))
-        if planner == "off" and n_res == cfg.n_layers and avail - n_res * layer_cost >= head_cost:
-            # Everything fits: there is nothing for the runtime to decide (every
-            # unit stays resident either way) - take the resident path, which
-            # pins once instead of leasing every unit at every use (config 2,
-            # 8B HBM-resident: 11.2 vs 6.4 ms/step).
+        if (planner == "off" and n_res == cfg.n_layers and avail - n_res * layer_cost >= head_cost
+                and os.environ.get("OGKM_FITS_STATIC", "0") != "0"):
+            # (round-4 fallback, now off: with the runtime's resident-extent
+            # lease fast path, leasing every unit at every use costs what the
+            # lifetime pins did - csrc/core/migrate.cpp fast_lease)
             planner = self.planner = "static"
         if planner == "off":
             n_res, avail = 0, 0
@@ -597,6 +597,16 @@ class TieredLlama:
         # ``max_ahead`` streamed units back instead (OGKM_MAX_AHEAD).
         self._ahead = collections.deque()
         self.max_ahead = int(os.environ.get("OGKM_MAX_AHEAD", "0")) or (self.lookahead + self.runahead)
+        # The per-unit protocol (clock, prefetch window, lease, GPU-side wait,
+        # next-use hint; release + run-ahead bound) runs natively: two calls
+        # per unit instead of ~100 us of Python (csrc/core/unit_stream.cpp).
+        # OGKM_NATIVE_UNITS=0: the Python protocol below (diagnostics use it).
+        self._us = None
+        if (self.sworld <= 1 and self.stream_seq and not self.dry_run
+                and os.environ.get("OGKM_NATIVE_UNITS", "1") != "0"):
+            self._us = lib.UnitStream(device, [self._buf(k).id for k in self.stream_seq], self.window_bytes,
+                                      self.next_use, 0 if self.fake else self.max_ahead)
+        self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
         self._views: dict = {}
         self.byte_trace = None     # diagnostics: {key: H2D bytes submitted around its use}
         self.use_trace = None      # diagnostics: [(key, acquire s, wait s)] per streamed use
@@ -937,7 +947,9 @@ class TieredLlama:
             pre = rt._tensor_from_ptr(ptr, (2, self.B, self.hkv, self.ctx, hd), torch.bfloat16,
                                       "cpu" if self.fake else "cuda", self.dev)
             sc[:, :, :, :self.ctx].copy_(pre)
-        if lease is not None:  # the prefix's readers are enqueued: the unit may be evicted behind them
+        if isinstance(lease, tuple):  # native unit protocol: release + run-ahead bound in one call
+            self._us.release(lease[1], self._stream_handle())
+        elif lease is not None:  # the prefix's readers are enqueued: the unit may be evicted behind them
             lease.release(0 if self.fake else None)
             self._mark_consumed()
         t = pos - self.ctx
@@ -1033,9 +1045,38 @@ class TieredLlama:
             p = self._seq_pos[key]
             self._buf(key).hint_next_use(self._pass * n + p + n)
 
+    def _native(self) -> bool:
+        """Native unit protocol in use (not when a diagnostic needs the Python one)."""
+        return self._us is not None and not (self.diag or self.byte_trace is not None or self.use_trace is not None)
+
+    def _stream_handle(self) -> int:
+        if self.fake:
+            return 0
+        if self._raw_stream is not None:
+            return self._raw_stream(self.dev)
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def stream_stats(self) -> dict:
+        """Streaming counters (bench.py aux stream_stats): prefetches issued /
+        refused by the victim floor, uses not prefetched, host ms in prefetch /
+        acquire / the run-ahead bound."""
+        out = dict(self.sstats)
+        if self._us is not None:
+            for k, v in self._us.stats().items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def reset_stream_stats(self) -> None:
+        self.sstats = dict.fromkeys(self.sstats, 0)
+        if self._us is not None:
+            self._us.reset_stats()
+
     def _prefetch_ahead(self) -> None:
         """Keep up to ``window_bytes`` of upcoming streamed tensors in flight on the ring."""
         if not self.stream_seq:
+            return
+        if self._native():
+            self._us.prefetch_window()
             return
         inflight = sum(self._inflight_b.get(k, 0) for k in self._inflight)
         n = len(self.stream_seq)
@@ -1084,6 +1125,14 @@ class TieredLlama:
             pin = self._pin_resident(key)
         if pin is not None:  # resident tensor: long-lived lease taken at init, refs cached
             return None, (self._unstage(key, pin.ptr) if self.staged else pin)
+        if self._native() and key in self._seq_pos:
+            stream = self._stream_handle()
+            lid, dptr = self._us.use(self._seq_pos[key], stream)
+            if self.staged:
+                st = self._unstage(key, dptr)
+                self._us.release(lid, stream)
+                return None, st
+            return ("native", lid), self._ref(key, dptr, self.pmode.get(key, dgemm.MODE_RAW))
         acct = self.byte_trace is not None
         if acct:
             b0 = lib.stats()["bytes_xfer_htd"]
@@ -1129,6 +1178,9 @@ class TieredLlama:
             ptr = self._pin_resident(key)
         if ptr is not None:
             return None, ptr
+        if self._native() and key in self._seq_pos:
+            lid, dptr = self._us.use(self._seq_pos[key], self._stream_handle())
+            return ("native", lid), dptr
         if not self._is_resident(key):
             if self._inflight and self._inflight[0] == key:
                 self._inflight.pop(0)
@@ -1185,7 +1237,9 @@ class TieredLlama:
         return dgemm.WeightRef(ptr, 0, n, k, mode, shift)
 
     def _done(self, lease) -> None:
-        if isinstance(lease, tuple):  # a gather slot read by the kernels just enqueued
+        if isinstance(lease, tuple) and lease[0] == "native":  # release + run-ahead bound, natively
+            self._us.release(lease[1], self._stream_handle())
+        elif isinstance(lease, tuple):  # a gather slot read by the kernels just enqueued
             self.gather.done(lease[1])
             self._mark_consumed()
         elif lease is not None:
@@ -1297,6 +1351,7 @@ class TieredLlama:
     def close(self) -> None:
         if self.gather is not None:
             self.gather.drain()
+        self._us = None  # (its run-ahead events synchronised) before the ranges go
         self.kv_lease.release(0 if self.fake else None)
         for lease in self._pin_leases:
             lease.release(0 if self.fake else None)

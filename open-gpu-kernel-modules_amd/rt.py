@@ -297,9 +297,10 @@ class ManagedBuffer:
         lib.evict(self.id, t, i)
 
     # -- software faults
-    def acquire(self, proc: int = 0, access: int = READ, offset: int = 0, length: Optional[int] = None) -> Lease:
+    def acquire(self, proc: int = 0, access: int = READ, offset: int = 0, length: Optional[int] = None,
+                allow_remote: bool = True) -> Lease:
         length = self.size - offset if length is None else length
-        return Lease(self, lib.acquire(self.id, offset, length, proc, access), proc, offset, length)
+        return Lease(self, lib.acquire(self.id, offset, length, proc, access, allow_remote), proc, offset, length)
 
     # -- data
     def write(self, data, offset: int = 0) -> None:

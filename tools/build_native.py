@@ -97,7 +97,10 @@ def build(debug: bool = False, jobs: int | None = None, verbose: bool = False) -
     newest = max(o.stat().st_mtime for o in objs)
     if out.exists() and out.stat().st_mtime >= newest:
         return out
-    link = [str(ROCM / "bin" / "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out)]
+    # link to a temporary file and rename it over the old library: processes
+    # that have the old one mapped (a running test suite) keep their inode
+    tmp = out.with_name(out.name + ".tmp")
+    link = [str(ROCM / "bin" / "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)]
     link += [str(o) for o in sorted(objs)]
     link += [f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64", "-lhsa-runtime64",
              "-lrocprofiler-sdk-roctx", "-lnuma",
@@ -105,6 +108,7 @@ def build(debug: bool = False, jobs: int | None = None, verbose: bool = False) -
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(link)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, out)
     return out
 
 
