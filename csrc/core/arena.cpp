@@ -735,6 +735,19 @@ bool ChunkArena::try_pin_many(const uint32_t* idx, size_t n) {
   return true;
 }
 
+bool ChunkArena::pin_touch_many(const TouchReq* r, size_t n) {
+  std::lock_guard<OrderedMutex> g(m_);
+  for (size_t k = 0; k < n; ++k)
+    if (chunks_[r[k].chunk].state != ChunkState::ALLOCATED) return false;
+  for (size_t k = 0; k < n; ++k) {
+    const TouchReq& t = r[k];
+    if (chunks_[t.chunk].pin_count++ == 0) st_.pinned += kBlockSize;
+    touch_locked(t.chunk, t.has_data, t.preferred, t.prefetched, t.refault_key, t.evicted_at, t.clean);
+    if (t.next_use) set_next_use_locked(t.chunk, t.next_use);
+  }
+  return true;
+}
+
 void ChunkArena::release_many(const uint32_t* idx, size_t n, const FenceRef& f) {
   std::lock_guard<OrderedMutex> g(m_);
   for (size_t k = 0; k < n; ++k) {

@@ -136,23 +136,32 @@ Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool 
 
 // LRU bump of a block's chunk at one location: data-less chunks go to the
 // unused list, chunks whose data prefers this location to the protected list.
-void Runtime::touch_residency(Block* b, Residency* r, bool prefetched) {
-  if (!r || r->chunk < 0) return;
-  bool pref = b->policy.has_preferred && b->policy.preferred == r->loc;
+// What touch_residency tells the arena about residency r of block b (lock held).
+static ChunkArena::TouchReq touch_req(Block* b, Residency* r, bool prefetched) {
+  ChunkArena::TouchReq t{};
+  t.chunk = (uint32_t)r->chunk;
+  t.preferred = b->policy.has_preferred && b->policy.preferred == r->loc;
+  t.has_data = !r->resident.empty();
+  t.prefetched = prefetched;
   const bool refault = r->loc.is_gpu() && b->gpu_evictions > 0;
-  bool clean = false;
+  t.refault_key = refault ? b->range->id + 1 : 0;
+  t.evicted_at = b->gpu_evicted_at;
   if (r->loc.is_gpu() && config().evict_clean_first) {
     PageMask others;
     for (auto& x : b->res)
       if (&x != r) others |= x.resident;
-    clean = r->resident.andnot(others).empty();
+    t.clean = r->resident.andnot(others).empty();
   }
-  r->arena->touch((uint32_t)r->chunk, !r->resident.empty(), pref, prefetched, refault ? b->range->id + 1 : 0,
-                  b->gpu_evicted_at, clean);
-  if (r->loc.is_gpu()) {
-    const uint64_t nu = b->range->dead.load(std::memory_order_relaxed) ? kDeadUse : b->range->next_use.load();
-    if (nu) r->arena->set_next_use((uint32_t)r->chunk, nu);
-  }
+  if (r->loc.is_gpu())
+    t.next_use = b->range->dead.load(std::memory_order_relaxed) ? kDeadUse : b->range->next_use.load();
+  return t;
+}
+
+void Runtime::touch_residency(Block* b, Residency* r, bool prefetched) {
+  if (!r || r->chunk < 0) return;
+  const ChunkArena::TouchReq t = touch_req(b, r, prefetched);
+  r->arena->touch(t.chunk, t.has_data, t.preferred, t.prefetched, t.refault_key, t.evicted_at, t.clean);
+  if (t.next_use) r->arena->set_next_use(t.chunk, t.next_use);
 }
 
 // Next-use hint of a whole range (the transparent mode's op trace): stored on
@@ -177,6 +186,29 @@ void Runtime::hint_next_use(Range* r, uint64_t when) {
       arena = x.arena;
       idx.push_back((uint32_t)x.chunk);
     }
+  }
+  if (arena && !idx.empty()) arena->set_next_use_many(idx.data(), idx.size(), when);
+}
+
+void Runtime::hint_next_use(Lease* l, uint64_t when) {
+  Range* r = l->range;
+  // a partial or remote lease does not hold every HBM chunk of the range
+  if (l->offset != 0 || l->bytes != r->size || l->remote || l->proc == kCpuProc ||
+      l->pinned_chunks.size() != r->blocks.size()) {
+    hint_next_use(r, when);
+    return;
+  }
+  when = classify_hint(r, when);
+  r->next_use.store(when);
+  std::vector<uint32_t> idx;
+  ChunkArena* arena = nullptr;
+  for (auto& pc : l->pinned_chunks) {
+    if (arena && pc.first != arena) {
+      arena->set_next_use_many(idx.data(), idx.size(), when);
+      idx.clear();
+    }
+    arena = pc.first;
+    idx.push_back(pc.second);
   }
   if (arena && !idx.empty()) arena->set_next_use_many(idx.data(), idx.size(), when);
 }
@@ -1778,8 +1810,10 @@ bool Runtime::fast_lease(Range* r, uint64_t off, uint64_t len, int proc, Lease* 
   const uint32_t n = (uint32_t)(b1 - b0 + 1);
   std::vector<Block*> bl;
   std::vector<uint32_t> ch;
+  std::vector<ChunkArena::TouchReq> tr;
   bl.reserve(n);
   ch.reserve(n);
+  tr.reserve(n);
   Tracker ready;
   bool ok = true;
   for (uint32_t k = 0; k < n && ok; ++k) {
@@ -1799,10 +1833,11 @@ bool Runtime::fast_lease(Range* r, uint64_t off, uint64_t len, int proc, Lease* 
     b->lease_pins++;
     bl.push_back(b);
     ch.push_back((uint32_t)x->chunk);
-    touch_residency(b, x);
+    tr.push_back(touch_req(b, x, false));
     ready.merge(b->tracker);
   }
-  if (ok) ok = ga->try_pin_many(ch.data(), ch.size());
+  // pins + LRU / next-use touches of every chunk under one arena lock
+  if (ok) ok = ga->pin_touch_many(tr.data(), tr.size());
   if (!ok) {
     for (Block* b : bl) {
       std::lock_guard<OrderedMutex> g(b->lock);
@@ -1818,7 +1853,7 @@ bool Runtime::fast_lease(Range* r, uint64_t off, uint64_t len, int proc, Lease* 
   return true;
 }
 
-Status Runtime::release(Lease* l, void* stream) {
+Status Runtime::release(Lease* l, void* stream, const FenceRef& use) {
   if (!l) return Status::INVALID_ARGUMENT;
   std::unique_ptr<Lease> own;
   {
@@ -1829,7 +1864,7 @@ Status Runtime::release(Lease* l, void* stream) {
     leases_.erase(it);
   }
   FenceRef f;
-  if (l->proc != kCpuProc && !l->pinned_chunks.empty()) f = fence_record(be_.get(), l->proc, stream);
+  if (l->proc != kCpuProc && !l->pinned_chunks.empty()) f = use ? use : fence_record(be_.get(), l->proc, stream);
   // Chunks of one arena: fence + unpin + LRU touch under one arena lock.
   std::vector<uint32_t> idx;
   ChunkArena* cur = nullptr;

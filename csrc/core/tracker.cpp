@@ -111,10 +111,19 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
     // previous readers ran on the consumer's own stream - every resident unit
     // of a decode step).
     if (f->event && f->stream == stream && stream) continue;
+    // Already retired (the flag is only set by whoever polled last): no packet.
+    if (f->ring && !f->event && f->ring->completed_seq() >= f->seq) {
+      f->done.store(true, std::memory_order_release);
+      continue;
+    }
     Status s;
     uint64_t t0 = now_ns();
     bool had_event = f->event != nullptr;
     bool ev_done = had_event && be->event_query(f->event);
+    if (ev_done && (!f->ring || f->ring->completed_seq() >= f->seq)) {
+      f->done.store(true, std::memory_order_release);
+      continue;
+    }
     if (f->event) s = be->stream_wait_event(stream, f->event);
     else if (f->ring) {
       // Tracking-value fence: make sure the ring work is submitted, then let

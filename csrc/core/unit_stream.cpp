@@ -12,10 +12,7 @@ UnitStream::UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_
       max_ahead_(max_ahead) {}
 
 UnitStream::~UnitStream() {
-  for (void* e : ahead_) {
-    (void)rt_->be()->event_sync(e);
-    rt_->be()->event_destroy(e);
-  }
+  for (auto& f : ahead_) (void)f->wait();
 }
 
 uint64_t UnitStream::due(uint32_t pos) const {
@@ -73,7 +70,7 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
   if (st != Status::OK) return st;
   // hinted once leased (before, the prefetches queued for this use would see it
   // as the furthest-needed unit and evict it): next used one pass later
-  if (next_use_) rt_->hint_next_use(r, pass_ * n + pos + n);
+  if (next_use_) rt_->hint_next_use(*out, pass_ * n + pos + n);
   // the consumer's stream waits GPU-side (no stream: the host waits)
   st = stream ? (*out)->ready.gpu_wait(rt_->be(), stream) : (*out)->ready.wait();
   if (st != Status::OK) {
@@ -84,23 +81,21 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
 }
 
 Status UnitStream::release(Lease* l, void* stream) {
-  Status st = rt_->release(l, stream);
-  if (!max_ahead_ || !stream) return st;
+  if (!stream) return rt_->release(l, stream);
+  // ONE event after the unit's kernels serves both the runtime's reuse fence of
+  // its chunks and the run-ahead bound below (each event record is a barrier
+  // packet with a cache writeback on the consumer's stream).
+  FenceRef f = l->proc != kCpuProc ? fence_record(rt_->be(), l->proc, stream) : nullptr;
+  Status st = rt_->release(l, stream, f);
+  if (!max_ahead_ || !f || !f->event) return st;
   // Bounded run-ahead: leases wait GPU-side, so without a bound the host would
   // prefetch a whole step ahead and the ring would evict (and wait on) chunks
   // whose readers are still queued - the copies then serialise behind compute.
-  void* e = rt_->be()->event_create(dev_);
-  if (!e) return st;
-  if (rt_->be()->event_record(e, stream) != Status::OK) {
-    rt_->be()->event_destroy(e);
-    return st;
-  }
-  ahead_.push_back(e);
+  ahead_.push_back(std::move(f));
   while (ahead_.size() > max_ahead_) {
     const uint64_t t0 = now_ns();
-    (void)rt_->be()->event_sync(ahead_.front());
+    (void)ahead_.front()->wait();
     st_.ahead_wait_ns += now_ns() - t0;
-    rt_->be()->event_destroy(ahead_.front());
     ahead_.pop_front();
   }
   return st;

@@ -154,6 +154,14 @@ class ChunkArena {
   // under one lock, or none (false) when any is no longer ALLOCATED; release
   // = reuse fence + unpin + LRU touch of each, under one lock.
   bool try_pin_many(const uint32_t* idx, size_t n);
+  // The same plus each chunk's touch (and next-use hint when nonzero): the
+  // whole lease fast path's arena work under one lock instead of two per block.
+  struct TouchReq {
+    uint32_t chunk;
+    bool has_data, preferred, prefetched, clean;
+    uint64_t refault_key, evicted_at, next_use;
+  };
+  bool pin_touch_many(const TouchReq* r, size_t n);
   void release_many(const uint32_t* idx, size_t n, const FenceRef& f);
   void pin(uint32_t i);
   // Pin only an ALLOCATED chunk: false when it is reserved for eviction (or

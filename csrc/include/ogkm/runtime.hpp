@@ -212,7 +212,9 @@ class Runtime {
   // fixed device address, e.g. the stable VA of a managed torch tensor).
   Status acquire(Range* r, uint64_t off, uint64_t len, int proc, Access access, Lease** out,
                  bool allow_remote = true);
-  Status release(Lease* l, void* stream);  // consumer's last use recorded on `stream`
+  // consumer's last use recorded on `stream` (or `use`: a fence the caller
+  // recorded on it after its last use, shared with its own bookkeeping)
+  Status release(Lease* l, void* stream, const FenceRef& use = nullptr);
   // acquire() fast path: a GPU read of a range span resident in one contiguous
   // extent of that GPU's arena - pin + touch + readiness only (false: take the
   // full path).
@@ -226,6 +228,9 @@ class Runtime {
   // Next-use (Belady) eviction hints: the op-clock time of r's next use, and the
   // current op clock of a device's HBM arena (see ChunkArena::set_next_use).
   void hint_next_use(Range* r, uint64_t when);
+  // The same for a range leased whole: its HBM chunks are the lease's pinned
+  // chunks (no block walk).
+  void hint_next_use(Lease* l, uint64_t when);
   void set_op_clock(int dev, uint64_t now);
   void reset_op_clock(int dev);
   // The spread class flag (0 / kEvictFirst) the runtime gives a hint of r that

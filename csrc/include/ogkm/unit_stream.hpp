@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "ogkm/common.hpp"
+#include "ogkm/tracker.hpp"
 
 namespace ogkm {
 
@@ -63,7 +64,7 @@ class UnitStream {
   uint64_t inflight_bytes_ = 0;
   uint64_t pass_ = 0;
   int64_t last_pos_ = -1;
-  std::deque<void*> ahead_;  // events of released units (host bound)
+  std::deque<FenceRef> ahead_;  // fences of released units (host bound)
   Stats st_;
 };
 

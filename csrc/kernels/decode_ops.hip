@@ -504,10 +504,8 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
     // half-wave-per-token loop had 2 KB in flight and capped the tp8 shape,
     // one KV head per batch row, at ~1.3 TB/s). The token groups' partial
     // sums are reduced with xor shuffles at the end.
-    // DPL dims per lane (template): 8 - one 16 B load per row piece, 8 KB in
-    // flight per wave, 164 VGPRs for 8 heads - when the grid has few waves per
-    // SIMD (one KV head per batch row: the tp8 shapes); 4 - 96 VGPRs, four
-    // waves per SIMD - when it has many, and always for 16 heads.
+    // DPL dims per lane (template): 8 - one 16 B load per row piece (groups of
+    // up to 4 heads); 4 - 96 VGPRs and four waves per SIMD for 8 and 16 heads.
     static_assert(DPL == 8 || DPL == 4, "dims per lane");
     constexpr int LPT = HD / DPL, TPI = 64 / LPT, NI = 64 / TPI;
     constexpr int VB = 8;
@@ -654,9 +652,10 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
   if (ws) {
 #define OGKM_ATTN_WS(HD, L, NW, D) \
   hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW, D>), grid, dim3(64 * NW), lds, s, a)
-    // few waves per SIMD (<= 2 of the chip's 1024 SIMDs' worth): the wide rows
-    static const int force_dpl = getenv("OGKM_ATTN_DPL") ? atoi(getenv("OGKM_ATTN_DPL")) : 0;  // A/B drills
-    const bool wide = force_dpl ? force_dpl == 8 : (uint64_t)grid.x * grid.y * grid.z * nw <= 2048;
+    // groups of 8: 4 dims per lane at every measured shape (70B tp8 1.56 vs 1.42 TB/s with 8,
+    // 70B 3.76 vs 2.70; gpurun_out/r5/g_attn_dpl*.log); OGKM_ATTN_DPL=8 for A/B drills
+    static const int force_dpl = getenv("OGKM_ATTN_DPL") ? atoi(getenv("OGKM_ATTN_DPL")) : 0;
+    const bool wide = force_dpl == 8;
 #define OGKM_ATTN_WS_G(HD, NW)                      \
   if (gg == 4) OGKM_ATTN_WS(HD, 4, NW, 8);          \
   else if (gg == 8 && wide) OGKM_ATTN_WS(HD, 8, NW, 8); \
