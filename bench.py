@@ -289,7 +289,11 @@ def run_torch_managed(a) -> None:
     # allocations >= OGKM_MANAGED_MIN_MB are managed (evictable) ranges; the
     # op-trace prefetcher looks OGKM_MANAGED_LOOKAHEAD_MB ahead (-1: a quarter of the arena)
     allocator.enable(managed_min_mb=int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")))
-    rt.init("hip", hbm_budget={0: budget}, host_budget_mb=0)
+    # packed host copies (packer.cpp): weights dropped clean from HBM are
+    # ANS1-packed by host encoder threads during warmup; OGKM_PACK=0 keeps raw
+    pack = int(os.environ.get("OGKM_PACK", "1"))
+    rt.init("hip", hbm_budget={0: budget}, host_budget_mb=0, pack_host_copies=pack,
+            pack_threads=int(os.environ.get("OGKM_PACK_THREADS", "12")))
     torch.cuda.set_device(0)
     prefill = a.context - (a.warmup + a.steps) - 1
     la = int(os.environ.get("OGKM_MANAGED_LOOKAHEAD_MB", "-1"))
@@ -312,6 +316,24 @@ def run_torch_managed(a) -> None:
             tok = model.step(tok, pos)
             pos += 1
         torch.cuda.synchronize()
+        # setup, not timed: let the packer finish the host copies the warmup
+        # steps released (then one more step refills HBM from them)
+        t_p = time.perf_counter()
+        packed_all = True
+        if pack:
+            limit = float(os.environ.get("OGKM_PACK_WAIT_S", "900"))
+            while not lib.pack_wait(20000):  # progress lines: a silent minute reads as a hang
+                ps = lib.pack_stats()
+                print(f"packing: {ps['packed_blocks']} blocks packed, {ps['queued']} queued "
+                      f"({time.perf_counter() - t_p:.0f} s)", file=sys.stderr, flush=True)
+                if time.perf_counter() - t_p > limit:
+                    packed_all = False
+                    break
+        pack_s = time.perf_counter() - t_p
+        if pack:
+            tok = model.step(tok, pos)
+            pos += 1
+            torch.cuda.synchronize()
         lib.reset_counters()
         al0 = allocator.stats()
         t0 = time.perf_counter()
@@ -347,6 +369,9 @@ def run_torch_managed(a) -> None:
                                      for k in ("place_stable", "vmm_map", "vmm_unmap", "tlb_flush", "stable_wait")},
                 "ring_per_step": _ring_per_step(s, a.steps),
                 "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches, "init_s": round(init_s, 1),
+                "pack": dict(lib.pack_stats(), wait_s=round(pack_s, 1), drained=packed_all,
+                             decodes_per_step=s["packed_decodes"] // max(1, a.steps),
+                             expansions=s["pack_expansions"]),
                 "trace_len": len(mode._trace), "hinted_ops": mode.hinted_ops, "trace_misses": mode.trace_misses,
                 "allocs_per_step": (al1["allocs"] - al0["allocs"]) // max(1, a.steps), "alloc_peak_gb":
                 round(al1["peak"] / 1e9, 2), "managed_min_mb": int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")),

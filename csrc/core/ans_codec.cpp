@@ -71,34 +71,53 @@ uint64_t ans_encode(const uint16_t* in, uint32_t n, uint8_t* out, uint64_t cap) 
   uint32_t cum[257];
   cum[0] = 0;
   for (int s = 0; s < 256; ++s) cum[s + 1] = cum[s] + h.freq[s];
+  // Division-free state update: x / f by a 64-bit reciprocal (exact for every
+  // 32-bit x and f >= 2: q = (ceil(2^64 / f) * x) >> 64); f == 1 is x itself.
+  struct Sym {
+    uint64_t rcp;
+    uint32_t f, x_max, cum;
+  } sy[256];
+  for (int s = 0; s < 256; ++s) {
+    const uint32_t f = h.freq[s];
+    sy[s].f = f;
+    sy[s].x_max = f << (32 - kAnsPrecBits);  // x_max = ((L >> prec) << 16) * f
+    sy[s].cum = cum[s];
+    sy[s].rcp = f > 1 ? ~0ull / f + 1 : 0;
+  }
   uint8_t* sm = out + kAnsHeaderBytes;
   for (uint32_t i = 0; i < n; ++i) sm[i] = (uint8_t)(((in[i] >> 8) & 0x80u) | (in[i] & 0x7Fu));
   std::vector<uint32_t> dir(n_seg + 1);
-  std::vector<uint16_t> words;
+  // Renormalisation words are written back to front (the decoder consumes them
+  // in the reverse of the encoding order): at most one per value.
+  std::vector<uint16_t> wbuf(kAnsSegValues + 1);
   for (uint32_t s = 0; s < n_seg; ++s) {
     const uint32_t base = s * kAnsSegValues;
     const uint32_t steps = std::min(kAnsSegValues, n - base) / 64u;
     uint32_t x[64];
     for (auto& v : x) v = kAnsLowBound;
-    words.clear();
+    uint16_t* const wend = wbuf.data() + wbuf.size();  // (w[-1] stays inside: one spare slot)
+    uint16_t* w = wend;
     for (uint32_t t = steps; t-- > 0;) {
+      const uint16_t* row = in + base + (t >> 3) * 512u + (t & 7u);  // value (t/8*64 + l)*8 + t%8
       for (uint32_t l = 64; l-- > 0;) {
-        const uint32_t sym = (in[base + seg_value(t, l)] >> 7) & 0xFF;
-        const uint32_t f = h.freq[sym];
-        if (x[l] >= (f << (32 - kAnsPrecBits))) {  // x_max = ((L >> prec) << 16) * f
-          words.push_back((uint16_t)(x[l] & 0xFFFFu));
-          x[l] >>= 16;
-        }
-        x[l] = ((x[l] / f) << kAnsPrecBits) + (x[l] % f) + cum[sym];
+        const Sym& y = sy[(row[l * 8u] >> 7) & 0xFF];
+        uint32_t v = x[l];
+        // branch-free renormalisation (the branch is a coin flip ~1 value in 6)
+        const uint32_t r = v >= y.x_max;
+        w[-1] = (uint16_t)(v & 0xFFFFu);
+        w -= r;
+        v = r ? v >> 16 : v;
+        const uint32_t q = y.rcp ? (uint32_t)(((unsigned __int128)y.rcp * v) >> 64) : v;
+        x[l] = (q << kAnsPrecBits) + (v - q * y.f) + y.cum;
       }
     }
-    std::reverse(words.begin(), words.end());
+    const uint64_t nw = (uint64_t)(wend - w);
     dir[s] = (uint32_t)pos;
-    const uint64_t bytes = 256 + ((words.size() * 2 + 3) & ~3ull);
+    const uint64_t bytes = 256 + ((nw * 2 + 3) & ~3ull);
     if (pos + bytes > cap) return 0;
     memcpy(out + pos, x, 256);
-    if (!words.empty()) memcpy(out + pos + 256, words.data(), words.size() * 2);
-    if (words.size() & 1) memset(out + pos + 256 + words.size() * 2, 0, 2);
+    if (nw) memcpy(out + pos + 256, w, nw * 2);
+    if (nw & 1) memset(out + pos + 256 + nw * 2, 0, 2);
     pos += bytes;
   }
   dir[n_seg] = (uint32_t)pos;

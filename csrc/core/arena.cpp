@@ -692,22 +692,42 @@ void ChunkArena::cancel(const Reservation& r) {
 
 void ChunkArena::free(uint32_t first, uint32_t n) {
   std::lock_guard<OrderedMutex> g(m_);
-  for (uint32_t i = 0; i < n; ++i) {
-    uint32_t k = first + i;
-    ChunkInfo& c = chunks_[k];
-    RT_ASSERT_RELEASE(c.state == ChunkState::ALLOCATED);
-    lru_remove(k);
-    if (c.pin_count) st_.pinned -= kBlockSize;
-    c.state = ChunkState::FREE;
-    c.owner = nullptr;
-    c.pin_count = 0;
-    c.next_use = 0;
-    c.zeroed = false;
-    deactivate(c);
+  for (uint32_t i = 0; i < n; ++i) free_locked(first + i);
+}
+
+void ChunkArena::free_locked(uint32_t k) {
+  ChunkInfo& c = chunks_[k];
+  RT_ASSERT_RELEASE(c.state == ChunkState::ALLOCATED);
+  lru_remove(k);
+  if (c.pin_count) st_.pinned -= kBlockSize;
+  c.state = ChunkState::FREE;
+  c.owner = nullptr;
+  c.pin_count = 0;
+  c.next_use = 0;
+  c.zeroed = false;
+  c.doomed = false;
+  deactivate(c);
+  add_run(k, 1);
+  st_.allocated -= kBlockSize;
+  st_.frees++;
+}
+
+void ChunkArena::free_when_unpinned(uint32_t i) {
+  std::lock_guard<OrderedMutex> g(m_);
+  ChunkInfo& c = chunks_[i];
+  if (c.pin_count == 0) {
+    free_locked(i);
+    return;
   }
-  add_run(first, n);
-  st_.allocated -= (uint64_t)n << kBlockShift;
-  st_.frees += n;
+  c.doomed = true;
+  c.owner = nullptr;
+  c.next_use = 0;
+  lru_remove(i);  // not a victim candidate (pinned anyway) nor an LRU entry
+}
+
+void ChunkArena::unpinned_locked(uint32_t k) {
+  st_.pinned -= kBlockSize;
+  if (chunks_[k].doomed) free_locked(k);
 }
 
 void ChunkArena::set_owner(uint32_t i, Block* b) {
@@ -735,17 +755,13 @@ bool ChunkArena::try_pin_many(const uint32_t* idx, size_t n) {
   return true;
 }
 
-bool ChunkArena::pin_touch_many(const TouchReq* r, size_t n) {
+void ChunkArena::touch_many(const TouchReq* r, size_t n) {
   std::lock_guard<OrderedMutex> g(m_);
-  for (size_t k = 0; k < n; ++k)
-    if (chunks_[r[k].chunk].state != ChunkState::ALLOCATED) return false;
   for (size_t k = 0; k < n; ++k) {
     const TouchReq& t = r[k];
-    if (chunks_[t.chunk].pin_count++ == 0) st_.pinned += kBlockSize;
     touch_locked(t.chunk, t.has_data, t.preferred, t.prefetched, t.refault_key, t.evicted_at, t.clean);
     if (t.next_use) set_next_use_locked(t.chunk, t.next_use);
   }
-  return true;
 }
 
 void ChunkArena::release_many(const uint32_t* idx, size_t n, const FenceRef& f) {
@@ -754,7 +770,13 @@ void ChunkArena::release_many(const uint32_t* idx, size_t n, const FenceRef& f) 
     ChunkInfo& c = chunks_[idx[k]];
     if (f) c.reuse_fence.add(f);
     RT_ASSERT_RELEASE(c.pin_count > 0);
-    if (--c.pin_count == 0) st_.pinned -= kBlockSize;
+    if (--c.pin_count == 0) {
+      if (c.doomed) {
+        unpinned_locked(idx[k]);
+        continue;
+      }
+      st_.pinned -= kBlockSize;
+    }
     touch_locked(idx[k], true, false, false, 0, 0, false);
   }
 }
@@ -798,7 +820,7 @@ bool ChunkArena::try_pin(uint32_t i) {
 void ChunkArena::unpin(uint32_t i) {
   std::lock_guard<OrderedMutex> g(m_);
   RT_ASSERT_RELEASE(chunks_[i].pin_count > 0);
-  if (--chunks_[i].pin_count == 0) st_.pinned -= kBlockSize;
+  if (--chunks_[i].pin_count == 0) unpinned_locked(i);
 }
 
 bool ChunkArena::pinned(uint32_t i) {

@@ -406,6 +406,14 @@ class FakeBackend : public Backend {
     });
     return Status::OK;
   }
+  Status decode_ans_blocks(int, const DecodeDesc* d, size_t n, void* s) override {
+    std::vector<DecodeDesc> v(d, d + n);
+    run(s, [v] {
+      for (auto& x : v)
+        if (!ans_decode((const uint8_t*)x.src, (uint16_t*)x.dst, x.n_values)) memset((void*)x.dst, 0, 2ull * x.n_values);
+    });
+    return Status::OK;
+  }
   Status unpack_bf12_stream(int, uint64_t src, uint64_t dst, uint32_t, uint32_t, uint64_t n, void* s,
                             uint32_t, uint64_t dst_stride, uint32_t row_shift) override {
     run(s, [src, dst, n, dst_stride, row_shift] {

@@ -694,6 +694,27 @@ class HipBackend : public Backend {
     return Status::OK;
   }
 
+  Status decode_ans_blocks(int, const DecodeDesc* d, size_t n, void* s) override {
+    for (size_t base = 0; base < n; base += kAnsInlineBlocks) {
+      const size_t cnt = std::min<size_t>(n - base, kAnsInlineBlocks);
+      KAnsBlocks b;
+      uint32_t items = 0;
+      for (size_t i = 0; i < cnt; ++i) {
+        const DecodeDesc& x = d[base + i];
+        b.src[i] = x.src;
+        b.dst[i] = x.dst;
+        b.n_values[i] = x.n_values;
+        b.item_start[i] = items;
+        const uint32_t segs = (x.n_values + kAnsSegValues - 1) / kAnsSegValues;
+        items += (segs + 3) / 4;  // 4 segments (waves) per 256-thread item
+      }
+      b.item_start[cnt] = items;
+      HIPCHK(launch_ans_blocks(b, (uint32_t)cnt, (hipStream_t)s, decode_err()));
+      launches_++;
+    }
+    return Status::OK;
+  }
+
   Status unpack_bf12_stream(int, uint64_t src, uint64_t dst, uint32_t nchunks, uint32_t chunk_values, uint64_t,
                             void* s, uint32_t workgroups, uint64_t dst_stride, uint32_t row_shift) override {
     HIPCHK(launch_bf12_unpack((const void*)src, (void*)dst, nchunks, chunk_values, workgroups, (hipStream_t)s,

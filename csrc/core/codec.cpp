@@ -9,6 +9,12 @@
 
 namespace ogkm {
 
+bool block_decode(uint8_t fmt, const uint8_t* in, uint16_t* out, uint32_t n_values) {
+  if (fmt == 1) return bf12_decode(in, out, n_values);
+  if (fmt == 2) return ans_decode(in, out, n_values);
+  return false;
+}
+
 uint64_t bf12_encode(const uint16_t* in, uint32_t n, uint8_t* out, uint64_t cap) {
   if (n == 0 || (n & 1) || n > kBf12Tile * kBf12MaxTiles) return 0;
   // 1) exponent histogram -> base maximising the values covered by codes 0..14

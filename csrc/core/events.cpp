@@ -154,7 +154,12 @@ const char* counter_name(Counter c) {
                             "ring_copy_calls",
                             "demotion_fallbacks",
                             "ledger_refusals",
-                            "lease_fast_paths"};
+                            "lease_fast_paths",
+                            "packed_blocks",
+                            "packed_bytes_saved",
+                            "pack_skips",
+                            "pack_expansions",
+                            "packed_decodes"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

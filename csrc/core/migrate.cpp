@@ -382,12 +382,22 @@ static Ring* ring_for(Runtime* rt, const Loc& s, const Loc& d) {
 static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from, Residency* to,
                          const PageMask& pages) {
   if (pages.empty()) return Status::OK;
+  // A packed copy that lost pages since (a write elsewhere revoked them) is no
+  // whole-block source any more: back to raw pages first.
+  if (from->fmt == 2 && !(from->resident == b->valid_pages())) {
+    Status st = rt->expand_packed(b, from);
+    if (st != Status::OK) return st;
+  }
+  if (to->fmt == 2 && !from->fmt) {  // raw pages into a packed copy (a write-back): raw first
+    Status st = rt->expand_packed(b, to);
+    if (st != Status::OK) return st;
+  }
   Ring* ring = ring_for(rt, from->loc, to->loc);
   Counter ctr = xfer_counter(from->loc, to->loc);
   // Bytes that actually cross the link (an encoded block moves its encoded size).
-  uint64_t bytes = from->fmt == 1 ? from->enc_bytes : (uint64_t)pages.count() << kPageShift;
+  uint64_t bytes = from->fmt ? from->enc_bytes : (uint64_t)pages.count() << kPageShift;
   Tools::get().inc(ctr, bytes);
-  if (from->fmt == 1 && to->loc.is_gpu()) Tools::get().inc(Counter::DecodedBytes, (uint64_t)b->npages << kPageShift);
+  if (from->fmt && to->loc.is_gpu()) Tools::get().inc(Counter::DecodedBytes, (uint64_t)b->npages << kPageShift);
   if (c.cause == Cause::Prefetch) {
     if (to->loc.is_gpu()) Tools::get().inc(Counter::PrefetchBytesXferHtD, bytes);
     else Tools::get().inc(Counter::PrefetchBytesXferDtH, bytes);
@@ -422,10 +432,10 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     // CPU <-> CPU (host / CXL tiers): synchronous memcpy.
     reuse.wait();
     pend.wait();
-    if (from->fmt == 1) {
+    if (from->fmt) {
       memcpy((void*)page_addr(to->arena, to->chunk, 0), (const void*)page_addr(from->arena, from->chunk, 0),
              from->enc_bytes);
-      to->fmt = 1;
+      to->fmt = from->fmt;
       to->enc_bytes = from->enc_bytes;
     } else {
       pages.for_each_run([&](uint32_t p, uint32_t n) {
@@ -445,20 +455,23 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
     ring->push_wait(f);
   }
-  if (from->fmt == 1) {
-    // Encoded source: one fused copy+decode of the whole block into HBM, or a
-    // verbatim copy of the encoded bytes into another host / CXL chunk.
+  if (from->fmt) {
+    // Encoded source: the whole block decoded into HBM - BF12 by one fused
+    // copy+decode kernel, ANS1 packed bytes staged by SDMA and decoded in HBM
+    // (Ring DECODE_ANS) - or a verbatim copy of the encoded bytes into another
+    // host / CXL chunk.
     Sqe s;
-    s.op = to->loc.is_gpu() ? SqeOp::DECODE_BF12 : SqeOp::COPY;
+    s.op = !to->loc.is_gpu() ? SqeOp::COPY : (from->fmt == 1 ? SqeOp::DECODE_BF12 : SqeOp::DECODE_ANS);
     s.dst = page_addr(to->arena, to->chunk, 0);
     s.src = page_addr(from->arena, from->chunk, 0);
-    s.bytes = to->loc.is_gpu() ? (uint64_t)b->npages << kPageShift : from->enc_bytes;
+    s.bytes = to->loc.is_gpu() && from->fmt == 1 ? (uint64_t)b->npages << kPageShift : from->enc_bytes;
+    s.n_values = b->npages << (kPageShift - 1);
     s.user_data = b->range->id;
     s.file = __FILE__;
     s.line = __LINE__;
     ring->push(std::move(s));
     if (!to->loc.is_gpu()) {
-      to->fmt = 1;
+      to->fmt = from->fmt;
       to->enc_bytes = from->enc_bytes;
     }
   } else if (pages.runs() >= (uint32_t)std::max<int64_t>(2, config().copy_page_list_min_runs)) {
@@ -568,7 +581,7 @@ static void drop_residency(Runtime::Ctx& c, Block* b, const Loc& l) {
     } else {
       Tracker t = b->tracker;  // pending writers into the chunk
       for (auto& f : t.fences()) r->arena->add_reuse_fence((uint32_t)r->chunk, f);
-      r->arena->free((uint32_t)r->chunk, 1);
+      r->arena->free_when_unpinned((uint32_t)r->chunk);  // (a lease may still read it)
     }
   }
   b->drop(l);
@@ -629,16 +642,13 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
     }
   }
   bool copied = false;
-  if (!missing.empty() && to->fmt == 1) {
-    // Raw pages are about to land in an encoded chunk: expand it in place first.
-    std::vector<uint16_t> tmp((size_t)b->npages << (kPageShift - 1));
-    uint8_t* base = (uint8_t*)to->arena->chunk_addr((uint32_t)to->chunk);
-    Tracker t = b->tracker;
-    t.wait();
-    if (!bf12_decode(base, tmp.data(), (uint32_t)tmp.size())) return Status::IO_ERROR;
-    memcpy(base, tmp.data(), tmp.size() * 2);
-    to->fmt = 0;
-    to->enc_bytes = 0;
+  // Raw pages are about to land in an encoded chunk, or a CPU consumer needs a
+  // packed host copy's pages: expand it in place first. (A migration / prefetch
+  // / eviction between CPU tiers keeps the packed form.)
+  const bool cpu_use = !dst.is_gpu() && (cause == Cause::User || cause == Cause::Coherence);
+  if (to->fmt && (!missing.empty() || (to->fmt == 2 && cpu_use))) {
+    st = expand_packed(b, to);
+    if (st != Status::OK) return st;
   }
   if (!missing.empty()) {
     // Source = closest resident copy per page: same tier first, then HBM peers,
@@ -651,6 +661,33 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
       return r->loc.tier == Tier::HOST ? 2 : 3;
     };
     std::sort(srcs.begin(), srcs.end(), [&](Residency* a, Residency* x) { return rank(a) < rank(x); });
+    // A complete packed copy is a whole-block source: used alone (its decode
+    // writes every page of the chunk - all of them become resident; the other
+    // copies of a complete packed block are clean duplicates) unless the raw
+    // copies hold every missing page.
+    Residency* packed = nullptr;
+    PageMask raw_cover;
+    for (Residency* x : srcs) {
+      if (x->fmt == 2 && x->resident == b->valid_pages()) {
+        if (!packed) packed = x;
+      } else if (!x->fmt) {
+        raw_cover |= x->resident;
+      }
+    }
+    if (packed && cpu_use) {
+      // the CPU reads the destination: raw pages
+      st = expand_packed(b, packed);
+      if (st != Status::OK) return st;
+      packed = nullptr;
+    }
+    if (packed) {
+      if (missing.andnot(raw_cover).empty()) {
+        srcs.erase(std::remove(srcs.begin(), srcs.end(), packed), srcs.end());
+      } else {
+        srcs.assign(1, packed);
+        missing = b->valid_pages().andnot(to->resident);
+      }
+    }
     PageMask left = missing;
     for (Residency* s : srcs) {
       PageMask from_here = left & s->resident;
@@ -741,7 +778,10 @@ static void release_residency_now(Block* b, const Loc& l) {
   if (r->chunk >= 0) {
     Runtime::get()->shootdown(b, r);
     for (auto& f : b->tracker.fences()) r->arena->add_reuse_fence((uint32_t)r->chunk, f);
-    r->arena->free((uint32_t)r->chunk, 1);
+    // A reader may have leased this copy while the migration that revokes it
+    // was in flight (the revocation lands at finish_ctx): the chunk is freed
+    // when that lease ends, never under it.
+    r->arena->free_when_unpinned((uint32_t)r->chunk);
   }
   b->drop(l);
 }
@@ -888,6 +928,9 @@ Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
   if (from.is_gpu()) {
     b->gpu_evictions++;
     b->gpu_evicted_at = a->evictions();
+    // dropped without a copy-out: a clean read duplicate (read-mostly data)
+    if (only_here.empty()) b->clean_evictions++;
+    pack_enqueue(b);
     if (is_local(from.id)) devs_[from.id]->spread.on_evict(b->range->id);
     // Users of the stable VA's mapping of this chunk (see Block::stable_users).
     if (b->range->dev_va && b->stable_chunk.load() == (int64_t)i) {
@@ -1115,6 +1158,10 @@ Status Runtime::evict_range(Range* r, Loc from) {
         drop_residency(c, b, from);
       }
       Tools::get().inc(Counter::Evictions);
+      if (from.is_gpu()) {
+        if (only_here.empty()) b->clean_evictions++;
+        pack_enqueue(b);
+      }
     }
     finish_ctx(c, nullptr);
   }
@@ -1686,6 +1733,8 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
             std::lock_guard<OrderedMutex> g(b->lock);
             int64_t hint = first >= 0 ? first + k : -1;
             Residency* x = b->find(dec[k].dst);
+            if (x && x->fmt) st = expand_packed(b, x);  // read in place: raw pages
+            if (st != Status::OK) break;
             if (!x) {
               st = populate(c, b, dec[k].dst, hint, &x);
               if (st == Status::OK) {
@@ -1830,21 +1879,29 @@ bool Runtime::fast_lease(Range* r, uint64_t off, uint64_t len, int proc, Lease* 
       ok = false;
       break;
     }
+    // The chunk is pinned with the block lock held, together with lease_pins:
+    // a migration that checks for leased copies (make_resident) must never see
+    // the lease count without the pin (it would revoke and free the copy).
+    if (!ga->try_pin((uint32_t)x->chunk)) {
+      ok = false;
+      break;
+    }
     b->lease_pins++;
     bl.push_back(b);
     ch.push_back((uint32_t)x->chunk);
     tr.push_back(touch_req(b, x, false));
     ready.merge(b->tracker);
   }
-  // pins + LRU / next-use touches of every chunk under one arena lock
-  if (ok) ok = ga->pin_touch_many(tr.data(), tr.size());
   if (!ok) {
-    for (Block* b : bl) {
-      std::lock_guard<OrderedMutex> g(b->lock);
-      b->lease_pins--;
+    for (size_t k = 0; k < bl.size(); ++k) {
+      std::lock_guard<OrderedMutex> g(bl[k]->lock);
+      bl[k]->lease_pins--;
+      ga->unpin(ch[k]);
     }
     return false;
   }
+  // LRU / next-use touches of every chunk under one arena lock
+  ga->touch_many(tr.data(), tr.size());
   L->blocks = std::move(bl);
   L->pinned_chunks.reserve(ch.size());
   for (uint32_t c : ch) L->pinned_chunks.emplace_back(ga, c);

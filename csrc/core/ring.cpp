@@ -48,6 +48,7 @@ Ring::~Ring() {
     last_fence_.reset();
     be_->stream_destroy(stream_);
   }
+  if (stage_) be_->hbm_free(dev_, stage_, stage_bytes_);
   if (sem_) be_->host_free_coherent(sem_);
 }
 
@@ -281,6 +282,8 @@ Status Ring::run_batch(Batch& b) {
   std::vector<CopyDesc> copies;
   std::vector<int> copy_dst;  // GPU_TO_GPU: the peer each copy writes
   std::vector<DecodeDesc> decodes;
+  std::vector<DecodeDesc> staged;  // packed blocks whose bytes are on their way into stage_
+  uint64_t stage_off = 0;
   Status st = Status::OK;
   bool kernels_pending = false;
   bool final_flush = false;
@@ -340,6 +343,21 @@ Status Ring::run_batch(Batch& b) {
     copies.clear();
     copy_dst.clear();
   };
+  // Packed blocks: their staging copies go out with the batch's other engine
+  // copies; once those landed ONE k_ans_blocks launch decodes them all. The
+  // next engine copy drains the stream first (flush_copies), so the staging
+  // buffer is never overwritten under a running decode.
+  auto flush_staged = [&] {
+    if (staged.empty()) return;
+    flush_copies();
+    if (st == Status::OK) {
+      st = be_->decode_ans_blocks(dev_, staged.data(), staged.size(), stream_);
+      kernels_pending = true;
+      Tools::get().inc(Counter::PackedDecodes, staged.size());
+    }
+    staged.clear();
+    stage_off = 0;
+  };
   for (auto& s : b.ops) {
     if (st != Status::OK) break;
     switch (s.op) {
@@ -354,13 +372,57 @@ Status Ring::run_batch(Batch& b) {
         }
         break;
       case SqeOp::DECODE_BF12:
+        flush_staged();
         flush_copies();
         decodes.push_back(DecodeDesc{s.src, s.dst, (uint32_t)(s.bytes / 2)});
         break;
+      case SqeOp::DECODE_ANS: {
+        flush_decodes();
+        const uint64_t need = (s.bytes + 255) & ~255ull;
+        if (!stage_ && st == Status::OK && config().ans_stage_mb > 0) {  // (0: decode from the host copy)
+          stage_bytes_ = std::max<uint64_t>((uint64_t)config().ans_stage_mb << 20, 2 * kBlockSize);
+          if (be_->hbm_alloc(dev_, stage_bytes_, &stage_) != Status::OK) {
+            stage_ = nullptr;
+            stage_bytes_ = 0;
+          }
+        }
+        if (!stage_) {  // no staging memory: the decode kernel reads the host copy itself
+          flush_staged();
+          flush_copies();
+          if (st == Status::OK) {
+            DecodeDesc d{s.src, s.dst, s.n_values};
+            st = be_->decode_ans_blocks(dev_, &d, 1, stream_);
+            kernels_pending = true;
+            Tools::get().inc(Counter::PackedDecodes);
+          }
+          break;
+        }
+        if (stage_off + need > stage_bytes_ || staged.size() >= 64) flush_staged();
+        const uint64_t at = (uint64_t)stage_ + stage_off;
+        CopyDesc d{at, s.src, need};
+        // Packed blocks are ~1.3 MB copies that never coalesce: spread them over
+        // several full-rate engines so one engine's per-copy setup overlaps
+        // another's transfer (config ans_stage_engines; 0 = the ring's engine).
+        if (const uint32_t m = (uint32_t)config().ans_stage_engines & be_->copy_engine_mask(dev_, -1)) {
+          const int nb = __builtin_popcount(m);
+          int want = (int)(engine_rot_++ % (uint32_t)nb);
+          for (int bit = 0; bit < 32; ++bit)
+            if (((m >> bit) & 1) && want-- == 0) {
+              d.engine = 1u << bit;
+              break;
+            }
+        }
+        copies.push_back(d);
+        copy_dst.push_back(-1);
+        staged.push_back(DecodeDesc{at, s.dst, s.n_values});
+        stage_off += need;
+        break;
+      }
       case SqeOp::WAIT_FENCE:
         // Dependencies are waited for where the work is issued: here, on the
         // host, before the engine / stream is handed anything after the wait.
         flush_decodes();
+        flush_staged();
         flush_copies();
         if (st == Status::OK && s.wait && !s.wait->done.load(std::memory_order_acquire)) {
           const uint64_t t_wait = now_ns();
@@ -377,6 +439,7 @@ Status Ring::run_batch(Batch& b) {
         break;
       default: {
         flush_decodes();
+        flush_staged();
         flush_copies();
         if (st != Status::OK) break;
         snprintf(phase_what_, sizeof(phase_what_), "kernel op %d (%s:%d %s)", (int)s.op, s.file, s.line,
@@ -396,6 +459,7 @@ Status Ring::run_batch(Batch& b) {
     }
   }
   flush_decodes();
+  flush_staged();
   if (!kernels_pending) final_flush = true;  // (with kernels queued, the drain below comes first)
   flush_copies();
   drain();
@@ -417,7 +481,8 @@ FenceRef Ring::submit_locked() {
   // can only delay a copy that did not need to wait. No wait can depend on a
   // copy of this submission (its fence does not exist until the end).
   auto copy_like = [](SqeOp op) {
-    return op == SqeOp::COPY || op == SqeOp::DECODE_BF12 || op == SqeOp::WAIT_FENCE || op == SqeOp::NOP;
+    return op == SqeOp::COPY || op == SqeOp::DECODE_BF12 || op == SqeOp::DECODE_ANS || op == SqeOp::WAIT_FENCE ||
+           op == SqeOp::NOP;
   };
   for (auto it = sq_.begin(); it != sq_.end();) {
     if (!copy_like(it->second.op)) {
@@ -434,6 +499,7 @@ FenceRef Ring::submit_locked() {
   uint64_t last = 0;
   std::vector<CopyDesc> batch;
   std::vector<DecodeDesc> dbatch;
+  std::vector<DecodeDesc> abatch;  // DECODE_ANS: decoded straight from the host copies
   int engine = kind_ == RingKind::GPU_INTERNAL ? 2
                : (kind_ == RingKind::GPU_TO_GPU && config().peer_copy_engine == 0) ? 4
                                                                                   : (int)config().copy_engine;
@@ -446,8 +512,14 @@ FenceRef Ring::submit_locked() {
       st = be_->decode_bf12(dev_, dbatch.data(), dbatch.size(), stream_);
       Tools::get().inc(Counter::CopyKernelLaunches);
     }
+    if (st == Status::OK && !abatch.empty()) {
+      st = be_->decode_ans_blocks(dev_, abatch.data(), abatch.size(), stream_);
+      Tools::get().inc(Counter::CopyKernelLaunches);
+      Tools::get().inc(Counter::PackedDecodes, abatch.size());
+    }
     batch.clear();
     dbatch.clear();
+    abatch.clear();
   };
   std::vector<std::pair<uint64_t, Cqe>> done;
   for (auto& e : sq_) {
@@ -466,7 +538,7 @@ FenceRef Ring::submit_locked() {
             st = Status::INJECTED_ERROR;
             break;
           }
-          if (!dbatch.empty()) flush();
+          if (!dbatch.empty() || !abatch.empty()) flush();
           // Coalesce physically adjacent copies (consecutive 2 MB blocks of one
           // extent) into a single descriptor.
           if (!batch.empty() && batch.back().dst + batch.back().bytes == s.dst &&
@@ -476,8 +548,12 @@ FenceRef Ring::submit_locked() {
             batch.push_back(CopyDesc{s.dst, s.src, s.bytes});
           break;
         case SqeOp::DECODE_BF12:
-          if (!batch.empty()) flush();
+          if (!batch.empty() || !abatch.empty()) flush();
           dbatch.push_back(DecodeDesc{s.src, s.dst, (uint32_t)(s.bytes / 2)});
+          break;
+        case SqeOp::DECODE_ANS:
+          if (!batch.empty() || !dbatch.empty()) flush();
+          abatch.push_back(DecodeDesc{s.src, s.dst, s.n_values});
           break;
         case SqeOp::GATHER:
         case SqeOp::SCATTER: {

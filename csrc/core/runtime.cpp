@@ -101,6 +101,7 @@ void Runtime::shutdown() {
 void torch_alloc_reset();
 
 Runtime::~Runtime() {
+  stop_packer();
   torch_alloc_reset();
   for (int t : perf_subs_) Tools::get().bus().unsubscribe(t);
   stop_cpu_fault_service();
@@ -469,7 +470,10 @@ Status Runtime::mem_advise(Range* r, uint64_t off, uint64_t len, Advice a, Loc l
       std::lock_guard<OrderedMutex> g(b->lock);
       Policy& p = b->policy;
       switch (a) {
-        case Advice::SET_READ_MOSTLY: p.read_dup = true; break;
+        case Advice::SET_READ_MOSTLY:
+          p.read_dup = true;
+          pack_enqueue(b);  // (packed once a GPU copy was dropped clean)
+          break;
         case Advice::UNSET_READ_MOSTLY: {
           p.read_dup = false;
           // Collapse duplicates: keep the preferred copy, else a host copy, else the first.
@@ -545,11 +549,13 @@ void Runtime::cpu_map_block(Block* b) {
   Range* r = b->range;
   if (!r->cpu_view) return;
   uint8_t* win = r->cpu_view + b->block_offset();
+  // (a packed copy holds no raw pages: never mapped - a CPU access faults and
+  // expands it)
   Residency* h = nullptr;
-  if (Residency* x = b->find(cpu_loc())) h = x;
+  if (Residency* x = b->find(cpu_loc()); x && x->fmt == 0) h = x;
   if (!h)
     for (auto& x : b->res)
-      if (!x.loc.is_gpu() && x.chunk >= 0) {
+      if (!x.loc.is_gpu() && x.chunk >= 0 && x.fmt == 0) {
         h = &x;
         break;
       }
@@ -1046,6 +1052,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
         Residency* to = nullptr;
         st = populate(c, b, stage, -1, &to);
         if (st == Status::OK) stage = to->loc;  // (a full node's data rests on the next one: populate)
+        if (st == Status::OK && to->fmt == 2) st = expand_packed(b, to);  // raw pages land in it
         if (st == Status::OK) {
           // Old data only for partially covered pages.
           PageMask partial = pages.andnot(full);
@@ -1136,7 +1143,7 @@ Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_
     Residency* encoded = nullptr;
     HostArena* scratch_arena = nullptr;
     for (auto& x : b->res)
-      if (x.fmt == 1) encoded = &x;
+      if (x.fmt) encoded = &x;
     if (encoded) {
       scratch_arena = host_arena(Tier::HOST, host_node_);
       uint32_t tmp;
@@ -1146,8 +1153,8 @@ Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_
       decoded.arena = scratch_arena;
       decoded.chunk = tmp;
       decoded.fmt = 0;
-      if (!bf12_decode((const uint8_t*)encoded->arena->chunk_addr((uint32_t)encoded->chunk),
-                       (uint16_t*)scratch_arena->chunk_addr(tmp), b->npages << (kPageShift - 1))) {
+      if (!block_decode(encoded->fmt, (const uint8_t*)encoded->arena->chunk_addr((uint32_t)encoded->chunk),
+                        (uint16_t*)scratch_arena->chunk_addr(tmp), b->npages << (kPageShift - 1))) {
         scratch_arena->free(tmp, 1);
         return Status::IO_ERROR;
       }
@@ -1280,7 +1287,7 @@ Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
     out->resident_on.push_back(x.loc);
     out->chunk.push_back(x.chunk);
     out->pages.push_back(x.resident.count());
-    out->enc_bytes.push_back(x.fmt == 1 ? x.enc_bytes : 0);
+    out->enc_bytes.push_back(x.fmt ? x.enc_bytes : 0);
     dup |= seen & x.resident;
     seen |= x.resident;
   }

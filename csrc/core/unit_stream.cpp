@@ -2,6 +2,7 @@
 #include "ogkm/unit_stream.hpp"
 
 #include "ogkm/arena.hpp"
+#include "ogkm/config.hpp"
 #include "ogkm/runtime.hpp"
 
 namespace ogkm {
@@ -12,6 +13,7 @@ UnitStream::UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_
       max_ahead_(max_ahead) {}
 
 UnitStream::~UnitStream() {
+  for (Lease* l : pending_) (void)rt_->release(l, nullptr);
   for (auto& f : ahead_) (void)f->wait();
 }
 
@@ -39,6 +41,7 @@ void UnitStream::prefetch_window() {
     if (st != Status::OK) {
       // refused by the floor (no victim needed later than it): left to its use
       ++st_.refused;
+      pressure_ = true;
       break;
     }
     inflight_.push_back(pf_next_);
@@ -50,6 +53,11 @@ void UnitStream::prefetch_window() {
 
 Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
   if (pos >= ranges_.size()) return Status::INVALID_ARGUMENT;
+  struct Clock {
+    uint64_t& acc;
+    uint64_t t0 = now_ns();
+    ~Clock() { acc += now_ns() - t0; }
+  } clock{st_.use_ns};
   const uint64_t n = ranges_.size();
   Range* r = ranges_[pos];
   if (!inflight_.empty() && inflight_.front() == pos) {
@@ -57,6 +65,7 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
     inflight_bytes_ -= r->size;
   } else {
     ++st_.demand;
+    pressure_ = true;
   }
   if (next_use_) {  // the op clock moves to this use
     if ((int64_t)pos <= last_pos_) ++pass_;
@@ -70,9 +79,13 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
   if (st != Status::OK) return st;
   // hinted once leased (before, the prefetches queued for this use would see it
   // as the furthest-needed unit and evict it): next used one pass later
+  const uint64_t t1 = now_ns();
   if (next_use_) rt_->hint_next_use(*out, pass_ * n + pos + n);
+  const uint64_t t2 = now_ns();
+  st_.hint_ns += t2 - t1;
   // the consumer's stream waits GPU-side (no stream: the host waits)
   st = stream ? (*out)->ready.gpu_wait(rt_->be(), stream) : (*out)->ready.wait();
+  st_.wait_ns += now_ns() - t2;
   if (st != Status::OK) {
     (void)rt_->release(*out, stream);
     *out = nullptr;
@@ -81,18 +94,37 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
 }
 
 Status UnitStream::release(Lease* l, void* stream) {
-  if (!stream) return rt_->release(l, stream);
-  // ONE event after the unit's kernels serves both the runtime's reuse fence of
-  // its chunks and the run-ahead bound below (each event record is a barrier
-  // packet with a cache writeback on the consumer's stream).
-  FenceRef f = l->proc != kCpuProc ? fence_record(rt_->be(), l->proc, stream) : nullptr;
-  Status st = rt_->release(l, stream, f);
+  if (!stream || l->proc == kCpuProc) return rt_->release(l, stream);
+  // Released units are handed back in groups of unit_release_batch behind ONE
+  // event recorded after the group's kernels: it is the runtime's reuse fence
+  // of their chunks and the run-ahead bound below (every event record is a
+  // barrier + release packet on the consumer's stream). A group closes early
+  // when this use had to stream (a prefetch was refused or the unit faulted on
+  // demand): then the chunks are needed back as victims right away.
+  pending_.push_back(l);
+  const uint32_t batch = (uint32_t)std::max<int64_t>(1, config().unit_release_batch);
+  if (pending_.size() < batch && !pressure_) return Status::OK;
+  return flush_released(stream);
+}
+
+Status UnitStream::flush_released(void* stream) {
+  if (pending_.empty()) return Status::OK;
+  FenceRef f = fence_record(rt_->be(), dev_, stream);
+  Status st = Status::OK;
+  for (Lease* x : pending_) {
+    Status s = rt_->release(x, stream, f);
+    if (st == Status::OK) st = s;
+  }
+  pending_.clear();
+  pressure_ = false;
   if (!max_ahead_ || !f || !f->event) return st;
   // Bounded run-ahead: leases wait GPU-side, so without a bound the host would
   // prefetch a whole step ahead and the ring would evict (and wait on) chunks
   // whose readers are still queued - the copies then serialise behind compute.
   ahead_.push_back(std::move(f));
-  while (ahead_.size() > max_ahead_) {
+  const uint32_t batch = (uint32_t)std::max<int64_t>(1, config().unit_release_batch);
+  const size_t keep = std::max<size_t>(1, (max_ahead_ + batch - 1) / batch);
+  while (ahead_.size() > keep) {
     const uint64_t t0 = now_ns();
     (void)ahead_.front()->wait();
     st_.ahead_wait_ns += now_ns() - t0;

@@ -40,6 +40,7 @@ struct ChunkInfo {
   ChunkState state = ChunkState::FREE;
   uint8_t list = 0;      // 0 none, 1 unused, 2 used, 3 used + preferred here
   bool zeroed = false;
+  bool doomed = false;   // freed by its owner while a lease pinned it: freed at the last unpin
   bool active = false;   // workingset-protected (a refaulted block's data): evicted after every inactive chunk
   uint32_t pin_count = 0;
   Block* owner = nullptr;
@@ -99,6 +100,10 @@ class ChunkArena {
   void commit(const Reservation& r, bool pin = false);  // window -> ALLOCATED (owners set later)
   void cancel(const Reservation& r);                // give the window back
   void free(uint32_t first, uint32_t n);
+  // Free chunk i now, or - while a lease still pins it (a reader that leased
+  // the copy before a migration revoked it) - at its last unpin. Owner-less
+  // from now on; never a victim meanwhile (pinned).
+  void free_when_unpinned(uint32_t i);
   void set_owner(uint32_t i, Block* b);
   Block* owner(uint32_t i);
   // Evictor calls this once the owner has let go of an EVICTING chunk.
@@ -154,14 +159,14 @@ class ChunkArena {
   // under one lock, or none (false) when any is no longer ALLOCATED; release
   // = reuse fence + unpin + LRU touch of each, under one lock.
   bool try_pin_many(const uint32_t* idx, size_t n);
-  // The same plus each chunk's touch (and next-use hint when nonzero): the
-  // whole lease fast path's arena work under one lock instead of two per block.
+  // Each chunk's LRU touch (and next-use hint when nonzero) under one lock:
+  // the lease fast path's recency updates of a whole unit.
   struct TouchReq {
     uint32_t chunk;
     bool has_data, preferred, prefetched, clean;
     uint64_t refault_key, evicted_at, next_use;
   };
-  bool pin_touch_many(const TouchReq* r, size_t n);
+  void touch_many(const TouchReq* r, size_t n);
   void release_many(const uint32_t* idx, size_t n, const FenceRef& f);
   void pin(uint32_t i);
   // Pin only an ALLOCATED chunk: false when it is reserved for eviction (or
@@ -194,6 +199,8 @@ class ChunkArena {
 
  private:
   void set_next_use_locked(uint32_t i, uint64_t when);
+  void free_locked(uint32_t k);  // one ALLOCATED chunk back to the free runs
+  void unpinned_locked(uint32_t k);  // pin count just reached 0
   void touch_locked(uint32_t i, bool has_data, bool preferred, bool prefetched, uint64_t refault_key,
                     uint64_t evicted_at, bool clean);
   int32_t pick_victim_locked();  // coldest evictable chunk (reserve(1) order), -1 = none

@@ -155,6 +155,9 @@ class Backend {
   // workgroups = 0: config().decode_workgroups (sized for H2D streaming); HBM->HBM
   // unpacking passes a full-chip grid.
   virtual Status decode_bf12(int dev, const DecodeDesc* d, size_t n, void* stream, uint32_t workgroups = 0) = 0;
+  // Decode single-chunk ANS1 blocks (codec.hpp; the runtime's packed host
+  // copies) from device-readable memory into bf16: one launch per <= 64 blocks.
+  virtual Status decode_ans_blocks(int dev, const DecodeDesc* d, size_t n, void* stream) = 0;
   // Unpack a device-resident BF12 stream (codec.hpp) of n_values into bf16 at dst.
   // Chunk c lands at dst + (c >> row_shift) * dst_stride + (c mod 2^row_shift) *
   // chunk_values values (dst_stride 0 = contiguous).

@@ -148,6 +148,10 @@ static_assert(sizeof(AnsHeader) == kAnsHeaderBytes, "ANS header is 1 KB");
 uint64_t ans_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);
 bool ans_decode(const uint8_t* in, uint16_t* out, uint32_t n_values);
 
+// Decode a block stored in residency format `fmt` (1 BF12, 2 ANS1) into
+// n_values 16-bit values.
+bool block_decode(uint8_t fmt, const uint8_t* in, uint16_t* out, uint32_t n_values);
+
 // Encode n_values bf16 (n_values even) into `out` (capacity `cap` bytes).
 // Returns the encoded size, or 0 when the block does not compress into `cap`.
 uint64_t bf12_encode(const uint16_t* in, uint32_t n_values, uint8_t* out, uint64_t cap);

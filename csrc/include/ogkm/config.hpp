@@ -63,6 +63,7 @@ namespace ogkm {
   X(perf_spread_step_pct, 2, "spread classes: keep-share reduction per adaptation (percent)") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
   X(lease_fast_path, 1, "acquire: a GPU read of data resident in one contiguous extent only pins, touches and waits (no placement pass)") \
+  X(unit_release_batch, 1, "UnitStream: released units are handed back in groups of this many behind one event (fewer event records on the consumer stream)") \
   X(ring_wait_issued, 1, "a GPU-side wait on a DMA ring value is enqueued only once that value's copies are on the engines (Ring::issued_seq; prevents an SDMA-engine cycle with HIP's own copies)") \
   X(arena_class_sides, 0, "spread classes: HBM extents of keep-class ranges are placed from the arena's low end, stream-class ones from its high end (less fragmentation of kept data by the stream turnover)") \
   X(arena_victim_rerank, 0, "next-use eviction: chunks whose key rose since the victim cache was built (re-hinted) are ranked ahead of its stale order. Off by default: the 70B headline is unchanged (129.5 vs 129.4) and the transparent 8B lost 12 % with it (profiles/r5_spread.md)") \
@@ -79,6 +80,12 @@ namespace ogkm {
   X(host_budget_mb, 0, "host-tier arena limit in MB (0 = the node budget)")                          \
   X(node_ledger, 1, "host / CXL arenas reserve their segments in a node-wide shared-memory ledger (every runtime process on the machine; OGKM_NODE_LEDGER = its path)") \
   X(node_budget_mb, 0, "per-NUMA-node byte budget of the node ledger in MB (0 = the node's MemTotal x cxl_pin_budget_pct)") \
+  X(pack_host_copies, 1, "keep lossless ANS1-packed host / CXL copies of read-mostly managed blocks (H2D moves the packed bytes; the ring decodes them in HBM)") \
+  X(pack_auto_clean_evictions, 2, "a block whose HBM copy was evicted this many times without a copy-out counts as read-mostly and gets packed (0 = only SET_READ_MOSTLY blocks)") \
+  X(pack_min_saving_pct, 8, "a block is kept packed only when its packed form saves at least this share of its bytes") \
+  X(pack_threads, 4, "host encoder threads of the packer") \
+  X(ans_stage_mb, 64, "per-H2D-ring HBM staging buffer the packed bytes land in before the decode kernel (0: the kernel reads the host copy over PCIe)") \
+  X(ans_stage_engines, 0x9, "SDMA engines (mask) the H2D ring spreads packed-block staging copies over (0 = the ring's own engine)") \
   X(host_segment_mb, 1024, "host / CXL arenas populate, pin and reserve their memory in segments of this many MB") \
   /* channels / ring */                                                                              \
   X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \

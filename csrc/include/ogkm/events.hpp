@@ -198,6 +198,11 @@ enum class Counter : int {
   DemotionFallbacks,   // evictions demoted past a full node (node-wide budget spent) to the next tier / node
   LedgerRefusals,      // host / CXL segments the node-wide ledger refused (budget shared by all ranks)
   LeaseFastPaths,      // acquires served by the resident-extent fast path (Runtime::fast_lease)
+  PackedBlocks,        // host / CXL copies packed to ANS1 (Runtime::pack_block)
+  PackedBytesSaved,    // bytes those packings saved
+  PackSkips,           // blocks found incompressible (left raw)
+  PackExpansions,      // packed copies expanded back to raw pages (a write / CPU access)
+  PackedDecodes,       // packed blocks decoded into HBM by the H2D ring (DECODE_ANS)
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -77,6 +77,17 @@ hipError_t launch_bf12_unpack(const void* stream, void* dst, uint32_t nchunks, u
 hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,
                              uint32_t workgroups, hipStream_t s, uint64_t dst_stride = 0, uint64_t* err = nullptr,
                              uint32_t row_shift = 0);
+// Decode a batch of single-chunk ANS1 blocks (the runtime's packed host copies,
+// staged in HBM by the migration ring): block i at src[i] -> n_values[i] bf16
+// at dst[i]. One launch, one work item per 4 segments of every block.
+constexpr int kAnsInlineBlocks = 64;
+struct KAnsBlocks {
+  uint64_t src[kAnsInlineBlocks];
+  uint64_t dst[kAnsInlineBlocks];
+  uint32_t n_values[kAnsInlineBlocks];
+  uint32_t item_start[kAnsInlineBlocks + 1];
+};
+hipError_t launch_ans_blocks(const KAnsBlocks& b, uint32_t n, hipStream_t s, uint64_t* err = nullptr);
 
 // Decode GEMM (csrc/kernels/decode_gemm.hip); argument structs in ogkm/dgemm.hpp.
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);

@@ -51,9 +51,13 @@ enum class RingKind : int {
 const char* ring_kind_str(RingKind k);
 
 // DECODE_BF12: fused copy + decode of an encoded block (dst = raw bf16, bytes = 2 * values).
+// DECODE_ANS: an ANS1-packed block (src, `bytes` packed bytes) -> n_values bf16
+// at dst: DMA rings land the packed bytes in an HBM staging buffer by SDMA and
+// decode them there (k_ans_blocks, many blocks per launch); stream rings
+// decode straight from the host copy.
 // PAGE_COPY: scattered pages of one block, page idx[i] of src -> page idx[i] of
 // dst (one LDS-staged kernel instead of one copy per run).
-enum class SqeOp : uint8_t { COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP, DECODE_BF12, PAGE_COPY };
+enum class SqeOp : uint8_t { COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP, DECODE_BF12, PAGE_COPY, DECODE_ANS };
 
 struct Sqe {
   SqeOp op = SqeOp::NOP;
@@ -62,6 +66,7 @@ struct Sqe {
   int32_t dst_dev = -1;            // COPY on a GPU_TO_GPU ring: the peer GPU written (engine-mask lookup)
   uint32_t pattern = 0;            // MEMSET
   uint32_t page_bytes = 0;         // GATHER / SCATTER
+  uint32_t n_values = 0;           // DECODE_ANS
   std::vector<uint32_t> idx;       // GATHER / SCATTER page indices
   FenceRef wait;                   // WAIT_FENCE
   const char* file = "";
@@ -157,6 +162,8 @@ class Ring {
   std::string err_desc_;
   // DMA mode
   bool dma_ = false;
+  void* stage_ = nullptr;          // HBM staging of packed blocks (DECODE_ANS, worker thread only)
+  uint64_t stage_bytes_ = 0;
   std::thread worker_;
   std::mutex wm_;
   std::condition_variable wcv_;

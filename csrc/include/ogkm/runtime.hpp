@@ -326,6 +326,17 @@ class Runtime {
   void stop_fault_service();
   uint64_t fault_service_batches() const { return fs_batches_.load(); }
 
+  // ---- packed host copies (packer.cpp): read-mostly blocks keep a lossless
+  // ANS1-packed host / CXL copy; the H2D ring moves and decodes the packed bytes.
+  Status expand_packed(Block* b, Residency* r);  // back to raw pages (block lock held)
+  void pack_enqueue(Block* b);                   // a packing candidate (block lock held)
+  bool pack_wait(uint64_t timeout_ms);           // true once nothing is queued or being packed
+  struct PackStats {
+    uint64_t queued = 0, busy = 0, threads = 0, packed_blocks = 0, packed_bytes = 0, raw_bytes = 0;
+  };
+  PackStats pack_stats();
+  void stop_packer();
+
   // ---- perf modules
   void set_prefetch_enabled(bool on);
   // internal helpers used by engine files
@@ -418,6 +429,19 @@ class Runtime {
   std::vector<int> perf_subs_;  // perf-module subscriptions on the tools bus
   std::mutex channels_m_;
   std::vector<Channel> channels_;  // slot id - 1 (id 0 = no channel); unregistered slots keep id 0
+  // packer (packer.cpp)
+  struct PackJob {
+    uint64_t range = 0, block = 0;
+    uint32_t tries = 0;
+  };
+  void pack_worker();
+  bool pack_block(uint64_t range_id, uint64_t bi, uint16_t* raw, uint8_t* enc);
+  std::mutex pack_m_;
+  std::condition_variable pack_cv_, pack_idle_cv_;
+  std::deque<PackJob> pack_q_;
+  std::vector<std::thread> pack_threads_;
+  uint32_t pack_busy_ = 0;
+  bool pack_stop_ = false;
 };
 
 // Scoped profiler range around a runtime operation (no-op on the fake backend).

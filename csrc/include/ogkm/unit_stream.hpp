@@ -31,7 +31,8 @@ struct Lease;
 class UnitStream {
  public:
   struct Stats {
-    uint64_t prefetched = 0, refused = 0, demand = 0, prefetch_ns = 0, acquire_ns = 0, ahead_wait_ns = 0;
+    uint64_t prefetched = 0, refused = 0, demand = 0, prefetch_ns = 0, acquire_ns = 0, ahead_wait_ns = 0, hint_ns = 0,
+             wait_ns = 0, use_ns = 0;
   };
   // `ranges`: the units in use order; `window_bytes`: bytes of following units
   // kept in flight; `next_use`: hint next uses / floor prefetches (planner off);
@@ -43,8 +44,10 @@ class UnitStream {
   // Unit `pos` is used now on `stream`: returns its lease (device pointer =
   // lease->dptr) with the stream already ordered after its copies.
   Status use(uint32_t pos, void* stream, Lease** out);
-  // Its kernels are enqueued on `stream`.
+  // Its kernels are enqueued on `stream` (handed back in groups, see .cpp).
   Status release(Lease* l, void* stream);
+  // Hand back every unit released so far (a step's end).
+  Status flush_released(void* stream);
   // Keep the window full (the step's start: nothing used yet).
   void prefetch_window();
   const Stats& stats() const { return st_; }
@@ -64,7 +67,9 @@ class UnitStream {
   uint64_t inflight_bytes_ = 0;
   uint64_t pass_ = 0;
   int64_t last_pos_ = -1;
-  std::deque<FenceRef> ahead_;  // fences of released units (host bound)
+  std::deque<FenceRef> ahead_;  // fences of released groups (host bound)
+  std::vector<Lease*> pending_; // released, not yet handed back
+  bool pressure_ = false;       // this group's uses streamed (close it now)
   Stats st_;
 };
 

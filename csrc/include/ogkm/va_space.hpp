@@ -73,8 +73,12 @@ struct Residency {
   PageMask resident;
   ChunkArena* arena = nullptr;
   int64_t chunk = -1;
-  uint8_t fmt = 0;           // chunk content: 0 raw pages, 1 BF12-encoded block (codec.hpp)
-  uint32_t enc_bytes = 0;    // encoded size when fmt == 1
+  // chunk content: 0 raw pages, 1 BF12-encoded block (RANGE_COMPRESS_BF16),
+  // 2 ANS1-packed block (a packed host / CXL copy of any managed block,
+  // Runtime::pack_block; lossless, whole block, never written in place -
+  // expanded back to raw pages before any write or CPU mapping).
+  uint8_t fmt = 0;
+  uint32_t enc_bytes = 0;    // encoded size when fmt != 0
 };
 
 class Block {
@@ -116,6 +120,12 @@ class Block {
   std::atomic<bool> stale_mapping{false};
   bool in_stale_list = false;  // listed in Runtime::stale_maps_ (guarded by stable_m_)
   uint32_t lease_pins = 0;
+  // Packed host copies (Runtime::pack_block): queued for the pack workers /
+  // found incompressible (cleared when the block is written) / GPU copies
+  // evicted without a copy-out (read-mostly detection).
+  bool pack_queued = false;
+  bool pack_skip = false;
+  uint32_t clean_evictions = 0;
   uint32_t gpu_evictions = 0;  // times an HBM copy of this block was evicted (refault detection)
   uint64_t gpu_evicted_at = 0; // the HBM arena's eviction count when it last was (refault distance)
   uint32_t user_pins = 0;      // range-group / explicit pins (non-migratable)

@@ -40,10 +40,114 @@ __device__ __forceinline__ uint32_t ans_bperm(uint32_t lane, uint32_t v) {
 
 }  // namespace
 
-// err (host-coherent, may be null): {count, stream, chunk, freq sum} of corrupt
+// Work item `sub` (4 segments, one per wave) of the ANS1 chunk at `blk`, whose
+// values land at dst[0, n_values). Called by the whole workgroup (barriers).
+// err (host-coherent, may be null): {count, tag, chunk, freq sum} of corrupt
 // ANS chunks - a frequency table that does not sum to 2^kAnsPrecBits (data that
 // is not a valid stream: a race or a wrong pointer upstream). Such a chunk is
 // zero-filled and reported instead of being decoded.
+__device__ __forceinline__ void ans_decode_item(const uint8_t* __restrict__ blk, uint32_t n_values, uint32_t sub,
+                                                uint16_t* __restrict__ dst, uint32_t* tab, uint32_t* cum,
+                                                uint32_t* wsum, uint64_t* __restrict__ err, uint64_t tag,
+                                                uint64_t c) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t v_lo = sub * kAnsSegsPerItem * kAnsSegValues;
+  if (v_lo >= n_values) return;  // uniform across the workgroup
+  const AnsHeader* h = reinterpret_cast<const AnsHeader*>(blk);
+  __syncthreads();  // the previous item's table readers are done
+  // cumulative frequencies: thread t owns symbol t (blockDim == 256 symbols)
+  uint32_t s = h->freq[threadIdx.x];
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(s, d, 64);
+    if (lane >= (uint32_t)d) s += y;
+  }
+  if (lane == 63u) wsum[wave] = s;
+  __syncthreads();
+  uint32_t add = 0;
+  for (uint32_t w = 0; w < wave; ++w) add += wsum[w];
+  cum[threadIdx.x + 1] = s + add;
+  if (threadIdx.x == 0) cum[0] = 0;
+  __syncthreads();
+  if (cum[256] != kAnsSlots) {  // not an ANS chunk: report + zero-fill (workgroup-uniform)
+    if (threadIdx.x == 0 && err) {
+      if (__hip_atomic_fetch_add(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+        __hip_atomic_store(err + 1, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(err + 2, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(err + 3, (uint64_t)cum[256], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    const uint32_t v_hi = n_values - v_lo < kAnsSegsPerItem * kAnsSegValues
+                              ? n_values : v_lo + kAnsSegsPerItem * kAnsSegValues;
+    for (uint32_t k = v_lo + threadIdx.x; k < v_hi; k += kAnsThreads) dst[k] = 0;
+    return;
+  }
+  {  // decode table: thread t fills slots [16 t, 16 t + 16)
+    const uint32_t k0 = threadIdx.x * (kAnsSlots / kAnsThreads);
+    uint32_t lo = 0, hi = 256;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (cum[mid] <= k0) lo = mid; else hi = mid;
+    }
+    uint32_t sym = lo;
+    for (uint32_t k = k0; k < k0 + kAnsSlots / kAnsThreads; ++k) {
+      while (sym < 255u && cum[sym + 1] <= k) ++sym;
+      tab[k] = sym | ((cum[sym + 1] - cum[sym]) << 8) | ((k - cum[sym]) << 20);
+    }
+  }
+  __syncthreads();
+  const uint32_t seg = sub * kAnsSegsPerItem + wave;
+  if (seg >= h->n_seg) return;  // wave-uniform (the next barrier is at the next item's start)
+  const uint32_t* dir = reinterpret_cast<const uint32_t*>(blk + h->off_dir);
+  const uint32_t off = dir[seg], end = dir[seg + 1];
+  const uint32_t npairs = (end - off - 256u) / 4u;  // word pairs (the encoder pads to an even count)
+  uint32_t x = reinterpret_cast<const uint32_t*>(blk + off)[lane];
+  const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(blk + off + 256u);
+  // word window: W0 = words [wb, wb + 128), W1 = the next 128, W2 = prefetch
+  uint32_t W0 = lane < npairs ? wsrc[lane] : 0u;
+  uint32_t W1 = 64u + lane < npairs ? wsrc[64u + lane] : 0u;
+  uint32_t W2 = 128u + lane < npairs ? wsrc[128u + lane] : 0u;
+  uint32_t wb = 0, wp = 0;
+  const uint32_t base = seg * kAnsSegValues;
+  const uint32_t nv = n_values - base < kAnsSegValues ? n_values - base : kAnsSegValues;
+  const uint32_t groups = nv / 512u;
+  const uint8_t* smp = blk + kAnsHeaderBytes;
+  au32x2 smn = __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + base + lane * 8u));
+  for (uint32_t g = 0; g < groups; ++g) {
+    const uint32_t v0 = base + (g * 64u + lane) * 8u;
+    const au32x2 sm = smn;
+    if (g + 1 < groups) smn = __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + v0 + 512u));
+    au32x4 o = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t t = tab[x & (kAnsSlots - 1u)];
+      x = ((t >> 8) & 0xFFFu) * (x >> kAnsPrecBits) + (t >> 20);
+      const bool need = x < kAnsLowBound;
+      const uint64_t m = __ballot(need);
+      if (m) {  // wave-uniform
+        const uint32_t rel = wp - wb + ans_mbcnt(m);  // < 192
+        const uint32_t a = ans_bperm((rel >> 1) & 63u, W0), b = ans_bperm((rel >> 1) & 63u, W1);
+        const uint32_t pr = rel < 128u ? a : b;
+        const uint32_t word = (rel & 1u) ? (pr >> 16) : (pr & 0xFFFFu);
+        if (need) x = (x << 16) | word;
+        wp += (uint32_t)__builtin_popcountll(m);
+        if (wp - wb >= 128u) {
+          W0 = W1;
+          W1 = W2;
+          wb += 128u;
+          const uint32_t q = (wb + 256u) / 2u + lane;
+          W2 = q < npairs ? wsrc[q] : 0u;
+        }
+      }
+      const uint32_t byte = (sm[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      const uint32_t val = ((byte & 0x80u) << 8) | ((t & 0xFFu) << 7) | (byte & 0x7Fu);
+      o[j >> 1] |= val << (16 * (j & 1));
+    }
+    __builtin_nontemporal_store(o, reinterpret_cast<au32x4*>(dst + v0));
+  }
+}
+
 __global__ void __launch_bounds__(kAnsThreads)
     k_ans_unpack(const uint8_t* __restrict__ stream, uint16_t* __restrict__ out, uint64_t dst_stride,
                  uint32_t items_per_chunk, uint64_t total_items, uint64_t* __restrict__ err, uint32_t row_shift,
@@ -52,8 +156,6 @@ __global__ void __launch_bounds__(kAnsThreads)
   __shared__ uint32_t cum[257];
   __shared__ uint32_t wsum[kAnsSegsPerItem];
   const Bf12StreamChunk* table = reinterpret_cast<const Bf12StreamChunk*>(stream + sizeof(Bf12StreamHeader));
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (uint64_t item = blockIdx.x; item < total_items; item += gridDim.x) {
     const uint64_t c = item / items_per_chunk;
     const uint32_t sub = (uint32_t)(item - c * items_per_chunk);
@@ -73,98 +175,40 @@ __global__ void __launch_bounds__(kAnsThreads)
       for (uint32_t k = g_hi * 8 + threadIdx.x; k < v_hi; k += kAnsThreads) dst[k] = src[k];
       continue;
     }
+    ans_decode_item(blk, ch.n_values, sub, dst, tab, cum, wsum, err, (uint64_t)stream, c);
+  }
+}
+
+// Packed host copies of the runtime (ring op DECODE_ANS): one ANS1 chunk per
+// 2 MB block, staged in HBM by the engines; block k's items are
+// [item_start[k], item_start[k + 1]). A block whose header does not match
+// (magic / value count) is reported and zero-filled like a bad table.
+__global__ void __launch_bounds__(kAnsThreads)
+    k_ans_blocks(const KAnsBlocks b, uint32_t n, uint64_t* __restrict__ err) {
+  __shared__ uint32_t tab[kAnsSlots];
+  __shared__ uint32_t cum[257];
+  __shared__ uint32_t wsum[kAnsSegsPerItem];
+  const uint32_t total = b.item_start[n];
+  for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
+    uint32_t k = 0;
+    while (k + 1 < n && b.item_start[k + 1] <= item) ++k;  // uniform scan (n <= 64)
+    const uint8_t* blk = reinterpret_cast<const uint8_t*>(b.src[k]);
+    uint16_t* dst = reinterpret_cast<uint16_t*>(b.dst[k]);
+    const uint32_t nv = b.n_values[k];
     const AnsHeader* h = reinterpret_cast<const AnsHeader*>(blk);
-    __syncthreads();  // the previous item's table readers are done
-    // cumulative frequencies: thread t owns symbol t (blockDim == 256 symbols)
-    uint32_t s = h->freq[threadIdx.x];
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(s, d, 64);
-      if (lane >= (uint32_t)d) s += y;
-    }
-    if (lane == 63u) wsum[wave] = s;
-    __syncthreads();
-    uint32_t add = 0;
-    for (uint32_t w = 0; w < wave; ++w) add += wsum[w];
-    cum[threadIdx.x + 1] = s + add;
-    if (threadIdx.x == 0) cum[0] = 0;
-    __syncthreads();
-    if (cum[256] != kAnsSlots) {  // not an ANS chunk: report + zero-fill (workgroup-uniform)
-      if (threadIdx.x == 0 && err) {
-        if (__hip_atomic_fetch_add(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
-          __hip_atomic_store(err + 1, (uint64_t)stream, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(err + 2, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(err + 3, (uint64_t)cum[256], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    if (h->magic != kAnsMagic || h->n_values != nv) {  // uniform
+      const uint32_t sub = item - b.item_start[k];
+      if (threadIdx.x == 0 && err && __hip_atomic_fetch_add(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+        __hip_atomic_store(err + 1, b.src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(err + 2, (uint64_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(err + 3, (uint64_t)h->magic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      const uint32_t v_hi = ch.n_values - v_lo < kAnsSegsPerItem * kAnsSegValues
-                                ? ch.n_values : v_lo + kAnsSegsPerItem * kAnsSegValues;
-      for (uint32_t k = v_lo + threadIdx.x; k < v_hi; k += kAnsThreads) dst[k] = 0;
+      const uint32_t v_lo = sub * kAnsSegsPerItem * kAnsSegValues;
+      const uint32_t v_hi = nv - v_lo < kAnsSegsPerItem * kAnsSegValues ? nv : v_lo + kAnsSegsPerItem * kAnsSegValues;
+      for (uint32_t v = v_lo + threadIdx.x; v < v_hi; v += kAnsThreads) dst[v] = 0;
       continue;
     }
-    {  // decode table: thread t fills slots [16 t, 16 t + 16)
-      const uint32_t k0 = threadIdx.x * (kAnsSlots / kAnsThreads);
-      uint32_t lo = 0, hi = 256;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (cum[mid] <= k0) lo = mid; else hi = mid;
-      }
-      uint32_t sym = lo;
-      for (uint32_t k = k0; k < k0 + kAnsSlots / kAnsThreads; ++k) {
-        while (sym < 255u && cum[sym + 1] <= k) ++sym;
-        tab[k] = sym | ((cum[sym + 1] - cum[sym]) << 8) | ((k - cum[sym]) << 20);
-      }
-    }
-    __syncthreads();
-    const uint32_t seg = sub * kAnsSegsPerItem + wave;
-    if (seg >= h->n_seg) continue;  // wave-uniform (the next barrier is at the next item's start)
-    const uint32_t* dir = reinterpret_cast<const uint32_t*>(blk + h->off_dir);
-    const uint32_t off = dir[seg], end = dir[seg + 1];
-    const uint32_t npairs = (end - off - 256u) / 4u;  // word pairs (the encoder pads to an even count)
-    uint32_t x = reinterpret_cast<const uint32_t*>(blk + off)[lane];
-    const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(blk + off + 256u);
-    // word window: W0 = words [wb, wb + 128), W1 = the next 128, W2 = prefetch
-    uint32_t W0 = lane < npairs ? wsrc[lane] : 0u;
-    uint32_t W1 = 64u + lane < npairs ? wsrc[64u + lane] : 0u;
-    uint32_t W2 = 128u + lane < npairs ? wsrc[128u + lane] : 0u;
-    uint32_t wb = 0, wp = 0;
-    const uint32_t base = seg * kAnsSegValues;
-    const uint32_t nv = ch.n_values - base < kAnsSegValues ? ch.n_values - base : kAnsSegValues;
-    const uint32_t groups = nv / 512u;
-    const uint8_t* smp = blk + kAnsHeaderBytes;
-    au32x2 smn = __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + base + lane * 8u));
-    for (uint32_t g = 0; g < groups; ++g) {
-      const uint32_t v0 = base + (g * 64u + lane) * 8u;
-      const au32x2 sm = smn;
-      if (g + 1 < groups) smn = __builtin_nontemporal_load(reinterpret_cast<const au32x2*>(smp + v0 + 512u));
-      au32x4 o = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t t = tab[x & (kAnsSlots - 1u)];
-        x = ((t >> 8) & 0xFFFu) * (x >> kAnsPrecBits) + (t >> 20);
-        const bool need = x < kAnsLowBound;
-        const uint64_t m = __ballot(need);
-        if (m) {  // wave-uniform
-          const uint32_t rel = wp - wb + ans_mbcnt(m);  // < 192
-          const uint32_t a = ans_bperm((rel >> 1) & 63u, W0), b = ans_bperm((rel >> 1) & 63u, W1);
-          const uint32_t pr = rel < 128u ? a : b;
-          const uint32_t word = (rel & 1u) ? (pr >> 16) : (pr & 0xFFFFu);
-          if (need) x = (x << 16) | word;
-          wp += (uint32_t)__builtin_popcountll(m);
-          if (wp - wb >= 128u) {
-            W0 = W1;
-            W1 = W2;
-            wb += 128u;
-            const uint32_t q = (wb + 256u) / 2u + lane;
-            W2 = q < npairs ? wsrc[q] : 0u;
-          }
-        }
-        const uint32_t byte = (sm[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-        const uint32_t val = ((byte & 0x80u) << 8) | ((t & 0xFFu) << 7) | (byte & 0x7Fu);
-        o[j >> 1] |= val << (16 * (j & 1));
-      }
-      __builtin_nontemporal_store(o, reinterpret_cast<au32x4*>(dst + v0));
-    }
+    ans_decode_item(blk, nv, item - b.item_start[k], dst, tab, cum, wsum, err, b.src[k], k);
   }
 }
 
@@ -181,6 +225,15 @@ hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, ui
   hipLaunchKernelGGL(k_ans_unpack, dim3((uint32_t)grid), dim3(kAnsThreads), 0, s, (const uint8_t*)stream,
                      (uint16_t*)dst, dst_stride ? dst_stride : (uint64_t)chunk_values, per_chunk, total, err, row_shift,
                      chunk_values);
+  return hipGetLastError();
+}
+
+hipError_t launch_ans_blocks(const KAnsBlocks& b, uint32_t n, hipStream_t s, uint64_t* err) {
+  if (n == 0) return hipSuccess;
+  if (n > (uint32_t)kAnsInlineBlocks) return hipErrorInvalidValue;
+  const uint32_t total = b.item_start[n];
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ans_blocks, dim3(total), dim3(kAnsThreads), 0, s, b, n, err);
   return hipGetLastError();
 }
 

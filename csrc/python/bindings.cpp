@@ -329,9 +329,32 @@ PYBIND11_MODULE(_ogkm, m) {
              d["prefetch_ms"] = st.prefetch_ns / 1e6;
              d["acquire_ms"] = st.acquire_ns / 1e6;
              d["ahead_wait_ms"] = st.ahead_wait_ns / 1e6;
+             d["hint_ms"] = st.hint_ns / 1e6;
+             d["wait_ms"] = st.wait_ns / 1e6;
+             d["use_ms"] = st.use_ns / 1e6;
              return d;
            })
       .def("reset_stats", &UnitStream::reset_stats);
+  // Packed host copies (packer.cpp).
+  m.def("pack_wait", [](uint64_t timeout_ms) {
+    py::gil_scoped_release nogil;
+    return rt()->pack_wait(timeout_ms);
+  }, py::arg("timeout_ms") = 60000);
+  m.def("pack_stats", []() {
+    Runtime::PackStats st;
+    {
+      py::gil_scoped_release nogil;
+      st = rt()->pack_stats();
+    }
+    py::dict d;
+    d["queued"] = st.queued;
+    d["busy"] = st.busy;
+    d["threads"] = st.threads;
+    d["packed_blocks"] = st.packed_blocks;
+    d["packed_bytes"] = st.packed_bytes;
+    d["raw_bytes"] = st.raw_bytes;
+    return d;
+  });
   m.def("spread_class", [](int dev, uint64_t id) { return rt()->spread_class(dev, id); });
   m.def("spread_stats", [](int dev) {
     auto st = rt()->spread_stats(dev);

@@ -48,7 +48,9 @@ def fake_rt():
         lib.shutdown()
     lib.config_reset()
     lib.clear_fatal_for_test()
-    rt.init("fake", fake_devices=2, fake_hbm_mb=64, lock_check=1, host_budget_mb=1024)
+    # packed host copies off: tests that count link bytes see raw transfers
+    # (tests/test_packing*.py turn it on)
+    rt.init("fake", fake_devices=2, fake_hbm_mb=64, lock_check=1, host_budget_mb=1024, pack_host_copies=0)
     lib.reset_lock_violations()
     lib.reset_counters()
     yield rt
@@ -67,7 +69,7 @@ def gpu_rt():
         lib.shutdown()
     lib.config_reset()
     lib.clear_fatal_for_test()
-    rt.init("hip", lock_check=1, host_budget_mb=16384, hbm_budget={0: 2 << 30})
+    rt.init("hip", lock_check=1, host_budget_mb=16384, hbm_budget={0: 2 << 30}, pack_host_copies=0)
     lib.reset_lock_violations()
     lib.reset_counters()
     yield rt

@@ -3,7 +3,7 @@ either plainly (torch's own allocator, everything resident) or under
 ``ogkm.managed()`` with its parameters oversubscribing the HBM arena; saves the
 outputs / gradients / updated parameters for a bitwise comparison.
 
-    python managed_mode_worker.py plain|managed OUT.pt [--lazy]
+    python managed_mode_worker.py plain|managed OUT.pt [--lazy] [--advise] [--pack]
 """
 from __future__ import annotations
 
@@ -114,6 +114,18 @@ def main() -> None:
                     allocator.advise(p, rt.ADVISE_SET_PREFERRED_LOCATION, f"host:{lib.host_node()}")
                     allocator.advise(p, rt.ADVISE_SET_ACCESSED_BY, proc=0)
                     advised += 1
+        if "--pack" in sys.argv:
+            # one inference pass first: the weights' GPU copies are dropped
+            # clean, the runtime packs their host copies (ANS1); the measured
+            # pass below refills them from the packed bytes (DECODE_ANS)
+            from ogkm._native import lib
+
+            model.eval()
+            for _ in range(2):
+                with torch.no_grad():
+                    model(x.cuda())
+                torch.cuda.synchronize()
+                lib.pack_wait(60000)
         res = run(model, x.cuda(), log=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -125,7 +137,8 @@ def main() -> None:
                          "dth_mb": st["bytes_xfer_dth"] >> 20, "vmm_remaps": st["vmm_remaps"],
                          "tlb_flushes": st["tlb_flushes"], "vmm_errors": st["vmm_errors"], "seconds": round(dt, 3),
                          "advised": advised, "remote_fallbacks": st["remote_fallbacks"],
-                         "write_invalidations": st["write_invalidations"]})
+                         "write_invalidations": st["write_invalidations"], "packed_blocks": st["packed_blocks"],
+                         "packed_decodes": st["packed_decodes"], "pack_expansions": st["pack_expansions"]})
 
 
 if __name__ == "__main__":

@@ -266,6 +266,26 @@ def test_stable_va_vmm(gpu_rt):
     b.free()
 
 
+def test_stable_va_after_arena_recreation_reads_new_chunks(gpu_rt):
+    """Re-creating the HBM arena releases its VMM handles together with the
+    ROCr handles cached for stable-VA remaps (backend_hip.cpp vmm_release): a
+    stable VA mapped in the new arena must read the new physical chunks, even
+    when hipMemCreate hands back the same handle values. Each generation fills
+    a different pattern, so a mapping to the old (leaked) memory shows up."""
+    lib.configure("hbm_provider", 1)
+    n = 6 * MB
+    for gen in range(3):
+        lib.init_device(0, 64 * MB)  # a fresh arena (the previous one is released)
+        b = rt.malloc_managed(n, f"gen{gen}", stable_va=True, device=0)
+        ref = torch.arange(n // 4, dtype=torch.int32) * (gen + 3) + 7 * gen
+        b.write(ref)
+        b.migrate("gpu:0")
+        t = rt._tensor_from_ptr(b.dev_va, (n // 4,), torch.int32, "cuda", 0, b.id)
+        assert torch.equal(t.cpu(), ref), f"generation {gen} reads stale memory"
+        del t
+        b.free()
+
+
 def test_device_health_reports_ras_counters(gpu_rt):
     """ECC / xGMI RAS counters of the real GPU (amdgpu sysfs ras/aca_<block> or
     ras/<block>_err_count, else amd-smi): baselined at init, and a healthy box

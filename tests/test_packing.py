@@ -1,0 +1,179 @@
+"""Packed host copies of read-mostly managed blocks (csrc/core/packer.cpp).
+
+A block whose HBM copy keeps being dropped clean (or a SET_READ_MOSTLY one)
+gets its host copy rewritten as one lossless ANS1 chunk; H2D refills then move
+the packed bytes and the ring decodes them (DECODE_ANS). Fake backend: the
+decode is the CPU reference codec, the protocol (eligibility, snapshot /
+compare / install, expansion on writes and CPU access, whole-block sources) is
+the runtime's own. The GPU twin (k_ans_blocks through the SDMA staging path)
+is tests/test_packing_gpu.py."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from ogkm import rt
+from ogkm._native import lib
+
+MB = 1 << 20
+
+
+def _weights(nbytes: int, seed: int = 0) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(nbytes // 2, generator=g) * 0.02).to(torch.bfloat16).view(torch.uint8)
+
+
+def _packed_entries(b):
+    out = []
+    for off in range(0, b.size, 2 * MB):
+        for e in b.residency(off)["resident_on"]:
+            if e.get("encoded_bytes"):
+                out.append((off, e["tier"], e["encoded_bytes"]))
+    return out
+
+
+def _pack(b) -> None:
+    """READ_MOSTLY + one GPU read duplicate dropped clean: packed."""
+    b.set_read_mostly(True)
+    l = b.acquire(0, rt.READ)
+    l.wait(0)
+    l.release(0)
+    b.evict("gpu:0")
+    assert lib.pack_wait(30000)
+
+
+def _gpu_read(b, dev=0, allow_remote=True) -> torch.Tensor:
+    l = b.acquire(dev, rt.READ, allow_remote=allow_remote)
+    l.wait(0)
+    t = l.tensor((b.size,), torch.uint8).clone()
+    l.release(0)
+    return t
+
+
+def test_read_mostly_block_packs_and_decodes_bit_exact(fake_rt):
+    rt.configure(pack_host_copies=1, pack_threads=2)
+    b = rt.malloc_managed(8 * MB, "w")
+    data = _weights(b.size)
+    b.write(data)
+    b.set_read_mostly(True)
+    assert lib.pack_wait(1000) and _packed_entries(b) == []  # the advice alone packs nothing
+    _pack(b)
+    packed = _packed_entries(b)
+    assert len(packed) == 4 and all(t == "host" for _, t, _ in packed)
+    ratio = sum(e for _, _, e in packed) / b.size
+    assert 0.5 < ratio < 0.8, ratio  # exponent entropy of N(0, 0.02) bf16
+    s0 = lib.stats()
+    assert _gpu_read(b).equal(data)  # the H2D decoded the packed blocks
+    s1 = lib.stats()
+    assert s1["packed_decodes"] - s0["packed_decodes"] == 4
+    # only the packed bytes crossed the link
+    assert s1["bytes_xfer_htd"] - s0["bytes_xfer_htd"] == sum(e for _, _, e in packed)
+    # read() and the CPU view see the raw data
+    assert b.read().equal(data)
+    st = lib.pack_stats()
+    assert st["packed_blocks"] == 4 and st["queued"] == 0
+    b.free()
+
+
+def test_clean_evictions_trigger_packing(fake_rt):
+    rt.configure(pack_host_copies=1, pack_threads=1, pack_auto_clean_evictions=2)
+    b = rt.malloc_managed(4 * MB, "auto")
+    data = _weights(b.size, 1)
+    b.write(data)
+    # accessed_by + a caller that needs the data at its own address (the
+    # transparent mode's op holds): each read is a local read duplicate
+    b.set_accessed_by(0)
+    for _ in range(3):
+        assert _gpu_read(b, allow_remote=False).equal(data)
+        b.evict("gpu:0")  # a read duplicate: dropped without a copy-out
+        lib.pack_wait(30000)
+    assert len(_packed_entries(b)) == 2
+    assert lib.stats()["packed_blocks"] == 2
+    assert _gpu_read(b, allow_remote=False).equal(data)
+    b.free()
+
+
+def test_cpu_write_expands_packed_copy(fake_rt):
+    rt.configure(pack_host_copies=1, pack_threads=1)
+    b = rt.malloc_managed(4 * MB, "cw")
+    data = _weights(b.size, 2)
+    b.write(data)
+    _pack(b)
+    assert len(_packed_entries(b)) == 2
+    # a CPU store through the CPU view: the packed copy is never mapped, so it
+    # faults, expands (raw pages) and lands
+    v = b.cpu_view()
+    v[100] = 7
+    data[100] = 7
+    assert lib.stats()["pack_expansions"] >= 1
+    assert b.read().equal(data)
+    assert _gpu_read(b).equal(data)
+    # a runtime write into the other block expands that one too
+    patch = torch.full((4096,), 3, dtype=torch.uint8)
+    b.write(patch, 3 * MB)
+    data[3 * MB:3 * MB + 4096] = 3
+    assert b.read().equal(data)
+    assert _gpu_read(b).equal(data)
+    b.free()
+
+
+def test_gpu_write_revokes_and_source_expands(fake_rt):
+    rt.configure(pack_host_copies=1, pack_threads=1)
+    b = rt.malloc_managed(2 * MB, "gw")
+    data = _weights(b.size, 3)
+    b.write(data)
+    _pack(b)
+    assert len(_packed_entries(b)) == 1
+    # a GPU write of one page revokes it in the packed host copy ...
+    l = b.acquire(0, rt.WRITE, 8192, 4096)
+    l.wait(0)
+    l.tensor((4096,), torch.uint8).fill_(11)
+    l.release(0)
+    data[8192:12288] = 11
+    # ... whose other pages still serve a refill of GPU 1 (expanded first: a
+    # partial packed copy is no whole-block source)
+    assert _gpu_read(b, 1).equal(data)
+    assert b.read().equal(data)
+    b.free()
+
+
+def test_incompressible_blocks_stay_raw(fake_rt):
+    rt.configure(pack_host_copies=1, pack_threads=1)
+    b = rt.malloc_managed(2 * MB, "rand")
+    data = torch.randint(0, 256, (b.size,), dtype=torch.uint8)
+    b.write(data)
+    _pack(b)
+    assert _packed_entries(b) == []
+    assert lib.stats()["pack_skips"] == 1
+    assert _gpu_read(b).equal(data)
+    b.free()
+
+
+def test_packing_off_by_config(fake_rt):
+    rt.configure(pack_host_copies=0)
+    b = rt.malloc_managed(2 * MB, "off")
+    b.write(_weights(b.size, 4))
+    _pack(b)
+    assert _packed_entries(b) == []
+    b.free()
+
+
+def test_packed_copy_moves_to_cxl_verbatim(fake_rt):
+    """A packed host copy migrated down a tier moves its packed bytes as they
+    are (no expansion) and still decodes bit-exact into HBM from there."""
+    lib.cxl_rediscover(0, "/sys")  # emulate NUMA node 0 as a CXL pool
+    rt.configure(pack_host_copies=1, pack_threads=1)
+    b = rt.malloc_managed(2 * MB, "cxl")
+    data = _weights(b.size, 5)
+    b.write(data)
+    _pack(b)
+    assert len(_packed_entries(b)) == 1
+    enc = _packed_entries(b)[0][2]
+    s0 = lib.stats()
+    b.migrate("cxl:0")  # (read-mostly: the host copy may stay as a duplicate)
+    cxl = [e for _, t, e in _packed_entries(b) if t == "cxl"]
+    assert cxl == [enc]
+    assert lib.stats()["pack_expansions"] == s0["pack_expansions"]
+    b.evict("host:0")
+    assert _gpu_read(b).equal(data)
+    b.free()

@@ -1,0 +1,101 @@
+"""Packed host copies on the GPU (csrc/core/packer.cpp + Ring DECODE_ANS +
+k_ans_blocks): a read-mostly managed buffer whose HBM copy was dropped clean is
+packed on the host; its next H2D refill moves only the packed bytes - SDMA into
+the ring's HBM staging buffer, then ONE k_ans_blocks launch per batch of
+blocks (the default engine path) or k_ans_blocks reading the host copy
+directly (CU copy-kernel rings) - and the HBM copy is bit-identical to the
+data written. The CPU twin is tests/test_packing.py."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from ogkm import rt
+from ogkm._native import lib
+
+pytestmark = pytest.mark.gpu
+
+MB = 1 << 20
+
+
+def _weights(nbytes: int, seed: int) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(nbytes // 2, generator=g) * 0.02).to(torch.bfloat16).view(torch.uint8)
+
+
+def _packed(b):
+    out = []
+    for off in range(0, b.size, 2 * MB):
+        for e in b.residency(off)["resident_on"]:
+            if e.get("encoded_bytes"):
+                out.append(e["encoded_bytes"])
+    return out
+
+
+@pytest.mark.parametrize("engine", [3, 0], ids=["sdma_staging", "kernel_direct"])
+def test_packed_refill_bit_exact(gpu_rt, engine):
+    if engine != rt.get_config("copy_engine"):
+        # the rings pick their engine path when they are created
+        lib.shutdown()
+        rt.init("hip", lock_check=1, host_budget_mb=16384, hbm_budget={0: 2 << 30}, copy_engine=engine)
+    rt.configure(pack_host_copies=1, pack_threads=4)
+    size = 96 * MB + 12 * 4096  # 48 full blocks + a partial last block
+    b = rt.malloc_managed(size, "packed")
+    data = _weights(size, 7)
+    b.write(data)
+    b.set_read_mostly(True)
+    l = b.acquire(0, rt.READ)
+    l.wait()
+    l.release()
+    b.evict("gpu:0")  # a clean read duplicate: the host copy gets packed
+    assert lib.pack_wait(60000)
+    enc = _packed(b)
+    assert len(enc) == 49, len(enc)
+    assert sum(enc) < 0.75 * size
+    s0 = lib.stats()
+    l = b.acquire(0, rt.READ)
+    l.wait()
+    got = l.tensor((size,), torch.uint8)
+    ok = torch.equal(got, data.cuda())
+    l.release()
+    s1 = lib.stats()
+    assert ok
+    assert s1["packed_decodes"] - s0["packed_decodes"] == 49
+    assert s1["bytes_xfer_htd"] - s0["bytes_xfer_htd"] == sum(enc)
+    err = lib.decode_errors(True)
+    assert err["count"] == 0, err
+    # the host copy stays packed (a read duplicate) and serves again
+    b.evict("gpu:0")
+    l = b.acquire(0, rt.READ, 50 * MB, 8 * MB)
+    l.wait()
+    assert torch.equal(l.tensor((8 * MB,), torch.uint8), data[50 * MB:58 * MB].cuda())
+    l.release()
+    b.free()
+
+
+def test_gpu_write_after_packing_round_trips(gpu_rt):
+    """A GPU write into a packed block revokes the packed pages; the data comes
+    back right through eviction (the write-back expands the host copy)."""
+    rt.configure(pack_host_copies=1, pack_threads=2)
+    b = rt.malloc_managed(8 * MB, "pw")
+    data = _weights(b.size, 8)
+    b.write(data)
+    b.set_read_mostly(True)
+    l = b.acquire(0, rt.READ)
+    l.wait()
+    l.release()
+    b.evict("gpu:0")
+    assert lib.pack_wait(60000) and len(_packed(b)) == 4
+    l = b.acquire(0, rt.WRITE, 3 * MB, 4096)
+    l.wait()
+    l.tensor((4096,), torch.uint8).fill_(5)
+    torch.cuda.synchronize()
+    l.release()
+    data[3 * MB:3 * MB + 4096] = 5
+    b.evict("gpu:0")
+    assert torch.equal(b.read(), data)
+    l = b.acquire(0, rt.READ)
+    l.wait()
+    assert torch.equal(l.tensor((b.size,), torch.uint8), data.cuda())
+    l.release()
+    b.free()
