@@ -388,9 +388,15 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     Status st = rt->expand_packed(b, from);
     if (st != Status::OK) return st;
   }
-  if (to->fmt == 2 && !from->fmt) {  // raw pages into a packed copy (a write-back): raw first
-    Status st = rt->expand_packed(b, to);
-    if (st != Status::OK) return st;
+  if (to->fmt == 2 && !from->fmt) {  // raw pages into a packed copy (a write-back)
+    if (pages == b->valid_pages()) {
+      // every page is overwritten (after the chunk's queued readers, below)
+      to->fmt = 0;
+      to->enc_bytes = 0;
+    } else {
+      Status st = rt->expand_packed(b, to);  // raw first, then the pages land
+      if (st != Status::OK) return st;
+    }
   }
   Ring* ring = ring_for(rt, from->loc, to->loc);
   Counter ctr = xfer_counter(from->loc, to->loc);
@@ -916,6 +922,10 @@ Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
     r = nullptr;
     for (auto& x : b->res)
       if (x.arena == a && x.chunk == (int64_t)i) r = &x;
+    // Written pages going back into a packed host copy: with every page here,
+    // the whole block is copied out raw over it (a D2H of the block instead of
+    // a host-side decode of the packed copy to merge a few pages into).
+    if (to->fmt == 2 && r->resident == b->valid_pages()) only_here = b->valid_pages();
     st = copy_pages(this, c, b, r, to, only_here);
     if (st != Status::OK) return st;
     to->resident |= only_here;
@@ -928,8 +938,10 @@ Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
   if (from.is_gpu()) {
     b->gpu_evictions++;
     b->gpu_evicted_at = a->evictions();
-    // dropped without a copy-out: a clean read duplicate (read-mostly data)
-    if (only_here.empty()) b->clean_evictions++;
+    // dropped without a copy-out: a clean read duplicate (read-mostly data);
+    // a written copy restarts the count (a KV cache gets a row in every block
+    // each step: packing it would only buy expansions)
+    b->clean_evictions = only_here.empty() ? b->clean_evictions + 1 : 0;
     pack_enqueue(b);
     if (is_local(from.id)) devs_[from.id]->spread.on_evict(b->range->id);
     // Users of the stable VA's mapping of this chunk (see Block::stable_users).
@@ -1145,6 +1157,14 @@ Status Runtime::evict_range(Range* r, Loc from) {
         Loc dst = demotion_target(from);
         if (from.is_gpu() && b->policy.has_preferred && !b->policy.preferred.is_gpu()) dst = b->policy.preferred;
         if (dst.id < 0) return Status::NO_MEMORY;
+        // Written pages of a block whose host copy is packed, every page here:
+        // drop the packed copy and write the whole block back raw (no host-side
+        // decode to merge the written pages into it).
+        if (Residency* h = b->find(dst); h && h->fmt == 2 && x->resident == b->valid_pages()) {
+          drop_residency(c, b, dst);
+          x = b->find(from);
+          only_here = x->resident;
+        }
         st = make_resident(c, b, only_here, dst, false, Cause::Eviction);
         if (st != Status::OK) {
           finish_ctx(c, nullptr);
@@ -1159,7 +1179,7 @@ Status Runtime::evict_range(Range* r, Loc from) {
       }
       Tools::get().inc(Counter::Evictions);
       if (from.is_gpu()) {
-        if (only_here.empty()) b->clean_evictions++;
+        b->clean_evictions = only_here.empty() ? b->clean_evictions + 1 : 0;
         pack_enqueue(b);
       }
     }

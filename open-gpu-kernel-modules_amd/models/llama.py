@@ -585,6 +585,7 @@ class TieredLlama:
         # shards are used (gathered) in the same cyclic order.
         self.next_use = (self.planner == "off" and os.environ.get("OGKM_NEXT_USE", "1") != "0"
                          and bool(self.stream_seq))
+        self._refs: dict = {}  # (unit, dptr, mode) -> WeightRef (_ref)
         self._seq_pos = {k: j for j, k in enumerate(self.stream_seq)}
         self._pass, self._last_pos = 0, -1
         if self.next_use and not self.dry_run:
@@ -1232,9 +1233,19 @@ class TieredLlama:
         return self._ref(key, self.stage.data_ptr(), dgemm.MODE_RAW)
 
     def _ref(self, key, ptr: int, mode: int) -> "dgemm.WeightRef":
-        shift = (self.pinfo[key].chunk_values.bit_length() - 1) if key in self.pinfo else 20
-        n, k = self._unit_shape(key)
-        return dgemm.WeightRef(ptr, 0, n, k, mode, shift)
+        # A unit that stays resident comes back at the same address every step:
+        # its WeightRef is built once (host time per unit use is the budget of
+        # a resident decode step - config 2 runs the whole model this way).
+        ck = (key, ptr, mode)
+        ref = self._refs.get(ck)
+        if ref is None:
+            shift = (self.pinfo[key].chunk_values.bit_length() - 1) if key in self.pinfo else 20
+            n, k = self._unit_shape(key)
+            ref = dgemm.WeightRef(ptr, 0, n, k, mode, shift)
+            if len(self._refs) > 8192:
+                self._refs.clear()
+            self._refs[ck] = ref
+        return ref
 
     def _done(self, lease) -> None:
         if isinstance(lease, tuple) and lease[0] == "native":  # release + run-ahead bound, natively

@@ -177,3 +177,29 @@ def test_packed_copy_moves_to_cxl_verbatim(fake_rt):
     b.evict("host:0")
     assert _gpu_read(b).equal(data)
     b.free()
+
+
+def test_written_block_goes_back_whole_without_expansion(fake_rt):
+    """A GPU write into a block with a packed host copy: its eviction copies the
+    whole block out raw over the packed copy (no host-side decode to merge the
+    written pages), and the block is not packed again until it is dropped clean
+    twice in a row."""
+    rt.configure(pack_host_copies=1, pack_threads=1)
+    b = rt.malloc_managed(2 * MB, "wb")
+    data = _weights(b.size, 6)
+    b.write(data)
+    _pack(b)
+    assert len(_packed_entries(b)) == 1
+    l = b.acquire(0, rt.WRITE, 4096, 4096)
+    l.wait(0)
+    l.tensor((4096,), torch.uint8).fill_(9)
+    l.release(0)
+    data[4096:8192] = 9
+    e0 = lib.stats()["pack_expansions"]
+    b.evict("gpu:0")
+    assert lib.stats()["pack_expansions"] == e0
+    assert _packed_entries(b) == []
+    assert lib.pack_wait(10000) and _packed_entries(b) == []  # written: not packed at once
+    assert b.read().equal(data)
+    assert _gpu_read(b).equal(data)
+    b.free()
