@@ -159,7 +159,8 @@ const char* counter_name(Counter c) {
                             "packed_bytes_saved",
                             "pack_skips",
                             "pack_expansions",
-                            "packed_decodes"};
+                            "packed_decodes",
+                            "pressure_reliefs"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -103,6 +103,33 @@ Status Runtime::alloc_chunks(ChunkArena* a, uint32_t n, int64_t hint, uint32_t* 
   return st;
 }
 
+uint64_t Runtime::add_pressure_handler(int dev, PressureFn f) {
+  std::lock_guard<std::mutex> g(pressure_m_);
+  pressure_.emplace_back(pressure_next_, dev, std::move(f));
+  return pressure_next_++;
+}
+
+void Runtime::remove_pressure_handler(uint64_t id) {
+  std::lock_guard<std::mutex> g(pressure_m_);
+  pressure_.erase(std::remove_if(pressure_.begin(), pressure_.end(),
+                                 [id](const auto& h) { return std::get<0>(h) == id; }),
+                  pressure_.end());
+}
+
+bool Runtime::relieve_pressure(const Loc& l) {
+  if (!l.is_gpu()) return false;
+  std::vector<PressureFn> fs;
+  {
+    std::lock_guard<std::mutex> g(pressure_m_);
+    for (auto& h : pressure_)
+      if (std::get<1>(h) == l.id) fs.push_back(std::get<2>(h));
+  }
+  bool any = false;
+  for (auto& f : fs) any |= f();
+  if (any) Tools::get().inc(Counter::PressureReliefs);
+  return any;
+}
+
 // Reserve n contiguous chunks, evicting victims (no block lock may be held).
 Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool pin) {
   if (a->loc().is_gpu() && !config().global_oversubscription) return Status::NO_MEMORY;
@@ -111,8 +138,13 @@ Status Runtime::ensure_capacity(ChunkArena* a, uint32_t n, Reservation* r, bool 
     return Status::NO_MEMORY;  // injected allocation failure: eviction cannot help either
   }
   Status st = Status::OK, es = Status::OK;
+  bool relieved = false;
   for (int attempt = 0;; ++attempt) {
     st = a->reserve(n, r);
+    if (st == Status::NO_MEMORY && !relieved) {  // soft pins (held leases) let go, once
+      relieved = true;
+      if (relieve_pressure(a->loc())) continue;
+    }
     if (st != Status::OK) return st;
     es = evict_batch(a, r->victims);
     if (es == Status::OK) break;
@@ -1463,6 +1495,7 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
       std::vector<uint32_t> got;
       Reservation rv;
       st = ga->reserve_for(hints, &got, &rv);
+      if (st == Status::NO_MEMORY && relieve_pressure(dst)) st = ga->reserve_for(hints, &got, &rv);
       for (int attempt = 0; st == Status::OK; ++attempt) {
         st = evict_batch(ga, rv.victims);
         if (st == Status::OK) break;
@@ -1495,6 +1528,7 @@ Status Runtime::place_stable(Range* r, uint64_t off, uint64_t len, int gpu, cons
         st = Status::NO_MEMORY;
       } else {
         st = ga->reserve_scattered(m, &rv);
+        if (st == Status::NO_MEMORY && relieve_pressure(dst)) st = ga->reserve_scattered(m, &rv);
       }
       for (int attempt = 0; st == Status::OK; ++attempt) {
         st = evict_batch(ga, rv.victims);
@@ -1957,15 +1991,15 @@ Status Runtime::release(Lease* l, void* stream, const FenceRef& use) {
     idx.push_back(pc.second);
   }
   flush();
-  {
-    std::shared_lock<OrderedRWLock> vg(vs_.lock);
-    for (Block* b : l->blocks) {
-      std::lock_guard<OrderedMutex> g(b->lock);
-      if (b->lease_pins) b->lease_pins--;
-      if (f && l->proc != kCpuProc) {
-        // GPU readers of this block: a later migration away must wait for them.
-        b->tracker.add(f);
-      }
+  // (no VA-space lock: the lease keeps its range alive - free_range refuses a
+  // range with views - and a memory-pressure handler releases leases from
+  // inside a placement that holds it already)
+  for (Block* b : l->blocks) {
+    std::lock_guard<OrderedMutex> g(b->lock);
+    if (b->lease_pins) b->lease_pins--;
+    if (f && l->proc != kCpuProc) {
+      // GPU readers of this block: a later migration away must wait for them.
+      b->tracker.add(f);
     }
   }
   l->range->views.fetch_sub(1);

@@ -48,6 +48,8 @@ Ring::~Ring() {
     last_fence_.reset();
     be_->stream_destroy(stream_);
   }
+  for (void*& e : stage_ev_)
+    if (e) be_->event_destroy(e);
   if (stage_) be_->hbm_free(dev_, stage_, stage_bytes_);
   if (sem_) be_->host_free_coherent(sem_);
 }
@@ -165,6 +167,24 @@ bool Ring::pure_copies(const Batch& b, std::vector<CopyDesc>* out) const {
   return true;
 }
 
+// Batches whose packed-block decodes still run on the stream (run_batch
+// batch_ev_) are published, in order, once their event completed (all: wait
+// for them). Worker thread only.
+Status Ring::publish_deferred_locked(bool all) {
+  Status st = Status::OK;
+  while (!deferred_.empty()) {
+    auto& d = deferred_.front();
+    if (!all && !be_->event_query(d.first)) break;
+    set_phase(Phase::STREAM_DRAIN, d.second);
+    Status s = be_->event_sync(d.first);
+    if (st == Status::OK) st = s;
+    be_->event_destroy(d.first);
+    publish(d.second);
+    deferred_.pop_front();
+  }
+  return st;
+}
+
 // DMA ring worker: batches complete in submission order. A batch of plain
 // copies is issued on one of two completion slots and the worker moves on:
 // the next batch goes to the engines while this one is still copying, so
@@ -183,12 +203,18 @@ void Ring::worker() {
       if (st != Status::INJECTED_ERROR) set_fatal(st, "DMA ring batch failed");
     }
   };
+  auto& deferred = deferred_;
+  auto publish_deferred = [&](bool all) {
+    Status st = publish_deferred_locked(all);
+    if (st != Status::OK) fail(st, submitted_.load());
+  };
   auto complete_pending = [&] {
     if (pend < 0) return;
     set_phase(Phase::COMPLETE, pend_last);
     const uint64_t t0 = now_ns();
     fail(be_->dma_complete(pend), pend_last);
     if (kind_ == RingKind::CPU_TO_GPU) Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
+    publish_deferred(true);  // (tracking values are published in order)
     publish(pend_last);
     pend = -1;
   };
@@ -197,9 +223,10 @@ void Ring::worker() {
     Batch b;
     {
       std::unique_lock<std::mutex> g(wm_);
-      if (work_.empty() && pend >= 0) {  // nothing to overlap with: finish the batch in flight
+      if (work_.empty() && (pend >= 0 || !deferred.empty())) {  // nothing to overlap with: finish what is in flight
         g.unlock();
         complete_pending();
+        publish_deferred(true);
         g.lock();
       }
       if (work_.empty() && !stop_) {
@@ -235,10 +262,22 @@ void Ring::worker() {
       continue;
     }
     complete_pending();
+    publish_deferred(false);  // decodes of earlier batches that are done already
     set_phase(Phase::ISSUE, b.last);
     Status st = err_ == Status::OK ? run_batch(b) : err_.load();
     fail(st, b.last);
+    if (batch_ev_ && st == Status::OK) {
+      deferred.emplace_back(batch_ev_, b.last);
+      batch_ev_ = nullptr;
+      continue;
+    }
+    if (batch_ev_) {
+      (void)be_->event_sync(batch_ev_);
+      be_->event_destroy(batch_ev_);
+      batch_ev_ = nullptr;
+    }
     // Publish even on error (robust channel): waiters then see err_.
+    publish_deferred(true);
     publish(b.last);
   }
 }
@@ -286,6 +325,7 @@ Status Ring::run_batch(Batch& b) {
   uint64_t stage_off = 0;
   Status st = Status::OK;
   bool kernels_pending = false;
+  bool decodes_deferred = false;  // packed-block decodes in flight on the stream (see flush_staged)
   bool final_flush = false;
   auto drain = [&] {
     if (st == Status::OK && kernels_pending) {
@@ -344,19 +384,33 @@ Status Ring::run_batch(Batch& b) {
     copy_dst.clear();
   };
   // Packed blocks: their staging copies go out with the batch's other engine
-  // copies; once those landed ONE k_ans_blocks launch decodes them all. The
-  // next engine copy drains the stream first (flush_copies), so the staging
-  // buffer is never overwritten under a running decode.
+  // copies; once those landed ONE k_ans_blocks launch decodes them all - and
+  // runs while the engines already fill the other half of the staging buffer
+  // (a half is refilled only after the decode that read it, its event). The
+  // decodes' outputs are consumed only through the batch's tracking value,
+  // which the worker publishes once they completed (deferred publish): the
+  // ring never drains its stream for them.
+  bool half_ready = false;  // the current staging half's previous decode is done
   auto flush_staged = [&] {
     if (staged.empty()) return;
     flush_copies();
     if (st == Status::OK) {
       st = be_->decode_ans_blocks(dev_, staged.data(), staged.size(), stream_);
-      kernels_pending = true;
       Tools::get().inc(Counter::PackedDecodes, staged.size());
+      if (st == Status::OK) {
+        if (!stage_ev_[stage_half_]) stage_ev_[stage_half_] = be_->event_create(dev_);
+        if (stage_ev_[stage_half_] && be_->event_record(stage_ev_[stage_half_], stream_) == Status::OK) {
+          stage_used_[stage_half_] = true;
+          decodes_deferred = true;
+        } else {
+          kernels_pending = true;  // no event: drain as for any kernel
+        }
+      }
     }
     staged.clear();
     stage_off = 0;
+    stage_half_ ^= 1;
+    half_ready = false;
   };
   for (auto& s : b.ops) {
     if (st != Status::OK) break;
@@ -380,7 +434,7 @@ Status Ring::run_batch(Batch& b) {
         flush_decodes();
         const uint64_t need = (s.bytes + 255) & ~255ull;
         if (!stage_ && st == Status::OK && config().ans_stage_mb > 0) {  // (0: decode from the host copy)
-          stage_bytes_ = std::max<uint64_t>((uint64_t)config().ans_stage_mb << 20, 2 * kBlockSize);
+          stage_bytes_ = std::max<uint64_t>((uint64_t)config().ans_stage_mb << 20, 4 * kBlockSize);  // two halves
           if (be_->hbm_alloc(dev_, stage_bytes_, &stage_) != Status::OK) {
             stage_ = nullptr;
             stage_bytes_ = 0;
@@ -397,8 +451,18 @@ Status Ring::run_batch(Batch& b) {
           }
           break;
         }
-        if (stage_off + need > stage_bytes_ || staged.size() >= 64) flush_staged();
-        const uint64_t at = (uint64_t)stage_ + stage_off;
+        const uint64_t half = stage_bytes_ / 2;
+        if (stage_off + need > half || staged.size() >= 64) flush_staged();
+        if (!half_ready) {  // the decode that read this half last must be done before the engines refill it
+          if (stage_used_[stage_half_] && st == Status::OK) {
+            set_phase(Phase::STREAM_DRAIN, b.last);
+            st = be_->event_sync(stage_ev_[stage_half_]);
+            set_phase(Phase::ISSUE, b.last);
+          }
+          stage_used_[stage_half_] = false;
+          half_ready = true;
+        }
+        const uint64_t at = (uint64_t)stage_ + stage_half_ * half + stage_off;
         CopyDesc d{at, s.src, need};
         // Packed blocks are ~1.3 MB copies that never coalesce: spread them over
         // several full-rate engines so one engine's per-copy setup overlaps
@@ -425,6 +489,9 @@ Status Ring::run_batch(Batch& b) {
         flush_staged();
         flush_copies();
         if (st == Status::OK && s.wait && !s.wait->done.load(std::memory_order_acquire)) {
+          // Our own deferred tracking values go out before we block on another
+          // ring: that ring may be waiting for one of them (no cycle).
+          if (!deferred_.empty()) st = publish_deferred_locked(true);
           const uint64_t t_wait = now_ns();
           snprintf(phase_what_, sizeof(phase_what_), "%s %s/%d seq %llu (%s:%d %s)",
                    s.wait->event ? "event" : "ring", s.wait->ring ? ring_kind_str(s.wait->ring->kind()) : "-",
@@ -463,6 +530,20 @@ Status Ring::run_batch(Batch& b) {
   if (!kernels_pending) final_flush = true;  // (with kernels queued, the drain below comes first)
   flush_copies();
   drain();
+  if (decodes_deferred && st == Status::OK && !kernels_pending) {
+    // every copy and decode of the batch is issued: the worker publishes its
+    // tracking value when this event completes (in order, Ring::worker)
+    void* ev = be_->event_create(dev_);
+    if (ev && be_->event_record(ev, stream_) == Status::OK) {
+      batch_ev_ = ev;
+      mark_issued(b.last);
+    } else {
+      if (ev) be_->event_destroy(ev);
+      set_phase(Phase::STREAM_DRAIN, b.last);
+      st = be_->stream_sync(stream_);
+      set_phase(Phase::ISSUE, b.last);
+    }
+  }
   return st;
 }
 

@@ -10,9 +10,26 @@ namespace ogkm {
 UnitStream::UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_t window_bytes, bool next_use,
                        uint32_t max_ahead)
     : rt_(rt), dev_(dev), ranges_(std::move(ranges)), window_(window_bytes), next_use_(next_use),
-      max_ahead_(max_ahead) {}
+      max_ahead_(max_ahead) {
+  // Held leases are soft pins: an allocation that finds nothing else to evict
+  // gets them back (from any thread; the owner's own acquire re-enters).
+  pressure_id_ = rt_->add_pressure_handler(dev_, [this] {
+    std::unique_lock<std::recursive_mutex> g(m_, std::try_to_lock);
+    if (!g.owns_lock()) {  // the owner is mid-use on another thread: it drops them next
+      drop_requested_.store(true);
+      return false;
+    }
+    bool any = false;
+    for (Lease* l : held_) any |= l != nullptr;
+    drop_holds(hold_stream_);
+    return any;
+  });
+}
 
 UnitStream::~UnitStream() {
+  rt_->remove_pressure_handler(pressure_id_);
+  std::lock_guard<std::recursive_mutex> g(m_);
+  drop_holds(hold_stream_);
   for (Lease* l : pending_) (void)rt_->release(l, nullptr);
   for (auto& f : ahead_) (void)f->wait();
 }
@@ -23,6 +40,7 @@ uint64_t UnitStream::due(uint32_t pos) const {
 }
 
 void UnitStream::prefetch_window() {
+  std::lock_guard<std::recursive_mutex> g(m_);
   const uint32_t n = (uint32_t)ranges_.size();
   const Loc gpu = Loc::gpu(dev_);
   while (inflight_.size() < n) {
@@ -42,6 +60,7 @@ void UnitStream::prefetch_window() {
       // refused by the floor (no victim needed later than it): left to its use
       ++st_.refused;
       pressure_ = true;
+      pass_quiet_ = false;
       break;
     }
     inflight_.push_back(pf_next_);
@@ -53,6 +72,8 @@ void UnitStream::prefetch_window() {
 
 Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
   if (pos >= ranges_.size()) return Status::INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> g(m_);
+  if (drop_requested_.exchange(false)) drop_holds(stream);
   struct Clock {
     uint64_t& acc;
     uint64_t t0 = now_ns();
@@ -60,12 +81,32 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
   } clock{st_.use_ns};
   const uint64_t n = ranges_.size();
   Range* r = ranges_[pos];
+  const bool new_pass = (int64_t)pos <= cur_pos_;
+  cur_pos_ = pos;
+  if (new_pass) update_hold(stream);
+  if (hold_ && !held_.empty() && held_[pos]) {
+    // Held since its last use (no memory pressure): the same lease again - its
+    // chunks stayed pinned and the stream already waited for them.
+    if (hold_arena_ && hold_arena_->evictions() != hold_ev_) {
+      drop_holds(stream);  // someone needed HBM meanwhile: back to leases per use
+    } else {
+      if (next_use_) {
+        if ((int64_t)pos <= last_pos_) ++pass_;
+        last_pos_ = pos;
+      }
+      *out = held_[pos];
+      held_[pos] = nullptr;
+      ++st_.held;
+      return Status::OK;
+    }
+  }
   if (!inflight_.empty() && inflight_.front() == pos) {
     inflight_.pop_front();
     inflight_bytes_ -= r->size;
   } else {
     ++st_.demand;
     pressure_ = true;
+    pass_quiet_ = false;
   }
   if (next_use_) {  // the op clock moves to this use
     if ((int64_t)pos <= last_pos_) ++pass_;
@@ -94,7 +135,13 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
 }
 
 Status UnitStream::release(Lease* l, void* stream) {
+  std::lock_guard<std::recursive_mutex> g(m_);
   if (!stream || l->proc == kCpuProc) return rt_->release(l, stream);
+  if (hold_ && cur_pos_ >= 0 && (size_t)cur_pos_ < held_.size() && ranges_[cur_pos_] == l->range && !held_[cur_pos_]) {
+    held_[cur_pos_] = l;  // kept until its next use (or until pressure)
+    hold_stream_ = stream;
+    return Status::OK;
+  }
   // Released units are handed back in groups of unit_release_batch behind ONE
   // event recorded after the group's kernels: it is the runtime's reuse fence
   // of their chunks and the run-ahead bound below (every event record is a
@@ -108,6 +155,7 @@ Status UnitStream::release(Lease* l, void* stream) {
 }
 
 Status UnitStream::flush_released(void* stream) {
+  std::lock_guard<std::recursive_mutex> g(m_);
   if (pending_.empty()) return Status::OK;
   FenceRef f = fence_record(rt_->be(), dev_, stream);
   Status st = Status::OK;
@@ -131,6 +179,42 @@ Status UnitStream::flush_released(void* stream) {
     ahead_.pop_front();
   }
   return st;
+}
+
+// Hold mode (config unit_hold): after a whole pass in which the arena evicted
+// nothing and no use streamed (every unit resident - e.g. a model that fits),
+// released units keep their leases until their next use: a use is then a
+// lookup instead of a lease (pins, LRU touches, readiness, hints) and a release
+// is no event record - the host cost of a resident decode step is what the
+// static plan has. The first eviction the arena reports (another allocation
+// needs HBM), a refused prefetch or a demand fault ends it: every held lease
+// is released behind one fence and the next pass decides again.
+void UnitStream::update_hold(void* stream) {
+  ChunkArena* a = rt_->arena_for(Loc::gpu(dev_));
+  const uint64_t ev = a ? a->evictions() : 0;
+  const bool quiet = config().unit_hold && a && pass_quiet_ && ev == pass_ev0_;
+  if (!quiet && hold_) drop_holds(stream);
+  hold_ = quiet;
+  hold_arena_ = a;
+  hold_ev_ = ev;
+  if (hold_ && held_.size() != ranges_.size()) held_.assign(ranges_.size(), nullptr);
+  pass_ev0_ = ev;
+  pass_quiet_ = true;
+}
+
+void UnitStream::drop_holds(void* stream) {
+  hold_ = false;
+  pass_quiet_ = false;
+  bool any = false;
+  for (Lease* l : held_) any |= l != nullptr;
+  if (!any) return;
+  FenceRef f = stream ? fence_record(rt_->be(), dev_, stream) : nullptr;
+  for (Lease*& l : held_)
+    if (l) {
+      (void)rt_->release(l, stream, f);
+      l = nullptr;
+    }
+  ++st_.hold_drops;
 }
 
 }  // namespace ogkm

@@ -63,6 +63,7 @@ namespace ogkm {
   X(perf_spread_step_pct, 2, "spread classes: keep-share reduction per adaptation (percent)") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
   X(lease_fast_path, 1, "acquire: a GPU read of data resident in one contiguous extent only pins, touches and waits (no placement pass)") \
+  X(unit_hold, 1, "UnitStream: after a pass with no eviction and no streaming, released units keep their leases until their next use (dropped at the first eviction / refused prefetch)") \
   X(unit_release_batch, 1, "UnitStream: released units are handed back in groups of this many behind one event (fewer event records on the consumer stream)") \
   X(ring_wait_issued, 1, "a GPU-side wait on a DMA ring value is enqueued only once that value's copies are on the engines (Ring::issued_seq; prevents an SDMA-engine cycle with HIP's own copies)") \
   X(arena_class_sides, 0, "spread classes: HBM extents of keep-class ranges are placed from the arena's low end, stream-class ones from its high end (less fragmentation of kept data by the stream turnover)") \

@@ -203,6 +203,7 @@ enum class Counter : int {
   PackSkips,           // blocks found incompressible (left raw)
   PackExpansions,      // packed copies expanded back to raw pages (a write / CPU access)
   PackedDecodes,       // packed blocks decoded into HBM by the H2D ring (DECODE_ANS)
+  PressureReliefs,     // reservations that found nothing evictable until soft pins let go
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -162,8 +162,14 @@ class Ring {
   std::string err_desc_;
   // DMA mode
   bool dma_ = false;
-  void* stage_ = nullptr;          // HBM staging of packed blocks (DECODE_ANS, worker thread only)
+  void* stage_ = nullptr;          // HBM staging of packed blocks (DECODE_ANS, worker thread only): two halves
   uint64_t stage_bytes_ = 0;
+  uint32_t stage_half_ = 0;        // the half being filled
+  void* stage_ev_[2] = {nullptr, nullptr};  // the last decode that read each half
+  bool stage_used_[2] = {false, false};
+  void* batch_ev_ = nullptr;       // run_batch -> worker: the batch's decodes complete with this event
+  std::deque<std::pair<void*, uint64_t>> deferred_;  // (event, tracking value) published once it completes
+  Status publish_deferred_locked(bool all);
   std::thread worker_;
   std::mutex wm_;
   std::condition_variable wcv_;

@@ -12,6 +12,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -326,6 +327,14 @@ class Runtime {
   void stop_fault_service();
   uint64_t fault_service_batches() const { return fs_batches_.load(); }
 
+  // ---- memory pressure: holders of soft pins (UnitStream hold mode) register a
+  // handler that lets go of them; a GPU reservation that finds nothing
+  // evictable runs the device's handlers once and retries.
+  using PressureFn = std::function<bool()>;  // true: something was released
+  uint64_t add_pressure_handler(int dev, PressureFn f);
+  void remove_pressure_handler(uint64_t id);
+  bool relieve_pressure(const Loc& l);
+
   // ---- packed host copies (packer.cpp): read-mostly blocks keep a lossless
   // ANS1-packed host / CXL copy; the H2D ring moves and decodes the packed bytes.
   Status expand_packed(Block* b, Residency* r);  // back to raw pages (block lock held)
@@ -429,6 +438,9 @@ class Runtime {
   std::vector<int> perf_subs_;  // perf-module subscriptions on the tools bus
   std::mutex channels_m_;
   std::vector<Channel> channels_;  // slot id - 1 (id 0 = no channel); unregistered slots keep id 0
+  std::mutex pressure_m_;
+  std::vector<std::tuple<uint64_t, int, PressureFn>> pressure_;
+  uint64_t pressure_next_ = 1;
   // packer (packer.cpp)
   struct PackJob {
     uint64_t range = 0, block = 0;

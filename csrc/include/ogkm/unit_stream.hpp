@@ -16,7 +16,9 @@
 #pragma once
 
 #include <cstdint>
+#include <atomic>
 #include <deque>
+#include <mutex>
 #include <vector>
 
 #include "ogkm/common.hpp"
@@ -26,13 +28,14 @@ namespace ogkm {
 
 class Runtime;
 class Range;
+class ChunkArena;
 struct Lease;
 
 class UnitStream {
  public:
   struct Stats {
     uint64_t prefetched = 0, refused = 0, demand = 0, prefetch_ns = 0, acquire_ns = 0, ahead_wait_ns = 0, hint_ns = 0,
-             wait_ns = 0, use_ns = 0;
+             wait_ns = 0, use_ns = 0, held = 0, hold_drops = 0;
   };
   // `ranges`: the units in use order; `window_bytes`: bytes of following units
   // kept in flight; `next_use`: hint next uses / floor prefetches (planner off);
@@ -70,6 +73,20 @@ class UnitStream {
   std::deque<FenceRef> ahead_;  // fences of released groups (host bound)
   std::vector<Lease*> pending_; // released, not yet handed back
   bool pressure_ = false;       // this group's uses streamed (close it now)
+  // hold mode (see update_hold)
+  void update_hold(void* stream);
+  void drop_holds(void* stream);
+  std::vector<Lease*> held_;    // per unit: its lease, kept since its last release
+  bool hold_ = false;
+  bool pass_quiet_ = false;     // this pass: no demand fault, no refused prefetch
+  uint64_t pass_ev0_ = ~0ull;   // arena evictions at the pass start
+  ChunkArena* hold_arena_ = nullptr;
+  uint64_t hold_ev_ = 0;
+  void* hold_stream_ = nullptr;
+  int64_t cur_pos_ = -1;        // the unit of the latest use
+  std::recursive_mutex m_;      // use / release / the pressure handler (any thread)
+  std::atomic<bool> drop_requested_{false};
+  uint64_t pressure_id_ = 0;
   Stats st_;
 };
 

@@ -491,13 +491,6 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // P.V on the vector ALUs, bound by how many V bytes are in flight: lane l
-    // owns 8 dims (dim group l % LPT) of every TPI-th token (token group
-    // l / LPT); one wave instruction loads TPI whole V rows (1 KB) and VB of
-    // them are issued before the first FMA (8 KB per wave for G <= 8 - the
-    // half-wave-per-token loop had 2 KB in flight and capped the tp8 shape,
-    // one KV head per batch row, at ~1.3 TB/s). The token groups' partial
-    // sums are reduced with xor shuffles at the end.
-    // P.V on the vector ALUs, bound by how many V bytes are in flight: lane l
     // owns DPL dims (dim group l % LPT) of every TPI-th token (token group
     // l / LPT); one wave instruction loads TPI whole V rows and VB of them are
     // issued before the first FMA (8 KB per wave for G <= 8 - the

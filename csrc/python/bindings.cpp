@@ -332,6 +332,8 @@ PYBIND11_MODULE(_ogkm, m) {
              d["hint_ms"] = st.hint_ns / 1e6;
              d["wait_ms"] = st.wait_ns / 1e6;
              d["use_ms"] = st.use_ns / 1e6;
+             d["held"] = st.held;
+             d["hold_drops"] = st.hold_drops;
              return d;
            })
       .def("reset_stats", &UnitStream::reset_stats);

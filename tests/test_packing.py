@@ -203,3 +203,21 @@ def test_written_block_goes_back_whole_without_expansion(fake_rt):
     assert b.read().equal(data)
     assert _gpu_read(b).equal(data)
     b.free()
+
+
+def test_staging_halves_rotate_under_many_packed_blocks(fake_rt):
+    """More packed blocks than one staging half holds, in one refill: the ring
+    alternates the halves (each refilled only after the decode that read it)
+    and publishes the batch once its decodes completed."""
+    rt.configure(pack_host_copies=1, pack_threads=2, ans_stage_mb=8)  # 2 x 4 MB halves: ~3 blocks each
+    b = rt.malloc_managed(24 * MB, "many")
+    data = _weights(b.size, 11)
+    b.write(data)
+    _pack(b)
+    assert len(_packed_entries(b)) == 12
+    s0 = lib.stats()
+    for _ in range(3):
+        assert _gpu_read(b).equal(data)
+        b.evict("gpu:0")
+    assert lib.stats()["packed_decodes"] - s0["packed_decodes"] == 36
+    b.free()

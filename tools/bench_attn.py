@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Decode-attention microbenchmark (k_attn_decode_ws + combine): one layer's KV
 at the bench shapes, time per call and effective KV-read bandwidth.
-    python tools/bench_attn.py"""
+    python tools/bench_attn.py            (GRAPH=0: eager calls, SPLIT=64|256, COLD=0)"""
 import os
 import sys
 
@@ -23,6 +23,7 @@ SHAPES = {  # name: (B, hq, hkv, hd, len)
 def main() -> None:
     rt.init("hip")
     iters = int(os.environ.get("ITERS", "50"))
+    graph = int(os.environ.get("GRAPH", "1"))  # 0: back-to-back eager calls (includes host launch cost)
     for name, (B, hq, hkv, hd, L) in SHAPES.items():
         T = L
         q = torch.randn(B, hq, hd, device="cuda").to(torch.bfloat16)
@@ -36,15 +37,30 @@ def main() -> None:
             fused.attention(q, caches[i % ncopy], L, split_tokens=st)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for i in range(iters):
-            fused.attention(q, caches[i % ncopy], L, split_tokens=st)
-        e1.record()
+        if graph:
+            # GPU time only: the calls captured once into a graph and replayed
+            # (a one-KV-head layer's KV is ~33 MB, ~10 us - less than the
+            # host-side launch cost of one call)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i in range(iters):
+                    fused.attention(q, caches[i % ncopy], L, split_tokens=st)
+            g.replay()
+            torch.cuda.synchronize()
+            e0.record()
+            g.replay()
+            e1.record()
+        else:
+            e0.record()
+            for i in range(iters):
+                fused.attention(q, caches[i % ncopy], L, split_tokens=st)
+            e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / iters
         gb = 2 * B * hkv * L * hd * 2 / 1e9
         print(f"{name:9s} B={B} hq={hq} hkv={hkv} hd={hd} len={L} {us:8.1f} us  "
-              f"KV {gb * 1e3:7.1f} MB  {gb / (us * 1e-6):7.0f} GB/s  split {st or 'auto'}", flush=True)
+              f"KV {gb * 1e3:7.1f} MB  {gb / (us * 1e-6):7.0f} GB/s  split {st or 'auto'}  {'graph' if graph else 'eager'}",
+              flush=True)
         del caches
 
 
