@@ -160,7 +160,8 @@ const char* counter_name(Counter c) {
                             "pack_skips",
                             "pack_expansions",
                             "packed_decodes",
-                            "pressure_reliefs"};
+                            "pressure_reliefs",
+                            "decode_reuse_waits"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -174,12 +174,12 @@ Status Ring::publish_deferred_locked(bool all) {
   Status st = Status::OK;
   while (!deferred_.empty()) {
     auto& d = deferred_.front();
-    if (!all && !be_->event_query(d.first)) break;
-    set_phase(Phase::STREAM_DRAIN, d.second);
-    Status s = be_->event_sync(d.first);
+    if (!all && !be_->event_query(d.ev)) break;
+    set_phase(Phase::STREAM_DRAIN, d.last);
+    Status s = be_->event_sync(d.ev);
     if (st == Status::OK) st = s;
-    be_->event_destroy(d.first);
-    publish(d.second);
+    be_->event_destroy(d.ev);
+    publish(d.last);
     deferred_.pop_front();
   }
   return st;
@@ -267,8 +267,9 @@ void Ring::worker() {
     Status st = err_ == Status::OK ? run_batch(b) : err_.load();
     fail(st, b.last);
     if (batch_ev_ && st == Status::OK) {
-      deferred.emplace_back(batch_ev_, b.last);
+      deferred.push_back(Deferred{batch_ev_, b.last, std::move(batch_dst_)});
       batch_ev_ = nullptr;
+      batch_dst_.clear();
       continue;
     }
     if (batch_ev_) {
@@ -276,6 +277,7 @@ void Ring::worker() {
       be_->event_destroy(batch_ev_);
       batch_ev_ = nullptr;
     }
+    batch_dst_.clear();
     // Publish even on error (robust channel): waiters then see err_.
     publish_deferred(true);
     publish(b.last);
@@ -363,6 +365,28 @@ Status Ring::run_batch(Batch& b) {
         }
         copies.swap(split);
       }
+      // A copy into a chunk a still-running packed-block decode writes (the
+      // chunk was freed and handed out again since - same-ring fences are not
+      // waited for, the ring used to be in order) waits for that decode:
+      // earlier batches' (deferred) or this batch's own.
+      if (st == Status::OK && (!deferred_.empty() || decodes_deferred)) {
+        auto hits = [&](const std::vector<std::pair<uint64_t, uint64_t>>& dst) {
+          for (const CopyDesc& c : copies)
+            for (const auto& d : dst)
+              if (c.dst < d.first + d.second && d.first < c.dst + c.bytes) return true;
+          return false;
+        };
+        bool prior = false;
+        for (const auto& d : deferred_) prior |= hits(d.dst);
+        if (prior) st = publish_deferred_locked(true);
+        if (st == Status::OK && decodes_deferred && hits(batch_dst_)) {
+          set_phase(Phase::STREAM_DRAIN, b.last);
+          st = be_->stream_sync(stream_);
+          set_phase(Phase::ISSUE, b.last);
+          Tools::get().inc(Counter::DecodeReuseWaits);
+        }
+        if (prior) Tools::get().inc(Counter::DecodeReuseWaits);
+      }
       if (st == Status::OK) {
         const uint64_t t_copy = now_ns();
         snprintf(phase_what_, sizeof(phase_what_), "engine copy: %zu descriptors, first %llu B", copies.size(),
@@ -397,9 +421,12 @@ Status Ring::run_batch(Batch& b) {
     if (st == Status::OK) {
       st = be_->decode_ans_blocks(dev_, staged.data(), staged.size(), stream_);
       Tools::get().inc(Counter::PackedDecodes, staged.size());
+      for (const DecodeDesc& d : staged) batch_dst_.emplace_back(d.dst, 2ull * d.n_values);
       if (st == Status::OK) {
         if (!stage_ev_[stage_half_]) stage_ev_[stage_half_] = be_->event_create(dev_);
-        if (stage_ev_[stage_half_] && be_->event_record(stage_ev_[stage_half_], stream_) == Status::OK) {
+        if (!config().ring_defer_decodes) {
+          kernels_pending = true;  // drained before the next copies, as any kernel
+        } else if (stage_ev_[stage_half_] && be_->event_record(stage_ev_[stage_half_], stream_) == Status::OK) {
           stage_used_[stage_half_] = true;
           decodes_deferred = true;
         } else {

@@ -86,6 +86,7 @@ namespace ogkm {
   X(pack_min_saving_pct, 8, "a block is kept packed only when its packed form saves at least this share of its bytes") \
   X(pack_threads, 4, "host encoder threads of the packer") \
   X(ans_stage_mb, 64, "per-H2D-ring HBM staging buffer the packed bytes land in before the decode kernel (0: the kernel reads the host copy over PCIe)") \
+  X(ring_defer_decodes, 1, "H2D ring: packed-block decodes overlap the next batch (two staging halves, deferred publish); 0 = drain after each batch's decodes") \
   X(ans_stage_engines, 0x9, "SDMA engines (mask) the H2D ring spreads packed-block staging copies over (0 = the ring's own engine)") \
   X(host_segment_mb, 1024, "host / CXL arenas populate, pin and reserve their memory in segments of this many MB") \
   /* channels / ring */                                                                              \

@@ -204,6 +204,7 @@ enum class Counter : int {
   PackExpansions,      // packed copies expanded back to raw pages (a write / CPU access)
   PackedDecodes,       // packed blocks decoded into HBM by the H2D ring (DECODE_ANS)
   PressureReliefs,     // reservations that found nothing evictable until soft pins let go
+  DecodeReuseWaits,    // H2D copies that waited for a running packed-block decode into the same chunk
   NumCounters
 };
 const char* counter_name(Counter c);

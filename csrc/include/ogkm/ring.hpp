@@ -168,7 +168,13 @@ class Ring {
   void* stage_ev_[2] = {nullptr, nullptr};  // the last decode that read each half
   bool stage_used_[2] = {false, false};
   void* batch_ev_ = nullptr;       // run_batch -> worker: the batch's decodes complete with this event
-  std::deque<std::pair<void*, uint64_t>> deferred_;  // (event, tracking value) published once it completes
+  std::vector<std::pair<uint64_t, uint64_t>> batch_dst_;  // this batch's decode destinations (addr, bytes)
+  struct Deferred {
+    void* ev;
+    uint64_t last;
+    std::vector<std::pair<uint64_t, uint64_t>> dst;  // HBM the decodes write
+  };
+  std::deque<Deferred> deferred_;  // published once its event completes
   Status publish_deferred_locked(bool all);
   std::thread worker_;
   std::mutex wm_;
