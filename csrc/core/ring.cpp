@@ -185,6 +185,14 @@ Status Ring::publish_deferred_locked(bool all) {
   return st;
 }
 
+bool Ring::copies_hit_deferred(const std::vector<CopyDesc>& copies) const {
+  for (const auto& d : deferred_)
+    for (const CopyDesc& c : copies)
+      for (const auto& r : d.dst)
+        if (c.dst < r.first + r.second && r.first < c.dst + c.bytes) return true;
+  return false;
+}
+
 // DMA ring worker: batches complete in submission order. A batch of plain
 // copies is issued on one of two completion slots and the worker moves on:
 // the next batch goes to the engines while this one is still copying, so
@@ -242,6 +250,12 @@ void Ring::worker() {
     }
     if (err_ == Status::OK && config().ring_pipeline && pure_copies(b, &copies)) {
       const int slot = pend == 0 ? 1 : 0;
+      // a copy into a chunk a deferred packed-block decode still writes (the
+      // chunk was handed out again): that decode first (see run_batch)
+      if (!deferred_.empty() && copies_hit_deferred(copies)) {
+        publish_deferred(true);
+        Tools::get().inc(Counter::DecodeReuseWaits);
+      }
       set_phase(Phase::ISSUE, b.last);
       const uint64_t t0 = now_ns();
       Status st = copies.empty() ? Status::OK : be_->dma_issue(dev_, copies.data(), copies.size(), (int)kind_, slot);
@@ -376,8 +390,7 @@ Status Ring::run_batch(Batch& b) {
               if (c.dst < d.first + d.second && d.first < c.dst + c.bytes) return true;
           return false;
         };
-        bool prior = false;
-        for (const auto& d : deferred_) prior |= hits(d.dst);
+        const bool prior = copies_hit_deferred(copies);
         if (prior) st = publish_deferred_locked(true);
         if (st == Status::OK && decodes_deferred && hits(batch_dst_)) {
           set_phase(Phase::STREAM_DRAIN, b.last);

@@ -176,6 +176,7 @@ class Ring {
   };
   std::deque<Deferred> deferred_;  // published once its event completes
   Status publish_deferred_locked(bool all);
+  bool copies_hit_deferred(const std::vector<CopyDesc>& copies) const;
   std::thread worker_;
   std::mutex wm_;
   std::condition_variable wcv_;
