@@ -408,7 +408,9 @@ class FakeBackend : public Backend {
   }
   Status decode_ans_blocks(int, const DecodeDesc* d, size_t n, void* s) override {
     std::vector<DecodeDesc> v(d, d + n);
-    run(s, [v] {
+    const int64_t delay = config().fake_kernel_delay_us;  // a slow decode: exposes ordering races in tests
+    run(s, [v, delay] {
+      if (delay) std::this_thread::sleep_for(std::chrono::microseconds(delay));
       for (auto& x : v)
         if (!ans_decode((const uint8_t*)x.src, (uint16_t*)x.dst, x.n_values)) memset((void*)x.dst, 0, 2ull * x.n_values);
     });

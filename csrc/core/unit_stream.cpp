@@ -11,6 +11,7 @@ UnitStream::UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_
                        uint32_t max_ahead)
     : rt_(rt), dev_(dev), ranges_(std::move(ranges)), window_(window_bytes), next_use_(next_use),
       max_ahead_(max_ahead) {
+  for (uint32_t i = 0; i < ranges_.size(); ++i) pos_of_.emplace(ranges_[i], i);
   // Held leases are soft pins: an allocation that finds nothing else to evict
   // gets them back (from any thread; the owner's own acquire re-enters).
   pressure_id_ = rt_->add_pressure_handler(dev_, [this] {
@@ -137,10 +138,13 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
 Status UnitStream::release(Lease* l, void* stream) {
   std::lock_guard<std::recursive_mutex> g(m_);
   if (!stream || l->proc == kCpuProc) return rt_->release(l, stream);
-  if (hold_ && cur_pos_ >= 0 && (size_t)cur_pos_ < held_.size() && ranges_[cur_pos_] == l->range && !held_[cur_pos_]) {
-    held_[cur_pos_] = l;  // kept until its next use (or until pressure)
-    hold_stream_ = stream;
-    return Status::OK;
+  if (hold_ && l->offset == 0 && l->bytes == l->range->size) {
+    auto it = pos_of_.find(l->range);
+    if (it != pos_of_.end() && it->second < held_.size() && !held_[it->second]) {
+      held_[it->second] = l;  // kept until its next use (or until pressure)
+      hold_stream_ = stream;
+      return Status::OK;
+    }
   }
   // Released units are handed back in groups of unit_release_batch behind ONE
   // event recorded after the group's kernels: it is the runtime's reuse fence

@@ -119,6 +119,7 @@ namespace ogkm {
   X(lock_check, 0, "enable the lock-order checker")                                                  \
   X(fake_race_check, 0, "fake backend: report kernels (debug_touch) that touch a chunk an engine copy is using") \
   X(fake_dma_delay_us, 0, "fake backend: microseconds every SDMA batch takes (ordering tests)")       \
+  X(fake_kernel_delay_us, 0, "fake backend: each packed-block decode launch sleeps this long on its stream (tests)") \
   X(leak_check, 1, "track outstanding arena bytes")                                                  \
   X(release_asserts, 1, "release asserts set the sticky fatal error")                                \
   X(tools_queue_entries, 4096, "entries per tools event queue")

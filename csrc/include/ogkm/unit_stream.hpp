@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <atomic>
 #include <deque>
+#include <unordered_map>
 #include <mutex>
 #include <vector>
 
@@ -84,6 +85,7 @@ class UnitStream {
   uint64_t hold_ev_ = 0;
   void* hold_stream_ = nullptr;
   int64_t cur_pos_ = -1;        // the unit of the latest use
+  std::unordered_map<const Range*, uint32_t> pos_of_;  // unit -> its position
   std::recursive_mutex m_;      // use / release / the pressure handler (any thread)
   std::atomic<bool> drop_requested_{false};
   uint64_t pressure_id_ = 0;

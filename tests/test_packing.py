@@ -221,3 +221,38 @@ def test_staging_halves_rotate_under_many_packed_blocks(fake_rt):
         b.evict("gpu:0")
     assert lib.stats()["packed_decodes"] - s0["packed_decodes"] == 36
     b.free()
+
+
+def test_slow_decodes_never_race_chunk_reuse(fake_rt):
+    """Packed-block decodes run behind the ring (their batch is published once
+    they are done) while the next batches' copies go out: with a slow decode
+    and an arena so small that just-decoded chunks are evicted and handed out
+    again at once, every refill still reads back exactly (a copy into a chunk a
+    decode still writes waits for that decode)."""
+    rt.configure(pack_host_copies=1, pack_threads=2, fake_kernel_delay_us=3000)
+    lib.init_device(0, 12 * MB)  # 6 chunks
+    bufs, datas = [], []
+    for i in range(6):
+        b = rt.malloc_managed(4 * MB, f"s{i}")
+        d = _weights(b.size, 20 + i) if i % 2 == 0 else torch.randint(0, 256, (4 * MB,), dtype=torch.uint8)
+        b.write(d)
+        b.set_read_mostly(True)
+        bufs.append(b)
+        datas.append(d)
+    for b in bufs:  # one clean drop each: the bf16-like ones get packed
+        l = b.acquire(0, rt.READ)
+        l.wait(0)
+        l.release(0)
+        b.evict("gpu:0")
+    assert lib.pack_wait(30000)
+    assert sum(len(_packed_entries(b)) for b in bufs) == 6
+    for rnd in range(4):
+        # a burst of prefetches nobody waits for: each evicts the oldest
+        # buffer's chunks - a packed one's decode may still be running there
+        for b in bufs:
+            b.prefetch("gpu:0")
+        for i in (5, 4, 3):  # the three the burst left resident
+            assert _gpu_read(bufs[i]).equal(datas[i]), (rnd, i)
+    assert lib.stats()["packed_decodes"] > 0
+    for b in bufs:
+        b.free()
