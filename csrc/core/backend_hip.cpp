@@ -209,6 +209,7 @@ class HipBackend : public Backend {
   }
   void hbm_free(int dev, void* p, size_t) override {
     if (!p) return;
+    reg_gen_.fetch_add(1, std::memory_order_acq_rel);
     (void)hipSetDevice(dev);
     (void)hipFree(p);
   }
@@ -460,6 +461,7 @@ class HipBackend : public Backend {
     return Status::OK;
   }
   void host_unregister(void* p) override {
+    reg_gen_.fetch_add(1, std::memory_order_acq_rel);
     (void)hipHostUnregister(p);
     std::lock_guard<std::mutex> g(reg_m_);
     regs_.erase((uint64_t)p);
@@ -477,7 +479,10 @@ class HipBackend : public Backend {
     memset(*p, 0, bytes);
     return Status::OK;
   }
-  void host_free_coherent(void* p) override { (void)hipHostFree(p); }
+  void host_free_coherent(void* p) override {
+    reg_gen_.fetch_add(1, std::memory_order_acq_rel);
+    (void)hipHostFree(p);
+  }
 
   void* stream_create(int dev, int prio) override {
     (void)hipSetDevice(dev);
@@ -1068,7 +1073,30 @@ class HipBackend : public Backend {
   }
   // Device-usable address and agent of `p` for an SDMA copy: HBM -> its GPU agent,
   // locked / pinned host (and CXL) memory -> the CPU agent at its agent address.
+  // ROCr allocation lookups cached per worker thread: a ring worker resolves
+  // two pointers per engine copy (~39k copies per transparent 70B step), each a
+  // locked map lookup inside ROCr. Entries are dropped when any registration or
+  // allocation goes away (reg_gen_).
+  struct ResolveHit {
+    uint64_t lo = 0, hi = 0, gen = ~0ull, agent = 0;
+    int64_t delta = 0;
+    const void* dd = nullptr;
+  };
   bool dma_resolve(void* p, const DmaDev& dd, void** out, hsa_agent_t* agent) {
+    thread_local ResolveHit cache[8];
+    thread_local uint32_t next_slot = 0;
+    const uint64_t a = (uint64_t)p, gen = reg_gen_.load(std::memory_order_acquire);
+    for (auto& c : cache)
+      if (c.gen == gen && c.dd == &dd && a >= c.lo && a < c.hi) {
+        agent->handle = c.agent;
+        *out = (void*)(a + c.delta);
+        return true;
+      }
+    auto remember = [&](uint64_t lo, uint64_t bytes) {
+      if (!bytes) return;
+      ResolveHit& c = cache[next_slot++ % 8];
+      c = ResolveHit{lo, lo + bytes, gen, agent->handle, (int64_t)((uint64_t)*out - a), &dd};
+    };
     hsa_amd_pointer_info_t info;
     memset(&info, 0, sizeof info);
     info.size = sizeof info;
@@ -1083,11 +1111,13 @@ class HipBackend : public Backend {
         if (info.agentOwner.handle) hsa_agent_get_info(info.agentOwner, HSA_AGENT_INFO_DEVICE, &t);
         *agent = (t == HSA_DEVICE_TYPE_CPU || !info.agentOwner.handle) ? dd.cpu : info.agentOwner;
         *out = p;
+        if (info.type != HSA_EXT_POINTER_TYPE_HSA_VMEM) remember((uint64_t)info.agentBaseAddress, info.sizeInBytes);
         return true;
       }
       case HSA_EXT_POINTER_TYPE_LOCKED:
         *agent = dd.cpu;
         *out = (char*)info.agentBaseAddress + ((char*)p - (char*)info.hostBaseAddress);
+        remember((uint64_t)info.hostBaseAddress, info.sizeInBytes);
         return true;
       default:
         // Host memory registered through HIP's SVM path is not in ROCr's
@@ -1130,6 +1160,7 @@ class HipBackend : public Backend {
   std::mutex ev_m_, df_m_, reg_m_;
   std::map<uint64_t, uint64_t> regs_;  // host registrations: base -> bytes
   std::map<uint64_t, std::pair<uint64_t, int>> vmm_maps_;  // VMM mappings: va -> (bytes, device)
+  std::atomic<uint64_t> reg_gen_{0};  // bumped when memory dma_resolve may have cached goes away
   std::map<uint64_t, std::pair<uint64_t, int>> rocr_vas_;  // stable VAs remapped through ROCr: base -> (bytes, device)
   std::unordered_map<uint64_t, uint64_t> handle_home_;     // HIP VMM handle -> a VA HIP mapped it at
   std::unordered_map<uint64_t, hsa_amd_vmem_alloc_handle_t> rocr_h_;  // HIP VMM handle -> retained ROCr handle

@@ -15,6 +15,7 @@ UnitStream::UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_
   // Held leases are soft pins: an allocation that finds nothing else to evict
   // gets them back (from any thread; the owner's own acquire re-enters).
   pressure_id_ = rt_->add_pressure_handler(dev_, [this] {
+    pressure_calls_.fetch_add(1, std::memory_order_relaxed);
     std::unique_lock<std::recursive_mutex> g(m_, std::try_to_lock);
     if (!g.owns_lock()) {  // the owner is mid-use on another thread: it drops them next
       drop_requested_.store(true);
@@ -105,9 +106,10 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
     inflight_.pop_front();
     inflight_bytes_ -= r->size;
   } else {
+    // not in the window: a use out of the prefetch order (not by itself
+    // pressure - a resident unit faults in for free; evictions tell)
     ++st_.demand;
     pressure_ = true;
-    pass_quiet_ = false;
   }
   if (next_use_) {  // the op clock moves to this use
     if ((int64_t)pos <= last_pos_) ++pass_;
@@ -197,6 +199,9 @@ void UnitStream::update_hold(void* stream) {
   ChunkArena* a = rt_->arena_for(Loc::gpu(dev_));
   const uint64_t ev = a ? a->evictions() : 0;
   const bool quiet = config().unit_hold && a && pass_quiet_ && ev == pass_ev0_;
+  if (quiet) ++st_.quiet_passes;
+  else if (!pass_quiet_) ++st_.loud_streaming;
+  else if (ev != pass_ev0_) ++st_.loud_evictions;
   if (!quiet && hold_) drop_holds(stream);
   hold_ = quiet;
   hold_arena_ = a;

@@ -36,7 +36,8 @@ class UnitStream {
  public:
   struct Stats {
     uint64_t prefetched = 0, refused = 0, demand = 0, prefetch_ns = 0, acquire_ns = 0, ahead_wait_ns = 0, hint_ns = 0,
-             wait_ns = 0, use_ns = 0, held = 0, hold_drops = 0;
+             wait_ns = 0, use_ns = 0, held = 0, hold_drops = 0, quiet_passes = 0, loud_streaming = 0,
+             loud_evictions = 0, pressure_calls = 0;
   };
   // `ranges`: the units in use order; `window_bytes`: bytes of following units
   // kept in flight; `next_use`: hint next uses / floor prefetches (planner off);
@@ -54,7 +55,11 @@ class UnitStream {
   Status flush_released(void* stream);
   // Keep the window full (the step's start: nothing used yet).
   void prefetch_window();
-  const Stats& stats() const { return st_; }
+  Stats stats() const {
+    Stats s = st_;
+    s.pressure_calls = pressure_calls_.load(std::memory_order_relaxed);
+    return s;
+  }
   void reset_stats() { st_ = Stats{}; }
   uint32_t size() const { return (uint32_t)ranges_.size(); }
 
@@ -89,6 +94,7 @@ class UnitStream {
   std::recursive_mutex m_;      // use / release / the pressure handler (any thread)
   std::atomic<bool> drop_requested_{false};
   uint64_t pressure_id_ = 0;
+  std::atomic<uint64_t> pressure_calls_{0};
   Stats st_;
 };
 

@@ -401,7 +401,9 @@ __global__ void __launch_bounds__(256) k_attn_decode(AttnArgs a) {
 typedef __bf16 attn_bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float attn_f32x4_t __attribute__((ext_vector_type(4)));
 
-template <int HD, int G, int NW, int DPL>
+// Variants (OGKM_ATTN_VAR, A/B drills): TH4 - all four K tiles in flight at
+// once; EV - the first V round is requested before the softmax.
+template <int HD, int G, int NW, int DPL, bool TH4, bool EV>
 __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
   constexpr int KS = HD / 32;         // 32-dim MFMA steps
   static_assert((HD == 64 || HD == 128) && G <= 16, "shape");
@@ -437,7 +439,7 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
     // A fragments: 4 token tiles x KS dim steps, two tiles' loads in flight at a
     // time for big groups (the P.V accumulators need the registers), all four
     // for small ones (rows past the context are clamped and masked below)
-    constexpr int TH = 2;
+    constexpr int TH = TH4 ? 4 : 2;
     attn_f32x4_t sc[4];
 #pragma unroll 1
     for (int t0 = 0; t0 < 4; t0 += TH) {
@@ -460,6 +462,32 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
         sc[t0 + t] = acc;
       }
     }
+    // P.V geometry (see below)
+    static_assert(DPL == 8 || DPL == 4, "dims per lane");
+    constexpr int LPT = HD / DPL, TPI = 64 / LPT, NI = 64 / TPI;
+    constexpr int VB = 8;
+    const uint32_t tg = lane / LPT, dg = lane % LPT;
+    const uint16_t* vcol = vbase + (uint64_t)wt0 * HD + dg * DPL;
+    uint32_t vv[VB][DPL / 2];
+    auto load_v = [&](int i0) {
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const int32_t t = (i0 + i) * TPI + (int32_t)tg;
+        const int32_t tt = t < wn ? t : wn - 1;  // past the context: clamped, its p is 0
+        if constexpr (DPL == 8) {
+          const uint4 w = *reinterpret_cast<const uint4*>(vcol + (uint64_t)tt * HD);
+          vv[i][0] = w.x;
+          vv[i][1] = w.y;
+          vv[i][2] = w.z;
+          vv[i][3] = w.w;
+        } else {
+          const uint2 w = *reinterpret_cast<const uint2*>(vcol + (uint64_t)tt * HD);
+          vv[i][0] = w.x;
+          vv[i][1] = w.y;
+        }
+      }
+    };
+    if constexpr (EV) load_v(0);  // the first V round flies during the softmax
     // softmax partials: lane = head col, tokens t*16 + 4*quad + r
     float m = -INFINITY;
 #pragma unroll
@@ -499,35 +527,14 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
     // sums are reduced with xor shuffles at the end.
     // DPL dims per lane (template): 8 - one 16 B load per row piece (groups of
     // up to 4 heads); 4 - 96 VGPRs and four waves per SIMD for 8 and 16 heads.
-    static_assert(DPL == 8 || DPL == 4, "dims per lane");
-    constexpr int LPT = HD / DPL, TPI = 64 / LPT, NI = 64 / TPI;
-    constexpr int VB = 8;
-    const uint32_t tg = lane / LPT, dg = lane % LPT;
     float o[G][DPL];
 #pragma unroll
     for (int h = 0; h < G; ++h)
 #pragma unroll
       for (int j = 0; j < DPL; ++j) o[h][j] = 0.f;
-    const uint16_t* vcol = vbase + (uint64_t)wt0 * HD + dg * DPL;
 #pragma unroll 1
     for (int i0 = 0; i0 < NI; i0 += VB) {
-      uint32_t vv[VB][DPL / 2];
-#pragma unroll
-      for (int i = 0; i < VB; ++i) {
-        const int32_t t = (i0 + i) * TPI + (int32_t)tg;
-        const int32_t tt = t < wn ? t : wn - 1;  // past the context: clamped, its p is 0
-        if constexpr (DPL == 8) {
-          const uint4 w = *reinterpret_cast<const uint4*>(vcol + (uint64_t)tt * HD);
-          vv[i][0] = w.x;
-          vv[i][1] = w.y;
-          vv[i][2] = w.z;
-          vv[i][3] = w.w;
-        } else {
-          const uint2 w = *reinterpret_cast<const uint2*>(vcol + (uint64_t)tt * HD);
-          vv[i][0] = w.x;
-          vv[i][1] = w.y;
-        }
-      }
+      if (!EV || i0) load_v(i0);
 #pragma unroll
       for (int i = 0; i < VB; ++i) {
         const int32_t t = (i0 + i) * TPI + (int32_t)tg;
@@ -643,12 +650,18 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
   const uint32_t nw = st / 64;
   const size_t lds = (size_t)nw * (gg * 64 + g * a.hd) * sizeof(float);  // token-major p (G padded) + outputs
   if (ws) {
-#define OGKM_ATTN_WS(HD, L, NW, D) \
-  hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW, D>), grid, dim3(64 * NW), lds, s, a)
+#define OGKM_ATTN_WS(HD, L, NW, D)                                                                      \
+  do switch (var) {                                                                                    \
+    case 1: hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW, D, true, false>), grid, dim3(64 * NW), lds, s, a); break; \
+    case 2: hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW, D, false, true>), grid, dim3(64 * NW), lds, s, a); break; \
+    case 3: hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW, D, true, true>), grid, dim3(64 * NW), lds, s, a); break;  \
+    default: hipLaunchKernelGGL((k_attn_decode_ws<HD, L, NW, D, false, false>), grid, dim3(64 * NW), lds, s, a);      \
+  } while (0)
     // groups of 8: 4 dims per lane at every measured shape (70B tp8 1.56 vs 1.42 TB/s with 8,
     // 70B 3.76 vs 2.70; gpurun_out/r5/g_attn_dpl*.log); OGKM_ATTN_DPL=8 for A/B drills
     static const int force_dpl = getenv("OGKM_ATTN_DPL") ? atoi(getenv("OGKM_ATTN_DPL")) : 0;
     const bool wide = force_dpl == 8;
+    static const int var = getenv("OGKM_ATTN_VAR") ? atoi(getenv("OGKM_ATTN_VAR")) : 0;
 #define OGKM_ATTN_WS_G(HD, NW)                      \
   if (gg == 4) OGKM_ATTN_WS(HD, 4, NW, 8);          \
   else if (gg == 8 && wide) OGKM_ATTN_WS(HD, 8, NW, 8); \

@@ -321,7 +321,7 @@ PYBIND11_MODULE(_ogkm, m) {
              u.prefetch_window();
            })
       .def("stats", [](UnitStream& u) {
-             const auto& st = u.stats();
+             const auto st = u.stats();
              py::dict d;
              d["prefetched"] = st.prefetched;
              d["refused"] = st.refused;
@@ -334,6 +334,10 @@ PYBIND11_MODULE(_ogkm, m) {
              d["use_ms"] = st.use_ns / 1e6;
              d["held"] = st.held;
              d["hold_drops"] = st.hold_drops;
+             d["quiet_passes"] = st.quiet_passes;
+             d["loud_streaming"] = st.loud_streaming;
+             d["loud_evictions"] = st.loud_evictions;
+             d["pressure_calls"] = st.pressure_calls;
              return d;
            })
       .def("reset_stats", &UnitStream::reset_stats);
