@@ -110,7 +110,8 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
     // anything enqueued on it now: no barrier packet (a lease of a unit whose
     // previous readers ran on the consumer's own stream - every resident unit
     // of a decode step).
-    if (f->event && f->stream == stream && stream) continue;
+    // (the null stream included: a GPU-side wait always names a real stream)
+    if (f->event && f->stream == stream) continue;
     // Already retired (the flag is only set by whoever polled last): no packet.
     if (f->ring && !f->event && f->ring->completed_seq() >= f->seq) {
       f->done.store(true, std::memory_order_release);

@@ -72,7 +72,7 @@ void UnitStream::prefetch_window() {
   }
 }
 
-Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
+Status UnitStream::use(uint32_t pos, void* stream, Lease** out, bool on_stream) {
   if (pos >= ranges_.size()) return Status::INVALID_ARGUMENT;
   std::lock_guard<std::recursive_mutex> g(m_);
   if (drop_requested_.exchange(false)) drop_holds(stream);
@@ -128,23 +128,24 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out) {
   const uint64_t t2 = now_ns();
   st_.hint_ns += t2 - t1;
   // the consumer's stream waits GPU-side (no stream: the host waits)
-  st = stream ? (*out)->ready.gpu_wait(rt_->be(), stream) : (*out)->ready.wait();
+  st = on_stream ? (*out)->ready.gpu_wait(rt_->be(), stream) : (*out)->ready.wait();
   st_.wait_ns += now_ns() - t2;
   if (st != Status::OK) {
-    (void)rt_->release(*out, stream);
+    (void)rt_->release(*out, on_stream ? stream : nullptr);
     *out = nullptr;
   }
   return st;
 }
 
-Status UnitStream::release(Lease* l, void* stream) {
+Status UnitStream::release(Lease* l, void* stream, bool on_stream) {
   std::lock_guard<std::recursive_mutex> g(m_);
-  if (!stream || l->proc == kCpuProc) return rt_->release(l, stream);
+  if (!on_stream || l->proc == kCpuProc) return rt_->release(l, nullptr);
   if (hold_ && l->offset == 0 && l->bytes == l->range->size) {
     auto it = pos_of_.find(l->range);
     if (it != pos_of_.end() && it->second < held_.size() && !held_[it->second]) {
       held_[it->second] = l;  // kept until its next use (or until pressure)
       hold_stream_ = stream;
+      hold_on_stream_ = true;
       return Status::OK;
     }
   }
@@ -217,7 +218,7 @@ void UnitStream::drop_holds(void* stream) {
   bool any = false;
   for (Lease* l : held_) any |= l != nullptr;
   if (!any) return;
-  FenceRef f = stream ? fence_record(rt_->be(), dev_, stream) : nullptr;
+  FenceRef f = hold_on_stream_ ? fence_record(rt_->be(), dev_, stream) : nullptr;
   for (Lease*& l : held_)
     if (l) {
       (void)rt_->release(l, stream, f);

@@ -48,9 +48,11 @@ class UnitStream {
   ~UnitStream();
   // Unit `pos` is used now on `stream`: returns its lease (device pointer =
   // lease->dptr) with the stream already ordered after its copies.
-  Status use(uint32_t pos, void* stream, Lease** out);
+  // on_stream: `stream` (nullptr = the null stream) waits GPU-side; false:
+  // the host waits (fake backend, tools).
+  Status use(uint32_t pos, void* stream, Lease** out, bool on_stream = true);
   // Its kernels are enqueued on `stream` (handed back in groups, see .cpp).
-  Status release(Lease* l, void* stream);
+  Status release(Lease* l, void* stream, bool on_stream = true);
   // Hand back every unit released so far (a step's end).
   Status flush_released(void* stream);
   // Keep the window full (the step's start: nothing used yet).
@@ -89,6 +91,7 @@ class UnitStream {
   ChunkArena* hold_arena_ = nullptr;
   uint64_t hold_ev_ = 0;
   void* hold_stream_ = nullptr;
+  bool hold_on_stream_ = false;
   int64_t cur_pos_ = -1;        // the unit of the latest use
   std::unordered_map<const Range*, uint32_t> pos_of_;  // unit -> its position
   std::recursive_mutex m_;      // use / release / the pressure handler (any thread)

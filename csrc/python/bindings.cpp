@@ -300,22 +300,23 @@ PYBIND11_MODULE(_ogkm, m) {
              return new UnitStream(rt(), dev, std::move(rs), window, next_use, max_ahead);
            }),
            py::arg("dev"), py::arg("ranges"), py::arg("window_bytes"), py::arg("next_use"), py::arg("max_ahead"))
-      .def("use", [](UnitStream& u, uint32_t pos, uint64_t stream) {
+      // on_stream: `stream` (0 = the null stream) waits GPU-side; False: the host waits
+      .def("use", [](UnitStream& u, uint32_t pos, uint64_t stream, bool on_stream) {
              Lease* l = nullptr;
              Status s;
              {
                py::gil_scoped_release nogil;
-               s = u.use(pos, (void*)stream, &l);
+               s = u.use(pos, (void*)stream, &l, on_stream);
              }
              check(s, "unit use");
              return py::make_tuple(l->id, l->dptr);
-           })
-      .def("release", [](UnitStream& u, uint64_t lid, uint64_t stream) {
+           }, py::arg("pos"), py::arg("stream"), py::arg("on_stream") = true)
+      .def("release", [](UnitStream& u, uint64_t lid, uint64_t stream, bool on_stream) {
              Lease* l = rt()->lease_by_id(lid);
              if (!l) throw StatusError("unknown lease");
              py::gil_scoped_release nogil;
-             check(u.release(l, (void*)stream), "unit release");
-           })
+             check(u.release(l, (void*)stream, on_stream), "unit release");
+           }, py::arg("lid"), py::arg("stream"), py::arg("on_stream") = true)
       .def("prefetch_window", [](UnitStream& u) {
              py::gil_scoped_release nogil;
              u.prefetch_window();

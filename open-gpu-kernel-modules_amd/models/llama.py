@@ -949,7 +949,7 @@ class TieredLlama:
                                       "cpu" if self.fake else "cuda", self.dev)
             sc[:, :, :, :self.ctx].copy_(pre)
         if isinstance(lease, tuple):  # native unit protocol: release + run-ahead bound in one call
-            self._us.release(lease[1], self._stream_handle())
+            self._us.release(lease[1], self._stream_handle(), not self.fake)
         elif lease is not None:  # the prefix's readers are enqueued: the unit may be evicted behind them
             lease.release(0 if self.fake else None)
             self._mark_consumed()
@@ -1128,10 +1128,10 @@ class TieredLlama:
             return None, (self._unstage(key, pin.ptr) if self.staged else pin)
         if self._native() and key in self._seq_pos:
             stream = self._stream_handle()
-            lid, dptr = self._us.use(self._seq_pos[key], stream)
+            lid, dptr = self._us.use(self._seq_pos[key], stream, not self.fake)
             if self.staged:
                 st = self._unstage(key, dptr)
-                self._us.release(lid, stream)
+                self._us.release(lid, stream, not self.fake)
                 return None, st
             return ("native", lid), self._ref(key, dptr, self.pmode.get(key, dgemm.MODE_RAW))
         acct = self.byte_trace is not None
@@ -1180,7 +1180,7 @@ class TieredLlama:
         if ptr is not None:
             return None, ptr
         if self._native() and key in self._seq_pos:
-            lid, dptr = self._us.use(self._seq_pos[key], self._stream_handle())
+            lid, dptr = self._us.use(self._seq_pos[key], self._stream_handle(), not self.fake)
             return ("native", lid), dptr
         if not self._is_resident(key):
             if self._inflight and self._inflight[0] == key:
@@ -1249,7 +1249,7 @@ class TieredLlama:
 
     def _done(self, lease) -> None:
         if isinstance(lease, tuple) and lease[0] == "native":  # release + run-ahead bound, natively
-            self._us.release(lease[1], self._stream_handle())
+            self._us.release(lease[1], self._stream_handle(), not self.fake)
         elif isinstance(lease, tuple):  # a gather slot read by the kernels just enqueued
             self.gather.done(lease[1])
             self._mark_consumed()
