@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Decode-attention microbenchmark (k_attn_decode_ws + combine): one layer's KV
 at the bench shapes, time per call and effective KV-read bandwidth.
-    python tools/bench_attn.py            (GRAPH=0: eager calls, SPLIT=64|256, COLD=0)"""
+    python tools/bench_attn.py            (GRAPH=0: eager calls, SPLIT=64|256, COLD=0, SHAPE=70b-tp8)"""
 import os
 import sys
 
@@ -24,7 +24,10 @@ def main() -> None:
     rt.init("hip")
     iters = int(os.environ.get("ITERS", "50"))
     graph = int(os.environ.get("GRAPH", "1"))  # 0: back-to-back eager calls (includes host launch cost)
+    only = os.environ.get("SHAPE")  # one shape (profiling runs)
     for name, (B, hq, hkv, hd, L) in SHAPES.items():
+        if only and name != only:
+            continue
         T = L
         q = torch.randn(B, hq, hd, device="cuda").to(torch.bfloat16)
         # MALL-cold: rotate over >= 1 GB of caches (a decode step reads every

@@ -10,9 +10,16 @@
 //     a stable VA from HBM to host), read by a kernel;
 //  3. ROCr hsa_amd_vmem_handle_create on the CPU agent's memory pools;
 //  4. /dev/udmabuf (memfd pages -> dma-buf -> ROCr import: the host arena's own
-//     pages at a device VA).
+//     pages at a device VA);
+//  5. is a hipMemCreate(Host) handle really host memory (device free-memory
+//     delta, a cold read bigger than the 256 MB MALL), and can ROCr map it:
+//     hsa_amd_vmem_retain_alloc_handle at a HIP mapping, then hsa_amd_vmem_map
+//     at a second VA (the runtime's stable VAs are ROCr-mapped), kernel
+//     read / write through it and the CPU view of the same pages.
 //   hipcc --offload-arch=gfx950 -O2 tools/probe_vmm_host.hip -lhsa-runtime64 -o build/probe_vmm_host
 #include <fcntl.h>
+#include <setjmp.h>
+#include <signal.h>
 #include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -201,11 +208,109 @@ static void probe_udmabuf() {
   if (fd >= 0) close(fd);
 }
 
+static sigjmp_buf g_jb;
+static void on_segv(int) { siglongjmp(g_jb, 1); }
+// a CPU load that may fault (the VA may have no CPU mapping): -1 then
+static int cpu_load(volatile int* p) {
+  struct sigaction sa = {}, old = {};
+  sa.sa_handler = on_segv;
+  sigaction(SIGSEGV, &sa, &old);
+  int v = -1;
+  if (!sigsetjmp(g_jb, 1)) v = *p;
+  else std::printf("  (CPU load faulted)\n");
+  sigaction(SIGSEGV, &old, nullptr);
+  return v;
+}
+
+static hsa_agent_t g_gpu{0};
+static hsa_status_t gpu_cb(hsa_agent_t a, void*) {
+  hsa_device_type_t t;
+  hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+  if (t == HSA_DEVICE_TYPE_GPU && !g_gpu.handle) g_gpu = a;
+  return HSA_STATUS_SUCCESS;
+}
+
+static void probe_rocr_host_map() {
+  std::printf("[5] hipMemCreate(Host): where it lives, and ROCr mapping of it\n");
+  hsa_iterate_agents(gpu_cb, nullptr);
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeHost;
+  prop.location.id = 0;
+  const size_t sz = 512 * kSz;  // 1 GB: past the MALL
+  size_t f0 = 0, f1 = 0, tot = 0;
+  (void)hipMemGetInfo(&f0, &tot);
+  hipMemGenericAllocationHandle_t h;
+  hipError_t e = hipMemCreate(&h, sz, &prop, 0);
+  (void)hipMemGetInfo(&f1, &tot);
+  std::printf("  hipMemCreate(1 GB host) -> %s; device free %.0f -> %.0f MB\n", hs(e), f0 / 1e6, f1 / 1e6);
+  if (e != hipSuccess) return;
+  void* va = nullptr;
+  if (hipMemAddressReserve(&va, sz, kSz, nullptr, 0) != hipSuccess || !map_access(va, sz, h, true, "host 1 GB")) return;
+  hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, (int*)va, 5, sz / 4);
+  e = hipDeviceSynchronize();
+  std::printf("  kernel fill 1 GB -> %s\n", hs(e));
+  // CPU view of the same pages (host access was granted at the HIP VA)
+  volatile int* cp = (volatile int*)va;
+  std::printf("  CPU load through the VA: %d (want 5)\n", cpu_load(cp + 777));
+  unsigned long long* d_out;
+  (void)hipMalloc(&d_out, 8);
+  for (int it = 0; it < 3; ++it) {
+    (void)hipMemset(d_out, 0, 8);
+    (void)hipDeviceSynchronize();
+    const double t0 = now_us();
+    hipLaunchKernelGGL(k_sum, dim3(2048), dim3(256), 0, 0, (const int4*)va, sz / 16, d_out);
+    e = hipDeviceSynchronize();
+    const double t1 = now_us();
+    unsigned long long s = 0;
+    (void)hipMemcpy(&s, d_out, 8, hipMemcpyDeviceToHost);
+    std::printf("  cold-ish read of 1 GB #%d -> %s, sum ok %d, %.1f GB/s\n", it, hs(e), (int)(s == 5ull * (sz / 4)),
+                sz / (t1 - t0) / 1e3);
+  }
+  // ROCr: retain the handle at the HIP mapping, map it at a second VA
+  hsa_amd_vmem_alloc_handle_t rh{0};
+  hsa_status_t st = hsa_amd_vmem_retain_alloc_handle(&rh, va);
+  std::printf("  hsa_amd_vmem_retain_alloc_handle -> %d\n", (int)st);
+  if (st == HSA_STATUS_SUCCESS && g_gpu.handle) {
+    void* va2 = nullptr;
+    st = hsa_amd_vmem_address_reserve(&va2, kSz, 0, 0);
+    std::printf("  hsa_amd_vmem_address_reserve -> %d\n", (int)st);
+    if (st == HSA_STATUS_SUCCESS) {
+      st = hsa_amd_vmem_map(va2, kSz, 0, rh, 0);
+      std::printf("  hsa_amd_vmem_map(first 2 MB of the host handle) -> %d\n", (int)st);
+      if (st == HSA_STATUS_SUCCESS) {
+        hsa_amd_memory_access_desc_t d{HSA_ACCESS_PERMISSION_RW, g_gpu};
+        st = hsa_amd_vmem_set_access(va2, kSz, &d, 1);
+        std::printf("  hsa_amd_vmem_set_access(gpu) -> %d\n", (int)st);
+        if (st == HSA_STATUS_SUCCESS) {
+          (void)hipMemset(d_out, 0, 8);
+          hipLaunchKernelGGL(k_sum, dim3(64), dim3(256), 0, 0, (const int4*)va2, kSz / 16, d_out);
+          e = hipDeviceSynchronize();
+          unsigned long long s = 0;
+          (void)hipMemcpy(&s, d_out, 8, hipMemcpyDeviceToHost);
+          std::printf("  kernel read through the ROCr mapping -> %s, sum ok %d\n", hs(e), (int)(s == 5ull * (kSz / 4)));
+          hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, 0, (int*)va2, 11, kSz / 4);
+          e = hipDeviceSynchronize();
+          std::printf("  kernel write through the ROCr mapping -> %s; CPU sees %d (want 11)\n", hs(e), cpu_load(cp + 4099));
+        }
+        (void)hsa_amd_vmem_unmap(va2, kSz);
+      }
+      (void)hsa_amd_vmem_address_free(va2, kSz);
+    }
+    (void)hsa_amd_vmem_handle_release(rh);
+  }
+  (void)hipFree(d_out);
+  (void)hipMemUnmap(va, sz);
+  (void)hipMemAddressFree(va, sz);
+  (void)hipMemRelease(h);
+}
+
 int main() {
   (void)hipFree(nullptr);
   probe_host_handles();
   probe_rocr();
   probe_udmabuf();
+  probe_rocr_host_map();
   std::printf("done\n");
   return 0;
 }
