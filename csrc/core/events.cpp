@@ -161,7 +161,8 @@ const char* counter_name(Counter c) {
                             "pack_expansions",
                             "packed_decodes",
                             "pressure_reliefs",
-                            "decode_reuse_waits"};
+                            "decode_reuse_waits",
+                            "ring_merged_batches"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

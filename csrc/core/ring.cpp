@@ -247,6 +247,26 @@ void Ring::worker() {
       b = std::move(work_.front());
       work_.pop_front();
       queued_.fetch_sub(1, std::memory_order_relaxed);
+      // Batches of packed-block decodes queued behind this one run as ONE batch
+      // (up to ring_merge_packed_mb of packed bytes): their staging copies and
+      // decodes then fill the staging halves instead of one launch per batch
+      // (the transparent 70B step: ~5 blocks per launch, a latency-bound
+      // decode each). Batches that wait on fences are never merged: a wait
+      // behind this batch's own tracking value would never end.
+      if (const uint64_t cap = (uint64_t)std::max<int64_t>(0, config().ring_merge_packed_mb) << 20) {
+        uint64_t packed = packed_bytes(b);
+        while (packed && packed < cap && !work_.empty()) {
+          const uint64_t np = packed_bytes(work_.front());
+          if (!np) break;
+          Batch& n = work_.front();
+          b.ops.insert(b.ops.end(), std::make_move_iterator(n.ops.begin()), std::make_move_iterator(n.ops.end()));
+          b.last = n.last;
+          packed += np;
+          work_.pop_front();
+          queued_.fetch_sub(1, std::memory_order_relaxed);
+          Tools::get().inc(Counter::RingMergedBatches);
+        }
+      }
     }
     if (err_ == Status::OK && config().ring_pipeline && pure_copies(b, &copies)) {
       const int slot = pend == 0 ? 1 : 0;
@@ -296,6 +316,17 @@ void Ring::worker() {
     publish_deferred(true);
     publish(b.last);
   }
+}
+
+// Packed bytes a batch stages for DECODE_ANS; 0 for a batch with none or with a
+// fence wait (never merged, Ring::worker).
+uint64_t Ring::packed_bytes(const Batch& b) {
+  uint64_t n = 0;
+  for (const Sqe& s : b.ops) {
+    if (s.op == SqeOp::WAIT_FENCE) return 0;
+    if (s.op == SqeOp::DECODE_ANS) n += s.bytes;
+  }
+  return n;
 }
 
 std::vector<CopyDesc> split_over_engines(const std::vector<CopyDesc>& in, uint32_t mask, uint64_t min_piece,
@@ -358,7 +389,46 @@ Status Ring::run_batch(Batch& b) {
     }
     decodes.clear();
   };
-  auto flush_copies = [&] {
+  // A staging half whose copies are on the engines and whose decode is not
+  // launched yet: the next half's copies are issued BEFORE the host waits for
+  // these (the engines never idle while the host launches a decode), then its
+  // decode goes out (complete_stage).
+  struct PendStage {
+    bool on = false;
+    int slot = 0, half = 0;
+    std::vector<DecodeDesc> staged;
+  } ps;
+  auto launch_decodes = [&](std::vector<DecodeDesc>& dec, int half) {
+    st = be_->decode_ans_blocks(dev_, dec.data(), dec.size(), stream_);
+    Tools::get().inc(Counter::PackedDecodes, dec.size());
+    for (const DecodeDesc& d : dec) batch_dst_.emplace_back(d.dst, 2ull * d.n_values);
+    if (st != Status::OK) return;
+    if (!stage_ev_[half]) stage_ev_[half] = be_->event_create(dev_);
+    if (!config().ring_defer_decodes) {
+      kernels_pending = true;  // drained before the next copies, as any kernel
+    } else if (stage_ev_[half] && be_->event_record(stage_ev_[half], stream_) == Status::OK) {
+      stage_used_[half] = true;
+      decodes_deferred = true;
+    } else {
+      kernels_pending = true;  // no event: drain as for any kernel
+    }
+  };
+  auto complete_stage = [&] {
+    if (!ps.on) return;
+    ps.on = false;
+    if (st == Status::OK) {
+      set_phase(Phase::ENGINE_WAIT, b.last);
+      const uint64_t t0 = now_ns();
+      st = be_->dma_complete(ps.slot);
+      if (kind_ == RingKind::CPU_TO_GPU) Tools::get().inc(Counter::RingCopyNs, now_ns() - t0);
+      set_phase(Phase::ISSUE, b.last);
+    }
+    if (st == Status::OK) launch_decodes(ps.staged, ps.half);
+    ps.staged.clear();
+  };
+  // Engine copies: issued on `slot`; waited for unless `async` (a staging
+  // half's copies: complete_stage waits).
+  auto issue_copies = [&](int slot, bool async) {
     if (!copies.empty()) {
       drain();
       if (kind_ == RingKind::GPU_TO_GPU) {
@@ -405,12 +475,14 @@ Status Ring::run_batch(Batch& b) {
         snprintf(phase_what_, sizeof(phase_what_), "engine copy: %zu descriptors, first %llu B", copies.size(),
                  (unsigned long long)copies[0].bytes);
         set_phase(Phase::ENGINE_ISSUE, b.last);
-        st = be_->dma_issue(dev_, copies.data(), copies.size(), (int)kind_, 0);
+        st = be_->dma_issue(dev_, copies.data(), copies.size(), (int)kind_, slot);
         // the batch's last copies are on the engines: GPU waits may be enqueued
         if (final_flush && st == Status::OK) mark_issued(b.last);
-        set_phase(Phase::ENGINE_WAIT, b.last);
-        if (st == Status::OK) st = be_->dma_complete(0);
-        set_phase(Phase::ISSUE, b.last);
+        if (!async) {
+          set_phase(Phase::ENGINE_WAIT, b.last);
+          if (st == Status::OK) st = be_->dma_complete(slot);
+          set_phase(Phase::ISSUE, b.last);
+        }
         if (kind_ == RingKind::CPU_TO_GPU) {
           Tools::get().inc(Counter::RingCopyNs, now_ns() - t_copy);
           Tools::get().inc(Counter::RingCopyCalls, copies.size());
@@ -419,6 +491,10 @@ Status Ring::run_batch(Batch& b) {
     }
     copies.clear();
     copy_dst.clear();
+  };
+  auto flush_copies = [&] {
+    complete_stage();  // a pending half's decode goes out first (order, chunk-reuse checks)
+    issue_copies(0, false);
   };
   // Packed blocks: their staging copies go out with the batch's other engine
   // copies; once those landed ONE k_ans_blocks launch decodes them all - and
@@ -430,22 +506,30 @@ Status Ring::run_batch(Batch& b) {
   bool half_ready = false;  // the current staging half's previous decode is done
   auto flush_staged = [&] {
     if (staged.empty()) return;
-    flush_copies();
-    if (st == Status::OK) {
-      st = be_->decode_ans_blocks(dev_, staged.data(), staged.size(), stream_);
-      Tools::get().inc(Counter::PackedDecodes, staged.size());
-      for (const DecodeDesc& d : staged) batch_dst_.emplace_back(d.dst, 2ull * d.n_values);
-      if (st == Status::OK) {
-        if (!stage_ev_[stage_half_]) stage_ev_[stage_half_] = be_->event_create(dev_);
-        if (!config().ring_defer_decodes) {
-          kernels_pending = true;  // drained before the next copies, as any kernel
-        } else if (stage_ev_[stage_half_] && be_->event_record(stage_ev_[stage_half_], stream_) == Status::OK) {
-          stage_used_[stage_half_] = true;
-          decodes_deferred = true;
-        } else {
-          kernels_pending = true;  // no event: drain as for any kernel
-        }
+    if (config().ring_stage_overlap) {
+      // this half's copies go out now; the previous half's (if any) are waited
+      // for and its decode launched while these run
+      // (other copies flushed with these that write a chunk the pending half
+      // decodes into - handed out again within this batch - wait for it)
+      if (ps.on) {
+        bool hit = false;
+        for (const CopyDesc& c : copies)
+          for (const DecodeDesc& d : ps.staged)
+            hit |= c.dst < d.dst + 2ull * d.n_values && d.dst < c.dst + c.bytes;
+        if (hit) complete_stage();
       }
+      const int slot = ps.on ? (ps.slot ^ 1) : 0;
+      issue_copies(slot, true);
+      complete_stage();
+      if (st == Status::OK) {
+        ps.on = true;
+        ps.slot = slot;
+        ps.half = stage_half_;
+        ps.staged.swap(staged);
+      }
+    } else {
+      flush_copies();
+      if (st == Status::OK) launch_decodes(staged, stage_half_);
     }
     staged.clear();
     stage_off = 0;
@@ -567,6 +651,7 @@ Status Ring::run_batch(Batch& b) {
   }
   flush_decodes();
   flush_staged();
+  complete_stage();
   if (!kernels_pending) final_flush = true;  // (with kernels queued, the drain below comes first)
   flush_copies();
   drain();

@@ -205,6 +205,7 @@ enum class Counter : int {
   PackedDecodes,       // packed blocks decoded into HBM by the H2D ring (DECODE_ANS)
   PressureReliefs,     // reservations that found nothing evictable until soft pins let go
   DecodeReuseWaits,    // H2D copies that waited for a running packed-block decode into the same chunk
+  RingMergedBatches,   // packed-decode batches the H2D ring ran merged into the batch before (Ring::worker)
   NumCounters
 };
 const char* counter_name(Counter c);

@@ -142,6 +142,7 @@ class Ring {
   FenceRef submit_dma_locked();
   void worker();
   bool pure_copies(const Batch& b, std::vector<CopyDesc>* out) const;
+  static uint64_t packed_bytes(const Batch& b);
   Status run_batch(Batch& b);
   void publish(uint64_t seq);
   Backend* be_;

@@ -621,8 +621,8 @@ __global__ void k_attn_combine(AttnArgs a) {
 // Guideline 16, counter form): partials stored write-through (sc1), every wave
 // drains its stores, a workgroup barrier, one relaxed agent-scope ticket add;
 // the last arriver acquires (agent) before reading them and resets the ticket.
-template <int HD, int G, int DPL, int NSLOT>
-__global__ void __launch_bounds__(1024) k_attn_decode_fl(AttnArgs a) {
+template <int HD, int G, int DPL, int NSLOT, bool FUSE>
+__global__ void __launch_bounds__(1024, 8) k_attn_decode_fl(AttnArgs a) {
   constexpr int NW = 16, KS = HD / 32;
   static_assert((HD == 64 || HD == 128) && G <= 16 && (DPL == 2 || DPL == 4 || DPL == 8) && NW % NSLOT == 0, "shape");
   extern __shared__ float smem[];
@@ -648,32 +648,39 @@ __global__ void __launch_bounds__(1024) k_attn_decode_fl(AttnArgs a) {
     for (int j = 0; j < DPL; ++j) o[h][j] = 0.f;
   uint32_t vv[NI][DPL / 2];
   if (wn > 0) {
-    // K tile (16 tokens x HD) and V tile (16 tokens x HD) requested together
+    // K tile (16 tokens x HD) and V tile (16 tokens x HD) requested together,
+    // through buffer descriptors bounded at the context length: rows past it
+    // read as zeros (no clamping; their scores are masked, their p is 0), one
+    // 32-bit offset per tile and immediate offsets for the rest
+    const uint32_t ctx_bytes = a.len * HD * 2u;
+    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, (int)ctx_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, (int)ctx_bytes, 0x00020000);
     uint4 ka[KS];
     {
-      const uint32_t row = wt0 + ((int32_t)col < wn ? col : (uint32_t)wn - 1);
-      const uint16_t* kr = kbase + (uint64_t)row * HD + 8 * quad;
+      const int koff = (int)(((wt0 + col) * HD + 8 * quad) * 2u);
 #pragma unroll
-      for (int k = 0; k < KS; ++k) ka[k] = *reinterpret_cast<const uint4*>(kr + 32 * k);
+      for (int k = 0; k < KS; ++k) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(krs, koff + 64 * k, 0, 0);
+        ka[k] = uint4{w[0], w[1], w[2], w[3]};
+      }
     }
     {
-      const uint16_t* vcol = vbase + (uint64_t)wt0 * HD + dg * DPL;
+      const int voff = (int)(((wt0 + tg) * HD + dg * DPL) * 2u);
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
-        const int32_t t = i * TPI + (int32_t)tg;
-        const int32_t tt = t < wn ? t : wn - 1;  // past the context: clamped, its p is 0
+        const int off = voff + i * TPI * HD * 2;
         if constexpr (DPL == 8) {
-          const uint4 w = *reinterpret_cast<const uint4*>(vcol + (uint64_t)tt * HD);
-          vv[i][0] = w.x;
-          vv[i][1] = w.y;
-          vv[i][2] = w.z;
-          vv[i][3] = w.w;
+          const auto w = __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0);
+          vv[i][0] = w[0];
+          vv[i][1] = w[1];
+          vv[i][2] = w[2];
+          vv[i][3] = w[3];
         } else if constexpr (DPL == 4) {
-          const uint2 w = *reinterpret_cast<const uint2*>(vcol + (uint64_t)tt * HD);
-          vv[i][0] = w.x;
-          vv[i][1] = w.y;
+          const auto w = __builtin_amdgcn_raw_buffer_load_b64(vrs, off, 0, 0);
+          vv[i][0] = w[0];
+          vv[i][1] = w[1];
         } else {
-          vv[i][0] = *reinterpret_cast<const uint32_t*>(vcol + (uint64_t)tt * HD);
+          vv[i][0] = __builtin_amdgcn_raw_buffer_load_b32(vrs, off, 0, 0);
         }
       }
     }
@@ -788,13 +795,21 @@ __global__ void __launch_bounds__(1024) k_attn_decode_fl(AttnArgs a) {
       continue;
     }
     const uint64_t row = row0 + (uint64_t)h * a.nsplit + split;
+    if constexpr (!FUSE) {  // plain partials for the combine launch
+      a.part_o[row * HD + d] = acc;
+      if (d == 0) {
+        a.part_ml[row * 2] = M;
+        a.part_ml[row * 2 + 1] = l;
+      }
+      continue;
+    }
     __hip_atomic_store(&a.part_o[row * HD + d], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (d == 0) {
       __hip_atomic_store(&a.part_ml[row * 2], M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.part_ml[row * 2 + 1], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (a.nsplit == 1) return;
+  if (!FUSE || a.nsplit == 1) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through stores have landed
   __syncthreads();
   uint32_t* ticket = a.tickets + (uint64_t)b * a.hkv + kvh;
@@ -875,12 +890,22 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
                   (force_fl == 1 || (force_fl < 0 && (uint64_t)a.nsplit * a.hkv * a.B < 1024));
   if (fl) {
     const size_t fl_lds = (size_t)(16 * gg * 16 + (gg == 4 ? 16 : gg == 8 ? 8 : 4) * g * a.hd) * sizeof(float);
-#define OGKM_ATTN_FL_G(HD)                                                                                     \
-  if (gg == 4) hipLaunchKernelGGL((k_attn_decode_fl<HD, 4, 8, 16>), grid, dim3(1024), fl_lds, s, a);           \
-  else if (gg == 8) hipLaunchKernelGGL((k_attn_decode_fl<HD, 8, 4, 8>), grid, dim3(1024), fl_lds, s, a);       \
-  else hipLaunchKernelGGL((k_attn_decode_fl<HD, 16, 2, 4>), grid, dim3(1024), fl_lds, s, a)
+    // OGKM_ATTN_FL_FUSE=0: the combine as its own launch (A/B drills)
+    static const bool fuse = !getenv("OGKM_ATTN_FL_FUSE") || atoi(getenv("OGKM_ATTN_FL_FUSE")) != 0;
+#define OGKM_ATTN_FL_K(HD, G, D, NS)                                                                       \
+  do {                                                                                                     \
+    if (fuse) hipLaunchKernelGGL((k_attn_decode_fl<HD, G, D, NS, true>), grid, dim3(1024), fl_lds, s, a);  \
+    else hipLaunchKernelGGL((k_attn_decode_fl<HD, G, D, NS, false>), grid, dim3(1024), fl_lds, s, a);      \
+  } while (0)
+#define OGKM_ATTN_FL_G(HD)                          \
+  if (gg == 4) OGKM_ATTN_FL_K(HD, 4, 8, 16);        \
+  else if (gg == 8) OGKM_ATTN_FL_K(HD, 8, 2, 8);    \
+  else OGKM_ATTN_FL_K(HD, 16, 2, 4)
     if (a.hd == 128) { OGKM_ATTN_FL_G(128); } else { OGKM_ATTN_FL_G(64); }
 #undef OGKM_ATTN_FL_G
+#undef OGKM_ATTN_FL_K
+    if (!fuse && a.nsplit > 1)
+      hipLaunchKernelGGL(k_attn_combine, dim3(a.B * a.hq), dim3(a.hd < 64 ? 64 : a.hd), 0, s, a);
     return hipGetLastError();
   }
   if (ws) {

@@ -256,3 +256,30 @@ def test_slow_decodes_never_race_chunk_reuse(fake_rt):
     assert lib.stats()["packed_decodes"] > 0
     for b in bufs:
         b.free()
+
+
+def test_queued_packed_batches_run_merged(fake_rt):
+    """Refills of packed blocks queued behind a running batch run as ONE ring
+    batch (ring_merge_packed_mb): fewer, fuller staging flushes; every buffer
+    still reads back exactly and every tracking value is published."""
+    rt.configure(pack_host_copies=1, pack_threads=2, fake_kernel_delay_us=2000, ring_merge_packed_mb=24)
+    bufs, datas = [], []
+    for i in range(8):
+        b = rt.malloc_managed(4 * MB, f"m{i}")
+        d = _weights(b.size, 40 + i)
+        b.write(d)
+        bufs.append(b)
+        datas.append(d)
+    for b in bufs:
+        _pack(b)
+    assert sum(len(_packed_entries(b)) for b in bufs) == 16
+    s0 = lib.stats()
+    for b in bufs:  # eight batches submitted back to back: the later ones queue
+        b.prefetch("gpu:0")
+    for b, d in zip(bufs, datas):
+        assert _gpu_read(b).equal(d)
+    s1 = lib.stats()
+    assert s1["packed_decodes"] - s0["packed_decodes"] == 16
+    assert s1["ring_merged_batches"] > s0["ring_merged_batches"]
+    for b in bufs:
+        b.free()

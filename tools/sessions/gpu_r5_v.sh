@@ -6,8 +6,9 @@ ulimit -c 0
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r5
 for fl in -1 1 0; do
-  OGKM_ATTN_FL=$fl timeout -k 10 300 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread tests/test_fused.py -k "attention" > gpurun_out/r5/v_attn_tests_$fl.log 2>&1 || { echo ATTN_TESTS_FAIL $fl; tail -30 gpurun_out/r5/v_attn_tests_$fl.log; exit 1; }
+  OGKM_ATTN_FL=$fl timeout -k 10 300 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread tests/test_fused.py -k "attention and not kv_rate" > gpurun_out/r5/v_attn_tests_$fl.log 2>&1 || { echo ATTN_TESTS_FAIL $fl; tail -30 gpurun_out/r5/v_attn_tests_$fl.log; exit 1; }
   echo "fl $fl tests: $(tail -1 gpurun_out/r5/v_attn_tests_$fl.log)"
+  OGKM_ATTN_FL=$fl timeout -k 10 120 python -u -m pytest -q -s --timeout 100 --timeout-method thread tests/test_fused.py -k "kv_rate" > gpurun_out/r5/v_rate_$fl.log 2>&1; echo "fl $fl rate rc=$?"; grep "TB/s of KV" gpurun_out/r5/v_rate_$fl.log
   OGKM_ATTN_FL=$fl timeout -k 10 180 python -u tools/bench_attn.py > gpurun_out/r5/v_attn_$fl.txt 2>&1 || { echo ATTN_FAIL $fl; tail -20 gpurun_out/r5/v_attn_$fl.txt; exit 1; }
   grep -v amdgpu.ids gpurun_out/r5/v_attn_$fl.txt | sed "s/^/fl $fl /"
 done
