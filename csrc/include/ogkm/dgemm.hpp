@@ -132,7 +132,6 @@ struct AttnArgs {
   uint32_t B, hq, hkv, hd, T, len, nsplit;
   float scale;
   uint32_t out_frag;       // 1: out is fragment-ordered [B16][hq * hd]
-  uint32_t* tickets;       // [B * hkv] zeroed arrival tickets (the fused-combine kernel; null: never used)
   uint32_t split_tokens;   // context tokens per workgroup: 256 (4 waves, default) or 64 (1 wave; hd 64 / 128 -
                            // measured slower at every bench shape, kept as an explicit option)
 };

@@ -606,240 +606,6 @@ __global__ void k_attn_combine(AttnArgs a) {
   }
 }
 
-// Latency-shaped decode attention with the split combine in the same launch,
-// for grids that do not fill the chip (one KV head per batch row - the tp8
-// shard shape: 64 rows x 5 splits = 320 workgroups on 256 CUs). There the
-// four-wave kernel is a chain of dependent memory round trips per wave (two K
-// rounds, four V rounds) at ~5 waves per CU, plus a separate combine launch
-// (rocprof, 70B-tp8 shape: 15.5 + 4.8 us). Here a workgroup is 16 waves x 16
-// tokens (the same 256-token split): every wave issues its whole K tile and
-// its whole V tile before the first wait, so a CU has its split's 128 KB in
-// flight at once. The 16 wave partials are merged in LDS in a fixed order
-// (rescaled to the workgroup max first; NSLOT slots, one round per 16 / NSLOT
-// waves: deterministic, <= 48 KB of LDS), and the workgroup that finishes a
-// (row, KV head) last merges the splits. Hand-off (cdna_hip_programming.md
-// Guideline 16, counter form): partials stored write-through (sc1), every wave
-// drains its stores, a workgroup barrier, one relaxed agent-scope ticket add;
-// the last arriver acquires (agent) before reading them and resets the ticket.
-template <int HD, int G, int DPL, int NSLOT, bool FUSE>
-__global__ void __launch_bounds__(1024, 8) k_attn_decode_fl(AttnArgs a) {
-  constexpr int NW = 16, KS = HD / 32;
-  static_assert((HD == 64 || HD == 128) && G <= 16 && (DPL == 2 || DPL == 4 || DPL == 8) && NW % NSLOT == 0, "shape");
-  extern __shared__ float smem[];
-  const uint32_t g = a.hq / a.hkv;
-  float* ps = smem;                   // [NW][16 tokens][G] probabilities
-  float* po = smem + NW * G * 16;     // [NSLOT][g][HD] rescaled output sums
-  __shared__ float wm[NW][G], wl[NW][G];
-  __shared__ uint32_t last;
-  const uint32_t split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t wt0 = split * (16u * NW) + wave * 16;
-  const int32_t wn = (int32_t)a.len - (int32_t)wt0 < 16 ? (int32_t)a.len - (int32_t)wt0 : 16;
-  float* wps = ps + wave * G * 16;
-  const uint16_t* kbase = a.cache + ((uint64_t)b * a.hkv + kvh) * (uint64_t)a.T * HD;
-  const uint16_t* vbase = a.cache + (((uint64_t)a.B + b) * a.hkv + kvh) * (uint64_t)a.T * HD;
-  const uint32_t col = lane & 15, quad = lane >> 4;
-  constexpr int LPT = HD / DPL, TPI = 64 / LPT, NI = 16 / TPI;
-  const uint32_t tg = lane / LPT, dg = lane % LPT;
-  float o[G][DPL];
-#pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int j = 0; j < DPL; ++j) o[h][j] = 0.f;
-  uint32_t vv[NI][DPL / 2];
-  if (wn > 0) {
-    // K tile (16 tokens x HD) and V tile (16 tokens x HD) requested together,
-    // through buffer descriptors bounded at the context length: rows past it
-    // read as zeros (no clamping; their scores are masked, their p is 0), one
-    // 32-bit offset per tile and immediate offsets for the rest
-    const uint32_t ctx_bytes = a.len * HD * 2u;
-    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, (int)ctx_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, (int)ctx_bytes, 0x00020000);
-    uint4 ka[KS];
-    {
-      const int koff = (int)(((wt0 + col) * HD + 8 * quad) * 2u);
-#pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        const auto w = __builtin_amdgcn_raw_buffer_load_b128(krs, koff + 64 * k, 0, 0);
-        ka[k] = uint4{w[0], w[1], w[2], w[3]};
-      }
-    }
-    {
-      const int voff = (int)(((wt0 + tg) * HD + dg * DPL) * 2u);
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int off = voff + i * TPI * HD * 2;
-        if constexpr (DPL == 8) {
-          const auto w = __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0);
-          vv[i][0] = w[0];
-          vv[i][1] = w[1];
-          vv[i][2] = w[2];
-          vv[i][3] = w[3];
-        } else if constexpr (DPL == 4) {
-          const auto w = __builtin_amdgcn_raw_buffer_load_b64(vrs, off, 0, 0);
-          vv[i][0] = w[0];
-          vv[i][1] = w[1];
-        } else {
-          vv[i][0] = __builtin_amdgcn_raw_buffer_load_b32(vrs, off, 0, 0);
-        }
-      }
-    }
-    uint4 qb[KS];
-    const uint16_t* qr = a.q + ((uint64_t)b * a.hq + kvh * g + (col < g ? col : 0)) * HD + 8 * quad;
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      qb[k] = *reinterpret_cast<const uint4*>(qr + 32 * k);
-      if (col >= g) qb[k] = uint4{0u, 0u, 0u, 0u};
-    }
-    attn_f32x4_t sc = attn_f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < KS; ++k)
-      sc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(attn_bf16x8_t, ka[k]),
-                                                   __builtin_bit_cast(attn_bf16x8_t, qb[k]), sc, 0, 0, 0);
-    // softmax partials: lane = head col, tokens 4 * quad + r
-    float m = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int32_t tok = 4 * (int32_t)quad + r;
-      const float v = tok < wn ? sc[r] * a.scale : -INFINITY;
-      sc[r] = v;
-      m = fmaxf(m, v);
-    }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    float l = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = __expf(sc[r] - m);
-      l += p;
-      if (col < G) wps[(4 * quad + r) * G + col] = col < g ? p : 0.f;
-    }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    if (quad == 0 && col < G) {
-      wm[wave][col] = col < g ? m : -INFINITY;
-      wl[wave][col] = col < g ? l : 0.f;
-    }
-  } else if (lane < G) {  // this wave's tokens are past the context: an empty partial
-    wm[wave][lane] = -INFINITY;
-    wl[wave][lane] = 0.f;
-  }
-  __syncthreads();
-  // this wave's rescale factor to the workgroup max: head h's in lane h
-  float fl = 0.f;
-  if (lane < G) {
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w][lane]);
-    fl = wm[wave][lane] == -INFINITY ? 0.f : __expf(wm[wave][lane] - M);
-  }
-  if (wn > 0) {
-    // P.V: lane owns DPL dims of every TPI-th token; token groups reduced by shuffles
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int32_t t = i * TPI + (int32_t)tg;
-      float vf[DPL];
-#pragma unroll
-      for (int j = 0; j < DPL / 2; ++j) {
-        vf[2 * j] = dbf((uint16_t)vv[i][j]);
-        vf[2 * j + 1] = dbf((uint16_t)(vv[i][j] >> 16));
-      }
-      const float* pt = wps + t * G;
-#pragma unroll
-      for (int h = 0; h < G; ++h) {
-        const float p = pt[h];
-#pragma unroll
-        for (int j = 0; j < DPL; ++j) o[h][j] += p * vf[j];
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      const float fh = __shfl(fl, h, 64);
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) {
-        float x = o[h][j];
-#pragma unroll
-        for (int sh = LPT; sh < 64; sh <<= 1) x += __shfl_xor(x, sh, 64);
-        o[h][j] = x * fh;
-      }
-    }
-  }
-  // fixed-order merge: round r adds waves r * NSLOT .. r * NSLOT + NSLOT - 1 into the slots
-  const uint32_t slot = wave % NSLOT;
-#pragma unroll 1
-  for (uint32_t r = 0; r < NW / NSLOT; ++r) {
-    if (wave / NSLOT == r && tg == 0) {
-      float* sp = po + slot * g * HD + dg * DPL;
-#pragma unroll
-      for (int h = 0; h < G; ++h)
-        if ((uint32_t)h < g)
-#pragma unroll
-          for (int j = 0; j < DPL; ++j) sp[h * HD + j] = r ? sp[h * HD + j] + o[h][j] : o[h][j];
-    }
-    __syncthreads();
-  }
-  const uint64_t row0 = ((uint64_t)b * a.hq + kvh * g) * a.nsplit;
-  for (uint32_t e = threadIdx.x; e < g * HD; e += 64 * NW) {
-    const uint32_t h = e / HD, d = e - h * HD;
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w][h]);
-    float acc = 0.f, l = 0.f;
-#pragma unroll
-    for (int s2 = 0; s2 < NSLOT; ++s2) acc += po[(s2 * g + h) * HD + d];
-#pragma unroll
-    for (int w = 0; w < NW; ++w) l += wm[w][h] == -INFINITY ? 0.f : __expf(wm[w][h] - M) * wl[w][h];
-    if (a.nsplit == 1) {
-      const uint32_t cc = (kvh * g + h) * HD + d;
-      a.out[a.out_frag ? frag_index(b, cc, a.hq * a.hd) : ((uint64_t)b * a.hq + kvh * g + h) * HD + d] = df2bf(acc / l);
-      continue;
-    }
-    const uint64_t row = row0 + (uint64_t)h * a.nsplit + split;
-    if constexpr (!FUSE) {  // plain partials for the combine launch
-      a.part_o[row * HD + d] = acc;
-      if (d == 0) {
-        a.part_ml[row * 2] = M;
-        a.part_ml[row * 2 + 1] = l;
-      }
-      continue;
-    }
-    __hip_atomic_store(&a.part_o[row * HD + d], acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == 0) {
-      __hip_atomic_store(&a.part_ml[row * 2], M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.part_ml[row * 2 + 1], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (!FUSE || a.nsplit == 1) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through stores have landed
-  __syncthreads();
-  uint32_t* ticket = a.tickets + (uint64_t)b * a.hkv + kvh;
-  if (threadIdx.x == 0) {
-    const uint32_t n = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = n + 1 == a.nsplit;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  for (uint32_t e = threadIdx.x; e < g * HD; e += 64 * NW) {
-    const uint32_t h = e / HD, d = e - h * HD;
-    const uint64_t rb = row0 + (uint64_t)h * a.nsplit;
-    float M = -INFINITY;
-    for (uint32_t s2 = 0; s2 < a.nsplit; ++s2) M = fmaxf(M, a.part_ml[(rb + s2) * 2]);
-    float num = 0.f, den = 0.f;
-    for (uint32_t s2 = 0; s2 < a.nsplit; ++s2) {
-      const float w = __expf(a.part_ml[(rb + s2) * 2] - M);
-      den += w * a.part_ml[(rb + s2) * 2 + 1];
-      num += w * a.part_o[(rb + s2) * HD + d];
-    }
-    const uint32_t cc = (kvh * g + h) * HD + d;
-    a.out[a.out_frag ? frag_index(b, cc, a.hq * a.hd) : ((uint64_t)b * a.hq + kvh * g + h) * HD + d] = df2bf(num / den);
-  }
-}
-
 hipError_t launch_rmsnorm(const ResidNormArgs& a, hipStream_t s) {
   if (a.dim % 4 || a.dim < 4 || a.dim > 16 * kNormCols || a.ldx % 4 || a.ldy % 4 || (a.y_frag && a.dim % 32))
     return hipErrorInvalidValue;
@@ -883,31 +649,6 @@ hipError_t launch_attn_decode(AttnArgs a, hipStream_t s) {
   const dim3 grid(a.nsplit, a.hkv, a.B);
   const uint32_t nw = st / 64;
   const size_t lds = (size_t)nw * (gg * 64 + g * a.hd) * sizeof(float);  // token-major p (G padded) + outputs
-  // the fused latency-shaped kernel (k_attn_decode_fl) for grids of < 4
-  // workgroups per CU; OGKM_ATTN_FL=0 / 1 forces it off / on (A/B drills)
-  static const int force_fl = getenv("OGKM_ATTN_FL") ? atoi(getenv("OGKM_ATTN_FL")) : -1;
-  const bool fl = ws && st == 256 && a.tickets &&
-                  (force_fl == 1 || (force_fl < 0 && (uint64_t)a.nsplit * a.hkv * a.B < 1024));
-  if (fl) {
-    const size_t fl_lds = (size_t)(16 * gg * 16 + (gg == 4 ? 16 : gg == 8 ? 8 : 4) * g * a.hd) * sizeof(float);
-    // OGKM_ATTN_FL_FUSE=0: the combine as its own launch (A/B drills)
-    static const bool fuse = !getenv("OGKM_ATTN_FL_FUSE") || atoi(getenv("OGKM_ATTN_FL_FUSE")) != 0;
-#define OGKM_ATTN_FL_K(HD, G, D, NS)                                                                       \
-  do {                                                                                                     \
-    if (fuse) hipLaunchKernelGGL((k_attn_decode_fl<HD, G, D, NS, true>), grid, dim3(1024), fl_lds, s, a);  \
-    else hipLaunchKernelGGL((k_attn_decode_fl<HD, G, D, NS, false>), grid, dim3(1024), fl_lds, s, a);      \
-  } while (0)
-#define OGKM_ATTN_FL_G(HD)                          \
-  if (gg == 4) OGKM_ATTN_FL_K(HD, 4, 8, 16);        \
-  else if (gg == 8) OGKM_ATTN_FL_K(HD, 8, 2, 8);    \
-  else OGKM_ATTN_FL_K(HD, 16, 2, 4)
-    if (a.hd == 128) { OGKM_ATTN_FL_G(128); } else { OGKM_ATTN_FL_G(64); }
-#undef OGKM_ATTN_FL_G
-#undef OGKM_ATTN_FL_K
-    if (!fuse && a.nsplit > 1)
-      hipLaunchKernelGGL(k_attn_combine, dim3(a.B * a.hq), dim3(a.hd < 64 ? 64 : a.hd), 0, s, a);
-    return hipGetLastError();
-  }
   if (ws) {
 #define OGKM_ATTN_WS(HD, L, NW, D)                                                                      \
   do switch (var) {                                                                                    \

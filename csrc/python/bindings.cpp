@@ -1043,7 +1043,7 @@ PYBIND11_MODULE(_ogkm, m) {
      py::arg("ksplit") = 0);
   m.def("attn_decode", [](int dev, uint64_t stream, uint64_t q, uint64_t cache, uint64_t out, uint64_t part,
                           uint64_t part_bytes, uint32_t B, uint32_t hq, uint32_t hkv, uint32_t hd, uint32_t T,
-                          uint32_t len, float scale, bool out_frag, uint32_t split_tokens, uint64_t tickets) {
+                          uint32_t len, float scale, bool out_frag, uint32_t split_tokens) {
     AttnArgs a{};
     a.out_frag = out_frag ? 1 : 0;
     const bool ws = hd == 64 || hd == 128;
@@ -1059,11 +1059,10 @@ PYBIND11_MODULE(_ogkm, m) {
     if (rows * (hd + 2) * 4 > part_bytes) throw StatusError("attn_decode: partial workspace too small");
     a.part_o = (float*)part;
     a.part_ml = (float*)part + rows * hd;
-    a.tickets = (uint32_t*)tickets;  // [B * hkv] zeroed words (the kernel leaves them zeroed)
     check(rt()->be()->attn_decode(dev, a, (void*)stream), "attn_decode");
   }, py::arg("dev"), py::arg("stream"), py::arg("q"), py::arg("cache"), py::arg("out"), py::arg("part"),
      py::arg("part_bytes"), py::arg("B"), py::arg("hq"), py::arg("hkv"), py::arg("hd"), py::arg("T"), py::arg("len"),
-     py::arg("scale"), py::arg("out_frag") = false, py::arg("split_tokens") = 0, py::arg("tickets") = 0);
+     py::arg("scale"), py::arg("out_frag") = false, py::arg("split_tokens") = 0);
   m.def("fault_buffer_info", [](int dev) {
     DeviceFaultBuffer& fb = rt()->dev(dev).fault_buf;
     py::dict d;

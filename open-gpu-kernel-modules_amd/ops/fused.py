@@ -90,7 +90,6 @@ def rope_kv(qkv, cos: torch.Tensor, sin: torch.Tensor, cache: torch.Tensor, pos:
 
 class _Work:
     buf: dict = {}
-    tickets: dict = {}
 
 
 def attention(q: torch.Tensor, cache: torch.Tensor, length: int, device_index: int = 0,
@@ -106,13 +105,8 @@ def attention(q: torch.Tensor, cache: torch.Tensor, length: int, device_index: i
     if ws is None or ws.numel() * 4 < need:
         ws = torch.empty(max(need, 1 << 20) // 4 + 1024, dtype=torch.float32, device=q.device)
         _Work.buf[key] = ws
-    # arrival tickets of the fused-combine kernel: zeroed once, every launch leaves them zeroed
-    tk = _Work.tickets.get(key)
-    if tk is None or tk.numel() < B * hkv:
-        tk = torch.zeros(max(B * hkv, 1024), dtype=torch.int32, device=q.device)
-        _Work.tickets[key] = tk
     out = torch.empty((B + 15) // 16 * 16 if out_frag else B, hq * hd, dtype=torch.bfloat16, device=q.device)
     lib.attn_decode(device_index, _stream(q, device_index), q.data_ptr(), cache.data_ptr(), out.data_ptr(),
                     ws.data_ptr(), ws.numel() * 4, B, hq, hkv, hd, T, length, 1.0 / math.sqrt(hd), out_frag,
-                    split_tokens, tk.data_ptr())
+                    split_tokens)
     return out

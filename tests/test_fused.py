@@ -219,35 +219,6 @@ def test_attention_group_shapes_gpu(gpu_rt, hq, hkv, hd, length, split_tokens):
     _check_attention(True, length, hq, hkv, hd, split_tokens)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("hq,hkv", [(8, 1), (16, 1), (4, 1)])
-def test_attention_fused_combine_repeat_gpu(gpu_rt, hq, hkv):
-    """The one-KV-head (tp8 shard) shape takes the fused-combine kernel: the
-    last workgroup of a row merges the splits after an agent-scope hand-off and
-    re-zeroes its ticket. 24 back-to-back launches with different caches and
-    lengths (the hand-off under uneven load, tickets reused every launch), every
-    output word checked against the fp32 reference, fragment-ordered output too."""
-    B, hd, T = 64, 128, 1100
-    g = torch.Generator().manual_seed(5)
-    q = torch.randn(B, hq, hd, generator=g).to(torch.bfloat16)
-    caches = [torch.randn(2, B, hkv, T, hd, generator=g).to(torch.bfloat16) for _ in range(3)]
-    dcaches = [c.to("cuda") for c in caches]
-    dq = q.to("cuda")
-    lengths = [1025, 700, 1100, 257, 256, 1024, 33, 513]
-    outs = []
-    for i in range(24):
-        L = lengths[i % len(lengths)]
-        outs.append((i, L, fused.attention(dq, dcaches[i % 3], L, out_frag=bool(i % 2))))
-    torch.cuda.synchronize()
-    for i, L, got in outs:
-        c = caches[i % 3]
-        want = D.gqa_decode_attention(q.float(), c[0].float(), c[1].float(), L)
-        if i % 2:  # fragment-ordered rows
-            from ogkm.ops import dgemm
-            got = dgemm.from_frag(got, B)
-        torch.testing.assert_close(got.float().cpu(), want, atol=2e-2, rtol=2e-2)
-
-
 # KV-read rate guards at ~85 % of the measured MALL-cold rates (tools/bench_attn.py,
 # profiles/r4_attn_variants.txt: 8B 4.28, 70B 3.69, 70B-tp8 1.42 TB/s).
 @pytest.mark.gpu
