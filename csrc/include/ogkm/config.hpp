@@ -85,11 +85,11 @@ namespace ogkm {
   X(pack_auto_clean_evictions, 2, "a block whose HBM copy was evicted this many times without a copy-out counts as read-mostly and gets packed (0 = only SET_READ_MOSTLY blocks)") \
   X(pack_min_saving_pct, 8, "a block is kept packed only when its packed form saves at least this share of its bytes") \
   X(pack_threads, 4, "host encoder threads of the packer") \
-  X(ans_stage_mb, 64, "per-H2D-ring HBM staging buffer the packed bytes land in before the decode kernel (0: the kernel reads the host copy over PCIe)") \
+  X(ans_stage_mb, 128, "per-H2D-ring HBM staging buffer the packed bytes land in before the decode kernel (0: the kernel reads the host copy over PCIe)") \
   X(ring_defer_decodes, 1, "H2D ring: packed-block decodes overlap the next batch (two staging halves, deferred publish); 0 = drain after each batch's decodes") \
   X(ring_stage_overlap, 1, "H2D ring: a staging half's copies are issued before the host waits for the previous half's and launches its decode (0 = issue, wait, decode per half)") \
-  X(ring_merge_packed_mb, 24, "H2D ring: queued batches of packed-block decodes run as one batch up to this many packed MB (0 = one batch at a time)") \
-  X(ans_stage_engines, 0x9, "SDMA engines (mask) the H2D ring spreads packed-block staging copies over (0 = the ring's own engine)") \
+  X(ring_merge_packed_mb, 64, "H2D ring: queued batches of packed-block decodes run as one batch up to this many packed MB (0 = one batch at a time)") \
+  X(ans_stage_engines, 0xF, "SDMA engines (mask) the H2D ring spreads packed-block staging copies over (0 = the ring's own engine)") \
   X(host_segment_mb, 1024, "host / CXL arenas populate, pin and reserve their memory in segments of this many MB") \
   /* channels / ring */                                                                              \
   X(channel_num_gpfifo_entries, 1024, "SQ/CQ entries per ring")                                      \

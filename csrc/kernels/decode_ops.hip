@@ -61,9 +61,14 @@ __device__ __forceinline__ void norm_store4(const ResidNormArgs& a, uint32_t row
       uint2{(uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16)};
 }
 
-template <int G>
-__global__ void __launch_bounds__(256) k_rmsnorm(ResidNormArgs a) {
-  __shared__ float red[4];
+// NT threads per row: 256 (G column groups of kNormCols), or 1024 for few-row
+// (decode-batch) norms - four times the loads in flight per row, so the split-K
+// partials of a 64-row residual take fewer dependent rounds (OGKM_NORM_1K=0:
+// the 256-thread form only).
+template <int G, int NT = 256>
+__global__ void __launch_bounds__(NT) k_rmsnorm(ResidNormArgs a) {
+  constexpr uint32_t kCols = 4 * NT;
+  __shared__ float red[NT / 64];
   const uint32_t row = blockIdx.x, t = threadIdx.x;
   uint16_t* xr = a.x + (uint64_t)row * a.ldx;
   uint32_t cl[G];  // clamped column of each group (loads); c < dim gates the use
@@ -71,7 +76,7 @@ __global__ void __launch_bounds__(256) k_rmsnorm(ResidNormArgs a) {
   uint2 xp[G], wp[G];
 #pragma unroll
   for (int j = 0; j < G; ++j) {
-    const uint32_t c = 4 * t + kNormCols * j;
+    const uint32_t c = 4 * t + kCols * j;
     on[j] = c < a.dim;
     cl[j] = on[j] ? c : a.dim - 4;
     xp[j] = *reinterpret_cast<const uint2*>(xr + cl[j]);
@@ -86,7 +91,7 @@ __global__ void __launch_bounds__(256) k_rmsnorm(ResidNormArgs a) {
     v[j][3] = dbf((uint16_t)(xp[j].y >> 16));
   }
   if (a.part) {
-    constexpr uint32_t KB = G <= 4 ? 8 : G <= 8 ? 4 : 2;  // splits per batch: KB x G loads in flight
+    constexpr uint32_t KB = G <= 2 ? 16 : G <= 4 ? 8 : G <= 8 ? 4 : 2;  // splits per batch: KB x G loads in flight
     float4 sum[G];
 #pragma unroll
     for (int j = 0; j < G; ++j) sum[j] = float4{0.f, 0.f, 0.f, 0.f};
@@ -132,7 +137,9 @@ __global__ void __launch_bounds__(256) k_rmsnorm(ResidNormArgs a) {
   ss = wave_sum(ss);
   if ((t & 63) == 0) red[t >> 6] = ss;
   __syncthreads();
-  const float tot = red[0] + red[1] + red[2] + red[3];
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) tot += red[w];
   const float r = rsqrtf(tot / (float)a.dim + a.eps);
 #pragma unroll
   for (int j = 0; j < G; ++j)
@@ -615,6 +622,14 @@ hipError_t launch_rmsnorm(const ResidNormArgs& a, hipStream_t s) {
     const dim3 grid((a.dim + kNormCols - 1) / kNormCols, a.rows);
     hipLaunchKernelGGL(k_norm_ssq, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_norm_scale, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  static const bool wide1k = !getenv("OGKM_NORM_1K") || atoi(getenv("OGKM_NORM_1K")) != 0;
+  if (wide1k && a.rows < kNormWideRows && a.dim > kNormCols && a.dim <= 8 * kNormCols) {
+    if (a.dim <= 4 * kNormCols)
+      hipLaunchKernelGGL((k_rmsnorm<1, 1024>), dim3(a.rows), dim3(1024), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_rmsnorm<2, 1024>), dim3(a.rows), dim3(1024), 0, s, a);
     return hipGetLastError();
   }
   if (a.dim <= kNormCols)
