@@ -344,6 +344,7 @@ def run_torch_managed(a) -> None:
         dt = time.perf_counter() - t0
         al1 = allocator.stats()
     s = lib.stats()
+    census = _block_census() if os.environ.get("OGKM_TM_CENSUS") == "1" else None
     name = {"llama3-70b": "Llama-3-70B", "llama3-405b": "Llama-3-405B", "llama3-8b": "Llama-3-8B"}.get(a.model, a.model)
     out = {
         "metric": f"tokens/sec {name} {a.oversub:g}x oversubscribe (stock torch model, transparent managed mode)",
@@ -375,10 +376,40 @@ def run_torch_managed(a) -> None:
                 "trace_len": len(mode._trace), "hinted_ops": mode.hinted_ops, "trace_misses": mode.trace_misses,
                 "allocs_per_step": (al1["allocs"] - al0["allocs"]) // max(1, a.steps), "alloc_peak_gb":
                 round(al1["peak"] / 1e9, 2), "managed_min_mb": int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")),
-                "lookahead_mb": la,
+                "lookahead_mb": la, "block_census": census,
                 "spread": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in lib.spread_stats(0).items()}},
     }
     print(json.dumps(out), flush=True)
+
+
+def _block_census(top: int = 8) -> dict:
+    """Where every managed 2 MB block rests (diagnostic, after the timed steps):
+    HBM-resident or not, host copy packed / raw; the ranges with the most
+    non-resident raw blocks (what refills move unpacked)."""
+    from collections import Counter
+
+    from ogkm._native import lib
+    kinds, per_range = Counter(), []
+    for rid in lib.range_ids():
+        info = lib.range_info(rid)
+        raw_out = 0
+        for bi in range(info["nblocks"]):
+            try:
+                ri = lib.residency_info(rid, bi << 21)
+            except Exception:  # noqa: BLE001 - a range freed meanwhile
+                break
+            tiers = [e["tier"] for e in ri["resident_on"]]
+            packed = any(e.get("encoded_bytes") for e in ri["resident_on"] if e["tier"] != "gpu")
+            gpu = "gpu" in tiers
+            host = any(t != "gpu" for t in tiers)
+            key = ("gpu" if gpu else "nogpu") + ("+packed" if packed else "+raw" if host else "")
+            kinds[key] += 1
+            raw_out += (not gpu) and host and not packed
+        if raw_out:
+            per_range.append((raw_out, info["name"], info["size"]))
+    per_range.sort(reverse=True)
+    return {"blocks": dict(kinds), "raw_not_resident_top": [
+        {"blocks": n, "name": nm, "mb": round(sz / 2**20, 1)} for n, nm, sz in per_range[:top]]}
 
 
 def _ring_per_step(s: dict, steps: int) -> dict:
