@@ -155,10 +155,15 @@ bool Runtime::pack_block(uint64_t range_id, uint64_t bi, uint16_t* raw, uint8_t*
     Block* b = r->block(bi);
     std::lock_guard<OrderedMutex> g(b->lock);
     Residency* x = pack_candidate(b);
-    if (!x || r->dead.load() || b->lease_pins || b->user_pins) {
+    if (!x || r->dead.load() || b->user_pins) {
       b->pack_queued = false;
       return false;
     }
+    // A lease of the host copy itself (a CPU or zero-copy remote lease pins its
+    // chunk) defers the packing; leases of the block's GPU copy do not read it
+    // (a hot block is leased again within a step: dropping the job here left
+    // it raw until its next clean eviction, which races the same way).
+    if (x->arena->pinned((uint32_t)x->chunk)) return true;
     if (b->unpublished || !b->tracker.query()) return true;  // copies into the block still in flight
     nv = b->npages << (kPageShift - 1);
     arena = x->arena;
@@ -178,10 +183,11 @@ bool Runtime::pack_block(uint64_t range_id, uint64_t bi, uint16_t* raw, uint8_t*
   Residency* y = nullptr;
   for (auto& x : b->res)
     if (x.arena == arena && x.chunk == chunk) y = &x;
-  if (!y || y->fmt != 0 || !(y->resident == b->valid_pages()) || r->dead.load() || b->lease_pins || b->user_pins) {
+  if (!y || y->fmt != 0 || !(y->resident == b->valid_pages()) || r->dead.load() || b->user_pins) {
     b->pack_queued = false;
     return false;
   }
+  if (arena->pinned((uint32_t)chunk)) return true;
   if (b->unpublished || !b->tracker.query()) return true;
   if (!e) {
     b->pack_queued = false;

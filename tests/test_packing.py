@@ -283,3 +283,29 @@ def test_queued_packed_batches_run_merged(fake_rt):
     assert s1["ring_merged_batches"] > s0["ring_merged_batches"]
     for b in bufs:
         b.free()
+
+
+def test_block_leased_on_gpu_still_packs(fake_rt):
+    """A block evicted clean and leased again on the GPU before the encoder
+    reaches it (a hot block of a cyclic workload) still gets its host copy
+    packed: the GPU lease never reads the host copy. Only a lease of the host
+    copy itself defers the packing."""
+    rt.configure(pack_host_copies=1, pack_threads=1)
+    b = rt.malloc_managed(32 * MB, "hot")
+    data = _weights(b.size, 77)
+    b.write(data)
+    b.set_read_mostly(True)
+    l = b.acquire(0, rt.READ)
+    l.wait(0)
+    l.release(0)
+    b.evict("gpu:0")  # 16 blocks queued for one encoder thread
+    last = 30 * MB
+    l = b.acquire(0, rt.READ, offset=last, length=2 * MB)  # the last block is back on the GPU, leased
+    l.wait(0)
+    assert lib.pack_wait(30000)
+    assert any(o == last for o, _, _ in _packed_entries(b))
+    t = l.tensor((2 * MB,), torch.uint8).clone()
+    l.release(0)
+    assert t.equal(data[last:last + 2 * MB])
+    assert _gpu_read(b).equal(data)
+    b.free()
