@@ -630,11 +630,58 @@ class TieredLlama:
         self._xrows = None
         self.last_logits = None
         self.gather = None
+        self.gather_cache_bytes = 0
         if self.sworld > 1:
             from ..parallel.shards import UnitGather
             self.gather = UnitGather([k for k in self.order if k[0] != "kv"], self._buf, self._unit_bytes, self.sworld, self.gather_depth,
                                      device=self.tdev, dev_index=device)
+            self._gather_cache_setup()
         self._settle()
+
+    def _gather_cache_setup(self) -> None:
+        """Shards mode with HBM to spare: whole gathered units kept as read
+        duplicates in a managed buffer leased for the model's lifetime (so the
+        runtime's arena accounts for them), chosen evenly over the use order;
+        they are all-gathered once and then read in place - the reference's
+        read duplication of data resident on another processor
+        (uvm_va_block.c:5164), sized to what the budget leaves after this
+        rank's shards, the resident KV and the streaming window.
+        OGKM_GATHER_CACHE_MB: 0 = off, N = at most N MB (default: auto)."""
+        from ..parallel import comm
+        self._gcache, self._gcache_lease, self.gather_cache_bytes = None, None, 0
+        cap_env = os.environ.get("OGKM_GATHER_CACHE_MB")
+        if cap_env == "0":
+            return
+        keys = self.gather.order
+        full = {k: _al(self._unit_bytes(k) * self.sworld) for k in keys}
+        shards = sum(self._unit_bytes(k) for k in keys)
+        spare = (self.arena_bytes - self.kv_resident_bytes - self.norm_bytes - shards - self.window_bytes
+                 - 2 * self.slot_bytes)
+        if cap_env:
+            spare = min(spare, int(float(cap_env) * 2**20))
+        # the same choice on every rank: it decides which collectives run
+        spare = -comm.max_over_ranks(-float(spare))
+        total = sum(full.values())
+        if spare < min(full.values()):
+            return
+        frac = min(1.0, spare / total)
+        chosen, used = [], 0
+        for j, k in enumerate(keys):  # evenly spread: floor((j + 1) f) > floor(j f)
+            if int((j + 1) * frac) > int(j * frac) and used + full[k] <= spare:
+                chosen.append(k)
+                used += full[k]
+        if not chosen:
+            return
+        self._gcache = rt.malloc_managed(used, "gather_cache")
+        self._gcache_lease = self._gcache.acquire(self.dev, rt.WRITE)
+        self._gcache_lease.wait()
+        buf = self._gcache_lease.tensor((used,), torch.uint8)
+        offs, o = {}, 0
+        for k in chosen:
+            offs[k] = o
+            o += full[k]
+        self.gather.set_cache(buf, offs)
+        self.gather_cache_bytes = used
 
     # ------------------------------------------------------------------ save / resume
     def save(self, path: str) -> dict:
@@ -1370,6 +1417,11 @@ class TieredLlama:
     def close(self) -> None:
         if self.gather is not None:
             self.gather.drain()
+            if getattr(self, "_gcache_lease", None) is not None:
+                self._gcache_lease.release(0 if self.fake else None)
+                lib.sync_all()
+                self._gcache.free()
+                self._gcache, self._gcache_lease = None, None
         self._us = None  # (its run-ahead events synchronised) before the ranges go
         self.kv_lease.release(0 if self.fake else None)
         for lease in self._pin_leases:

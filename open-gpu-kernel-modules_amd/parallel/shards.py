@@ -69,10 +69,23 @@ class UnitGather:
         self.stream = torch.cuda.Stream(device=self.device) if self.cuda else None
         self.slot_free_ev: list = [None] * self.depth
         self.slot_busy = [False] * self.depth
-        self.pending: dict = {}   # key -> (slot, ready event)
+        self.pending: dict = {}   # key -> (slot, ready event); slot -1: the unit's cached copy
         self.next_issue = 0
         self.next_slot = 0
-        self.stats = {"gathers": 0, "bytes_in": 0}
+        self.stats = {"gathers": 0, "bytes_in": 0, "cache_hits": 0}
+        # Read duplicates of whole units kept in spare HBM (set_cache): gathered
+        # once, then served in place - no collective, no slot.
+        self.cache_buf: Optional[torch.Tensor] = None
+        self.cache_off: dict = {}
+        self.cache_filled: set = set()
+
+    def set_cache(self, buf: torch.Tensor, offsets: dict) -> None:
+        """Keep the units in ``offsets`` (key -> byte offset into ``buf``, room
+        for shard bytes x world each) gathered: the first use all-gathers into
+        the cache, later uses read it. The key set must be the same on every
+        rank (it decides which collectives are issued)."""
+        self.drain()
+        self.cache_buf, self.cache_off, self.cache_filled = buf, dict(offsets), set()
 
     # ---------------------------------------------------------------- internals
     def _free_slot(self) -> Optional[int]:
@@ -83,18 +96,32 @@ class UnitGather:
                 return s
         return None
 
+    def _out(self, key, slot: int) -> torch.Tensor:
+        if slot < 0:
+            off = self.cache_off[key]
+            return self.cache_buf[off:off + self.size_of(key) * self.world]
+        return self.bufs[slot]
+
     def _issue(self, key) -> bool:
-        slot = self._free_slot()
-        if slot is None:
-            return False
-        self.slot_busy[slot] = True
-        buf = self.shard_of(key)
         S = self.size_of(key)
+        if key in self.cache_off:
+            slot = -1
+            if key in self.cache_filled:  # a resident read duplicate: nothing to move
+                self.pending[key] = (-1, None)
+                self.stats["cache_hits"] += 1
+                return True
+            self.cache_filled.add(key)  # (filled by the gather issued below)
+        else:
+            slot = self._free_slot()
+            if slot is None:
+                return False
+            self.slot_busy[slot] = True
+        buf = self.shard_of(key)
         lease = buf.acquire(self.dev_index, rt.READ, 0, S)
-        out = self.bufs[slot][:S * self.world]
+        out = self._out(key, slot)[:S * self.world]
         if self.cuda:
             with torch.cuda.stream(self.stream):
-                if self.slot_free_ev[slot] is not None:
+                if slot >= 0 and self.slot_free_ev[slot] is not None:
                     self.stream.wait_event(self.slot_free_ev[slot])
                 lease.wait(self.stream.cuda_stream)
                 shard = lease.tensor((S,), torch.uint8)
@@ -129,7 +156,10 @@ class UnitGather:
                 self.done(k)
             self.next_issue = self.pos[key]
         i = self.pos[key]
-        while (self.next_issue - i) % n < self.depth:
+        # (with a cache the look-ahead runs past cached units: the free slots,
+        # not the unit count, bound the gathers in flight)
+        limit = max(self.depth, n - 1) if self.cache_off else self.depth
+        while (self.next_issue - i) % n < limit:
             k = self.order[self.next_issue]
             if k in self.pending or not self._issue(k):
                 break
@@ -141,10 +171,12 @@ class UnitGather:
         slot, ev = self.pending[key]
         if ev is not None:
             torch.cuda.current_stream(self.device).wait_event(ev)
-        return self.bufs[slot]
+        return self._out(key, slot)
 
     def done(self, key) -> None:
         slot, _ = self.pending.pop(key)
+        if slot < 0:  # the cached copy is never rewritten
+            return
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))

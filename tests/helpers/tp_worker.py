@@ -33,8 +33,11 @@ def main():
     for s in range(3):  # fixed input schedule: comparisons do not depend on near-tie argmax
         glob = torch.tensor([3 + s + 8 * j for j in range(batch)])
         tok = m.step(glob[m.b0:m.b0 + m.B])
-        out.append({"tokens": tok.tolist(), "logits": m.last_logits[:, :64].tolist()})
-    out.append({"host_node": lib.host_node(), "gathers": m.gather.stats["gathers"] if m.gather else 0})
+        out.append({"tokens": tok.tolist(), "logits": m.last_logits[:, :64].tolist(),
+                    "gathers": m.gather.stats["gathers"] if m.gather else 0})
+    out.append({"host_node": lib.host_node(), "gathers": m.gather.stats["gathers"] if m.gather else 0,
+                "cache_hits": m.gather.stats["cache_hits"] if m.gather else 0,
+                "cache_bytes": m.gather_cache_bytes})
     if e.rank == 0:
         print("TPRESULT " + json.dumps(out), flush=True)
     m.close()

@@ -182,6 +182,29 @@ def test_peer_shards_two_ranks_matches_single(fake_rt):
         assert step["tokens"] == tok1[:2]  # rank 0's own sequences
 
 
+def test_peer_shards_keep_read_duplicates_when_hbm_allows(fake_rt):
+    """Shards mode with HBM to spare (no oversubscription): whole gathered units
+    stay as read duplicates in a managed buffer the runtime accounts for - the
+    first step all-gathers every unit once, later steps gather nothing - and
+    the logits still match one GPU."""
+    lib.shutdown()
+    rt.init("fake", fake_devices=1, fake_hbm_mb=512, lock_check=1, host_budget_mb=2048)
+    single = _single_run(batch=4, oversub=1.0, model="small")
+    # budget 2.5x the rank's shard footprint: room for every whole unit
+    sh = _multi_run(2, "shards", batch=4, oversub=0.4, model="small")
+    assert len(sh) == 4 and sh[-1]["cache_bytes"] > 0 and sh[-1]["cache_hits"] > 0
+    assert sh[1]["gathers"] == sh[0]["gathers"] == sh[2]["gathers"] > 0  # nothing gathered after step 1
+    # budget 1x: part of the units duplicated, evenly over the use order
+    part = _multi_run(2, "shards", batch=4, oversub=1.0, model="small")
+    per_step = part[2]["gathers"] - part[1]["gathers"]
+    assert part[-1]["cache_bytes"] > 0 and 0 < per_step < part[0]["gathers"]
+    for (tok1, log1), step in zip(single, part):
+        torch.testing.assert_close(torch.tensor(step["logits"]), log1, atol=1e-3, rtol=1e-3)
+    for (tok1, log1), step in zip(single, sh):
+        torch.testing.assert_close(torch.tensor(step["logits"]), log1, atol=1e-3, rtol=1e-3)
+        assert step["tokens"] == tok1[:2]
+
+
 def test_three_tier_host_and_cxl_streaming(fake_rt):
     """Config 5 shape: HBM + host DRAM + CXL.mem. Streamed tensors rest
     interleaved on the host and (emulated) CXL tiers; decode output is identical
