@@ -676,6 +676,7 @@ def main() -> None:
                 "launcher": ("bench.py" if os.environ.get("OGKM_BENCH_LAUNCHED") == "1"
                              else "external" if world > 1 else "none"),
                 "planner": model.planner,
+                "gather_cache_gb_per_gpu": round(getattr(model, "gather_cache_bytes", 0) / 1e9, 3),
                 "kv_tiering": a.kv_tiering,
                 "torch_allocator": "ogkm-arena" if a.allocator else "torch-caching",
                 "rank_host_numa_nodes": host_nodes,

@@ -28,9 +28,10 @@ def _port() -> int:
 
 
 def _bench(tmp_path, nproc: int, extra: list, force_dist: bool = False,
-           self_launch: bool = False) -> tuple[dict, torch.Tensor]:
-    dump = str(tmp_path / f"logits_{nproc}_{int(force_dist)}_{int(self_launch)}_{'_'.join(extra)}.pt")
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", OGKM_UNIT_MIN_MB="0")
+           self_launch: bool = False, env_extra: dict | None = None) -> tuple[dict, torch.Tensor]:
+    tag = "_".join(f"{k}{v}" for k, v in (env_extra or {}).items())
+    dump = str(tmp_path / f"logits_{nproc}_{int(force_dist)}_{int(self_launch)}_{'_'.join(extra)}{tag}.pt")
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", OGKM_UNIT_MIN_MB="0", **(env_extra or {}))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     if force_dist:
@@ -209,4 +210,16 @@ def test_shards_two_ranks_planner_off_small_arena(single, tmp_path):
     cfg = out["config"]
     assert cfg["planner"] == "off" and cfg["parallelism"] == "shards2"
     assert out["aux"]["evictions"] > 0
+    assert torch.equal(logits, ref)
+
+
+def test_shards_two_ranks_read_duplicates(tmp_path):
+    """Peer shards with HBM to spare (oversub 0.4: 2.5x the rank's shard
+    footprint): every gathered unit stays on each rank as a read duplicate
+    after its first gather; the decode is bit-exact against the same job
+    re-gathering every unit (OGKM_GATHER_CACHE_MB=0)."""
+    args = ["--parallel", "shards", "--oversub", "0.4", "--launch-timeout", "300", "--steps", "3"]
+    out, logits = _bench(tmp_path, 2, args, self_launch=True)
+    base, ref = _bench(tmp_path, 2, args, self_launch=True, env_extra={"OGKM_GATHER_CACHE_MB": "0"})
+    assert out["config"]["gather_cache_gb_per_gpu"] > 0 and base["config"]["gather_cache_gb_per_gpu"] == 0
     assert torch.equal(logits, ref)

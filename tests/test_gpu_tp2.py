@@ -26,7 +26,7 @@ ARGS = ["--model", "small", "--batch", str(B), "--context", str(CTX), "--steps",
         "--weights", "ans", "--kv-format", "bf16", "--oversub", "1.5"]
 
 
-def _run2(tmp_path, parallel: str) -> tuple[dict, torch.Tensor]:
+def _run2(tmp_path, parallel: str, extra: tuple = ()) -> tuple[dict, torch.Tensor]:
     # the two rank processes share the GPU with this one: hand back what this
     # process's earlier tests cached first
     if torch.cuda.is_initialized():
@@ -37,7 +37,7 @@ def _run2(tmp_path, parallel: str) -> tuple[dict, torch.Tensor]:
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-gpu", "--launch-timeout", "120",
-           "--parallel", parallel] + ARGS + ["--dump-logits", dump]
+           "--parallel", parallel] + ARGS + list(extra) + ["--dump-logits", dump]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-4000:]
@@ -70,10 +70,16 @@ def fp32_reference():
 
 
 @pytest.mark.timeout(300)  # three processes start HIP (2 ranks + this one); the bench itself takes seconds
-@pytest.mark.parametrize("parallel", ["tp", "shards"])
+@pytest.mark.parametrize("parallel", ["tp", "shards", "shards-dup"])
 def test_two_ranks_match_fp32_reference(fp32_reference, tmp_path, parallel):
-    out, logits = _run2(tmp_path, parallel)
+    # shards-dup: a budget of 2.5x the rank's shard footprint - every gathered
+    # unit stays on each rank as a read duplicate after its first gather
+    extra = ("--oversub", "0.4") if parallel == "shards-dup" else ()
+    parallel = parallel.split("-")[0]
+    out, logits = _run2(tmp_path, parallel, extra)
     cfg = out["config"]
+    if extra:
+        assert cfg["gather_cache_gb_per_gpu"] > 0
     assert out["n_gpus"] == 2 and cfg["rccl_world"] == 2 and cfg["launcher"] == "bench.py"
     assert cfg["parallelism"] == f"{parallel}2"
     assert logits.shape == fp32_reference.shape
