@@ -400,13 +400,14 @@ class TieredLlama:
         fixed = chunks(self.kv_resident_bytes + self.norm_bytes)
         # With the KV cache streamed (tiering: a ~1 GB unit per layer at 32k
         # context) and the runtime deciding residency, the host's prefetch calls
-        # for those units are long (they evict as much): a window of ~16 KV units
+        # for those units are long (they evict as much): a window of ~13 KV units
         # keeps the link busy through them (70B, 32k, batch 8: 10.3 tok/s at
-        # 56.8 GB/s with 13 units vs 8.1 at 41 with 384 MB, 8.8-10.0 with 6-8
-        # units depending on the host; profiles/r5_longctx.jsonl).
+        # 56.8 GB/s with 13 units vs 8.1 at 41 with 384 MB; 6-8 units 8.8-10.0,
+        # 16 units 9.2-9.3 - the host's prefetch calls grow with the window;
+        # profiles/r5_longctx.jsonl).
         wdef = 384 * 2**20
         if self.kv_tier and planner == "off" and self.kv_unit_bytes:
-            wdef = max(wdef, 16 * chunks(self.kv_unit_bytes))
+            wdef = max(wdef, 13 * chunks(self.kv_unit_bytes))
         window_min = int(float(os.environ.get("OGKM_WINDOW_MB", "0")) * 2**20) or wdef
         lookahead_arg = lookahead
         lookahead = max(lookahead, min(-(-window_min // slot), max(0, self.arena_bytes - fixed) // (4 * slot)))
