@@ -417,9 +417,11 @@ def _ring_per_step(s: dict, steps: int) -> dict:
     dependencies, in engine copies, idle; engine copy calls per step."""
     out = {k: round(s.get(f"ring_{k}_ns", 0) / 1e6 / max(1, steps), 1) for k in ("fence_wait", "copy", "idle")}
     out["copy_calls"] = s.get("ring_copy_calls", 0) // max(1, steps)
-    for k in ("packed_decodes", "ring_merged_batches", "decode_reuse_waits"):
+    for k in ("packed_decodes", "ring_merged_batches", "decode_reuse_waits", "victim_risen_seen"):
         if s.get(k):
             out[k] = s[k] // max(1, steps)
+    if s.get("victim_search_ns"):  # host time in next-use victim searches
+        out["victim_search_ms"] = round(s["victim_search_ns"] / 1e6 / max(1, steps), 1)
     return out
 
 

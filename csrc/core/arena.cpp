@@ -391,6 +391,11 @@ bool ChunkArena::floor_protects_locked(const ChunkInfo& c, uint64_t floor) const
 void ChunkArena::next_victims_locked(uint32_t want, uint64_t floor, std::vector<std::pair<uint64_t, uint32_t>>* out) {
   out->clear();
   if (!want) return;
+  struct Clock {  // host cost of the victim search (stats victim_search_ns)
+    uint64_t t0 = now_ns();
+    ~Clock() { Tools::get().inc(Counter::VictimSearchNs, now_ns() - t0); }
+  } clock;
+  Tools::get().inc(Counter::VictimRisenSeen, vrisen_.size());
   const int64_t every = config().arena_victim_cache_ops;
   for (int pass = 0; pass < 2 && out->size() < want; ++pass) {
     const bool stale = !vcache_valid_ || vcache_pos_ >= vcache_.size() || every <= 0 ||

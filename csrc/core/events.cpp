@@ -162,7 +162,9 @@ const char* counter_name(Counter c) {
                             "packed_decodes",
                             "pressure_reliefs",
                             "decode_reuse_waits",
-                            "ring_merged_batches"};
+                            "ring_merged_batches",
+                            "victim_search_ns",
+                            "victim_risen_seen"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

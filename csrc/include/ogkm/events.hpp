@@ -206,6 +206,8 @@ enum class Counter : int {
   PressureReliefs,     // reservations that found nothing evictable until soft pins let go
   DecodeReuseWaits,    // H2D copies that waited for a running packed-block decode into the same chunk
   RingMergedBatches,   // packed-decode batches the H2D ring ran merged into the batch before (Ring::worker)
+  VictimSearchNs,      // host time in next-use victim searches (ChunkArena::next_victims_locked)
+  VictimRisenSeen,     // re-hinted chunks those searches re-ranked (summed over calls)
   NumCounters
 };
 const char* counter_name(Counter c);
