@@ -408,10 +408,21 @@ void ChunkArena::next_victims_locked(uint32_t want, uint64_t floor, std::vector<
         if (c.state != ChunkState::ALLOCATED || c.pin_count != 0) continue;
         vcache_.emplace_back(victim_key_locked(c), i);
       }
-      std::sort(vcache_.begin(), vcache_.end(),
-                [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
-                  return a.first > b.first || (a.first == b.first && a.second < b.second);
-                });
+      auto better = [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
+        return a.first > b.first || (a.first == b.first && a.second < b.second);
+      };
+      // A periodic rebuild ranks only the best few thousand (a selection, then
+      // a sort of those - the full sort of a 100+ GB arena's chunks on every
+      // rebuild was most of a long-context step's prefetch time); the
+      // fallback pass ranks everything, so no victim is ever missed.
+      const int64_t rank_top = config().arena_victim_rank_top;
+      const size_t top = pass == 0 && rank_top > 0 ? std::max<size_t>((size_t)rank_top, 8 * (size_t)want)
+                                                   : vcache_.size();
+      if (top < vcache_.size()) {
+        std::nth_element(vcache_.begin(), vcache_.begin() + top, vcache_.end(), better);
+        vcache_.resize(top);
+      }
+      std::sort(vcache_.begin(), vcache_.end(), better);
       vcache_pos_ = 0;
       vcache_clock_ = op_clock_;
       vcache_valid_ = true;

@@ -61,6 +61,7 @@ namespace ogkm {
   X(perf_spread_keep_pct, 97, "spread classes: percent of the HBM arena's unpinned capacity the keep class may fill") \
   X(perf_spread_adapt, 0, "spread classes: a pass that evicted keep-class data shrinks the keep class (online, from refaults). Off by default: on the 70B headline the keep-class evictions are structural (contiguous extents), shrinking the class only streams more (123.1 vs 129.4 tok/s, profiles/r5_spread.md)") \
   X(perf_spread_step_pct, 2, "spread classes: keep-share reduction per adaptation (percent)") \
+  X(arena_victim_rank_top, 4096, "next-use eviction: a periodic victim-cache rebuild ranks only this many best chunks (at least 8x the request; the fallback pass ranks all; 0 = always all)") \
   X(arena_victim_cache_ops, 16, "next-use eviction: rebuild the ranked victim list after the op clock moved this far (0 = full scan per call)") \
   X(lease_fast_path, 1, "acquire: a GPU read of data resident in one contiguous extent only pins, touches and waits (no placement pass)") \
   X(unit_hold, 1, "UnitStream: after a pass with no eviction and no streaming, released units keep their leases until their next use (dropped at the first eviction / refused prefetch)") \

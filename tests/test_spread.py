@@ -124,3 +124,18 @@ def test_reset_op_clock_forgets_the_cycle(fake_rt):
     assert st["ranges"] == N_UNITS
     lib.reset_op_clock(0)
     assert lib.spread_stats(0)["ranges"] == 0
+
+
+@pytest.mark.parametrize("spread", [True, False])
+def test_partial_victim_ranking_matches_full(fake_rt, spread):
+    """A victim-cache rebuild that ranks only the best few chunks (the default
+    ranks 4096 - here 1, so the 32-chunk arena takes the partial path on every
+    rebuild) picks the same victims as ranking every chunk: identical traffic
+    per pass and the same resident set."""
+    lib.configure("arena_victim_cache_ops", 4)
+    lib.configure("arena_victim_rank_top", 0)
+    full = _run_cycle(passes=4, spread=spread)
+    lib.configure("arena_victim_rank_top", 1)
+    part = _run_cycle(passes=4, spread=spread)
+    assert full[3] and part[3]
+    assert full[1] == part[1] and full[2] == part[2]
