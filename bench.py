@@ -60,8 +60,8 @@ if hasattr(__import__("signal"), "pthread_sigmask"):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--model", default="llama3-70b")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--context", type=int, default=1024)
