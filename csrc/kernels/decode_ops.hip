@@ -594,18 +594,42 @@ __global__ void __launch_bounds__(256) k_attn_decode_ws(AttnArgs a) {
   }
 }
 
-// One workgroup of hd threads per (b, q head): merge the splits.
+// One workgroup of hd threads per (b, q head): merge the splits. Splits are
+// read 8 at a time, all loads of a group issued before the first use (one
+// dependent memory round per 8 splits instead of two passes over them), with
+// the running max rescaling the sums between groups; up to 8 splits (2048
+// tokens) the arithmetic is exactly the two-pass merge's.
 __global__ void k_attn_combine(AttnArgs a) {
   const uint32_t bh = blockIdx.x;  // b * hq + h
   const uint32_t d = threadIdx.x;
-  float M = -INFINITY;
-  for (uint32_t s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.part_ml[((uint64_t)bh * a.nsplit + s) * 2]);
-  float num = 0.f, den = 0.f;
-  for (uint32_t s = 0; s < a.nsplit; ++s) {
-    const uint64_t row = (uint64_t)bh * a.nsplit + s;
-    const float w = __expf(a.part_ml[row * 2] - M);
-    den += w * a.part_ml[row * 2 + 1];
-    if (d < a.hd) num += w * a.part_o[row * a.hd + d];
+  const uint64_t r0 = (uint64_t)bh * a.nsplit;
+  float M = -INFINITY, num = 0.f, den = 0.f;
+  for (uint32_t s0 = 0; s0 < a.nsplit; s0 += 8) {
+    float m[8], l[8], o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t row = r0 + (s0 + j < a.nsplit ? s0 + j : a.nsplit - 1);  // clamped: masked below
+      m[j] = a.part_ml[row * 2];
+      l[j] = a.part_ml[row * 2 + 1];
+      o[j] = d < a.hd ? a.part_o[row * a.hd + d] : 0.f;
+    }
+    float mb = M;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (s0 + j < a.nsplit) mb = fmaxf(mb, m[j]);
+    if (M != -INFINITY) {  // earlier groups' sums, rescaled to the new max
+      const float sc = __expf(M - mb);
+      num *= sc;
+      den *= sc;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (s0 + j < a.nsplit) {
+        const float w = __expf(m[j] - mb);
+        den += w * l[j];
+        num += w * o[j];
+      }
+    M = mb;
   }
   if (d < a.hd) {
     const uint32_t b = bh / a.hq, col = (bh - b * a.hq) * a.hd + d;
