@@ -726,6 +726,9 @@ class TieredLlama:
         plan = TieredLlama(cfg, dry_run=True, pack_ratio=1.0, attach=None, **kw)
         lib.init_device(kw["device"], plan.arena_init_bytes)
         checkpoint.load(path + ".rmap", with_data=True, in_place=True)
+        for rid in lib.range_ids():  # shards read duplicates: rebuilt from the shards, not restored
+            if lib.range_info(rid)["name"] == "gather_cache":
+                rt.ManagedBuffer(rid).free()
         return TieredLlama(cfg, verbose=verbose, attach=side, **kw)
 
     def _attach(self, side: dict) -> None:
