@@ -889,7 +889,7 @@ uint64_t ChunkArena::outstanding_bytes() {
 std::string ChunkArena::check() {
   std::lock_guard<OrderedMutex> g(m_);
   std::ostringstream os;
-  uint32_t nfree = 0, nalloc = 0;
+  uint32_t nfree = 0, nalloc = 0, nfree_state = 0;
   std::vector<uint8_t> in_run(nchunks_, 0);
   uint32_t prev_end = 0;
   bool first = true;
@@ -907,7 +907,9 @@ std::string ChunkArena::check() {
   for (uint32_t i = 0; i < nchunks_; ++i) {
     if (chunks_[i].state == ChunkState::FREE && !in_run[i]) os << "FREE chunk " << i << " not in runs; ";
     if (chunks_[i].state == ChunkState::ALLOCATED) nalloc++;
+    if (chunks_[i].state == ChunkState::FREE) nfree_state++;
   }
+  if (nfree != nfree_state) os << "free runs hold " << nfree << " chunks but " << nfree_state << " are FREE; ";
   uint64_t n_on_lists = 0;
   for (int l : {1, 2, 3})
     for (int32_t i = head_[l]; i >= 0; i = chunks_[i].next) {
