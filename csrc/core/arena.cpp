@@ -889,7 +889,7 @@ uint64_t ChunkArena::outstanding_bytes() {
 std::string ChunkArena::check() {
   std::lock_guard<OrderedMutex> g(m_);
   std::ostringstream os;
-  uint32_t nfree = 0, nalloc = 0, nfree_state = 0;
+  uint32_t nfree = 0, nalloc = 0, nfree_state = 0, ndoomed = 0;
   std::vector<uint8_t> in_run(nchunks_, 0);
   uint32_t prev_end = 0;
   bool first = true;
@@ -907,6 +907,10 @@ std::string ChunkArena::check() {
   for (uint32_t i = 0; i < nchunks_; ++i) {
     if (chunks_[i].state == ChunkState::FREE && !in_run[i]) os << "FREE chunk " << i << " not in runs; ";
     if (chunks_[i].state == ChunkState::ALLOCATED) nalloc++;
+    if (chunks_[i].state == ChunkState::ALLOCATED && chunks_[i].doomed) {
+      ndoomed++;  // revoked under a lease: freed at its last unpin, off the LRU lists meanwhile
+      if (chunks_[i].pin_count == 0) os << "doomed chunk " << i << " unpinned but not freed; ";
+    }
     if (chunks_[i].state == ChunkState::FREE) nfree_state++;
   }
   if (nfree != nfree_state) os << "free runs hold " << nfree << " chunks but " << nfree_state << " are FREE; ";
@@ -917,7 +921,8 @@ std::string ChunkArena::check() {
       if (chunks_[i].state != ChunkState::ALLOCATED) os << "non-allocated chunk " << i << " on LRU; ";
       if (n_on_lists > nchunks_) { os << "LRU cycle; "; break; }
     }
-  if (n_on_lists != nalloc) os << "LRU holds " << n_on_lists << " but " << nalloc << " allocated; ";
+  if (n_on_lists + ndoomed != nalloc)
+    os << "LRU holds " << n_on_lists << " (+" << ndoomed << " doomed) but " << nalloc << " allocated; ";
   if ((uint64_t)nalloc << kBlockShift != st_.allocated) os << "allocated bytes mismatch; ";
   return os.str();
 }

@@ -3,6 +3,7 @@
 
 #include <fcntl.h>
 #include <signal.h>
+#include <sys/file.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -65,51 +66,52 @@ Status NodeLedger::attach() {
     RT_WARN("node ledger %s unavailable (errno %d): host / CXL budgets are per process", path_.c_str(), errno);
     return Status::IO_ERROR;
   }
+  // Every structural change of the ledger (first initialisation, the reset of
+  // a file nobody uses any more, slot claims and dead-slot reclaims) happens
+  // under an exclusive flock on the file: 8 ranks starting together on a file
+  // left by a crashed job must not interleave "nobody is live" scans with
+  // another rank's reset and claim (a reset after a claim would wipe the
+  // claimer's reservations and let its releases underflow the node counter).
+  // The kernel drops the lock with the descriptor, so a rank that dies inside
+  // never blocks the others. Reservations themselves stay lock-free CAS.
+  while (flock(fd, LOCK_EX) != 0) {
+    if (errno != EINTR) {
+      close(fd);
+      return Status::IO_ERROR;
+    }
+  }
   struct stat st;
   if (fstat(fd, &st) != 0 || ((uint64_t)st.st_size < sizeof(Shared) && ftruncate(fd, sizeof(Shared)) != 0)) {
     close(fd);
     return Status::IO_ERROR;
   }
   void* p = mmap(nullptr, sizeof(Shared), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  close(fd);
-  if (p == MAP_FAILED) return Status::IO_ERROR;
+  if (p == MAP_FAILED) {
+    close(fd);
+    return Status::IO_ERROR;
+  }
   Shared* s = (Shared*)p;
-  // First process: claim the initialisation (magic 0 -> 1), fill in the
-  // budgets, publish kMagic. Everyone else waits for kMagic.
-  uint64_t zero = 0;
-  if (__atomic_compare_exchange_n(&s->magic, &zero, 1ull, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+  // A ledger nobody uses any more (never initialised, a creator that died
+  // mid-way, or every slot free or its process gone) is (re-)initialised:
+  // budgets from this process's configuration, nothing reserved - a file left
+  // behind by an earlier job (or a test's budget) must not constrain this one.
+  bool live = false;
+  if (__atomic_load_n(&s->magic, __ATOMIC_ACQUIRE) == kMagic) {
+    for (uint32_t i = 0; i < kSlots && !live; ++i) {
+      const int32_t pid = __atomic_load_n(&s->slots[i].pid, __ATOMIC_ACQUIRE);
+      live = pid != 0 && (pid < 0 || kill(pid, 0) == 0 || errno != ESRCH);
+    }
+  }
+  // (test hook: widen the scan -> reset window, tests/test_node_ledger.py)
+  if (const char* d = getenv("OGKM_LEDGER_TEST_DELAY_US"))
+    std::this_thread::sleep_for(std::chrono::microseconds(atoi(d)));
+  if (!live) {
+    __atomic_store_n(&s->magic, 1ull, __ATOMIC_RELEASE);  // reserve() waits while this is not kMagic
     s->version = 1;
     s->nnodes = kMaxNodes;
     for (int n = 0; n < kMaxNodes; ++n) {
       s->capacity[n] = node_budget_bytes(n);
-      s->reserved[n] = 0;
-    }
-    __atomic_store_n(&s->magic, kMagic, __ATOMIC_RELEASE);
-  } else {
-    for (int i = 0; __atomic_load_n(&s->magic, __ATOMIC_ACQUIRE) != kMagic; ++i) {
-      if (i > 200000) {  // a creator that died mid-initialisation (~2 s): take over
-        for (int n = 0; n < kMaxNodes; ++n) s->capacity[n] = node_budget_bytes(n);
-        __atomic_store_n(&s->magic, kMagic, __ATOMIC_RELEASE);
-        break;
-      }
-      std::this_thread::sleep_for(std::chrono::microseconds(10));
-    }
-  }
-  // A ledger nobody uses any more (every slot free or its process gone) is
-  // re-initialised: budgets from this process's configuration, nothing
-  // reserved - a file left behind by an earlier job (or a test's budget)
-  // must not constrain this one.
-  sh_ = s;
-  bool live = false;
-  for (uint32_t i = 0; i < kSlots && !live; ++i) {
-    const int32_t pid = __atomic_load_n(&s->slots[i].pid, __ATOMIC_ACQUIRE);
-    live = pid != 0 && (pid < 0 || kill(pid, 0) == 0 || errno != ESRCH);
-  }
-  uint64_t ready = kMagic;
-  if (!live && __atomic_compare_exchange_n(&s->magic, &ready, 1ull, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
-    for (int n = 0; n < kMaxNodes; ++n) {
-      s->capacity[n] = node_budget_bytes(n);
-      s->reserved[n] = 0;
+      __atomic_store_n(&s->reserved[n], 0ull, __ATOMIC_RELEASE);
     }
     for (uint32_t i = 0; i < kSlots; ++i) {
       s->slots[i].pid = 0;
@@ -117,7 +119,7 @@ Status NodeLedger::attach() {
     }
     __atomic_store_n(&s->magic, kMagic, __ATOMIC_RELEASE);
   }
-  while (__atomic_load_n(&s->magic, __ATOMIC_ACQUIRE) != kMagic) std::this_thread::yield();
+  sh_ = s;
   ++epoch_;
   const int32_t me = (int32_t)getpid();
   for (int pass = 0; pass < 2 && !mine_; ++pass) {
@@ -129,14 +131,35 @@ Status NodeLedger::attach() {
         break;
       }
     }
-    if (!mine_) reclaim_dead();
+    if (!mine_) reclaim_dead_locked();
   }
+  lock_fd_ = fd;  // kept for reclaim_dead(); unlocked here
+  flock(fd, LOCK_UN);
   if (!mine_) RT_WARN("node ledger %s: no free process slot (reservations are global only)", path_.c_str());
   return Status::OK;
 }
 
-// Slots of processes that no longer exist: their reservations go back to the nodes.
+// Subtract `b` from a shared counter, never below zero (a release that does not
+// match a reservation - e.g. one made before a reset - must not wrap the
+// counter to ~2^64 and make every later reservation on the node fail).
+static void sub_clamped(uint64_t* c, uint64_t b) {
+  uint64_t cur = __atomic_load_n(c, __ATOMIC_ACQUIRE);
+  while (!__atomic_compare_exchange_n(c, &cur, cur > b ? cur - b : 0ull, true, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+  }
+}
+
 bool NodeLedger::reclaim_dead() {
+  if (lock_fd_ < 0) return reclaim_dead_locked();
+  while (flock(lock_fd_, LOCK_EX) != 0 && errno == EINTR) {
+  }
+  const bool any = reclaim_dead_locked();
+  flock(lock_fd_, LOCK_UN);
+  return any;
+}
+
+// Slots of processes that no longer exist: their reservations go back to the
+// nodes (caller holds the file lock).
+bool NodeLedger::reclaim_dead_locked() {
   bool any = false;
   for (uint32_t i = 0; i < kSlots; ++i) {
     Slot& sl = sh_->slots[i];
@@ -147,7 +170,7 @@ bool NodeLedger::reclaim_dead() {
     if (!__atomic_compare_exchange_n(&sl.pid, &pid, -pid, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) continue;
     for (int n = 0; n < kMaxNodes; ++n) {
       uint64_t b = __atomic_exchange_n(&sl.reserved[n], 0ull, __ATOMIC_ACQ_REL);
-      if (b) __atomic_fetch_sub(&sh_->reserved[n], b, __ATOMIC_ACQ_REL);
+      if (b) sub_clamped(&sh_->reserved[n], b);
     }
     __atomic_store_n(&sl.pid, 0, __ATOMIC_RELEASE);
     any = true;
@@ -158,6 +181,9 @@ bool NodeLedger::reclaim_dead() {
 
 bool NodeLedger::reserve(int node, uint64_t bytes) {
   if (!sh_ || node < 0 || node >= kMaxNodes || !bytes) return true;
+  // (a re-initialisation in progress - only ever of a ledger without live
+  // slots, i.e. this process has none - finishes first)
+  while (__atomic_load_n(&sh_->magic, __ATOMIC_ACQUIRE) != kMagic) std::this_thread::yield();
   for (int attempt = 0; attempt < 2; ++attempt) {
     uint64_t cur = __atomic_load_n(&sh_->reserved[node], __ATOMIC_ACQUIRE);
     const uint64_t cap = sh_->capacity[node];
@@ -183,8 +209,8 @@ bool NodeLedger::reserve(int node, uint64_t bytes) {
 
 void NodeLedger::release(int node, uint64_t bytes) {
   if (!sh_ || node < 0 || node >= kMaxNodes || !bytes) return;
-  __atomic_fetch_sub(&sh_->reserved[node], bytes, __ATOMIC_ACQ_REL);
-  if (mine_) __atomic_fetch_sub(&mine_->reserved[node], bytes, __ATOMIC_ACQ_REL);
+  sub_clamped(&sh_->reserved[node], bytes);
+  if (mine_) sub_clamped(&mine_->reserved[node], bytes);
 }
 
 NodeLedger::NodeView NodeLedger::view(int node) {
@@ -202,13 +228,15 @@ void NodeLedger::detach() {
   if (mine_) {
     for (int n = 0; n < kMaxNodes; ++n) {
       uint64_t b = __atomic_exchange_n(&mine_->reserved[n], 0ull, __ATOMIC_ACQ_REL);
-      if (b) __atomic_fetch_sub(&sh_->reserved[n], b, __ATOMIC_ACQ_REL);
+      if (b) sub_clamped(&sh_->reserved[n], b);
     }
     __atomic_store_n(&mine_->pid, 0, __ATOMIC_RELEASE);
     mine_ = nullptr;
   }
   munmap(sh_, sizeof(Shared));
   sh_ = nullptr;
+  if (lock_fd_ >= 0) close(lock_fd_);
+  lock_fd_ = -1;
 }
 
 }  // namespace ogkm

@@ -502,7 +502,7 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     s.op = !to->loc.is_gpu() ? SqeOp::COPY : (from->fmt == 1 ? SqeOp::DECODE_BF12 : SqeOp::DECODE_ANS);
     s.dst = page_addr(to->arena, to->chunk, 0);
     s.src = page_addr(from->arena, from->chunk, 0);
-    s.bytes = to->loc.is_gpu() && from->fmt == 1 ? (uint64_t)b->npages << kPageShift : from->enc_bytes;
+    s.bytes = from->enc_bytes;  // encoded bytes read (the output is n_values bf16)
     s.n_values = b->npages << (kPageShift - 1);
     s.user_data = b->range->id;
     s.file = __FILE__;
@@ -770,6 +770,7 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
                       b->range->addr() + b->block_offset(), (uint64_t)(r.resident & pages).count() << kPageShift,
                       b->range->id);
         r.resident = r.resident.andnot(pages);
+        b->range->mod_gen.fetch_add(1, std::memory_order_acq_rel);
         if (r.resident.empty()) empty_locs.push_back(r.loc);
       }
     }
@@ -878,6 +879,7 @@ Status Runtime::finish_ctx(Ctx& c, Tracker* out) {
       if (!r.resident.intersects(pages)) continue;
       if (!bad) Tools::get().inc(Counter::Revocations);
       r.resident = r.resident.andnot(pages);
+      iv.b->range->mod_gen.fetch_add(1, std::memory_order_acq_rel);
       if (r.resident.empty()) empty.push_back(r.loc);
     }
     for (auto& l : empty) release_residency_now(iv.b, l);

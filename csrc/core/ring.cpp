@@ -324,7 +324,7 @@ uint64_t Ring::packed_bytes(const Batch& b) {
   uint64_t n = 0;
   for (const Sqe& s : b.ops) {
     if (s.op == SqeOp::WAIT_FENCE) return 0;
-    if (s.op == SqeOp::DECODE_ANS) n += s.bytes;
+    if (s.op == SqeOp::DECODE_ANS || (s.op == SqeOp::DECODE_BF12 && config().bf12_stage)) n += s.bytes;
   }
   return n;
 }
@@ -399,7 +399,11 @@ Status Ring::run_batch(Batch& b) {
     std::vector<DecodeDesc> staged;
   } ps;
   auto launch_decodes = [&](std::vector<DecodeDesc>& dec, int half) {
-    st = be_->decode_ans_blocks(dev_, dec.data(), dec.size(), stream_);
+    // one launch per format present (ANS1 blocks: k_ans_blocks; BF12: k_bf12_decode)
+    std::vector<DecodeDesc> ans, b12;
+    for (const DecodeDesc& d : dec) (d.fmt == 1 ? b12 : ans).push_back(d);
+    if (!ans.empty()) st = be_->decode_ans_blocks(dev_, ans.data(), ans.size(), stream_);
+    if (st == Status::OK && !b12.empty()) st = be_->decode_bf12(dev_, b12.data(), b12.size(), stream_);
     Tools::get().inc(Counter::PackedDecodes, dec.size());
     for (const DecodeDesc& d : dec) batch_dst_.emplace_back(d.dst, 2ull * d.n_values);
     if (st != Status::OK) return;
@@ -550,11 +554,16 @@ Status Ring::run_batch(Batch& b) {
         }
         break;
       case SqeOp::DECODE_BF12:
-        flush_staged();
-        flush_copies();
-        decodes.push_back(DecodeDesc{s.src, s.dst, (uint32_t)(s.bytes / 2)});
-        break;
+        if (!config().bf12_stage || (!stage_ && config().ans_stage_mb <= 0)) {
+          // fused copy + decode: the kernel reads the host copy itself
+          flush_staged();
+          flush_copies();
+          decodes.push_back(DecodeDesc{s.src, s.dst, s.n_values});
+          break;
+        }
+        [[fallthrough]];
       case SqeOp::DECODE_ANS: {
+        const uint32_t fmt = s.op == SqeOp::DECODE_BF12 ? 1 : 0;
         flush_decodes();
         const uint64_t need = (s.bytes + 255) & ~255ull;
         if (!stage_ && st == Status::OK && config().ans_stage_mb > 0) {  // (0: decode from the host copy)
@@ -569,7 +578,7 @@ Status Ring::run_batch(Batch& b) {
           flush_copies();
           if (st == Status::OK) {
             DecodeDesc d{s.src, s.dst, s.n_values};
-            st = be_->decode_ans_blocks(dev_, &d, 1, stream_);
+            st = fmt ? be_->decode_bf12(dev_, &d, 1, stream_) : be_->decode_ans_blocks(dev_, &d, 1, stream_);
             kernels_pending = true;
             Tools::get().inc(Counter::PackedDecodes);
           }
@@ -602,7 +611,7 @@ Status Ring::run_batch(Batch& b) {
         }
         copies.push_back(d);
         copy_dst.push_back(-1);
-        staged.push_back(DecodeDesc{at, s.dst, s.n_values});
+        staged.push_back(DecodeDesc{at, s.dst, s.n_values, fmt});
         stage_off += need;
         break;
       }
@@ -755,7 +764,7 @@ FenceRef Ring::submit_locked() {
           break;
         case SqeOp::DECODE_BF12:
           if (!batch.empty() || !abatch.empty()) flush();
-          dbatch.push_back(DecodeDesc{s.src, s.dst, (uint32_t)(s.bytes / 2)});
+          dbatch.push_back(DecodeDesc{s.src, s.dst, s.n_values});
           break;
         case SqeOp::DECODE_ANS:
           if (!batch.empty() || !dbatch.empty()) flush();

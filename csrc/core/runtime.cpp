@@ -2,6 +2,7 @@
 // CPU/stable-VA mapping maintenance, CXL DMA, quiesce/resume and the
 // residency-map checkpoint format.
 #include "ogkm/runtime.hpp"
+#include "ogkm/unit_stream.hpp"
 #include "ogkm/ledger.hpp"
 #include "ogkm/codec.hpp"
 
@@ -95,6 +96,7 @@ std::vector<int> Runtime::local_devices() const {
 void Runtime::shutdown() {
   std::lock_guard<std::mutex> g(g_rt_m);
   Runtime* rt = g_rt.exchange(nullptr);
+  if (rt) UnitStream::detach_all(rt);  // (streams still alive in Python hold leases of rt)
   delete rt;
 }
 
@@ -491,6 +493,7 @@ Status Runtime::mem_advise(Range* r, uint64_t off, uint64_t len, Advice a, Loc l
             seen |= x->resident;
             if (!dup.empty()) {
               x->resident = x->resident.andnot(dup);
+              b->range->mod_gen.fetch_add(1, std::memory_order_acq_rel);
               Tools::get().inc(Counter::Revocations);
               if (x->resident.empty()) empty.push_back(x->loc);
             }
@@ -1023,6 +1026,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
   if (quiesced_.load()) return Status::BUSY;  // checkpoint in progress
   if (r->type != RangeType::MANAGED) return Status::NOT_SUPPORTED;
   if (bytes == 0) return Status::OK;
+  r->mod_gen.fetch_add(1, std::memory_order_acq_rel);
   if (r->flags & RANGE_COMPRESS_BF16) return write_compressed(r, off, src, bytes, src_dev);
   std::shared_lock<OrderedRWLock> vg(vs_.lock);
   uint64_t pos = off;

@@ -110,8 +110,9 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
     // anything enqueued on it now: no barrier packet (a lease of a unit whose
     // previous readers ran on the consumer's own stream - every resident unit
     // of a decode step).
-    // (the null stream included: a GPU-side wait always names a real stream)
-    if (f->event && f->stream == stream) continue;
+    // Never for the null stream: nullptr names a different stream on each
+    // device, so a fence on GPU0's null stream says nothing about GPU1's.
+    if (f->event && stream && f->stream == stream) continue;
     // Already retired (the flag is only set by whoever polled last): no packet.
     if (f->ring && !f->event && f->ring->completed_seq() >= f->seq) {
       f->done.store(true, std::memory_order_release);

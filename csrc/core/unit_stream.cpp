@@ -1,11 +1,43 @@
 // Native per-unit protocol of a cyclic consumer (see ogkm/unit_stream.hpp).
 #include "ogkm/unit_stream.hpp"
 
+#include <algorithm>
+
 #include "ogkm/arena.hpp"
 #include "ogkm/config.hpp"
 #include "ogkm/runtime.hpp"
 
 namespace ogkm {
+
+// Live streams, for Runtime::shutdown (detach_all).
+static std::mutex g_streams_m;
+static std::vector<UnitStream*> g_streams;
+
+void UnitStream::detach_all(Runtime* rt) {
+  std::lock_guard<std::mutex> g(g_streams_m);
+  for (UnitStream* u : g_streams)
+    if (u->rt_ == rt) u->detach(true);
+}
+
+// at_shutdown: the consumer's stream may be gone already (the runtime drains
+// the device itself), so the leases go back without a stream fence.
+void UnitStream::detach(bool at_shutdown) {
+  if (!rt_) return;
+  rt_->remove_pressure_handler(pressure_id_);
+  std::lock_guard<std::recursive_mutex> g(m_);
+  if (at_shutdown) {
+    hold_on_stream_ = false;
+    hold_stream_ = nullptr;
+  }
+  drop_holds(hold_stream_);
+  for (Lease* l : pending_) (void)rt_->release(l, nullptr);
+  pending_.clear();
+  for (auto& f : ahead_) (void)f->wait();
+  ahead_.clear();
+  inflight_.clear();
+  inflight_bytes_ = 0;
+  rt_ = nullptr;
+}
 
 UnitStream::UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_t window_bytes, bool next_use,
                        uint32_t max_ahead)
@@ -26,14 +58,14 @@ UnitStream::UnitStream(Runtime* rt, int dev, std::vector<Range*> ranges, uint64_
     drop_holds(hold_stream_);
     return any;
   });
+  std::lock_guard<std::mutex> g(g_streams_m);
+  g_streams.push_back(this);
 }
 
 UnitStream::~UnitStream() {
-  rt_->remove_pressure_handler(pressure_id_);
-  std::lock_guard<std::recursive_mutex> g(m_);
-  drop_holds(hold_stream_);
-  for (Lease* l : pending_) (void)rt_->release(l, nullptr);
-  for (auto& f : ahead_) (void)f->wait();
+  std::lock_guard<std::mutex> g(g_streams_m);
+  detach(false);
+  g_streams.erase(std::remove(g_streams.begin(), g_streams.end(), this), g_streams.end());
 }
 
 uint64_t UnitStream::due(uint32_t pos) const {
@@ -43,6 +75,7 @@ uint64_t UnitStream::due(uint32_t pos) const {
 
 void UnitStream::prefetch_window() {
   std::lock_guard<std::recursive_mutex> g(m_);
+  if (!rt_) return;
   const uint32_t n = (uint32_t)ranges_.size();
   const Loc gpu = Loc::gpu(dev_);
   while (inflight_.size() < n) {
@@ -75,6 +108,7 @@ void UnitStream::prefetch_window() {
 Status UnitStream::use(uint32_t pos, void* stream, Lease** out, bool on_stream) {
   if (pos >= ranges_.size()) return Status::INVALID_ARGUMENT;
   std::lock_guard<std::recursive_mutex> g(m_);
+  if (!rt_) return Status::NOT_SUPPORTED;  // detached: the runtime was shut down
   if (drop_requested_.exchange(false)) drop_holds(stream);
   struct Clock {
     uint64_t& acc;
@@ -91,6 +125,13 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out, bool on_stream) 
     // chunks stayed pinned and the stream already waited for them.
     if (hold_arena_ && hold_arena_->evictions() != hold_ev_) {
       drop_holds(stream);  // someone needed HBM meanwhile: back to leases per use
+    } else if (r->mod_gen.load(std::memory_order_acquire) != held_gen_[pos]) {
+      // written or migrated since it was kept: the held copy may be stale or
+      // revoked - hand it back and lease the unit afresh (below)
+      FenceRef f = hold_on_stream_ ? fence_record(rt_->be(), dev_, stream) : nullptr;
+      (void)rt_->release(held_[pos], stream, f);
+      held_[pos] = nullptr;
+      ++st_.hold_drops;
     } else {
       if (next_use_) {
         if ((int64_t)pos <= last_pos_) ++pass_;
@@ -139,11 +180,13 @@ Status UnitStream::use(uint32_t pos, void* stream, Lease** out, bool on_stream) 
 
 Status UnitStream::release(Lease* l, void* stream, bool on_stream) {
   std::lock_guard<std::recursive_mutex> g(m_);
+  if (!rt_) return Status::NOT_SUPPORTED;
   if (!on_stream || l->proc == kCpuProc) return rt_->release(l, nullptr);
   if (hold_ && l->offset == 0 && l->bytes == l->range->size) {
     auto it = pos_of_.find(l->range);
     if (it != pos_of_.end() && it->second < held_.size() && !held_[it->second]) {
       held_[it->second] = l;  // kept until its next use (or until pressure)
+      held_gen_[it->second] = l->range->mod_gen.load(std::memory_order_acquire);
       hold_stream_ = stream;
       hold_on_stream_ = true;
       return Status::OK;
@@ -163,6 +206,7 @@ Status UnitStream::release(Lease* l, void* stream, bool on_stream) {
 
 Status UnitStream::flush_released(void* stream) {
   std::lock_guard<std::recursive_mutex> g(m_);
+  if (!rt_) return Status::NOT_SUPPORTED;
   if (pending_.empty()) return Status::OK;
   FenceRef f = fence_record(rt_->be(), dev_, stream);
   Status st = Status::OK;
@@ -207,7 +251,10 @@ void UnitStream::update_hold(void* stream) {
   hold_ = quiet;
   hold_arena_ = a;
   hold_ev_ = ev;
-  if (hold_ && held_.size() != ranges_.size()) held_.assign(ranges_.size(), nullptr);
+  if (hold_ && held_.size() != ranges_.size()) {
+    held_.assign(ranges_.size(), nullptr);
+    held_gen_.assign(ranges_.size(), 0);
+  }
   pass_ev0_ = ev;
   pass_quiet_ = true;
 }

@@ -46,6 +46,7 @@ struct DecodeDesc {
   uint64_t src;       // encoded block (device-readable host / CXL memory)
   uint64_t dst;       // raw bf16 output (HBM)
   uint32_t n_values;
+  uint32_t fmt = 0;   // staged ring decodes: 0 = ANS1 block, 1 = BF12 block
 };
 
 enum class LinkType : int { NONE = 0, SELF = 1, PCIE = 2, XGMI = 3 };

@@ -87,6 +87,7 @@ namespace ogkm {
   X(pack_min_saving_pct, 8, "a block is kept packed only when its packed form saves at least this share of its bytes") \
   X(pack_threads, 4, "host encoder threads of the packer") \
   X(ans_stage_mb, 128, "per-H2D-ring HBM staging buffer the packed bytes land in before the decode kernel (0: the kernel reads the host copy over PCIe)") \
+  X(bf12_stage, 1, "H2D ring: BF12 blocks are staged into HBM by SDMA and decoded there, as ANS1 blocks are (0: the fused kernel reads the host copy over PCIe - its rate depends on CU-driven host reads)") \
   X(ring_defer_decodes, 1, "H2D ring: packed-block decodes overlap the next batch (two staging halves, deferred publish); 0 = drain after each batch's decodes") \
   X(ring_stage_overlap, 1, "H2D ring: a staging half's copies are issued before the host waits for the previous half's and launches its decode (0 = issue, wait, decode per half)") \
   X(ring_merge_packed_mb, 64, "H2D ring: queued batches of packed-block decodes run as one batch up to this many packed MB (0 = one batch at a time)") \

@@ -14,7 +14,8 @@
 // and the bytes reserved on it, plus one slot per attached process with its
 // own reservations. Host arenas reserve a segment before they populate and pin
 // it and return it when they are destroyed; reservations are lock-free CAS
-// updates on the shared counters. A process that died without releasing is
+// updates on the shared counters (clamped at zero on release); attach's
+// liveness scan, reset and slot claim run under an flock on the file. A process that died without releasing is
 // reclaimed by the next process whose reservation does not fit (its pid no
 // longer exists).
 #pragma once
@@ -66,8 +67,10 @@ class NodeLedger {
   };
 
  private:
-  bool reclaim_dead();
+  bool reclaim_dead();         // takes the file lock
+  bool reclaim_dead_locked();  // caller holds it
   std::mutex m_;
+  int lock_fd_ = -1;  // the ledger file: flock'ed around attach / reclaim
   Shared* sh_ = nullptr;
   Slot* mine_ = nullptr;
   std::string path_;

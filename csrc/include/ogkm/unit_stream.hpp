@@ -64,9 +64,16 @@ class UnitStream {
   }
   void reset_stats() { st_ = Stats{}; }
   uint32_t size() const { return (uint32_t)ranges_.size(); }
+  bool detached() const { return rt_ == nullptr; }
+  // Runtime shutdown: every live stream hands back its holds and pending
+  // leases and forgets the runtime (its own destructor - a Python object
+  // collected later - then touches nothing the runtime owned; its calls fail
+  // with NOT_INITIALIZED).
+  static void detach_all(Runtime* rt);
 
  private:
   uint64_t due(uint32_t pos) const;
+  void detach(bool at_shutdown);
   Runtime* rt_;
   int dev_;
   std::vector<Range*> ranges_;
@@ -85,6 +92,7 @@ class UnitStream {
   void update_hold(void* stream);
   void drop_holds(void* stream);
   std::vector<Lease*> held_;    // per unit: its lease, kept since its last release
+  std::vector<uint64_t> held_gen_;  // per unit: its range's mod_gen when it was kept
   bool hold_ = false;
   bool pass_quiet_ = false;     // this pass: no demand fault, no refused prefetch
   uint64_t pass_ev0_ = ~0ull;   // arena evictions at the pass start

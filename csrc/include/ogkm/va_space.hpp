@@ -200,6 +200,10 @@ class Range {
   // opposite ends of the arena (PlacementSide) so the stream class's turnover
   // does not fragment the keep class's chunks.
   std::atomic<int> spread_cls{-1};
+  // Bumped by every write through the runtime and every revocation of a copy's
+  // pages: a lease kept across uses (UnitStream hold mode) is re-validated
+  // against it instead of re-walking the blocks.
+  std::atomic<uint64_t> mod_gen{0};
   bool destroyed = false;
   OrderedMutex place_lock{LockOrder::RANGE_PLACE};  // GPU extent placement
 

@@ -292,6 +292,11 @@ PYBIND11_MODULE(_ogkm, m) {
     d["nodes"] = nodes;
     return d;
   }, py::arg("max_nodes") = 8);
+  // Raw ledger operations (no runtime needed): the multi-process attach / reserve stress test.
+  m.def("ledger_attach", [] { return NodeLedger::get().attach() == Status::OK; });
+  m.def("ledger_reserve", [](int node, uint64_t bytes) { return NodeLedger::get().reserve(node, bytes); });
+  m.def("ledger_release", [](int node, uint64_t bytes) { NodeLedger::get().release(node, bytes); });
+  m.def("ledger_detach", [] { NodeLedger::get().detach(); });
   // Native per-unit fault / prefetch protocol of a cyclic consumer (TieredLlama, planner off).
   py::class_<UnitStream>(m, "UnitStream")
       .def(py::init([](int dev, const std::vector<uint64_t>& ids, uint64_t window, bool next_use, uint32_t max_ahead) {

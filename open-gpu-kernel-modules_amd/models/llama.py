@@ -99,6 +99,9 @@ CONFIGS = {
     "llama3-405b": LlamaConfig("llama3-405b", 16384, 126, 128, 8, 53248, 128256),
     "tiny": LlamaConfig("tiny", 512, 4, 8, 2, 1536, 4096),
     "small": LlamaConfig("small", 1024, 8, 16, 4, 2816, 8192),
+    # 8 KV heads like the Llama-3 family: tp8 runs one KV head per rank (the
+    # per-rank shape of 70B / 405B tp8), for the 8-rank CPU rehearsal
+    "small-kv8": LlamaConfig("small-kv8", 1024, 16, 16, 8, 2816, 4096),
 }
 
 
@@ -1470,18 +1473,31 @@ def reference_step(cfg: LlamaConfig, model: TieredLlama, tokens: torch.Tensor, p
 
 
 def smoke(device: int = 0) -> dict:
-    """Tiny tiered decode on cuda:0 with the HBM budget below the footprint."""
+    """Tiny tiered decode on cuda:0 with the HBM budget below the footprint, on
+    the headline bench's path (runtime-decided residency - planner off - with
+    rANS-packed weights and KV), checked against the plain fp32 PyTorch
+    reference (``reference_step``) every step: a wrong-logits regression in the
+    default path fails here, not just a path that moves no bytes."""
     if not lib.is_initialized():
         rt.init("hip", host_budget_mb=4096)
     cfg = CONFIGS["small"]
-    m = TieredLlama(cfg, batch=4, context=32, max_new_tokens=8, oversub=2.0, device=device, lookahead=1)
+    m = TieredLlama(cfg, batch=4, context=128, max_new_tokens=8, oversub=2.0, device=device, lookahead=1,
+                    weight_format="ans", kv_format="ans", planner="off")
+    m.keep_logits = True
     tok = torch.randint(0, cfg.vocab, (4,), device=m.tdev)
-    for _ in range(2):
+    max_err = 0.0
+    for _ in range(3):
+        ref = reference_step(cfg, m, tok.cpu(), m.pos).float()
         tok = m.step(tok)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        got = m.last_logits.float().to(ref.device)
+        err = (got - ref).abs().max().item()
+        max_err = max(max_err, err)
+        assert torch.allclose(got, ref, atol=0.05, rtol=0.05), f"smoke logits off the fp32 reference: max err {err}"
+        tok = ref.argmax(-1).to(m.tdev)  # stay on the reference's trajectory
     s = lib.stats()
-    out = {"tokens": tok.tolist(), "evictions": s["evictions"], "bytes_htd": s["bytes_xfer_htd"],
-           "copy_launches": s["copy_kernel_launches"], "plan": m.describe()}
+    out = {"tokens": tok.tolist(), "max_logit_err_vs_fp32": round(max_err, 5), "evictions": s["evictions"],
+           "bytes_htd": s["bytes_xfer_htd"], "plan": m.describe()}
     m.close()
     assert s["bytes_xfer_htd"] > 0, "smoke did not stream any weights"
     return out

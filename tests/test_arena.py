@@ -162,3 +162,21 @@ def test_workingset_protects_refaulted_blocks_under_cyclic_scan(fake_rt):
     assert lru_active == 0 and lru == 64 * MB
     assert 0 < ws_active <= 8                     # 50% of 16 chunks
     assert ws <= 48 * MB, (ws, lru)               # at least 2 of 8 ranges stay resident
+
+
+def test_check_counts_chunks_revoked_under_a_lease(fake_rt):
+    """A GPU copy revoked while a lease still reads it (a CPU write) stays
+    allocated until the lease ends but leaves the LRU lists: the arena's self
+    check accounts for it instead of reporting a spurious mismatch."""
+    lib.init_device(0, 16 * MB)
+    b = fake_rt.malloc_managed(4 * MB, "rv")
+    b.write(torch.ones(4 * MB, dtype=torch.uint8))
+    l = b.acquire(0, fake_rt.READ)
+    l.wait(0)
+    b.set_preferred_location("cpu")
+    b.write(torch.full((4 * MB,), 7, dtype=torch.uint8))  # revokes the leased HBM copy
+    assert lib.arena_check(0, 0) == ""
+    l.release(0)
+    assert lib.arena_check(0, 0) == ""
+    assert int(b.read()[0]) == 7
+    b.free()

@@ -442,26 +442,52 @@ def test_bf12_packed_stream_is_bit_exact(gpu_rt):
     b.free()
 
 
+def _refill_gbps(buf, n: int, reps: int = 3) -> float:
+    """Best-of-`reps` rate (bf16 bytes delivered / s) of a host -> HBM refill of
+    `buf`'s `n` bytes through the H2D ring (acquire of an evicted buffer)."""
+    best = 0.0
+    for _ in range(reps):
+        buf.evict("gpu:0")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        l = buf.acquire(0, rt.READ)
+        l.wait(0)
+        dt = time.perf_counter() - t0
+        l.release()
+        best = max(best, n / dt / 1e9)
+    return best
+
+
 def test_bf12_decode_bandwidth(gpu_rt):
-    """Packed streaming must deliver more bf16 bytes/s than the raw PCIe copy."""
+    """Packed streaming must deliver more bf16 bytes/s than the raw PCIe copy of
+    the same GiB on the same box (a same-process ratio, not an absolute number:
+    round 5's driver box measured 43 GB/s where earlier boxes gave 73 because
+    the fused kernel's CU-driven host reads are box-dependent; BF12 refills now
+    stage through SDMA into HBM and decode there, like ANS1 blocks)."""
     lib.init_device(0, 3 << 30)
     n = 1 << 30
+    data = (torch.randn(n // 2, device="cuda") * 0.02).to(torch.bfloat16)
+    raw = rt.malloc_managed(n, "raw")
+    raw.write(data)
+    raw.set_read_mostly(True)
+    raw_gbps = _refill_gbps(raw, n)
+    raw.free()
     b = rt.malloc_managed(n, "pk", packed_bf16=True)
-    b.write((torch.randn(n // 2, device="cuda") * 0.02).to(torch.bfloat16))
+    b.write(data)
     b.set_read_mostly(True)
-    l = b.acquire(0, rt.READ)
-    l.wait(0)
-    l.release()
-    b.evict("gpu:0")
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    l = b.acquire(0, rt.READ)
-    l.wait(0)
-    dt = time.perf_counter() - t0
-    l.release()
-    gbps = n / dt / 1e9
-    print(f"packed acquire 1 GiB: {gbps:.1f} GB/s of bf16 delivered")
-    assert gbps > 50  # raw acquire of the same GiB measures ~42-47 GB/s on the box
+    s0 = lib.stats()
+    gbps = _refill_gbps(b, n)
+    s1 = lib.stats()
+    rt.configure(bf12_stage=0)  # diagnostics: the fused kernel reading host memory
+    fused = _refill_gbps(b, n, reps=2)
+    rt.configure(bf12_stage=1)
+    print(f"refill 1 GiB: raw {raw_gbps:.1f} GB/s, packed BF12 staged {gbps:.1f}, fused {fused:.1f} GB/s of bf16; "
+          f"gpu numa {lib.device_numa_node(0)} host node {lib.host_node()}; "
+          f"packed decodes {s1['packed_decodes'] - s0['packed_decodes']}")
+    assert s1["packed_decodes"] > s0["packed_decodes"]  # the staged path ran
+    # BF12 moves 0.75x the bytes: the ideal ratio is 1.33; guard at 90% of it
+    # (measured 73.3 vs 57.1 GB/s = 1.28, gpurun_out r6 / profiles/r6_gpu_suite.txt)
+    assert gbps >= 1.2 * raw_gbps, (gbps, raw_gbps, fused)
     b.free()
 
 

@@ -109,3 +109,57 @@ def test_full_node_demotes_evictions_to_the_other_node(tmp_path, monkeypatch):
     finally:
         lib.shutdown()
         lib.config_reset()
+
+
+@pytest.mark.parametrize("round_", range(3))
+def test_concurrent_attach_on_stale_file(tmp_path, round_):
+    """8 processes attach at the same moment to a ledger file a crashed job left
+    behind (a dead pid holding a slot and a reservation). The stale file is
+    reset exactly once - no rank's reservation is wiped by another rank's
+    reset - so while every rank holds its reservations the node counter equals
+    the sum of the slots, and after every rank released it returns to zero
+    (a release never underflows the shared counter)."""
+    ledger = str(tmp_path / "ledger")
+    env = dict(os.environ, OGKM_NODE_LEDGER=ledger, NODE_BUDGET_MB="4096", OMP_NUM_THREADS="1",
+               OGKM_LEDGER_TEST_DELAY_US=str(20000 * round_))  # widen the scan -> reset window
+    worker = os.path.join(HERE, "helpers", "ledger_attach_worker.py")
+    subprocess.run([sys.executable, worker, "--die", str(300 * MB)], env=env, check=True, timeout=120)
+    bar = tmp_path / "bar"
+    bar.mkdir()
+    world, nbytes = 8, 8 * MB
+    procs = [subprocess.Popen([sys.executable, worker, str(bar), str(world), str(nbytes)],
+                              env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in range(world)]
+    import time
+    t0 = time.time()
+    while len([f for f in os.listdir(bar) if f.endswith(".ready")]) < world:
+        assert time.time() - t0 < 240 and all(p.poll() is None for p in procs)
+        time.sleep(0.01)
+    (bar / "go").touch()
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e[-3000:]
+        outs.append(json.loads([l for l in o.splitlines() if l.startswith("{")][-1]))
+    for o in outs:
+        assert all(o["ok"]), o
+        # the dead job's 300 MB is gone (reset), every live rank's 4 x 8 MB counted
+        assert o["view"]["reserved"] == world * 4 * nbytes, o
+        assert o["view"]["mine"] == 4 * nbytes, o
+        assert o["after"]["reserved"] == 0 and o["after"]["mine"] == 0, o
+
+
+def test_unmatched_release_clamps_at_zero(tmp_path, monkeypatch):
+    """A release without a matching reservation (e.g. made before a reset) must
+    not wrap the node counter to ~2^64 and refuse every later reservation."""
+    env = dict(os.environ, OGKM_NODE_LEDGER=str(tmp_path / "l2"), NODE_BUDGET_MB="64")
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from ogkm._native import lib\n"
+            "assert lib.ledger_attach()\n"
+            "assert lib.ledger_reserve(0, 1 << 20)\n"
+            "lib.ledger_release(0, 5 << 20)\n"
+            "v = lib.node_ledger(1)['nodes'][0]\n"
+            "assert v['reserved'] == 0 and v['mine'] == 0, v\n"
+            "assert lib.ledger_reserve(0, 32 << 20)\n"
+            "lib.ledger_detach()\n") % os.path.dirname(HERE)
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=120)

@@ -309,3 +309,27 @@ def test_block_leased_on_gpu_still_packs(fake_rt):
     assert t.equal(data[last:last + 2 * MB])
     assert _gpu_read(b).equal(data)
     b.free()
+
+
+@pytest.mark.parametrize("stage", [1, 0])
+def test_bf12_refill_staged_and_fused_bit_exact(fake_rt, stage):
+    """BF12-packed host copies refill HBM bit-exactly both through SDMA staging
+    + HBM decode (bf12_stage=1, the default) and through the fused kernel that
+    reads the host copy (bf12_stage=0); the staged path moves only encoded bytes."""
+    fake_rt.configure(bf12_stage=stage)
+    lib.init_device(0, 32 * MB)
+    n = 6 * MB + 4096
+    ref = (torch.randn(n // 2) * 0.02).to(torch.bfloat16)
+    ref[:4] = torch.tensor([0.0, float("inf"), float("nan"), -2.5], dtype=torch.bfloat16)
+    b = fake_rt.malloc_managed(n, "pk", packed_bf16=True)
+    b.write(ref)
+    for _ in range(2):
+        b.evict("gpu:0")
+        d0 = lib.stats()["packed_decodes"]
+        with b.acquire(0, fake_rt.READ) as l:
+            l.wait(0)
+            got = l.tensor((n // 2,), torch.bfloat16).clone()  # the HBM copy the decode wrote
+        assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+        if stage:
+            assert lib.stats()["packed_decodes"] > d0
+    b.free()

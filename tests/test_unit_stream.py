@@ -4,6 +4,7 @@ pass with no eviction and no streaming, released units keep their leases until
 their next use; the first eviction somebody else causes ends it."""
 from __future__ import annotations
 
+import pytest
 import torch
 
 from ogkm import rt
@@ -69,3 +70,53 @@ def test_no_hold_under_oversubscription(fake_rt):
     lib.debug_stream_destroy(s)
     for b in bufs:
         b.free()
+
+
+def test_write_to_held_unit_is_not_refused(fake_rt):
+    """Hold mode keeps a lease on every unit between passes; a weight update
+    between decode steps (a CPU write to a held unit) must still go through -
+    the held leases are soft pins, let go on demand - and the next pass sees
+    the new data."""
+    lib.init_device(0, 48 * MB)
+    bufs = _units(4, 8)
+    s = lib.debug_stream_create(0)
+    us = lib.UnitStream(0, [b.id for b in bufs], 16 * MB, True, 2)
+    for _ in range(4):
+        _pass(us, bufs, s)
+    assert us.stats()["held"] >= 4
+    lib.debug_stream_sync(s)
+    bufs[1].write(torch.full((8 * MB,), 42, dtype=torch.uint8))
+    bufs[1].set_preferred_location("cpu")  # a migration away from the held HBM copy
+    bufs[1].prefetch("cpu")
+    assert int(bufs[1].read()[0]) == 42
+    lid, dptr = us.use(1, s)
+    lib.debug_stream_sync(s)
+    t = rt._tensor_from_ptr(dptr, (4096,), torch.uint8, "cpu", 0, bufs[1].id)
+    assert int(t[0]) == 42 and int(t[-1]) == 42
+    us.release(lid, s)
+    lib.debug_stream_sync(s)
+    del us
+    lib.debug_stream_destroy(s)
+    for b in bufs:
+        b.free()
+
+
+def test_shutdown_with_live_unit_stream(fake_rt):
+    """A UnitStream still alive when the runtime shuts down (a model whose
+    construction raised, a caller that never closed it) is detached by the
+    shutdown: its holds go back first, and collecting it later touches nothing
+    of the deleted runtime; its calls then fail cleanly."""
+    lib.init_device(0, 48 * MB)
+    bufs = _units(4, 8)
+    s = lib.debug_stream_create(0)
+    us = lib.UnitStream(0, [b.id for b in bufs], 16 * MB, True, 2)
+    for _ in range(4):
+        _pass(us, bufs, s)
+    assert us.stats()["held"] >= 4
+    lib.debug_stream_sync(s)
+    lib.debug_stream_destroy(s)
+    lib.shutdown()
+    with pytest.raises(Exception):
+        us.use(0, 0)
+    del us  # must not crash (use-after-free of the runtime before the fix)
+    rt.init("fake", fake_devices=2, fake_hbm_mb=64, lock_check=1, host_budget_mb=1024, pack_host_copies=0)
