@@ -164,7 +164,10 @@ const char* counter_name(Counter c) {
                             "decode_reuse_waits",
                             "ring_merged_batches",
                             "victim_search_ns",
-                            "victim_risen_seen"};
+                            "victim_risen_seen",
+                            "seg_packed",
+                            "seg_expansions",
+                            "seg_decodes"};
   static_assert(sizeof(n) / sizeof(n[0]) == (size_t)Counter::NumCounters, "counter names");
   return n[(int)c];
 }

@@ -420,7 +420,21 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     Status st = rt->expand_packed(b, from);
     if (st != Status::OK) return st;
   }
-  if (to->fmt == 2 && !from->fmt) {  // raw pages into a packed copy (a write-back)
+  // A segmented copy as the source: a packed segment is decoded whole, so one
+  // only partly requested (or any, towards a CPU tier) is expanded on the host
+  // first and moves as raw pages.
+  uint32_t seg_dec = 0;  // packed segments decoded into the destination by the ring
+  if (from->fmt == 3 && from->seg) {
+    const uint32_t req = segs_of(pages) & from->seg->packed;
+    const uint32_t part = to->loc.is_gpu() ? (req & ~segs_full(pages)) : req;
+    if (part) {
+      Status st = rt->expand_segments(b, from, part);
+      if (st != Status::OK) return st;
+    }
+    if (from->seg && to->loc.is_gpu()) seg_dec = req & from->seg->packed;
+  }
+  const bool whole_enc = from->fmt == 1 || from->fmt == 2;  // an encoded block moves whole
+  if (to->fmt == 2 && !whole_enc) {  // raw pages into a packed copy (a write-back)
     if (pages == b->valid_pages()) {
       // every page is overwritten (after the chunk's queued readers, below)
       to->fmt = 0;
@@ -430,12 +444,34 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
       if (st != Status::OK) return st;
     }
   }
+  const bool write_back = from->loc.is_gpu() && !to->loc.is_gpu();
+  if (write_back) {
+    // written pages reach the host copy: note its written segments (a
+    // segmented copy expands only those; the untouched ones may pack, below)
+    Status st = rt->note_host_write(b, to, pages, pages);
+    if (st != Status::OK) return st;
+  } else if (to->fmt == 3 && !whole_enc) {
+    Status st = rt->expand_segments(b, to, segs_of(pages), segs_full(pages));
+    if (st != Status::OK) return st;
+  }
   Ring* ring = ring_for(rt, from->loc, to->loc);
   Counter ctr = xfer_counter(from->loc, to->loc);
   // Bytes that actually cross the link (an encoded block moves its encoded size).
-  uint64_t bytes = from->fmt ? from->enc_bytes : (uint64_t)pages.count() << kPageShift;
+  PageMask raw_pages = pages;
+  uint64_t bytes = 0;
+  if (whole_enc) {
+    bytes = from->enc_bytes;
+  } else {
+    for (uint32_t sg = 0; sg < kSegsPerBlock; ++sg)
+      if ((seg_dec >> sg) & 1u) {
+        bytes += from->seg->len[sg];
+        raw_pages = raw_pages.andnot(seg_pages(sg));
+      }
+    bytes += (uint64_t)raw_pages.count() << kPageShift;
+  }
   Tools::get().inc(ctr, bytes);
-  if (from->fmt && to->loc.is_gpu()) Tools::get().inc(Counter::DecodedBytes, (uint64_t)b->npages << kPageShift);
+  if (whole_enc && to->loc.is_gpu()) Tools::get().inc(Counter::DecodedBytes, (uint64_t)b->npages << kPageShift);
+  if (seg_dec) Tools::get().inc(Counter::DecodedBytes, (uint64_t)__builtin_popcount(seg_dec) * kSegBytes);
   if (c.cause == Cause::Prefetch) {
     if (to->loc.is_gpu()) Tools::get().inc(Counter::PrefetchBytesXferHtD, bytes);
     else Tools::get().inc(Counter::PrefetchBytesXferDtH, bytes);
@@ -470,7 +506,7 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     // CPU <-> CPU (host / CXL tiers): synchronous memcpy.
     reuse.wait();
     pend.wait();
-    if (from->fmt) {
+    if (whole_enc) {
       memcpy((void*)page_addr(to->arena, to->chunk, 0), (const void*)page_addr(from->arena, from->chunk, 0),
              from->enc_bytes);
       to->fmt = from->fmt;
@@ -493,7 +529,28 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
     ring->push_wait(f);
   }
-  if (from->fmt) {
+  if (seg_dec) {
+    // Packed segments of a segmented copy: each its own ANS1 chunk, back to
+    // back in the sidecar - the ring stages them with one engine copy (their
+    // staging slots follow each other) and decodes them in one launch.
+    const SegDir& d = *from->seg;
+    for (uint32_t sg = 0; sg < kSegsPerBlock; ++sg) {
+      if (!((seg_dec >> sg) & 1u)) continue;
+      Sqe s;
+      s.op = SqeOp::DECODE_ANS;
+      s.dst = page_addr(to->arena, to->chunk, sg * kSegPages);
+      s.src = (uint64_t)d.arena->chunk_addr((uint32_t)d.chunk) + d.off[sg];
+      s.bytes = d.len[sg];
+      s.n_values = kSegBytes / 2;
+      s.user_data = b->range->id;
+      s.file = __FILE__;
+      s.line = __LINE__;
+      ring->push(std::move(s));
+    }
+    Tools::get().inc(Counter::SegDecodes, (uint64_t)__builtin_popcount(seg_dec));
+    c.chunk_uses.push_back({ring, d.arena, (uint32_t)d.chunk, false});
+  }
+  if (whole_enc) {
     // Encoded source: the whole block decoded into HBM - BF12 by one fused
     // copy+decode kernel, ANS1 packed bytes staged by SDMA and decoded in HBM
     // (Ring DECODE_ANS) - or a verbatim copy of the encoded bytes into another
@@ -512,16 +569,18 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
       to->fmt = from->fmt;
       to->enc_bytes = from->enc_bytes;
     }
-  } else if (pages.runs() >= (uint32_t)std::max<int64_t>(2, config().copy_page_list_min_runs)) {
+  } else if (raw_pages.empty()) {
+    // (every requested page comes from packed segments)
+  } else if (raw_pages.runs() >= (uint32_t)std::max<int64_t>(2, config().copy_page_list_min_runs)) {
     // Fragmented mask: one page-list kernel (LDS-staged) instead of one copy
     // per run - the staged pack of uvm_va_block.c:4278-4326 / 3673-3860.
     Sqe s;
     s.op = SqeOp::PAGE_COPY;
     s.dst = page_addr(to->arena, to->chunk, 0);
     s.src = page_addr(from->arena, from->chunk, 0);
-    s.bytes = (uint64_t)pages.count() << kPageShift;
-    s.idx.reserve(pages.count());
-    pages.for_each_run([&](uint32_t p, uint32_t n) {
+    s.bytes = (uint64_t)raw_pages.count() << kPageShift;
+    s.idx.reserve(raw_pages.count());
+    raw_pages.for_each_run([&](uint32_t p, uint32_t n) {
       for (uint32_t k = 0; k < n; ++k) s.idx.push_back(p + k);
     });
     s.user_data = b->range->id;
@@ -530,7 +589,7 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     ring->push(std::move(s));
     Tools::get().inc(Counter::PageListCopies);
   } else {
-    pages.for_each_run([&](uint32_t p, uint32_t n) {
+    raw_pages.for_each_run([&](uint32_t p, uint32_t n) {
       Sqe s;
       s.op = SqeOp::COPY;
       s.dst = page_addr(to->arena, to->chunk, p);
@@ -555,6 +614,7 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
   c.chunk_uses.push_back({ring, from->arena, (uint32_t)from->chunk, false});
   tools_event(ToolsEventType::Migration, c.cause, from->loc, to->loc, to->loc.is_gpu() ? to->loc.id : kCpuProc,
               b->range->addr() + b->block_offset(), bytes, b->range->id, t0, 0, ring->pushed_seq());
+  if (write_back) rt->seg_pack_enqueue(b);  // (the job waits until the write-back has landed)
   return Status::OK;
 }
 
@@ -622,6 +682,7 @@ static void drop_residency(Runtime::Ctx& c, Block* b, const Loc& l) {
       r->arena->free_when_unpinned((uint32_t)r->chunk);  // (a lease may still read it)
     }
   }
+  Runtime::get()->free_sidecar(b, r);
   b->drop(l);
 }
 
@@ -684,7 +745,13 @@ Status Runtime::make_resident(Ctx& c, Block* b, const PageMask& pages_in, Loc ds
   // packed host copy's pages: expand it in place first. (A migration / prefetch
   // / eviction between CPU tiers keeps the packed form.)
   const bool cpu_use = !dst.is_gpu() && (cause == Cause::User || cause == Cause::Coherence);
-  if (to->fmt && (!missing.empty() || (to->fmt == 2 && cpu_use))) {
+  if (to->fmt == 3) {
+    // segmented: raw pages landing expand only their segments (copy_pages); a
+    // CPU consumer needs the segments of its pages raw (the CPU view maps the
+    // raw segments)
+    if (cpu_use) st = expand_segments(b, to, segs_of(pages));
+    if (st != Status::OK) return st;
+  } else if (to->fmt && (!missing.empty() || (to->fmt == 2 && cpu_use))) {
     st = expand_packed(b, to);
     if (st != Status::OK) return st;
   }
@@ -822,6 +889,7 @@ static void release_residency_now(Block* b, const Loc& l) {
     // when that lease ends, never under it.
     r->arena->free_when_unpinned((uint32_t)r->chunk);
   }
+  Runtime::get()->free_sidecar(b, r);
   b->drop(l);
 }
 
@@ -977,6 +1045,10 @@ Status Runtime::evict_one(Ctx& c, ChunkArena* a, uint32_t i, bool* detached) {
     // each step: packing it would only buy expansions)
     b->clean_evictions = only_here.empty() ? b->clean_evictions + 1 : 0;
     pack_enqueue(b);
+    if (only_here.empty() && b->seg_written) {  // written segments cooled down: they may pack too
+      b->seg_written = 0;
+      seg_pack_enqueue(b);
+    }
     if (is_local(from.id)) devs_[from.id]->spread.on_evict(b->range->id);
     // Users of the stable VA's mapping of this chunk (see Block::stable_users).
     if (b->range->dev_va && b->stable_chunk.load() == (int64_t)i) {
@@ -1789,7 +1861,9 @@ Status Runtime::acquire(Range* r, uint64_t off, uint64_t len, int proc, Access a
             std::lock_guard<OrderedMutex> g(b->lock);
             int64_t hint = first >= 0 ? first + k : -1;
             Residency* x = b->find(dec[k].dst);
-            if (x && x->fmt) st = expand_packed(b, x);  // read in place: raw pages
+            // read in place: raw pages (a segmented copy: the leased pages' segments)
+            if (x && x->fmt == 3) st = expand_segments(b, x, segs_of(pages_of(b0 + k)));
+            else if (x && x->fmt) st = expand_packed(b, x);
             if (st != Status::OK) break;
             if (!x) {
               st = populate(c, b, dec[k].dst, hint, &x);

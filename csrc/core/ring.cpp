@@ -585,7 +585,7 @@ Status Ring::run_batch(Batch& b) {
           break;
         }
         const uint64_t half = stage_bytes_ / 2;
-        if (stage_off + need > half || staged.size() >= 64) flush_staged();
+        if (stage_off + need > half || staged.size() >= 256) flush_staged();
         if (!half_ready) {  // the decode that read this half last must be done before the engines refill it
           if (stage_used_[stage_half_] && st == Status::OK) {
             set_phase(Phase::STREAM_DRAIN, b.last);
@@ -596,6 +596,15 @@ Status Ring::run_batch(Batch& b) {
           half_ready = true;
         }
         const uint64_t at = (uint64_t)stage_ + stage_half_ * half + stage_off;
+        staged.push_back(DecodeDesc{at, s.dst, s.n_values, fmt});
+        stage_off += need;
+        // Packed segments of one block are back to back in its sidecar and land
+        // back to back here: one engine copy for all of them.
+        if (!copies.empty() && copy_dst.back() == -1 && copies.back().src + copies.back().bytes == s.src &&
+            copies.back().dst + copies.back().bytes == at) {
+          copies.back().bytes += need;
+          break;
+        }
         CopyDesc d{at, s.src, need};
         // Packed blocks are ~1.3 MB copies that never coalesce: spread them over
         // several full-rate engines so one engine's per-copy setup overlaps
@@ -611,8 +620,6 @@ Status Ring::run_batch(Batch& b) {
         }
         copies.push_back(d);
         copy_dst.push_back(-1);
-        staged.push_back(DecodeDesc{at, s.dst, s.n_values, fmt});
-        stage_off += need;
         break;
       }
       case SqeOp::WAIT_FENCE:

@@ -5,6 +5,7 @@
 #include "ogkm/unit_stream.hpp"
 #include "ogkm/ledger.hpp"
 #include "ogkm/codec.hpp"
+#include "ogkm/torch_alloc.hpp"
 
 #include <sys/mman.h>
 #include <unistd.h>
@@ -139,6 +140,7 @@ Runtime::~Runtime() {
 // ------------------------------------------------------------------ tiers
 Status Runtime::init_device(int d, uint64_t budget) {
   if (!is_local(d)) return Status::INVALID_ARGUMENT;
+  torch_alloc_trim(d);  // freed torch memory the pluggable allocator still caches goes back first
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
   if (devs_[d]->hbm && devs_[d]->hbm->outstanding_bytes()) return Status::BUSY;
   devs_[d]->hbm_live.store(nullptr);
@@ -408,8 +410,10 @@ Status Runtime::free_range(Range* r) {
         b->in_stale_list = false;
       }
     }
-    for (auto& x : b->res)
+    for (auto& x : b->res) {
       if (x.chunk >= 0) x.arena->free((uint32_t)x.chunk, 1);
+      if (x.seg && x.seg->chunk >= 0) x.seg->arena->free((uint32_t)x.seg->chunk, 1);
+    }
     b->res.clear();
     Tools::get().bus().notify(PerfEventData{PerfEvent::BLOCK_DESTROY, r->id, b->index});
   }
@@ -553,12 +557,12 @@ void Runtime::cpu_map_block(Block* b) {
   if (!r->cpu_view) return;
   uint8_t* win = r->cpu_view + b->block_offset();
   // (a packed copy holds no raw pages: never mapped - a CPU access faults and
-  // expands it)
+  // expands it; a segmented one maps its raw segments' pages only)
   Residency* h = nullptr;
-  if (Residency* x = b->find(cpu_loc()); x && x->fmt == 0) h = x;
+  if (Residency* x = b->find(cpu_loc()); x && (x->fmt == 0 || x->fmt == 3)) h = x;
   if (!h)
     for (auto& x : b->res)
-      if (!x.loc.is_gpu() && x.chunk >= 0 && x.fmt == 0) {
+      if (!x.loc.is_gpu() && x.chunk >= 0 && (x.fmt == 0 || x.fmt == 3)) {
         h = &x;
         break;
       }
@@ -590,9 +594,13 @@ void Runtime::cpu_map_block(Block* b) {
   for (auto& x : b->res)
     if (&x != h) others |= x.resident;
   PageMask rw, ro;
+  PageMask usable = h->resident;
+  if (h->fmt == 3 && h->seg)
+    for (uint32_t sg = 0; sg < kSegsPerBlock; ++sg)
+      if ((h->seg->packed >> sg) & 1u) usable = usable.andnot(seg_pages(sg));
   if (!pending) {
-    rw = h->resident.andnot(others) & b->valid_pages();
-    ro = (h->resident & others) & b->valid_pages();
+    rw = usable.andnot(others) & b->valid_pages();
+    ro = (usable & others) & b->valid_pages();
   }
   if (rw == b->cpu_rw && ro == b->cpu_ro) return;
   // Apply protections run by run.
@@ -1057,6 +1065,7 @@ Status Runtime::write(Range* r, uint64_t off, const void* src, uint64_t bytes, i
         st = populate(c, b, stage, -1, &to);
         if (st == Status::OK) stage = to->loc;  // (a full node's data rests on the next one: populate)
         if (st == Status::OK && to->fmt == 2) st = expand_packed(b, to);  // raw pages land in it
+        if (st == Status::OK && to->fmt == 3) st = note_host_write(b, to, pages, full);  // only their segments
         if (st == Status::OK) {
           // Old data only for partially covered pages.
           PageMask partial = pages.andnot(full);
@@ -1147,7 +1156,9 @@ Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_
     Residency* encoded = nullptr;
     HostArena* scratch_arena = nullptr;
     for (auto& x : b->res)
-      if (x.fmt) encoded = &x;
+      if (x.fmt && x.resident.intersects(PageMask::range((uint32_t)(lo >> kPageShift),
+                                                         (uint32_t)((end - pos + kPageSize - 1) >> kPageShift))))
+        encoded = &x;
     if (encoded) {
       scratch_arena = host_arena(Tier::HOST, host_node_);
       uint32_t tmp;
@@ -1157,8 +1168,21 @@ Status Runtime::read(Range* r, uint64_t off, void* dst, uint64_t bytes, int dst_
       decoded.arena = scratch_arena;
       decoded.chunk = tmp;
       decoded.fmt = 0;
-      if (!block_decode(encoded->fmt, (const uint8_t*)encoded->arena->chunk_addr((uint32_t)encoded->chunk),
-                        (uint16_t*)scratch_arena->chunk_addr(tmp), b->npages << (kPageShift - 1))) {
+      decoded.seg.reset();
+      bool ok = true;
+      if (encoded->fmt == 3) {  // raw segments as they are, packed ones decoded
+        uint8_t* o = (uint8_t*)scratch_arena->chunk_addr(tmp);
+        memcpy(o, (const void*)encoded->arena->chunk_addr((uint32_t)encoded->chunk), (size_t)b->npages << kPageShift);
+        const SegDir& d = *encoded->seg;
+        for (uint32_t sg = 0; sg < kSegsPerBlock && ok; ++sg)
+          if ((d.packed >> sg) & 1u)
+            ok = ans_decode((const uint8_t*)d.arena->chunk_addr((uint32_t)d.chunk) + d.off[sg],
+                            (uint16_t*)(o + (uint64_t)sg * kSegBytes), kSegBytes / 2);
+      } else {
+        ok = block_decode(encoded->fmt, (const uint8_t*)encoded->arena->chunk_addr((uint32_t)encoded->chunk),
+                          (uint16_t*)scratch_arena->chunk_addr(tmp), b->npages << (kPageShift - 1));
+      }
+      if (!ok) {
         scratch_arena->free(tmp, 1);
         return Status::IO_ERROR;
       }

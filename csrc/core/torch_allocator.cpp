@@ -9,11 +9,19 @@
 //
 // Stream ordering (the caching-allocator contract torch expects, and what the
 // reference's PMM gets from its trackers, uvm_pmm_gpu.c free-with-tracker):
-//   * free(ptr, stream) records a fence on the freeing stream; the memory is
-//     reusable at once, but every later user waits for that fence GPU-side;
-//   * alloc(size, stream) makes the allocating stream wait (hipStreamWaitEvent,
-//     no host stall) for the fences of the slot / chunks it hands out - the
-//     previous tensor's kernels and any ring copy that last touched the chunk.
+//   * free(ptr, stream) tags the slot / extent with the freeing stream and
+//     records nothing: reuse by an allocation on the SAME stream needs no
+//     fence (stream order already puts the old tensor's kernels first), which
+//     is the common case of a decode step (hundreds of frees per step);
+//   * a reuse from another stream, or the memory going back to the runtime's
+//     arena (where ring copies and other users may take it), records the fence
+//     on the freeing stream at that moment (later than the free: conservative,
+//     never early) and the allocating stream waits for it GPU-side
+//     (hipStreamWaitEvent, no host stall) - with any ring copy that last
+//     touched the chunk.
+//   * freed extents (> 1 MB) stay in a small per-device cache for same-size
+//     reuse; the runtime's pressure handler hands them back to the arena when
+//     it needs chunks.
 //   * chunks are taken from the arena already pinned and returned while still
 //     pinned (one critical section each): an allocator chunk is never an
 //     eviction victim, and never visible to reserve() between two steps.
@@ -56,7 +64,15 @@ constexpr int kNumClasses = 12;  // 512 B .. 1 MB
 
 struct Slot {
   uint32_t index;
-  Tracker fence;  // uses of the previous tensor in this slot
+  Tracker fence;  // uses of the previous tensor in this slot (recorded lazily, see settle)
+  void* free_stream = nullptr;  // the stream that freed it (fence not yet recorded)
+  bool tagged = false;
+};
+
+// A freed extent kept for same-size reuse (DevAlloc::extents).
+struct ExtentFree {
+  uint32_t first, n;
+  void* free_stream;
 };
 
 struct Slab {
@@ -75,6 +91,10 @@ struct DevAlloc {
     uint64_t size;
   };
   std::unordered_map<uint64_t, Entry> live;
+  std::vector<ExtentFree> extents;  // freed extents, oldest first (torch_alloc_extent_cache_mb)
+  uint64_t extent_bytes = 0, extent_hits = 0, lazy_fences = 0;
+  uint64_t pressure_id = 0;
+  bool pressure_registered = false;
   struct Managed {
     Range* r;
     Lease* lease;      // nullptr while parked (no holds)
@@ -133,6 +153,11 @@ struct DevAlloc {
 
 std::mutex g_m;
 std::vector<std::unique_ptr<DevAlloc>> g_devs;
+thread_local int t_in_alloc = 0;  // this thread holds a DevAlloc lock (pressure handler re-entry)
+struct InAlloc {
+  InAlloc() { ++t_in_alloc; }
+  ~InAlloc() { --t_in_alloc; }
+};
 
 DevAlloc* dev_alloc(int d) {
   std::lock_guard<std::mutex> g(g_m);
@@ -146,6 +171,68 @@ int class_of(uint64_t size) {
   for (int i = 0; i < kNumClasses; ++i, c <<= 1)
     if (size <= c) return i;
   return -1;
+}
+
+// A tagged slot's fence, recorded now on the stream that freed it (later than
+// the free itself: it covers the old tensor's kernels and possibly more).
+void settle(Runtime* rt, DevAlloc* da, int device, Slot& s) {
+  if (!s.tagged) return;
+  s.tagged = false;
+  if (FenceRef f = fence_record(rt->be(), device, s.free_stream)) s.fence.add(f);
+  da->lazy_fences++;
+}
+
+// An extent leaves the cache for the arena: its reuse fence is recorded on the
+// stream that freed it, then the (still pinned) chunks are freed.
+void extent_to_arena(Runtime* rt, DevAlloc* da, ChunkArena* a, int device, const ExtentFree& e) {
+  FenceRef f = fence_record(rt->be(), device, e.free_stream);
+  da->lazy_fences++;
+  for (uint32_t i = 0; i < e.n; ++i)
+    if (f) a->add_reuse_fence(e.first + i, f);
+  a->free(e.first, e.n);
+}
+
+bool flush_extents(Runtime* rt, DevAlloc* da, ChunkArena* a, int device) {
+  if (da->extents.empty()) return false;
+  for (const ExtentFree& e : da->extents) extent_to_arena(rt, da, a, device, e);
+  da->extents.clear();
+  da->extent_bytes = 0;
+  return true;
+}
+
+// An empty slab goes back to the arena: one fence per stream that freed a slot
+// in it (recorded now), the chunk's reuse fences.
+void slab_to_arena(Runtime* rt, DevAlloc* da, ChunkArena* a, int device, std::vector<Slab>& slabs, size_t i) {
+  std::vector<std::pair<void*, FenceRef>> per_stream;
+  for (auto& s : slabs[i].free_slots) {
+    if (s.tagged) {
+      FenceRef fr;
+      for (auto& ps : per_stream)
+        if (ps.first == s.free_stream) fr = ps.second;
+      if (!fr) {
+        fr = fence_record(rt->be(), device, s.free_stream);
+        da->lazy_fences++;
+        per_stream.emplace_back(s.free_stream, fr);
+      }
+      if (fr) s.fence.add(fr);
+      s.tagged = false;
+    }
+    for (auto& x : s.fence.fences()) a->add_reuse_fence(slabs[i].chunk, x);
+  }
+  a->free(slabs[i].chunk, 1);
+  slabs.erase(slabs.begin() + (ptrdiff_t)i);
+}
+
+// Cached extents and empty slabs back to the arena (pressure, re-init).
+bool trim_locked(Runtime* rt, DevAlloc* da, ChunkArena* a, int device) {
+  bool any = flush_extents(rt, da, a, device);
+  for (auto& slabs : da->slabs)
+    for (size_t i = slabs.size(); i-- > 0;)
+      if (slabs[i].used == 0) {
+        slab_to_arena(rt, da, a, device, slabs, i);
+        any = true;
+      }
+  return any;
 }
 
 // n pinned chunks from the arena (evicting cold managed data if needed).
@@ -280,6 +367,7 @@ void* torch_alloc(size_t size, int device, void* stream) {
   if (size == 0) size = 1;
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);
+  InAlloc in_alloc;
   da->last_error.clear();
   if (!da->deferred.empty()) reap_deferred(rt, da);
   void* p = torch_alloc_locked(rt, a, da, size, device, stream);
@@ -308,11 +396,14 @@ static void* torch_alloc_locked(Runtime* rt, ChunkArena* a, DevAlloc* da, size_t
   if (cls >= 0) {
     uint64_t csz = kMinClass << cls;
     Slab* s = nullptr;
-    // A slot whose previous tensor is done beats one still in flight.
-    for (int pass = 0; pass < 2 && !s; ++pass)
+    // A slot freed on this very stream (no fence at all) beats one whose
+    // previous tensor is done, which beats one still in flight.
+    for (int pass = 0; pass < 3 && !s; ++pass)
       for (auto& x : da->slabs[cls]) {
         if (x.free_slots.empty()) continue;
-        if (pass == 0 && !x.free_slots.back().fence.query()) continue;
+        const Slot& b = x.free_slots.back();
+        if (pass == 0 && !(b.tagged && b.free_stream == stream)) continue;
+        if (pass == 1 && (b.tagged || !const_cast<Tracker&>(b.fence).query())) continue;
         s = &x;
         break;
       }
@@ -330,17 +421,41 @@ static void* torch_alloc_locked(Runtime* rt, ChunkArena* a, DevAlloc* da, size_t
     Slot slot = std::move(s->free_slots.back());
     s->free_slots.pop_back();
     s->used++;
+    if (slot.tagged && slot.free_stream != stream) settle(rt, da, device, slot);
     order_after(rt, da, slot.fence, stream);
     addr = a->chunk_addr(s->chunk) + (uint64_t)slot.index * csz;
     da->live[addr] = DevAlloc::Entry{cls, s->chunk, 0, csz};
     da->allocated += csz;
   } else {
     uint32_t n = (uint32_t)((size + kBlockSize - 1) >> kBlockShift);
-    uint32_t first;
-    if (!take_chunks(rt, a, n, &first)) return nullptr;
-    Tracker t;
-    for (uint32_t i = 0; i < n; ++i) t.merge(a->reuse_fence(first + i));
-    order_after(rt, da, t, stream);
+    uint32_t first = 0;
+    bool reused = false;
+    // a cached extent of this size: freed on this stream first (no fence), newest first
+    for (int pass = 0; pass < 2 && !reused; ++pass)
+      for (size_t i = da->extents.size(); i-- > 0;) {
+        const ExtentFree e = da->extents[i];
+        if (e.n != n || (pass == 0 && e.free_stream != stream)) continue;
+        da->extents.erase(da->extents.begin() + (ptrdiff_t)i);
+        da->extent_bytes -= (uint64_t)n << kBlockShift;
+        da->extent_hits++;
+        first = e.first;
+        if (e.free_stream != stream) {
+          Tracker t;
+          t.add(fence_record(rt->be(), device, e.free_stream));
+          da->lazy_fences++;
+          order_after(rt, da, t, stream);
+        }
+        reused = true;
+        break;
+      }
+    if (!reused) {
+      if (!take_chunks(rt, a, n, &first)) {
+        if (!trim_locked(rt, da, a, device) || !take_chunks(rt, a, n, &first)) return nullptr;
+      }
+      Tracker t;
+      for (uint32_t i = 0; i < n; ++i) t.merge(a->reuse_fence(first + i));
+      order_after(rt, da, t, stream);
+    }
     addr = a->chunk_addr(first);
     da->live[addr] = DevAlloc::Entry{-1, first, n, (uint64_t)n << kBlockShift};
     da->allocated += (uint64_t)n << kBlockShift;
@@ -356,9 +471,8 @@ void torch_free(void* p, int device, void* stream) {
   if (!rt || !p || !rt->is_local(device)) return;
   ChunkArena* a = rt->arena_for(Loc::gpu(device));
   DevAlloc* da = dev_alloc(device);
-  // The freeing stream's queued work may still use the memory.
-  FenceRef f = fence_record(rt->be(), device, stream);
   std::unique_lock<std::mutex> g(da->m);
+  InAlloc in_alloc;
   auto mt = da->managed.find((uint64_t)p);
   if (mt != da->managed.end() && mt->second.prefetching) {
     // the worker is placing it right now: let that finish before the range goes
@@ -375,6 +489,8 @@ void torch_free(void* p, int device, void* stream) {
     da->managed_bytes -= m.size;
     if (m.lease) rt->release(m.lease, stream);
     rt->set_dead(m.r, true);  // evicting it now copies nothing out; off-GPU copies are dropped
+    // The freeing stream's queued work may still use the memory.
+    FenceRef f = fence_record(rt->be(), device, stream);
     Tracker t;
     if (f) t.add(f);
     const uint64_t cap = (uint64_t)std::max<int64_t>(0, config().torch_alloc_cache_mb) << 20;
@@ -398,23 +514,41 @@ void torch_free(void* p, int device, void* stream) {
   da->live.erase(it);
   da->allocated -= e.size;
   if (e.cls < 0) {
-    for (uint32_t i = 0; i < e.n; ++i)
-      if (f) a->add_reuse_fence(e.chunk + i, f);
-    a->free(e.chunk, e.n);  // still pinned: free() drops the pin atomically
+    // kept for same-size reuse (no fence yet: the freeing stream's order is
+    // the fence for its own next allocation), the oldest go back to the arena
+    const uint64_t cap = (uint64_t)std::max<int64_t>(0, config().torch_alloc_extent_cache_mb) << 20;
+    da->extents.push_back(ExtentFree{e.chunk, e.n, stream});
+    da->extent_bytes += (uint64_t)e.n << kBlockShift;
+    while (da->extent_bytes > cap && !da->extents.empty()) {
+      extent_to_arena(rt, da, a, device, da->extents.front());  // still pinned: free() drops the pin
+      da->extent_bytes -= (uint64_t)da->extents.front().n << kBlockShift;
+      da->extents.erase(da->extents.begin());
+    }
+    if (!da->pressure_registered) {
+      // the runtime needs chunks (nothing else evictable): the cached extents go back
+      da->pressure_registered = true;
+      da->pressure_id = rt->add_pressure_handler(device, [rt, da, a, device] {
+        if (t_in_alloc) return false;  // the allocator itself is the one asking (it flushes)
+        std::unique_lock<std::mutex> pg(da->m, std::try_to_lock);
+        if (!pg.owns_lock()) return false;
+        return trim_locked(rt, da, a, device);
+      });
+    }
     return;
   }
   auto& slabs = da->slabs[e.cls];
   for (size_t i = 0; i < slabs.size(); ++i) {
     if (slabs[i].chunk != e.chunk) continue;
     uint64_t csz = kMinClass << e.cls;
-    Slot slot{(uint32_t)(((uint64_t)p - a->chunk_addr(e.chunk)) / csz), Tracker{}};
-    if (f) slot.fence.add(f);
+    Slot slot{(uint32_t)(((uint64_t)p - a->chunk_addr(e.chunk)) / csz), Tracker{}, stream, true};
     slabs[i].free_slots.push_back(std::move(slot));
     if (--slabs[i].used == 0) {
-      for (auto& s : slabs[i].free_slots)
-        for (auto& x : s.fence.fences()) a->add_reuse_fence(e.chunk, x);
-      a->free(e.chunk, 1);
-      slabs.erase(slabs.begin() + i);
+      // an empty slab stays for the next allocations of its class (up to
+      // torch_alloc_empty_slabs of them); the others go back to the arena
+      uint32_t empty = 0;
+      for (auto& x : slabs)
+        if (x.used == 0) ++empty;
+      if ((int64_t)empty > std::max<int64_t>(0, config().torch_alloc_empty_slabs)) slab_to_arena(rt, da, a, device, slabs, i);
     }
     return;
   }
@@ -423,10 +557,25 @@ void torch_free(void* p, int device, void* stream) {
 // Runtime teardown: forget every slab / live entry (their fences reference
 // the backend being destroyed). Tensors still alive after shutdown dangle, as
 // any device memory does once its context is gone.
+void torch_alloc_trim(int device) {
+  Runtime* rt = Runtime::get();
+  if (!rt || !rt->is_local(device)) return;
+  ChunkArena* a = rt->arena_for(Loc::gpu(device));
+  if (!a) return;
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  InAlloc in_alloc;
+  trim_locked(rt, da, a, device);
+}
+
 void torch_alloc_reset() {
   std::lock_guard<std::mutex> g(g_m);
+  Runtime* rt = Runtime::get();
   for (auto& d : g_devs)
-    if (d) d->stop_worker();
+    if (d) {
+      d->stop_worker();
+      if (d->pressure_registered && rt) rt->remove_pressure_handler(d->pressure_id);
+    }
   g_devs.clear();
 }
 
@@ -666,6 +815,7 @@ static bool prefetch_one(Runtime* rt, Range* r, uint64_t size, int device, uint6
 // placed is marked so that a concurrent free waits for it.
 static void prefetch_worker(DevAlloc* da, int device) {
   std::unique_lock<std::mutex> g(da->m);
+  InAlloc in_alloc;
   for (;;) {
     da->pq_cv.wait(g, [&] { return da->stop || !da->pq.empty(); });
     if (da->stop) return;
@@ -705,6 +855,7 @@ size_t torch_prefetch(const std::vector<std::pair<uint64_t, uint64_t>>& ptrs, in
   if (!rt || !rt->is_local(device)) return 0;
   DevAlloc* da = dev_alloc(device);
   std::unique_lock<std::mutex> g(da->m);
+  InAlloc in_alloc;
   size_t n = 0;
   const bool async = config().torch_async_prefetch != 0;
   for (auto& pw : ptrs) {
@@ -733,6 +884,7 @@ size_t torch_prefetch(const std::vector<std::pair<uint64_t, uint64_t>>& ptrs, in
 void torch_prefetch_wait(int device) {
   DevAlloc* da = dev_alloc(device);
   std::unique_lock<std::mutex> g(da->m);
+  InAlloc in_alloc;
   da->pf_done_cv.wait(g, [&] { return da->pq.empty() && da->pf_done + da->pf_skipped >= da->pf_queued; });
 }
 
@@ -787,13 +939,16 @@ void torch_managed_stats(int device, uint64_t* active, uint64_t* parked, uint64_
   *unparks = da->unparks;
 }
 
-void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits) {
+void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits,
+                       uint64_t* lazy_fences, uint64_t* extent_hits) {
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);
   *allocated = da->allocated;
   *peak = da->peak;
   *nallocs = da->nallocs;
   *stream_waits = da->stream_waits;
+  if (lazy_fences) *lazy_fences = da->lazy_fences;
+  if (extent_hits) *extent_hits = da->extent_hits;
 }
 
 }  // namespace ogkm

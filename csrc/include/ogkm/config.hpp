@@ -74,6 +74,8 @@ namespace ogkm {
   X(torch_persistent_ops, 128, "transparent mode: a managed tensor held again this many ops after its first hold is long-lived (keys the op-trace prefetcher)") \
   X(evict_clean_first, 0, "HBM LRU: GPU-preferred data with a valid copy elsewhere (clean) is evicted before data only in HBM (dirty: a copy-out plus a refill). Off: on the stock-torch managed 8B it protected every activation and thrashed the weights (193 -> 47 tok/s)") \
   X(torch_async_prefetch, 0, "transparent mode: op-trace prefetches (their evictions, stable-VA remaps and translation flushes) run on a per-GPU worker thread instead of the dispatching thread (measured slower on the stock 8B: 117 vs 197 tok/s - lock contention with the dispatching thread; 0 = inline)") \
+  X(torch_alloc_empty_slabs, 2, "pluggable allocator: empty small-size slabs kept per size class for reuse (the rest go back to the HBM arena)") \
+  X(torch_alloc_extent_cache_mb, 1024, "pluggable allocator: freed extents (> 1 MB) kept for same-size reuse on the freeing stream without a fence; handed back to the arena beyond this or under pressure") \
   X(torch_alloc_cache_mb, 256, "pluggable allocator: freed managed ranges kept (by size) for reuse at the same stable VA - no VA reserve / remap / translation flush per activation (0 = off)") \
   X(torch_alloc_managed_min_mb, 0, "pluggable allocator: allocations >= this many MB are evictable stable-VA managed ranges (0 = off; needs hbm_provider=1)") \
   X(host_node, -1, "NUMA node for the host tier (-1 = NUMA node of the first local GPU)")             \
@@ -85,6 +87,8 @@ namespace ogkm {
   X(pack_host_copies, 1, "keep lossless ANS1-packed host / CXL copies of read-mostly managed blocks (H2D moves the packed bytes; the ring decodes them in HBM)") \
   X(pack_auto_clean_evictions, 2, "a block whose HBM copy was evicted this many times without a copy-out counts as read-mostly and gets packed (0 = only SET_READ_MOSTLY blocks)") \
   X(pack_min_saving_pct, 8, "a block is kept packed only when its packed form saves at least this share of its bytes") \
+  X(pack_segments, 1, "segmented packed host copies (64 KB ANS1 segments, fmt 3) for blocks that are written: a write-back expands only the segments it touches, the rest stay packed (0 = whole blocks only)") \
+  X(pack_seg_min, 4, "a written block's host copy is segment-packed when at least this many of its 64 KB segments were untouched by its latest write-back") \
   X(pack_threads, 4, "host encoder threads of the packer") \
   X(ans_stage_mb, 128, "per-H2D-ring HBM staging buffer the packed bytes land in before the decode kernel (0: the kernel reads the host copy over PCIe)") \
   X(bf12_stage, 1, "H2D ring: BF12 blocks are staged into HBM by SDMA and decoded there, as ANS1 blocks are (0: the fused kernel reads the host copy over PCIe - its rate depends on CU-driven host reads)") \

@@ -208,6 +208,9 @@ enum class Counter : int {
   RingMergedBatches,   // packed-decode batches the H2D ring ran merged into the batch before (Ring::worker)
   VictimSearchNs,      // host time in next-use victim searches (ChunkArena::next_victims_locked)
   VictimRisenSeen,     // re-hinted chunks those searches re-ranked (summed over calls)
+  SegPacked,           // 64 KB segments of written blocks' host copies packed (fmt 3, Runtime::pack_segments)
+  SegExpansions,       // packed segments decoded back to raw pages (a write-back touched them)
+  SegDecodes,          // packed segments decoded into HBM by the H2D ring
   NumCounters
 };
 const char* counter_name(Counter c);

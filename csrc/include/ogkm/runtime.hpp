@@ -339,9 +339,21 @@ class Runtime {
   // ANS1-packed host / CXL copy; the H2D ring moves and decodes the packed bytes.
   Status expand_packed(Block* b, Residency* r);  // back to raw pages (block lock held)
   void pack_enqueue(Block* b);                   // a packing candidate (block lock held)
+  // Segmented packed copies (fmt 3, SegDir): decode packed segments `segs`
+  // into the raw chunk (`overwrite`: segments whose every page is about to be
+  // written - no decode, only the bit), and free the sidecar once nothing
+  // rests packed (block lock held).
+  Status expand_segments(Block* b, Residency* r, uint32_t segs, uint32_t overwrite = 0);
+  // A write of `pages` into host copy r (`full`: the pages written entirely):
+  // the written segments are noted (and a fmt 3 copy expands them); the
+  // untouched ones become segment-packing candidates (block lock held).
+  Status note_host_write(Block* b, Residency* r, const PageMask& pages, const PageMask& full);
+  void seg_pack_enqueue(Block* b);
+  void free_sidecar(Block* b, Residency* r);     // fmt 3 -> drop the sidecar (after its readers)
   bool pack_wait(uint64_t timeout_ms);           // true once nothing is queued or being packed
   struct PackStats {
     uint64_t queued = 0, busy = 0, threads = 0, packed_blocks = 0, packed_bytes = 0, raw_bytes = 0;
+    uint64_t seg_blocks = 0, seg_packed = 0, seg_raw = 0;  // fmt 3 copies, their packed / raw segments
   };
   PackStats pack_stats();
   void stop_packer();
@@ -445,9 +457,11 @@ class Runtime {
   struct PackJob {
     uint64_t range = 0, block = 0;
     uint32_t tries = 0;
+    bool seg = false;  // segment packing (pack_segments) instead of a whole-block pack
   };
   void pack_worker();
   bool pack_block(uint64_t range_id, uint64_t bi, uint16_t* raw, uint8_t* enc);
+  bool pack_segments(uint64_t range_id, uint64_t bi, uint16_t* raw, uint8_t* enc);
   std::mutex pack_m_;
   std::condition_variable pack_cv_, pack_idle_cv_;
   std::deque<PackJob> pack_q_;

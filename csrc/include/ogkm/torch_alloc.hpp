@@ -22,7 +22,10 @@ struct TorchOperand {
   std::vector<std::pair<uint64_t, uint64_t>> written;
 };
 
-void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits);
+// Cached extents / empty slabs back to the HBM arena (before an arena re-init).
+void torch_alloc_trim(int device);
+void torch_alloc_stats(int device, uint64_t* allocated, uint64_t* peak, uint64_t* nallocs, uint64_t* stream_waits,
+                       uint64_t* lazy_fences = nullptr, uint64_t* extent_hits = nullptr);
 void* torch_alloc(size_t size, int device, void* stream);
 void torch_free(void* p, int device, void* stream);
 Status torch_park(void* p, int device, void* stream);

@@ -67,6 +67,49 @@ struct AccessCounterState {
   bool promote[kMaxGpus + 1] = {false};
 };
 
+// Segmented packed host copy (Residency::fmt 3): the block's 2 MB cut into
+// 32 segments of 64 KB (16 pages). Segments that are not being written rest
+// packed - each its own ANS1 chunk, laid out back to back in a sidecar chunk of
+// the same arena - while written segments stay raw at their natural offsets in
+// the residency's own chunk. A write-back of a few pages expands (decodes)
+// only the segments it touches; a refill moves the packed segments' bytes
+// (ONE staging copy: they are contiguous) plus the raw segments' pages. The
+// reference tracks residency per 4 KB page inside each 2 MB block
+// (uvm_va_block.h:104-112) and moves per-page runs through staging
+// (uvm_va_block.c:3673-3760); this keeps its packed form per 64 KB.
+constexpr uint32_t kSegPages = 16;
+constexpr uint32_t kSegsPerBlock = kPagesPerBlock / kSegPages;  // 32
+constexpr uint32_t kSegBytes = kSegPages << kPageShift;        // 64 KB
+struct SegDir {
+  ChunkArena* arena = nullptr;
+  int64_t chunk = -1;           // the sidecar chunk holding the packed segments
+  uint32_t packed = 0;          // bit s: segment s rests packed (its raw pages are stale)
+  uint32_t used = 0;            // sidecar bytes in use (256-B aligned appends)
+  uint32_t off[kSegsPerBlock] = {0};
+  uint32_t len[kSegsPerBlock] = {0};
+  uint32_t packed_bytes() const {
+    uint32_t n = 0;
+    for (uint32_t s = 0; s < kSegsPerBlock; ++s)
+      if ((packed >> s) & 1u) n += len[s];
+    return n;
+  }
+};
+// Pages of segment s / the segments a page mask touches.
+inline PageMask seg_pages(uint32_t s) { return PageMask::range(s * kSegPages, kSegPages); }
+inline uint32_t segs_of(const PageMask& m) {
+  uint32_t r = 0;
+  for (uint32_t s = 0; s < kSegsPerBlock; ++s)
+    if (m.count_range(s * kSegPages, kSegPages)) r |= 1u << s;
+  return r;
+}
+// Segments every page of which is in m.
+inline uint32_t segs_full(const PageMask& m) {
+  uint32_t r = 0;
+  for (uint32_t s = 0; s < kSegsPerBlock; ++s)
+    if (m.count_range(s * kSegPages, kSegPages) == kSegPages) r |= 1u << s;
+  return r;
+}
+
 struct Residency {
   int slot = -1;             // Loc::slot()
   Loc loc{};
@@ -77,8 +120,11 @@ struct Residency {
   // 2 ANS1-packed block (a packed host / CXL copy of any managed block,
   // Runtime::pack_block; lossless, whole block, never written in place -
   // expanded back to raw pages before any write or CPU mapping).
+  // 3: segmented packed host copy (SegDir above): raw segments in `chunk`,
+  // packed ones in `seg->chunk`.
   uint8_t fmt = 0;
-  uint32_t enc_bytes = 0;    // encoded size when fmt != 0
+  uint32_t enc_bytes = 0;    // encoded size when fmt 1 / 2
+  std::shared_ptr<SegDir> seg;  // fmt 3
 };
 
 class Block {
@@ -125,6 +171,12 @@ class Block {
   // evicted without a copy-out (read-mostly detection).
   bool pack_queued = false;
   bool pack_skip = false;
+  // Segments written by the latest write-back into the host copy (fmt 0 / 3):
+  // the others are candidates for segment packing; seg_gen counts such writes
+  // (a segment pack in flight that sees it move starts over).
+  uint32_t seg_written = 0;
+  uint64_t seg_gen = 0;
+  bool seg_pack_queued = false;
   uint32_t clean_evictions = 0;
   uint32_t gpu_evictions = 0;  // times an HBM copy of this block was evicted (refault detection)
   uint64_t gpu_evicted_at = 0; // the HBM arena's eviction count when it last was (refault distance)

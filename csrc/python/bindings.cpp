@@ -273,6 +273,13 @@ PYBIND11_MODULE(_ogkm, m) {
     return rt()->resident_bytes(r, make_loc(tier, loc), off, len);
   }, py::arg("id"), py::arg("tier"), py::arg("loc"), py::arg("off") = 0, py::arg("len") = ~0ull);
   m.def("hint_next_use", [](uint64_t id, uint64_t when) { rt()->hint_next_use(range(id), when); });
+  // Page-granular write invalidation (what the transparent mode's op holds do
+  // for the byte intervals an op writes): the other copies of those pages go.
+  m.def("invalidate_others", [](uint64_t id, const std::vector<std::pair<uint64_t, uint64_t>>& bytes, int gpu) {
+    Range* r = range(id);
+    py::gil_scoped_release nogil;
+    check(rt()->invalidate_others(r, bytes, gpu), "invalidate_others");
+  });
   m.def("node_ledger", [](int max_nodes) {
     NodeLedger& L = NodeLedger::get();
     py::dict d;
@@ -365,6 +372,9 @@ PYBIND11_MODULE(_ogkm, m) {
     d["packed_blocks"] = st.packed_blocks;
     d["packed_bytes"] = st.packed_bytes;
     d["raw_bytes"] = st.raw_bytes;
+    d["seg_blocks"] = st.seg_blocks;
+    d["seg_packed"] = st.seg_packed;
+    d["seg_raw"] = st.seg_raw;
     return d;
   });
   m.def("spread_class", [](int dev, uint64_t id) { return rt()->spread_class(dev, id); });
@@ -1371,9 +1381,13 @@ PYBIND11_MODULE(_ogkm, m) {
     d["unparks"] = nu;
     return d;
   });
+  m.def("torch_alloc_trim", [](int dev) {  // cached free memory back to the arena (torch.cuda.empty_cache)
+    py::gil_scoped_release nogil;
+    torch_alloc_trim(dev);
+  });
   m.def("torch_alloc_stats", [](int dev) {
-    uint64_t a, p, n, w;
-    torch_alloc_stats(dev, &a, &p, &n, &w);
-    return py::make_tuple(a, p, n, w);
+    uint64_t a, p, n, w, lf, eh;
+    torch_alloc_stats(dev, &a, &p, &n, &w, &lf, &eh);
+    return py::make_tuple(a, p, n, w, lf, eh);
   });
 }

@@ -49,8 +49,14 @@ def enabled() -> bool:
     return _enabled
 
 
+def empty_cache(device: int = 0) -> None:
+    """Hand the freed memory the allocator caches for reuse (extents, empty
+    slabs) back to the runtime's HBM arena - torch.cuda.empty_cache()'s role."""
+    lib.torch_alloc_trim(device)
+
+
 def stats(device: int = 0) -> dict:
-    a, p, n, w = lib.torch_alloc_stats(device)
+    a, p, n, w = lib.torch_alloc_stats(device)[:4]
     return {"allocated": a, "peak": p, "allocs": n, "stream_waits": w}
 
 

@@ -22,6 +22,7 @@ def test_alloc_free_leak_check(fake_rt):
     assert st["pinned"] == 16 * MB  # allocator chunks are pinned
     for p in ptrs:
         lib.torch_free(p, 0)
+    lib.torch_alloc_trim(0)  # freed extents are cached for reuse until trimmed
     st = lib.arena_stats(0, 0)
     assert st["allocated"] == 0, "leak"
     assert lib.arena_check(0, 0) == ""
@@ -34,6 +35,7 @@ def test_small_allocations_share_chunks(fake_rt):
     assert lib.arena_stats(0, 0)["allocated"] == 2 * MB  # one slab chunk for the 4 KB class
     for p in ps:
         lib.torch_free(p, 0)
+    lib.torch_alloc_trim(0)  # (an empty slab stays cached until trimmed)
     assert lib.arena_stats(0, 0)["allocated"] == 0
 
 

@@ -420,6 +420,42 @@ def test_allocator_same_stream_reuse_needs_no_wait(gpu_rt):
     lib.torch_free(q, 0, s1.cuda_stream)
 
 
+def test_allocator_small_slots_lazy_fences(gpu_rt):
+    """Slab slots (<= 1 MB): a free records no event; reuse on the freeing
+    stream records none either (stream order suffices), reuse from another
+    stream records the fence then - on the freeing stream, so the new owner
+    still runs after the old owner's late kernel."""
+    n = 256 << 10
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    st0 = lib.torch_alloc_stats(0)
+    ptrs = [lib.torch_alloc(n, 0, s1.cuda_stream) for _ in range(8)]  # one 2 MB slab
+    for p in ptrs:
+        lib.torch_free(p, 0, s1.cuda_stream)  # (the empty slab stays cached)
+    again = [lib.torch_alloc(n, 0, s1.cuda_stream) for _ in range(8)]
+    assert sorted(again) == sorted(ptrs)
+    st1 = lib.torch_alloc_stats(0)
+    assert st1[4] == st0[4] and st1[3] == st0[3], (st0, st1)  # no fence, no wait
+    # cross-stream: the old owner is still queued behind a sleep on s1
+    p = again[0]
+    old = rt._tensor_from_ptr(p, (n // 4,), torch.int32, "cuda", 0)
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(200_000_000)
+        old.fill_(1)
+    lib.torch_free(p, 0, s1.cuda_stream)
+    q = lib.torch_alloc(n, 0, s2.cuda_stream)
+    assert q == p
+    new = rt._tensor_from_ptr(q, (n // 4,), torch.int32, "cuda", 0)
+    with torch.cuda.stream(s2):
+        new.fill_(2)
+    torch.cuda.synchronize()
+    assert bool((new == 2).all())
+    st2 = lib.torch_alloc_stats(0)
+    assert st2[4] == st1[4] + 1 and st2[3] >= st1[3] + 1, (st1, st2)
+    lib.torch_free(q, 0, s2.cuda_stream)
+    for x in again[1:]:
+        lib.torch_free(x, 0, s1.cuda_stream)
+
+
 def test_bf12_packed_stream_is_bit_exact(gpu_rt):
     """Fused H2D copy + BF12 decode kernel reproduces every bf16 bit pattern."""
     n = 5 * (1 << 20) + 4096  # 2.5 blocks, partial last block

@@ -333,3 +333,92 @@ def test_bf12_refill_staged_and_fused_bit_exact(fake_rt, stage):
         if stage:
             assert lib.stats()["packed_decodes"] > d0
     b.free()
+
+
+def _kv_step(b, data, pos):
+    """One decode step of a KV-cache-like buffer, as the transparent mode runs
+    it: the buffer leased on the GPU (a read duplicate of its host copy), ONE
+    256 B entry written per 256 KB row, the written byte intervals revoking the
+    other copies of just those pages (op-hold write invalidation), then evicted
+    (only the written pages go back to the host copy)."""
+    l = b.acquire(0, rt.READ)
+    l.wait(0)
+    t = l.tensor((b.size,), torch.uint8)
+    assert t.equal(data)
+    val = pos % 250 + 1
+    spans = []
+    for row in range(b.size // (256 << 10)):
+        off = row * (256 << 10) + pos * 256
+        t[off:off + 256] = val
+        data[off:off + 256] = val
+        spans.append((off, off + 256))
+    lib.invalidate_others(b.id, spans, 0)
+    l.release(0)
+    b.evict("gpu:0")
+    assert lib.pack_wait(30000)
+
+
+def test_written_block_host_copy_packs_by_segment(fake_rt):
+    """Page-granular packed residency for data written every step (a KV cache:
+    one entry per row per step). The write-back marks the 64 KB segments it
+    touched; the block's other segments pack (fmt 3: each segment its own ANS1
+    chunk in a sidecar, written segments raw at their natural offsets). A
+    refill decodes the packed segments and copies the raw ones; later writes
+    into the same segments expand nothing, a write into a packed segment
+    expands only that segment - and every read is bit-exact."""
+    rt.configure(pack_host_copies=1, pack_threads=2)
+    b = rt.malloc_managed(4 * MB, "kv")  # 2 blocks x 8 rows of 256 KB (4 segments per row)
+    data = _weights(b.size, 21)
+    b.write(data)
+    b.set_read_mostly(True)
+    _kv_step(b, data, 0)
+    st = lib.pack_stats()
+    assert st["seg_blocks"] == 2 and st["seg_packed"] == 2 * 24 and st["seg_raw"] == 2 * 8, st
+    s0 = lib.stats()
+    assert _gpu_read(b).equal(data)  # packed segments decoded, raw ones copied
+    s1 = lib.stats()
+    assert s1["seg_decodes"] - s0["seg_decodes"] == 48
+    htd = s1["bytes_xfer_htd"] - s0["bytes_xfer_htd"]
+    assert htd < 0.85 * b.size, htd  # 8 raw of 32 segments + ~0.68 of the 24 packed ones
+    b.evict("gpu:0")
+    e0 = lib.stats()["seg_expansions"]
+    for pos in (1, 2, 3):  # the same (raw) segments: nothing expands, nothing re-packs
+        _kv_step(b, data, pos)
+    assert lib.stats()["seg_expansions"] == e0
+    assert lib.pack_stats()["seg_packed"] == 48
+    assert b.read().equal(data)
+    # position 256 lies in each row's next segment, which rests packed: the
+    # write-back decodes exactly those 16 segments; the cooled ones pack
+    _kv_step(b, data, 256)
+    assert lib.stats()["seg_expansions"] - e0 == 16
+    assert lib.pack_stats()["seg_packed"] == 48
+    assert b.read().equal(data)
+    assert _gpu_read(b).equal(data)
+    b.free()
+
+
+def test_segmented_copy_cpu_access_and_runtime_write(fake_rt):
+    """A runtime write into a packed segment expands that segment only; a CPU
+    store through the CPU view faults (the view maps raw segments only) and
+    the fault service - whole-block granular - expands the copy; all stay
+    bit-exact through GPU refills."""
+    rt.configure(pack_host_copies=1, pack_threads=1)
+    b = rt.malloc_managed(2 * MB, "kv1")
+    data = _weights(b.size, 22)
+    b.write(data)
+    b.set_read_mostly(True)
+    _kv_step(b, data, 0)
+    assert lib.pack_stats()["seg_packed"] == 24
+    patch = torch.full((100,), 5, dtype=torch.uint8)
+    b.write(patch, 70 * 1024)  # segment 1 (packed): expanded, then written
+    data[70 * 1024:70 * 1024 + 100] = 5
+    assert lib.pack_stats()["seg_packed"] == 23
+    assert _gpu_read(b).equal(data)
+    b.evict("gpu:0")
+    v = b.cpu_view()
+    v[3 * 65536 + 9] = 77  # CPU view store into packed segment 3
+    data[3 * 65536 + 9] = 77
+    assert lib.pack_stats()["seg_blocks"] == 0
+    assert b.read().equal(data)
+    assert _gpu_read(b).equal(data)
+    b.free()

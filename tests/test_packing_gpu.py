@@ -99,3 +99,54 @@ def test_gpu_write_after_packing_round_trips(gpu_rt):
     assert torch.equal(l.tensor((b.size,), torch.uint8), data.cuda())
     l.release()
     b.free()
+
+
+@pytest.mark.parametrize("engine", [3, 0], ids=["sdma_staging", "kernel_direct"])
+def test_segmented_kv_refill_bit_exact(gpu_rt, engine):
+    """A KV-cache-like buffer written every step (one 256 B entry per 256 KB
+    row, page-granular write invalidation as the transparent mode's op holds
+    do): its host copy rests segment-packed (fmt 3) - 24 of every block's 32
+    segments as ANS1 chunks, the written ones raw - and refills through the
+    ring decode the packed segments (k_ans_blocks, one staging copy per block)
+    and copy the raw ones, bit-exact every step, including the step whose
+    writes move into packed segments."""
+    if engine != rt.get_config("copy_engine"):
+        lib.shutdown()
+        rt.init("hip", lock_check=1, host_budget_mb=16384, hbm_budget={0: 2 << 30}, copy_engine=engine)
+    rt.configure(pack_host_copies=1, pack_threads=4)
+    size = 32 * MB
+    b = rt.malloc_managed(size, "kv")
+    data = _weights(size, 9).cuda()
+    b.write(data)
+    b.set_read_mostly(True)
+    rows = size // (256 << 10)
+    for step, pos in enumerate((0, 1, 2, 256, 257)):
+        l = b.acquire(0, rt.READ)
+        l.wait()
+        t = l.tensor((size,), torch.uint8)
+        assert torch.equal(t, data), (step, pos)
+        spans = []
+        val = pos % 250 + 1
+        for row in range(rows):
+            off = row * (256 << 10) + pos * 256
+            t[off:off + 256] = val
+            data[off:off + 256] = val
+            spans.append((off, off + 256))
+        torch.cuda.synchronize()
+        lib.invalidate_others(b.id, spans, 0)
+        l.release()
+        b.evict("gpu:0")
+        assert lib.pack_wait(60000)
+        if step == 0:
+            st = lib.pack_stats()
+            assert st["seg_blocks"] == size // (2 * MB) and st["seg_packed"] == 24 * (size // (2 * MB)), st
+    s0 = lib.stats()
+    l = b.acquire(0, rt.READ)
+    l.wait()
+    assert torch.equal(l.tensor((size,), torch.uint8), data)
+    l.release()
+    s1 = lib.stats()
+    assert s1["seg_decodes"] - s0["seg_decodes"] == 24 * (size // (2 * MB))
+    assert s1["bytes_xfer_htd"] - s0["bytes_xfer_htd"] < 0.85 * size
+    assert torch.equal(b.read().cuda(), data)
+    b.free()
