@@ -372,7 +372,9 @@ def run_torch_managed(a) -> None:
                 "faulted_ops": mode.faulted_ops, "prefetches": mode.prefetches, "init_s": round(init_s, 1),
                 "pack": dict(lib.pack_stats(), wait_s=round(pack_s, 1), drained=packed_all,
                              decodes_per_step=s["packed_decodes"] // max(1, a.steps),
-                             expansions=s["pack_expansions"]),
+                             expansions=s["pack_expansions"],
+                             seg_decodes_per_step=s["seg_decodes"] // max(1, a.steps),
+                             seg_expansions=s["seg_expansions"]),
                 "trace_len": len(mode._trace), "hinted_ops": mode.hinted_ops, "trace_misses": mode.trace_misses,
                 "allocs_per_step": (al1["allocs"] - al0["allocs"]) // max(1, a.steps), "alloc_peak_gb":
                 round(al1["peak"] / 1e9, 2), "managed_min_mb": int(os.environ.get("OGKM_MANAGED_MIN_MB", "1")),
@@ -400,9 +402,10 @@ def _block_census(top: int = 8) -> dict:
                 break
             tiers = [e["tier"] for e in ri["resident_on"]]
             packed = any(e.get("encoded_bytes") for e in ri["resident_on"] if e["tier"] != "gpu")
+            seg = any(e.get("packed_segments") for e in ri["resident_on"] if e["tier"] != "gpu")
             gpu = "gpu" in tiers
             host = any(t != "gpu" for t in tiers)
-            key = ("gpu" if gpu else "nogpu") + ("+packed" if packed else "+raw" if host else "")
+            key = ("gpu" if gpu else "nogpu") + ("+segpacked" if seg else "+packed" if packed else "+raw" if host else "")
             kinds[key] += 1
             raw_out += (not gpu) and host and not packed
         if raw_out:

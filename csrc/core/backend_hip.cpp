@@ -700,6 +700,31 @@ class HipBackend : public Backend {
   }
 
   Status decode_ans_blocks(int, const DecodeDesc* d, size_t n, void* s) override {
+    // Single-segment chunks (segmented host copies): one wave each (k_ans_segs).
+    std::vector<DecodeDesc> blocks;
+    KAnsSegs sg;
+    uint32_t ns = 0;
+    for (size_t i = 0; i < n; ++i) {
+      if (d[i].n_values != kAnsSegValues) {
+        blocks.push_back(d[i]);
+        continue;
+      }
+      sg.src[ns] = d[i].src;
+      sg.dst[ns] = d[i].dst;
+      if (++ns == (uint32_t)kAnsInlineSegs) {
+        HIPCHK(launch_ans_segs(sg, ns, (hipStream_t)s, decode_err()));
+        launches_++;
+        ns = 0;
+      }
+    }
+    if (ns) {
+      HIPCHK(launch_ans_segs(sg, ns, (hipStream_t)s, decode_err()));
+      launches_++;
+    }
+    if (blocks.size() != n) {
+      d = blocks.data();
+      n = blocks.size();
+    }
     for (size_t base = 0; base < n; base += kAnsInlineBlocks) {
       const size_t cnt = std::min<size_t>(n - base, kAnsInlineBlocks);
       KAnsBlocks b;

@@ -531,22 +531,29 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
   }
   if (seg_dec) {
     // Packed segments of a segmented copy: each its own ANS1 chunk, back to
-    // back in the sidecar - the ring stages them with one engine copy (their
-    // staging slots follow each other) and decodes them in one launch.
+    // back in the sidecar - ONE ring op for the block: one staging copy of the
+    // span holding them, one decode descriptor per segment.
     const SegDir& d = *from->seg;
-    for (uint32_t sg = 0; sg < kSegsPerBlock; ++sg) {
-      if (!((seg_dec >> sg) & 1u)) continue;
-      Sqe s;
-      s.op = SqeOp::DECODE_ANS;
-      s.dst = page_addr(to->arena, to->chunk, sg * kSegPages);
-      s.src = (uint64_t)d.arena->chunk_addr((uint32_t)d.chunk) + d.off[sg];
-      s.bytes = d.len[sg];
-      s.n_values = kSegBytes / 2;
-      s.user_data = b->range->id;
-      s.file = __FILE__;
-      s.line = __LINE__;
-      ring->push(std::move(s));
-    }
+    uint32_t lo = ~0u, hi = 0;
+    for (uint32_t sg = 0; sg < kSegsPerBlock; ++sg)
+      if ((seg_dec >> sg) & 1u) {
+        lo = std::min(lo, d.off[sg]);
+        hi = std::max(hi, d.off[sg] + d.len[sg]);
+      }
+    Sqe s;
+    s.op = SqeOp::DECODE_SEGS;
+    s.dst = page_addr(to->arena, to->chunk, 0);
+    s.src = (uint64_t)d.arena->chunk_addr((uint32_t)d.chunk) + lo;
+    s.bytes = hi - lo;
+    for (uint32_t sg = 0; sg < kSegsPerBlock; ++sg)
+      if ((seg_dec >> sg) & 1u) {
+        s.idx.push_back(sg | (d.len[sg] << 5));
+        s.idx.push_back(d.off[sg] - lo);
+      }
+    s.user_data = b->range->id;
+    s.file = __FILE__;
+    s.line = __LINE__;
+    ring->push(std::move(s));
     Tools::get().inc(Counter::SegDecodes, (uint64_t)__builtin_popcount(seg_dec));
     c.chunk_uses.push_back({ring, d.arena, (uint32_t)d.chunk, false});
   }

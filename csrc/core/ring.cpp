@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <thread>
 
+#include "ogkm/codec.hpp"
 #include "ogkm/config.hpp"
 #include "ogkm/events.hpp"
 #include "ogkm/runtime.hpp"
@@ -324,7 +325,8 @@ uint64_t Ring::packed_bytes(const Batch& b) {
   uint64_t n = 0;
   for (const Sqe& s : b.ops) {
     if (s.op == SqeOp::WAIT_FENCE) return 0;
-    if (s.op == SqeOp::DECODE_ANS || (s.op == SqeOp::DECODE_BF12 && config().bf12_stage)) n += s.bytes;
+    if (s.op == SqeOp::DECODE_ANS || s.op == SqeOp::DECODE_SEGS || (s.op == SqeOp::DECODE_BF12 && config().bf12_stage))
+      n += s.bytes;
   }
   return n;
 }
@@ -562,8 +564,10 @@ Status Ring::run_batch(Batch& b) {
           break;
         }
         [[fallthrough]];
+      case SqeOp::DECODE_SEGS:
       case SqeOp::DECODE_ANS: {
         const uint32_t fmt = s.op == SqeOp::DECODE_BF12 ? 1 : 0;
+        const bool segs = s.op == SqeOp::DECODE_SEGS;
         flush_decodes();
         const uint64_t need = (s.bytes + 255) & ~255ull;
         if (!stage_ && st == Status::OK && config().ans_stage_mb > 0) {  // (0: decode from the host copy)
@@ -577,15 +581,24 @@ Status Ring::run_batch(Batch& b) {
           flush_staged();
           flush_copies();
           if (st == Status::OK) {
-            DecodeDesc d{s.src, s.dst, s.n_values};
-            st = fmt ? be_->decode_bf12(dev_, &d, 1, stream_) : be_->decode_ans_blocks(dev_, &d, 1, stream_);
+            std::vector<DecodeDesc> dd;
+            if (segs) {
+              for (size_t i = 0; i + 1 < s.idx.size(); i += 2)
+                dd.push_back(DecodeDesc{s.src + s.idx[i + 1], s.dst + (uint64_t)(s.idx[i] & 31u) * (64u << 10),
+                                        kAnsSegValues});
+            } else {
+              dd.push_back(DecodeDesc{s.src, s.dst, s.n_values});
+            }
+            st = fmt ? be_->decode_bf12(dev_, dd.data(), dd.size(), stream_)
+                     : be_->decode_ans_blocks(dev_, dd.data(), dd.size(), stream_);
             kernels_pending = true;
-            Tools::get().inc(Counter::PackedDecodes);
+            Tools::get().inc(Counter::PackedDecodes, dd.size());
           }
           break;
         }
         const uint64_t half = stage_bytes_ / 2;
-        if (stage_off + need > half || staged.size() >= 256) flush_staged();
+        const size_t ndesc = segs ? s.idx.size() / 2 : 1;
+        if (stage_off + need > half || staged.size() + ndesc > 256) flush_staged();
         if (!half_ready) {  // the decode that read this half last must be done before the engines refill it
           if (stage_used_[stage_half_] && st == Status::OK) {
             set_phase(Phase::STREAM_DRAIN, b.last);
@@ -596,7 +609,13 @@ Status Ring::run_batch(Batch& b) {
           half_ready = true;
         }
         const uint64_t at = (uint64_t)stage_ + stage_half_ * half + stage_off;
-        staged.push_back(DecodeDesc{at, s.dst, s.n_values, fmt});
+        if (segs) {
+          for (size_t i = 0; i + 1 < s.idx.size(); i += 2)
+            staged.push_back(DecodeDesc{at + s.idx[i + 1], s.dst + (uint64_t)(s.idx[i] & 31u) * (64u << 10),
+                                        kAnsSegValues, 0});
+        } else {
+          staged.push_back(DecodeDesc{at, s.dst, s.n_values, fmt});
+        }
         stage_off += need;
         // Packed segments of one block are back to back in its sidecar and land
         // back to back here: one engine copy for all of them.
@@ -703,8 +722,8 @@ FenceRef Ring::submit_locked() {
   // can only delay a copy that did not need to wait. No wait can depend on a
   // copy of this submission (its fence does not exist until the end).
   auto copy_like = [](SqeOp op) {
-    return op == SqeOp::COPY || op == SqeOp::DECODE_BF12 || op == SqeOp::DECODE_ANS || op == SqeOp::WAIT_FENCE ||
-           op == SqeOp::NOP;
+    return op == SqeOp::COPY || op == SqeOp::DECODE_BF12 || op == SqeOp::DECODE_ANS || op == SqeOp::DECODE_SEGS ||
+           op == SqeOp::WAIT_FENCE || op == SqeOp::NOP;
   };
   for (auto it = sq_.begin(); it != sq_.end();) {
     if (!copy_like(it->second.op)) {
@@ -776,6 +795,12 @@ FenceRef Ring::submit_locked() {
         case SqeOp::DECODE_ANS:
           if (!batch.empty() || !dbatch.empty()) flush();
           abatch.push_back(DecodeDesc{s.src, s.dst, s.n_values});
+          break;
+        case SqeOp::DECODE_SEGS:
+          if (!batch.empty() || !dbatch.empty()) flush();
+          for (size_t i = 0; i + 1 < s.idx.size(); i += 2)
+            abatch.push_back(DecodeDesc{s.src + s.idx[i + 1], s.dst + (uint64_t)(s.idx[i] & 31u) * (64u << 10),
+                                        kAnsSegValues});
           break;
         case SqeOp::GATHER:
         case SqeOp::SCATTER: {

@@ -1315,7 +1315,14 @@ Status Runtime::residency_info(Range* r, uint64_t off, ResidencyInfo* out) {
     out->resident_on.push_back(x.loc);
     out->chunk.push_back(x.chunk);
     out->pages.push_back(x.resident.count());
-    out->enc_bytes.push_back(x.fmt ? x.enc_bytes : 0);
+    if (x.fmt == 3 && x.seg) {
+      const uint32_t np = (uint32_t)__builtin_popcount(x.seg->packed);
+      out->enc_bytes.push_back(x.seg->packed_bytes() + (kSegsPerBlock - np) * kSegBytes);
+      out->seg_packed.push_back(np);
+    } else {
+      out->enc_bytes.push_back(x.fmt ? x.enc_bytes : 0);
+      out->seg_packed.push_back(0);
+    }
     dup |= seen & x.resident;
     seen |= x.resident;
   }

@@ -88,6 +88,14 @@ struct KAnsBlocks {
   uint32_t item_start[kAnsInlineBlocks + 1];
 };
 hipError_t launch_ans_blocks(const KAnsBlocks& b, uint32_t n, hipStream_t s, uint64_t* err = nullptr);
+// Single-segment ANS1 chunks (32 Ki values each: segmented packed host copies),
+// one wave per chunk.
+constexpr int kAnsInlineSegs = 128;
+struct KAnsSegs {
+  uint64_t src[kAnsInlineSegs];
+  uint64_t dst[kAnsInlineSegs];
+};
+hipError_t launch_ans_segs(const KAnsSegs& d, uint32_t n, hipStream_t s, uint64_t* err = nullptr);
 
 // Decode GEMM (csrc/kernels/decode_gemm.hip); argument structs in ogkm/dgemm.hpp.
 hipError_t launch_dgemm(const DGemmArgs& a, int mode, hipStream_t s);

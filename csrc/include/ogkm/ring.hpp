@@ -57,7 +57,13 @@ const char* ring_kind_str(RingKind k);
 // decode straight from the host copy.
 // PAGE_COPY: scattered pages of one block, page idx[i] of src -> page idx[i] of
 // dst (one LDS-staged kernel instead of one copy per run).
-enum class SqeOp : uint8_t { COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP, DECODE_BF12, PAGE_COPY, DECODE_ANS };
+// DECODE_SEGS: packed segments of a segmented host copy (Residency fmt 3): the
+// `bytes` at src (the sidecar span holding them, ONE staging copy) hold
+// single-segment ANS1 chunks; idx = pairs (segment s | length << 5, offset of
+// its chunk from src) and segment s decodes to dst + s * 64 KB.
+enum class SqeOp : uint8_t {
+  COPY = 0, GATHER, SCATTER, MEMSET, WAIT_FENCE, NOP, DECODE_BF12, PAGE_COPY, DECODE_ANS, DECODE_SEGS
+};
 
 struct Sqe {
   SqeOp op = SqeOp::NOP;

@@ -144,7 +144,8 @@ struct ResidencyInfo {   // UVM_TEST_VA_RESIDENCY_INFO analog (uvm_test_ioctl.h:
   std::vector<Loc> resident_on;
   std::vector<int64_t> chunk;       // per resident_on entry
   std::vector<uint32_t> pages;      // resident page count per entry
-  std::vector<uint32_t> enc_bytes;  // encoded size per entry (0 = raw)
+  std::vector<uint32_t> enc_bytes;  // encoded size per entry (0 = raw; fmt 3: the bytes a full refill moves)
+  std::vector<uint32_t> seg_packed; // fmt 3: packed 64 KB segments per entry (0 otherwise)
   std::vector<int> mapped_on;       // processors with a mapping (CPU view / stable VA / leases)
   bool read_dup = false;
   bool pinned = false;

@@ -40,6 +40,9 @@ __device__ __forceinline__ uint32_t ans_bperm(uint32_t lane, uint32_t v) {
 
 }  // namespace
 
+__device__ __forceinline__ void ans_decode_seg(const uint8_t* __restrict__ blk, uint32_t n_values, uint32_t seg,
+                                               uint16_t* __restrict__ dst, const uint32_t* tab);
+
 // Work item `sub` (4 segments, one per wave) of the ANS1 chunk at `blk`, whose
 // values land at dst[0, n_values). Called by the whole workgroup (barriers).
 // err (host-coherent, may be null): {count, tag, chunk, freq sum} of corrupt
@@ -99,6 +102,15 @@ __device__ __forceinline__ void ans_decode_item(const uint8_t* __restrict__ blk,
   __syncthreads();
   const uint32_t seg = sub * kAnsSegsPerItem + wave;
   if (seg >= h->n_seg) return;  // wave-uniform (the next barrier is at the next item's start)
+  ans_decode_seg(blk, n_values, seg, dst, tab);
+}
+
+// One wave decodes segment `seg` of the ANS1 chunk at `blk` (its decode table
+// already in `tab`).
+__device__ __forceinline__ void ans_decode_seg(const uint8_t* __restrict__ blk, uint32_t n_values, uint32_t seg,
+                                               uint16_t* __restrict__ dst, const uint32_t* tab) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const AnsHeader* h = reinterpret_cast<const AnsHeader*>(blk);
   const uint32_t* dir = reinterpret_cast<const uint32_t*>(blk + h->off_dir);
   const uint32_t off = dir[seg], end = dir[seg + 1];
   const uint32_t npairs = (end - off - 256u) / 4u;  // word pairs (the encoder pads to an even count)
@@ -210,6 +222,85 @@ __global__ void __launch_bounds__(kAnsThreads)
     }
     ans_decode_item(blk, nv, item - b.item_start[k], dst, tab, cum, wsum, err, b.src[k], k);
   }
+}
+
+// Segmented packed host copies (Residency fmt 3, ring DECODE_SEGS): many small
+// ANS1 chunks of ONE 32 Ki-value segment each. One wave per chunk - its own
+// decode table in its own 16 KB of LDS, built by the wave alone (no
+// workgroup barrier) - so all four waves of a workgroup decode; with the block
+// kernel's 4-segment items three of them would idle on such chunks.
+__global__ void __launch_bounds__(kAnsThreads)
+    k_ans_segs(const KAnsSegs d, uint32_t n, uint64_t* __restrict__ err) {
+  __shared__ uint32_t tabs[kAnsSegsPerItem][kAnsSlots];
+  __shared__ uint32_t cums[kAnsSegsPerItem][257];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t k = blockIdx.x * kAnsSegsPerItem + wave;
+  if (k >= n) return;  // wave-uniform; no workgroup barrier below
+  const uint8_t* blk = reinterpret_cast<const uint8_t*>(d.src[k]);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(d.dst[k]);
+  const AnsHeader* h = reinterpret_cast<const AnsHeader*>(blk);
+  uint32_t* tab = tabs[wave];
+  uint32_t* cum = cums[wave];
+  // cumulative frequencies: lane owns symbols 4 lane .. 4 lane + 3
+  uint32_t f[4], t = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[j] = h->freq[4 * lane + j];
+    t += f[j];
+  }
+  uint32_t inc = t;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const uint32_t y = __shfl_up(inc, s, 64);
+    if (lane >= (uint32_t)s) inc += y;
+  }
+  uint32_t c = inc - t;  // exclusive prefix
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    cum[4 * lane + j] = c;
+    c += f[j];
+  }
+  if (lane == 63u) cum[256] = c;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const bool bad = h->magic != kAnsMagic || h->n_values != kAnsSegValues || h->n_seg != 1 || cum[256] != kAnsSlots;
+  if (bad) {  // wave-uniform: report + zero-fill the segment
+    if (lane == 0 && err && __hip_atomic_fetch_add(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+      __hip_atomic_store(err + 1, d.src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(err + 2, (uint64_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(err + 3, (uint64_t)h->magic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    for (uint32_t g = lane; g < kAnsSegValues / 8; g += 64)
+      reinterpret_cast<au32x4*>(dst)[g] = au32x4{0u, 0u, 0u, 0u};
+    return;
+  }
+  {  // decode table: lane fills slots [64 lane, 64 lane + 64)
+    const uint32_t k0 = lane * (kAnsSlots / 64);
+    uint32_t lo = 0, hi = 256;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (cum[mid] <= k0) lo = mid; else hi = mid;
+    }
+    uint32_t sym = lo;
+    for (uint32_t q = k0; q < k0 + kAnsSlots / 64; ++q) {
+      while (sym < 255u && cum[sym + 1] <= q) ++sym;
+      tab[q] = sym | ((cum[sym + 1] - cum[sym]) << 8) | ((q - cum[sym]) << 20);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  ans_decode_seg(blk, kAnsSegValues, 0, dst, tab);
+}
+
+hipError_t launch_ans_segs(const KAnsSegs& d, uint32_t n, hipStream_t s, uint64_t* err) {
+  if (n == 0) return hipSuccess;
+  if (n > (uint32_t)kAnsInlineSegs) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_ans_segs, dim3((n + kAnsSegsPerItem - 1) / kAnsSegsPerItem), dim3(kAnsThreads), 0, s, d, n,
+                     err);
+  return hipGetLastError();
 }
 
 hipError_t launch_ans_unpack(const void* stream, void* dst, uint32_t nchunks, uint32_t chunk_values,

@@ -624,6 +624,7 @@ PYBIND11_MODULE(_ogkm, m) {
       e["pages"] = ri.pages[i];
       e["chunk"] = ri.chunk[i];
       if (i < ri.enc_bytes.size() && ri.enc_bytes[i]) e["encoded_bytes"] = ri.enc_bytes[i];
+      if (i < ri.seg_packed.size() && ri.seg_packed[i]) e["packed_segments"] = ri.seg_packed[i];
       res.append(e);
     }
     d["resident_on"] = res;

@@ -514,12 +514,14 @@ def test_bf12_decode_bandwidth(gpu_rt):
     s0 = lib.stats()
     gbps = _refill_gbps(b, n)
     s1 = lib.stats()
+    ring = {k: s1[k] - s0[k] for k in ("ring_copy_ns", "ring_copy_calls", "ring_fence_wait_ns", "ring_idle_ns",
+                                       "decode_reuse_waits", "ring_merged_batches", "bytes_xfer_htd")}
     rt.configure(bf12_stage=0)  # diagnostics: the fused kernel reading host memory
     fused = _refill_gbps(b, n, reps=2)
     rt.configure(bf12_stage=1)
     print(f"refill 1 GiB: raw {raw_gbps:.1f} GB/s, packed BF12 staged {gbps:.1f}, fused {fused:.1f} GB/s of bf16; "
           f"gpu numa {lib.device_numa_node(0)} host node {lib.host_node()}; "
-          f"packed decodes {s1['packed_decodes'] - s0['packed_decodes']}")
+          f"packed decodes {s1['packed_decodes'] - s0['packed_decodes']}; ring {ring}")
     assert s1["packed_decodes"] > s0["packed_decodes"]  # the staged path ran
     # BF12 moves 0.75x the bytes: the ideal ratio is 1.33; guard at 90% of it
     # (measured 73.3 vs 57.1 GB/s = 1.28, gpurun_out r6 / profiles/r6_gpu_suite.txt)
