@@ -97,8 +97,10 @@ def parse():
                          "classes) and its prefetch / eviction. static: a hand-made plan pins whole layers")
     ap.add_argument("--kv-tiering", action="store_true",
                     help="KV prefixes as evictable per-layer units (resident with their layer, else streamed)")
-    ap.add_argument("--allocator", action="store_true",
-                    help="route torch CUDA allocations through the runtime's HBM arena (pluggable allocator)")
+    ap.add_argument("--allocator", action=argparse.BooleanOptionalAction, default=None,
+                    help="route torch CUDA allocations through the runtime's HBM arena (pluggable allocator); "
+                         "default: on for HBM-resident runs (--oversub <= 1, config 2 - the allocator baseline), "
+                         "off for oversubscribed ones")
     ap.add_argument("--torch-managed", action="store_true",
                     help="run a stock torch.nn Llama (models/torch_llama.py) under ogkm.managed(): every tensor "
                          "oversubscribes HBM through the transparent mode, no hand-planned residency (1 GPU)")
@@ -528,6 +530,8 @@ def main() -> None:
     from ogkm.parallel import comm
 
     fake = a.backend == "fake"
+    if a.allocator is None:
+        a.allocator = a.oversub <= 1.0 and not a.torch_managed
     if a.allocator and not fake:
         # config 2: torch tensors share the runtime's HBM arena. Swapped in
         # before torch initialises its caching allocator (and before any CUDA

@@ -578,7 +578,10 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
     }
   } else if (raw_pages.empty()) {
     // (every requested page comes from packed segments)
-  } else if (raw_pages.runs() >= (uint32_t)std::max<int64_t>(2, config().copy_page_list_min_runs)) {
+  } else if (!seg_dec && raw_pages.runs() >= (uint32_t)std::max<int64_t>(2, config().copy_page_list_min_runs)) {
+    // (a segmented copy's raw segments go as engine copies: a page-list kernel
+    // would read the host over PCIe from the CUs and drain the ring's staged
+    // decodes around it)
     // Fragmented mask: one page-list kernel (LDS-staged) instead of one copy
     // per run - the staged pack of uvm_va_block.c:4278-4326 / 3673-3860.
     Sqe s;

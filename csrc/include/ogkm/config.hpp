@@ -91,7 +91,7 @@ namespace ogkm {
   X(pack_seg_min, 4, "a written block's host copy is segment-packed when at least this many of its 64 KB segments were untouched by its latest write-back") \
   X(pack_threads, 4, "host encoder threads of the packer") \
   X(ans_stage_mb, 128, "per-H2D-ring HBM staging buffer the packed bytes land in before the decode kernel (0: the kernel reads the host copy over PCIe)") \
-  X(bf12_stage, 1, "H2D ring: BF12 blocks are staged into HBM by SDMA and decoded there, as ANS1 blocks are (0: the fused kernel reads the host copy over PCIe - its rate depends on CU-driven host reads)") \
+  X(bf12_stage, 0, "H2D ring: BF12 blocks are staged into HBM by SDMA (4 engines) and decoded there, as ANS1 blocks are (0: the fused kernel reads the host copy over PCIe). Measured on 1 GiB, best of 3, across boxes: fused 70.9-73.9 GB/s of bf16 every run; staged 72-73 on some processes and 41-42 on others of the same build (tools/diag_bf12_refill.py, profiles/r6_bf12_refill.md)") \
   X(ring_defer_decodes, 1, "H2D ring: packed-block decodes overlap the next batch (two staging halves, deferred publish); 0 = drain after each batch's decodes") \
   X(ring_stage_overlap, 1, "H2D ring: a staging half's copies are issued before the host waits for the previous half's and launches its decode (0 = issue, wait, decode per half)") \
   X(ring_merge_packed_mb, 64, "H2D ring: queued batches of packed-block decodes run as one batch up to this many packed MB (0 = one batch at a time)") \

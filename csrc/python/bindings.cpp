@@ -956,6 +956,15 @@ PYBIND11_MODULE(_ogkm, m) {
           "ans_unpack");
   }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("nchunks"), py::arg("chunk_values"),
      py::arg("n_values"), py::arg("stream") = 0, py::arg("workgroups") = 0, py::arg("dst_stride") = 0, py::arg("row_shift") = 0);
+  // Decode ANS1 chunks at device addresses (the ring's DECODE_ANS / DECODE_SEGS
+  // kernels: single-segment chunks run one wave each, k_ans_segs).
+  m.def("decode_ans_chunks", [](int dev, const std::vector<uint64_t>& src, const std::vector<uint64_t>& dst,
+                                const std::vector<uint32_t>& n_values, uint64_t stream) {
+    if (src.size() != dst.size() || src.size() != n_values.size()) throw StatusError("decode_ans_chunks: sizes");
+    std::vector<DecodeDesc> d;
+    for (size_t i = 0; i < src.size(); ++i) d.push_back(DecodeDesc{src[i], dst[i], n_values[i]});
+    check(rt()->be()->decode_ans_blocks(dev, d.data(), d.size(), (void*)stream), "decode_ans_chunks");
+  }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("n_values"), py::arg("stream") = 0);
   m.def("decode_errors", [](bool reset) {
     uint64_t e[4];
     rt()->be()->decode_errors(e, reset);

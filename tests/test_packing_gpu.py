@@ -150,3 +150,58 @@ def test_segmented_kv_refill_bit_exact(gpu_rt, engine):
     assert s1["bytes_xfer_htd"] - s0["bytes_xfer_htd"] < 0.85 * size
     assert torch.equal(b.read().cuda(), data)
     b.free()
+
+
+def test_single_segment_chunks_decode_one_wave_each(gpu_rt):
+    """k_ans_segs (one wave per single-segment ANS1 chunk - the chunks of
+    segmented host copies) decodes every bit, including special values and a
+    corrupt chunk (reported and zero-filled, the others unaffected), and
+    prints its throughput next to the 4-segment-item stream kernel."""
+    from ogkm.ops import bf12
+    import time
+
+    nseg = 2048  # 128 MB of bf16
+    n = nseg * 32768
+    ref = (torch.randn(n) * 0.02).to(torch.bfloat16)
+    ref[:4] = torch.tensor([0.0, float("inf"), float("nan"), -2.5], dtype=torch.bfloat16)
+    stream, info = bf12.pack(ref, chunk_values=32768, fmt="ans")
+    assert info.nchunks == nseg
+    table = stream[32:32 + 16 * nseg].view(torch.int64).view(-1, 2)
+    offs = table[:, 0].tolist()
+    kinds = table[:, 1].view(torch.int32).view(-1, 2)[:, 1].tolist()
+    assert set(kinds) == {3}  # every chunk ANS1
+    src = stream.cuda()
+    dst = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    base = src.data_ptr()
+    srcs = [base + o for o in offs]
+    dsts = [dst.data_ptr() + 2 * 32768 * i for i in range(nseg)]
+    nv = [32768] * nseg
+    lib.decode_errors(True)
+    lib.decode_ans_chunks(0, srcs, dsts, nv, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(dst.view(torch.int16).cpu(), ref.view(torch.int16))
+    for _ in range(2):
+        lib.decode_ans_chunks(0, srcs, dsts, nv, 0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        lib.decode_ans_chunks(0, srcs, dsts, nv, 0)
+    torch.cuda.synchronize()
+    seg_gbps = 10 * 2 * n / (time.perf_counter() - t0) / 1e9
+    t0 = time.perf_counter()
+    for _ in range(10):
+        bf12.unpack_into(dst, src.data_ptr(), info, 0)
+    torch.cuda.synchronize()
+    item_gbps = 10 * 2 * n / (time.perf_counter() - t0) / 1e9
+    print(f"single-segment chunks: k_ans_segs {seg_gbps:.0f} GB/s, k_ans_unpack {item_gbps:.0f} GB/s of bf16")
+    assert seg_gbps > 1.5 * item_gbps
+    # a corrupt chunk: reported, zero-filled; its neighbours still decode
+    bad = src.clone()
+    bad[offs[5]:offs[5] + 4] = 0  # magic
+    lib.decode_errors(True)
+    lib.decode_ans_chunks(0, [bad.data_ptr() + o for o in offs[:8]], dsts[:8], nv[:8], 0)
+    torch.cuda.synchronize()
+    assert lib.decode_errors(True)["count"] >= 1
+    got = dst[:8 * 32768].view(torch.int16).cpu()
+    assert torch.equal(got[5 * 32768:6 * 32768], torch.zeros(32768, dtype=torch.int16))
+    assert torch.equal(got[4 * 32768:5 * 32768], ref[4 * 32768:5 * 32768].view(torch.int16))
