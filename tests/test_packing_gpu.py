@@ -166,9 +166,9 @@ def test_single_segment_chunks_decode_one_wave_each(gpu_rt):
     ref[:4] = torch.tensor([0.0, float("inf"), float("nan"), -2.5], dtype=torch.bfloat16)
     stream, info = bf12.pack(ref, chunk_values=32768, fmt="ans")
     assert info.nchunks == nseg
-    table = stream[32:32 + 16 * nseg].view(torch.int64).view(-1, 2)
-    offs = table[:, 0].tolist()
-    kinds = table[:, 1].view(torch.int32).view(-1, 2)[:, 1].tolist()
+    table = stream[32:32 + 16 * nseg].view(torch.int32).view(-1, 4)  # {u64 offset, u32 n_values, u32 encoded}
+    offs = [int(lo) & 0xFFFFFFFF | (int(hi) << 32) for lo, hi in table[:, :2].tolist()]
+    kinds = table[:, 3].tolist()
     assert set(kinds) == {3}  # every chunk ANS1
     src = stream.cuda()
     dst = torch.empty(n, dtype=torch.bfloat16, device="cuda")

@@ -1,15 +1,19 @@
 #!/bin/bash
-# round 6 (m): headline bench (default config, 70B 2x) on the current tree,
-# attention split A/B at every bench shape, config 2 through the allocator
-# default + its kernel profile.
+# round 6 (m): GPU tests of this round's paths, transparent 70B with segmented
+# host copies, headline bench, attention split A/B, config 2 (arena allocator
+# default) + its kernel profile (kernel trace only).
 set -o pipefail
 ulimit -c 0
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r6
-timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r6/m_headline.log 2>&1 || { echo HEADLINE_FAIL; tail -30 gpurun_out/r6/m_headline.log; exit 1; }
-grep '^{' gpurun_out/r6/m_headline.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); a=d['aux']; print('headline', d['value'], d['ms_per_step'], a.get('link_gbps_per_gpu'), a.get('traffic_per_step_gb'))"
-for sp in 0 64 256; do SPLIT=$sp timeout -k 10 200 python -u tools/bench_attn.py > gpurun_out/r6/m_attn_split$sp.log 2>&1 || exit 1; sed "s/^/split$sp /" gpurun_out/r6/m_attn_split$sp.log | grep -v amdgpu.ids; done
-timeout -k 10 400 python -u bench.py --model llama3-8b --oversub 1.0 --steps 30 --warmup 5 > gpurun_out/r6/m_c2.log 2>&1 || exit 1
-grep '^{' gpurun_out/r6/m_c2.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('c2 default', d['value'], d['ms_per_step'], d['config'].get('torch_allocator'))"
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r6/m_prof_c2 -o c2 -- python3 $GRAFT_REPO_ROOT/bench.py --model llama3-8b --oversub 1.0 --steps 20 --warmup 5 --no-aux > $GRAFT_REPO_ROOT/gpurun_out/r6/m_prof_c2.log 2>&1 || { echo PROF_FAIL; tail -5 $GRAFT_REPO_ROOT/gpurun_out/r6/m_prof_c2.log; exit 1; }
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/r6
+cd $R
+timeout -k 10 400 python -u -m pytest tests/test_packing_gpu.py tests/test_gpu_runtime.py -q -s -k "packing or segment or packed or allocator or bf12" --timeout 120 --timeout-method thread > gpurun_out/r6/m_tests.log 2>&1; rc=$?
+grep -E "refill 1 GiB|single-segment|passed|failed" gpurun_out/r6/m_tests.log | cut -c1-300
+[ $rc -le 1 ] || exit 1
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r6/m_smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 gpurun_out/r6/m_smoke.log; exit 1; }
+grep -o "max_logit_err_vs_fp32': [0-9.]*" gpurun_out/r6/m_smoke.log
+summ() { grep '^{' "$1" | python -c "import json,sys; d=json.loads(sys.stdin.read()); a=d['aux']; print('$2', d['value'], d['ms_per_step'], a['htd_gb_per_step'], a['dth_gb_per_step'], a['host_ms_per_step'], a['ring_per_step']); print(json.dumps(a['block_census'])); print(a['pack'])"; }
+OGKM_TM_CENSUS=1 timeout -k 10 900 python -u bench.py --torch-managed --model llama3-70b --oversub 2 --steps 5 --warmup 3 > gpurun_out/r6/m_tm70b_seg.log 2>&1 || { echo TM_FAIL; tail -30 gpurun_out/r6/m_tm70b_seg.log; exit 1; }
+summ gpurun_out/r6/m_tm70b_seg.log seg_on
 echo ALL_OK
