@@ -366,7 +366,7 @@ def test_written_block_host_copy_packs_by_segment(fake_rt):
     refill decodes the packed segments and copies the raw ones; later writes
     into the same segments expand nothing, a write into a packed segment
     expands only that segment - and every read is bit-exact."""
-    rt.configure(pack_host_copies=1, pack_threads=2)
+    rt.configure(pack_host_copies=1, pack_segments=1, pack_threads=2)
     b = rt.malloc_managed(4 * MB, "kv")  # 2 blocks x 8 rows of 256 KB (4 segments per row)
     data = _weights(b.size, 21)
     b.write(data)
@@ -402,7 +402,7 @@ def test_segmented_copy_cpu_access_and_runtime_write(fake_rt):
     store through the CPU view faults (the view maps raw segments only) and
     the fault service - whole-block granular - expands the copy; all stay
     bit-exact through GPU refills."""
-    rt.configure(pack_host_copies=1, pack_threads=1)
+    rt.configure(pack_host_copies=1, pack_segments=1, pack_threads=1)
     b = rt.malloc_managed(2 * MB, "kv1")
     data = _weights(b.size, 22)
     b.write(data)

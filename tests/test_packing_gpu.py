@@ -113,7 +113,7 @@ def test_segmented_kv_refill_bit_exact(gpu_rt, engine):
     if engine != rt.get_config("copy_engine"):
         lib.shutdown()
         rt.init("hip", lock_check=1, host_budget_mb=16384, hbm_budget={0: 2 << 30}, copy_engine=engine)
-    rt.configure(pack_host_copies=1, pack_threads=4)
+    rt.configure(pack_host_copies=1, pack_segments=1, pack_threads=4)
     size = 32 * MB
     b = rt.malloc_managed(size, "kv")
     data = _weights(size, 9).cuda()
