@@ -99,8 +99,8 @@ def parse():
                     help="KV prefixes as evictable per-layer units (resident with their layer, else streamed)")
     ap.add_argument("--allocator", action=argparse.BooleanOptionalAction, default=None,
                     help="route torch CUDA allocations through the runtime's HBM arena (pluggable allocator); "
-                         "default: on for HBM-resident runs (--oversub <= 1, config 2 - the allocator baseline), "
-                         "off for oversubscribed ones")
+                         "default: on for the HBM-resident single-GPU run (--oversub 1, config 2 - the allocator "
+                         "baseline), off otherwise")
     ap.add_argument("--torch-managed", action="store_true",
                     help="run a stock torch.nn Llama (models/torch_llama.py) under ogkm.managed(): every tensor "
                          "oversubscribes HBM through the transparent mode, no hand-planned residency (1 GPU)")
@@ -531,7 +531,7 @@ def main() -> None:
 
     fake = a.backend == "fake"
     if a.allocator is None:
-        a.allocator = a.oversub <= 1.0 and not a.torch_managed
+        a.allocator = a.oversub == 1.0 and not a.torch_managed and a.gpus <= 1
     if a.allocator and not fake:
         # config 2: torch tensors share the runtime's HBM arena. Swapped in
         # before torch initialises its caching allocator (and before any CUDA

@@ -140,7 +140,11 @@ Runtime::~Runtime() {
 // ------------------------------------------------------------------ tiers
 Status Runtime::init_device(int d, uint64_t budget) {
   if (!is_local(d)) return Status::INVALID_ARGUMENT;
-  torch_alloc_trim(d);  // freed torch memory the pluggable allocator still caches goes back first
+  // Freed torch memory the pluggable allocator still caches goes back first -
+  // only when the arena is not empty (trimming on every init measurably hung
+  // the GPU dgemm test sequence in a driver fence wait at the next arena
+  // creation; gpurun_out/r6 sessions s-u: 235 passed without, a hang with).
+  if (devs_[d]->hbm && devs_[d]->hbm->outstanding_bytes()) torch_alloc_trim(d);
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
   if (devs_[d]->hbm && devs_[d]->hbm->outstanding_bytes()) return Status::BUSY;
   devs_[d]->hbm_live.store(nullptr);
