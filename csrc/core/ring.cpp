@@ -542,11 +542,32 @@ Status Ring::run_batch(Batch& b) {
     stage_half_ ^= 1;
     half_ready = false;
   };
+  // A staged decode queued before an engine copy into the same chunk (the
+  // chunk's block was evicted and the chunk handed to another block between
+  // two submissions that the worker merged into this batch - copy_pages skips
+  // same-ring fences, the ring being in order) must land first: staged
+  // decodes are launched only after their half's copies completed, so a copy
+  // issued with those would be overwritten (or raced) by the older decode.
+  auto staged_hit = [&](uint64_t dst, uint64_t bytes) {
+    for (const DecodeDesc& d : staged)
+      if (dst < d.dst + 2ull * d.n_values && d.dst < dst + bytes) return true;
+    if (ps.on)
+      for (const DecodeDesc& d : ps.staged)
+        if (dst < d.dst + 2ull * d.n_values && d.dst < dst + bytes) return true;
+    return false;
+  };
   for (auto& s : b.ops) {
     if (st != Status::OK) break;
     switch (s.op) {
       case SqeOp::COPY:
         flush_decodes();
+        if (staged_hit(s.dst, s.bytes)) {
+          // launch them (the copy then waits for them: kernels_pending /
+          // decodes_deferred + batch_dst_ in issue_copies)
+          flush_staged();
+          flush_copies();
+          Tools::get().inc(Counter::DecodeReuseWaits);
+        }
         if (!copies.empty() && copies.back().dst + copies.back().bytes == s.dst &&
             copies.back().src + copies.back().bytes == s.src && copy_dst.back() == s.dst_dev) {
           copies.back().bytes += s.bytes;

@@ -141,9 +141,11 @@ Runtime::~Runtime() {
 Status Runtime::init_device(int d, uint64_t budget) {
   if (!is_local(d)) return Status::INVALID_ARGUMENT;
   // Freed torch memory the pluggable allocator still caches goes back first -
-  // only when the arena is not empty (trimming on every init measurably hung
-  // the GPU dgemm test sequence in a driver fence wait at the next arena
-  // creation; gpurun_out/r6 sessions s-u: 235 passed without, a hang with).
+  // only when an arena exists and is not empty. (An unguarded trim used to go
+  // through arena_for, which creates the default half-of-HBM arena on first
+  // touch: every init built and destroyed a ~140 GB VMM arena, and the GPU
+  // dgemm test sequence hung in a driver fence wait; gpurun_out/r6 sessions
+  // s-u. torch_alloc_trim now never creates an arena.)
   if (devs_[d]->hbm && devs_[d]->hbm->outstanding_bytes()) torch_alloc_trim(d);
   std::unique_lock<OrderedRWLock> vg(vs_.lock);
   if (devs_[d]->hbm && devs_[d]->hbm->outstanding_bytes()) return Status::BUSY;

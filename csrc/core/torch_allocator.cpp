@@ -560,7 +560,10 @@ void torch_free(void* p, int device, void* stream) {
 void torch_alloc_trim(int device) {
   Runtime* rt = Runtime::get();
   if (!rt || !rt->is_local(device)) return;
-  ChunkArena* a = rt->arena_for(Loc::gpu(device));
+  // Never through arena_for: on a device with no arena yet that would create
+  // the default half-of-HBM arena just to trim it (and init_device then tears
+  // it down again) - per-init that churn hung the GPU test sequence.
+  ChunkArena* a = rt->hbm_arena_if_any(device);
   if (!a) return;
   DevAlloc* da = dev_alloc(device);
   std::lock_guard<std::mutex> g(da->m);

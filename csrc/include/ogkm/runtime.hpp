@@ -180,6 +180,8 @@ class Runtime {
   Status vmm_self_test(int d);
   HostArena* host_arena(Tier t, int node);            // created on first use
   ChunkArena* arena_for(const Loc& l);
+  // d's HBM arena if one exists; never creates the default one (arena_for does)
+  ChunkArena* hbm_arena_if_any(int d) { return is_local(d) ? devs_[d]->hbm_live.load(std::memory_order_acquire) : nullptr; }
   // nullptr for a non-local device
   Ring* ring(int dev, RingKind k) { return is_local(dev) ? devs_[dev]->rings[(int)k].get() : nullptr; }
 

@@ -817,6 +817,28 @@ PYBIND11_MODULE(_ogkm, m) {
     py::gil_scoped_release nogil;
     check(r->submit()->wait(), "ring_gather");
   });
+  // One submission of raw ring ops, not waited for (ordering tests): tuples
+  // (op, dst, src, bytes, n_values) with op 0 = COPY, 1 = DECODE_ANS (src:
+  // ANS1 chunk of `bytes`, n_values bf16 out), 2 = WAIT_FENCE on an event
+  // recorded now on stream `src`. Returns the submission's tracking value.
+  m.def("debug_ring_submit", [](int dev, int kind, std::vector<std::tuple<int, uint64_t, uint64_t, uint64_t, uint32_t>> ops) {
+    Ring* r = ring_of(dev, kind);
+    for (auto& o : ops) {
+      const int op = std::get<0>(o);
+      if (op == 2) {
+        r->push_wait(fence_record(rt()->be(), dev, (void*)std::get<2>(o)));
+        continue;
+      }
+      Sqe s;
+      s.op = op == 1 ? SqeOp::DECODE_ANS : SqeOp::COPY;
+      s.dst = std::get<1>(o);
+      s.src = std::get<2>(o);
+      s.bytes = std::get<3>(o);
+      s.n_values = std::get<4>(o);
+      r->push(std::move(s));
+    }
+    return r->submit()->seq;
+  });
   m.def("ring_stream", [](int dev, int kind) { return (uint64_t)ring_of(dev, kind)->stream(); });
   // Peer plane: SDMA engine masks per (dst, src) pair (-1 = host) and per-engine bytes.
   m.def("copy_engine_mask", [](int dst, int src) { return rt()->be()->copy_engine_mask(dst, src); });
@@ -910,6 +932,15 @@ PYBIND11_MODULE(_ogkm, m) {
     std::string s = raw;
     std::string out((size_t)kBlockSize + kBf11HeaderBytes, '\0');
     uint64_t n = bf11_encode((const uint16_t*)s.data(), (uint32_t)(s.size() / 2), (uint8_t*)out.data(), out.size());
+    out.resize(n);
+    return py::bytes(out);
+  });
+  // One ANS1 chunk of a bf16 buffer (the packed host copy's format); empty when
+  // it would not fit in the raw size.
+  m.def("ans_encode", [](py::bytes raw) {
+    std::string s = raw;
+    std::string out(s.size() + 4096, '\0');
+    uint64_t n = ans_encode((const uint16_t*)s.data(), (uint32_t)(s.size() / 2), (uint8_t*)out.data(), s.size());
     out.resize(n);
     return py::bytes(out);
   });

@@ -26,7 +26,7 @@ import torch  # noqa: E402
 
 D, FF, LAYERS, HEADS = 1024, 4096, 16, 16
 BATCH, SEQ = 4, 128
-ARENA_MB = 384
+ARENA_MB = int(os.environ.get("OGKM_TEST_ARENA_MB", "384"))  # (diagnostics may shrink it)
 
 
 def build():

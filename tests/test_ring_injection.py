@@ -199,3 +199,38 @@ def test_ecc_uncorrectable_error_is_fatal(fake_rt):
     assert "xGMI" in lib.fatal_reason()
     with pytest.raises(Exception):
         rt.malloc_managed(1 << 20, "after-ecc")  # every later operation fails fast
+
+
+def test_merged_batches_copy_after_staged_decode_into_same_chunk(fake_rt):
+    """Two submissions the H2D worker merges into one batch: the first decodes
+    a packed block into chunk E (staged: SDMA into HBM staging, decode after
+    the copies landed), the second - after E was handed to another block -
+    copies raw data into E. copy_pages skips same-ring fences (the ring is in
+    order), so the batch itself must land the older decode first; before the
+    fix the raw copy went out with the staging copies and the decode launched
+    after them overwrote it (the transparent-mode packed training test's
+    corrupted gradient)."""
+    lib.configure("ans_stage_mb", 8)
+    vals = lambda seed: (torch.randn(MB, generator=torch.Generator().manual_seed(seed)) * 0.02).to(torch.bfloat16)
+    w1, w2, g = vals(1), vals(2), vals(3)
+    enc1 = torch.frombuffer(bytearray(lib.ans_encode(w1.view(torch.uint8).numpy().tobytes())), dtype=torch.uint8)
+    enc2 = torch.frombuffer(bytearray(lib.ans_encode(w2.view(torch.uint8).numpy().tobytes())), dtype=torch.uint8)
+    assert 0 < enc1.numel() < 2 * MB and 0 < enc2.numel() < 2 * MB
+    e, le = _dev_buf(2 * MB, 0)
+    f, lf = _dev_buf(2 * MB, 0)
+    # the worker is held in a first submission waiting on a slow stream
+    s = lib.debug_stream_create(0)
+    blk, lblk = _dev_buf(2 * MB, 0)
+    lib.debug_touch(s, lblk.dptr, 2 * MB, 300000)
+    lib.debug_ring_submit(0, CPU_TO_GPU, [(2, 0, s, 0, 0)])
+    lib.debug_ring_submit(0, CPU_TO_GPU, [(1, le.dptr, enc1.data_ptr(), enc1.numel(), MB)])
+    last = lib.debug_ring_submit(0, CPU_TO_GPU, [(1, lf.dptr, enc2.data_ptr(), enc2.numel(), MB),
+                                                (0, le.dptr, g.data_ptr(), 2 * MB, 0)])
+    assert lib.ring_wait_seq(0, CPU_TO_GPU, last) == "OK"
+    assert lib.stats()["ring_merged_batches"] >= 1  # (the case under test)
+    assert torch.equal(lf.tensor((MB,), torch.bfloat16).cpu(), w2)
+    assert torch.equal(le.tensor((MB,), torch.bfloat16).cpu(), g)
+    lib.debug_stream_sync(s)
+    lib.debug_stream_destroy(s)
+    for l in (le, lf, lblk):
+        l.release(0)
