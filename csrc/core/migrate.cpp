@@ -521,12 +521,19 @@ static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from
                 bytes, b->range->id, t0, now_ns());
     return Status::OK;
   }
+  if (const int64_t dw = config().debug_copy_host_wait; dw == 2 || (dw == 1 && to->loc.is_gpu())) {
+    // (diagnostics) dependencies met on the host before anything is queued
+    for (auto& f : reuse.fences())
+      if (f->ring != ring) (void)f->wait();
+    for (auto& f : pend.fences())
+      if (f->ring != ring) (void)f->wait();
+  }
   for (auto& f : reuse.fences()) {
-    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
+    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f)) continue;
     ring->push_wait(f);
   }
   for (auto& f : pend.fences()) {
-    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
+    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f)) continue;
     ring->push_wait(f);
   }
   if (seg_dec) {
@@ -648,7 +655,7 @@ static Status zero_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* to, 
   }
   Tracker reuse = to->arena->reuse_fence((uint32_t)to->chunk);
   for (auto& f : reuse.fences()) {
-    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f.get())) continue;
+    if (f->ring == ring || f->done.load(std::memory_order_relaxed) || !c.first_wait(ring, f)) continue;
     ring->push_wait(f);
   }
   pages.for_each_run([&](uint32_t p, uint32_t n) {

@@ -94,7 +94,7 @@ namespace ogkm {
   X(bf12_stage, 0, "H2D ring: BF12 blocks are staged into HBM by SDMA (4 engines) and decoded there, as ANS1 blocks are (0: the fused kernel reads the host copy over PCIe). Measured on 1 GiB, best of 3, across boxes: fused 70.9-73.9 GB/s of bf16 every run; staged 72-73 on some processes and 41-42 on others of the same build (tools/diag_bf12_refill.py, profiles/r6_bf12_refill.md)") \
   X(ring_defer_decodes, 1, "H2D ring: packed-block decodes overlap the next batch (two staging halves, deferred publish); 0 = drain after each batch's decodes") \
   X(ring_stage_overlap, 1, "H2D ring: a staging half's copies are issued before the host waits for the previous half's and launches its decode (0 = issue, wait, decode per half)") \
-  X(ring_merge_packed_mb, 64, "H2D ring: queued batches of packed-block decodes run as one batch up to this many packed MB (0 = one batch at a time)") \
+  X(ring_merge_packed_mb, 0, "H2D ring: queued batches of packed-block decodes run as one batch up to this many packed MB (0 = one batch at a time) Off by default: with it on, the packed transparent-mode training test read another block's decoded weights in a gradient, 6/6 runs, unresolved (profiles/r6_ring_merge_fix)") \
   X(ans_stage_engines, 0xF, "SDMA engines (mask) the H2D ring spreads packed-block staging copies over (0 = the ring's own engine)") \
   X(host_segment_mb, 1024, "host / CXL arenas populate, pin and reserve their memory in segments of this many MB") \
   /* channels / ring */                                                                              \
@@ -125,6 +125,7 @@ namespace ogkm {
   X(cxl_emulate_mask, 0, "bitmask of NUMA nodes treated as CXL pools when no CXL hardware")          \
   /* debug */                                                                                        \
   X(lock_check, 0, "enable the lock-order checker")                                                  \
+  X(debug_copy_host_wait, 0, "diagnostics: a copy into a chunk host-waits for the chunk's reuse fence and the block's pending work before it is queued (1 = copies to a GPU, 2 = every copy)") \
   X(fake_race_check, 0, "fake backend: report kernels (debug_touch) that touch a chunk an engine copy is using") \
   X(fake_dma_delay_us, 0, "fake backend: microseconds every SDMA batch takes (ordering tests)")       \
   X(fake_kernel_delay_us, 0, "fake backend: each packed-block decode launch sleeps this long on its stream (tests)") \

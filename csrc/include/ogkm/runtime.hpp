@@ -501,7 +501,10 @@ struct Runtime::Ctx {
   std::vector<Block*> cpu_refresh;    // CPU views to refresh after submission
   ChunkArena* need_arena = nullptr;   // set on MORE_PROCESSING_REQUIRED
   uint32_t need_n = 0;
-  std::vector<std::pair<Ring*, Fence*>> waited;  // GPU-side waits already queued
+  // GPU-side waits already queued. The fences are held: a raw pointer would
+  // let a freed fence's address come back as a new, unsignalled fence that
+  // this context then believes it already waited for.
+  std::vector<std::pair<Ring*, FenceRef>> waited;
   bool defer_flush = false;           // finish_ctx leaves the translation flush to the caller
   // Migration invalidations are applied only once the copies that replace the
   // data were submitted successfully; a failed submission invalidates the
@@ -514,7 +517,7 @@ struct Runtime::Ctx {
     rings.push_back(r);
   }
   // True the first time (ring, fence) is seen: one WAIT_FENCE per pair per operation.
-  bool first_wait(Ring* r, Fence* f) {
+  bool first_wait(Ring* r, const FenceRef& f) {
     for (auto& w : waited)
       if (w.first == r && w.second == f) return false;
     waited.emplace_back(r, f);

@@ -53,6 +53,9 @@ def run(model, x, log=False):
     loss = y.float().pow(2).mean()
     loss.backward()
     say("backward done")
+    if os.environ.get("OGKM_DIAG_SNAP"):  # (diagnostics) a gradient's value right after backward
+        w = dict(model.named_parameters())[os.environ["OGKM_DIAG_SNAP"]]
+        torch.save(w.grad.detach().cpu().clone(), os.environ["OGKM_DIAG_SNAP_OUT"])
     opt.step()
     say("step done")
     out = {"y_inf": y_inf, "loss": loss.detach()}

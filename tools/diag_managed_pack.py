@@ -40,6 +40,35 @@ def describe(a: torch.Tensor, b: torch.Tensor) -> str:
             f"zeros in managed {(fb[ne] == 0).sum().item()}")
 
 
+def page_sources(a, b, k):
+    """Where the wrong 4 KB pages of b[k] come from: the same page (or any page)
+    of the initial / updated weights and gradients of the plain run."""
+    sys.path.insert(0, os.path.dirname(WORKER))
+    import managed_mode_worker as w
+    model, _ = w.build()
+    init = {"init." + n: p.detach() for n, p in model.named_parameters()}
+    cands = dict(init)
+    cands.update({n: t for n, t in a.items() if n.startswith(("p.", "g."))})
+    esz = a[k].element_size()
+    per = 4096 // esz
+    fa, fb = a[k].reshape(-1), b[k].reshape(-1)
+    bad = [p for p in range(fa.numel() // per) if not torch.equal(fa[p * per:(p + 1) * per], fb[p * per:(p + 1) * per])]
+    index = {}
+    for n, t in cands.items():
+        if t.element_size() != esz:
+            continue
+        ft = t.reshape(-1)
+        for q in range(ft.numel() // per):
+            index.setdefault(ft[q * per:(q + 1) * per].numpy().tobytes(), (n, q))
+    hits = {}
+    for p in bad:
+        src = index.get(fb[p * per:(p + 1) * per].numpy().tobytes())
+        key = "none" if src is None else f"{src[0]} ({'same page' if src[1] == p else f'page {src[1]} vs {p}'})"
+        key = key if src is None or src[1] == p else f"{src[0]} (other page, offset {src[1] - p:+d})"
+        hits[key] = hits.get(key, 0) + 1
+    return dict(sorted(hits.items(), key=lambda x: -x[1])[:6])
+
+
 def main():
     out, runs, extra = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
     os.makedirs(out, exist_ok=True)
@@ -54,8 +83,15 @@ def main():
         b = torch.load(p, weights_only=True)
         bad = [k for k in a if not torch.equal(a[k], b[k])]
         print(f"run {i}: {len(bad)} differ  {info}", flush=True)
+        snap = os.environ.get("OGKM_DIAG_SNAP_OUT")
+        if snap and os.path.exists(snap):
+            k = "g." + os.environ["OGKM_DIAG_SNAP"]
+            s = torch.load(snap, weights_only=True)
+            print(f"   after backward {k}: " + ("equal" if torch.equal(a[k], s) else describe(a[k], s)), flush=True)
+            os.remove(snap)
         for k in bad:
             print(f"   {k} {tuple(a[k].shape)}: {describe(a[k], b[k])}", flush=True)
+            print(f"      wrong pages match: {page_sources(a, b, k)}", flush=True)
         bad_runs += bool(bad)
         os.remove(p)
     print(f"DIAG_DONE bad_runs={bad_runs}/{runs}", flush=True)
