@@ -207,6 +207,17 @@ class HipBackend : public Backend {
     HIPCHK(e);
     return Status::OK;
   }
+  Status hbm_alloc_kind(int dev, size_t bytes, void** p, int kind) override {
+    if (kind <= 0) return hbm_alloc(dev, bytes, p);
+    HIPCHK(hipSetDevice(dev));
+    hipError_t e = hipExtMallocWithFlags(p, bytes, kind == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+      (void)hipGetLastError();
+      return Status::NO_MEMORY;
+    }
+    HIPCHK(e);
+    return Status::OK;
+  }
   void hbm_free(int dev, void* p, size_t) override {
     if (!p) return;
     reg_gen_.fetch_add(1, std::memory_order_acq_rel);

@@ -33,6 +33,8 @@ namespace ogkm {
 namespace {
 
 inline uint64_t page_addr(ChunkArena* a, int64_t chunk, uint32_t page) {
+  // (a residency without a chunk must never become a copy address)
+  RT_ASSERT_RELEASE(chunk >= 0 && (uint64_t)chunk < a->nchunks() && page < kPagesPerBlock);
   return a->chunk_addr((uint32_t)chunk) + ((uint64_t)page << kPageShift);
 }
 

@@ -593,7 +593,7 @@ Status Ring::run_batch(Batch& b) {
         const uint64_t need = (s.bytes + 255) & ~255ull;
         if (!stage_ && st == Status::OK && config().ans_stage_mb > 0) {  // (0: decode from the host copy)
           stage_bytes_ = std::max<uint64_t>((uint64_t)config().ans_stage_mb << 20, 4 * kBlockSize);  // two halves
-          if (be_->hbm_alloc(dev_, stage_bytes_, &stage_) != Status::OK) {
+          if (be_->hbm_alloc_kind(dev_, stage_bytes_, &stage_, (int)config().ans_stage_mem) != Status::OK) {
             stage_ = nullptr;
             stage_bytes_ = 0;
           }

@@ -803,7 +803,8 @@ void Runtime::flush_translations() {
     if (!(m & 1)) continue;
     const uint64_t k = tlb_started_[d].fetch_add(1) + 1;  // covers every unmap before this point
     const uint64_t t_fl = now_ns();
-    const Status fst = be_->tlb_flush(d);
+    Status fst = be_->tlb_flush(d);
+    for (int64_t r = 1; fst == Status::OK && r < config().tlb_flush_repeat; ++r) fst = be_->tlb_flush(d);
     Tools::get().inc(Counter::TlbFlushNs, now_ns() - t_fl);
     if (fst != Status::OK) {
       Tools::get().inc(Counter::VmmErrors);

@@ -906,6 +906,13 @@ uint64_t torch_managed_size(void* p, int device) {
   return it == da->managed.end() ? 0 : it->second.size;
 }
 
+uint64_t torch_managed_range_id(void* p, int device) {
+  DevAlloc* da = dev_alloc(device);
+  std::lock_guard<std::mutex> g(da->m);
+  auto it = da->managed.find((uint64_t)p);
+  return it == da->managed.end() ? 0 : it->second.r->id;
+}
+
 uint64_t torch_resident_bytes(void* p, int device) {
   Runtime* rt = Runtime::get();
   Range* r = nullptr;

@@ -63,6 +63,13 @@ class Backend {
 
   // ---- HBM slab provider (one large allocation carved into 2 MB root chunks)
   virtual Status hbm_alloc(int dev, size_t bytes, void** ptr) = 0;
+  // Device memory of a coherence kind: 0 = as hbm_alloc (coarse-grained),
+  // 1 = fine-grained, 2 = uncached (loads never hit a stale L2 line after
+  // another agent - an SDMA engine - wrote it).
+  virtual Status hbm_alloc_kind(int dev, size_t bytes, void** ptr, int kind) {
+    (void)kind;
+    return hbm_alloc(dev, bytes, ptr);
+  }
   virtual void hbm_free(int dev, void* ptr, size_t bytes) = 0;
   // ---- VMM provider (stable VA): physical 2 MB handles mapped into reserved VA
   virtual bool vmm_supported(int dev) = 0;

@@ -46,6 +46,7 @@ bool torch_is_managed(void* p, int device);
 size_t torch_prefetch(const std::vector<std::pair<uint64_t, uint64_t>>& ptrs, int device);
 void torch_prefetch_wait(int device);  // every queued (asynchronous) prefetch placed
 uint64_t torch_managed_size(void* p, int device);
+uint64_t torch_managed_range_id(void* p, int device);  // 0: not a managed tensor
 uint64_t torch_resident_bytes(void* p, int device);  // bytes of the tensor resident in HBM
 // Last allocation failure on `device` (empty: none): the message a caller
 // surfaces instead of aborting.

@@ -1407,6 +1407,7 @@ PYBIND11_MODULE(_ogkm, m) {
     return torch_prefetch(ptrs, dev);
   });
   m.def("torch_managed_size", [](uint64_t p, int dev) { return torch_managed_size((void*)p, dev); });
+  m.def("torch_managed_range_id", [](uint64_t p, int dev) { return torch_managed_range_id((void*)p, dev); });
   m.def("torch_prefetch_wait", [](int dev) {
     py::gil_scoped_release nogil;
     torch_prefetch_wait(dev);

@@ -53,16 +53,45 @@ def run(model, x, log=False):
     loss = y.float().pow(2).mean()
     loss.backward()
     say("backward done")
-    if os.environ.get("OGKM_DIAG_SNAP"):  # (diagnostics) a gradient's value right after backward
+    if os.environ.get("OGKM_DIAG_SNAP_OUT"):  # (diagnostics) a gradient's value right after backward
         w = dict(model.named_parameters())[os.environ["OGKM_DIAG_SNAP"]]
         torch.save(w.grad.detach().cpu().clone(), os.environ["OGKM_DIAG_SNAP_OUT"])
     opt.step()
     say("step done")
+    if os.environ.get("OGKM_DIAG_SNAP2_OUT"):  # (diagnostics) the same gradient right after the step
+        w = dict(model.named_parameters())[os.environ["OGKM_DIAG_SNAP"]]
+        torch.save(w.grad.detach().cpu().clone(), os.environ["OGKM_DIAG_SNAP2_OUT"])
+    if os.environ.get("OGKM_DIAG_RES"):  # (diagnostics) chunks owned by two tensors' blocks
+        _chunk_owners(model, "after step")
     out = {"y_inf": y_inf, "loss": loss.detach()}
     for name, p in model.named_parameters():
         out["p." + name] = p.detach()
         out["g." + name] = p.grad.detach()
+    if os.environ.get("OGKM_DIAG_PINNED_CPU"):  # (diagnostics) copy-outs into pinned host memory
+        return {k: torch.empty(v.shape, dtype=v.dtype, pin_memory=True).copy_(v) for k, v in out.items()}
     return {k: v.cpu() for k, v in out.items()}
+
+
+def _chunk_owners(model, when):
+    from ogkm._native import lib
+
+    owners = {}
+    for name, p in model.named_parameters():
+        for kind, t in (("p", p), ("g", p.grad)):
+            if t is None:
+                continue
+            rid = lib.torch_managed_range_id(t.untyped_storage().data_ptr(), 0)
+            if not rid:
+                continue
+            for b in range((t.untyped_storage().nbytes() + (2 << 20) - 1) >> 21):
+                ri = lib.residency_info(rid, b << 21)
+                for e in ri["resident_on"]:
+                    key = (str(sorted((k, v) for k, v in e.items() if k not in ("pages", "encoded_bytes"))))
+                    owners.setdefault(key, []).append(f"{kind}.{name}[{b}]")
+    dup = {k: v for k, v in owners.items() if len(v) > 1}
+    print(f"CHUNK_OWNERS {when}: {len(owners)} chunks, {len(dup)} shared", flush=True)
+    for k, v in list(dup.items())[:10]:
+        print(f"   {k}: {v}", flush=True)
 
 
 def main() -> None:
@@ -130,6 +159,8 @@ def main() -> None:
                 torch.cuda.synchronize()
                 lib.pack_wait(60000)
         res = run(model, x.cuda(), log=True)
+        if os.environ.get("OGKM_DIAG_RES"):
+            _chunk_owners(model, "after copy-out")
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     torch.save(res, path)

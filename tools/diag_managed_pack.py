@@ -80,6 +80,9 @@ def main():
         p = os.path.join(out, f"managed{i}.pt")
         log = run(["managed", p, "--pack"] + extra)
         info = log.split("MANAGED_OK", 1)[1].strip().splitlines()[0]
+        for line in log.splitlines():
+            if line.startswith(("CHUNK_OWNERS", "   (")) or line.startswith("   [("):
+                print(line[:300], flush=True)
         b = torch.load(p, weights_only=True)
         bad = [k for k in a if not torch.equal(a[k], b[k])]
         print(f"run {i}: {len(bad)} differ  {info}", flush=True)
@@ -89,6 +92,12 @@ def main():
             s = torch.load(snap, weights_only=True)
             print(f"   after backward {k}: " + ("equal" if torch.equal(a[k], s) else describe(a[k], s)), flush=True)
             os.remove(snap)
+        snap2 = os.environ.get("OGKM_DIAG_SNAP2_OUT")
+        if snap2 and os.path.exists(snap2):
+            k = "g." + os.environ["OGKM_DIAG_SNAP"]
+            s = torch.load(snap2, weights_only=True)
+            print(f"   after step {k}: " + ("equal" if torch.equal(a[k], s) else describe(a[k], s)), flush=True)
+            os.remove(snap2)
         for k in bad:
             print(f"   {k} {tuple(a[k].shape)}: {describe(a[k], b[k])}", flush=True)
             print(f"      wrong pages match: {page_sources(a, b, k)}", flush=True)
