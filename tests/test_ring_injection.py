@@ -211,6 +211,7 @@ def test_merged_batches_copy_after_staged_decode_into_same_chunk(fake_rt):
     after them overwrote it (the transparent-mode packed training test's
     corrupted gradient)."""
     lib.configure("ans_stage_mb", 8)
+    lib.configure("ring_merge_packed_mb", 64)  # (off by default)
     vals = lambda seed: (torch.randn(MB, generator=torch.Generator().manual_seed(seed)) * 0.02).to(torch.bfloat16)
     w1, w2, g = vals(1), vals(2), vals(3)
     enc1 = torch.frombuffer(bytearray(lib.ans_encode(w1.view(torch.uint8).numpy().tobytes())), dtype=torch.uint8)
