@@ -846,6 +846,10 @@ class HipBackend : public Backend {
     HIPCHK(hipStreamWaitValue64((hipStream_t)s, addr, v, hipStreamWaitValueGte, ~0ull));
     return Status::OK;
   }
+  Status acquire_caches(void* s) override {
+    HIPCHK(launch_acquire((hipStream_t)s));
+    return Status::OK;
+  }
 
   LinkType link_type(int a, int b) override {
     if (a == b) return LinkType::SELF;

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 
+#include "ogkm/config.hpp"
 #include "ogkm/ring.hpp"
 
 namespace ogkm {
@@ -104,6 +105,7 @@ Status Tracker::wait() {
 }
 
 Status Tracker::gpu_wait(Backend* be, void* stream) const {
+  bool ring_wait = false;  // a GPU-side wait on a ring's tracking value was queued
   for (auto& f : fences_) {
     if (f->done.load(std::memory_order_relaxed)) continue;
     // An event recorded on this very stream is already ordered before
@@ -135,6 +137,7 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
       // enqueued after this wait (Ring::issued_seq)
       s = f->ring->wait_issued(f->seq);
       if (s == Status::OK) s = be->wait_value(stream, f->ring->semaphore(), f->seq);
+      ring_wait = true;
     }
     else s = f->wait();
     uint64_t dt = now_ns() - t0;
@@ -145,6 +148,7 @@ Status Tracker::gpu_wait(Backend* be, void* stream) const {
               (unsigned long long)(f->ring ? f->ring->submitted_seq() : 0));
     if (s != Status::OK) return s;
   }
+  if (ring_wait && config().gpu_wait_acquire) return be->acquire_caches(stream);
   return Status::OK;
 }
 

@@ -215,6 +215,12 @@ class Backend {
   virtual Status signal(int dev, uint64_t* addr, uint64_t value, void* stream) = 0;
   // Make `stream` wait until *addr >= value (GPU-side wait, no CPU involvement).
   virtual Status wait_value(void* stream, uint64_t* addr, uint64_t value) = 0;
+  // Invalidate the GPU's caches for the work queued on `stream` after this
+  // point (data another engine wrote since). Default: nothing to do.
+  virtual Status acquire_caches(void* stream) {
+    (void)stream;
+    return Status::OK;
+  }
   // Test hook (fake backend): a "kernel" on `stream` that sleeps delay_us and
   // then reads (and with `write`, increments) one word of every 4 KB page of
   // [ptr, ptr+bytes) - an access through an unmapped VA is a SIGSEGV on the

@@ -50,6 +50,7 @@ struct KPageList {
 hipError_t launch_page_copy(uint64_t dst_base, uint64_t src_base, const KPageList& pl, uint32_t npages,
                             uint32_t workgroups, hipStream_t s);
 hipError_t launch_signal(uint64_t* host_addr, uint64_t value, hipStream_t s);
+hipError_t launch_acquire(hipStream_t s);  // system-scope cache acquire on every XCD (k_acquire)
 
 // Fused copy + BF12 decode of up to kInlineDescs encoded blocks (codec.hpp).
 struct KBf12Desc {

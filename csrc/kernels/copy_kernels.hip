@@ -265,6 +265,19 @@ hipError_t launch_signal(uint64_t* host_addr, uint64_t value, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Consumer-side acquire after a GPU-side wait on a ring's tracking value: the
+// data the ring delivered (SDMA copies, decodes on the ring's own stream) must
+// not be read through a line an XCD's L2 still holds from the chunk's previous
+// contents. Every workgroup runs a system-scope acquire (vector cache
+// invalidate of its CU and its XCD's L2); 256 workgroups cover every XCD
+// (workgroups go round-robin over the 8 XCDs) and every CU.
+__global__ void __launch_bounds__(64) k_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+
+hipError_t launch_acquire(hipStream_t s) {
+  hipLaunchKernelGGL(k_acquire, dim3(256), dim3(64), 0, s);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- fault buffer
 // Producer side of the GET/PUT fault ring (ogkm/fault_abi.hpp): drop on a
 // full ring at first look (may_drop), else reserve a slot with one atomic add

@@ -67,6 +67,21 @@ def run(model, x, log=False):
     for name, p in model.named_parameters():
         out["p." + name] = p.detach()
         out["g." + name] = p.grad.detach()
+    if os.environ.get("OGKM_DIAG_STABLE"):  # (diagnostics) stable-VA chunk vs resident chunk after each copy-out
+        from ogkm._native import lib
+
+        res = {}
+        for k, v in out.items():
+            res[k] = v.cpu()
+            rid = lib.torch_managed_range_id(v.untyped_storage().data_ptr(), 0)
+            if not rid:
+                continue
+            for b in range((v.untyped_storage().nbytes() + (2 << 20) - 1) >> 21):
+                ri = lib.residency_info(rid, b << 21)
+                gpu = [e for e in ri["resident_on"] if e.get("tier") == "hbm" or e.get("kind") == "gpu" or "gpu" in str(e)]
+                if gpu and ri["stable_chunk"] >= 0 and all(e["chunk"] != ri["stable_chunk"] for e in gpu):
+                    print(f"STABLE_MISMATCH {k}[{b}] stable_chunk {ri['stable_chunk']} resident {gpu}", flush=True)
+        return res
     if os.environ.get("OGKM_DIAG_PINNED_CPU"):  # (diagnostics) copy-outs into pinned host memory
         return {k: torch.empty(v.shape, dtype=v.dtype, pin_memory=True).copy_(v) for k, v in out.items()}
     return {k: v.cpu() for k, v in out.items()}
