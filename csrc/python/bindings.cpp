@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <map>
+#include <shared_mutex>
 #include <cstring>
 
 #include "ogkm/codec.hpp"
@@ -1407,6 +1409,35 @@ PYBIND11_MODULE(_ogkm, m) {
     return torch_prefetch(ptrs, dev);
   });
   m.def("torch_managed_size", [](uint64_t p, int dev) { return torch_managed_size((void*)p, dev); });
+  // (diagnostics) Every block residency's chunk: owned by that block in its
+  // HBM arena, and held by no other residency. "" = consistent.
+  m.def("check_ownership", [] {
+    Runtime* r = rt();
+    std::string out;
+    std::map<std::pair<ChunkArena*, int64_t>, std::string> seen;
+    std::shared_lock<OrderedRWLock> vg(r->vs().lock);
+    for (auto& kv : r->vs().ranges) {
+      Range* rg = kv.second.get();
+      for (uint64_t bi = 0; bi < rg->nblocks; ++bi) {
+        Block* b = rg->block(bi);
+        std::lock_guard<OrderedMutex> g(b->lock);
+        for (auto& x : b->res) {
+          if (x.chunk < 0) continue;
+          const std::string who = std::to_string(rg->id) + "[" + std::to_string(bi) + "]@" + x.loc.str() +
+                                  (rg->dead.load() ? "(dead)" : "");
+          auto key = std::make_pair(x.arena, x.chunk);
+          auto it = seen.find(key);
+          if (it != seen.end())
+            out += "shared chunk " + std::to_string(x.chunk) + ": " + it->second + " and " + who + "; ";
+          else
+            seen.emplace(key, who);
+          if (x.loc.is_gpu() && x.arena->owner((uint32_t)x.chunk) != b)
+            out += "owner mismatch " + who + " chunk " + std::to_string(x.chunk) + "; ";
+        }
+      }
+    }
+    return out;
+  });
   m.def("torch_managed_range_id", [](uint64_t p, int dev) { return torch_managed_range_id((void*)p, dev); });
   m.def("torch_prefetch_wait", [](int dev) {
     py::gil_scoped_release nogil;

@@ -67,12 +67,16 @@ def run(model, x, log=False):
     for name, p in model.named_parameters():
         out["p." + name] = p.detach()
         out["g." + name] = p.grad.detach()
-    if os.environ.get("OGKM_DIAG_STABLE"):  # (diagnostics) stable-VA chunk vs resident chunk after each copy-out
+    if os.environ.get("OGKM_DIAG_STABLE") and "ogkm" in sys.modules:  # (diagnostics, managed run only)
         from ogkm._native import lib
 
         res = {}
         for k, v in out.items():
             res[k] = v.cpu()
+            if os.environ.get("OGKM_DIAG_OWN"):
+                bad = lib.check_ownership()
+                if bad:
+                    print(f"OWNERSHIP after {k}: {bad[:600]}", flush=True)
             rid = lib.torch_managed_range_id(v.untyped_storage().data_ptr(), 0)
             if not rid:
                 continue

@@ -81,7 +81,7 @@ def main():
         log = run(["managed", p, "--pack"] + extra)
         info = log.split("MANAGED_OK", 1)[1].strip().splitlines()[0]
         for line in log.splitlines():
-            if line.startswith(("CHUNK_OWNERS", "   (", "STABLE_MISMATCH")) or line.startswith("   [("):
+            if line.startswith(("CHUNK_OWNERS", "   (", "STABLE_MISMATCH", "OWNERSHIP")) or line.startswith("   [("):
                 print(line[:300], flush=True)
         b = torch.load(p, weights_only=True)
         bad = [k for k in a if not torch.equal(a[k], b[k])]
