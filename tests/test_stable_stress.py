@@ -98,6 +98,8 @@ for p, n in live:
         bad += 1
         print("DATA_MISMATCH", hex(p), n, touches[p], sorted(set(words))[:8])
 assert bad == 0, bad
+own = lib.check_ownership()  # every residency's chunk owned by its block, none shared
+assert own == "", own[:2000]
 st = rt.stats()
 print("STRESS_OK", st["evictions"], st["vmm_remaps"], st["tlb_flushes"], st["vmm_errors"])
 '''
