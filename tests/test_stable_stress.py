@@ -121,3 +121,22 @@ def test_stable_va_stress_async_users(lazy, batch, seed, tlb, prefetch, hints):
     assert "[fake RACE]" not in r.stderr, r.stderr[-3000:]
     ev, remaps, flushes, errors = map(int, r.stdout.split("STRESS_OK")[1].split()[:4])
     assert ev > 50 and remaps > 0 and errors == 0, r.stdout
+
+
+@pytest.mark.parametrize("seed,prefetch", [(201, 0), (204, 1), (213, 1)])
+def test_stable_va_stress_packed_merged_refills(seed, prefetch):
+    """The same adversarial run with refills from ANS1-packed host copies staged
+    through a small HBM staging buffer, slow decodes (the fake decode kernel
+    sleeps 2 ms) and the H2D worker merging queued decode batches - the
+    configuration of the transparent-mode gradient corruption bisected in
+    profiles/r6_ring_merge_fix (not reproduced here, on the fake backend)."""
+    extra = ('lib.configure("ring_merge_packed_mb", 64)\nlib.configure("ans_stage_mb", 8)\n'
+             'lib.configure("fake_kernel_delay_us", 2000)\n')
+    code = WORKER % (ROOT, seed % 2, [1, 2, 4, 32][seed % 4], (seed // 2) % 2, prefetch, (seed // 4) % 2, seed, 600)
+    code = code.replace('lib.configure("fake_race_check", 1)', 'lib.configure("fake_race_check", 1)\n' + extra)
+    code = code.replace('print("STRESS_OK"', 'print("PACKED", st["packed_decodes"])\nprint("STRESS_OK"')
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
+    assert "STRESS_OK" in r.stdout
+    assert int(r.stdout.split("PACKED")[1].split()[0]) > 0, r.stdout  # refills did come from packed copies
+    assert "[fake RACE]" not in r.stderr, r.stderr[-3000:]
