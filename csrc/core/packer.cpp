@@ -340,7 +340,8 @@ void Runtime::pack_enqueue(Block* b) {
   // transparent mode's allocator sets it on every tensor for read duplication),
   // pack_auto_clean_evictions times for any other.
   const int64_t auto_n = config().pack_auto_clean_evictions;
-  if (!(b->policy.read_dup && b->clean_evictions >= 1) && !(auto_n > 0 && b->clean_evictions >= (uint64_t)auto_n))
+  const uint64_t dup_n = (uint64_t)std::max<int64_t>(1, config().pack_read_dup_clean_evictions);
+  if (!(b->policy.read_dup && b->clean_evictions >= dup_n) && !(auto_n > 0 && b->clean_evictions >= (uint64_t)auto_n))
     return;
   if (!pack_candidate(b)) return;
   b->pack_queued = true;

@@ -87,6 +87,7 @@ namespace ogkm {
   X(pack_host_copies, 1, "keep lossless ANS1-packed host / CXL copies of read-mostly managed blocks (H2D moves the packed bytes; the ring decodes them in HBM)") \
   X(pack_auto_clean_evictions, 2, "a block whose HBM copy was evicted this many times without a copy-out counts as read-mostly and gets packed (0 = only SET_READ_MOSTLY blocks)") \
   X(pack_min_saving_pct, 8, "a block is kept packed only when its packed form saves at least this share of its bytes") \
+  X(pack_read_dup_clean_evictions, 1, "clean HBM evictions after which a READ_MOSTLY block's host copy is packed") \
   X(pack_segments, 0, "segmented packed host copies (64 KB ANS1 segments, fmt 3) for blocks that are written: a write-back expands only the segments it touches, the rest stay packed (0 = whole blocks only). Off by default: on the stock 70B under ogkm.managed() it saves 2.5 of 63 GB/step H2D but costs more ring / host time than that (38.4 vs 49.6 tok/s, profiles/r6_segmented.md)") \
   X(pack_seg_min, 4, "a written block's host copy is segment-packed when at least this many of its 64 KB segments were untouched by its latest write-back") \
   X(pack_threads, 4, "host encoder threads of the packer") \
