@@ -182,6 +182,10 @@ def main() -> None:
             _chunk_owners(model, "after copy-out")
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    from ogkm._native import lib
+
+    own = lib.check_ownership()  # every residency's chunk owned by its block, none shared
+    assert own == "", own[:2000]
     torch.save(res, path)
     st = rt.stats()
     print("MANAGED_OK", {"param_mb": param_bytes >> 20, "arena_mb": ARENA_MB, "ops": mode.ops,
