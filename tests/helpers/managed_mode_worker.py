@@ -180,6 +180,15 @@ def main() -> None:
         res = run(model, x.cuda(), log=True)
         if os.environ.get("OGKM_DIAG_RES"):
             _chunk_owners(model, "after copy-out")
+        if os.environ.get("OGKM_DIAG_HOSTREAD_OUT"):  # (diagnostics) the runtime's host-side view of a gradient
+            from ogkm._native import lib
+
+            g = dict(model.named_parameters())[os.environ["OGKM_DIAG_SNAP"]].grad
+            st = g.untyped_storage()
+            rid = lib.torch_managed_range_id(st.data_ptr(), 0)
+            buf = torch.empty(st.nbytes(), dtype=torch.uint8)
+            lib.read(rid, 0, buf.data_ptr(), st.nbytes(), -1)
+            torch.save(buf.view(g.dtype).view(g.shape).clone(), os.environ["OGKM_DIAG_HOSTREAD_OUT"])
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     from ogkm._native import lib

@@ -92,6 +92,12 @@ def main():
             s = torch.load(snap, weights_only=True)
             print(f"   after backward {k}: " + ("equal" if torch.equal(a[k], s) else describe(a[k], s)), flush=True)
             os.remove(snap)
+        hr = os.environ.get("OGKM_DIAG_HOSTREAD_OUT")
+        if hr and os.path.exists(hr):
+            k = "g." + os.environ["OGKM_DIAG_SNAP"]
+            s = torch.load(hr, weights_only=True)
+            print(f"   runtime read of {k} at the end: " + ("equal" if torch.equal(a[k], s) else describe(a[k], s)), flush=True)
+            os.remove(hr)
         snap2 = os.environ.get("OGKM_DIAG_SNAP2_OUT")
         if snap2 and os.path.exists(snap2):
             k = "g." + os.environ["OGKM_DIAG_SNAP"]
