@@ -73,6 +73,9 @@ def run(model, x, log=False):
         res = {}
         for k, v in out.items():
             res[k] = v.cpu()
+            if os.environ.get("OGKM_DIAG_SECOND_OUT") and k == "g." + os.environ.get("OGKM_DIAG_SNAP", ""):
+                torch.cuda.synchronize()
+                torch.save(v.cpu().clone(), os.environ["OGKM_DIAG_SECOND_OUT"])  # the same tensor copied out again
             if os.environ.get("OGKM_DIAG_OWN"):
                 bad = lib.check_ownership()
                 if bad:

@@ -92,6 +92,13 @@ def main():
             s = torch.load(snap, weights_only=True)
             print(f"   after backward {k}: " + ("equal" if torch.equal(a[k], s) else describe(a[k], s)), flush=True)
             os.remove(snap)
+        sc = os.environ.get("OGKM_DIAG_SECOND_OUT")
+        if sc and os.path.exists(sc):
+            k = "g." + os.environ["OGKM_DIAG_SNAP"]
+            s = torch.load(sc, weights_only=True)
+            print(f"   second copy-out of {k}: " + ("equal" if torch.equal(a[k], s) else describe(a[k], s))
+                  + ("; first copy-out equal" if torch.equal(a[k], b[k]) else "; first copy-out differs"), flush=True)
+            os.remove(sc)
         hr = os.environ.get("OGKM_DIAG_HOSTREAD_OUT")
         if hr and os.path.exists(hr):
             k = "g." + os.environ["OGKM_DIAG_SNAP"]
