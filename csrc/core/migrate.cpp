@@ -416,6 +416,17 @@ static Ring* ring_for(Runtime* rt, const Loc& s, const Loc& d) {
 static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from, Residency* to,
                          const PageMask& pages) {
   if (pages.empty()) return Status::OK;
+  // Both residencies belong to this block, and an HBM destination chunk is
+  // owned by it: a copy never lands in a chunk another block holds (cheap
+  // checks; a stale Residency* after b->res changed would fail here).
+  auto owned = [&](const Residency* x) {
+    for (const auto& y : b->res)
+      if (&y == x) return true;
+    return false;
+  };
+  RT_ASSERT_RELEASE(owned(from) && owned(to) && from != to);
+  if (config().debug_check_copy_owner && to->loc.is_gpu() && to->chunk >= 0)
+    RT_ASSERT_RELEASE(to->arena->owner((uint32_t)to->chunk) == b);
   // A packed copy that lost pages since (a write elsewhere revoked them) is no
   // whole-block source any more: back to raw pages first.
   if (from->fmt == 2 && !(from->resident == b->valid_pages())) {

@@ -97,6 +97,7 @@ namespace ogkm {
   X(ring_stage_overlap, 1, "H2D ring: a staging half's copies are issued before the host waits for the previous half's and launches its decode (0 = issue, wait, decode per half)") \
   X(ring_merge_packed_mb, 0, "H2D ring: queued batches of packed-block decodes run as one batch up to this many packed MB (0 = one batch at a time) Off by default: with it on, the packed transparent-mode training test read another block's decoded weights in a gradient, 6/6 runs, unresolved (profiles/r6_ring_merge_fix)") \
   X(gpu_wait_acquire, 0, "after a stream's GPU-side wait on a ring tracking value, a system-scope cache acquire kernel on that stream (every XCD's L2)") \
+  X(debug_check_copy_owner, 0, "diagnostics: every copy into an HBM chunk asserts the chunk's arena owner is the destination block") \
   X(tlb_flush_repeat, 1, "diagnostics: translation flushes issued per flush_translations call") \
   X(ans_stage_mem, 0, "H2D ring staging buffer memory: 0 coarse-grained (hipMalloc), 1 fine-grained, 2 uncached") \
   X(ans_stage_engines, 0xF, "SDMA engines (mask) the H2D ring spreads packed-block staging copies over (0 = the ring's own engine)") \
