@@ -416,15 +416,16 @@ static Ring* ring_for(Runtime* rt, const Loc& s, const Loc& d) {
 static Status copy_pages(Runtime* rt, Runtime::Ctx& c, Block* b, Residency* from, Residency* to,
                          const PageMask& pages) {
   if (pages.empty()) return Status::OK;
-  // Both residencies belong to this block, and an HBM destination chunk is
-  // owned by it: a copy never lands in a chunk another block holds (cheap
-  // checks; a stale Residency* after b->res changed would fail here).
+  // The source is one of this block's residencies (a stale Residency* after
+  // b->res changed would fail here; the destination may be a relocation's
+  // temporary, place_extent), and an HBM destination chunk is owned by the
+  // block: a copy never lands in a chunk another block holds.
   auto owned = [&](const Residency* x) {
     for (const auto& y : b->res)
       if (&y == x) return true;
     return false;
   };
-  RT_ASSERT_RELEASE(owned(from) && owned(to) && from != to);
+  RT_ASSERT_RELEASE(owned(from) && from != to);
   if (config().debug_check_copy_owner && to->loc.is_gpu() && to->chunk >= 0)
     RT_ASSERT_RELEASE(to->arena->owner((uint32_t)to->chunk) == b);
   // A packed copy that lost pages since (a write elsewhere revoked them) is no
